@@ -1,0 +1,331 @@
+/*
+ * oracle/ref_harness.c -- TEST INFRASTRUCTURE ONLY (never shipped, never linked
+ * into the product).  Our own driver, linked against the reference LoRADS
+ * objects built by oracle/Makefile.ref, used to produce golden fixtures that pin
+ * the CPU restatement (oracle/lrsdp_oracle.c) and, on the GPU box, to time the
+ * real reference CPU path for bench.py's cpu_baseline.
+ *
+ * Modes
+ *   solve   <file.dat-s> [--flag value ...]
+ *       The init sequence of main.c:380-418, then LORADS_ALMOptimize
+ *       (main.c:450), LORADS_ALMtoADMM + LORADSADMMOptimize (main.c:456-457)
+ *       and the reoptLevel>=1 loop (main.c:491-513).  The ARPACK dual
+ *       infeasibility (main.c:515) is skipped (ARPACK is not in the image).
+ *       Prints "REF_RESULT ..." lines and writes --jsonfile like
+ *       lorads_logging.c:618.
+ *   alm_rate <file.dat-s> <rank> <iters>
+ *       Runs phase 1 at --fixedRank <rank> for a bounded number of ALM inner
+ *       iterations (maxALMIter large, phase1Tol tiny) and prints the rate.
+ *   kernels <file.dat-s> <rank> <in.bin> <out.bin>
+ *       One call of each hot-path operator on caller-provided iterates (see
+ *       scripts/make_golden.py for the exact binary layout).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include <getopt.h>
+#include <sys/time.h>
+
+#include "lorads_file_io.h"
+#include "def_lorads_user_data.h"
+#include "lorads_user_data.h"
+#include "lorads_utils.h"
+#include "def_lorads_solver.h"
+#include "lorads_solver.h"
+#include "lorads_alm.h"
+#include "lorads_admm.h"
+#include "lorads_alg_common.h"
+#include "lorads_logging.h"
+#include "lorads_cgs.h"
+
+extern int MAX_ALM_SUB_ITER;
+
+static double now_s(void) {
+    struct timeval tv; gettimeofday(&tv, NULL);
+    return tv.tv_sec + 1e-6 * tv.tv_usec;
+}
+
+static void default_params(lorads_params *p) {
+    memset(p, 0, sizeof(*p));
+    p->fname = "NULL"; p->logFile = NULL; p->jsonFile = NULL;
+    p->initRho = 0.0; p->rhoMax = 5000.0; p->rhoCellingALM = 1e8;
+    p->rhoCellingADMM = 5000.0 * 200; p->maxALMIter = 200; p->maxADMMIter = 10000;
+    p->timesLogRank = 2.0; p->fixedRank = -1; p->initRank = -1; p->rhoFreq = 5;
+    p->rhoFactor = 1.2; p->ALMRhoFactor = 2.0; p->rankUpdateFactor = 1.5;
+    p->phase1Tol = 1e-3; p->phase2Tol = 1e-5; p->timeSecLimit = 3600.0;
+    p->heuristicFactor = 1.0; p->lbfgsListLength = 2; p->endTauTol = 1e-16;
+    p->endALMSubTol = 1e-10; p->l2Rescaling = false; p->reoptLevel = 2;
+    p->dyrankLevel = 2; p->highAccMode = false;
+    p->oracleRankMethod = LORADS_ORACLE_RANK_GRAM;
+}
+
+static struct option long_opts[] = {
+    {"logfile", required_argument, 0, 1025}, {"jsonfile", required_argument, 0, 1026},
+    {"initRho", required_argument, 0, 1000}, {"rhoMax", required_argument, 0, 1001},
+    {"rhoCellingALM", required_argument, 0, 1002}, {"rhoCellingADMM", required_argument, 0, 1003},
+    {"maxALMIter", required_argument, 0, 1004}, {"maxADMMIter", required_argument, 0, 1005},
+    {"timesLogRank", required_argument, 0, 1006}, {"fixedRank", required_argument, 0, 1022},
+    {"initRank", required_argument, 0, 1023}, {"rhoFreq", required_argument, 0, 1007},
+    {"rhoFactor", required_argument, 0, 1008}, {"ALMRhoFactor", required_argument, 0, 1009},
+    {"rankUpdateFactor", required_argument, 0, 1024}, {"phase1Tol", required_argument, 0, 1010},
+    {"phase2Tol", required_argument, 0, 1011}, {"timeSecLimit", required_argument, 0, 1012},
+    {"heuristicFactor", required_argument, 0, 1013}, {"lbfgsListLength", required_argument, 0, 1014},
+    {"endTauTol", required_argument, 0, 1015}, {"endALMSubTol", required_argument, 0, 1016},
+    {"l2Rescaling", required_argument, 0, 1017}, {"reoptLevel", required_argument, 0, 1018},
+    {"dyrankLevel", required_argument, 0, 1019}, {"highAccMode", required_argument, 0, 1020},
+    {"oracleRankNaive", no_argument, 0, 1021}, {0, 0, 0, 0}};
+
+static void parse_flags(lorads_params *p, int argc, char **argv) {
+    int opt, li = 0;
+    optind = 1;
+    while ((opt = getopt_long(argc, argv, "r:", long_opts, &li)) != -1) {
+        switch (opt) {
+        case 1025: p->logFile = optarg; break;          case 1026: p->jsonFile = optarg; break;
+        case 1000: p->initRho = atof(optarg); break;    case 1001: p->rhoMax = atof(optarg); break;
+        case 1002: p->rhoCellingALM = atof(optarg); break;
+        case 1003: p->rhoCellingADMM = atof(optarg); break;
+        case 1004: p->maxALMIter = atoi(optarg); break; case 1005: p->maxADMMIter = atoi(optarg); break;
+        case 1006: p->timesLogRank = atof(optarg); break;
+        case 1022: p->fixedRank = atoi(optarg); break;  case 1023: p->initRank = atoi(optarg); break;
+        case 1007: p->rhoFreq = atoi(optarg); break;    case 1008: p->rhoFactor = atof(optarg); break;
+        case 1009: p->ALMRhoFactor = atof(optarg); break;
+        case 1024: p->rankUpdateFactor = atof(optarg); break;
+        case 1010: p->phase1Tol = atof(optarg); break;  case 1011: p->phase2Tol = atof(optarg); break;
+        case 1012: p->timeSecLimit = atof(optarg); break;
+        case 1013: p->heuristicFactor = atof(optarg); break;
+        case 1014: p->lbfgsListLength = atoi(optarg); break;
+        case 1015: p->endTauTol = atof(optarg); break;  case 1016: p->endALMSubTol = atof(optarg); break;
+        case 1017: p->l2Rescaling = atoi(optarg); break; case 1018: p->reoptLevel = atoi(optarg); break;
+        case 1019: p->dyrankLevel = atoi(optarg); break; case 1020: p->highAccMode = atoi(optarg); break;
+        case 1021: p->oracleRankMethod = LORADS_ORACLE_RANK_NAIVE; break;
+        default: break;
+        }
+    }
+    p->rhoCellingADMM = p->rhoMax * 200;   /* main.c:350 */
+}
+
+typedef struct {
+    lorads_solver *S;
+    lorads_int nConstrs, nBlks, *BlkDims, nLpCols;
+    lorads_int **coneMatBeg, **coneMatIdx; double **coneMatElem, *rowRHS;
+    lorads_int *LpMatBeg, *LpMatIdx; double *LpMatElem;
+    user_data **SDPDatas;
+    lorads_alm_state alm; lorads_admm_state admm; SDPConst sc;
+} ref_ctx;
+
+/* main.c:380-419 */
+static int ref_setup(ref_ctx *c, lorads_params *p, double *t_read, double *t_solve_start) {
+    lorads_int nCols = 0, nElem = 0;
+    double t0 = now_s();
+    if (LReadSDPA(p->fname, &c->nConstrs, &c->nBlks, &c->BlkDims, &c->rowRHS, &c->coneMatBeg,
+                  &c->coneMatIdx, &c->coneMatElem, &nCols, &c->nLpCols, &c->LpMatBeg,
+                  &c->LpMatIdx, &c->LpMatElem, &nElem) != LORADS_RETCODE_OK)
+        return -1;
+    *t_read = now_s() - t0;
+    *t_solve_start = now_s();
+    LORADS_INIT(c->S, lorads_solver, 1);
+    LORADS_INIT(c->S->var, lorads_variable, 1);
+    LORADSInitSolver(c->S, c->nConstrs, c->nBlks, c->BlkDims, c->nLpCols);
+    LORADS_INIT(c->SDPDatas, user_data *, c->nBlks);
+    LORADSSetDualObjective(c->S, c->rowRHS);
+    LORADSInitConeData(c->S, c->SDPDatas, c->coneMatElem, c->coneMatBeg, c->coneMatIdx, c->BlkDims,
+                       c->nConstrs, c->nBlks, c->nLpCols, c->LpMatBeg, c->LpMatIdx, c->LpMatElem);
+    LORADSPreprocess(c->S, c->BlkDims);
+    LORADSDetermineRank(c->S, c->BlkDims, p->timesLogRank, p->fixedRank, p->initRank);
+    LORADSInitALMVars(c->S, c->S->var->rankElem, c->BlkDims, c->nBlks, c->nLpCols, p->lbfgsListLength);
+    c->S->hisRecT = p->lbfgsListLength;
+    LORADSInitADMMVars(c->S, c->S->var->rankElem, c->BlkDims, c->nBlks, c->nLpCols);
+    initial_solver_state(p, c->S, &c->alm, &c->admm, &c->sc);
+    lorads_logging_init(c->S, p, *t_solve_start);
+    return 0;
+}
+
+static int mode_solve(int argc, char **argv) {
+    lorads_params p; default_params(&p);
+    p.fname = argv[2];
+    parse_flags(&p, argc - 2, argv + 2);
+    ref_ctx c; memset(&c, 0, sizeof(c));
+    double t_read, tss;
+    if (ref_setup(&c, &p, &t_read, &tss)) { printf("REF_RESULT read_failed\n"); return 0; }
+    lorads_solver *S = c.S;
+    double all_time = 0.0;
+    int bad = 0;
+    double ts = now_s();
+    double t_alm0 = now_s();
+    LORADS_ALMOptimize(&p, S, &c.alm, p.maxALMIter, tss);
+    double t_alm = now_s() - t_alm0;
+    long alm_inner = (long)c.alm.innerIter;
+    if (now_s() - tss > p.timeSecLimit) goto END;
+    LORADS_ALMtoADMM(S, &p, &c.alm, &c.admm);
+    if (LORADSADMMOptimize(&p, S, &c.admm, p.maxADMMIter, tss) == RET_CODE_BAD_ITER) bad = 1;
+    all_time += now_s() - ts;
+    if (p.reoptLevel >= 1) {
+        double rp = 5; lorads_int ai = 3, di = 50;
+        int cnt = 0;
+        while ((c.alm.primal_dual_gap > p.phase2Tol || c.alm.l_1_primal_infeasibility > p.phase2Tol) &&
+               (c.admm.primal_dual_gap > p.phase2Tol || c.admm.l_1_primal_infeasibility > p.phase2Tol)) {
+            if (cnt >= 1) break;
+            double t1 = now_s();
+            reopt(&p, S, &c.alm, &c.admm, &rp, &ai, &di, tss, &bad, 1);
+            all_time += now_s() - t1;
+            cnt++;
+            if (now_s() - tss > p.timeSecLimit) break;
+        }
+    }
+END:;
+    lorads_int orank = lorads_compute_oracle_rank(S, 2);
+    if (orank < 0) orank = 0;
+    lorads_write_json_output(S, orank, c.admm.primal_objective_value, c.admm.dual_objective_value,
+                             c.admm.l_1_primal_infeasibility, c.admm.l_inf_primal_infeasibility,
+                             c.admm.primal_dual_gap, all_time, p.rhoMax, p.heuristicFactor);
+    lorads_logging_close(S);
+    printf("REF_RESULT alm_inner=%ld alm_outer=%ld alm_time=%.9e alm_pobj=%.17e alm_dobj=%.17e "
+           "alm_pinf=%.17e alm_gap=%.17e alm_rho=%.17e\n",
+           alm_inner, (long)c.alm.outerIter, t_alm, c.alm.primal_objective_value,
+           c.alm.dual_objective_value, c.alm.l_1_primal_infeasibility, c.alm.primal_dual_gap, c.alm.rho);
+    printf("REF_RESULT admm_iter=%ld admm_pobj=%.17e admm_dobj=%.17e admm_pinf=%.17e admm_gap=%.17e "
+           "admm_rho=%.17e solve_time=%.9e read_time=%.9e rank=%ld\n",
+           (long)c.admm.iter, c.admm.primal_objective_value, c.admm.dual_objective_value,
+           c.admm.l_1_primal_infeasibility, c.admm.primal_dual_gap, c.admm.rho, all_time, t_read,
+           (long)S->var->R[0]->rank);
+    fflush(stdout);
+    return 0;
+}
+
+/* Bounded phase-1 timing: ALM inner iterations / phase-1 wall time at fixed rank. */
+static int mode_alm_rate(int argc, char **argv) {
+    lorads_params p; default_params(&p);
+    p.fname = argv[2];
+    p.fixedRank = atoi(argv[3]);
+    long iters = atol(argv[4]);
+    p.phase1Tol = 1e-300;           /* never satisfied: keep iterating */
+    p.maxALMIter = 100000;
+    p.timeSecLimit = argc > 5 ? atof(argv[5]) : 30.0;  /* wall budget (the sample bound) */
+    p.reoptLevel = 0;
+    ref_ctx c; memset(&c, 0, sizeof(c));
+    double t_read, tss;
+    if (ref_setup(&c, &p, &t_read, &tss)) { printf("REF_RATE read_failed\n"); return 0; }
+    (void)iters;
+    double t0 = now_s();
+    LORADS_ALMOptimize(&p, c.S, &c.alm, p.maxALMIter, t0);
+    double dt = now_s() - t0;
+    printf("REF_RATE inner=%ld seconds=%.9e rate=%.9e rank=%ld\n", (long)c.alm.innerIter, dt,
+           c.alm.innerIter / dt, (long)c.S->var->R[0]->rank);
+    return 0;
+}
+
+/* ---------------- kernels mode: one call of each hot-path operator ---------------- */
+static void col_copy(double *dst, const double **src, lorads_int len) {
+    memcpy(dst, *src, sizeof(double) * len); *src += len;
+}
+
+static int mode_kernels(int argc, char **argv) {
+    lorads_params p; default_params(&p);
+    p.fname = argv[2];
+    p.fixedRank = atoi(argv[3]);
+    ref_ctx c; memset(&c, 0, sizeof(c));
+    double t_read, tss;
+    if (ref_setup(&c, &p, &t_read, &tss)) { fprintf(stderr, "read failed\n"); return 1; }
+    lorads_solver *S = c.S;
+    lorads_int m = S->nRows, K = S->nCones, NR = 0;
+    for (lorads_int k = 0; k < K; ++k) NR += S->var->R[k]->nRows * S->var->R[k]->rank;
+    FILE *fi = fopen(argv[4], "rb");
+    if (!fi) return 1;
+    fseek(fi, 0, SEEK_END); long sz = ftell(fi); fseek(fi, 0, SEEK_SET);
+    double *in = malloc(sz); if (fread(in, 1, sz, fi) != (size_t)sz) return 1; fclose(fi);
+    const double *ip = in;
+    /* layout: R, D, G, s1, y1, s2, y2, U, V (each NR, col-major per cone, cones concatenated),
+               lambda[m], cvs[m], rho, beta1, beta2, rho_admm, cg_tol */
+    double *R = malloc(8 * NR), *D = malloc(8 * NR), *G = malloc(8 * NR), *s1 = malloc(8 * NR),
+           *y1 = malloc(8 * NR), *s2 = malloc(8 * NR), *y2 = malloc(8 * NR), *U = malloc(8 * NR),
+           *V = malloc(8 * NR);
+    col_copy(R, &ip, NR); col_copy(D, &ip, NR); col_copy(G, &ip, NR); col_copy(s1, &ip, NR);
+    col_copy(y1, &ip, NR); col_copy(s2, &ip, NR); col_copy(y2, &ip, NR); col_copy(U, &ip, NR);
+    col_copy(V, &ip, NR);
+    double *lam = malloc(8 * m), *cvs = malloc(8 * m);
+    col_copy(lam, &ip, m); col_copy(cvs, &ip, m);
+    double rho = *ip++, beta1 = *ip++, beta2 = *ip++, rho_admm = *ip++, cg_tol = *ip++;
+
+    FILE *fo = fopen(argv[5], "wb");
+    lorads_int off;
+#define LOAD(dstArr, src) do { off = 0; for (lorads_int k = 0; k < K; ++k) { \
+        lorads_int len = dstArr[k]->nRows * dstArr[k]->rank; \
+        memcpy(dstArr[k]->matElem, (src) + off, 8 * len); off += len; } } while (0)
+#define DUMPF(arr) do { off = 0; for (lorads_int k = 0; k < K; ++k) { \
+        lorads_int len = arr[k]->nRows * arr[k]->rank; \
+        fwrite(arr[k]->matElem, 8, len, fo); off += len; } } while (0)
+
+    /* (1) q1 = 2 A(sym(R D^T)), p1 = 2 <C, sym(R D^T)>, q2 = A(D D^T), p2 = <C, D D^T>
+           via ALMCalq12p12 (lorads_alm.c:714) */
+    LOAD(S->var->R, R);
+    LOAD(S->var->U, D);
+    double p12[2];
+    ALMCalq12p12(S, S->var->rLp, S->var->uLp, S->var->R, S->var->U, S->var->ARDSum, S->var->ADDSum, p12);
+    fwrite(S->var->ARDSum, 8, m, fo); fwrite(&p12[0], 8, 1, fo);
+    fwrite(S->var->ADDSum, 8, m, fo); fwrite(&p12[1], 8, 1, fo);
+    /* (2) A(R R^T) from scratch + pinf (primalInfeasibility, alg_common.c:386) and <C, R R^T> */
+    S->pObjVal = 0.0; S->dObjVal = 0.0;
+    primalInfeasibility(S, S->var->R, S->var->R, S->var->rLp, S->var->rLp);
+    fwrite(S->var->constrValSum, 8, m, fo);
+    fwrite(&S->dimacError[LORADS_DIMAC_ERROR_CONSTRVIO_L1], 8, 1, fo);
+    LORADSCalObjRR_ALM(S);
+    fwrite(&S->pObjVal, 8, 1, fo);
+    /* (3) gradient G = 2 (C + A^*(rho (cvs - b) - lambda)) R  (ALMCalGrad, lorads_alm.c:74) */
+    memcpy(S->var->dualVar, lam, 8 * m);
+    memcpy(S->var->constrValSum, cvs, 8 * m);
+    double lag = 0.0;
+    ALMCalGrad(S, S->var->rLp, S->var->gradLp, S->var->R, S->var->Grad, &lag, rho);
+    DUMPF(S->var->Grad); fwrite(&lag, 8, 1, fo);
+    /* (4) line search on (q0 = b - cvs, q1, q2, p1, p2)  (ALMLineSearch, lorads_alm.c:266) */
+    {
+        /* recompute q1,q2 for (R,D) since (2) overwrote constrVal */
+        LOAD(S->var->R, R); LOAD(S->var->U, D);
+        ALMCalq12p12(S, S->var->rLp, S->var->uLp, S->var->R, S->var->U, S->var->ARDSum, S->var->ADDSum, p12);
+        double *q0 = malloc(8 * m);
+        for (lorads_int i = 0; i < m; ++i) q0[i] = S->rowRHS[i] - cvs[i];
+        double tau = 0.0;
+        lorads_int rn = ALMLineSearch(rho, m, lam, p12[0], p12[1], q0, S->var->ARDSum, S->var->ADDSum, &tau);
+        double rnd = (double)rn;
+        fwrite(&tau, 8, 1, fo); fwrite(&rnd, 8, 1, fo);
+        free(q0);
+    }
+    /* (5) L-BFGS two-loop with 2 pairs (LBFGSDirection, lorads_alm.c:468-505):
+           newest pair = (s1, y1, beta1), older = (s2, y2, beta2) */
+    {
+        LOAD(S->var->Grad, G);
+        lbfgs_node *head = S->lbfgsHis;          /* next slot to write  */
+        lbfgs_node *newest = head->prev, *older = newest->prev;
+        memcpy(newest->s, s1, 8 * NR); memcpy(newest->y, y1, 8 * NR); newest->beta = beta1;
+        memcpy(older->s, s2, 8 * NR); memcpy(older->y, y2, 8 * NR); older->beta = beta2;
+        LBFGSDirection(&p, S, head, S->var->gradLp, S->var->uLp, S->var->Grad, S->var->U, 5);
+        LBFGSDirectionUseGrad(S, S->var->uLp, S->var->gradLp, S->var->U, S->var->Grad);
+        DUMPF(S->var->U);
+        LBFGSDirection(&p, S, head, S->var->gradLp, S->var->uLp, S->var->Grad, S->var->U, 1);
+        DUMPF(S->var->U);
+    }
+    /* (6) one ADMM half-step: solve for U with V fixed (LORADSUpdateSDPVarOne,
+           lorads_admm.c:564), state A(UV^T) from (U, V), dual = lambda */
+    {
+        LOAD(S->var->U, U); LOAD(S->var->V, V);
+        memcpy(S->var->dualVar, lam, 8 * m);
+        LORADSInitConstrValAll(S, S->var->uLp, S->var->vLp, S->var->U, S->var->V);
+        LORADSInitConstrValSum(S);
+        S->cgIter = 0;
+        LORADSUpdateSDPVarOne(S, S->var->U[0], S->var->V[0], 0, rho_admm, cg_tol, 800);
+        DUMPF(S->var->U);
+        fwrite(S->var->bLinSys[0], 8, S->var->U[0]->nRows * S->var->U[0]->rank, fo);
+        double it = (double)S->CGLinsys[0]->iter;
+        fwrite(&it, 8, 1, fo);
+    }
+    fclose(fo);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 3) { fprintf(stderr, "usage: %s solve|alm_rate|kernels file ...\n", argv[0]); return 2; }
+    if (!strcmp(argv[1], "solve")) return mode_solve(argc, argv);
+    if (!strcmp(argv[1], "alm_rate")) return mode_alm_rate(argc, argv);
+    if (!strcmp(argv[1], "kernels")) return mode_kernels(argc, argv);
+    return 2;
+}
