@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""ALM iterations/s of the MI355X low-rank SDP solver on MaxCut G67 (BASELINE.json).
+
+Workload: G67-structured MaxCut (2-D toroidal grid 100 x 100, weights +-1, n = m =
+10 000; the real Gset file is not in the reference checkout),
+default LoRADS rank r = ceil(2 ln n) = 19 held fixed so every step costs the same.
+A "step" is one ALM inner iteration (alm_state.innerIter, lorads_alm.c:1372) of the
+real phase-1 control flow (dual/rho updates and oracle-rank records included) on
+the device.  Multi-GPU: one process per GPU, each solving its own instance (the
+reference's instance-level batching, dataset/run_lorads.sh:85-114): weak scaling,
+no data-path collective; barrier + max-over-ranks timing.
+
+Prints one JSON line (rank 0).  Extra fields: wall-clock to eps = 1e-5 (full
+ALM+ADMM solve, Gset flags), the A(UU^T) kernel roofline, and the reference CPU
+path timed on this host (cpu_baseline).
+"""
+import argparse
+import importlib
+import json
+import os
+import re
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "ltr-lowrank-sdp_amd"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def instance_for(rank_id, rows, cols, cache):
+    inst = importlib.import_module(PKG + ".instances")
+    path = os.path.join(cache, f"torus{rows}x{cols}_s{67 + rank_id}.dat-s")
+    if not os.path.exists(path):
+        tmp = path + f".tmp{os.getpid()}"
+        inst.maxcut_torus(tmp, rows, cols, seed=67 + rank_id)
+        os.replace(tmp, path)
+    return path
+
+
+def cpu_reference_rate(path, rank, seconds):
+    """Reference LoRADS (oracle/_ref, built from /root/reference sources) phase-1
+    rate on the host; falls back to the CPU restatement if the reference build is absent."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "lorads_ref_harness")
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1")
+    if os.path.exists(harness):
+        r = subprocess.run([harness, "alm_rate", path, str(rank), "0", str(seconds)], capture_output=True,
+                           text=True, env=env, timeout=seconds * 6 + 120)
+        m = re.search(r"REF_RATE inner=(\d+) seconds=(\S+)", r.stdout)
+        if m:
+            return int(m.group(1)), float(m.group(2)), "reference"
+    orc = os.path.join(ROOT, "oracle", "_build", "lrsdp_oracle")
+    if not os.path.exists(orc):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    r = subprocess.run([orc, "alm_rate", path, str(rank), str(seconds)], capture_output=True, text=True,
+                       timeout=seconds * 6 + 120)
+    m = re.search(r"ORACLE_RATE inner=(\d+) seconds=(\S+)", r.stdout)
+    return int(m.group(1)), float(m.group(2)), "port"
+
+
+def cpu_reference_solve(path, flags, timeout):
+    harness = os.path.join(ROOT, "oracle", "_ref", "lorads_ref_harness")
+    if not os.path.exists(harness):
+        return None
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1")
+    t0 = time.perf_counter()
+    r = subprocess.run([harness, "solve", path] + flags, capture_output=True, text=True, env=env, timeout=timeout)
+    wall = time.perf_counter() - t0
+    m = re.search(r"solve_time=(\S+)", r.stdout)
+    p = re.search(r"alm_pobj=(\S+)", r.stdout)
+    if not m:
+        return None
+    return {"solve_time_sec": float(m.group(1)), "process_wall_sec": wall, "alm_pobj": float(p.group(1))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--rows", type=int, default=100)
+    ap.add_argument("--cols", type=int, default=100)
+    ap.add_argument("--rank", type=int, default=0, help="fixed rank (0 = LoRADS default)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-eps", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank_id = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    def allreduce(v, op):
+        if dist is None:
+            return v
+        import torch
+        t = torch.tensor([float(v)], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    solver = importlib.import_module(PKG + ".solver")
+    cache = os.path.join(ROOT, ".bench_instances")
+    os.makedirs(cache, exist_ok=True)
+    path = instance_for(rank_id, args.rows, args.cols, cache)
+    sv = solver.Solver(path, device=local)
+    r = args.rank if args.rank > 0 else sv.determine_rank()[0]
+    n = sv.dims[0]
+    kw = dict(fixedRank=r, reoptLevel=0)
+
+    # warmup: W untimed inner iterations (same start point as the timed run)
+    if args.warmup > 0:
+        sv.alm_throughput(0, args.warmup, **kw)
+    barrier_sync()
+    t0 = time.perf_counter()
+    out = sv.alm_throughput(0, args.steps, **kw)
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    t_max = allreduce(dt, dist.ReduceOp.MAX if dist else None)
+    done = out["done"]
+    done_tot = allreduce(done, dist.ReduceOp.SUM if dist else None)
+
+    # A(U U^T) kernel (SDDMM on the pattern + per-constraint gather) on the final iterate,
+    # HIP events on the solver stream; algorithmic bytes (delta = 1):
+    #   8 n r + 16 Z + 4 (m + 1) + 8 m
+    auut_ms = sv.time_auut(200)
+    m, Z = sv.m, sv.nnz
+    bytes_a = 8.0 * n * r + 16.0 * Z + 4.0 * (m + 1) + 8.0 * m
+    achieved = bytes_a / (auut_ms * 1e-3) / 1e9
+
+    line = {
+        "metric": "ALM iters/sec, MaxCut G67 (torus 100x100 +-1, n=m=10000), fixed default rank",
+        "value": done_tot / t_max,
+        "unit": "ALM inner iterations/s",
+        "n_gpus": world,
+        "steps": int(done),
+        "warmup": args.warmup,
+        "ms_per_step": t_max * 1e3 / max(1, done),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: seeded G67-structured toroidal grid (real Gset file absent), one instance per rank",
+        "config": {"workload": f"MaxCut torus {args.rows}x{args.cols} (G67 structure)", "n": n, "m": m,
+                   "rank": r, "pattern_slots": sv.nslots, "constraint_nnz": Z,
+                   "flags": "--fixedRank %d --reoptLevel 0, phase-1 exit disabled, budget = steps" % r,
+                   "parallelism": f"replicas x{world} (instance-level, weak)"},
+        "roofline": {"bound": "hbm", "kernel": "A(UU^T): k_sddmm<XX^T> + k_gather", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": bytes_a, "avg_launch_us": auut_ms * 1e3},
+    }
+    if rank_id == 0 and world == 1 and not args.no_eps:
+        eps_flags = dict(reoptLevel=0, heuristicFactor=10.0, phase1Tol=1e-2, phase2Tol=1e-5)
+        t1 = time.perf_counter()
+        sol = sv.solve(**eps_flags)
+        wall = time.perf_counter() - t1
+        line["wall_clock_to_eps"] = {"eps": 1e-5, "flags": "--reoptLevel 0 --heuristicFactor 10 --phase1Tol 1e-2",
+                                     "solve_time_sec": sol["solve_time"], "call_wall_sec": wall,
+                                     "alm_inner": sol["alm_inner"], "admm_iter": sol["admm_iter"],
+                                     "primal_obj": sol["pobj"], "alm_primal_obj": sol["alm_pobj"],
+                                     "pinf": sol["pinf"], "gap": sol["gap"], "rank": sol["final_rank"]}
+    if rank_id == 0 and world == 1 and not args.no_cpu:
+        it, sec, kind = cpu_reference_rate(path, r, args.cpu_seconds)
+        line["cpu_baseline"] = {"value": it / sec, "unit": "ALM inner iterations/s", "cores": 1, "kind": kind,
+                                "sample": f"phase-1 ALM on the same instance at rank {r}, {it} inner iterations "
+                                          f"in {sec:.1f} s wall (OPENBLAS_NUM_THREADS=1)"}
+        if not args.no_eps:
+            ref = cpu_reference_solve(path, ["--reoptLevel", "0", "--heuristicFactor", "10", "--phase1Tol", "1e-2"],
+                                      timeout=600)
+            if ref:
+                line["cpu_baseline"]["wall_clock_to_eps"] = ref
+    sv.close()
+    if rank_id == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

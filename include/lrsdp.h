@@ -1,0 +1,134 @@
+/*
+ * lrsdp.h -- C-ABI of the MI355X-native low-rank SDP inner solver (liblrsdp.so).
+ *
+ * This is the in-process boundary that replaces the reference's operator
+ * vtables on the hot path:
+ *   - algorithm slots  lorads_func        (lorads/src/src_semi/data/def_lorads_solver.h:169-187,
+ *                                          bound in data/lorads_solver.c:1014-1053)
+ *   - cone slots       lorads_sdp_cone    (data/def_lorads_sdp_conic.h:100-124,
+ *                                          bound in data/lorads_sdp_conic.c:974-1029)
+ *   - coefficient slots sdp_coeff         (data/def_lorads_sdp_data.h:66-85)
+ *   - CG callback      Mvec               (linalg/def_lorads_cgs.h:71-72, linalg/lorads_cgs.c:107)
+ * The process boundary (the LoRADS CLI that benchmark.py calls,
+ * benchmark.py:240-262 / src_semi/main.c:256) is the `LoRADS_v_2_0_1-alpha`
+ * binary built on top of this library.
+ *
+ * Conventions: every function returns 0 on success and a negative code on
+ * failure (message via lrs_last_error()); no function calls exit().  All
+ * arrays crossing the boundary are host memory, column-major n x r per cone
+ * (the reference layout, lorads_alg_common.c:62-68), cones concatenated in
+ * cone order.  Device memory is owned by the context.
+ */
+#ifndef LRSDP_H
+#define LRSDP_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lrs_ctx lrs_ctx;
+
+/* LoRADS flags (main.c:56-86 defaults, main.c:125-154 names) + the three flags
+ * benchmark.py passes that the reference never implemented. */
+typedef struct {
+    double initRho, rhoMax, rhoCellingALM, rhoCellingADMM;
+    int maxALMIter, maxADMMIter;
+    double timesLogRank;
+    int fixedRank, initRank, rhoFreq;
+    double rhoFactor, ALMRhoFactor, rankUpdateFactor, phase1Tol, phase2Tol, timeSecLimit, heuristicFactor;
+    int lbfgsListLength;
+    double endTauTol, endALMSubTol;
+    int l2Rescaling, reoptLevel, dyrankLevel, highAccMode, oracleRankNaive;
+    /* additions (INTEGRATION.md "rank-schedule hook") */
+    int disableOracle;
+    double nearStallFactor;
+    const int *rankSchedule;
+    int rankScheduleLen;
+    int verbose;          /* print the LoRADS-format iteration log to stdout */
+    long almInnerBudget;  /* >0: stop phase 1 after this many inner iterations (benchmarking) */
+    int skipADMM;         /* 1: phase 1 only */
+} lrs_params;
+
+typedef struct {
+    long alm_inner, alm_outer, admm_iter, cg_iter;
+    double alm_pobj, alm_dobj, alm_pinf, alm_gap, alm_rho;
+    double pobj, dobj, pinf, pinf_inf, gap, rho;   /* admm_state after main.c:519-525 */
+    double solve_time, alm_time, admm_time, read_time;
+    int status;          /* lorads_status: 0 unknown, 1 primal-dual optimal, 2 primal optimal, 3 maxiter, 4 time limit */
+    int retcode;         /* RET_CODE_* of phase 1 */
+    int final_rank, oracle_rank;
+    int traj1_len, traj2_len;
+    double rho_max;      /* params.rhoMax after LORADS_ALMtoADMM (written to the JSON) */
+} lrs_result;
+
+/* factor / vector selectors */
+enum { LRS_R = 0, LRS_D = 1, LRS_G = 2, LRS_U = 3, LRS_V = 4, LRS_S0 = 5, LRS_Y0 = 6, LRS_S1 = 7, LRS_Y1 = 8 };
+enum { LRS_LAMBDA = 0, LRS_CVS = 1, LRS_Q1 = 2, LRS_Q2 = 3, LRS_B = 4 };
+
+void lrs_params_default(lrs_params *p);
+const char *lrs_last_error(void);
+const char *lrs_version(void);
+
+int lrs_ctx_create(int device, lrs_ctx **out);
+void lrs_ctx_destroy(lrs_ctx *ctx);
+
+/* SDPA .dat-s reader + presolve + upload (replaces LReadSDPA io/lorads_file_io.c:59,
+ * LORADSPreprocess data/lorads_solver.c:278, AConePresolveData data/lorads_sdp_conic.c:1185).
+ * read_seconds may be NULL. */
+int lrs_load_sdpa(lrs_ctx *ctx, const char *path, double *read_seconds);
+int lrs_problem_info(lrs_ctx *ctx, int *m, int *ncones, int *dims, long *nslots, long *nnz_constraints);
+
+/* ranks: LORADSDetermineRank (data/lorads_solver.c:406) given flags; or explicit. */
+int lrs_determine_rank(lrs_ctx *ctx, const lrs_params *p, int *ranks_out);
+int lrs_set_rank(lrs_ctx *ctx, const int *ranks);
+int lrs_get_rank(lrs_ctx *ctx, int *ranks);
+
+int lrs_factor_set(lrs_ctx *ctx, int which, const double *colmajor);
+int lrs_factor_get(lrs_ctx *ctx, int which, double *colmajor);
+int lrs_vec_set(lrs_ctx *ctx, int which, const double *v);
+int lrs_vec_get(lrs_ctx *ctx, int which, double *v);
+
+/* ---- operators (one device pass each; scalars returned through pointers) ---- */
+/* ALMCalq12p12 (lorads_alm.c:714): q1 = 2A(sym RD^T), p1 = 2<C,sym RD^T>, q2 = A(DD^T), p2 = <C,DD^T> */
+int lrs_op_q12(lrs_ctx *ctx, double *q1, double *p1, double *q2, double *p2);
+/* primalInfeasibility (lorads_alg_common.c:386) on R: CVS <- A(RR^T); pinf; and <C,RR^T> */
+int lrs_op_constr_rr(lrs_ctx *ctx, double *cvs, double *pinf, double *pobj);
+/* ALMCalGrad (lorads_alm.c:74) from LAMBDA, CVS at rho: G <- 2(C + A^*(M1))R */
+int lrs_op_grad(lrs_ctx *ctx, double rho, double *lag_norm_sq);
+/* ALMLineSearch (lorads_alm.c:266) on the state left by lrs_op_q12 with q0 = b - CVS */
+int lrs_op_line_search(lrs_ctx *ctx, double rho, double *tau, int *root_num);
+/* LBFGSDirection + LBFGSDirectionUseGrad (lorads_alm.c:468-505, :607-627) from G and
+ * the ring (S0,Y0 = newest pair with beta_new; S1,Y1 = older pair with beta_old),
+ * node_num in {0,1,2}; result in D. */
+int lrs_op_lbfgs(lrs_ctx *ctx, int node_num, double beta_new, double beta_old);
+/* LORADSUpdateSDPVarOne (lorads_admm.c:564) for U of cone 0 with V fixed; state:
+ * LAMBDA and A(UV^T) from the current U, V.  Returns CG iterations and the RHS. */
+int lrs_op_admm_half(lrs_ctx *ctx, double rho, double cg_tol, int cg_maxit, int *cg_iters, double *rhs);
+/* Gram R^T R of cone k (r x r, row-major) */
+int lrs_op_gram(lrs_ctx *ctx, int cone, int which, double *gram);
+
+/* ---- whole solves ---- */
+/* main.c:380-610 flow (reoptLevel>=1 restarts not yet on the device path: see DESIGN.md). */
+int lrs_solve(lrs_ctx *ctx, const lrs_params *p, lrs_result *res);
+/* trajectory (phase 1 then phase 2) after lrs_solve: curr and oracle ranks */
+int lrs_trajectory(lrs_ctx *ctx, int phase, int *curr_rank, int *oracle_rank, int cap);
+/* JSON like lorads_logging.c:618-712 */
+int lrs_write_json(lrs_ctx *ctx, const char *path, const char *problem_id, const char *file_path,
+                   const lrs_result *res, const lrs_params *p);
+
+/* Phase-1 throughput: runs `warmup` then `steps` ALM inner iterations at the
+ * current rank (phase1Tol effectively off), timing the steps with device events.
+ * kernel_ms (optional) receives per-kernel average durations of the A(UU^T)
+ * SDDMM kernel measured with HIP events on the solver stream. */
+int lrs_alm_throughput(lrs_ctx *ctx, const lrs_params *p, long warmup, long steps, double *seconds,
+                       long *done, double *sddmm_avg_ms, double *iter_avg_ms);
+
+/* Mirror the iteration log into a file (the reference's --logfile). */
+int lrs_set_log_path(lrs_ctx *ctx, const char *path);
+
+/* Standalone A(UU^T) (SDDMM + gather) timing on R: reps launches, average ms per launch. */
+int lrs_time_auut(lrs_ctx *ctx, int reps, double *avg_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,164 @@
+// lrs_device.h -- device-side data model and kernel launchers for the MI355X
+// (gfx950) low-rank SDP inner solver.  Host code (lrs_solver.cpp) owns all
+// scalar control; the hot path runs as the kernels declared here.
+//
+// Data layout in HBM (DESIGN.md "Data layout"):
+//  * factors R, D, G, L-BFGS s/y, U, V: ROW-major n x ld per cone (ld = G*E >= r,
+//    zero padded), all cones concatenated in one buffer ("factor buffer").  A row
+//    is read by one lane group of G lanes, E consecutive doubles per lane.
+//  * pattern ("slots"): the union of the lower-triangle nonzeros of C and every
+//    A_i of a cone, ordered row-major (row i, col <= i); all cones' slots
+//    concatenated in one global slot space.
+//  * symmetric adjacency per cone (row i -> (j, slot)) for the row-owned SpMM;
+//    its prefix with j <= i is the lower part used by the row-owned SDDMM.
+//  * constraints: CSR over global slots with the symmetric weight folded in
+//    ((2 - delta_ij) * a, data/lorads_sdp_data.c:803-856) for A(.) ; the inverse
+//    slot -> (constraint, a) CSR for A^*(y) (data/lorads_sdp_data.c:878-922).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace lrs {
+
+constexpr int kBlock = 256;          // threads per block (4 waves)
+constexpr int kMaxPartialBlocks = 1024;
+constexpr int kMaxPartialVals = 16;
+
+// ---- ALM inner-loop control block (double array, double-buffered by iteration parity)
+enum CtrlIdx {
+    C_ACTIVE = 0,   // 1 while the inner L-BFGS loop runs
+    C_EXIT,         // exit reason (ExitReason)
+    C_INNER,        // alm_state.innerIter
+    C_LOCAL,        // localIter
+    C_CLEAR,        // clearLBFGS
+    C_HEAD,         // L-BFGS ring head (next slot to write)
+    C_GCUR,         // which G buffer holds the current gradient
+    C_PENDING,      // previous iteration left partials to fold
+    C_RCVAL,        // rho_certificate_val
+    C_LAG,          // ||G||^2
+    C_PINF1,        // l_1 primal infeasibility
+    C_PINFINF,      // l_inf primal infeasibility
+    C_BETA0, C_BETA1,   // 1/<y,s> per ring slot
+    C_YY0, C_YY1,       // <y,y> per ring slot
+    C_NODENUM,
+    C_CG, C_CS0, C_CY0, C_CS1, C_CY1,  // D = -(cG G + cs0 s0 + cy0 y0 + cs1 s1 + cy1 y1)
+    C_DG,           // <D, G> after LBFGSDirectionUseGrad
+    C_LASTTAU,
+    // dots of the current gradient with the ring (stash, valid when PENDING == 2)
+    C_DSG, C_DYG, C_DSOG, C_DYOG, C_DSOY, C_DYOY,
+    C_NCTRL = 40
+};
+enum ExitReason {
+    EXIT_NONE = 0,
+    EXIT_CONVERGED = 1,   // rho_certificate_val - tol <= endALMSubTol (while condition)
+    EXIT_PHASE1 = 2,      // l_inf pinf <= phase1Tol  -> END_ALM
+    EXIT_LOCAL800 = 3,    // localIter > 800          -> break
+    EXIT_TINYTAU = 4,     // |tau| < endTauTol        -> UpdateRho
+    EXIT_NUMERR = 5,      // no root                  -> RET_CODE_NUM_ERR
+    EXIT_BUDGET = 6       // bench budget of inner iterations reached
+};
+// ---- parameters read by the device loop
+enum ParIdx {
+    P_RHO = 0, P_RCTOL, P_ENDSUB, P_ENDTAU, P_PH1TOL, P_BN1, P_BNINF, P_CNINF,
+    P_HIGHACC, P_BUDGET, P_L, P_GAP, P_NPAR = 16
+};
+// ---- line-search result, double-buffered by parity: tau, rootNum, flag
+enum LsIdx { LS_TAU = 0, LS_ROOTNUM, LS_FLAG, LS_N = 4 };
+// ---- finals of the standalone launchers (g_tmpfin offsets)
+enum TmpFinIdx { TF_SD = 0, TF_GATHER = 128, TF_RESID = 129, TF_DOT = 130, TF_SPMM = 131, TF_N = 256 };
+constexpr int kMaxCones = 64;
+
+struct Layout {
+    int G = 1, E = 1, ld = 1;
+};
+Layout choose_layout(int r);
+
+struct DevCone {
+    int n = 0, r = 0, ld = 0, G = 0, E = 0;
+    long foff = 0;      // offset (doubles) of this cone in the factor buffer
+    int slot_off = 0, P = 0;
+    int *adj_ptr = nullptr, *adj_low = nullptr, *adj_col = nullptr, *adj_slot = nullptr;
+    long adj_nnz = 0;
+};
+
+struct DevProblem {
+    int m = 0, K = 0;
+    long NRpad = 0;     // factor buffer length (doubles)
+    int Ptot = 0;
+    long Z = 0;
+    double *b = nullptr;
+    double *Cw = nullptr, *Craw = nullptr;                   // [Ptot]
+    int *con_ptr = nullptr, *con_slot = nullptr;             // [m+1], [Z]
+    double *con_w = nullptr;                                 // [Z]
+    int *slot_ptr = nullptr, *slot_con = nullptr;            // [Ptot+1], [Z]
+    double *slot_a = nullptr;                                // [Z]
+    std::vector<DevCone> cones;
+};
+
+// Scratch shared by the kernels of one solve.
+struct DevWork {
+    double *R = nullptr, *D = nullptr, *G[2] = {nullptr, nullptr};
+    double *ls[2] = {nullptr, nullptr}, *ly[2] = {nullptr, nullptr};
+    double *U = nullptr, *V = nullptr, *X = nullptr;         // ADMM / scratch factors
+    double *cg_r = nullptr, *cg_p = nullptr, *cg_Q = nullptr, *cg_b = nullptr, *M2 = nullptr;
+    double *uvt0 = nullptr, *uvt1 = nullptr, *uvt2 = nullptr, *S = nullptr;   // [Ptot]
+    double *lam = nullptr, *cvs = nullptr, *q1 = nullptr, *q2 = nullptr, *M1 = nullptr, *wtmp = nullptr;
+    double *cvc = nullptr;                                   // per-cone A(UV^T), K*m
+    double *part = nullptr;    // [kMaxPartialVals][kMaxPartialBlocks] partial sums (scratch A)
+    double *partB = nullptr;   // second partial buffer (scratch B)
+    double *partC = nullptr;   // third partial buffer (scratch C)
+    double *ctrl = nullptr;    // [2][C_NCTRL]
+    double *lsres = nullptr;   // [2][LS_N]
+    double *par = nullptr;     // [P_NPAR]
+    double *gram = nullptr;    // gram partials
+};
+
+// ---------------------------- launchers -----------------------------------
+// All launchers enqueue on `st` and return hipSuccess / an error code.
+
+// uvt_out0[slot] (and uvt_out1) over the cone's pattern; objective partials
+// sum_slot Cw*uvt -> part[0 or 1][pblk_off + b].  mode: 0 = sym(X Y^T),
+// 1 = X X^T (Y ignored), 2 = sym(X Y^T) into out0 and Y Y^T into out1.
+int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const double *Y,
+                 double *out0, double *out1, double *part, int pblk_off, int *nblk_used,
+                 hipStream_t st);
+// out[i] = scale * sum_e w_e uvt[slot_e] for every constraint (A(.)), plus
+// partial sum of (b - out)^2 if vio_part != nullptr (primal residual).
+int launch_gather(const DevProblem &P, const double *uvt, double scale, double *out,
+                  const double *b_for_vio, double *vio_part, hipStream_t st, int *nblk_used);
+// S[slot] = (withC ? Craw[slot] : 0) + sum_(con,a) w[con] * a
+int launch_wsum(const DevProblem &P, const double *w, int withC, double *S, hipStream_t st);
+// out = scale * S X (+ addX * X) per cone, partial ||out||^2 -> part[0][pblk_off+b]
+int launch_spmm(const DevProblem &P, int cone, const double *S, const double *X, double scale,
+                const double *addX, double addScale, double *out, double *part, int pblk_off,
+                int *nblk_used, hipStream_t st);
+// generic BLAS-1 over the factor buffer / m-vectors with partial dots
+int launch_axpby(long n, double a, const double *x, double b, double *y, hipStream_t st);
+int launch_dot(long n, const double *x, const double *y, double *part, hipStream_t st, int *nblk_used);
+int launch_fill(long n, double v, double *x, hipStream_t st);
+// lam += rho (b - cvs)
+int launch_dual_update(const DevProblem &P, double rho, double *lam, const double *cvs, hipStream_t st);
+// M1 = -lam - rho b + rho cvs   (ALMSetGrad, lorads_alm.c:38-50)
+int launch_alm_m1(const DevProblem &P, double rho, const double *lam, const double *cvs, double *M1,
+                  hipStream_t st);
+// Gram partials X^T X (avg=0) or ((U+V)/2)^T((U+V)/2) (avg=1) of one cone -> gram [nblk][r*r]
+int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y, int avg,
+                double *gram_part, int *nblk_used, hipStream_t st);
+
+// ---- fused ALM inner iteration (device-side control; see lrs_kernels.hip) ----
+struct AlmIterArgs {
+    const DevProblem *P;
+    DevWork *W;
+    int nblk_grad;     // partial blocks written by grad (sum over cones)
+    int nblk_rr;       // partial blocks written by gather_rr
+    int nblk_sddmm;    // partial blocks written by sddmm
+    int nblk_q;        // partial blocks written by gather_q
+};
+int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st);
+
+const char *last_device_error();
+
+}  // namespace lrs

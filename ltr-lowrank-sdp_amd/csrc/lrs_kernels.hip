@@ -1,0 +1,1082 @@
+// lrs_kernels.hip -- hand-written CDNA4 (gfx950) kernels for the low-rank SDP
+// hot path.  FP64 everywhere (the reference computes in double).
+//
+// Row-owned kernels give each factor row to a group of G lanes (E doubles per
+// lane, ld = G*E); cross-lane dot products are shuffle butterflies inside the
+// group.  Scalar reductions are written as per-block partials and finalised by
+// the last-arriving block (agent-scope release/acquire ticket, cdna_hip_programming
+// Guideline 16), so every sum is taken in a fixed order: results are bitwise
+// reproducible run to run.
+//
+// Operator map (reference file:line in /root/reference/lorads/src/src_semi):
+//   k_sddmm      LORADSUVt sparse branch      lorads_alg/lorads_alg_common.c:51-71
+//                + objAUV (<C, .>)            data/lorads_sdp_conic.c:395-402
+//   k_gather     coneAUV / sparseAUV          data/lorads_sdp_conic.c:378-385, data/lorads_sdp_data.c:803-856
+//   k_wsum       addObjCoeff + sdpDataWSum    data/lorads_sdp_conic.c:448-460, :608-616
+//   k_spmm       mul_rk                        data/lorads_sdp_data.c:750-763
+//   ALM fused iteration (device control)     lorads_alg/lorads_alm.c:1302-1379
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "lrs_device.h"
+
+namespace lrs {
+
+static thread_local char g_err[512] = "";
+const char *last_device_error() { return g_err; }
+
+#define LRS_CHECK_LAUNCH()                                                               \
+    do {                                                                                 \
+        hipError_t e_ = hipGetLastError();                                               \
+        if (e_ != hipSuccess) {                                                          \
+            snprintf(g_err, sizeof(g_err), "%s:%d %s", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            return (int)e_;                                                              \
+        }                                                                                \
+    } while (0)
+
+Layout choose_layout(int r) {
+    static const int Gs[4] = {8, 16, 32, 64};
+    static const int Es[4] = {2, 1, 4, 3};   // preference order at equal ld
+    Layout best;
+    best.ld = 1 << 30;
+    for (int ei = 0; ei < 4; ++ei)
+        for (int gi = 0; gi < 4; ++gi) {
+            int ld = Gs[gi] * Es[ei];
+            if (ld >= r && ld < best.ld) { best.G = Gs[gi]; best.E = Es[ei]; best.ld = ld; }
+        }
+    return best;
+}
+
+// ------------------------------------------------------------------------
+// small device helpers
+// ------------------------------------------------------------------------
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <int E>
+__device__ __forceinline__ void ld_row(const double *__restrict__ p, double (&v)[E]) {
+    if constexpr (E == 2) {
+        double2 t = *reinterpret_cast<const double2 *>(p);
+        v[0] = t.x; v[1] = t.y;
+    } else if constexpr (E == 4) {
+        double2 t0 = reinterpret_cast<const double2 *>(p)[0];
+        double2 t1 = reinterpret_cast<const double2 *>(p)[1];
+        v[0] = t0.x; v[1] = t0.y; v[2] = t1.x; v[3] = t1.y;
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = p[e];
+    }
+}
+
+template <int E>
+__device__ __forceinline__ void st_row(double *__restrict__ p, const double (&v)[E]) {
+    if constexpr (E == 2) {
+        *reinterpret_cast<double2 *>(p) = make_double2(v[0], v[1]);
+    } else if constexpr (E == 4) {
+        reinterpret_cast<double2 *>(p)[0] = make_double2(v[0], v[1]);
+        reinterpret_cast<double2 *>(p)[1] = make_double2(v[2], v[3]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) p[e] = v[e];
+    }
+}
+
+// Block-reduce NV per-thread accumulators; thread 0 gets the block sums in s[].
+template <int NV>
+__device__ __forceinline__ void block_reduce(double (&acc)[NV], double (&s)[NV]) {
+    __shared__ double sh[NV][kBlock / 64];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        double t = wave_sum(acc[v]);
+        if (lane == 0) sh[v][wid] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            double t = 0.0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) t += sh[v][w];
+            s[v] = t;
+        }
+    }
+    __syncthreads();
+}
+
+// Write this block's partials; the last-arriving block sums all partials in
+// block order and stores fin[0..NV).  Release/acquire per Guideline 16.
+template <int NV>
+__device__ void partials_finalize(double (&acc)[NV], double *__restrict__ part, unsigned *ticket,
+                                  double *__restrict__ fin) {
+    double s[NV];
+    block_reduce<NV>(acc, s);
+    __shared__ unsigned is_last;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) part[v * kMaxPartialBlocks + blockIdx.x] = s[v];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (t == gridDim.x - 1) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!is_last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    double a2[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        double t = 0.0;
+        for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) t += part[v * kMaxPartialBlocks + b];
+        a2[v] = t;
+    }
+    double s2[NV];
+    block_reduce<NV>(a2, s2);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) fin[v] = s2[v];
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+static inline int grid_rows(long rows, int G) {
+    long threads = rows * G;
+    long b = (threads + kBlock - 1) / kBlock;
+    if (b < 1) b = 1;
+    if (b > kMaxPartialBlocks) b = kMaxPartialBlocks;
+    return (int)b;
+}
+static inline int grid_elems(long n, int per_thread) {
+    long b = (n / per_thread + kBlock - 1) / kBlock;
+    if (b < 1) b = 1;
+    if (b > kMaxPartialBlocks) b = kMaxPartialBlocks;
+    return (int)b;
+}
+
+// ------------------------------------------------------------------------
+// Scratch for tickets / finals (module-level device memory)
+// ------------------------------------------------------------------------
+enum TicketId { T_SDDMM = 0, T_GATHER, T_SPMM, T_DOT, T_GRAD, T_RR, T_Q, T_NT = 16 };
+__device__ unsigned g_tickets[64];
+
+// ------------------------------------------------------------------------
+// SDDMM over the lower pattern (row-owned).  MODE 0: sym(X Y^T); MODE 1: X X^T;
+// MODE 2: sym(X Y^T) -> out0 and Y Y^T -> out1.  Objective partials with Cw.
+// ------------------------------------------------------------------------
+template <int G, int E, int MODE>
+__global__ void __launch_bounds__(kBlock) k_sddmm(int n, int ld, const int *__restrict__ adj_ptr,
+                                                  const int *__restrict__ adj_low, const int *__restrict__ adj_col,
+                                                  const int *__restrict__ adj_slot, const double *__restrict__ X,
+                                                  const double *__restrict__ Y, double *__restrict__ out0,
+                                                  double *__restrict__ out1, const double *__restrict__ Cw,
+                                                  double *part, unsigned *ticket, double *fin,
+                                                  const double *__restrict__ guard) {
+    if (guard && guard[C_ACTIVE] == 0.0) return;
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kBlock / G;
+    double acc[2] = {0.0, 0.0};
+    for (int i = grp; i < n; i += ngrp) {
+        double xi[E], yi[E];
+        ld_row<E>(X + (long)i * ld + lane * E, xi);
+        if constexpr (MODE != 1) ld_row<E>(Y + (long)i * ld + lane * E, yi);
+        const int kb = adj_ptr[i], ke = adj_low[i];
+        for (int k = kb; k < ke; ++k) {
+            const int j = adj_col[k];
+            const int s = adj_slot[k];
+            double xj[E];
+            ld_row<E>(X + (long)j * ld + lane * E, xj);
+            if constexpr (MODE == 1) {
+                double d = 0.0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) d += xi[e] * xj[e];
+                d = group_sum<G>(d);
+                if (lane == 0) { out0[s] = d; acc[0] += Cw[s] * d; }
+            } else {
+                double yj[E];
+                ld_row<E>(Y + (long)j * ld + lane * E, yj);
+                double d0 = 0.0, d1 = 0.0;
+                if (j != i) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) d0 += xi[e] * yj[e] + xj[e] * yi[e];
+                    d0 *= 0.5;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) d0 += xi[e] * yi[e];
+                }
+                d0 = group_sum<G>(d0);
+                if constexpr (MODE == 2) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) d1 += yi[e] * yj[e];
+                    d1 = group_sum<G>(d1);
+                }
+                if (lane == 0) {
+                    out0[s] = d0;
+                    acc[0] += Cw[s] * d0;
+                    if constexpr (MODE == 2) { out1[s] = d1; acc[1] += Cw[s] * d1; }
+                }
+            }
+        }
+    }
+    partials_finalize<2>(acc, part, ticket, fin);
+}
+
+// ------------------------------------------------------------------------
+// Gather A(uvt): one thread per constraint (cone < 0: all cones, summed in
+// cone order like LORADSInitConstrValSum).  out = scale * value.
+// Optional residual partial sum((b - out)^2).
+// ------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_gather(int m, int K, int cone, const int *__restrict__ con_ptr,
+                                                   const int *__restrict__ con_slot, const double *__restrict__ con_w,
+                                                   const double *__restrict__ uvt, double scale,
+                                                   double *__restrict__ out, const double *__restrict__ b,
+                                                   double *part, unsigned *ticket, double *fin) {
+    double acc[1] = {0.0};
+    const int k0 = cone < 0 ? 0 : cone, k1 = cone < 0 ? K : cone + 1;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        double tot = 0.0;
+        for (int k = k0; k < k1; ++k) {
+            const long row = (long)k * m + i;
+            double v = 0.0;
+            for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) v += con_w[e] * uvt[con_slot[e]];
+            tot += v;
+        }
+        tot *= scale;
+        out[i] = tot;
+        if (b) { double d = b[i] - tot; acc[0] += d * d; }
+    }
+    if (part) partials_finalize<1>(acc, part, ticket, fin);
+}
+
+// S[slot] = (withC ? Craw : 0) + sum w[con] a
+__global__ void __launch_bounds__(kBlock) k_wsum(int Ptot, const int *__restrict__ slot_ptr,
+                                                 const int *__restrict__ slot_con, const double *__restrict__ slot_a,
+                                                 const double *__restrict__ Craw, int withC,
+                                                 const double *__restrict__ w, double *__restrict__ S,
+                                                 const double *__restrict__ guard, const double *__restrict__ lsguard) {
+    if (guard && guard[C_ACTIVE] == 0.0) return;
+    if (lsguard && lsguard[LS_FLAG] != 0.0) return;
+    for (int s = blockIdx.x * kBlock + threadIdx.x; s < Ptot; s += gridDim.x * kBlock) {
+        double v = withC ? Craw[s] : 0.0;
+        for (int e = slot_ptr[s]; e < slot_ptr[s + 1]; ++e) v += w[slot_con[e]] * slot_a[e];
+        S[s] = v;
+    }
+}
+
+// out = scale * S X + addScale * addX (row-owned symmetric SpMM), partial ||out||^2
+template <int G, int E>
+__global__ void __launch_bounds__(kBlock) k_spmm(int n, int ld, const int *__restrict__ adj_ptr,
+                                                 const int *__restrict__ adj_col, const int *__restrict__ adj_slot,
+                                                 const double *__restrict__ S, const double *__restrict__ X,
+                                                 double scale, const double *__restrict__ addX, double addScale,
+                                                 double *__restrict__ out, double *part, unsigned *ticket,
+                                                 double *fin) {
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kBlock / G;
+    double nrm[1] = {0.0};
+    for (int i = grp; i < n; i += ngrp) {
+        double acc[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = 0.0;
+        for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
+            const double sv = S[adj_slot[k]];
+            double xj[E];
+            ld_row<E>(X + (long)adj_col[k] * ld + lane * E, xj);
+#pragma unroll
+            for (int e = 0; e < E; ++e) acc[e] += sv * xj[e];
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] *= scale;
+        if (addX) {
+            double a[E];
+            ld_row<E>(addX + (long)i * ld + lane * E, a);
+#pragma unroll
+            for (int e = 0; e < E; ++e) acc[e] += addScale * a[e];
+        }
+        st_row<E>(out + (long)i * ld + lane * E, acc);
+#pragma unroll
+        for (int e = 0; e < E; ++e) nrm[0] += acc[e] * acc[e];
+    }
+    if (part) partials_finalize<1>(nrm, part, ticket, fin);
+}
+
+// ---------------------------- BLAS-1 -------------------------------------
+__global__ void __launch_bounds__(kBlock) k_axpby(long n, double a, const double *__restrict__ x, double b,
+                                                  double *__restrict__ y) {
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long)gridDim.x * kBlock)
+        y[i] = a * x[i] + b * y[i];
+}
+__global__ void __launch_bounds__(kBlock) k_fill(long n, double v, double *__restrict__ x) {
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long)gridDim.x * kBlock) x[i] = v;
+}
+__global__ void __launch_bounds__(kBlock) k_dot(long n, const double *__restrict__ x, const double *__restrict__ y,
+                                                double *part, unsigned *ticket, double *fin) {
+    double acc[1] = {0.0};
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long)gridDim.x * kBlock) acc[0] += x[i] * y[i];
+    partials_finalize<1>(acc, part, ticket, fin);
+}
+__global__ void __launch_bounds__(kBlock) k_dual_update(int m, double rho, const double *__restrict__ b,
+                                                        double *__restrict__ lam, const double *__restrict__ cvs) {
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        double l = lam[i] + rho * b[i];      // lorads_alg_common.c:521
+        lam[i] = l + (-rho) * cvs[i];        // :523
+    }
+}
+__global__ void __launch_bounds__(kBlock) k_alm_m1(int m, double rho, const double *__restrict__ b,
+                                                   const double *__restrict__ lam, const double *__restrict__ cvs,
+                                                   double *__restrict__ M1) {
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock)
+        M1[i] = ((-lam[i]) + (-rho) * b[i]) + rho * cvs[i];   // lorads_alm.c:45-49
+}
+
+// Gram partials: block b accumulates rows [b*chunk, (b+1)*chunk) of X^T X into
+// gram_part[b][r][r] (upper+lower).  avg: rows are (X+Y)/2.
+__global__ void __launch_bounds__(kBlock) k_gram(int n, int r, int ld, const double *__restrict__ X,
+                                                 const double *__restrict__ Y, int avg,
+                                                 double *__restrict__ gram_part) {
+    extern __shared__ double rowbuf[];   // [8][ld]
+    const int chunk = (n + gridDim.x - 1) / gridDim.x;
+    const int i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+    const int rr = r * r;
+    double acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+    for (int ib = i0; ib < i1; ib += 8) {
+        const int nr = min(8, i1 - ib);
+        for (int t = threadIdx.x; t < nr * ld; t += kBlock) {
+            const int a = t / ld, c = t % ld;
+            double v = X[(long)(ib + a) * ld + c];
+            if (avg) v = 0.5 * (v + Y[(long)(ib + a) * ld + c]);
+            rowbuf[a * ld + c] = v;
+        }
+        __syncthreads();
+        for (int a = 0; a < nr; ++a) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int idx = threadIdx.x + q * kBlock;
+                if (idx < rr) {
+                    const int c1 = idx / r, c2 = idx % r;
+                    acc[q] += rowbuf[a * ld + c1] * rowbuf[a * ld + c2];
+                }
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int idx = threadIdx.x + q * kBlock;
+        if (idx < rr) gram_part[(long)blockIdx.x * rr + idx] = acc[q];
+    }
+}
+
+// ------------------------------------------------------------------------
+// Fused ALM inner iteration, lorads_alm.c:1302-1379.  Control state is
+// double-buffered by iteration parity: iteration t reads ctrl[(t-1)&1] and
+// block 0 of k_alm_dir writes ctrl[t&1]; every block computes the same state.
+// ------------------------------------------------------------------------
+struct AlmFinal {            // finals produced inside one iteration (device memory)
+    double sd[2];            // p1-part, p2-part  (sum over cones is done by the consumer)
+};
+
+// finals layout in `fin` (double array):
+//   FIN_SD  + 2*k : sddmm objective partials of cone k (RD, DD)
+//   FIN_Q   .. +5 : gather_q dots
+//   FIN_GR  + 9*k : grad dots of cone k
+//   FIN_RR        : residual
+enum FinIdx { FIN_SD = 0, FIN_Q = 64, FIN_GR = 80, FIN_RR = 400, FIN_N = 416 };
+__device__ double g_fin[FIN_N];
+__device__ double g_tmpfin[TF_N];
+
+__device__ int ctrl_compute(double *c, const double *__restrict__ prev, const double *__restrict__ par,
+                            const double *__restrict__ lsprev, int K) {
+    // executed by thread 0 only; c is shared memory.
+    // PENDING: 0 = nothing to fold (host start: clear == 0), 1 = fold the previous
+    // iteration's finals, 2 = dots already stashed in C_DSG..C_DYOY.
+    for (int q = 0; q < C_NCTRL; ++q) c[q] = prev[q];
+    const int L = (int)par[P_L];
+    if (c[C_ACTIVE] != 0.0 && c[C_PENDING] == 1.0) {
+        const double flag = lsprev[LS_FLAG];
+        if (flag == 1.0) {                      // rootNum == 0: RET_CODE_NUM_ERR (lorads_alm.c:1327)
+            c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_NUMERR;
+            c[C_PENDING] = 0.0;
+        } else if (flag == 2.0) {               // |tau| < endTauTol (lorads_alm.c:1331-1339)
+            c[C_INNER] += 1; c[C_LOCAL] += 1; c[C_CLEAR] += 1;
+            c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_TINYTAU;
+            c[C_PENDING] = 0.0;
+        } else {
+            double d[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            for (int k = 0; k < K; ++k)
+                for (int q = 0; q < 9; ++q) d[q] += g_fin[FIN_GR + 9 * k + q];
+            const int h = (int)c[C_HEAD];
+            // setlbfgsHisTwo (lorads_alm.c:861): beta = 1/<y,s>; ring head advances (:862)
+            c[C_BETA0 + h] = 1.0 / d[1];
+            c[C_YY0 + h] = d[2];
+            c[C_HEAD] = (double)((h + 1) % L);
+            c[C_GCUR] = 1.0 - c[C_GCUR];
+            c[C_LAG] = d[0];
+            c[C_LASTTAU] = lsprev[LS_TAU];
+            // primalInfeasibility (lorads_alg_common.c:393) and l_inf (lorads_alm.c:1359)
+            const double pinf1 = sqrt(g_fin[FIN_RR]) / (1.0 + par[P_BN1]);
+            c[C_PINF1] = pinf1;
+            c[C_PINFINF] = pinf1 * (1.0 + par[P_BN1]) / (1.0 + par[P_BNINF]);
+            c[C_DSG] = d[3]; c[C_DYG] = d[4]; c[C_DSOG] = d[5]; c[C_DYOG] = d[6];
+            c[C_DSOY] = d[7]; c[C_DYOY] = d[8];
+            c[C_PENDING] = 2.0;
+            if ((c[C_PINFINF] <= par[P_PH1TOL]) && ((par[P_GAP] <= par[P_PH1TOL]) || (par[P_HIGHACC] == 0.0))) {
+                c[C_INNER] += 1; c[C_LOCAL] += 1; c[C_CLEAR] += 1;
+                c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_PHASE1;
+            } else {
+                c[C_RCVAL] = sqrt(c[C_LAG]) / (1.0 + par[P_CNINF]);
+                c[C_INNER] += 1; c[C_LOCAL] += 1; c[C_CLEAR] += 1;
+                if (c[C_LOCAL] > 800) { c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_LOCAL800; }
+            }
+        }
+    } else if (c[C_PENDING] == 0.0) {
+        c[C_DSG] = c[C_DYG] = c[C_DSOG] = c[C_DYOG] = c[C_DSOY] = c[C_DYOY] = 0.0;
+    }
+    if (c[C_ACTIVE] != 0.0) {
+        if (!(c[C_RCVAL] - par[P_RCTOL] > par[P_ENDSUB])) { c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_CONVERGED; }
+        else if (par[P_BUDGET] > 0 && c[C_INNER] >= par[P_BUDGET]) { c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_BUDGET; }
+    }
+    if (c[C_ACTIVE] == 0.0) return 0;
+    // LBFGSDirection (lorads_alm.c:468-505) in coefficient space
+    if (((long)c[C_LOCAL]) % 300 == 0) c[C_CLEAR] = 0;
+    const int clear = (int)c[C_CLEAR];
+    const int nodeNum = clear == 0 ? 0 : (clear <= L - 1 ? clear : L);
+    c[C_NODENUM] = nodeNum;
+    const double GG = c[C_LAG];
+    const double sG = c[C_DSG], yG = c[C_DYG], soG = c[C_DSOG], yoG = c[C_DYOG], soy = c[C_DSOY], yoy = c[C_DYOY];
+    const int hn = ((int)c[C_HEAD] - 1 + L) % L;     // newest slot
+    const int ho = (hn - 1 + L) % L;                  // older slot
+    double cs[2] = {0, 0}, cy[2] = {0, 0};
+    double dg;
+    if (nodeNum == 0) {
+        dg = -GG;
+    } else if (nodeNum == 1) {
+        const double bn = c[C_BETA0 + hn], yyn = c[C_YY0 + hn];
+        const double a1 = bn * sG;
+        const double w1 = a1 - bn * (yG - a1 * yyn);
+        cy[hn] += -a1; cs[hn] += w1;
+        dg = -(GG - a1 * yG + w1 * sG);
+    } else {
+        const double bn = c[C_BETA0 + hn], yyn = c[C_YY0 + hn];
+        const double bo = c[C_BETA0 + ho], yyo = c[C_YY0 + ho];
+        const double a1 = bn * sG;
+        const double a2 = bo * (soG - a1 * soy);
+        const double w2 = a2 - bo * (yoG - a1 * yoy - a2 * yyo);
+        const double w1 = a1 - bn * (yG - a1 * yyn - a2 * yoy + w2 * soy);
+        cy[hn] += -a1; cy[ho] += -a2; cs[ho] += w2; cs[hn] += w1;
+        dg = -(GG - a1 * yG - a2 * yoG + w2 * soG + w1 * sG);
+    }
+    c[C_CG] = 1.0;
+    c[C_CS0] = cs[0]; c[C_CY0] = cy[0]; c[C_CS1] = cs[1]; c[C_CY1] = cy[1];
+    // LBFGSDirectionUseGrad (lorads_alm.c:618-626)
+    if (dg >= 0) { c[C_CS0] = c[C_CY0] = c[C_CS1] = c[C_CY1] = 0.0; dg = -GG; }
+    c[C_DG] = dg;
+    c[C_PENDING] = 1.0;
+    return 1;
+}
+
+__global__ void __launch_bounds__(kBlock) k_alm_dir(long NR, const double *__restrict__ par,
+                                                    const double *__restrict__ ctrl_prev, double *__restrict__ ctrl_cur,
+                                                    const double *__restrict__ lsprev, int K,
+                                                    double *__restrict__ D, const double *__restrict__ G0,
+                                                    const double *__restrict__ G1, const double *__restrict__ s0,
+                                                    const double *__restrict__ y0, const double *__restrict__ s1,
+                                                    const double *__restrict__ y1) {
+    __shared__ double c[C_NCTRL];
+    if (threadIdx.x == 0) ctrl_compute(c, ctrl_prev, par, lsprev, K);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < C_NCTRL) ctrl_cur[threadIdx.x] = c[threadIdx.x];
+    if (c[C_ACTIVE] == 0.0) return;
+    const double cg = c[C_CG], cs0 = c[C_CS0], cy0 = c[C_CY0], cs1 = c[C_CS1], cy1 = c[C_CY1];
+    const double *__restrict__ Gc = c[C_GCUR] == 0.0 ? G0 : G1;
+    const bool u0 = (cs0 != 0.0 || cy0 != 0.0), u1 = (cs1 != 0.0 || cy1 != 0.0);
+    for (long i = ((long)blockIdx.x * kBlock + threadIdx.x) * 2; i < NR; i += (long)gridDim.x * kBlock * 2) {
+        double2 g = *reinterpret_cast<const double2 *>(Gc + i);
+        double dx = cg * g.x, dy = cg * g.y;
+        if (u0) {
+            double2 a = *reinterpret_cast<const double2 *>(s0 + i), b = *reinterpret_cast<const double2 *>(y0 + i);
+            dx += cs0 * a.x + cy0 * b.x; dy += cs0 * a.y + cy0 * b.y;
+        }
+        if (u1) {
+            double2 a = *reinterpret_cast<const double2 *>(s1 + i), b = *reinterpret_cast<const double2 *>(y1 + i);
+            dx += cs1 * a.x + cy1 * b.x; dy += cs1 * a.y + cy1 * b.y;
+        }
+        *reinterpret_cast<double2 *>(D + i) = make_double2(-dx, -dy);
+    }
+}
+
+// q1 = 2 A(sym RD^T), q2 = A(DD^T) and the five line-search reductions
+// (ALMCalq12p12 lorads_alm.c:714-734 + ALMLineSearch :269-277)
+__global__ void __launch_bounds__(kBlock) k_alm_gather_q(int m, int K, const int *__restrict__ con_ptr,
+                                                         const int *__restrict__ con_slot,
+                                                         const double *__restrict__ con_w,
+                                                         const double *__restrict__ uRD, const double *__restrict__ uDD,
+                                                         const double *__restrict__ b, const double *__restrict__ cvs,
+                                                         const double *__restrict__ lam, const double *__restrict__ par,
+                                                         double *__restrict__ q1o, double *__restrict__ q2o,
+                                                         double *part, unsigned *ticket, double *fin,
+                                                         const double *__restrict__ guard) {
+    if (guard[C_ACTIVE] == 0.0) return;
+    const double rhoInv = 1.0 / par[P_RHO];
+    double acc[5] = {0, 0, 0, 0, 0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        double v1 = 0.0, v2 = 0.0;
+        for (int k = 0; k < K; ++k) {
+            const long row = (long)k * m + i;
+            double a1 = 0.0, a2 = 0.0;
+            for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) {
+                const double w = con_w[e];
+                const int s = con_slot[e];
+                a1 += w * uRD[s];
+                a2 += w * uDD[s];
+            }
+            v1 += a1; v2 += a2;
+        }
+        v1 *= 2.0;
+        q1o[i] = v1; q2o[i] = v2;
+        const double q0 = (b[i] - cvs[i]) + rhoInv * lam[i];
+        acc[0] += v2 * v2; acc[1] += v1 * v2; acc[2] += q0 * v2; acc[3] += v1 * v1; acc[4] += q0 * v1;
+    }
+    partials_finalize<5>(acc, part, ticket, fin);
+}
+
+// LORADScubic_equation (lorads_alm.c:191-231)
+__device__ int dev_cubic(double a, double b, double c, double d, double *res) {
+    const double A = b * b - 3 * a * c, B = b * c - 9 * a * d, C = c * c - 3 * b * d;
+    const double delta = B * B - 4 * A * C;
+    res[0] = res[1] = res[2] = 0.0;
+    if (A == 0 && B == 0) { res[0] = fmax(res[0], -c / b); return 1; }
+    if (delta > 0) {
+        const double Y1 = A * b + 1.5 * a * (-B + sqrt(delta));
+        const double Y2 = A * b + 1.5 * a * (-B - sqrt(delta));
+        const double Y13 = Y1 > 0 ? pow(Y1, 1.0 / 3) : -pow(-Y1, 1.0 / 3);
+        const double Y23 = Y2 > 0 ? pow(Y2, 1.0 / 3) : -pow(-Y2, 1.0 / 3);
+        res[0] = fmax(res[0], (-b - Y13 - Y23) / 3 / a);
+        return 1;
+    }
+    if (delta == 0 && A != 0 && B != 0) {
+        const double Kk = B / A;
+        res[0] = -b / a + Kk; res[1] = -Kk / 2;
+        return 2;
+    }
+    if (delta < 0) {
+        const double sqA = sqrt(A);
+        const double T = (A * b - 1.5 * a * B) / (A * sqA);
+        const double th = acos(T);
+        const double cs = cos(th / 3), sn = sqrt(3.0) * sin(th / 3);
+        res[0] = (-b - 2 * sqA * cs) / 3 / a;
+        res[1] = (-b + sqA * (cs + sn)) / 3 / a;
+        res[2] = (-b + sqA * (cs - sn)) / 3 / a;
+        return 3;
+    }
+    return 0;
+}
+
+__device__ __forceinline__ double quartic(double a, double b, double c, double d, double x) {
+    const double x2 = x * x;
+    return a * (x2 * x2) + b * (x2 * x) + c * x2 + d * x;
+}
+
+// ALMLineSearch (lorads_alm.c:266-333) from the finals; writes ls[0..2]
+__device__ void line_search(const double *__restrict__ par, int K, double *ls) {
+    double p1 = 0.0, p2 = 0.0;
+    for (int k = 0; k < K; ++k) { p1 += g_fin[FIN_SD + 2 * k]; p2 += g_fin[FIN_SD + 2 * k + 1]; }
+    p1 *= 2.0;
+    const double rho = par[P_RHO];
+    const double q2q2 = g_fin[FIN_Q + 0], q1q2 = g_fin[FIN_Q + 1], q0q2 = g_fin[FIN_Q + 2];
+    const double q1q1 = g_fin[FIN_Q + 3], q0q1 = g_fin[FIN_Q + 4];
+    const double a = rho * q2q2 / 2;
+    const double b = rho * q1q2;
+    const double c = p2 - rho * q0q2 + rho * q1q1 / 2;
+    const double d = p1 - rho * q0q1;
+    double roots[3];
+    const int rn = dev_cubic(4 * a, 3 * b, 2 * c, d, roots);
+    double tau = 0.0;
+    const double f0 = 0.0, f1 = quartic(a, b, c, d, 1.0);
+    double fr1 = 1e30, fr2 = 1e30, fr3 = 1e30;
+    if (rn >= 1 && roots[0] > 1e-20 && roots[0] <= 1.0) fr1 = quartic(a, b, c, d, roots[0]);
+    if (rn >= 2 && roots[1] > 1e-20 && roots[1] <= 1.0) fr2 = quartic(a, b, c, d, roots[1]);
+    if (rn == 3 && roots[2] > 1e-20 && roots[2] <= 1.0) fr3 = quartic(a, b, c, d, roots[2]);
+    const double mn = fmin(fmin(fmin(fmin(f0, f1), fr1), fr2), fr3);
+    if (fabs(mn - f0) < 1e-10) tau = 0.0;
+    if (fabs(mn - f1) < 1e-10) tau = 1.0;
+    if (fabs(mn - fr1) < 1e-10) tau = roots[0];
+    if (fabs(mn - fr2) < 1e-10) tau = roots[1];
+    if (fabs(mn - fr3) < 1e-10) tau = roots[2];
+    ls[LS_TAU] = tau;
+    ls[LS_ROOTNUM] = rn;
+    ls[LS_FLAG] = rn == 0 ? 1.0 : (fabs(tau) < par[P_ENDTAU] ? 2.0 : 0.0);
+}
+
+// R += tau D ; cvs += tau q1 + tau^2 q2 ; M1 = -lam - rho b + rho cvs
+// (ALMupdateVar lorads_alm.c:826-830, :1351-1353, ALMSetGrad :45-49)
+__global__ void __launch_bounds__(kBlock) k_alm_update(long NR, int m, int K, const double *__restrict__ par,
+                                                       const double *__restrict__ guard, double *__restrict__ lsout,
+                                                       double *__restrict__ R, const double *__restrict__ D,
+                                                       double *__restrict__ cvs, const double *__restrict__ q1,
+                                                       const double *__restrict__ q2, const double *__restrict__ lam,
+                                                       const double *__restrict__ b, double *__restrict__ M1) {
+    if (guard[C_ACTIVE] == 0.0) return;
+    __shared__ double ls[LS_N];
+    if (threadIdx.x == 0) line_search(par, K, ls);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < LS_N) lsout[threadIdx.x] = ls[threadIdx.x];
+    if (ls[LS_FLAG] != 0.0) return;
+    const double tau = ls[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
+    for (long i = ((long)blockIdx.x * kBlock + threadIdx.x) * 2; i < NR; i += (long)gridDim.x * kBlock * 2) {
+        double2 r = *reinterpret_cast<const double2 *>(R + i);
+        double2 d = *reinterpret_cast<const double2 *>(D + i);
+        r.x += tau * d.x; r.y += tau * d.y;
+        *reinterpret_cast<double2 *>(R + i) = r;
+    }
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        double v = cvs[i] + tau * q1[i];
+        v = v + tau2 * q2[i];
+        cvs[i] = v;
+        M1[i] = ((-lam[i]) + (-rho) * b[i]) + rho * v;
+    }
+}
+
+// G_new = 2 S R (row-owned), A(RR^T) slots (lower), L-BFGS pair
+// s = tau D, y = G_new - G_old into ring slot `head`, and the nine dots
+// needed by the next direction.  (ALMCalGrad :74-87, setlbfgsHisTwo :842-863,
+// primalInfeasibility's LORADSUVt(R,R) lorads_alg_common.c:387)
+template <int G, int E>
+__global__ void __launch_bounds__(kBlock) k_alm_grad(int n, int ld, long foff, const int *__restrict__ adj_ptr,
+                                                     const int *__restrict__ adj_low, const int *__restrict__ adj_col,
+                                                     const int *__restrict__ adj_slot, const double *__restrict__ S,
+                                                     const double *__restrict__ Rall, const double *__restrict__ Dall,
+                                                     double *G0, double *G1, double *s0, double *y0, double *s1,
+                                                     double *y1, double *__restrict__ uRR,
+                                                     const double *__restrict__ ctrl, const double *__restrict__ ls,
+                                                     int L, double *part, unsigned *ticket, double *fin) {
+    if (ctrl[C_ACTIVE] == 0.0 || ls[LS_FLAG] != 0.0) return;
+    const int gcur = (int)ctrl[C_GCUR];
+    const int h = (int)ctrl[C_HEAD];
+    const double tau = ls[LS_TAU];
+    const double *__restrict__ R = Rall + foff;
+    const double *__restrict__ D = Dall + foff;
+    double *__restrict__ Gold = (gcur == 0 ? G0 : G1) + foff;
+    double *__restrict__ Gnew = (gcur == 0 ? G1 : G0) + foff;
+    double *__restrict__ sh = (h == 0 ? s0 : s1) + foff;
+    double *__restrict__ yh = (h == 0 ? y0 : y1) + foff;
+    const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
+    const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
+    const bool two = (L == 2);
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kBlock / G;
+    // acc: GG, ys, yy, sG, yG, soG, yoG, soy, yoy
+    double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = grp; i < n; i += ngrp) {
+        double ri[E], g[E];
+        ld_row<E>(R + (long)i * ld + lane * E, ri);
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[e] = 0.0;
+        const int kb = adj_ptr[i], kl = adj_low[i], ke = adj_ptr[i + 1];
+        for (int k = kb; k < ke; ++k) {
+            const int j = adj_col[k];
+            const int s = adj_slot[k];
+            const double sv = S[s];
+            double rj[E];
+            ld_row<E>(R + (long)j * ld + lane * E, rj);
+#pragma unroll
+            for (int e = 0; e < E; ++e) g[e] += sv * rj[e];
+            if (k < kl) {   // lower entry (j <= i): A(RR^T) slot owned by this row
+                double d = 0.0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) d += ri[e] * rj[e];
+                d = group_sum<G>(d);
+                if (lane == 0) uRR[s] = d;
+            }
+        }
+        double go[E], di[E], sv[E], yv[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[e] *= 2.0;
+        ld_row<E>(Gold + (long)i * ld + lane * E, go);
+        ld_row<E>(D + (long)i * ld + lane * E, di);
+#pragma unroll
+        for (int e = 0; e < E; ++e) { sv[e] = tau * di[e]; yv[e] = g[e] - go[e]; }
+        st_row<E>(Gnew + (long)i * ld + lane * E, g);
+        st_row<E>(sh + (long)i * ld + lane * E, sv);
+        st_row<E>(yh + (long)i * ld + lane * E, yv);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            acc[0] += g[e] * g[e];
+            acc[1] += yv[e] * sv[e];
+            acc[2] += yv[e] * yv[e];
+            acc[3] += sv[e] * g[e];
+            acc[4] += yv[e] * g[e];
+        }
+        if (two) {
+            double sov[E], yov[E];
+            ld_row<E>(so + (long)i * ld + lane * E, sov);
+            ld_row<E>(yo + (long)i * ld + lane * E, yov);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                acc[5] += sov[e] * g[e];
+                acc[6] += yov[e] * g[e];
+                acc[7] += sov[e] * yv[e];
+                acc[8] += yov[e] * yv[e];
+            }
+        }
+    }
+    partials_finalize<9>(acc, part, ticket, fin);
+}
+
+// cvs = A(RR^T) from scratch + residual ||b - cvs||^2 (primalInfeasibility)
+__global__ void __launch_bounds__(kBlock) k_alm_gather_rr(int m, int K, const int *__restrict__ con_ptr,
+                                                          const int *__restrict__ con_slot,
+                                                          const double *__restrict__ con_w,
+                                                          const double *__restrict__ uRR, const double *__restrict__ b,
+                                                          double *__restrict__ cvs, const double *__restrict__ ctrl,
+                                                          const double *__restrict__ ls, double *part,
+                                                          unsigned *ticket, double *fin) {
+    if (ctrl[C_ACTIVE] == 0.0 || ls[LS_FLAG] != 0.0) return;
+    double acc[1] = {0.0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        double tot = 0.0;
+        for (int k = 0; k < K; ++k) {
+            const long row = (long)k * m + i;
+            double v = 0.0;
+            for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) v += con_w[e] * uRR[con_slot[e]];
+            tot += v;
+        }
+        cvs[i] = tot;
+        const double dd = b[i] - tot;
+        acc[0] += dd * dd;
+    }
+    partials_finalize<1>(acc, part, ticket, fin);
+}
+
+// ------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------
+static unsigned *ticket_ptr(int id) {
+    unsigned *p = nullptr;
+    (void)hipGetSymbolAddress((void **)&p, HIP_SYMBOL(g_tickets));
+    return p + id;
+}
+static double *fin_ptr() {
+    double *p = nullptr;
+    (void)hipGetSymbolAddress((void **)&p, HIP_SYMBOL(g_fin));
+    return p;
+}
+static double *tmpfin_ptr() {
+    double *p = nullptr;
+    (void)hipGetSymbolAddress((void **)&p, HIP_SYMBOL(g_tmpfin));
+    return p;
+}
+double *device_tmpfin() { return tmpfin_ptr(); }
+double *device_fin() { return fin_ptr(); }
+
+#define LRS_LAYOUT_SWITCH(Gv, Ev, BODY)                                                        \
+    switch ((Gv) * 8 + (Ev)) {                                                                 \
+    case 8 * 8 + 1: { constexpr int GG = 8, EE = 1; BODY; } break;                             \
+    case 8 * 8 + 2: { constexpr int GG = 8, EE = 2; BODY; } break;                             \
+    case 8 * 8 + 3: { constexpr int GG = 8, EE = 3; BODY; } break;                             \
+    case 8 * 8 + 4: { constexpr int GG = 8, EE = 4; BODY; } break;                             \
+    case 16 * 8 + 1: { constexpr int GG = 16, EE = 1; BODY; } break;                           \
+    case 16 * 8 + 2: { constexpr int GG = 16, EE = 2; BODY; } break;                           \
+    case 16 * 8 + 3: { constexpr int GG = 16, EE = 3; BODY; } break;                           \
+    case 16 * 8 + 4: { constexpr int GG = 16, EE = 4; BODY; } break;                           \
+    case 32 * 8 + 1: { constexpr int GG = 32, EE = 1; BODY; } break;                           \
+    case 32 * 8 + 2: { constexpr int GG = 32, EE = 2; BODY; } break;                           \
+    case 32 * 8 + 3: { constexpr int GG = 32, EE = 3; BODY; } break;                           \
+    case 32 * 8 + 4: { constexpr int GG = 32, EE = 4; BODY; } break;                           \
+    case 64 * 8 + 1: { constexpr int GG = 64, EE = 1; BODY; } break;                           \
+    case 64 * 8 + 2: { constexpr int GG = 64, EE = 2; BODY; } break;                           \
+    case 64 * 8 + 3: { constexpr int GG = 64, EE = 3; BODY; } break;                           \
+    case 64 * 8 + 4: { constexpr int GG = 64, EE = 4; BODY; } break;                           \
+    default:                                                                                   \
+        snprintf(g_err, sizeof(g_err), "unsupported layout G=%d E=%d", (Gv), (Ev));            \
+        return -1;                                                                             \
+    }
+
+int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double *out0,
+                 double *out1, double *part, int pblk_off, int *nblk_used, hipStream_t st) {
+    (void)pblk_off;
+    const DevCone &c = P.cones[cone];
+    const int grid = grid_rows(c.n, c.G);
+    double *fin = tmpfin_ptr() + TF_SD + 2 * cone;
+    const double *Xc = X + c.foff;
+    const double *Yc = Y ? Y + c.foff : nullptr;
+    LRS_LAYOUT_SWITCH(c.G, c.E, {
+        if (mode == 0)
+            hipLaunchKernelGGL((k_sddmm<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr,
+                               c.adj_low, c.adj_col, c.adj_slot, Xc, Yc, out0, out1, P.Cw, part,
+                               ticket_ptr(T_SDDMM), fin, nullptr);
+        else if (mode == 1)
+            hipLaunchKernelGGL((k_sddmm<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr,
+                               c.adj_low, c.adj_col, c.adj_slot, Xc, Yc, out0, out1, P.Cw, part,
+                               ticket_ptr(T_SDDMM), fin, nullptr);
+        else
+            hipLaunchKernelGGL((k_sddmm<GG, EE, 2>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr,
+                               c.adj_low, c.adj_col, c.adj_slot, Xc, Yc, out0, out1, P.Cw, part,
+                               ticket_ptr(T_SDDMM), fin, nullptr);
+    });
+    LRS_CHECK_LAUNCH();
+    if (nblk_used) *nblk_used = grid;
+    return 0;
+}
+
+int launch_gather(const DevProblem &P, const double *uvt, double scale, double *out, const double *b_for_vio,
+                  double *vio_part, hipStream_t st, int *nblk_used) {
+    const int grid = grid_elems(P.m, 1);
+    hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, P.m, P.K, -1, P.con_ptr, P.con_slot, P.con_w,
+                       uvt, scale, out, b_for_vio, vio_part, ticket_ptr(T_GATHER), tmpfin_ptr() + TF_GATHER);
+    LRS_CHECK_LAUNCH();
+    if (nblk_used) *nblk_used = grid;
+    return 0;
+}
+
+int launch_gather_cone(const DevProblem &P, int cone, const double *uvt, double *out, hipStream_t st) {
+    const int grid = grid_elems(P.m, 1);
+    hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, P.m, P.K, cone, P.con_ptr, P.con_slot, P.con_w,
+                       uvt, 1.0, out, nullptr, nullptr, ticket_ptr(T_GATHER), tmpfin_ptr() + TF_GATHER);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+int launch_wsum(const DevProblem &P, const double *w, int withC, double *S, hipStream_t st) {
+    const int grid = grid_elems(P.Ptot, 1);
+    hipLaunchKernelGGL(k_wsum, dim3(grid), dim3(kBlock), 0, st, P.Ptot, P.slot_ptr, P.slot_con, P.slot_a, P.Craw,
+                       withC, w, S, nullptr, nullptr);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+int launch_spmm(const DevProblem &P, int cone, const double *S, const double *X, double scale, const double *addX,
+                double addScale, double *out, double *part, int pblk_off, int *nblk_used, hipStream_t st) {
+    (void)pblk_off;
+    const DevCone &c = P.cones[cone];
+    const int grid = grid_rows(c.n, c.G);
+    double *fin = tmpfin_ptr() + TF_SPMM + cone;
+    LRS_LAYOUT_SWITCH(c.G, c.E, {
+        hipLaunchKernelGGL((k_spmm<GG, EE>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr, c.adj_col,
+                           c.adj_slot, S, X + c.foff, scale, addX ? addX + c.foff : nullptr, addScale,
+                           out + c.foff, part, ticket_ptr(T_SPMM), fin);
+    });
+    LRS_CHECK_LAUNCH();
+    if (nblk_used) *nblk_used = grid;
+    return 0;
+}
+
+int launch_axpby(long n, double a, const double *x, double b, double *y, hipStream_t st) {
+    hipLaunchKernelGGL(k_axpby, dim3(grid_elems(n, 4)), dim3(kBlock), 0, st, n, a, x, b, y);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int launch_fill(long n, double v, double *x, hipStream_t st) {
+    hipLaunchKernelGGL(k_fill, dim3(grid_elems(n, 4)), dim3(kBlock), 0, st, n, v, x);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int launch_dot(long n, const double *x, const double *y, double *part, hipStream_t st, int *nblk_used) {
+    const int grid = grid_elems(n, 8);
+    hipLaunchKernelGGL(k_dot, dim3(grid), dim3(kBlock), 0, st, n, x, y, part, ticket_ptr(T_DOT),
+                       tmpfin_ptr() + TF_DOT);
+    LRS_CHECK_LAUNCH();
+    if (nblk_used) *nblk_used = grid;
+    return 0;
+}
+int launch_dual_update(const DevProblem &P, double rho, double *lam, const double *cvs, hipStream_t st) {
+    hipLaunchKernelGGL(k_dual_update, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, rho, P.b, lam, cvs);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int launch_alm_m1(const DevProblem &P, double rho, const double *lam, const double *cvs, double *M1,
+                  hipStream_t st) {
+    hipLaunchKernelGGL(k_alm_m1, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, rho, P.b, lam, cvs, M1);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y, int avg, double *gram_part,
+                int *nblk_used, hipStream_t st) {
+    const DevCone &c = P.cones[cone];
+    if (c.r * c.r > 16 * kBlock) {
+        snprintf(g_err, sizeof(g_err), "gram: rank %d too large", c.r);
+        return -1;
+    }
+    int grid = (c.n + 255) / 256;
+    if (grid > 64) grid = 64;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(k_gram, dim3(grid), dim3(kBlock), 8 * c.ld * sizeof(double), st, c.n, c.r, c.ld,
+                       X + c.foff, Y ? Y + c.foff : nullptr, avg, gram_part);
+    LRS_CHECK_LAUNCH();
+    if (nblk_used) *nblk_used = grid;
+    return 0;
+}
+
+// One fused ALM inner iteration.  Parity selects the control buffers.
+int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
+    const DevProblem &P = *a.P;
+    DevWork &W = *a.W;
+    double *ctrl_prev = W.ctrl + (parity ^ 1) * C_NCTRL;
+    double *ctrl_cur = W.ctrl + parity * C_NCTRL;
+    double *ls_prev = W.lsres + (parity ^ 1) * LS_N;
+    double *ls_cur = W.lsres + parity * LS_N;
+    double *fin = fin_ptr();
+    const int L = 2;
+    // 1. direction (+ control)
+    hipLaunchKernelGGL(k_alm_dir, dim3(grid_elems(P.NRpad, 2)), dim3(kBlock), 0, st, P.NRpad, W.par, ctrl_prev,
+                       ctrl_cur, ls_prev, P.K, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1]);
+    LRS_CHECK_LAUNCH();
+    // 2. sym(RD^T), DD^T on the pattern (+ objective parts)
+    for (int k = 0; k < P.K; ++k) {
+        const DevCone &c = P.cones[k];
+        const int grid = grid_rows(c.n, c.G);
+        LRS_LAYOUT_SWITCH(c.G, c.E, {
+            hipLaunchKernelGGL((k_sddmm<GG, EE, 2>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr,
+                               c.adj_low, c.adj_col, c.adj_slot, W.R + c.foff, W.D + c.foff, W.uvt0, W.uvt1, P.Cw,
+                               W.part, ticket_ptr(T_SDDMM + 8 + k % 8), fin + FIN_SD + 2 * k, ctrl_cur);
+        });
+        LRS_CHECK_LAUNCH();
+    }
+    // 3. q1, q2 + line-search dots
+    hipLaunchKernelGGL(k_alm_gather_q, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, P.K, P.con_ptr,
+                       P.con_slot, P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, W.q1, W.q2, W.partB,
+                       ticket_ptr(T_Q), fin + FIN_Q, ctrl_cur);
+    LRS_CHECK_LAUNCH();
+    // 4. line search + updates of R, A(RR^T), M1
+    hipLaunchKernelGGL(k_alm_update, dim3(grid_elems(P.NRpad > P.m ? P.NRpad : P.m, 2)), dim3(kBlock), 0, st,
+                       P.NRpad, P.m, P.K, W.par, ctrl_cur, ls_cur, W.R, W.D, W.cvs, W.q1, W.q2, W.lam, P.b, W.M1);
+    LRS_CHECK_LAUNCH();
+    // 5. S = C + A^*(M1)
+    hipLaunchKernelGGL(k_wsum, dim3(grid_elems(P.Ptot, 1)), dim3(kBlock), 0, st, P.Ptot, P.slot_ptr, P.slot_con,
+                       P.slot_a, P.Craw, 1, W.M1, W.S, ctrl_cur, ls_cur);
+    LRS_CHECK_LAUNCH();
+    // 6. gradient + A(RR^T) slots + L-BFGS pair
+    for (int k = 0; k < P.K; ++k) {
+        const DevCone &c = P.cones[k];
+        const int grid = grid_rows(c.n, c.G);
+        LRS_LAYOUT_SWITCH(c.G, c.E, {
+            hipLaunchKernelGGL((k_alm_grad<GG, EE>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr,
+                               c.adj_low, c.adj_col, c.adj_slot, W.S, W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
+                               W.ls[1], W.ly[1], W.uvt2, ctrl_cur, ls_cur, L, W.partC,
+                               ticket_ptr(T_GRAD + 24 + k % 8), fin + FIN_GR + 9 * k);
+        });
+        LRS_CHECK_LAUNCH();
+    }
+    // 7. A(RR^T) -> cvs, residual
+    hipLaunchKernelGGL(k_alm_gather_rr, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, P.K, P.con_ptr,
+                       P.con_slot, P.con_w, W.uvt2, P.b, W.cvs, ctrl_cur, ls_cur, W.part, ticket_ptr(T_RR),
+                       fin + FIN_RR);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+// ------------------------------------------------------------------------
+// small helper kernels used by the host-driven phases
+// ------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_resid(int m, const double *__restrict__ b, const double *__restrict__ x,
+                                                  double *part, unsigned *ticket, double *fin) {
+    double acc[1] = {0.0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        const double d = b[i] - x[i];
+        acc[0] += d * d;
+    }
+    partials_finalize<1>(acc, part, ticket, fin);
+}
+// averageUV (lorads_admm.c:372-377)
+__global__ void __launch_bounds__(kBlock) k_avg(long n, const double *__restrict__ U, const double *__restrict__ V,
+                                                double *__restrict__ R) {
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long)gridDim.x * kBlock)
+        R[i] = (U[i] + V[i]) / 2;
+}
+// M1 = rho (cvs - cv - b) - lam in the reference's operation order (lorads_admm.c:568-581)
+__global__ void __launch_bounds__(kBlock) k_admm_m1(int m, double rho, const double *__restrict__ b,
+                                                    const double *__restrict__ cvs, const double *__restrict__ cv,
+                                                    const double *__restrict__ lam, double *__restrict__ M1) {
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        double v = -b[i];
+        v = v + cvs[i];
+        v = v + (-1.0) * cv[i];
+        v = v * rho;
+        M1[i] = v + (-1.0) * lam[i];
+    }
+}
+__global__ void k_ls_only(const double *__restrict__ par, int K, double *__restrict__ lsout) {
+    __shared__ double ls[LS_N];
+    if (threadIdx.x == 0) line_search(par, K, ls);
+    __syncthreads();
+    if (threadIdx.x < LS_N) lsout[threadIdx.x] = ls[threadIdx.x];
+}
+__global__ void __launch_bounds__(kBlock) k_gram_reduce(int nblk, int rr, const double *__restrict__ part,
+                                                        double *__restrict__ out) {
+    for (int idx = blockIdx.x * kBlock + threadIdx.x; idx < rr; idx += gridDim.x * kBlock) {
+        double s = 0.0;
+        for (int b = 0; b < nblk; ++b) s += part[(long)b * rr + idx];
+        out[idx] = s;
+    }
+}
+
+int launch_resid(int m, const double *b, const double *x, hipStream_t st) {
+    static double *part = nullptr;
+    if (!part && hipMalloc((void **)&part, sizeof(double) * kMaxPartialBlocks) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_resid, dim3(grid_elems(m, 1)), dim3(kBlock), 0, st, m, b, x, part, ticket_ptr(T_RR + 40),
+                       tmpfin_ptr() + TF_RESID);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int launch_avg(long n, const double *U, const double *V, double *R, hipStream_t st) {
+    hipLaunchKernelGGL(k_avg, dim3(grid_elems(n, 4)), dim3(kBlock), 0, st, n, U, V, R);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int launch_admm_m1(int m, double rho, const double *b, const double *cvs, const double *cv, const double *lam,
+                   double *M1, hipStream_t st) {
+    hipLaunchKernelGGL(k_admm_m1, dim3(grid_elems(m, 1)), dim3(kBlock), 0, st, m, rho, b, cvs, cv, lam, M1);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int launch_gram_reduce(int nblk, int rr, const double *part, double *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_gram_reduce, dim3(grid_elems(rr, 1)), dim3(kBlock), 0, st, nblk, rr, part, out);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+// gather_q on the current (uvt0, uvt1, cvs, lam) + device line search -> lsres[0..]
+int launch_ls_only(const DevProblem &P, DevWork &W, hipStream_t st) {
+    double one[C_NCTRL] = {0};
+    one[C_ACTIVE] = 1.0;
+    if (hipMemcpyAsync(W.ctrl, one, sizeof(one), hipMemcpyHostToDevice, st) != hipSuccess) return -1;
+    double *fin = fin_ptr();
+    hipLaunchKernelGGL(k_alm_gather_q, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, P.K, P.con_ptr,
+                       P.con_slot, P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, W.q1, W.q2, W.partB,
+                       ticket_ptr(T_Q), fin + FIN_Q, W.ctrl);
+    LRS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_ls_only, dim3(1), dim3(64), 0, st, W.par, P.K, W.lsres);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+// direction kernel alone, reading ctrl[1] and writing ctrl[0] (white-box tests)
+int launch_alm_dir_only(const DevProblem &P, DevWork &W, hipStream_t st) {
+    hipLaunchKernelGGL(k_alm_dir, dim3(grid_elems(P.NRpad, 2)), dim3(kBlock), 0, st, P.NRpad, W.par,
+                       W.ctrl + C_NCTRL, W.ctrl, W.lsres + LS_N, P.K, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
+                       W.ls[1], W.ly[1]);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // namespace lrs

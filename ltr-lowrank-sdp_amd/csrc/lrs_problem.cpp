@@ -1,0 +1,310 @@
+// lrs_problem.cpp -- SDPA reader and presolve (host), producing the device
+// formats described in lrs_device.h.  Reference semantics:
+//   reader    io/lorads_file_io.c:59-455
+//   presolve  data/lorads_sdp_conic.c:1185-1393 (union pattern + slot maps)
+//             data/lorads_sdp_data.c:313-329     (nnzIdx2ResIdx)
+// The presolve is sort-based (O(Z log Z)) instead of the reference's chained
+// hash (data/lorads_sdp_data.c:48-69), which dominates its wall time at large m.
+#include "lrs_problem.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+namespace lrs {
+
+namespace {
+
+struct RawEntry {
+    int cone, con, row, col;   // row >= col
+    double v;
+};
+
+bool is_sep(char c) {
+    return c == '{' || c == '}' || c == '(' || c == ')' || c == ',' || c == '\'' || c == ' ' || c == '\t' ||
+           c == '\r' || c == '\n';
+}
+
+}  // namespace
+
+bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot open " + path; return false; }
+    fseek(f, 0, SEEK_END);
+    long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    std::string s;
+    s.resize(sz);
+    if (sz > 0 && fread(&s[0], 1, sz, f) != (size_t)sz) { fclose(f); err = "short read"; return false; }
+    fclose(f);
+    size_t pos = 0;
+    auto next_line = [&](std::string &line) -> bool {
+        if (pos >= s.size()) return false;
+        size_t e = s.find('\n', pos);
+        if (e == std::string::npos) e = s.size();
+        line.assign(s, pos, e - pos);
+        pos = e + 1;
+        return true;
+    };
+    std::string line;
+    do {
+        if (!next_line(line)) { err = "empty file"; return false; }
+    } while (!line.empty() && (line[0] == '*' || line[0] == '"'));
+    int m = 0, nb = 0;
+    if (sscanf(line.c_str(), "%d", &m) != 1) { err = "bad constraint count"; return false; }
+    if (!next_line(line) || sscanf(line.c_str(), "%d", &nb) != 1) { err = "bad block count"; return false; }
+    std::vector<int> dims(nb);
+    auto skip = [&]() { while (pos < s.size() && is_sep(s[pos])) pos++; return pos < s.size(); };
+    for (int k = 0; k < nb; ++k) {
+        if (!skip()) { err = "bad block sizes"; return false; }
+        char *endp;
+        long d = strtol(s.c_str() + pos, &endp, 10);
+        if (endp == s.c_str() + pos) { err = "bad block size token"; return false; }
+        pos = endp - s.c_str();
+        if (k < nb - 1 && d <= 0) { err = "only the last block may be an LP block"; return false; }
+        dims[k] = (int)d;
+    }
+    int K = nb, nLp = 0;
+    if (nb > 0 && dims[nb - 1] < 0) { nLp = -dims[nb - 1]; K = nb - 1; }
+    hp.b.assign(m, 0.0);
+    for (int i = 0; i < m; ++i) {
+        if (!skip()) { err = "bad rhs"; return false; }
+        char *endp;
+        double v = strtod(s.c_str() + pos, &endp);
+        if (endp == s.c_str() + pos) { pos++; --i; continue; }
+        pos = endp - s.c_str();
+        hp.b[i] = v;
+    }
+    while (pos < s.size() && s[pos] != '\n') pos++;
+    if (pos < s.size()) pos++;
+    std::vector<RawEntry> raw;
+    raw.reserve(1 << 16);
+    bool lpEntries = false;
+    while (next_line(line)) {
+        int ic, ib, ii, ij;
+        double v;
+        if (sscanf(line.c_str(), "%d %d %d %d %lg", &ic, &ib, &ii, &ij, &v) != 5) {
+            bool blank = true;
+            for (char c : line) if (c != ' ' && c != '\t' && c != '\r') blank = false;
+            if (blank) continue;
+            break;
+        }
+        ib -= 1; ii -= 1; ij -= 1;
+        if (std::fabs(v) < 1e-12) continue;                 // :288-294
+        if (ib == K && nLp > 0) { lpEntries = true; continue; }
+        if (ib < 0 || ib >= K || ic < 0 || ic > m) { err = "entry out of range"; return false; }
+        if (ii > ij) std::swap(ii, ij);                     // :311-315
+        if (ii < 0 || ij >= dims[ib]) { err = "entry index out of block"; return false; }
+        if (ic == 0) v = -v;                                // :317-319 (C = -F0)
+        raw.push_back({ib, ic, ij, ii, v});
+    }
+    if (nLp > 0 || lpEntries) {
+        err = "LP blocks are not supported by the device path yet (SURVEY.md §2, out of scope)";
+        return false;
+    }
+    hp.m = m; hp.K = K; hp.nLp = nLp;
+    hp.nEntries = (long)raw.size();
+    hp.cones.assign(K, HostCone());
+    // sort: cone, con, row, col -> merge duplicates (the reference sums them in AUV / WSum)
+    std::sort(raw.begin(), raw.end(), [](const RawEntry &a, const RawEntry &b) {
+        if (a.cone != b.cone) return a.cone < b.cone;
+        if (a.con != b.con) return a.con < b.con;
+        if (a.row != b.row) return a.row < b.row;
+        return a.col < b.col;
+    });
+    size_t q = 0;
+    for (int k = 0; k < K; ++k) {
+        HostCone &c = hp.cones[k];
+        c.n = dims[k];
+        size_t b0 = q;
+        while (q < raw.size() && raw[q].cone == k) q++;
+        // merged entries of this cone
+        std::vector<RawEntry> me;
+        me.reserve(q - b0);
+        for (size_t e = b0; e < q; ++e) {
+            if (!me.empty() && me.back().con == raw[e].con && me.back().row == raw[e].row && me.back().col == raw[e].col)
+                me.back().v += raw[e].v;
+            else
+                me.push_back(raw[e]);
+        }
+        // pattern = unique (row,col), row-major
+        std::vector<std::pair<int, int>> pr;
+        pr.reserve(me.size());
+        for (auto &e : me) pr.push_back({e.row, e.col});
+        std::sort(pr.begin(), pr.end());
+        pr.erase(std::unique(pr.begin(), pr.end()), pr.end());
+        const int P = (int)pr.size();
+        c.prow.resize(P); c.pcol.resize(P);
+        for (int t = 0; t < P; ++t) { c.prow[t] = pr[t].first; c.pcol[t] = pr[t].second; }
+        auto slot_of = [&](int row, int col) {
+            auto it = std::lower_bound(pr.begin(), pr.end(), std::make_pair(row, col));
+            return (int)(it - pr.begin());
+        };
+        c.Craw.assign(P, 0.0);
+        c.Chas.assign(P, 0);
+        long cn = 0;
+        int lastCon = -1, cnt = 0;
+        const double fill = 0.1 * (double)((long)c.n * (c.n + 1) / 2);
+        for (size_t e = 0; e < me.size(); ++e) {
+            const RawEntry &r = me[e];
+            int sl = slot_of(r.row, r.col);
+            if (r.con == 0) {
+                c.Craw[sl] += r.v;
+                c.Chas[sl] = 1;
+                cn++;
+            } else {
+                c.ent.push_back({r.con - 1, sl, r.v, r.row == r.col});
+                if (r.con != lastCon) {
+                    if (lastCon > 0 && cnt > fill) c.denseCoeff = true;
+                    c.nnzRows++;
+                    lastCon = r.con;
+                    cnt = 0;
+                }
+                cnt++;
+            }
+        }
+        if (lastCon > 0 && cnt > fill) c.denseCoeff = true;
+        if ((double)cn > fill) c.denseCoeff = true;
+        // objective norms (sdpSparseConeObjNrm*, data/lorads_sdp_data.c:217-262)
+        for (int t = 0; t < P; ++t) {
+            if (!c.Chas[t]) continue;
+            double a = c.Craw[t];
+            bool dg = c.prow[t] == c.pcol[t];
+            c.cNrm1 += dg ? std::fabs(a) : 2 * std::fabs(a);
+            c.cNrm2sq += dg ? a * a : 2 * a * a;
+            c.cNrmInf = std::max(c.cNrmInf, std::fabs(a));
+        }
+        // symmetric adjacency, columns ascending per row; lower prefix = col <= row
+        std::vector<int> deg(c.n, 0);
+        for (int t = 0; t < P; ++t) {
+            deg[c.prow[t]]++;
+            if (c.prow[t] != c.pcol[t]) deg[c.pcol[t]]++;
+        }
+        c.adj_ptr.assign(c.n + 1, 0);
+        for (int i = 0; i < c.n; ++i) c.adj_ptr[i + 1] = c.adj_ptr[i] + deg[i];
+        const long nadj = c.adj_ptr[c.n];
+        c.adj_col.assign(nadj, 0);
+        c.adj_slot.assign(nadj, 0);
+        std::vector<int> fillp(c.adj_ptr.begin(), c.adj_ptr.end() - 1);
+        // pass 1: lower entries in row-major order already sorted by col within a row
+        for (int t = 0; t < P; ++t) {
+            int i = c.prow[t];
+            c.adj_col[fillp[i]] = c.pcol[t];
+            c.adj_slot[fillp[i]] = t;
+            fillp[i]++;
+        }
+        c.adj_low.assign(c.n, 0);
+        for (int i = 0; i < c.n; ++i) c.adj_low[i] = fillp[i];
+        // pass 2: upper entries (j > i): slot (j, i) -> row i, col j; rows j ascending
+        for (int t = 0; t < P; ++t) {
+            int i = c.prow[t], j = c.pcol[t];
+            if (i == j) continue;
+            c.adj_col[fillp[j]] = i;
+            c.adj_slot[fillp[j]] = t;
+            fillp[j]++;
+        }
+    }
+    double bn1 = 0, bn2 = 0, bni = 0;
+    for (double v : hp.b) { bn1 += std::fabs(v); bn2 += v * v; bni = std::max(bni, std::fabs(v)); }
+    hp.bNrm1 = bn1; hp.bNrm2 = std::sqrt(bn2); hp.bNrmInf = bni;
+    double c1 = 0, c2 = 0, ci = 0;
+    for (auto &c : hp.cones) { c1 += c.cNrm1; c2 += c.cNrm2sq; ci = std::max(ci, c.cNrmInf); }
+    hp.cNrm1 = c1; hp.cNrm2 = std::pow(c2, 0.5); hp.cNrmInf = ci;
+    return true;
+}
+
+template <typename T>
+static bool dput(T **dst, const std::vector<T> &v, std::string &err) {
+    size_t bytes = std::max<size_t>(1, v.size()) * sizeof(T);
+    if (hipMalloc((void **)dst, bytes) != hipSuccess) { err = "hipMalloc failed"; return false; }
+    if (!v.empty() && hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) {
+        err = "hipMemcpy failed";
+        return false;
+    }
+    return true;
+}
+
+bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
+    dp.m = hp.m;
+    dp.K = hp.K;
+    dp.cones.assign(hp.K, DevCone());
+    int Ptot = 0;
+    for (int k = 0; k < hp.K; ++k) { dp.cones[k].slot_off = Ptot; dp.cones[k].P = (int)hp.cones[k].prow.size(); Ptot += dp.cones[k].P; }
+    dp.Ptot = Ptot;
+    std::vector<double> Cw(Ptot), Craw(Ptot);
+    for (int k = 0; k < hp.K; ++k) {
+        const HostCone &c = hp.cones[k];
+        for (int t = 0; t < (int)c.prow.size(); ++t) {
+            const int g = dp.cones[k].slot_off + t;
+            Craw[g] = c.Craw[t];
+            Cw[g] = (c.prow[t] == c.pcol[t] ? 1.0 : 2.0) * c.Craw[t];
+        }
+    }
+    // constraint CSR, cone-major rows: row = k*m + i
+    const int m = hp.m;
+    std::vector<int> con_ptr((long)hp.K * m + 1, 0), con_slot;
+    std::vector<double> con_w;
+    long Z = 0;
+    for (int k = 0; k < hp.K; ++k) Z += (long)hp.cones[k].ent.size();
+    con_slot.reserve(Z);
+    con_w.reserve(Z);
+    for (int k = 0; k < hp.K; ++k) {
+        const HostCone &c = hp.cones[k];
+        size_t e = 0;
+        for (int i = 0; i < m; ++i) {
+            while (e < c.ent.size() && c.ent[e].con == i) {
+                con_slot.push_back(dp.cones[k].slot_off + c.ent[e].slot);
+                con_w.push_back((c.ent[e].diag ? 1.0 : 2.0) * c.ent[e].a);
+                e++;
+            }
+            con_ptr[(long)k * m + i + 1] = (int)con_slot.size();
+        }
+    }
+    // slot -> (con, a) CSR, constraints ascending per slot
+    std::vector<int> slot_ptr(Ptot + 1, 0), slot_con(Z);
+    std::vector<double> slot_a(Z);
+    for (int k = 0; k < hp.K; ++k)
+        for (auto &e : hp.cones[k].ent) slot_ptr[dp.cones[k].slot_off + e.slot + 1]++;
+    for (int s = 0; s < Ptot; ++s) slot_ptr[s + 1] += slot_ptr[s];
+    std::vector<int> fp(slot_ptr.begin(), slot_ptr.end() - 1);
+    for (int k = 0; k < hp.K; ++k)
+        for (auto &e : hp.cones[k].ent) {   // entries sorted by (con, slot) -> per-slot con ascending
+            const int g = dp.cones[k].slot_off + e.slot;
+            slot_con[fp[g]] = e.con;
+            slot_a[fp[g]] = e.a;
+            fp[g]++;
+        }
+    dp.Z = Z;
+    if (!dput(&dp.b, hp.b, err) || !dput(&dp.Cw, Cw, err) || !dput(&dp.Craw, Craw, err) ||
+        !dput(&dp.con_ptr, con_ptr, err) || !dput(&dp.con_slot, con_slot, err) || !dput(&dp.con_w, con_w, err) ||
+        !dput(&dp.slot_ptr, slot_ptr, err) || !dput(&dp.slot_con, slot_con, err) || !dput(&dp.slot_a, slot_a, err))
+        return false;
+    for (int k = 0; k < hp.K; ++k) {
+        const HostCone &c = hp.cones[k];
+        DevCone &d = dp.cones[k];
+        d.n = c.n;
+        std::vector<int> adj_slot_g(c.adj_slot.size());
+        for (size_t t = 0; t < c.adj_slot.size(); ++t) adj_slot_g[t] = d.slot_off + c.adj_slot[t];
+        d.adj_nnz = (long)c.adj_col.size();
+        if (!dput(&d.adj_ptr, c.adj_ptr, err) || !dput(&d.adj_low, c.adj_low, err) ||
+            !dput(&d.adj_col, c.adj_col, err) || !dput(&d.adj_slot, adj_slot_g, err))
+            return false;
+    }
+    return true;
+}
+
+void free_problem(DevProblem &dp) {
+    auto f = [](void *p) { if (p) (void)hipFree(p); };
+    f(dp.b); f(dp.Cw); f(dp.Craw); f(dp.con_ptr); f(dp.con_slot); f(dp.con_w);
+    f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
+    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); }
+    dp = DevProblem();
+}
+
+}  // namespace lrs

@@ -1,0 +1,47 @@
+// lrs_problem.h -- host-side problem model: SDPA reader, presolve into the
+// device formats of lrs_device.h, and upload.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "lrs_device.h"
+
+namespace lrs {
+
+struct HostEntry {      // one merged coefficient entry of constraint `con` in a cone
+    int con;            // 0-based constraint index
+    int slot;           // local slot in the cone pattern
+    double a;           // raw value (lower triangle)
+    bool diag;
+};
+
+struct HostCone {
+    int n = 0;
+    int nnzRows = 0;                     // constraints with a nonzero coefficient (statNnz)
+    bool denseCoeff = false;             // some coefficient >10% fill (reference dense path)
+    std::vector<int> prow, pcol;         // pattern, row-major lower (col <= row)
+    std::vector<double> Craw;            // C per slot (0 where absent)
+    std::vector<char> Chas;              // C has an entry at this slot
+    std::vector<HostEntry> ent;          // constraint entries sorted by (con, slot)
+    std::vector<int> adj_ptr, adj_low, adj_col, adj_slot;   // symmetric adjacency
+    double cNrm1 = 0, cNrm2sq = 0, cNrmInf = 0;
+};
+
+struct HostProblem {
+    int m = 0, K = 0, nLp = 0;
+    std::vector<double> b;
+    std::vector<HostCone> cones;
+    long nEntries = 0;
+    double bNrm1 = 0, bNrm2 = 0, bNrmInf = 0;
+    double cNrm1 = 0, cNrm2 = 0, cNrmInf = 0;
+};
+
+// SDPA reader with the semantics of io/lorads_file_io.c:59-455
+// (C = -F0, |v| < 1e-12 dropped, (i,j) swapped into the lower triangle).
+bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err);
+
+// Device upload of everything that does not depend on the rank.
+bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err);
+void free_problem(DevProblem &dp);
+
+}  // namespace lrs

@@ -1,0 +1,1348 @@
+// lrs_solver.cpp -- host control of the solve (ALM phase 1, ADMM phase 2) on
+// top of the device operators, and the C-ABI of include/lrsdp.h.
+//
+// The control flow restates the reference (paths relative to
+// /root/reference/lorads/src/src_semi): LORADS_ALMOptimize lorads_alm.c:1220-1484,
+// LORADSADMMOptimize lorads_alg/lorads_admm.c:84-209, LORADS_ALMtoADMM
+// data/lorads_solver.c:1351-1387, main.c:380-610.  The ALM inner L-BFGS loop
+// runs as batches of fused device iterations (enqueue_alm_iteration) with
+// device-side control; the host only intervenes between inner loops.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lrsdp.h"
+#include "lrs_device.h"
+#include "lrs_problem.h"
+
+namespace lrs {
+double *device_fin();
+double *device_tmpfin();
+int launch_gather_cone(const DevProblem &P, int cone, const double *uvt, double *out, hipStream_t st);
+int launch_resid(int m, const double *b, const double *x, hipStream_t st);
+int launch_avg(long n, const double *U, const double *V, double *R, hipStream_t st);
+int launch_admm_m1(int m, double rho, const double *b, const double *cvs, const double *cv, const double *lam,
+                   double *M1, hipStream_t st);
+int launch_ls_only(const DevProblem &P, DevWork &W, hipStream_t st);
+int launch_alm_dir_only(const DevProblem &P, DevWork &W, hipStream_t st);
+int launch_gram_reduce(int nblk, int rr, const double *part, double *out, hipStream_t st);
+}  // namespace lrs
+
+using namespace lrs;
+
+static thread_local std::string g_lrs_err;
+static void set_err(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_lrs_err = buf;
+}
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+#define HIPC(x)                                                                               \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            set_err("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_));          \
+            return -1;                                                                        \
+        }                                                                                     \
+    } while (0)
+#define OPC(x)                                                                                \
+    do {                                                                                      \
+        int r_ = (x);                                                                         \
+        if (r_ != 0) {                                                                        \
+            set_err("%s:%d %s failed: %s", __FILE__, __LINE__, #x, last_device_error());     \
+            return -1;                                                                        \
+        }                                                                                     \
+    } while (0)
+
+// glibc random_r TYPE_3 restated (srand(925) initial point, data/lorads_solver.c:625, :529-539)
+struct GlibcRand {
+    int32_t t[31];
+    int f = 0;
+    explicit GlibcRand(unsigned seed) {
+        int32_t r[344];
+        if (seed == 0) seed = 1;
+        r[0] = (int32_t)seed;
+        for (int i = 1; i < 31; i++) {
+            int64_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+            int64_t w = 16807 * lo - 2836 * hi;
+            if (w < 0) w += 2147483647;
+            r[i] = (int32_t)w;
+        }
+        for (int i = 31; i < 34; i++) r[i] = r[i - 31];
+        for (int i = 34; i < 344; i++) r[i] = (int32_t)((uint32_t)r[i - 31] + (uint32_t)r[i - 3]);
+        for (int i = 0; i < 31; i++) t[i] = r[313 + i];
+    }
+    int next() {
+        int i = f, j = (f + 28) % 31;
+        int32_t v = (int32_t)((uint32_t)t[i] + (uint32_t)t[j]);
+        t[i] = v;
+        f = (f + 1) % 31;
+        return (int)((uint32_t)v >> 1);
+    }
+};
+
+struct AlmState {
+    long outerIter = 0, innerIter = 0;
+    double rho = 0, pobj = 1e30, dobj = 1e30, pinf1 = 1e30, pinfinf = 1e30, gap = 0;
+};
+struct AdmmState {
+    long iter = 0, cg_iter = 0;
+    double rho = 0, pobj = 1e30, dobj = 1e30, pinf1 = 1e30, pinfinf = 1e30, gap = 1e30;
+};
+
+struct lrs_ctx {
+    int device = 0;
+    hipStream_t st = nullptr;
+    HostProblem hp;
+    DevProblem dp;
+    bool loaded = false;
+    std::vector<int> rank, rank_max;
+    std::vector<Layout> lay;
+    DevWork W;
+    bool walloc = false;
+    double *hpin = nullptr;     // pinned scalars
+    // L-BFGS mirror
+    int head = 0, gcur = 0;
+    double beta[2] = {0, 0}, yy[2] = {0, 0};
+    double scaleObjHis = 1.0;
+    double pObjVal = 0, dObjVal = 0, dimPinf = 0, dimGap = 0;
+    std::vector<int> t1c, t1o, t2c, t2o;
+    long cgIterTotal = 0;
+    std::vector<long> cgIterCone;
+    std::string path;
+    FILE *logfp = nullptr;
+};
+
+static void logf_(lrs_ctx *c, const lrs_params *p, const char *fmt, ...) {
+    char buf[2048];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (p->verbose) fputs(buf, stdout);
+    if (c->logfp) { fputs(buf, c->logfp); fflush(c->logfp); }
+}
+
+// ------------------------------------------------------------------------
+// workspace
+// ------------------------------------------------------------------------
+static void free_work(lrs_ctx *c) {
+    if (!c->walloc) return;
+    DevWork &W = c->W;
+    double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
+                      W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
+                      W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram};
+    for (double *p : ptrs)
+        if (p) (void)hipFree(p);
+    c->W = DevWork();
+    c->walloc = false;
+}
+
+static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
+    free_work(c);
+    DevProblem &P = c->dp;
+    c->rank = ranks;
+    c->lay.assign(P.K, Layout());
+    long off = 0;
+    int rmax = 1;
+    for (int k = 0; k < P.K; ++k) {
+        Layout L = choose_layout(ranks[k]);
+        if (ranks[k] > L.ld || L.ld > 256) { set_err("rank %d unsupported (max 256)", ranks[k]); return -1; }
+        c->lay[k] = L;
+        DevCone &dc = P.cones[k];
+        dc.r = ranks[k]; dc.ld = L.ld; dc.G = L.G; dc.E = L.E; dc.foff = off;
+        off += (long)dc.n * L.ld;
+        rmax = std::max(rmax, ranks[k]);
+    }
+    P.NRpad = off;
+    DevWork &W = c->W;
+    const long NR = std::max(2L, off);
+    const int m = std::max(1, P.m);
+    const int Pt = std::max(1, P.Ptot);
+    auto A = [&](double **p, long n) -> int {
+        HIPC(hipMalloc((void **)p, sizeof(double) * n));
+        HIPC(hipMemsetAsync(*p, 0, sizeof(double) * n, c->st));
+        return 0;
+    };
+    if (A(&W.R, NR) || A(&W.D, NR) || A(&W.G[0], NR) || A(&W.G[1], NR) || A(&W.ls[0], NR) || A(&W.ly[0], NR) ||
+        A(&W.ls[1], NR) || A(&W.ly[1], NR) || A(&W.U, NR) || A(&W.V, NR) || A(&W.X, NR) || A(&W.cg_r, NR) ||
+        A(&W.cg_p, NR) || A(&W.cg_Q, NR) || A(&W.cg_b, NR) || A(&W.M2, NR) || A(&W.uvt0, Pt) || A(&W.uvt1, Pt) ||
+        A(&W.uvt2, Pt) || A(&W.S, Pt) || A(&W.lam, m) || A(&W.cvs, m) || A(&W.q1, m) || A(&W.q2, m) ||
+        A(&W.M1, m) || A(&W.wtmp, m) || A(&W.cvc, (long)m * std::max(1, P.K)) ||
+        A(&W.part, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.partB, (long)kMaxPartialVals * kMaxPartialBlocks) ||
+        A(&W.partC, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.ctrl, 2 * C_NCTRL) ||
+        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax))
+        return -1;
+    HIPC(hipStreamSynchronize(c->st));
+    c->walloc = true;
+    c->head = 0; c->gcur = 0;
+    c->beta[0] = c->beta[1] = c->yy[0] = c->yy[1] = 0;
+    return 0;
+}
+
+// column-major (reference) <-> row-major ld-padded device layout
+static int factor_put(lrs_ctx *c, double *dst, const double *colmajor) {
+    std::vector<double> h(c->dp.NRpad, 0.0);
+    long src = 0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        const DevCone &d = c->dp.cones[k];
+        for (int q = 0; q < d.r; ++q)
+            for (int i = 0; i < d.n; ++i) h[d.foff + (long)i * d.ld + q] = colmajor[src + i + (long)q * d.n];
+        src += (long)d.n * d.r;
+    }
+    HIPC(hipMemcpy(dst, h.data(), sizeof(double) * c->dp.NRpad, hipMemcpyHostToDevice));
+    return 0;
+}
+static int factor_fetch(lrs_ctx *c, const double *srcd, double *colmajor) {
+    std::vector<double> h(c->dp.NRpad);
+    HIPC(hipStreamSynchronize(c->st));
+    HIPC(hipMemcpy(h.data(), srcd, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToHost));
+    long dst = 0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        const DevCone &d = c->dp.cones[k];
+        for (int q = 0; q < d.r; ++q)
+            for (int i = 0; i < d.n; ++i) colmajor[dst + i + (long)q * d.n] = h[d.foff + (long)i * d.ld + q];
+        dst += (long)d.n * d.r;
+    }
+    return 0;
+}
+
+static double *factor_ptr(lrs_ctx *c, int which) {
+    DevWork &W = c->W;
+    switch (which) {
+    case LRS_R: return W.R;
+    case LRS_D: return W.D;
+    case LRS_G: return W.G[c->gcur];
+    case LRS_U: return W.U;
+    case LRS_V: return W.V;
+    case LRS_S0: return W.ls[0];
+    case LRS_Y0: return W.ly[0];
+    case LRS_S1: return W.ls[1];
+    case LRS_Y1: return W.ly[1];
+    }
+    return nullptr;
+}
+static double *vec_ptr(lrs_ctx *c, int which) {
+    switch (which) {
+    case LRS_LAMBDA: return c->W.lam;
+    case LRS_CVS: return c->W.cvs;
+    case LRS_Q1: return c->W.q1;
+    case LRS_Q2: return c->W.q2;
+    case LRS_B: return c->dp.b;
+    }
+    return nullptr;
+}
+
+static int read_tmpfin(lrs_ctx *c, int idx, int n, double *out) {
+    HIPC(hipMemcpyAsync(c->hpin, device_tmpfin() + idx, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
+    HIPC(hipStreamSynchronize(c->st));
+    for (int i = 0; i < n; ++i) out[i] = c->hpin[i];
+    return 0;
+}
+
+// ------------------------------------------------------------------------
+// host-driven operators
+// ------------------------------------------------------------------------
+// A(X X^T) for every cone -> cvc[k], cvs = sum_k, returns pinf (primalInfeasibility)
+// and the objective <C, X X^T> (unscaled), with X given per-cone rows in factor buffer.
+static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pinf, double *obj) {
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    double o = 0.0;
+    for (int k = 0; k < P.K; ++k) {
+        OPC(launch_sddmm(P, k, Y ? 0 : 1, X, Y, W.uvt2, nullptr, W.part, 0, nullptr, c->st));
+        double t[2];
+        if (read_tmpfin(c, TF_SD + 2 * k, 1, t)) return -1;
+        o += t[0];
+    }
+    if (P.K == 1) {
+        OPC(launch_gather(P, W.uvt2, 1.0, W.cvs, P.b, W.part, c->st, nullptr));
+        HIPC(hipMemcpyAsync(W.cvc, W.cvs, sizeof(double) * P.m, hipMemcpyDeviceToDevice, c->st));
+        double v;
+        if (read_tmpfin(c, TF_GATHER, 1, &v)) return -1;
+        if (pinf) *pinf = std::sqrt(v) / (1 + c->hp.bNrm1);
+    } else {
+        OPC(launch_fill(P.m, 0.0, W.cvs, c->st));
+        for (int k = 0; k < P.K; ++k) {
+            OPC(launch_gather_cone(P, k, W.uvt2, W.cvc + (long)k * P.m, c->st));
+            OPC(launch_axpby(P.m, 1.0, W.cvc + (long)k * P.m, 1.0, W.cvs, c->st));
+        }
+        OPC(launch_resid(P.m, P.b, W.cvs, c->st));
+        double v;
+        if (read_tmpfin(c, TF_RESID, 1, &v)) return -1;
+        if (pinf) *pinf = std::sqrt(v) / (1 + c->hp.bNrm1);
+    }
+    if (obj) *obj = o;
+    return 0;
+}
+
+// ALMCalGrad (lorads_alm.c:74-87): G[gcur] = 2 (C + A^*(M1)) R, returns ||G||^2
+static int op_grad(lrs_ctx *c, double rho, double *lag) {
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    OPC(launch_alm_m1(P, rho, W.lam, W.cvs, W.M1, c->st));
+    OPC(launch_wsum(P, W.M1, 1, W.S, c->st));
+    double tot = 0.0;
+    for (int k = 0; k < P.K; ++k) {
+        OPC(launch_spmm(P, k, W.S, W.R, 2.0, nullptr, 0.0, W.G[c->gcur], W.part, 0, nullptr, c->st));
+        double v;
+        if (read_tmpfin(c, TF_SPMM + k, 1, &v)) return -1;
+        double nrm = std::sqrt(v);
+        tot += nrm * nrm;
+    }
+    *lag = tot;
+    return 0;
+}
+
+static int op_dot(lrs_ctx *c, long n, const double *x, const double *y, double *out) {
+    OPC(launch_dot(n, x, y, c->W.part, c->st, nullptr));
+    return read_tmpfin(c, TF_DOT, 1, out);
+}
+
+static void cal_dual_obj(lrs_ctx *c) {   // LORADSCalDualObj lorads_alg_common.c:531
+    double v = 0;
+    op_dot(c, c->dp.m, c->dp.b, c->W.lam, &v);
+    c->dObjVal = v / c->scaleObjHis;
+}
+
+// updateDimacsALM on R (lorads_alg_common.c:424-428) + objective
+static int update_dimacs(lrs_ctx *c, const double *X, const double *Y, bool with_obj) {
+    double pinf, obj;
+    if (op_constr_xx(c, X, Y, &pinf, &obj)) return -1;
+    if (with_obj) c->pObjVal = obj / c->scaleObjHis;
+    c->dimPinf = pinf;
+    double gap = c->pObjVal - c->dObjVal;
+    c->dimGap = std::fabs(gap) / (1 + std::fabs(c->pObjVal) + std::fabs(c->dObjVal));
+    return 0;
+}
+
+// ---- oracle rank: device Gram + host Jacobi eigenvalues (lorads_logging.c:216-366)
+static int sym_count(int r, std::vector<double> A, double eps) {
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0.0;
+        for (int i = 0; i < r; ++i)
+            for (int j = i + 1; j < r; ++j) off += A[i * r + j] * A[i * r + j];
+        if (off < 1e-30) break;
+        for (int p = 0; p < r; ++p)
+            for (int q = p + 1; q < r; ++q) {
+                double apq = A[p * r + q];
+                if (std::fabs(apq) < 1e-300) continue;
+                double th = 0.5 * (A[q * r + q] - A[p * r + p]) / apq;
+                double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+                double cs = 1.0 / std::sqrt(t * t + 1.0), sn = t * cs;
+                for (int k = 0; k < r; ++k) {
+                    double akp = A[k * r + p], akq = A[k * r + q];
+                    A[k * r + p] = cs * akp - sn * akq;
+                    A[k * r + q] = sn * akp + cs * akq;
+                }
+                for (int k = 0; k < r; ++k) {
+                    double apk = A[p * r + k], aqk = A[q * r + k];
+                    A[p * r + k] = cs * apk - sn * aqk;
+                    A[q * r + k] = sn * apk + cs * aqk;
+                }
+            }
+    }
+    double mx = -1e300;
+    for (int i = 0; i < r; ++i) mx = std::max(mx, A[i * r + i]);
+    int cnt = 0;
+    if (mx > 0)
+        for (int i = 0; i < r; ++i)
+            if (A[i * r + i] > eps * mx) cnt++;
+    return cnt;
+}
+
+static int gram_of(lrs_ctx *c, int k, const double *X, const double *Y, int avg, std::vector<double> &g) {
+    int nblk = 0;
+    OPC(launch_gram(c->dp, k, X, Y, avg, c->W.gram, &nblk, c->st));
+    const int rr = c->rank[k] * c->rank[k];
+    OPC(launch_gram_reduce(nblk, rr, c->W.gram, c->W.gram + 64L * rr, c->st));
+    g.resize(rr);
+    HIPC(hipMemcpyAsync(g.data(), c->W.gram + 64L * rr, sizeof(double) * rr, hipMemcpyDeviceToHost, c->st));
+    HIPC(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+static int oracle_rank(lrs_ctx *c, int phase) {
+    int tot = 0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        std::vector<double> g;
+        if (phase == 1) {
+            if (gram_of(c, k, c->W.R, nullptr, 0, g)) return -1;
+        } else {
+            if (gram_of(c, k, c->W.U, c->W.V, 1, g)) return -1;
+        }
+        tot += sym_count(c->rank[k], g, 1e-6);
+    }
+    return tot;
+}
+static int sum_rank(lrs_ctx *c) {
+    int t = 0;
+    for (int r : c->rank) t += r;
+    return t;
+}
+
+static void record_state(lrs_ctx *c, const lrs_params *p, int phase) {
+    int cur = sum_rank(c);
+    int orc = p->disableOracle ? cur : oracle_rank(c, phase);
+    if (orc < 0) orc = 0;
+    if (phase == 1) { c->t1c.push_back(cur); c->t1o.push_back(orc); }
+    else { c->t2c.push_back(cur); c->t2o.push_back(orc); }
+}
+
+// ---- rank determination (data/lorads_solver.c:406-459) + schedule hook
+static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &rank, std::vector<int> &rmax) {
+    const int K = c->hp.K;
+    rank.assign(K, 1);
+    rmax.assign(K, 1);
+    int tot_default = 0;
+    std::vector<int> dflt(K);
+    for (int k = 0; k < K; ++k) {
+        const HostCone &hc = c->hp.cones[k];
+        int nnzRows = hc.nnzRows;
+        int calc = std::min((int)std::sqrt(2.0 * nnzRows) + 1, hc.n);
+        if (p->fixedRank > 0) {
+            rank[k] = std::max(1, std::min(p->fixedRank, hc.n));
+            rmax[k] = rank[k];
+            dflt[k] = rank[k];
+            tot_default += rank[k];
+            continue;
+        }
+        rmax[k] = calc;
+        int rk;
+        if (p->initRank > 0) rk = std::min(p->initRank, hc.n);
+        else if (p->timesLogRank <= 1e-6) rk = calc;
+        else if (nnzRows / hc.n >= 20 && hc.n <= 400 && K <= 3) rk = calc;
+        else rk = (int)std::min(std::ceil(p->timesLogRank * std::log((double)hc.n)), (double)calc);
+        rank[k] = std::max(1, rk);
+        dflt[k] = rank[k];
+        tot_default += rank[k];
+    }
+    if (p->rankSchedule && p->rankScheduleLen > 0 && p->fixedRank <= 0) {
+        // entry 0 is the initial TOTAL rank, split across cones in proportion to the default ranks
+        int tot = std::max(1, p->rankSchedule[0]);
+        for (int k = 0; k < K; ++k) {
+            int rk = (int)std::lround((double)tot * dflt[k] / std::max(1, tot_default));
+            rank[k] = std::max(1, std::min(rk, c->hp.cones[k].n));
+            rmax[k] = std::max(rmax[k], rank[k]);
+        }
+    }
+}
+
+// random initial point R (LORADS_RANDOM_rk_MAT), cones in order, column-major draw order
+static int init_point(lrs_ctx *c) {
+    GlibcRand g(925);
+    long NRc = 0;
+    for (int k = 0; k < c->dp.K; ++k) NRc += (long)c->dp.cones[k].n * c->rank[k];
+    std::vector<double> R(NRc);
+    for (long i = 0; i < NRc; ++i) {
+        double v = (double)g.next() / 2147483647.0;
+        v -= (double)g.next() / 2147483647.0;
+        R[i] = v;
+    }
+    return factor_put(c, c->W.R, R.data());
+}
+
+// ---- AUG_RANK (data/lorads_solver.c:1154-1254)
+static int check_all_rank_max(lrs_ctx *c, double f) {
+    int cnt = 0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        int nr = (int)std::min(std::ceil(c->rank[k] * f), (double)c->rank_max[k]);
+        if (nr >= c->rank_max[k]) cnt++;
+    }
+    return cnt == c->dp.K;
+}
+
+static int regrow(lrs_ctx *c, const std::vector<int> &nr) {
+    // fetch R, U, V, G in reference layout, extend columns, reallocate, upload
+    long NRo = 0;
+    for (int k = 0; k < c->dp.K; ++k) NRo += (long)c->dp.cones[k].n * c->rank[k];
+    std::vector<double> R(NRo), U(NRo), V(NRo), G(NRo);
+    if (factor_fetch(c, c->W.R, R.data()) || factor_fetch(c, c->W.U, U.data()) ||
+        factor_fetch(c, c->W.V, V.data()) || factor_fetch(c, c->W.G[c->gcur], G.data()))
+        return -1;
+    std::vector<double> lam(c->dp.m), cvs(c->dp.m);
+    HIPC(hipMemcpy(lam.data(), c->W.lam, sizeof(double) * c->dp.m, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(cvs.data(), c->W.cvs, sizeof(double) * c->dp.m, hipMemcpyDeviceToHost));
+    long NRn = 0;
+    for (int k = 0; k < c->dp.K; ++k) NRn += (long)c->dp.cones[k].n * nr[k];
+    std::vector<double> Rn(NRn, 0.0), Un(NRn, 0.0), Vn(NRn, 0.0), Gn(NRn, 0.0);
+    long so = 0, dn = 0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        const int n = c->dp.cones[k].n, ro = c->rank[k], rn = nr[k];
+        auto grow = [&](const std::vector<double> &src, std::vector<double> &dst) {
+            std::copy(src.begin() + so, src.begin() + so + (long)n * ro, dst.begin() + dn);
+            const int aug = rn - ro, r = std::min(n, aug);   // lpRandomDiag :1096-1106
+            for (int i = 0; i < r; ++i) dst[dn + (long)n * ro + (long)i * n + i] = 1 / std::sqrt((double)r);
+        };
+        grow(R, Rn); grow(U, Un); grow(V, Vn); grow(G, Gn);
+        so += (long)n * ro;
+        dn += (long)n * rn;
+    }
+    int gc = c->gcur;
+    if (alloc_work(c, nr)) return -1;
+    c->gcur = gc;
+    if (factor_put(c, c->W.R, Rn.data()) || factor_put(c, c->W.U, Un.data()) || factor_put(c, c->W.V, Vn.data()) ||
+        factor_put(c, c->W.G[c->gcur], Gn.data()))
+        return -1;
+    HIPC(hipMemcpy(c->W.lam, lam.data(), sizeof(double) * c->dp.m, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(c->W.cvs, cvs.data(), sizeof(double) * c->dp.m, hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int aug_rank(lrs_ctx *c, double f, const lrs_params *p, int *sched_pos, int *is_max) {
+    if (check_all_rank_max(c, 1.0)) { *is_max = 1; return 0; }
+    std::vector<int> nr(c->dp.K);
+    bool sched = p->rankSchedule && p->rankScheduleLen > 0 && p->fixedRank <= 0;
+    if (sched) {
+        int pos = *sched_pos + 1;
+        if (pos >= p->rankScheduleLen) { *is_max = 1; return 0; }
+        *sched_pos = pos;
+        int tot = std::max(1, p->rankSchedule[pos]), cur = sum_rank(c);
+        for (int k = 0; k < c->dp.K; ++k) {
+            int rk = (int)std::lround((double)tot * c->rank[k] / std::max(1, cur));
+            nr[k] = std::max(c->rank[k], std::min(rk, c->hp.cones[k].n));
+            c->rank_max[k] = std::max(c->rank_max[k], nr[k]);
+        }
+    } else {
+        for (int k = 0; k < c->dp.K; ++k) nr[k] = (int)std::min(std::ceil(c->rank[k] * f), (double)c->rank_max[k]);
+    }
+    if (regrow(c, nr)) return -1;
+    if (sched) *is_max = (*sched_pos + 1 >= p->rankScheduleLen) ? 1 : 0;
+    else *is_max = check_all_rank_max(c, f);
+    return 0;
+}
+
+// LUtilUpdateCheckEma (lorads_utils.c:564-594)
+static int update_check_ema(double *cur, double *old, double v, double alpha, double thr, int interval, int *counter) {
+    int result = 1;
+    *cur = alpha * v + (1 - alpha) * (*cur);
+    if (*counter >= interval) {
+        if (*old != 0) {
+            double ch = (*cur - *old) / *old;
+            result = (ch >= -thr) && (ch <= thr);
+        }
+        *old = *cur;
+        *counter = 1;
+    } else {
+        (*counter)++;
+    }
+    return result;
+}
+
+// ---- device inner loop
+struct InnerIo {
+    long inner, local, clear;
+    double rcval, lag, pinf1, pinfinf;
+    int exitReason;
+};
+
+static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, double gap, long budget, InnerIo &io) {
+    double par[P_NPAR] = {0};
+    par[P_RHO] = rho; par[P_RCTOL] = rctol; par[P_ENDSUB] = p->endALMSubTol; par[P_ENDTAU] = p->endTauTol;
+    par[P_PH1TOL] = p->phase1Tol; par[P_BN1] = c->hp.bNrm1; par[P_BNINF] = c->hp.bNrmInf; par[P_CNINF] = c->hp.cNrmInf;
+    par[P_HIGHACC] = p->highAccMode; par[P_BUDGET] = (double)budget; par[P_L] = p->lbfgsListLength; par[P_GAP] = gap;
+    double ctl[C_NCTRL] = {0};
+    ctl[C_ACTIVE] = 1; ctl[C_EXIT] = EXIT_NONE; ctl[C_INNER] = (double)io.inner; ctl[C_LOCAL] = (double)io.local;
+    ctl[C_CLEAR] = (double)io.clear; ctl[C_HEAD] = c->head; ctl[C_GCUR] = c->gcur; ctl[C_PENDING] = 0;
+    ctl[C_RCVAL] = io.rcval; ctl[C_LAG] = io.lag; ctl[C_PINF1] = io.pinf1; ctl[C_PINFINF] = io.pinfinf;
+    ctl[C_BETA0] = c->beta[0]; ctl[C_BETA1] = c->beta[1]; ctl[C_YY0] = c->yy[0]; ctl[C_YY1] = c->yy[1];
+    memcpy(c->hpin, par, sizeof(par));
+    HIPC(hipMemcpyAsync(c->W.par, c->hpin, sizeof(par), hipMemcpyHostToDevice, c->st));
+    memcpy(c->hpin + 64, ctl, sizeof(ctl));
+    HIPC(hipMemcpyAsync(c->W.ctrl + C_NCTRL, c->hpin + 64, sizeof(ctl), hipMemcpyHostToDevice, c->st));
+    AlmIterArgs a{&c->dp, &c->W, 0, 0, 0, 0};
+    int B = 4;
+    double *res = c->hpin + 128;
+    for (;;) {
+        for (int j = 0; j < B; ++j) OPC(enqueue_alm_iteration(a, j & 1, c->st));
+        HIPC(hipMemcpyAsync(res, c->W.ctrl + C_NCTRL, sizeof(double) * C_NCTRL, hipMemcpyDeviceToHost, c->st));
+        HIPC(hipStreamSynchronize(c->st));
+        if (res[C_ACTIVE] == 0.0) break;
+        B = std::min(B * 2, 64);
+    }
+    io.inner = (long)res[C_INNER]; io.local = (long)res[C_LOCAL]; io.clear = (long)res[C_CLEAR];
+    io.rcval = res[C_RCVAL]; io.lag = res[C_LAG]; io.pinf1 = res[C_PINF1]; io.pinfinf = res[C_PINFINF];
+    io.exitReason = (int)res[C_EXIT];
+    c->head = (int)res[C_HEAD]; c->gcur = (int)res[C_GCUR];
+    c->beta[0] = res[C_BETA0]; c->beta[1] = res[C_BETA1]; c->yy[0] = res[C_YY0]; c->yy[1] = res[C_YY1];
+    return 0;
+}
+
+static void alm_log(lrs_ctx *c, const lrs_params *p, const AlmState &st, double t) {
+    int cur = c->t1c.empty() ? sum_rank(c) : c->t1c.back();
+    int orc = c->t1o.empty() ? cur : c->t1o.back();
+    logf_(c, p, "ALM OuterIter:%ld InnerIter:%ld pObj:%5.5e dObj:%5.5e pInfea(1):%5.5e pInfea(Inf):%5.5e pdGap:%5.5e "
+           "rho:%3.2f CurrRank:%d OracleRank:%d Time:%3.2f\n",
+           st.outerIter, st.innerIter, st.pobj, st.dobj, st.pinf1, st.pinfinf, st.gap, st.rho, cur, orc, t);
+}
+
+// LORADS_ALMOptimize, lorads_alm.c:1220-1484
+static int alm_optimize(lrs_ctx *c, const lrs_params *p, AlmState &st, double tss) {
+    const double ori = now_s();
+    int MAX_SUB = 5000;
+    int is_rank_max = check_all_rank_max(c, 1.0);
+    int retcode = 0, last_outer_start = 1, sched_pos = 0;
+    double rc, rc_tol, rc_val = 0, lag = 0;
+    char difficulty;
+    long localIter = 0, clearL = 0;
+    int rank_flag = 0, rho_factor_flag = 0, upd_cnt = 0;
+    double rank_update_factor, rho_update_factor, thres = 15;
+    const int max_inc = 10000, max_ceil = 25000;
+    const bool sched = p->rankSchedule && p->rankScheduleLen > 0 && p->fixedRank <= 0;
+    if (sched && p->rankScheduleLen <= 1) is_rank_max = 1;
+ALG_START:
+    upd_cnt = 0;
+    rc = 0.1;
+    rc_tol = rc / st.rho;
+    if (op_constr_xx(c, c->W.R, nullptr, nullptr, nullptr)) return -1;
+    if (op_grad(c, st.rho, &lag)) return -1;
+    rc_val = std::sqrt(lag) / (1 + c->hp.cNrmInf);
+    difficulty = 'h';
+    localIter = 0; clearL = 0; rank_flag = 0;
+    rank_update_factor = p->rankUpdateFactor;
+    rho_update_factor = p->ALMRhoFactor;
+    rho_factor_flag = 0;
+    if (p->dyrankLevel == 0) thres = 1e8;
+    else if (p->dyrankLevel == 1) thres = 150;
+    else if (p->dyrankLevel == 2) thres = 15;
+    else if (p->dyrankLevel == 3) thres = 5;
+    if (sched && p->nearStallFactor > 0) thres = std::max(1.0, thres * p->nearStallFactor);
+    for (long k = st.outerIter; k <= p->maxALMIter; k++) {
+        double ema_cur = 0, ema_old = 0;
+        int ema_cnt = 1;
+        long cur_iter_counter = 1;
+        if (upd_cnt >= 2) { upd_cnt = 0; MAX_SUB = std::min(MAX_SUB + max_inc, max_ceil); }
+        while (difficulty != 'e') {
+            localIter = 0;
+            int if_break = update_check_ema(&ema_cur, &ema_old, rc_val, 0.1, 0.005, 5, &ema_cnt);
+            if (!if_break && !p->highAccMode) break;
+            if (cur_iter_counter >= MAX_SUB) { upd_cnt += 1; break; }
+            if (rank_flag >= thres && !is_rank_max && (k - last_outer_start >= 3)) break;
+            if (rc_val <= rc_tol) break;
+            // ---- inner L-BFGS loop on the device (lorads_alm.c:1302-1379)
+            InnerIo io;
+            io.inner = st.innerIter; io.local = localIter; io.clear = clearL; io.rcval = rc_val; io.lag = lag;
+            io.pinf1 = st.pinf1; io.pinfinf = st.pinfinf;
+            const long before = st.innerIter;
+            if (run_inner(c, p, st.rho, rc_tol, st.gap, p->almInnerBudget, io)) return -1;
+            st.innerIter = io.inner; localIter = io.local; clearL = io.clear;
+            cur_iter_counter += io.inner - before;
+            rc_val = io.rcval; lag = io.lag; st.pinf1 = io.pinf1; st.pinfinf = io.pinfinf;
+            if (io.exitReason == EXIT_PHASE1) { st.outerIter = k; goto END_ALM; }
+            if (io.exitReason == EXIT_NUMERR) { retcode = 4; goto END_ALM; }
+            if (io.exitReason == EXIT_BUDGET) goto PRINT_AND_EXIT;
+            if (io.exitReason == EXIT_TINYTAU) {
+                if (p->verbose) printf("update rho since tau is too small.\n");
+                goto UpdateRho;
+            }
+            // LORADSUpdateDualVar (lorads_alg_common.c:511) + gradient
+            OPC(launch_dual_update(c->dp, st.rho, c->W.lam, c->W.cvs, c->st));
+            if (op_grad(c, st.rho, &lag)) return -1;
+            rc_val = std::sqrt(lag) / (1 + c->hp.cNrmInf);
+            if (localIter <= 20) difficulty = 'e';
+            else if (localIter <= 100) { difficulty = 'm'; rank_flag += 2; }
+            else if (localIter < 400) { difficulty = 'h'; rank_flag += 3; }
+            else { difficulty = 's'; rank_flag += 4; }
+            if (difficulty == 'e') rank_flag = 0;
+        }
+    UpdateRho:
+        do {
+            st.rho *= rho_update_factor;
+            if (op_grad(c, st.rho, &lag)) return -1;
+            rc_val = std::sqrt(lag) / (1 + c->hp.cNrmInf);
+            rc_tol = rc / st.rho;
+        } while (rc_tol >= rc_val);
+        if (st.rho >= 5e4 && rho_factor_flag < 4) { rho_update_factor = std::sqrt(std::sqrt(rho_update_factor)); rho_factor_flag = 4; }
+        else if (st.rho >= 5e6 && rho_factor_flag < 6) { rho_update_factor = std::sqrt(std::sqrt(rho_update_factor)); rho_factor_flag = 6; }
+        else if (st.rho >= 5e8 && rho_factor_flag < 8) { rho_update_factor = std::sqrt(std::sqrt(rho_update_factor)); rho_factor_flag = 8; }
+        difficulty = 'h';
+        clearL = 0;
+        st.outerIter = k;
+        {
+            if ((st.pinfinf <= p->phase1Tol) && ((st.gap <= p->phase1Tol) || !p->highAccMode)) goto END_ALM;
+            double pinf, obj;
+            if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj)) return -1;
+            c->pObjVal = obj / c->scaleObjHis;
+            cal_dual_obj(c);
+            c->dimPinf = pinf;
+            c->dimGap = std::fabs(c->pObjVal - c->dObjVal) / (1 + std::fabs(c->pObjVal) + std::fabs(c->dObjVal));
+            st.gap = c->dimGap; st.pobj = c->pObjVal; st.dobj = c->dObjVal;
+            st.pinf1 = c->dimPinf;
+            st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+            if (st.gap <= p->phase1Tol * 1e-3 && st.pinf1 <= p->phase1Tol * 1e-3) goto PRINT_AND_EXIT;
+            record_state(c, p, 1);
+            alm_log(c, p, st, now_s() - ori);
+            if (now_s() - tss >= p->timeSecLimit) goto PRINT_AND_EXIT;
+        }
+        if (rank_flag >= thres && !is_rank_max) {
+            rank_flag = 0;
+            if (k - last_outer_start >= 2) {
+                if (p->verbose) printf("increase the rank, factor:%f.\n", rank_update_factor);
+                if (aug_rank(c, rank_update_factor, p, &sched_pos, &is_rank_max)) return -1;
+                st.outerIter = k;
+                last_outer_start = (int)st.outerIter;
+                goto ALG_START;
+            }
+        }
+    }
+END_ALM: {
+        double pinf, obj;
+        if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj)) return -1;
+        c->pObjVal = obj / c->scaleObjHis;
+        cal_dual_obj(c);
+        c->dimPinf = pinf;
+        c->dimGap = std::fabs(c->pObjVal - c->dObjVal) / (1 + std::fabs(c->pObjVal) + std::fabs(c->dObjVal));
+        st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.gap = c->dimGap;
+        st.pinf1 = c->dimPinf;
+        st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+    }
+PRINT_AND_EXIT:
+    logf_(c, p, "-----------------------------------------------------------------------\nExit ALM:\n");
+    record_state(c, p, 1);
+    alm_log(c, p, st, now_s() - ori);
+    return retcode;
+}
+
+// ------------------------------------------------------------------------
+// ADMM phase (lorads_admm.c), host-driven CG on device operators
+// ------------------------------------------------------------------------
+// x -> x + A^*(A(sym(x Y^T))) Y for cone k (linSysProduct, lorads_admm.c:471-486)
+static int lin_sys_product(lrs_ctx *c, int k, const double *Y, const double *x, double *res) {
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    OPC(launch_sddmm(P, k, 0, x, Y, W.uvt2, nullptr, W.part, 0, nullptr, c->st));
+    OPC(launch_gather_cone(P, k, W.uvt2, W.wtmp, c->st));
+    OPC(launch_wsum(P, W.wtmp, 0, W.S, c->st));
+    OPC(launch_spmm(P, k, W.S, Y, 1.0, x, 1.0, res, nullptr, 0, nullptr, c->st));
+    return 0;
+}
+
+static int cone_dot(lrs_ctx *c, int k, const double *x, const double *y, double *out) {
+    const DevCone &d = c->dp.cones[k];
+    return op_dot(c, (long)d.n * d.ld, x + d.foff, y + d.foff, out);
+}
+static int cone_nrm1(lrs_ctx *c, int k, const double *x, double *out) {
+    const DevCone &d = c->dp.cones[k];
+    std::vector<double> h((long)d.n * d.ld);
+    HIPC(hipStreamSynchronize(c->st));
+    HIPC(hipMemcpy(h.data(), x + d.foff, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+    double s = 0;
+    for (double v : h) s += std::fabs(v);
+    *out = s;
+    return 0;
+}
+
+// CGSolve, linalg/lorads_cgs.c:128-287
+static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double *b, double tol, int maxit) {
+    DevWork &W = c->W;
+    const DevCone &d = c->dp.cones[k];
+    const long nr = (long)d.n * d.ld;
+    double *r = W.cg_r + d.foff, *p = W.cg_p + d.foff, *Q = W.cg_Q + d.foff;
+    double *xk = X + d.foff;
+    const double *bk = b + d.foff;
+    double bNorm;
+    if (cone_nrm1(c, k, b, &bNorm)) return -1;
+    if (lin_sys_product(c, k, Y, X, W.cg_r)) return -1;
+    OPC(launch_axpby(nr, 1.0, bk, -1.0, r, c->st));   // r = b - r
+    double rr;
+    if (op_dot(c, nr, r, r, &rr)) return -1;
+    double resi = std::sqrt(rr);
+    if (resi / bNorm < tol) return 0;
+    HIPC(hipMemcpyAsync(p, r, sizeof(double) * nr, hipMemcpyDeviceToDevice, c->st));
+    double qTr = rr;
+    c->cgIterCone[k] = 0;
+    for (int it = 0; it < maxit; ++it) {
+        c->cgIterCone[k] += 1;
+        if (lin_sys_product(c, k, Y, W.cg_p, W.cg_Q)) return -1;
+        double pTQ;
+        if (op_dot(c, nr, p, Q, &pTQ)) return -1;
+        const double alpha = qTr / pTQ;
+        OPC(launch_axpby(nr, alpha, p, 1.0, xk, c->st));
+        OPC(launch_axpby(nr, -alpha, Q, 1.0, r, c->st));
+        if (op_dot(c, nr, r, r, &rr)) return -1;
+        resi = std::sqrt(rr);
+        if (resi / bNorm < tol) return 0;
+        if (it % 20 == 0) {
+            if (lin_sys_product(c, k, Y, X, W.cg_r)) return -1;
+            OPC(launch_axpby(nr, 1.0, bk, -1.0, r, c->st));
+            HIPC(hipMemcpyAsync(p, r, sizeof(double) * nr, hipMemcpyDeviceToDevice, c->st));
+            if (op_dot(c, nr, r, r, &rr)) return -1;
+            qTr = rr;
+        }
+        const double qTrNew = rr;
+        const double beta = qTrNew / qTr;
+        OPC(launch_axpby(nr, 1.0, r, beta, p, c->st));   // p = beta p + r
+        qTr = qTrNew;
+        if (resi != resi) break;
+    }
+    return 0;
+}
+
+// LORADSUpdateSDPVarOne (lorads_admm.c:564-616): solve for X with Y fixed
+static int update_var_one(lrs_ctx *c, int k, double *X, const double *Y, double rho, double tol, int maxit) {
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    const DevCone &d = P.cones[k];
+    OPC(launch_admm_m1(P.m, rho, P.b, W.cvs, W.cvc + (long)k * P.m, W.lam, W.M1, c->st));
+    OPC(launch_wsum(P, W.M1, 1, W.S, c->st));
+    OPC(launch_spmm(P, k, W.S, Y, 1.0, Y, -rho, W.M2, nullptr, 0, nullptr, c->st));   // M2 = S Y - rho Y
+    OPC(launch_axpby((long)d.n * d.ld, -1.0 / rho, W.M2 + d.foff, 0.0, W.cg_b + d.foff, c->st));
+    if (cg_solve(c, k, Y, X, W.cg_b, tol, maxit)) return -1;
+    c->cgIterTotal += c->cgIterCone[k];
+    return 0;
+}
+
+static int refresh_cone(lrs_ctx *c, int k) {   // lorads_alg_common.c:310-314
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    double *cv = W.cvc + (long)k * P.m;
+    OPC(launch_axpby(P.m, -1.0, cv, 1.0, W.cvs, c->st));
+    OPC(launch_sddmm(P, k, 0, W.U, W.V, W.uvt2, nullptr, W.part, 0, nullptr, c->st));
+    OPC(launch_gather_cone(P, k, W.uvt2, cv, c->st));
+    OPC(launch_axpby(P.m, 1.0, cv, 1.0, W.cvs, c->st));
+    return 0;
+}
+
+static int admm_update_var(lrs_ctx *c, double rho, double tol, int maxit) {
+    for (int k = 0; k < c->dp.K; ++k) {
+        if (update_var_one(c, k, c->W.U, c->W.V, rho, tol, maxit)) return -1;
+        if (refresh_cone(c, k)) return -1;
+        if (update_var_one(c, k, c->W.V, c->W.U, rho, tol, maxit)) return -1;
+        if (refresh_cone(c, k)) return -1;
+    }
+    return 0;
+}
+
+static int cal_obj_admm(lrs_ctx *c) {   // LORADSCalObjUV_ADMM lorads_admm.c:398-410
+    OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
+    double o = 0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        OPC(launch_sddmm(c->dp, k, 1, c->W.R, nullptr, c->W.uvt0, nullptr, c->W.part, 0, nullptr, c->st));
+        double t;
+        if (read_tmpfin(c, TF_SD + 2 * k, 1, &t)) return -1;
+        o += t;
+    }
+    c->pObjVal = o / c->scaleObjHis;
+    return 0;
+}
+static int update_dimacs_admm(lrs_ctx *c) {   // lorads_alg_common.c:454-462
+    OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
+    return update_dimacs(c, c->W.R, nullptr, false);
+}
+
+static void admm_log(lrs_ctx *c, const lrs_params *p, const AdmmState &st, double t) {
+    logf_(c, p, "ADMM Iter:%ld pObj:%5.5e dObj:%5.5e pInfea(1):%5.5e pInfea(Inf):%5.5e pdGap:%5.5e rho:%3.2f cgIter:%d "
+           "CurrRank:%d OracleRank:%d Time:%3.2f\n",
+           st.iter, st.pobj, st.dobj, st.pinf1, st.pinfinf, st.gap, st.rho,
+           (int)((double)st.cg_iter / (double)c->dp.K), c->t2c.empty() ? 0 : c->t2c.back(),
+           c->t2o.empty() ? 0 : c->t2o.back(), t);
+}
+
+static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling, double tss) {
+    if (st.gap <= p->phase2Tol && st.pinf1 <= p->phase2Tol) return 0;
+    const int maxCG = 800;
+    const double orig = now_s();
+    st.rho = std::min(st.rho, p->rhoMax);
+    c->cgIterTotal = 0;
+    // LORADSInitConstrValAll(U,V) + Sum
+    {
+        DevProblem &P = c->dp;
+        OPC(launch_fill(P.m, 0.0, c->W.cvs, c->st));
+        for (int k = 0; k < P.K; ++k) {
+            OPC(launch_sddmm(P, k, 0, c->W.U, c->W.V, c->W.uvt2, nullptr, c->W.part, 0, nullptr, c->st));
+            OPC(launch_gather_cone(P, k, c->W.uvt2, c->W.cvc + (long)k * P.m, c->st));
+            OPC(launch_axpby(P.m, 1.0, c->W.cvc + (long)k * P.m, 1.0, c->W.cvs, c->st));
+        }
+    }
+    if (cal_obj_admm(c)) return -1;
+    cal_dual_obj(c);
+    if (update_dimacs_admm(c)) return -1;
+    st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.gap = c->dimGap; st.pinf1 = c->dimPinf;
+    st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+    double cur_rho_max = p->rhoMax, old_mean = 1e30, buf[10] = {0};
+    int bad_pd = 0, count = 0;
+    while (st.iter <= p->maxADMMIter || st.gap >= p->phase2Tol || st.pinf1 >= p->phase2Tol) {
+        if (st.iter >= ceiling) break;
+        const double cgtol = std::min(st.pinf1 * 1e-2, 1e-8);
+        if (admm_update_var(c, st.rho, cgtol, maxCG)) return -1;
+        st.cg_iter = c->cgIterTotal;
+        if (cal_obj_admm(c)) return -1;
+        cal_dual_obj(c);
+        if (update_dimacs_admm(c)) return -1;
+        st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.pinf1 = c->dimPinf;
+        st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+        st.gap = c->dimGap;
+        record_state(c, p, 2);
+        admm_log(c, p, st, now_s() - orig);
+        if (st.pinfinf >= 1e10 || st.gap >= 1 - 1e-8) return 4;
+        if (st.gap <= p->phase2Tol * 5) { bad_pd -= 5; bad_pd = std::max(0, bad_pd); }
+        else if (st.gap <= p->phase2Tol) { bad_pd -= 10; bad_pd = std::max(0, bad_pd); }
+        if (st.gap >= p->phase1Tol * 1e2) bad_pd += 2;
+        if (bad_pd >= 800) return 0;
+        buf[count % 10] = st.pinfinf;
+        if (st.pinfinf <= p->phase2Tol) {
+            if (update_dimacs_admm(c)) return -1;
+            st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.gap = c->dimGap; st.pinf1 = c->dimPinf;
+            return 0;
+        }
+        OPC(launch_dual_update(c->dp, st.rho, c->W.lam, c->W.cvs, c->st));
+        if ((st.iter + 1) % p->rhoFreq == 0) {
+            st.rho *= p->rhoFactor;
+            if (st.rho >= cur_rho_max) {
+                st.rho = cur_rho_max;
+                if ((st.iter + 1) % (p->rhoFreq * 100) == 0) {
+                    double mean = 0;
+                    for (double v : buf) mean += std::fabs(v);
+                    mean /= 10.0;
+                    if (mean / old_mean >= 0.65) {
+                        st.rho *= std::pow(p->rhoFactor, std::round(std::log(p->rhoFreq * 100) / std::log(p->rhoFreq)));
+                        cur_rho_max = st.rho;
+                    }
+                    old_mean = mean;
+                }
+            }
+            if (st.rho >= p->rhoCellingADMM) st.rho = p->rhoCellingADMM;
+        }
+        if (st.iter % 50 == 0) {
+            if (update_dimacs_admm(c)) return -1;
+            st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.gap = c->dimGap; st.pinf1 = c->dimPinf;
+            if (now_s() - tss >= p->timeSecLimit) return 1;
+        }
+        if (st.gap <= p->phase2Tol * 1e-3 && st.pinf1 <= p->phase2Tol * 1e-3) return 0;
+        st.iter++;
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------------
+// C-ABI
+// ------------------------------------------------------------------------
+extern "C" {
+
+void lrs_params_default(lrs_params *p) {   // main.c:56-86
+    memset(p, 0, sizeof(*p));
+    p->initRho = 0.0; p->rhoMax = 5000.0; p->rhoCellingALM = 1e8; p->rhoCellingADMM = 5000.0 * 200;
+    p->maxALMIter = 200; p->maxADMMIter = 10000; p->timesLogRank = 2.0; p->fixedRank = -1; p->initRank = -1;
+    p->rhoFreq = 5; p->rhoFactor = 1.2; p->ALMRhoFactor = 2.0; p->rankUpdateFactor = 1.5; p->phase1Tol = 1e-3;
+    p->phase2Tol = 1e-5; p->timeSecLimit = 3600.0; p->heuristicFactor = 1.0; p->lbfgsListLength = 2;
+    p->endTauTol = 1e-16; p->endALMSubTol = 1e-10; p->l2Rescaling = 0; p->reoptLevel = 2; p->dyrankLevel = 2;
+    p->highAccMode = 0; p->oracleRankNaive = 0; p->disableOracle = 0; p->nearStallFactor = 0.0;
+    p->rankSchedule = nullptr; p->rankScheduleLen = 0; p->verbose = 0; p->almInnerBudget = 0; p->skipADMM = 0;
+}
+
+const char *lrs_last_error(void) { return g_lrs_err.c_str(); }
+const char *lrs_version(void) { return "lrsdp-mi355x 0.1 (gfx950)"; }
+
+int lrs_ctx_create(int device, lrs_ctx **out) {
+    lrs_ctx *c = new lrs_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess) { set_err("hipSetDevice(%d) failed", device); delete c; return -1; }
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); delete c; return -1; }
+    if (hipHostMalloc((void **)&c->hpin, 4096 * sizeof(double), 0) != hipSuccess) { set_err("pinned alloc failed"); delete c; return -1; }
+    *out = c;
+    return 0;
+}
+
+int lrs_set_log_path(lrs_ctx *c, const char *path) {
+    if (c->logfp) fclose(c->logfp);
+    c->logfp = fopen(path, "w");
+    if (!c->logfp) { set_err("cannot open log %s", path); return -1; }
+    size_t sl = std::string(path).find_last_of('/');
+    (void)sl;
+    return 0;
+}
+
+void lrs_ctx_destroy(lrs_ctx *c) {
+    if (!c) return;
+    if (c->logfp) fclose(c->logfp);
+    free_work(c);
+    if (c->loaded) free_problem(c->dp);
+    if (c->hpin) (void)hipHostFree(c->hpin);
+    if (c->st) (void)hipStreamDestroy(c->st);
+    delete c;
+}
+
+int lrs_load_sdpa(lrs_ctx *c, const char *path, double *read_seconds) {
+    const double t0 = now_s();
+    std::string err;
+    HostProblem hp;
+    if (!read_sdpa(path, hp, err)) { set_err("read_sdpa: %s", err.c_str()); return -1; }
+    if (read_seconds) *read_seconds = now_s() - t0;
+    free_work(c);
+    if (c->loaded) free_problem(c->dp);
+    c->hp = std::move(hp);
+    if (!upload_problem(c->hp, c->dp, err)) { set_err("upload: %s", err.c_str()); return -1; }
+    c->loaded = true;
+    c->path = path;
+    c->cgIterCone.assign(c->hp.K, 0);
+    return 0;
+}
+
+int lrs_problem_info(lrs_ctx *c, int *m, int *ncones, int *dims, long *nslots, long *nnzc) {
+    if (!c->loaded) { set_err("no problem loaded"); return -1; }
+    if (m) *m = c->hp.m;
+    if (ncones) *ncones = c->hp.K;
+    if (dims) for (int k = 0; k < c->hp.K; ++k) dims[k] = c->hp.cones[k].n;
+    if (nslots) *nslots = c->dp.Ptot;
+    if (nnzc) *nnzc = c->dp.Z;
+    return 0;
+}
+
+int lrs_determine_rank(lrs_ctx *c, const lrs_params *p, int *ranks_out) {
+    if (!c->loaded) { set_err("no problem loaded"); return -1; }
+    std::vector<int> r, rm;
+    determine_rank(c, p, r, rm);
+    for (int k = 0; k < c->hp.K; ++k) ranks_out[k] = r[k];
+    return 0;
+}
+
+int lrs_set_rank(lrs_ctx *c, const int *ranks) {
+    if (!c->loaded) { set_err("no problem loaded"); return -1; }
+    std::vector<int> r(ranks, ranks + c->hp.K);
+    c->rank_max = r;
+    return alloc_work(c, r);
+}
+int lrs_get_rank(lrs_ctx *c, int *ranks) {
+    for (size_t k = 0; k < c->rank.size(); ++k) ranks[k] = c->rank[k];
+    return 0;
+}
+
+int lrs_factor_set(lrs_ctx *c, int which, const double *colmajor) {
+    if (!c->walloc) { set_err("ranks not set"); return -1; }
+    double *d = factor_ptr(c, which);
+    if (!d) { set_err("bad factor id"); return -1; }
+    return factor_put(c, d, colmajor);
+}
+int lrs_factor_get(lrs_ctx *c, int which, double *colmajor) {
+    if (!c->walloc) { set_err("ranks not set"); return -1; }
+    double *d = factor_ptr(c, which);
+    if (!d) { set_err("bad factor id"); return -1; }
+    return factor_fetch(c, d, colmajor);
+}
+int lrs_vec_set(lrs_ctx *c, int which, const double *v) {
+    if (!c->walloc) { set_err("ranks not set"); return -1; }
+    double *d = vec_ptr(c, which);
+    if (!d) { set_err("bad vector id"); return -1; }
+    HIPC(hipMemcpy(d, v, sizeof(double) * c->dp.m, hipMemcpyHostToDevice));
+    return 0;
+}
+int lrs_vec_get(lrs_ctx *c, int which, double *v) {
+    if (!c->walloc) { set_err("ranks not set"); return -1; }
+    double *d = vec_ptr(c, which);
+    if (!d) { set_err("bad vector id"); return -1; }
+    HIPC(hipStreamSynchronize(c->st));
+    HIPC(hipMemcpy(v, d, sizeof(double) * c->dp.m, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lrs_op_q12(lrs_ctx *c, double *q1, double *p1, double *q2, double *p2) {
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    double a = 0, b = 0;
+    for (int k = 0; k < P.K; ++k) {
+        OPC(launch_sddmm(P, k, 2, W.R, W.D, W.uvt0, W.uvt1, W.part, 0, nullptr, c->st));
+        double t[2];
+        if (read_tmpfin(c, TF_SD + 2 * k, 2, t)) return -1;
+        a += t[0]; b += t[1];
+    }
+    OPC(launch_gather(P, W.uvt0, 2.0, W.q1, nullptr, nullptr, c->st, nullptr));
+    OPC(launch_gather(P, W.uvt1, 1.0, W.q2, nullptr, nullptr, c->st, nullptr));
+    // also leave the finals the device line search consumes
+    double *fin = device_fin();
+    double h[128] = {0};
+    for (int k = 0; k < P.K && k < 32; ++k) { h[2 * k] = (k == 0 ? a : 0.0); h[2 * k + 1] = (k == 0 ? b : 0.0); }
+    HIPC(hipMemcpy(fin, h, sizeof(double) * 2 * std::max(1, std::min(P.K, 32)), hipMemcpyHostToDevice));
+    if (p1) *p1 = 2 * a;
+    if (p2) *p2 = b;
+    HIPC(hipStreamSynchronize(c->st));
+    if (q1) HIPC(hipMemcpy(q1, W.q1, sizeof(double) * P.m, hipMemcpyDeviceToHost));
+    if (q2) HIPC(hipMemcpy(q2, W.q2, sizeof(double) * P.m, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int lrs_op_constr_rr(lrs_ctx *c, double *cvs, double *pinf, double *pobj) {
+    double pi, ob;
+    if (op_constr_xx(c, c->W.R, nullptr, &pi, &ob)) return -1;
+    if (pinf) *pinf = pi;
+    if (pobj) *pobj = ob / c->scaleObjHis;
+    if (cvs) {
+        HIPC(hipStreamSynchronize(c->st));
+        HIPC(hipMemcpy(cvs, c->W.cvs, sizeof(double) * c->dp.m, hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+int lrs_op_grad(lrs_ctx *c, double rho, double *lag) {
+    double l;
+    if (op_grad(c, rho, &l)) return -1;
+    if (lag) *lag = l;
+    return 0;
+}
+
+int lrs_op_line_search(lrs_ctx *c, double rho, double *tau, int *root_num) {
+    double par[P_NPAR] = {0};
+    par[P_RHO] = rho;
+    par[P_ENDTAU] = 1e-16;
+    HIPC(hipMemcpy(c->W.par, par, sizeof(par), hipMemcpyHostToDevice));
+    OPC(launch_ls_only(c->dp, c->W, c->st));
+    double ls[LS_N];
+    HIPC(hipStreamSynchronize(c->st));
+    HIPC(hipMemcpy(ls, c->W.lsres, sizeof(ls), hipMemcpyDeviceToHost));
+    if (tau) *tau = ls[LS_TAU];
+    if (root_num) *root_num = (int)ls[LS_ROOTNUM];
+    return 0;
+}
+
+int lrs_op_lbfgs(lrs_ctx *c, int node_num, double beta_new, double beta_old) {
+    // White-box test of the fused direction kernel: ring slot 0 = newest pair
+    // (S0, Y0, beta_new), slot 1 = older pair (S1, Y1, beta_old), gradient G[gcur].
+    if (node_num < 0 || node_num > 2) { set_err("node_num must be 0..2"); return -1; }
+    DevWork &W = c->W;
+    const long NR = c->dp.NRpad;
+    const double *G = W.G[c->gcur];
+    double d[9];
+    const double *pairs[9][2] = {{G, G}, {W.ls[0], G}, {W.ly[0], G}, {W.ls[1], G}, {W.ly[1], G},
+                                 {W.ls[1], W.ly[0]}, {W.ly[1], W.ly[0]}, {W.ly[0], W.ly[0]}, {W.ly[1], W.ly[1]}};
+    for (int q = 0; q < 9; ++q)
+        if (op_dot(c, NR, pairs[q][0], pairs[q][1], &d[q])) return -1;
+    double par[P_NPAR] = {0};
+    par[P_L] = 2; par[P_RCTOL] = -1e300; par[P_ENDSUB] = 0;
+    HIPC(hipMemcpy(W.par, par, sizeof(par), hipMemcpyHostToDevice));
+    double ctl[C_NCTRL] = {0};
+    ctl[C_ACTIVE] = 1; ctl[C_PENDING] = 2; ctl[C_RCVAL] = 1.0;
+    ctl[C_LOCAL] = node_num == 0 ? 0 : 1; ctl[C_CLEAR] = node_num;
+    ctl[C_HEAD] = 1;                 // newest = slot 0, older = slot 1
+    ctl[C_GCUR] = c->gcur; ctl[C_LAG] = d[0];
+    ctl[C_BETA0] = beta_new; ctl[C_BETA1] = beta_old; ctl[C_YY0] = d[7]; ctl[C_YY1] = d[8];
+    ctl[C_DSG] = d[1]; ctl[C_DYG] = d[2]; ctl[C_DSOG] = d[3]; ctl[C_DYOG] = d[4]; ctl[C_DSOY] = d[5];
+    ctl[C_DYOY] = d[6];
+    HIPC(hipMemcpy(W.ctrl + C_NCTRL, ctl, sizeof(ctl), hipMemcpyHostToDevice));
+    OPC(launch_alm_dir_only(c->dp, W, c->st));
+    HIPC(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int lrs_op_admm_half(lrs_ctx *c, double rho, double cg_tol, int cg_maxit, int *cg_iters, double *rhs) {
+    DevProblem &P = c->dp;
+    OPC(launch_fill(P.m, 0.0, c->W.cvs, c->st));
+    for (int k = 0; k < P.K; ++k) {
+        OPC(launch_sddmm(P, k, 0, c->W.U, c->W.V, c->W.uvt2, nullptr, c->W.part, 0, nullptr, c->st));
+        OPC(launch_gather_cone(P, k, c->W.uvt2, c->W.cvc + (long)k * P.m, c->st));
+        OPC(launch_axpby(P.m, 1.0, c->W.cvc + (long)k * P.m, 1.0, c->W.cvs, c->st));
+    }
+    c->cgIterCone.assign(P.K, 0);
+    if (update_var_one(c, 0, c->W.U, c->W.V, rho, cg_tol, cg_maxit)) return -1;
+    if (cg_iters) *cg_iters = (int)c->cgIterCone[0];
+    if (rhs) {
+        std::vector<double> h(c->dp.NRpad);
+        HIPC(hipStreamSynchronize(c->st));
+        HIPC(hipMemcpy(h.data(), c->W.cg_b, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+        const DevCone &d = P.cones[0];
+        for (int q = 0; q < d.r; ++q)
+            for (int i = 0; i < d.n; ++i) rhs[i + (long)q * d.n] = h[d.foff + (long)i * d.ld + q];
+    }
+    return 0;
+}
+
+int lrs_op_gram(lrs_ctx *c, int cone, int which, double *gram) {
+    std::vector<double> g;
+    if (which == LRS_R) { if (gram_of(c, cone, c->W.R, nullptr, 0, g)) return -1; }
+    else { if (gram_of(c, cone, c->W.U, c->W.V, 1, g)) return -1; }
+    memcpy(gram, g.data(), sizeof(double) * g.size());
+    return 0;
+}
+
+static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
+    lrs_params prm = *pin;
+    lrs_params *p = &prm;
+    p->rhoCellingADMM = p->rhoMax * 200;   // main.c:350
+    memset(res, 0, sizeof(*res));
+    const double tss = now_s();
+    std::vector<int> r, rm;
+    determine_rank(c, p, r, rm);
+    if (alloc_work(c, r)) return -1;
+    c->rank_max = rm;
+    if (init_point(c)) return -1;
+    c->t1c.clear(); c->t1o.clear(); c->t2c.clear(); c->t2o.clear();
+    c->scaleObjHis = 1.0;
+    c->pObjVal = c->dObjVal = 0;
+    AlmState alm;
+    AdmmState admm;
+    double rho = p->initRho;
+    if (rho == 0) {   // initial_solver_state, data/lorads_solver.c:1599-1606
+        long sd = 0;
+        for (auto &hc : c->hp.cones) sd += hc.n;
+        rho = 1 / std::sqrt((double)sd);
+    }
+    alm.rho = rho; admm.rho = rho;
+    const double t0 = now_s();
+    int rc = alm_optimize(c, p, alm, tss);
+    if (rc < 0) return -1;
+    res->retcode = rc;
+    const double t_alm = now_s() - t0;
+    res->alm_inner = alm.innerIter; res->alm_outer = alm.outerIter;
+    res->alm_pobj = alm.pobj; res->alm_dobj = alm.dobj; res->alm_pinf = alm.pinf1; res->alm_gap = alm.gap;
+    res->alm_rho = alm.rho;
+    res->alm_time = t_alm;
+    bool timeout = now_s() - tss > p->timeSecLimit;
+    double t_admm = 0;
+    if (!timeout && !p->skipADMM) {
+        // LORADS_ALMtoADMM (data/lorads_solver.c:1351-1387)
+        HIPC(hipMemcpyAsync(c->W.V, c->W.R, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
+        HIPC(hipMemcpyAsync(c->W.U, c->W.V, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
+        admm.pinf1 = alm.pinf1; admm.pinfinf = alm.pinfinf; admm.gap = alm.gap;
+        admm.rho = alm.rho * p->heuristicFactor;
+        if (alm.rho > p->rhoMax) {
+            admm.rho = std::min(std::sqrt(std::max(p->rhoMax, alm.rho) / p->rhoMax) * p->rhoMax, alm.rho);
+            p->rhoMax = admm.rho;
+        }
+        const double ta = now_s();
+        int arc = admm_optimize(c, p, admm, p->maxADMMIter, tss);
+        if (arc < 0) return -1;
+        t_admm = now_s() - ta;
+    }
+    HIPC(hipStreamSynchronize(c->st));
+    const double all_time = now_s() - t0;
+    // main.c:519-525
+    admm.gap = c->dimGap;
+    admm.pinf1 = c->dimPinf;
+    admm.pinfinf = c->dimPinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+    res->admm_iter = admm.iter; res->cg_iter = admm.cg_iter;
+    res->pobj = admm.pobj; res->dobj = admm.dobj; res->pinf = admm.pinf1; res->pinf_inf = admm.pinfinf;
+    res->gap = admm.gap; res->rho = admm.rho;
+    res->solve_time = all_time; res->admm_time = t_admm;
+    res->rho_max = p->rhoMax;
+    if (timeout) res->status = 4;
+    else if (admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol) res->status = 2;   // dual infeasibility not evaluated
+    else res->status = 3;
+    res->final_rank = sum_rank(c);
+    int orc = (p->disableOracle || p->skipADMM) ? res->final_rank : oracle_rank(c, 2);
+    res->oracle_rank = orc < 0 ? 0 : orc;
+    res->traj1_len = (int)c->t1c.size();
+    res->traj2_len = (int)c->t2c.size();
+    return 0;
+}
+
+int lrs_solve(lrs_ctx *c, const lrs_params *p, lrs_result *res) {
+    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    return solve_impl(c, p, res);
+}
+
+int lrs_trajectory(lrs_ctx *c, int phase, int *curr, int *orc, int cap) {
+    const std::vector<int> &a = phase == 1 ? c->t1c : c->t2c, &b = phase == 1 ? c->t1o : c->t2o;
+    int n = std::min(cap, (int)a.size());
+    for (int i = 0; i < n; ++i) { if (curr) curr[i] = a[i]; if (orc) orc[i] = b[i]; }
+    return (int)a.size();
+}
+
+int lrs_write_json(lrs_ctx *c, const char *path, const char *pid, const char *fpath, const lrs_result *r,
+                   const lrs_params *p) {
+    FILE *f = fopen(path, "w");
+    if (!f) { set_err("cannot open %s", path); return -1; }
+    fprintf(f, "{\n");
+    fprintf(f, "  \"problem_id\": \"%s\",\n", pid);
+    fprintf(f, "  \"file_path\": \"%s\",\n", fpath);
+    fprintf(f, "  \"metrics\": {\n");
+    fprintf(f, "    \"oracle_rank\": %lld,\n", (long long)r->oracle_rank);
+    fprintf(f, "    \"primal_obj\": %.16e,\n", r->pobj);
+    fprintf(f, "    \"dual_obj\": %.16e,\n", r->dobj);
+    fprintf(f, "    \"constr_violation_l1\": %.16e,\n", r->pinf);
+    fprintf(f, "    \"constr_violation_inf\": %.16e,\n", r->pinf_inf);
+    fprintf(f, "    \"primal_dual_gap\": %.16e,\n", r->gap);
+    fprintf(f, "    \"solve_time_sec\": %.16e,\n", r->solve_time);
+    fprintf(f, "    \"rho_max\": %.16e,\n", r->rho_max != 0 ? r->rho_max : p->rhoMax);
+    fprintf(f, "    \"heuristic_factor\": %.16e\n", p->heuristicFactor);
+    fprintf(f, "  },\n");
+    fprintf(f, "  \"trajectory\": {\n");
+    for (int ph = 1; ph <= 2; ++ph) {
+        const std::vector<int> &a = ph == 1 ? c->t1c : c->t2c, &b = ph == 1 ? c->t1o : c->t2o;
+        fprintf(f, "    \"phase_%d\": {\n      \"curr_rank\": [", ph);
+        for (size_t i = 0; i < a.size(); ++i) fprintf(f, "%s%lld", i ? ", " : "", (long long)a[i]);
+        fprintf(f, "],\n      \"oracle_rank\": [");
+        for (size_t i = 0; i < b.size(); ++i) fprintf(f, "%s%lld", i ? ", " : "", (long long)b[i]);
+        fprintf(f, "]\n    }%s\n", ph == 1 ? "," : "");
+    }
+    fprintf(f, "  }\n}\n");
+    fclose(f);
+    return 0;
+}
+
+int lrs_alm_throughput(lrs_ctx *c, const lrs_params *pin, long warmup, long steps, double *seconds, long *done,
+                       double *sddmm_avg_ms, double *iter_avg_ms) {
+    // ALM iters/s: the real phase-1 control flow (lorads_alm.c:1220)
+    // at fixed rank with the phase-1 exit disabled, stopped after a budget of inner
+    // iterations.  Warmup = an untimed run of `warmup` iterations from the same start;
+    // the timed run does exactly `steps` inner iterations.
+    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    lrs_params prm = *pin;
+    prm.phase1Tol = 1e-300;
+    prm.maxALMIter = 1000000000;
+    prm.skipADMM = 1;
+    prm.timeSecLimit = 1e30;
+    lrs_result r;
+    if (warmup > 0) {
+        prm.almInnerBudget = warmup;
+        if (solve_impl(c, &prm, &r)) return -1;
+    }
+    prm.almInnerBudget = steps;
+    hipEvent_t e0, e1;
+    HIPC(hipEventCreate(&e0));
+    HIPC(hipEventCreate(&e1));
+    HIPC(hipDeviceSynchronize());
+    const double h0 = now_s();
+    HIPC(hipEventRecord(e0, c->st));
+    if (solve_impl(c, &prm, &r)) return -1;
+    HIPC(hipEventRecord(e1, c->st));
+    HIPC(hipEventSynchronize(e1));
+    const double h1 = now_s();
+    if (seconds) *seconds = h1 - h0;
+    if (done) *done = r.alm_inner;
+    if (iter_avg_ms) *iter_avg_ms = (h1 - h0) * 1e3 / std::max(1L, r.alm_inner);
+    if (sddmm_avg_ms) {
+        // A(U U^T) operator on the final iterate, same stream: SDDMM(R,R) over the pattern
+        // + per-constraint gather, timed with HIP events (lrs_time_auut)
+        double ms = 0;
+        if (lrs_time_auut(c, 200, &ms)) return -1;
+        *sddmm_avg_ms = ms;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 0;
+}
+
+int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {
+    hipEvent_t e0, e1;
+    HIPC(hipEventCreate(&e0));
+    HIPC(hipEventCreate(&e1));
+    HIPC(hipEventRecord(e0, c->st));
+    for (int q = 0; q < reps; ++q) {
+        for (int k = 0; k < c->dp.K; ++k)
+            OPC(launch_sddmm(c->dp, k, 1, c->W.R, nullptr, c->W.uvt2, nullptr, c->W.part, 0, nullptr, c->st));
+        OPC(launch_gather(c->dp, c->W.uvt2, 1.0, c->W.q1, nullptr, nullptr, c->st, nullptr));
+    }
+    HIPC(hipEventRecord(e1, c->st));
+    HIPC(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPC(hipEventElapsedTime(&ms, e0, e1));
+    *avg_ms = ms / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 0;
+}
+
+}  // extern "C"

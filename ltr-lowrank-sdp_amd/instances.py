@@ -1,0 +1,187 @@
+"""Seeded synthetic SDPA instances for the BASELINE configs.
+
+The real Gset / SDPLIB files named by BASELINE.json (G1, G22, G67, G81, theta3)
+are not in the reference checkout (`.MISSING_LARGE_BLOBS`), so every config is
+restated as a generator with the same structure:
+
+* MaxCut (lorads/data/gen_MaxCut.jl:213-243): A_i = e_i e_i^T, b_i = 1, and the
+  objective written as ``0 1 i j v`` with v = L_ij / 2 for i <= j, so the
+  reader's ``C = -F0`` (io/lorads_file_io.c:317-319) gives C = -L/2.
+* Lovász theta: C = -J (dense), tr(X) = 1, X_ij = 0 on edges.
+* random sparse SDP (C5): C = I (or dense), A_i with k random lower entries,
+  b_i = <A_i, I> so X = I is feasible.
+
+Files are written in plain SDPA ``.dat-s`` text, one entry per line.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+__all__ = [
+    "maxcut_random",
+    "maxcut_torus",
+    "theta",
+    "theta_multiblock",
+    "random_sparse",
+    "write_sdpa",
+    "config_instance",
+]
+
+
+def write_sdpa(path, m, dims, b, entries):
+    """entries: iterable of arrays (con, blk, i, j, v) with 1-based blk/i/j, i <= j."""
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        f.write(f"{m}\n{len(dims)}\n")
+        f.write(" ".join(str(int(d)) for d in dims) + "\n")
+        f.write(" ".join(repr(float(x)) for x in b) + "\n")
+        for con, blk, ii, jj, vv in entries:
+            con = np.asarray(con, dtype=np.int64)
+            blk = np.broadcast_to(np.asarray(blk, dtype=np.int64), con.shape)
+            lines = [
+                f"{c} {bk} {i} {j} {v!r}\n"
+                for c, bk, i, j, v in zip(con.tolist(), blk.tolist(), np.asarray(ii).tolist(),
+                                          np.asarray(jj).tolist(), np.asarray(vv, dtype=float).tolist())
+            ]
+            f.writelines(lines)
+    return path
+
+
+def _maxcut_from_edges(path, n, ei, ej, w):
+    """MaxCut SDP from an edge list (0-based, i != j)."""
+    lo = np.minimum(ei, ej)
+    hi = np.maximum(ei, ej)
+    deg = np.zeros(n)
+    np.add.at(deg, lo, w)
+    np.add.at(deg, hi, w)
+    # objective: 0.5 * L, L = D - A: off-diagonal -w/2, diagonal deg/2
+    obj_i = np.concatenate([lo, np.arange(n)]) + 1
+    obj_j = np.concatenate([hi, np.arange(n)]) + 1
+    obj_v = np.concatenate([-0.5 * w, 0.5 * deg])
+    keep = np.abs(obj_v) >= 1e-12
+    con_i = np.arange(1, n + 1)
+    entries = [
+        (np.zeros(int(keep.sum()), dtype=np.int64), 1, obj_i[keep], obj_j[keep], obj_v[keep]),
+        (con_i, 1, con_i, con_i, np.ones(n)),
+    ]
+    return write_sdpa(path, n, [n], np.ones(n), entries)
+
+
+def maxcut_random(path, n, n_edges, seed, weights="one"):
+    """G1/G22-like: uniform random graph with exactly n_edges edges."""
+    rng = np.random.default_rng(seed)
+    total = n * (n - 1) // 2
+    pick = rng.choice(total, size=n_edges, replace=False)
+    # unrank pair index -> (i, j), i < j
+    i = (n - 2 - np.floor(np.sqrt(-8 * pick + 4 * n * (n - 1) - 7) / 2.0 - 0.5)).astype(np.int64)
+    j = (pick + i + 1 - n * (n - 1) // 2 + (n - i) * ((n - i) - 1) // 2).astype(np.int64)
+    w = np.ones(n_edges) if weights == "one" else rng.choice([-1.0, 1.0], size=n_edges)
+    return _maxcut_from_edges(path, n, i, j, w)
+
+
+def maxcut_torus(path, rows, cols, seed):
+    """G67/G81-like: 2-D toroidal grid rows x cols, weights uniform in {-1, +1}."""
+    rng = np.random.default_rng(seed)
+    n = rows * cols
+    idx = np.arange(n).reshape(rows, cols)
+    right = np.roll(idx, -1, axis=1)
+    down = np.roll(idx, -1, axis=0)
+    ei = np.concatenate([idx.ravel(), idx.ravel()])
+    ej = np.concatenate([right.ravel(), down.ravel()])
+    w = rng.choice([-1.0, 1.0], size=ei.size)
+    return _maxcut_from_edges(path, n, ei, ej, w)
+
+
+def _theta_entries(n, ei, ej, blk, con0):
+    iu, ju = np.triu_indices(n)
+    entries = [(np.zeros(iu.size, dtype=np.int64), blk, iu + 1, ju + 1, np.ones(iu.size))]
+    d = np.arange(1, n + 1)
+    entries.append((np.full(n, con0, dtype=np.int64), blk, d, d, np.ones(n)))
+    lo = np.minimum(ei, ej) + 1
+    hi = np.maximum(ei, ej) + 1
+    entries.append((con0 + 1 + np.arange(ei.size), blk, lo, hi, np.ones(ei.size)))
+    return entries
+
+
+def _random_edges(rng, n, n_edges):
+    total = n * (n - 1) // 2
+    pick = rng.choice(total, size=n_edges, replace=False)
+    i = (n - 2 - np.floor(np.sqrt(-8 * pick + 4 * n * (n - 1) - 7) / 2.0 - 0.5)).astype(np.int64)
+    j = (pick + i + 1 - n * (n - 1) // 2 + (n - i) * ((n - i) - 1) // 2).astype(np.int64)
+    return i, j
+
+
+def theta(path, n, n_edges, seed):
+    """theta3-like Lovász theta SDP (single block, dense C = -J)."""
+    rng = np.random.default_rng(seed)
+    ei, ej = _random_edges(rng, n, n_edges)
+    m = 1 + n_edges
+    b = np.zeros(m)
+    b[0] = 1.0
+    return write_sdpa(path, m, [n], b, _theta_entries(n, ei, ej, 1, 1))
+
+
+def theta_multiblock(path, n, n_edges, nblocks, seed):
+    """Block-diagonal stack of independent theta instances (multi-cone coverage)."""
+    rng = np.random.default_rng(seed)
+    entries, b = [], []
+    con0 = 1
+    for blk in range(1, nblocks + 1):
+        ei, ej = _random_edges(rng, n, n_edges)
+        entries += _theta_entries(n, ei, ej, blk, con0)
+        b += [1.0] + [0.0] * n_edges
+        con0 += 1 + n_edges
+    return write_sdpa(path, len(b), [n] * nblocks, np.array(b), entries)
+
+
+def random_sparse(path, n, m, k, seed, dense_c=False):
+    """C5-like: C = I (or dense), each A_i has k random lower-triangle N(0,1) entries,
+    b_i = <A_i, I> (X = I feasible)."""
+    rng = np.random.default_rng(seed)
+    ii = rng.integers(0, n, size=(m, k))
+    jj = rng.integers(0, n, size=(m, k))
+    lo = np.minimum(ii, jj)
+    hi = np.maximum(ii, jj)
+    v = rng.standard_normal((m, k))
+    b = np.where(lo == hi, v, 0.0).sum(axis=1)
+    con = np.repeat(np.arange(1, m + 1), k)
+    entries = []
+    if dense_c:
+        iu, ju = np.triu_indices(n)
+        cv = rng.standard_normal(iu.size) / np.sqrt(n)
+        cv[iu == ju] += n
+        entries.append((np.zeros(iu.size, dtype=np.int64), 1, iu + 1, ju + 1, -cv))
+    else:
+        d = np.arange(1, n + 1)
+        entries.append((np.zeros(n, dtype=np.int64), 1, d, d, -np.ones(n)))
+    entries.append((con, 1, lo.ravel() + 1, hi.ravel() + 1, v.ravel()))
+    return write_sdpa(path, m, [n], b, entries)
+
+
+# BASELINE.json configs restated; small = parity-test sizes
+CONFIGS = {
+    "G1": dict(kind="maxcut_random", n=800, n_edges=19176, seed=1),
+    "G22": dict(kind="maxcut_random", n=2000, n_edges=19990, seed=22),
+    "G67": dict(kind="maxcut_torus", rows=100, cols=100, seed=67),
+    "G81": dict(kind="maxcut_torus", rows=100, cols=200, seed=81),
+    "theta3": dict(kind="theta", n=150, n_edges=1105, seed=3),
+    "theta3x3": dict(kind="theta_multiblock", n=150, n_edges=1105, nblocks=3, seed=3),
+    "R2000": dict(kind="maxcut_torus", rows=2000, cols=2000, seed=2000),
+}
+
+
+def config_instance(name, directory):
+    """Write (once) and return the path of a config instance."""
+    spec = dict(CONFIGS[name])
+    kind = spec.pop("kind")
+    path = os.path.join(directory, f"{name}.dat-s")
+    if os.path.exists(path):
+        return path
+    fn = {"maxcut_random": maxcut_random, "maxcut_torus": maxcut_torus, "theta": theta,
+          "theta_multiblock": theta_multiblock, "random_sparse": random_sparse}[kind]
+    tmp = path + f".tmp{os.getpid()}"
+    fn(tmp, **spec)
+    os.replace(tmp, path)
+    return path

@@ -1,0 +1,294 @@
+"""Host-side mirror of the reference's solver interface over the C-ABI
+(include/lrsdp.h).
+
+* :func:`run_lorads` mirrors benchmark.py's ``run_lorads`` (benchmark.py:219-285):
+  same argv contract, runs the MI355X drop-in binary, returns
+  ``(success, solve_time_sec, primal_obj)`` from the JSON metrics.
+* :class:`Solver` exposes the per-operator entry points (the reference's
+  ``lorads_func`` / cone / coefficient vtable slots, lorads_solver.c:1014-1053)
+  for tests and benchmarking.
+
+The product path is the HIP library; there is no CPU fallback: importing this
+module on a machine without the built ``liblrsdp.so`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "_build" / "liblrsdp.so"
+BIN_PATH = _HERE / "_build" / "LoRADS_v_2_0_1-alpha"
+
+R, D, G, U, V, S0, Y0, S1, Y1 = range(9)
+LAMBDA, CVS, Q1, Q2, B = range(5)
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("initRho", C.c_double), ("rhoMax", C.c_double), ("rhoCellingALM", C.c_double),
+        ("rhoCellingADMM", C.c_double), ("maxALMIter", C.c_int), ("maxADMMIter", C.c_int),
+        ("timesLogRank", C.c_double), ("fixedRank", C.c_int), ("initRank", C.c_int), ("rhoFreq", C.c_int),
+        ("rhoFactor", C.c_double), ("ALMRhoFactor", C.c_double), ("rankUpdateFactor", C.c_double),
+        ("phase1Tol", C.c_double), ("phase2Tol", C.c_double), ("timeSecLimit", C.c_double),
+        ("heuristicFactor", C.c_double), ("lbfgsListLength", C.c_int), ("endTauTol", C.c_double),
+        ("endALMSubTol", C.c_double), ("l2Rescaling", C.c_int), ("reoptLevel", C.c_int),
+        ("dyrankLevel", C.c_int), ("highAccMode", C.c_int), ("oracleRankNaive", C.c_int),
+        ("disableOracle", C.c_int), ("nearStallFactor", C.c_double), ("rankSchedule", C.POINTER(C.c_int)),
+        ("rankScheduleLen", C.c_int), ("verbose", C.c_int), ("almInnerBudget", C.c_long), ("skipADMM", C.c_int),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [
+        ("alm_inner", C.c_long), ("alm_outer", C.c_long), ("admm_iter", C.c_long), ("cg_iter", C.c_long),
+        ("alm_pobj", C.c_double), ("alm_dobj", C.c_double), ("alm_pinf", C.c_double), ("alm_gap", C.c_double),
+        ("alm_rho", C.c_double), ("pobj", C.c_double), ("dobj", C.c_double), ("pinf", C.c_double),
+        ("pinf_inf", C.c_double), ("gap", C.c_double), ("rho", C.c_double), ("solve_time", C.c_double),
+        ("alm_time", C.c_double), ("admm_time", C.c_double), ("read_time", C.c_double), ("status", C.c_int),
+        ("retcode", C.c_int), ("final_rank", C.c_int), ("oracle_rank", C.c_int), ("traj1_len", C.c_int),
+        ("traj2_len", C.c_int), ("rho_max", C.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load liblrsdp.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(f"HIP library not built: {p} (run __graft_entry__.build())")
+    lib = C.CDLL(str(p))
+    dp = C.POINTER(C.c_double)
+    ip = C.POINTER(C.c_int)
+    vp = C.c_void_p
+    sig = {
+        "lrs_params_default": (None, [C.POINTER(Params)]),
+        "lrs_last_error": (C.c_char_p, []),
+        "lrs_version": (C.c_char_p, []),
+        "lrs_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "lrs_ctx_destroy": (None, [vp]),
+        "lrs_load_sdpa": (C.c_int, [vp, C.c_char_p, dp]),
+        "lrs_problem_info": (C.c_int, [vp, ip, ip, ip, C.POINTER(C.c_long), C.POINTER(C.c_long)]),
+        "lrs_determine_rank": (C.c_int, [vp, C.POINTER(Params), ip]),
+        "lrs_set_rank": (C.c_int, [vp, ip]),
+        "lrs_get_rank": (C.c_int, [vp, ip]),
+        "lrs_factor_set": (C.c_int, [vp, C.c_int, dp]),
+        "lrs_factor_get": (C.c_int, [vp, C.c_int, dp]),
+        "lrs_vec_set": (C.c_int, [vp, C.c_int, dp]),
+        "lrs_vec_get": (C.c_int, [vp, C.c_int, dp]),
+        "lrs_op_q12": (C.c_int, [vp, dp, dp, dp, dp]),
+        "lrs_op_constr_rr": (C.c_int, [vp, dp, dp, dp]),
+        "lrs_op_grad": (C.c_int, [vp, C.c_double, dp]),
+        "lrs_op_line_search": (C.c_int, [vp, C.c_double, dp, ip]),
+        "lrs_op_lbfgs": (C.c_int, [vp, C.c_int, C.c_double, C.c_double]),
+        "lrs_op_admm_half": (C.c_int, [vp, C.c_double, C.c_double, C.c_int, ip, dp]),
+        "lrs_op_gram": (C.c_int, [vp, C.c_int, C.c_int, dp]),
+        "lrs_solve": (C.c_int, [vp, C.POINTER(Params), C.POINTER(Result)]),
+        "lrs_trajectory": (C.c_int, [vp, C.c_int, ip, ip, C.c_int]),
+        "lrs_write_json": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(Result),
+                                     C.POINTER(Params)]),
+        "lrs_alm_throughput": (C.c_int, [vp, C.POINTER(Params), C.c_long, C.c_long, dp, C.POINTER(C.c_long),
+                                         dp, dp]),
+        "lrs_set_log_path": (C.c_int, [vp, C.c_char_p]),
+        "lrs_time_auut": (C.c_int, [vp, C.c_int, dp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def default_params(**kw):
+    lib = load_library()
+    p = Params()
+    lib.lrs_params_default(C.byref(p))
+    sched = kw.pop("rankSchedule", None)
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise AttributeError(k)
+        setattr(p, k, v)
+    if sched:
+        arr = (C.c_int * len(sched))(*sched)
+        p.rankSchedule = arr
+        p.rankScheduleLen = len(sched)
+        p._sched_keepalive = arr
+    return p
+
+
+def _dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Solver:
+    """One device context with a loaded SDPA problem."""
+
+    def __init__(self, path, device=0):
+        self.lib = load_library()
+        self.ctx = C.c_void_p()
+        self._check(self.lib.lrs_ctx_create(device, C.byref(self.ctx)), "ctx_create")
+        t = C.c_double()
+        self._check(self.lib.lrs_load_sdpa(self.ctx, str(path).encode(), C.byref(t)), "load_sdpa")
+        self.read_time = t.value
+        m, k = C.c_int(), C.c_int()
+        self._check(self.lib.lrs_problem_info(self.ctx, C.byref(m), C.byref(k), None, None, None), "info")
+        self.m, self.K = m.value, k.value
+        dims = (C.c_int * self.K)()
+        ns, nz = C.c_long(), C.c_long()
+        self._check(self.lib.lrs_problem_info(self.ctx, None, None, dims, C.byref(ns), C.byref(nz)), "info")
+        self.dims = list(dims)
+        self.nslots, self.nnz = ns.value, nz.value
+        self.ranks = None
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what}: {self.lib.lrs_last_error().decode()}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.lrs_ctx_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- ranks / state
+    def determine_rank(self, **kw):
+        out = (C.c_int * self.K)()
+        self._check(self.lib.lrs_determine_rank(self.ctx, C.byref(default_params(**kw)), out), "determine_rank")
+        return list(out)
+
+    def set_rank(self, ranks):
+        ranks = list(ranks)
+        self._check(self.lib.lrs_set_rank(self.ctx, (C.c_int * self.K)(*ranks)), "set_rank")
+        self.ranks = ranks
+
+    def nr(self):
+        return sum(n * r for n, r in zip(self.dims, self.ranks))
+
+    def set_factor(self, which, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        assert x.size == self.nr()
+        self._check(self.lib.lrs_factor_set(self.ctx, which, _dptr(x)), "factor_set")
+
+    def get_factor(self, which):
+        x = np.empty(self.nr())
+        self._check(self.lib.lrs_factor_get(self.ctx, which, _dptr(x)), "factor_get")
+        return x
+
+    def set_vec(self, which, v):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        assert v.size == self.m
+        self._check(self.lib.lrs_vec_set(self.ctx, which, _dptr(v)), "vec_set")
+
+    def get_vec(self, which):
+        v = np.empty(self.m)
+        self._check(self.lib.lrs_vec_get(self.ctx, which, _dptr(v)), "vec_get")
+        return v
+
+    # ---- operators
+    def q12(self):
+        q1, q2 = np.empty(self.m), np.empty(self.m)
+        p1, p2 = C.c_double(), C.c_double()
+        self._check(self.lib.lrs_op_q12(self.ctx, _dptr(q1), C.byref(p1), _dptr(q2), C.byref(p2)), "q12")
+        return q1, p1.value, q2, p2.value
+
+    def constr_rr(self):
+        cvs = np.empty(self.m)
+        pinf, pobj = C.c_double(), C.c_double()
+        self._check(self.lib.lrs_op_constr_rr(self.ctx, _dptr(cvs), C.byref(pinf), C.byref(pobj)), "constr_rr")
+        return cvs, pinf.value, pobj.value
+
+    def grad(self, rho):
+        lag = C.c_double()
+        self._check(self.lib.lrs_op_grad(self.ctx, rho, C.byref(lag)), "grad")
+        return self.get_factor(G), lag.value
+
+    def line_search(self, rho):
+        tau, rn = C.c_double(), C.c_int()
+        self._check(self.lib.lrs_op_line_search(self.ctx, rho, C.byref(tau), C.byref(rn)), "line_search")
+        return tau.value, rn.value
+
+    def lbfgs(self, node_num, beta_new, beta_old):
+        self._check(self.lib.lrs_op_lbfgs(self.ctx, node_num, beta_new, beta_old), "lbfgs")
+        return self.get_factor(D)
+
+    def admm_half(self, rho, cg_tol, cg_maxit=800):
+        it = C.c_int()
+        rhs = np.empty(self.dims[0] * self.ranks[0])
+        self._check(self.lib.lrs_op_admm_half(self.ctx, rho, cg_tol, cg_maxit, C.byref(it), _dptr(rhs)), "admm_half")
+        return self.get_factor(U), rhs, it.value
+
+    def gram(self, cone=0, which=R):
+        r = self.ranks[cone]
+        g = np.empty(r * r)
+        self._check(self.lib.lrs_op_gram(self.ctx, cone, which, _dptr(g)), "gram")
+        return g.reshape(r, r)
+
+    # ---- solves
+    def solve(self, **kw):
+        p = default_params(**kw)
+        res = Result()
+        self._check(self.lib.lrs_solve(self.ctx, C.byref(p), C.byref(res)), "solve")
+        return res.as_dict()
+
+    def trajectory(self, phase):
+        n = self.lib.lrs_trajectory(self.ctx, phase, None, None, 0)
+        cur, orc = (C.c_int * max(n, 1))(), (C.c_int * max(n, 1))()
+        self.lib.lrs_trajectory(self.ctx, phase, cur, orc, n)
+        return list(cur)[:n], list(orc)[:n]
+
+    def alm_throughput(self, warmup, steps, **kw):
+        p = default_params(**kw)
+        sec, kms, ims = C.c_double(), C.c_double(), C.c_double()
+        done = C.c_long()
+        self._check(self.lib.lrs_alm_throughput(self.ctx, C.byref(p), warmup, steps, C.byref(sec), C.byref(done),
+                                                C.byref(kms), C.byref(ims)), "alm_throughput")
+        return {"seconds": sec.value, "done": done.value, "auut_ms": kms.value, "iter_ms": ims.value}
+
+    def time_auut(self, reps=100):
+        ms = C.c_double()
+        self._check(self.lib.lrs_time_auut(self.ctx, reps, C.byref(ms)), "time_auut")
+        return ms.value
+
+
+def run_lorads(instance_path, json_output_path, params, fixed_rank=None, rank_schedule_path=None,
+               near_stall_factor=0.7, timeout=3600, device=0):
+    """Same contract as benchmark.py:219-285, on the MI355X binary."""
+    if not BIN_PATH.exists():
+        raise RuntimeError(f"binary not built: {BIN_PATH}")
+    json_output_path = Path(json_output_path)
+    json_output_path.parent.mkdir(parents=True, exist_ok=True)
+    cmd = [str(BIN_PATH), str(instance_path)]
+    for k, v in params.items():
+        cmd += [f"--{k}", str(v)]
+    cmd += ["--jsonfile", str(json_output_path), "--disableOracle", "--device", str(device)]
+    if fixed_rank is not None and rank_schedule_path is not None:
+        raise ValueError("fixed_rank and rank_schedule_path are mutually exclusive")
+    if rank_schedule_path is not None:
+        cmd += ["--rankSchedule", str(rank_schedule_path), "--nearStallFactor", str(near_stall_factor)]
+    elif fixed_rank is not None:
+        cmd += ["--fixedRank", str(fixed_rank)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0 or not json_output_path.exists():
+        return False, None, None
+    with open(json_output_path) as f:
+        m = json.load(f)["metrics"]
+    return True, m.get("solve_time_sec"), m.get("primal_obj")

@@ -1008,6 +1008,9 @@ ALG_START:
             st->pinfinf = st->pinf1 * (1 + s->bNrm1) / (1 + s->bNrmInf);
             if (st->gap <= prm->phase1Tol * 1e-3 && st->pinf1 <= prm->phase1Tol * 1e-3) goto PRINT_AND_EXIT;
             record_state(s, 1);
+            if (getenv("ORACLE_VERBOSE"))
+                printf("ALM OuterIter:%ld InnerIter:%ld pObj:%.10e dObj:%.10e pInfea(1):%.6e rho:%g rank:%d\n",
+                       st->outerIter, st->innerIter, st->pobj, st->dobj, st->pinf1, st->rho, s->rank[0]);
             if (o_now() - timeSolveStart >= prm->timeSecLimit) goto PRINT_AND_EXIT;
         }
         if (rank_flag >= rank_flag_thres && !is_rank_max) {
@@ -1381,6 +1384,7 @@ int oracle_kernels(oproblem *p, int rank, const double *in, double *out) {
     lbfgs_use_grad(s);
     memcpy(op, s->U, 8 * NR); op += NR;
     lbfgs_direction(s, 1);
+    lbfgs_use_grad(s);
     memcpy(op, s->U, 8 * NR); op += NR;
     /* (6) */
     memcpy(s->U, U, 8 * NR); memcpy(s->V, V, 8 * NR);

@@ -174,6 +174,10 @@ static int mode_solve(int argc, char **argv) {
         }
     }
 END:;
+    /* main.c:519-525 (the dual-infeasibility value itself needs ARPACK and is not computed) */
+    c.admm.primal_dual_gap = S->dimacError[LORADS_DIMAC_ERROR_PDGAP];
+    c.admm.l_1_primal_infeasibility = S->dimacError[LORADS_DIMAC_ERROR_CONSTRVIO_L1];
+    c.admm.l_inf_primal_infeasibility = S->dimacError[LORADS_DIMAC_ERROR_CONSTRVIO_L1] * (1 + S->bRHSNrm1) / (1 + S->bRHSNrmInf);
     lorads_int orank = lorads_compute_oracle_rank(S, 2);
     if (orank < 0) orank = 0;
     lorads_write_json_output(S, orank, c.admm.primal_objective_value, c.admm.dual_objective_value,
@@ -302,6 +306,7 @@ static int mode_kernels(int argc, char **argv) {
         LBFGSDirectionUseGrad(S, S->var->uLp, S->var->gradLp, S->var->U, S->var->Grad);
         DUMPF(S->var->U);
         LBFGSDirection(&p, S, head, S->var->gradLp, S->var->uLp, S->var->Grad, S->var->U, 1);
+        LBFGSDirectionUseGrad(S, S->var->uLp, S->var->gradLp, S->var->U, S->var->Grad);
         DUMPF(S->var->U);
     }
     /* (6) one ADMM half-step: solve for U with V fixed (LORADSUpdateSDPVarOne,

@@ -1,0 +1,87 @@
+"""Helpers shared by the parity tests: golden fixtures written by the reference
+itself (scripts/make_golden.py) and the oracle call wrappers."""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+KERNEL_CASES = ["mc_rand200", "mc_torus12x10", "mc_rand300w", "theta40", "theta25x3", "rsparse60"]
+
+
+def instance(name):
+    return os.path.join(GOLDEN, "instances", f"{name}.dat-s")
+
+
+def load_kernels(name):
+    z = np.load(os.path.join(GOLDEN, f"kernels_{name}.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def load_solves():
+    with open(os.path.join(GOLDEN, "solves.json")) as f:
+        return json.load(f)
+
+
+def split_inputs(g):
+    m = int(g["m"])
+    dims = [int(d) for d in g["dims"]]
+    rank = int(g["rank"])
+    NR = sum(n * rank for n in dims)
+    v = g["inputs"]
+    names = ["R", "D", "G", "s1", "y1", "s2", "y2", "U", "V"]
+    out = {nm: v[i * NR:(i + 1) * NR] for i, nm in enumerate(names)}
+    out["lam"] = v[9 * NR:9 * NR + m]
+    out["cvs"] = v[9 * NR + m:9 * NR + 2 * m]
+    tail = v[9 * NR + 2 * m:]
+    out.update(rho=tail[0], beta1=tail[1], beta2=tail[2], rho_admm=tail[3], cg_tol=tail[4])
+    out.update(m=m, dims=dims, rank=rank, NR=NR)
+    return out
+
+
+def split_outputs(out, m, NR, n0r0):
+    o, p = {}, 0
+
+    def take(k):
+        nonlocal p
+        v = out[p:p + k]
+        p += k
+        return v
+    o["q1"] = take(m); o["p1"] = take(1)[0]; o["q2"] = take(m); o["p2"] = take(1)[0]
+    o["cvs_rr"] = take(m); o["pinf_rr"] = take(1)[0]; o["pobj_rr"] = take(1)[0]
+    o["grad"] = take(NR); o["lag"] = take(1)[0]
+    o["tau"] = take(1)[0]; o["rootnum"] = take(1)[0]
+    o["d_lbfgs2"] = take(NR); o["d_lbfgs1"] = take(NR)
+    o["u_cg"] = take(NR); o["rhs_cg"] = take(n0r0); o["cg_iters"] = take(1)[0]
+    return o
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=float)
+    b = np.asarray(b, dtype=float)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def oracle_kernels(lib, name):
+    g = load_kernels(name)
+    s = split_inputs(g)
+    p = lib.oracle_read(instance(name).encode())
+    assert p, "oracle_read failed"
+    inp = np.ascontiguousarray(g["inputs"], dtype=np.float64)
+    out = np.zeros(inp.size * 2 + 1024)
+    n = lib.oracle_kernels(p, s["rank"], inp.ctypes.data_as(C.POINTER(C.c_double)),
+                           out.ctypes.data_as(C.POINTER(C.c_double)))
+    lib.oracle_free(p)
+    return g, split_outputs(out[:n], s["m"], s["NR"], s["dims"][0] * s["rank"])
+
+
+def oracle_solve(lib, name, flags):
+    arr = (C.c_char_p * len(flags))(*[f.encode() for f in flags])
+    res = (C.c_double * 16)()
+    rc = lib.oracle_solve(instance(name).encode(), len(flags), arr, res)
+    assert rc == 0
+    keys = ["alm_inner", "alm_outer", "alm_pobj", "alm_dobj", "alm_pinf", "alm_gap", "alm_rho", "admm_iter",
+            "admm_pobj", "admm_dobj", "admm_pinf", "admm_gap", "admm_rho", "solve_time", "rank", "alm_time"]
+    return dict(zip(keys, list(res)))
