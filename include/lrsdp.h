@@ -128,6 +128,18 @@ int lrs_set_log_path(lrs_ctx *ctx, const char *path);
 /* Standalone A(UU^T) (SDDMM + gather) timing on R: reps launches, average ms per launch. */
 int lrs_time_auut(lrs_ctx *ctx, int reps, double *avg_ms);
 
+/* Per-stage timing of the split ALM inner iteration: runs `steps` inner iterations at
+ * the current rank like lrs_alm_throughput, with HIP events on the solver stream
+ * around each of the four launches (S1 direction+SDDMM, S2 q-gather, S3 update+
+ * adjoint, S4 gradient).  stage_ms[4] = average ms per launch; *done = iterations. */
+int lrs_profile_stages(lrs_ctx *ctx, const lrs_params *p, long steps, double *stage_ms, long *done);
+
+/* Diagnostics: in-kernel phase timestamps of the last split iteration (block 0,
+ * 100 MHz wall clock), out[4][16], and (blk, optional) per-block entry/exit stamps
+ * blk[4][1024][2].  Returns 64 from the diagnostics build (liblrsdp_timing.so), 0
+ * from the product build. */
+int lrs_debug_phase_times(lrs_ctx *ctx, unsigned long long *out, unsigned long long *blk);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,6 +26,7 @@ namespace lrs {
 constexpr int kBlock = 256;          // threads per block (4 waves)
 constexpr int kMaxPartialBlocks = 1024;
 constexpr int kMaxPartialVals = 16;
+constexpr int kIterMaxBlocks = 512;   // row-kernel grid cap of the split iteration
 
 // ---- ALM inner-loop control block (double array, double-buffered by iteration parity)
 enum CtrlIdx {
@@ -49,6 +50,10 @@ enum CtrlIdx {
     C_LASTTAU,
     // dots of the current gradient with the ring (stash, valid when PENDING == 2)
     C_DSG, C_DYG, C_DSOG, C_DYOG, C_DSOY, C_DYOY,
+    // written by the gather stage of the split iteration (authoritative after it ran)
+    C_ACT2,         // ACTIVE after the phase-1 (l_inf pinf) test of the completed iteration
+    C_EXIT2,        // exit reason after that test
+    C_RRDONE,       // 1 if this iteration's first stage refreshed A(RR^T) and the residual
     C_NCTRL = 40
 };
 enum ExitReason {
@@ -114,6 +119,7 @@ struct DevWork {
     double *lsres = nullptr;   // [2][LS_N]
     double *par = nullptr;     // [P_NPAR]
     double *gram = nullptr;    // gram partials
+    double *rec = nullptr;     // [m][4] per-constraint {A(RR^T), q1, q2, -lam - rho b}
 };
 
 // ---------------------------- launchers -----------------------------------
@@ -152,13 +158,13 @@ int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y,
 struct AlmIterArgs {
     const DevProblem *P;
     DevWork *W;
-    int nblk_grad;     // partial blocks written by grad (sum over cones)
-    int nblk_rr;       // partial blocks written by gather_rr
-    int nblk_sddmm;    // partial blocks written by sddmm
-    int nblk_q;        // partial blocks written by gather_q
+    hipEvent_t *ev;    // optional: 5 events recorded before S1..S4 and after S4
 };
+// Four launches per inner iteration (lrs_kernels.hip "split iteration").
 int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st);
 
 const char *last_device_error();
+// diagnostics build only: copies g_phase[4][16] (returns 64), else returns 0
+int read_phase_times(unsigned long long *out, unsigned long long *blk);
 
 }  // namespace lrs

@@ -20,12 +20,58 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 
 #include "lrs_device.h"
 
 namespace lrs {
 
 static thread_local char g_err[512] = "";
+
+// Optional in-kernel phase timestamps (block 0, thread 0; s_memrealtime, 100 MHz):
+// built only into the diagnostics library (make timing -> liblrsdp_timing.so).
+__device__ unsigned long long g_phase[4][16];
+__device__ unsigned long long g_phase_tmp[4][16];
+#ifdef LRS_PHASE_TIMING
+#define LRS_TS(k, p)                                                                  \
+    do {                                                                              \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_phase_tmp[k][p] = wall_clock64();  \
+    } while (0)
+// last phase of a kernel that ran its full path: publish the staged stamps
+#define LRS_TS_END(k, p)                                                              \
+    do {                                                                              \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
+            g_phase_tmp[k][p] = wall_clock64();                                       \
+            for (int q_ = 0; q_ <= (p); ++q_) g_phase[k][q_] = g_phase_tmp[k][q_];    \
+        }                                                                             \
+    } while (0)
+// per-block [entry, exit] of the last full run of each split-iteration kernel
+__device__ unsigned long long g_blk[4][1024][2];
+#define LRS_BLK_BEGIN() const unsigned long long t_begin_ = wall_clock64()
+#define LRS_BLK_END(k)                                                                 \
+    do {                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < 1024) {                                   \
+            g_blk[k][blockIdx.x][0] = t_begin_;                                        \
+            g_blk[k][blockIdx.x][1] = wall_clock64();                                  \
+        }                                                                              \
+    } while (0)
+#else
+#define LRS_TS(k, p) do { } while (0)
+#define LRS_TS_END(k, p) do { } while (0)
+#define LRS_BLK_BEGIN() do { } while (0)
+#define LRS_BLK_END(k) do { } while (0)
+#endif
+int read_phase_times(unsigned long long *out, unsigned long long *blk) {
+#ifdef LRS_PHASE_TIMING
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase)) != hipSuccess) return -1;
+    if (blk && hipMemcpyFromSymbol(blk, HIP_SYMBOL(g_blk), sizeof(g_blk)) != hipSuccess) return -1;
+    return 64;
+#else
+    (void)out;
+    (void)blk;
+    return 0;
+#endif
+}
 const char *last_device_error() { return g_err; }
 
 #define LRS_CHECK_LAUNCH()                                                               \
@@ -53,17 +99,42 @@ Layout choose_layout(int r) {
 // ------------------------------------------------------------------------
 // small device helpers
 // ------------------------------------------------------------------------
+// DPP lane moves on the two 32-bit halves of a double (no LDS round trip, unlike
+// __shfl_xor's ds_bpermute).  CTRL: 0xB1 quad_perm[1,0,3,2] (xor 1), 0x4E
+// quad_perm[2,3,0,1] (xor 2), 0x141 row_half_mirror (i <-> 7-i in 8 lanes),
+// 0x140 row_mirror (i <-> 15-i in 16 lanes).
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Sum over an aligned group of G lanes; every lane of the group gets the same value.
 template <int G>
 __device__ __forceinline__ double group_sum(double v) {
-#pragma unroll
-    for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    v += dpp_mov<0xB1>(v);
+    v += dpp_mov<0x4E>(v);
+    if constexpr (G >= 8) v += dpp_mov<0x141>(v);
+    if constexpr (G >= 16) v += dpp_mov<0x140>(v);
+    if constexpr (G >= 32) v += __shfl_xor(v, 16, 64);
+    if constexpr (G >= 64) v += __shfl_xor(v, 32, 64);
     return v;
 }
 
+__device__ __forceinline__ double read_lane(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Wave (64-lane) sum, wave-uniform result: DPP within rows of 16, then the four
+// row sums through readlane.
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v = group_sum<16>(v);
+    return (read_lane(v, 0) + read_lane(v, 16)) + (read_lane(v, 32) + read_lane(v, 48));
 }
 
 template <int E>
@@ -95,9 +166,9 @@ __device__ __forceinline__ void st_row(double *__restrict__ p, const double (&v)
 }
 
 // Block-reduce NV per-thread accumulators; thread 0 gets the block sums in s[].
-template <int NV>
+template <int NV, int NT = kBlock>
 __device__ __forceinline__ void block_reduce(double (&acc)[NV], double (&s)[NV]) {
-    __shared__ double sh[NV][kBlock / 64];
+    __shared__ double sh[NV][NT / 64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -110,7 +181,7 @@ __device__ __forceinline__ void block_reduce(double (&acc)[NV], double (&s)[NV])
         for (int v = 0; v < NV; ++v) {
             double t = 0.0;
 #pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) t += sh[v][w];
+            for (int w = 0; w < NT / 64; ++w) t += sh[v][w];
             s[v] = t;
         }
     }
@@ -593,25 +664,153 @@ __device__ int dev_cubic(double a, double b, double c, double d, double *res) {
     return 0;
 }
 
+// Same as dev_cubic, executed by a whole wave (uniform result): the two independent
+// cube roots of the delta > 0 branch run on lanes 0 and 1 at once.
+__device__ int dev_cubic_wave(double a, double b, double c, double d, double *res) {
+    const double A = b * b - 3 * a * c, B = b * c - 9 * a * d, C = c * c - 3 * b * d;
+    const double delta = B * B - 4 * A * C;
+    res[0] = res[1] = res[2] = 0.0;
+    if (A == 0 && B == 0) { res[0] = fmax(res[0], -c / b); return 1; }
+    if (delta > 0) {
+        const double sq = sqrt(delta);
+        const double Y1 = A * b + 1.5 * a * (-B + sq);
+        const double Y2 = A * b + 1.5 * a * (-B - sq);
+        const double y = (threadIdx.x & 1) ? Y2 : Y1;
+        const double ay = y > 0 ? y : -y;
+        double r = pow(ay, 1.0 / 3);
+        r = y > 0 ? r : -r;
+        const double Y13 = read_lane(r, 0), Y23 = read_lane(r, 1);
+        res[0] = fmax(res[0], (-b - Y13 - Y23) / 3 / a);
+        return 1;
+    }
+    if (delta == 0 && A != 0 && B != 0) {
+        const double Kk = B / A;
+        res[0] = -b / a + Kk; res[1] = -Kk / 2;
+        return 2;
+    }
+    if (delta < 0) {
+        const double sqA = sqrt(A);
+        const double T = (A * b - 1.5 * a * B) / (A * sqA);
+        const double th = acos(T);
+        double sn, cs;
+        sincos(th / 3, &sn, &cs);
+        sn *= sqrt(3.0);
+        res[0] = (-b - 2 * sqA * cs) / 3 / a;
+        res[1] = (-b + sqA * (cs + sn)) / 3 / a;
+        res[2] = (-b + sqA * (cs - sn)) / 3 / a;
+        return 3;
+    }
+    return 0;
+}
+
 __device__ __forceinline__ double quartic(double a, double b, double c, double d, double x) {
     const double x2 = x * x;
     return a * (x2 * x2) + b * (x2 * x) + c * x2 + d * x;
 }
 
 // ALMLineSearch (lorads_alm.c:266-333) from the finals; writes ls[0..2]
+__device__ void line_search_v(const double *__restrict__ par, double p1, double p2, const double *dots, double *ls);
 __device__ void line_search(const double *__restrict__ par, int K, double *ls) {
     double p1 = 0.0, p2 = 0.0;
     for (int k = 0; k < K; ++k) { p1 += g_fin[FIN_SD + 2 * k]; p2 += g_fin[FIN_SD + 2 * k + 1]; }
+    double dots[5];
+    for (int q = 0; q < 5; ++q) dots[q] = g_fin[FIN_Q + q];
+    line_search_v(par, p1, p2, dots, ls);
+}
+// ------------------------------------------------------------------------
+// Split ALM inner iteration: FOUR launches per iteration (lorads_alm.c:1302-1379).
+//   S1 k_it_dir_sddmm<G,E> control (folds the previous iteration's dots), the
+//                          A(RR^T) refresh + residual of the previous iteration
+//                          (primalInfeasibility, lorads_alg_common.c:386-394), the
+//                          L-BFGS direction D = -H G (rows recomputed for the
+//                          neighbours instead of a launch boundary) and sym(RD^T),
+//                          DD^T on the pattern with the objective partials
+//   S2 k_it_q              phase-1 test on the residual (lorads_alm.c:1359-1364),
+//                          q1 = 2A(sym RD^T), q2 = A(DD^T), five line-search dots
+//   S3 k_it_update         line search, R += tau D, S = C + A^*(M1) with M1 formed
+//                          per constraint on the fly (ALMSetGrad, lorads_alm.c:38-57)
+//   S4 k_it_grad<G,E>      G = 2 S R, A(RR^T) slots, L-BFGS pair, nine dots
+// Cross-block sums: every producer block writes its partials; EVERY block of the
+// consuming launch reduces them in the same fixed order.  No in-launch hand-off, no
+// fences; the launch boundary is the only synchronisation.  Bitwise reproducible.
+// ------------------------------------------------------------------------
+template <int NV, int NT = kBlock>
+__device__ __forceinline__ void write_partials(double (&acc)[NV], double *__restrict__ part, int slot) {
+    double s[NV];
+    block_reduce<NV, NT>(acc, s);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) part[v * kMaxPartialBlocks + slot] = s[v];
+    }
+}
+
+// Partial loads of the consumer side, split from the reduction so that they are
+// issued together with other independent loads (every thread: kMaxPartialBlocks/NT
+// loads per value, all in flight at once).  Summation order = reduce_partials'.
+template <int NV, int NT>
+struct PartialLoad {
+    static constexpr int NL = kMaxPartialBlocks / NT;
+    double a[NV];
+    __device__ __forceinline__ void load(const double *__restrict__ part, int nblk) {
+        double x[NV][NL];
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+                const int b = threadIdx.x + l * NT;
+                x[v][l] = b < nblk ? part[v * kMaxPartialBlocks + b] : 0.0;
+            }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            double t = 0.0;
+#pragma unroll
+            for (int l = 0; l < NL; ++l) t += x[v][l];
+            a[v] = t;
+        }
+    }
+    // all threads; out (shared) receives the NV sums, visible to the block on return
+    __device__ __forceinline__ void reduce(double *out) {
+        double s[NV];
+        block_reduce<NV, NT>(a, s);
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) out[v] = s[v];
+        }
+        __syncthreads();
+    }
+};
+
+// all threads; generic nblk
+template <int NV, int NT = kBlock>
+__device__ __forceinline__ void reduce_partials(const double *__restrict__ part, int nblk, double *out) {
+    double a[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) a[v] = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += NT) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) a[v] += part[v * kMaxPartialBlocks + b];
+    }
+    double s[NV];
+    block_reduce<NV, NT>(a, s);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) out[v] = s[v];
+    }
+    __syncthreads();
+}
+
+// ALMLineSearch (lorads_alm.c:266-333) from reduced values: p1, p2 objective parts
+// (p1 before its factor 2), dots = {q2q2, q1q2, q0q2, q1q1, q0q1}.
+template <bool WAVE>
+__device__ void line_search_t(const double *__restrict__ par, double p1, double p2, const double *dots, double *ls) {
     p1 *= 2.0;
     const double rho = par[P_RHO];
-    const double q2q2 = g_fin[FIN_Q + 0], q1q2 = g_fin[FIN_Q + 1], q0q2 = g_fin[FIN_Q + 2];
-    const double q1q1 = g_fin[FIN_Q + 3], q0q1 = g_fin[FIN_Q + 4];
-    const double a = rho * q2q2 / 2;
-    const double b = rho * q1q2;
-    const double c = p2 - rho * q0q2 + rho * q1q1 / 2;
-    const double d = p1 - rho * q0q1;
+    const double a = rho * dots[0] / 2;
+    const double b = rho * dots[1];
+    const double c = p2 - rho * dots[2] + rho * dots[3] / 2;
+    const double d = p1 - rho * dots[4];
     double roots[3];
-    const int rn = dev_cubic(4 * a, 3 * b, 2 * c, d, roots);
+    const int rn = WAVE ? dev_cubic_wave(4 * a, 3 * b, 2 * c, d, roots) : dev_cubic(4 * a, 3 * b, 2 * c, d, roots);
     double tau = 0.0;
     const double f0 = 0.0, f1 = quartic(a, b, c, d, 1.0);
     double fr1 = 1e30, fr2 = 1e30, fr3 = 1e30;
@@ -624,54 +823,417 @@ __device__ void line_search(const double *__restrict__ par, int K, double *ls) {
     if (fabs(mn - fr1) < 1e-10) tau = roots[0];
     if (fabs(mn - fr2) < 1e-10) tau = roots[1];
     if (fabs(mn - fr3) < 1e-10) tau = roots[2];
-    ls[LS_TAU] = tau;
-    ls[LS_ROOTNUM] = rn;
-    ls[LS_FLAG] = rn == 0 ? 1.0 : (fabs(tau) < par[P_ENDTAU] ? 2.0 : 0.0);
+    if (!WAVE || threadIdx.x == 0) {
+        ls[LS_TAU] = tau;
+        ls[LS_ROOTNUM] = rn;
+        ls[LS_FLAG] = rn == 0 ? 1.0 : (fabs(tau) < par[P_ENDTAU] ? 2.0 : 0.0);
+    }
+}
+__device__ void line_search_v(const double *__restrict__ par, double p1, double p2, const double *dots, double *ls) {
+    line_search_t<false>(par, p1, p2, dots, ls);
 }
 
-// R += tau D ; cvs += tau q1 + tau^2 q2 ; M1 = -lam - rho b + rho cvs
-// (ALMupdateVar lorads_alm.c:826-830, :1351-1353, ALMSetGrad :45-49)
-__global__ void __launch_bounds__(kBlock) k_alm_update(long NR, int m, int K, const double *__restrict__ par,
-                                                       const double *__restrict__ guard, double *__restrict__ lsout,
-                                                       double *__restrict__ R, const double *__restrict__ D,
-                                                       double *__restrict__ cvs, const double *__restrict__ q1,
-                                                       const double *__restrict__ q2, const double *__restrict__ lam,
-                                                       const double *__restrict__ b, double *__restrict__ M1) {
-    if (guard[C_ACTIVE] == 0.0) return;
-    __shared__ double ls[LS_N];
-    if (threadIdx.x == 0) line_search(par, K, ls);
+// Control of one split iteration (thread 0).  c: shared copy of the previous control,
+// updated in place; the arithmetic runs on a register copy (constant indices only).
+// d = the nine dots of the previous gradient stage when `fold`.
+__device__ void ctrl_step(double *csh, const double *__restrict__ par, double lsflag, double lstau, int fold,
+                          const double *d) {
+    double c[C_NCTRL];
+#pragma unroll
+    for (int q = 0; q < C_NCTRL; ++q) c[q] = csh[q];
+    const int L = (int)par[P_L];
+    const double cninf = par[P_CNINF], rctol = par[P_RCTOL], endsub = par[P_ENDSUB], budget = par[P_BUDGET];
+    c[C_ACTIVE] = c[C_ACT2];
+    c[C_EXIT] = c[C_EXIT2];
+    c[C_RRDONE] = 0.0;
+    if (c[C_ACTIVE] != 0.0 && c[C_PENDING] == 1.0) {
+        if (lsflag == 1.0) {                    // rootNum == 0: RET_CODE_NUM_ERR (lorads_alm.c:1327)
+            c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_NUMERR;
+            c[C_PENDING] = 0.0;
+        } else if (lsflag == 2.0) {             // |tau| < endTauTol (lorads_alm.c:1331-1339)
+            c[C_INNER] += 1; c[C_LOCAL] += 1; c[C_CLEAR] += 1;
+            c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_TINYTAU;
+            c[C_PENDING] = 0.0;
+        } else if (fold) {
+            const int h = (int)c[C_HEAD];
+            // setlbfgsHisTwo (lorads_alm.c:861): beta = 1/<y,s>; ring head advances (:862)
+            const double beta = 1.0 / d[1];
+            if (h == 0) { c[C_BETA0] = beta; c[C_YY0] = d[2]; }
+            else { c[C_BETA1] = beta; c[C_YY1] = d[2]; }
+            c[C_HEAD] = (double)((h + 1) % L);
+            c[C_GCUR] = 1.0 - c[C_GCUR];
+            c[C_LAG] = d[0];
+            c[C_LASTTAU] = lstau;
+            c[C_DSG] = d[3]; c[C_DYG] = d[4]; c[C_DSOG] = d[5]; c[C_DYOG] = d[6];
+            c[C_DSOY] = d[7]; c[C_DYOY] = d[8];
+            c[C_PENDING] = 2.0;
+            c[C_RRDONE] = 1.0;
+            // the phase-1 test on the refreshed residual (which takes precedence) runs in S2
+            c[C_RCVAL] = sqrt(c[C_LAG]) / (1.0 + cninf);
+            c[C_INNER] += 1; c[C_LOCAL] += 1; c[C_CLEAR] += 1;
+            if (c[C_LOCAL] > 800) { c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_LOCAL800; }
+        }
+    } else if (c[C_PENDING] == 0.0) {
+        c[C_DSG] = c[C_DYG] = c[C_DSOG] = c[C_DYOG] = c[C_DSOY] = c[C_DYOY] = 0.0;
+    }
+    if (c[C_ACTIVE] != 0.0) {
+        if (!(c[C_RCVAL] - rctol > endsub)) { c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_CONVERGED; }
+        else if (budget > 0 && c[C_INNER] >= budget) { c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_BUDGET; }
+    }
+    if (c[C_ACTIVE] != 0.0) {
+        // LBFGSDirection (lorads_alm.c:468-505) in coefficient space
+        if (((long)c[C_LOCAL]) % 300 == 0) c[C_CLEAR] = 0;
+        const int clear = (int)c[C_CLEAR];
+        const int nodeNum = clear == 0 ? 0 : (clear <= L - 1 ? clear : L);
+        c[C_NODENUM] = nodeNum;
+        const double GG = c[C_LAG];
+        const double sG = c[C_DSG], yG = c[C_DYG], soG = c[C_DSOG], yoG = c[C_DYOG], soy = c[C_DSOY],
+                     yoy = c[C_DYOY];
+        const int hn = ((int)c[C_HEAD] - 1 + L) % L;     // newest slot
+        double cs0 = 0, cs1 = 0, cy0 = 0, cy1 = 0;
+        double dg;
+        if (nodeNum == 0) {
+            dg = -GG;
+        } else if (nodeNum == 1) {
+            const double bn = hn ? c[C_BETA1] : c[C_BETA0], yyn = hn ? c[C_YY1] : c[C_YY0];
+            const double a1 = bn * sG;
+            const double w1 = a1 - bn * (yG - a1 * yyn);
+            if (hn) { cy1 += -a1; cs1 += w1; } else { cy0 += -a1; cs0 += w1; }
+            dg = -(GG - a1 * yG + w1 * sG);
+        } else {
+            // L == 2: the older slot is the other one
+            const double bn = hn ? c[C_BETA1] : c[C_BETA0], yyn = hn ? c[C_YY1] : c[C_YY0];
+            const double bo = hn ? c[C_BETA0] : c[C_BETA1], yyo = hn ? c[C_YY0] : c[C_YY1];
+            const double a1 = bn * sG;
+            const double a2 = bo * (soG - a1 * soy);
+            const double w2 = a2 - bo * (yoG - a1 * yoy - a2 * yyo);
+            const double w1 = a1 - bn * (yG - a1 * yyn - a2 * yoy + w2 * soy);
+            if (hn) { cy1 += -a1; cy0 += -a2; cs0 += w2; cs1 += w1; }
+            else { cy0 += -a1; cy1 += -a2; cs1 += w2; cs0 += w1; }
+            dg = -(GG - a1 * yG - a2 * yoG + w2 * soG + w1 * sG);
+        }
+        c[C_CG] = 1.0;
+        c[C_CS0] = cs0; c[C_CY0] = cy0; c[C_CS1] = cs1; c[C_CY1] = cy1;
+        // LBFGSDirectionUseGrad (lorads_alm.c:618-626)
+        if (dg >= 0) { c[C_CS0] = c[C_CY0] = c[C_CS1] = c[C_CY1] = 0.0; dg = -GG; }
+        c[C_DG] = dg;
+        c[C_PENDING] = 1.0;
+    }
+#pragma unroll
+    for (int q = 0; q < C_NCTRL; ++q) csh[q] = c[q];
+}
+
+struct DirCoef {
+    double cg, cs0, cy0, cs1, cy1;
+    bool u0, u1;
+};
+
+// one row of D = -(cg G + cs0 s0 + cy0 y0 + cs1 s1 + cy1 y1), same arithmetic as k_alm_dir;
+// the operand rows are loaded by dir_load so that the loads can run ahead.
+template <int E>
+struct DirRow {
+    double g[E], a0[E], b0[E], a1[E], b1[E];
+    __device__ __forceinline__ void load(const DirCoef &k, const double *__restrict__ Gc,
+                                         const double *__restrict__ s0, const double *__restrict__ y0,
+                                         const double *__restrict__ s1, const double *__restrict__ y1, long off) {
+        ld_row<E>(Gc + off, g);
+        if (k.u0) { ld_row<E>(s0 + off, a0); ld_row<E>(y0 + off, b0); }
+        if (k.u1) { ld_row<E>(s1 + off, a1); ld_row<E>(y1 + off, b1); }
+    }
+    __device__ __forceinline__ void eval(const DirCoef &k, double (&d)[E]) const {
+#pragma unroll
+        for (int e = 0; e < E; ++e) d[e] = k.cg * g[e];
+        if (k.u0) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) d[e] += k.cs0 * a0[e] + k.cy0 * b0[e];
+        }
+        if (k.u1) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) d[e] += k.cs1 * a1[e] + k.cy1 * b1[e];
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) d[e] = -d[e];
+    }
+};
+
+constexpr int kRowBlock = 512;   // threads per block of the row kernels S1 / S4
+
+// S1.  Partials written (3): objective part of <C, sym RD^T>, of <C, DD^T>, residual.
+template <int G, int E>
+__global__ void __launch_bounds__(kRowBlock) k_it_dir_sddmm(
+    int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
+    const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
+    const double *__restrict__ Rall, double *__restrict__ Dall, const double *__restrict__ G0,
+    const double *__restrict__ G1, const double *__restrict__ s0a, const double *__restrict__ y0a,
+    const double *__restrict__ s1a, const double *__restrict__ y1a, double *__restrict__ uRD,
+    double *__restrict__ uDD, int do_rr, int m, int K, const int *__restrict__ con_ptr,
+    const int *__restrict__ con_slot, const double *__restrict__ con_w, const double *__restrict__ uRR,
+    const double *__restrict__ b, double *__restrict__ cvs, const double *__restrict__ par,
+    const double *__restrict__ ctrl_prev, double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev,
+    const double *__restrict__ partG, int nblkG, double *__restrict__ partA, int pblk_off) {
+    __shared__ double c[C_NCTRL];
+    __shared__ double red[9];
+    __shared__ double lsv[2];
+    LRS_TS(0, 0);
+    LRS_BLK_BEGIN();
+    // control words, ls result and the gradient-stage partials load together
+    if (threadIdx.x < C_NCTRL) c[threadIdx.x] = ctrl_prev[threadIdx.x];
+    if (threadIdx.x == 0) { lsv[0] = ls_prev[LS_FLAG]; lsv[1] = ls_prev[LS_TAU]; }
     __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x < LS_N) lsout[threadIdx.x] = ls[threadIdx.x];
+    LRS_TS(0, 1);
+    const int fold = (c[C_ACT2] != 0.0 && c[C_PENDING] == 1.0 && lsv[0] == 0.0) ? 1 : 0;
+    if (fold) reduce_partials<9, kRowBlock>(partG, nblkG, red);
+    else __syncthreads();   // every wave has read c[] before thread 0 rewrites it
+    LRS_TS(0, 2);
+    if (threadIdx.x == 0) ctrl_step(c, par, lsv[0], lsv[1], fold, red);
+    double acc[3] = {0.0, 0.0, 0.0};
+    if (fold && do_rr) {
+        // cvs = A(RR^T) from scratch, residual ||b - cvs||^2 (primalInfeasibility);
+        // independent of this iteration's control, so it runs beside ctrl_step
+        for (int i = blockIdx.x * kRowBlock + threadIdx.x; i < m; i += gridDim.x * kRowBlock) {
+            double tot = 0.0;
+            for (int k = 0; k < K; ++k) {
+                const long row = (long)k * m + i;
+                double v = 0.0;
+                for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) v += con_w[e] * uRR[con_slot[e]];
+                tot += v;
+            }
+            cvs[i] = tot;
+            const double dd = b[i] - tot;
+            acc[2] += dd * dd;
+        }
+    }
+    __syncthreads();
+    LRS_TS(0, 3);
+    if (do_rr && blockIdx.x == 0 && threadIdx.x < C_NCTRL) ctrl_cur[threadIdx.x] = c[threadIdx.x];
+    const bool active = c[C_ACTIVE] != 0.0;
+    if (!fold && !active) return;
+    LRS_TS(0, 4);
+    if (active) {
+        DirCoef kc;
+        kc.cg = c[C_CG]; kc.cs0 = c[C_CS0]; kc.cy0 = c[C_CY0]; kc.cs1 = c[C_CS1]; kc.cy1 = c[C_CY1];
+        kc.u0 = (kc.cs0 != 0.0 || kc.cy0 != 0.0);
+        kc.u1 = (kc.cs1 != 0.0 || kc.cy1 != 0.0);
+        const double *__restrict__ R = Rall + foff;
+        double *__restrict__ D = Dall + foff;
+        const double *__restrict__ Gc = (c[C_GCUR] == 0.0 ? G0 : G1) + foff;
+        const double *__restrict__ s0 = s0a + foff, *__restrict__ y0 = y0a + foff;
+        const double *__restrict__ s1 = s1a + foff, *__restrict__ y1 = y1a + foff;
+        const int lane = threadIdx.x & (G - 1);
+        const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
+        const int ngrp = gridDim.x * kRowBlock / G;
+        for (int i = grp; i < n; i += ngrp) {
+            const long oi = (long)i * ld + lane * E;
+            const int kb = adj_ptr[i], ke = adj_low[i];
+            double xi[E], yi[E];
+            ld_row<E>(R + oi, xi);
+            {
+                DirRow<E> dr;
+                dr.load(kc, Gc, s0, y0, s1, y1, oi);
+                dr.eval(kc, yi);
+            }
+            st_row<E>(D + oi, yi);
+            // lower entries two at a time: both neighbours' operand loads in flight together
+            for (int k0 = kb; k0 < ke; k0 += 2) {
+                const int kA = k0, kB = min(k0 + 1, ke - 1);
+                const int jA = adj_col[kA], jB = adj_col[kB];
+                const int sA = adj_slot[kA], sB = adj_slot[kB];
+                const long oA = (long)jA * ld + lane * E, oB = (long)jB * ld + lane * E;
+                double xA[E], xB[E];
+                DirRow<E> dA, dB;
+                ld_row<E>(R + oA, xA);
+                ld_row<E>(R + oB, xB);
+                dA.load(kc, Gc, s0, y0, s1, y1, oA);
+                dB.load(kc, Gc, s0, y0, s1, y1, oB);
+                const double cwA = Cw[sA], cwB = Cw[sB];
+                double yA[E], yB[E];
+                dA.eval(kc, yA);
+                dB.eval(kc, yB);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int j = u ? jB : jA;
+                    const double(&xj)[E] = u ? xB : xA;
+                    const double(&yj)[E] = u ? yB : yA;
+                    double d0 = 0.0, d1 = 0.0;
+                    if (j != i) {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) d0 += xi[e] * yj[e] + xj[e] * yi[e];
+                        d0 *= 0.5;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) d0 += xi[e] * yi[e];
+                    }
+#pragma unroll
+                    for (int e = 0; e < E; ++e) d1 += yi[e] * yj[e];
+                    d0 = group_sum<G>(d0);
+                    d1 = group_sum<G>(d1);
+                    if (lane == 0 && (u == 0 || k0 + 1 < ke)) {
+                        const int sl = u ? sB : sA;
+                        const double cw = u ? cwB : cwA;
+                        uRD[sl] = d0;
+                        uDD[sl] = d1;
+                        acc[0] += cw * d0;
+                        acc[1] += cw * d1;
+                    }
+                }
+            }
+        }
+    }
+    LRS_TS(0, 5);
+    write_partials<3, kRowBlock>(acc, partA, pblk_off + blockIdx.x);
+    LRS_TS_END(0, 6);
+    LRS_BLK_END(0);
+}
+
+// S2.  Partials written (5): q2q2, q1q2, q0q2, q1q1, q0q1.  rec[i] = {A(RR^T)_i, q1_i,
+// q2_i, -lam_i - rho b_i} feeds S3's on-the-fly M1.
+__global__ void __launch_bounds__(kBlock) k_it_q(int m, int K, const int *__restrict__ con_ptr,
+                                                 const int *__restrict__ con_slot, const double *__restrict__ con_w,
+                                                 const double *__restrict__ uRD, const double *__restrict__ uDD,
+                                                 const double *__restrict__ b, const double *__restrict__ cvs,
+                                                 const double *__restrict__ lam, const double *__restrict__ par,
+                                                 double *__restrict__ ctrl_cur, const double *__restrict__ partA,
+                                                 int nblkA, double *__restrict__ rec, double *__restrict__ partB) {
+    __shared__ double cs[3];
+    __shared__ double red[1];
+    LRS_TS(1, 0);
+    LRS_BLK_BEGIN();
+    if (threadIdx.x == 0) { cs[0] = ctrl_cur[C_ACTIVE]; cs[1] = ctrl_cur[C_EXIT]; cs[2] = ctrl_cur[C_RRDONE]; }
+    PartialLoad<1, kBlock> pl;
+    pl.load(partA + 2 * kMaxPartialBlocks, nblkA);
+    // this thread's first constraint: loads independent of the control decision
+    const int i0 = blockIdx.x * kBlock + threadIdx.x;
+    double b0 = 0.0, c0 = 0.0, l0 = 0.0;
+    if (i0 < m) { b0 = b[i0]; c0 = cvs[i0]; l0 = lam[i0]; }
+    __syncthreads();
+    bool act = cs[0] != 0.0;
+    double ex = cs[1];
+    if (cs[2] != 0.0) {
+        pl.reduce(red);
+        // primalInfeasibility (lorads_alg_common.c:393) and l_inf (lorads_alm.c:1359)
+        const double pinf1 = sqrt(red[0]) / (1.0 + par[P_BN1]);
+        const double pinfinf = pinf1 * (1.0 + par[P_BN1]) / (1.0 + par[P_BNINF]);
+        if ((pinfinf <= par[P_PH1TOL]) && ((par[P_GAP] <= par[P_PH1TOL]) || (par[P_HIGHACC] == 0.0))) {
+            act = false;
+            ex = EXIT_PHASE1;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) { ctrl_cur[C_PINF1] = pinf1; ctrl_cur[C_PINFINF] = pinfinf; }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) { ctrl_cur[C_ACT2] = act ? 1.0 : 0.0; ctrl_cur[C_EXIT2] = ex; }
+    LRS_TS(1, 1);
+    if (!act) return;
+    const double rho = par[P_RHO];
+    const double rhoInv = 1.0 / rho;
+    double acc[5] = {0, 0, 0, 0, 0};
+    for (int i = i0; i < m; i += gridDim.x * kBlock) {
+        double v1 = 0.0, v2 = 0.0;
+        for (int k = 0; k < K; ++k) {
+            const long row = (long)k * m + i;
+            double a1 = 0.0, a2 = 0.0;
+            for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) {
+                const double w = con_w[e];
+                const int s = con_slot[e];
+                a1 += w * uRD[s];
+                a2 += w * uDD[s];
+            }
+            v1 += a1; v2 += a2;
+        }
+        v1 *= 2.0;
+        const double bi = i == i0 ? b0 : b[i], ci = i == i0 ? c0 : cvs[i], li = i == i0 ? l0 : lam[i];
+        const double q0 = (bi - ci) + rhoInv * li;
+        acc[0] += v2 * v2; acc[1] += v1 * v2; acc[2] += q0 * v2; acc[3] += v1 * v1; acc[4] += q0 * v1;
+        double2 *r = reinterpret_cast<double2 *>(rec + 4L * i);
+        r[0] = make_double2(ci, v1);
+        r[1] = make_double2(v2, (-li) + (-rho) * bi);
+    }
+    LRS_TS(1, 2);
+    write_partials<5>(acc, partB, blockIdx.x);
+    LRS_TS_END(1, 3);
+    LRS_BLK_END(1);
+}
+
+// S3.  No partials.  ALMupdateVar (lorads_alm.c:826-830), A(RR^T) update (:1351-1353),
+// M1 (ALMSetGrad :45-49) and S = C + A^*(M1) (addObjCoeff + sdpDataWSum).  The
+// first element of each grid-stride loop is loaded before the line search.
+__global__ void __launch_bounds__(kBlock) k_it_update(long NR, int Ptot, const int *__restrict__ slot_ptr,
+                                                      const int *__restrict__ slot_con,
+                                                      const double *__restrict__ slot_a,
+                                                      const double *__restrict__ Craw, const double *__restrict__ rec,
+                                                      double *__restrict__ R, const double *__restrict__ D,
+                                                      const double *__restrict__ par,
+                                                      const double *__restrict__ ctrl_cur,
+                                                      const double *__restrict__ partA, int nblkA,
+                                                      const double *__restrict__ partB, int nblkB,
+                                                      double *__restrict__ ls_cur, double *__restrict__ S) {
+    __shared__ double red[7];
+    __shared__ double ls[LS_N];
+    __shared__ int act;
+    LRS_TS(2, 0);
+    LRS_BLK_BEGIN();
+    if (threadIdx.x == 0) act = ctrl_cur[C_ACT2] != 0.0;
+    // first factor pair and first slot of this thread
+    const long i0 = ((long)blockIdx.x * kBlock + threadIdx.x) * 2;
+    double2 r0 = make_double2(0.0, 0.0), d0 = make_double2(0.0, 0.0);
+    if (i0 < NR) { r0 = *reinterpret_cast<const double2 *>(R + i0); d0 = *reinterpret_cast<const double2 *>(D + i0); }
+    const int s0 = blockIdx.x * kBlock + threadIdx.x;
+    double cr0 = 0.0;
+    int e0 = 0, e1 = 0;
+    if (s0 < Ptot) { cr0 = Craw[s0]; e0 = slot_ptr[s0]; e1 = slot_ptr[s0 + 1]; }
+    __syncthreads();
+    if (!act) return;
+    reduce_partials<2>(partA, nblkA, red);
+    LRS_TS(2, 1);
+    reduce_partials<5>(partB, nblkB, red + 2);
+    LRS_TS(2, 2);
+    if (threadIdx.x < 64) line_search_t<true>(par, red[0], red[1], red + 2, ls);   // wave 0
+    __syncthreads();
+    LRS_TS(2, 3);
+    if (blockIdx.x == 0 && threadIdx.x < LS_N) ls_cur[threadIdx.x] = ls[threadIdx.x];
     if (ls[LS_FLAG] != 0.0) return;
     const double tau = ls[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
-    for (long i = ((long)blockIdx.x * kBlock + threadIdx.x) * 2; i < NR; i += (long)gridDim.x * kBlock * 2) {
-        double2 r = *reinterpret_cast<const double2 *>(R + i);
-        double2 d = *reinterpret_cast<const double2 *>(D + i);
+    for (long i = i0; i < NR; i += (long)gridDim.x * kBlock * 2) {
+        double2 r = r0, d = d0;
+        if (i != i0) { r = *reinterpret_cast<const double2 *>(R + i); d = *reinterpret_cast<const double2 *>(D + i); }
         r.x += tau * d.x; r.y += tau * d.y;
         *reinterpret_cast<double2 *>(R + i) = r;
     }
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
-        double v = cvs[i] + tau * q1[i];
-        v = v + tau2 * q2[i];
-        cvs[i] = v;
-        M1[i] = ((-lam[i]) + (-rho) * b[i]) + rho * v;
+    LRS_TS(2, 4);
+    for (int s = s0; s < Ptot; s += gridDim.x * kBlock) {
+        double v = cr0;
+        int eb = e0, ee = e1;
+        if (s != s0) { v = Craw[s]; eb = slot_ptr[s]; ee = slot_ptr[s + 1]; }
+        for (int e = eb; e < ee; ++e) {
+            const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
+            const double2 ra = r[0], rb = r[1];
+            double cv = ra.x + tau * ra.y;
+            cv = cv + tau2 * rb.x;
+            const double M1 = rb.y + rho * cv;
+            v += M1 * slot_a[e];
+        }
+        S[s] = v;
     }
+    LRS_TS_END(2, 5);
+    LRS_BLK_END(2);
 }
 
-// G_new = 2 S R (row-owned), A(RR^T) slots (lower), L-BFGS pair
-// s = tau D, y = G_new - G_old into ring slot `head`, and the nine dots
-// needed by the next direction.  (ALMCalGrad :74-87, setlbfgsHisTwo :842-863,
+// S4.  G_new = 2 S R (row-owned), A(RR^T) slots (lower), L-BFGS pair s = tau D,
+// y = G_new - G_old into ring slot `head`, and the nine dots needed by the next
+// direction.  Partials written (9).  (ALMCalGrad :74-87, setlbfgsHisTwo :842-863,
 // primalInfeasibility's LORADSUVt(R,R) lorads_alg_common.c:387)
 template <int G, int E>
-__global__ void __launch_bounds__(kBlock) k_alm_grad(int n, int ld, long foff, const int *__restrict__ adj_ptr,
-                                                     const int *__restrict__ adj_low, const int *__restrict__ adj_col,
-                                                     const int *__restrict__ adj_slot, const double *__restrict__ S,
-                                                     const double *__restrict__ Rall, const double *__restrict__ Dall,
-                                                     double *G0, double *G1, double *s0, double *y0, double *s1,
-                                                     double *y1, double *__restrict__ uRR,
-                                                     const double *__restrict__ ctrl, const double *__restrict__ ls,
-                                                     int L, double *part, unsigned *ticket, double *fin) {
-    if (ctrl[C_ACTIVE] == 0.0 || ls[LS_FLAG] != 0.0) return;
+__global__ void __launch_bounds__(kRowBlock) k_it_grad(int n, int ld, long foff, const int *__restrict__ adj_ptr,
+                                                       const int *__restrict__ adj_low,
+                                                       const int *__restrict__ adj_col,
+                                                       const int *__restrict__ adj_slot, const double *__restrict__ S,
+                                                       const double *__restrict__ Rall, const double *__restrict__ Dall,
+                                                       double *G0, double *G1, double *s0, double *y0, double *s1,
+                                                       double *y1, double *__restrict__ uRR,
+                                                       const double *__restrict__ ctrl, const double *__restrict__ ls,
+                                                       int L, double *__restrict__ partC, int pblk_off) {
+    LRS_TS(3, 0);
+    LRS_BLK_BEGIN();
+    if (ctrl[C_ACT2] == 0.0 || ls[LS_FLAG] != 0.0) return;
+    LRS_TS(3, 1);
     const int gcur = (int)ctrl[C_GCUR];
     const int h = (int)ctrl[C_HEAD];
     const double tau = ls[LS_TAU];
@@ -685,42 +1247,63 @@ __global__ void __launch_bounds__(kBlock) k_alm_grad(int n, int ld, long foff, c
     const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
     const bool two = (L == 2);
     const int lane = threadIdx.x & (G - 1);
-    const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
-    const int ngrp = gridDim.x * kBlock / G;
+    const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kRowBlock / G;
     // acc: GG, ys, yy, sG, yG, soG, yoG, soy, yoy
     double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = grp; i < n; i += ngrp) {
-        double ri[E], g[E];
-        ld_row<E>(R + (long)i * ld + lane * E, ri);
+        const long oi = (long)i * ld + lane * E;
+        double ri[E], g[E], go[E], di[E], sov[E], yov[E];
+        // row-local operands first: their loads overlap the neighbour gathers
+        ld_row<E>(R + oi, ri);
+        ld_row<E>(Gold + oi, go);
+        ld_row<E>(D + oi, di);
+        if (two) {
+            ld_row<E>(so + oi, sov);
+            ld_row<E>(yo + oi, yov);
+        }
 #pragma unroll
         for (int e = 0; e < E; ++e) g[e] = 0.0;
         const int kb = adj_ptr[i], kl = adj_low[i], ke = adj_ptr[i + 1];
-        for (int k = kb; k < ke; ++k) {
-            const int j = adj_col[k];
-            const int s = adj_slot[k];
-            const double sv = S[s];
-            double rj[E];
-            ld_row<E>(R + (long)j * ld + lane * E, rj);
+        // neighbours four at a time (indices clamped to the row; extra lanes add 0)
+        for (int k0 = kb; k0 < ke; k0 += 4) {
+            int jj[4], ss[4];
 #pragma unroll
-            for (int e = 0; e < E; ++e) g[e] += sv * rj[e];
-            if (k < kl) {   // lower entry (j <= i): A(RR^T) slot owned by this row
-                double d = 0.0;
+            for (int u = 0; u < 4; ++u) {
+                const int k = min(k0 + u, ke - 1);
+                jj[u] = adj_col[k];
+                ss[u] = adj_slot[k];
+            }
+            double sv[4], rj[4][E];
 #pragma unroll
-                for (int e = 0; e < E; ++e) d += ri[e] * rj[e];
-                d = group_sum<G>(d);
-                if (lane == 0) uRR[s] = d;
+            for (int u = 0; u < 4; ++u) {
+                sv[u] = S[ss[u]];
+                ld_row<E>(R + (long)jj[u] * ld + lane * E, rj[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u;
+                if (k < ke) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) g[e] += sv[u] * rj[u][e];
+                }
+                if (k < kl) {   // lower entry (j <= i): A(RR^T) slot owned by this row
+                    double d = 0.0;
+#pragma unroll
+                    for (int e = 0; e < E; ++e) d += ri[e] * rj[u][e];
+                    d = group_sum<G>(d);
+                    if (lane == 0) uRR[ss[u]] = d;
+                }
             }
         }
-        double go[E], di[E], sv[E], yv[E];
+        double sv[E], yv[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) g[e] *= 2.0;
-        ld_row<E>(Gold + (long)i * ld + lane * E, go);
-        ld_row<E>(D + (long)i * ld + lane * E, di);
 #pragma unroll
         for (int e = 0; e < E; ++e) { sv[e] = tau * di[e]; yv[e] = g[e] - go[e]; }
-        st_row<E>(Gnew + (long)i * ld + lane * E, g);
-        st_row<E>(sh + (long)i * ld + lane * E, sv);
-        st_row<E>(yh + (long)i * ld + lane * E, yv);
+        st_row<E>(Gnew + oi, g);
+        st_row<E>(sh + oi, sv);
+        st_row<E>(yh + oi, yv);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             acc[0] += g[e] * g[e];
@@ -730,9 +1313,6 @@ __global__ void __launch_bounds__(kBlock) k_alm_grad(int n, int ld, long foff, c
             acc[4] += yv[e] * g[e];
         }
         if (two) {
-            double sov[E], yov[E];
-            ld_row<E>(so + (long)i * ld + lane * E, sov);
-            ld_row<E>(yo + (long)i * ld + lane * E, yov);
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 acc[5] += sov[e] * g[e];
@@ -742,32 +1322,10 @@ __global__ void __launch_bounds__(kBlock) k_alm_grad(int n, int ld, long foff, c
             }
         }
     }
-    partials_finalize<9>(acc, part, ticket, fin);
-}
-
-// cvs = A(RR^T) from scratch + residual ||b - cvs||^2 (primalInfeasibility)
-__global__ void __launch_bounds__(kBlock) k_alm_gather_rr(int m, int K, const int *__restrict__ con_ptr,
-                                                          const int *__restrict__ con_slot,
-                                                          const double *__restrict__ con_w,
-                                                          const double *__restrict__ uRR, const double *__restrict__ b,
-                                                          double *__restrict__ cvs, const double *__restrict__ ctrl,
-                                                          const double *__restrict__ ls, double *part,
-                                                          unsigned *ticket, double *fin) {
-    if (ctrl[C_ACTIVE] == 0.0 || ls[LS_FLAG] != 0.0) return;
-    double acc[1] = {0.0};
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
-        double tot = 0.0;
-        for (int k = 0; k < K; ++k) {
-            const long row = (long)k * m + i;
-            double v = 0.0;
-            for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) v += con_w[e] * uRR[con_slot[e]];
-            tot += v;
-        }
-        cvs[i] = tot;
-        const double dd = b[i] - tot;
-        acc[0] += dd * dd;
-    }
-    partials_finalize<1>(acc, part, ticket, fin);
+    LRS_TS(3, 2);
+    write_partials<9, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+    LRS_TS_END(3, 3);
+    LRS_BLK_END(3);
 }
 
 // ------------------------------------------------------------------------
@@ -929,7 +1487,16 @@ int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y,
     return 0;
 }
 
-// One fused ALM inner iteration.  Parity selects the control buffers.
+// Row-kernel grid of the split iteration: per cone, capped so that the sum over
+// cones fits the partial buffers.
+static inline int iter_grid(const DevCone &c, int K) {
+    long threads = (long)c.n * c.G;
+    int g = (int)std::max(1L, (threads + kRowBlock - 1) / kRowBlock);
+    const int cap = std::max(1, std::min(kIterMaxBlocks, kMaxPartialBlocks / std::max(1, K)));
+    return std::min(g, cap);
+}
+
+// One ALM inner iteration = four launches.  Parity selects the control buffers.
 int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
     const DevProblem &P = *a.P;
     DevWork &W = *a.W;
@@ -937,54 +1504,60 @@ int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
     double *ctrl_cur = W.ctrl + parity * C_NCTRL;
     double *ls_prev = W.lsres + (parity ^ 1) * LS_N;
     double *ls_cur = W.lsres + parity * LS_N;
-    double *fin = fin_ptr();
     const int L = 2;
-    // 1. direction (+ control)
-    hipLaunchKernelGGL(k_alm_dir, dim3(grid_elems(P.NRpad, 2)), dim3(kBlock), 0, st, P.NRpad, W.par, ctrl_prev,
-                       ctrl_cur, ls_prev, P.K, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1]);
-    LRS_CHECK_LAUNCH();
-    // 2. sym(RD^T), DD^T on the pattern (+ objective parts)
+    int nblk_rows = 0;
+    for (int k = 0; k < P.K; ++k) nblk_rows += iter_grid(P.cones[k], P.K);
+    auto mark = [&](int q) -> int {
+        if (a.ev && hipEventRecord(a.ev[q], st) != hipSuccess) {
+            snprintf(g_err, sizeof(g_err), "hipEventRecord failed");
+            return -1;
+        }
+        return 0;
+    };
+    if (mark(0)) return -1;
+    // S1: control, A(RR^T) refresh, direction, sym(RD^T) / DD^T
+    int off = 0;
     for (int k = 0; k < P.K; ++k) {
         const DevCone &c = P.cones[k];
-        const int grid = grid_rows(c.n, c.G);
+        const int grid = iter_grid(c, P.K);
         LRS_LAYOUT_SWITCH(c.G, c.E, {
-            hipLaunchKernelGGL((k_sddmm<GG, EE, 2>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr,
-                               c.adj_low, c.adj_col, c.adj_slot, W.R + c.foff, W.D + c.foff, W.uvt0, W.uvt1, P.Cw,
-                               W.part, ticket_ptr(T_SDDMM + 8 + k % 8), fin + FIN_SD + 2 * k, ctrl_cur);
+            hipLaunchKernelGGL((k_it_dir_sddmm<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
+                               c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.D, W.G[0], W.G[1],
+                               W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, k == 0 ? 1 : 0, P.m, P.K,
+                               P.con_ptr, P.con_slot, P.con_w, W.uvt2, P.b, W.cvs, W.par, ctrl_prev, ctrl_cur,
+                               ls_prev, W.partC, nblk_rows, W.part, off);
         });
         LRS_CHECK_LAUNCH();
+        off += grid;
     }
-    // 3. q1, q2 + line-search dots
-    hipLaunchKernelGGL(k_alm_gather_q, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, P.K, P.con_ptr,
-                       P.con_slot, P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, W.q1, W.q2, W.partB,
-                       ticket_ptr(T_Q), fin + FIN_Q, ctrl_cur);
+    if (mark(1)) return -1;
+    // S2: phase-1 test, q1, q2, line-search dots
+    const int gq = std::min(grid_elems(P.m, 1), kMaxPartialBlocks);
+    hipLaunchKernelGGL(k_it_q, dim3(gq), dim3(kBlock), 0, st, P.m, P.K, P.con_ptr, P.con_slot, P.con_w, W.uvt0,
+                       W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.part, nblk_rows, W.rec, W.partB);
     LRS_CHECK_LAUNCH();
-    // 4. line search + updates of R, A(RR^T), M1
-    hipLaunchKernelGGL(k_alm_update, dim3(grid_elems(P.NRpad > P.m ? P.NRpad : P.m, 2)), dim3(kBlock), 0, st,
-                       P.NRpad, P.m, P.K, W.par, ctrl_cur, ls_cur, W.R, W.D, W.cvs, W.q1, W.q2, W.lam, P.b, W.M1);
+    if (mark(2)) return -1;
+    // S3: line search, R update, S = C + A^*(M1)
+    const int gu = std::max(grid_elems(P.NRpad, 2), grid_elems(P.Ptot, 1));
+    hipLaunchKernelGGL(k_it_update, dim3(gu), dim3(kBlock), 0, st, P.NRpad, P.Ptot, P.slot_ptr, P.slot_con,
+                       P.slot_a, P.Craw, W.rec, W.R, W.D, W.par, ctrl_cur, W.part, nblk_rows, W.partB, gq, ls_cur,
+                       W.S);
     LRS_CHECK_LAUNCH();
-    // 5. S = C + A^*(M1)
-    hipLaunchKernelGGL(k_wsum, dim3(grid_elems(P.Ptot, 1)), dim3(kBlock), 0, st, P.Ptot, P.slot_ptr, P.slot_con,
-                       P.slot_a, P.Craw, 1, W.M1, W.S, ctrl_cur, ls_cur);
-    LRS_CHECK_LAUNCH();
-    // 6. gradient + A(RR^T) slots + L-BFGS pair
+    if (mark(3)) return -1;
+    // S4: gradient, A(RR^T) slots, L-BFGS pair, dots
+    off = 0;
     for (int k = 0; k < P.K; ++k) {
         const DevCone &c = P.cones[k];
-        const int grid = grid_rows(c.n, c.G);
+        const int grid = iter_grid(c, P.K);
         LRS_LAYOUT_SWITCH(c.G, c.E, {
-            hipLaunchKernelGGL((k_alm_grad<GG, EE>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr,
+            hipLaunchKernelGGL((k_it_grad<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr,
                                c.adj_low, c.adj_col, c.adj_slot, W.S, W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
-                               W.ls[1], W.ly[1], W.uvt2, ctrl_cur, ls_cur, L, W.partC,
-                               ticket_ptr(T_GRAD + 24 + k % 8), fin + FIN_GR + 9 * k);
+                               W.ls[1], W.ly[1], W.uvt2, ctrl_cur, ls_cur, L, W.partC, off);
         });
         LRS_CHECK_LAUNCH();
+        off += grid;
     }
-    // 7. A(RR^T) -> cvs, residual
-    hipLaunchKernelGGL(k_alm_gather_rr, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, P.K, P.con_ptr,
-                       P.con_slot, P.con_w, W.uvt2, P.b, W.cvs, ctrl_cur, ls_cur, W.part, ticket_ptr(T_RR),
-                       fin + FIN_RR);
-    LRS_CHECK_LAUNCH();
-    return 0;
+    return mark(4);
 }
 
 // ------------------------------------------------------------------------

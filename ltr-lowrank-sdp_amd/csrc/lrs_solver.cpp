@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "../../include/lrsdp.h"
@@ -126,7 +127,25 @@ struct lrs_ctx {
     std::vector<long> cgIterCone;
     std::string path;
     FILE *logfp = nullptr;
+    // hipGraph cache of inner-iteration batches (keyed by batch size; the kernels'
+    // arguments are the workspace pointers, so a new workspace drops the cache)
+    std::map<int, hipGraphExec_t> graphs;
+    bool use_graphs = true;
+    // per-stage event profiling (lrs_profile_stages)
+    bool prof = false;
+    // host-loop statistics (LRS_STATS=1): run_inner calls, batches, iterations, seconds
+    bool stats = false;
+    long st_calls = 0, st_batches = 0, st_iters = 0, st_nop = 0;
+    double st_inner_s = 0;
+    hipEvent_t pev[2][5] = {};
+    double pacc[4] = {0, 0, 0, 0};
+    long pn = 0;
 };
+
+static void drop_graphs(lrs_ctx *c) {
+    for (auto &kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
+    c->graphs.clear();
+}
 
 static void logf_(lrs_ctx *c, const lrs_params *p, const char *fmt, ...) {
     char buf[2048];
@@ -142,11 +161,12 @@ static void logf_(lrs_ctx *c, const lrs_params *p, const char *fmt, ...) {
 // workspace
 // ------------------------------------------------------------------------
 static void free_work(lrs_ctx *c) {
+    drop_graphs(c);
     if (!c->walloc) return;
     DevWork &W = c->W;
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
-                      W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram};
+                      W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     c->W = DevWork();
@@ -186,7 +206,7 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         A(&W.M1, m) || A(&W.wtmp, m) || A(&W.cvc, (long)m * std::max(1, P.K)) ||
         A(&W.part, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.partB, (long)kMaxPartialVals * kMaxPartialBlocks) ||
         A(&W.partC, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.ctrl, 2 * C_NCTRL) ||
-        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax))
+        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax) || A(&W.rec, 4L * m))
         return -1;
     HIPC(hipStreamSynchronize(c->st));
     c->walloc = true;
@@ -545,6 +565,28 @@ static int update_check_ema(double *cur, double *old, double v, double alpha, do
 }
 
 // ---- device inner loop
+// Batch of B inner iterations (B even, so the batch ends on parity 1) captured once
+// into a hipGraph and replayed: one host launch per batch instead of 4B.
+static int get_batch_graph(lrs_ctx *c, int B, hipGraphExec_t *out) {
+    auto it = c->graphs.find(B);
+    if (it != c->graphs.end()) { *out = it->second; return 0; }
+    AlmIterArgs a{&c->dp, &c->W, nullptr};
+    hipGraph_t g = nullptr;
+    HIPC(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+    int rc = 0;
+    for (int j = 0; j < B && rc == 0; ++j) rc = enqueue_alm_iteration(a, j & 1, c->st);
+    hipError_t e = hipStreamEndCapture(c->st, &g);
+    if (rc != 0) { if (g) (void)hipGraphDestroy(g); set_err("capture: %s", last_device_error()); return -1; }
+    if (e != hipSuccess) { set_err("hipStreamEndCapture: %s", hipGetErrorString(e)); return -1; }
+    hipGraphExec_t ge = nullptr;
+    e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) { set_err("hipGraphInstantiate: %s", hipGetErrorString(e)); return -1; }
+    c->graphs[B] = ge;
+    *out = ge;
+    return 0;
+}
+
 struct InnerIo {
     long inner, local, clear;
     double rcval, lag, pinf1, pinfinf;
@@ -558,6 +600,7 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     par[P_HIGHACC] = p->highAccMode; par[P_BUDGET] = (double)budget; par[P_L] = p->lbfgsListLength; par[P_GAP] = gap;
     double ctl[C_NCTRL] = {0};
     ctl[C_ACTIVE] = 1; ctl[C_EXIT] = EXIT_NONE; ctl[C_INNER] = (double)io.inner; ctl[C_LOCAL] = (double)io.local;
+    ctl[C_ACT2] = 1; ctl[C_EXIT2] = EXIT_NONE; ctl[C_RRDONE] = 0;
     ctl[C_CLEAR] = (double)io.clear; ctl[C_HEAD] = c->head; ctl[C_GCUR] = c->gcur; ctl[C_PENDING] = 0;
     ctl[C_RCVAL] = io.rcval; ctl[C_LAG] = io.lag; ctl[C_PINF1] = io.pinf1; ctl[C_PINFINF] = io.pinfinf;
     ctl[C_BETA0] = c->beta[0]; ctl[C_BETA1] = c->beta[1]; ctl[C_YY0] = c->yy[0]; ctl[C_YY1] = c->yy[1];
@@ -565,19 +608,52 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     HIPC(hipMemcpyAsync(c->W.par, c->hpin, sizeof(par), hipMemcpyHostToDevice, c->st));
     memcpy(c->hpin + 64, ctl, sizeof(ctl));
     HIPC(hipMemcpyAsync(c->W.ctrl + C_NCTRL, c->hpin + 64, sizeof(ctl), hipMemcpyHostToDevice, c->st));
-    AlmIterArgs a{&c->dp, &c->W, 0, 0, 0, 0};
+    AlmIterArgs a{&c->dp, &c->W, nullptr};
     int B = 4;
     double *res = c->hpin + 128;
+    const double t_in = c->stats ? now_s() : 0.0;
+    long enq = 0;
     for (;;) {
-        for (int j = 0; j < B; ++j) OPC(enqueue_alm_iteration(a, j & 1, c->st));
+        enq += B;
+        if (c->prof) {
+            // two iterations with events around each launch, then read the control
+            B = 2;
+            for (int j = 0; j < B; ++j) {
+                a.ev = c->pev[j];
+                OPC(enqueue_alm_iteration(a, j & 1, c->st));
+            }
+            a.ev = nullptr;
+        } else if (c->use_graphs) {
+            hipGraphExec_t ge;
+            if (get_batch_graph(c, B, &ge)) return -1;
+            HIPC(hipGraphLaunch(ge, c->st));
+        } else {
+            for (int j = 0; j < B; ++j) OPC(enqueue_alm_iteration(a, j & 1, c->st));
+        }
         HIPC(hipMemcpyAsync(res, c->W.ctrl + C_NCTRL, sizeof(double) * C_NCTRL, hipMemcpyDeviceToHost, c->st));
         HIPC(hipStreamSynchronize(c->st));
-        if (res[C_ACTIVE] == 0.0) break;
+        if (c->prof && res[C_ACT2] != 0.0) {
+            for (int j = 0; j < 2; ++j)
+                for (int q = 0; q < 4; ++q) {
+                    float ms = 0;
+                    HIPC(hipEventElapsedTime(&ms, c->pev[j][q], c->pev[j][q + 1]));
+                    c->pacc[q] += ms;
+                }
+            c->pn += 2;
+        }
+        if (c->stats) c->st_batches++;
+        if (res[C_ACT2] == 0.0) break;
         B = std::min(B * 2, 64);
+    }
+    if (c->stats) {
+        c->st_calls++;
+        c->st_iters += (long)res[C_INNER] - io.inner;
+        c->st_nop += enq - ((long)res[C_INNER] - io.inner);
+        c->st_inner_s += now_s() - t_in;
     }
     io.inner = (long)res[C_INNER]; io.local = (long)res[C_LOCAL]; io.clear = (long)res[C_CLEAR];
     io.rcval = res[C_RCVAL]; io.lag = res[C_LAG]; io.pinf1 = res[C_PINF1]; io.pinfinf = res[C_PINFINF];
-    io.exitReason = (int)res[C_EXIT];
+    io.exitReason = (int)res[C_EXIT2];
     c->head = (int)res[C_HEAD]; c->gcur = (int)res[C_GCUR];
     c->beta[0] = res[C_BETA0]; c->beta[1] = res[C_BETA1]; c->yy[0] = res[C_YY0]; c->yy[1] = res[C_YY1];
     return 0;
@@ -592,7 +668,20 @@ static void alm_log(lrs_ctx *c, const lrs_params *p, const AlmState &st, double 
 }
 
 // LORADS_ALMOptimize, lorads_alm.c:1220-1484
+static int alm_optimize_body(lrs_ctx *c, const lrs_params *p, AlmState &st, double tss);
 static int alm_optimize(lrs_ctx *c, const lrs_params *p, AlmState &st, double tss) {
+    c->st_calls = c->st_batches = c->st_iters = c->st_nop = 0;
+    c->st_inner_s = 0;
+    const double t0 = now_s();
+    const int rc = alm_optimize_body(c, p, st, tss);
+    if (c->stats)
+        fprintf(stderr, "[lrs stats] alm %.3f ms: run_inner calls %ld, batches %ld, iterations %ld, "
+                "no-op iterations %ld, in batches %.3f ms, host outside %.3f ms, outer %ld\n",
+                (now_s() - t0) * 1e3, c->st_calls, c->st_batches, c->st_iters, c->st_nop, c->st_inner_s * 1e3,
+                (now_s() - t0 - c->st_inner_s) * 1e3, st.outerIter);
+    return rc;
+}
+static int alm_optimize_body(lrs_ctx *c, const lrs_params *p, AlmState &st, double tss) {
     const double ori = now_s();
     int MAX_SUB = 5000;
     int is_rank_max = check_all_rank_max(c, 1.0);
@@ -953,6 +1042,8 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
     c->device = device;
     if (hipSetDevice(device) != hipSuccess) { set_err("hipSetDevice(%d) failed", device); delete c; return -1; }
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); delete c; return -1; }
+    if (const char *ng = getenv("LRS_NO_GRAPHS")) c->use_graphs = (atoi(ng) == 0);
+    if (const char *sv = getenv("LRS_STATS")) c->stats = (atoi(sv) != 0);
     if (hipHostMalloc((void **)&c->hpin, 4096 * sizeof(double), 0) != hipSuccess) { set_err("pinned alloc failed"); delete c; return -1; }
     *out = c;
     return 0;
@@ -1323,6 +1414,36 @@ int lrs_alm_throughput(lrs_ctx *c, const lrs_params *pin, long warmup, long step
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return 0;
+}
+
+int lrs_profile_stages(lrs_ctx *c, const lrs_params *pin, long steps, double *stage_ms, long *done) {
+    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    lrs_params prm = *pin;
+    prm.phase1Tol = 1e-300;
+    prm.maxALMIter = 1000000000;
+    prm.skipADMM = 1;
+    prm.timeSecLimit = 1e30;
+    prm.almInnerBudget = steps;
+    for (auto &row : c->pev)
+        for (auto &e : row) HIPC(hipEventCreate(&e));
+    c->prof = true;
+    c->pn = 0;
+    for (double &v : c->pacc) v = 0;
+    lrs_result r;
+    const int rc = solve_impl(c, &prm, &r);
+    c->prof = false;
+    for (auto &row : c->pev)
+        for (auto &e : row) { (void)hipEventDestroy(e); e = nullptr; }
+    if (rc) return -1;
+    for (int q = 0; q < 4; ++q) stage_ms[q] = c->pn ? c->pacc[q] / c->pn : 0.0;
+    if (done) *done = r.alm_inner;
+    return 0;
+}
+
+int lrs_debug_phase_times(lrs_ctx *c, unsigned long long *out, unsigned long long *blk) {
+    if (!c) { set_err("null ctx"); return -1; }
+    HIPC(hipDeviceSynchronize());
+    return read_phase_times(out, blk);
 }
 
 int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {

@@ -104,6 +104,8 @@ def load_library(path=None):
                                          dp, dp]),
         "lrs_set_log_path": (C.c_int, [vp, C.c_char_p]),
         "lrs_time_auut": (C.c_int, [vp, C.c_int, dp]),
+        "lrs_profile_stages": (C.c_int, [vp, C.POINTER(Params), C.c_long, dp, C.POINTER(C.c_long)]),
+        "lrs_debug_phase_times": (C.c_int, [vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -255,13 +257,36 @@ class Solver:
         self.lib.lrs_trajectory(self.ctx, phase, cur, orc, n)
         return list(cur)[:n], list(orc)[:n]
 
-    def alm_throughput(self, warmup, steps, **kw):
+    def alm_throughput(self, warmup, steps, auut=False, **kw):
         p = default_params(**kw)
         sec, kms, ims = C.c_double(), C.c_double(), C.c_double()
         done = C.c_long()
         self._check(self.lib.lrs_alm_throughput(self.ctx, C.byref(p), warmup, steps, C.byref(sec), C.byref(done),
-                                                C.byref(kms), C.byref(ims)), "alm_throughput")
-        return {"seconds": sec.value, "done": done.value, "auut_ms": kms.value, "iter_ms": ims.value}
+                                                C.byref(kms) if auut else None, C.byref(ims)), "alm_throughput")
+        return {"seconds": sec.value, "done": done.value, "auut_ms": kms.value if auut else None,
+                "iter_ms": ims.value}
+
+    def profile_stages(self, steps, **kw):
+        """Average ms per launch of the four split-iteration stages (HIP events)."""
+        p = default_params(**kw)
+        ms = (C.c_double * 4)()
+        done = C.c_long()
+        self._check(self.lib.lrs_profile_stages(self.ctx, C.byref(p), steps, ms, C.byref(done)), "profile_stages")
+        return list(ms), done.value
+
+    def debug_phase_times(self):
+        """In-kernel timestamps (diagnostics library only): ([4][16] block-0 phase ticks,
+        [4][1024][2] per-block entry/exit ticks) or None from the product library."""
+        out = (C.c_ulonglong * 64)()
+        blk = (C.c_ulonglong * (4 * 1024 * 2))()
+        rc = self.lib.lrs_debug_phase_times(self.ctx, out, blk)
+        if rc < 0:
+            raise RuntimeError(self.lib.lrs_last_error().decode())
+        if rc != 64:
+            return None
+        ph = [list(out[16 * k:16 * k + 16]) for k in range(4)]
+        b = [[(blk[(k * 1024 + i) * 2], blk[(k * 1024 + i) * 2 + 1]) for i in range(1024)] for k in range(4)]
+        return ph, b
 
     def time_auut(self, reps=100):
         ms = C.c_double()

@@ -80,7 +80,9 @@ def test_device_solve_matches_reference(solver_mod, case):
     sv = solver_mod.Solver(instance(s["instance"]))
     res = sv.solve(**kw)
     r = s["result"]
-    assert res["final_rank"] == r["rank"]
+    # final_rank is the sum over cones (lorads_sum_rank, lorads_logging.c:199-213);
+    # REF_RESULT rank is cone 0's only
+    assert res["final_rank"] == s["json"]["trajectory"]["phase_1"]["curr_rank"][-1]
     if s["instance"].startswith("mc_"):
         assert abs(res["alm_inner"] - r["alm_inner"]) <= max(2, 0.02 * r["alm_inner"])
         for ours, ref in (("alm_pobj", "alm_pobj"), ("alm_dobj", "alm_dobj"), ("pobj", "admm_pobj")):
