@@ -54,6 +54,7 @@ enum CtrlIdx {
     C_ACT2,         // ACTIVE after the phase-1 (l_inf pinf) test of the completed iteration
     C_EXIT2,        // exit reason after that test
     C_RRDONE,       // 1 if this iteration's first stage refreshed A(RR^T) and the residual
+    C_RCUR,         // which factor buffer (R, R2) holds the current iterate
     C_NCTRL = 40
 };
 enum ExitReason {
@@ -100,12 +101,18 @@ struct DevProblem {
     double *con_w = nullptr;                                 // [Z]
     int *slot_ptr = nullptr, *slot_con = nullptr;            // [Ptot+1], [Z]
     double *slot_a = nullptr;                                // [Z]
+    // single-slot ("local") constraints per slot, and the list of the others
+    int mg = 0;                                              // number of global constraints
+    int *glob = nullptr;                                     // [mg]
+    int *loc_ptr = nullptr, *loc_con = nullptr;              // [Ptot+1], [m - mg]
+    double *loc_w = nullptr;                                 // (2 - delta) a of that one entry
     std::vector<DevCone> cones;
 };
 
 // Scratch shared by the kernels of one solve.
 struct DevWork {
     double *R = nullptr, *D = nullptr, *G[2] = {nullptr, nullptr};
+    double *R2 = nullptr;      // second factor buffer of the split iteration (R double-buffered)
     double *ls[2] = {nullptr, nullptr}, *ly[2] = {nullptr, nullptr};
     double *U = nullptr, *V = nullptr, *X = nullptr;         // ADMM / scratch factors
     double *cg_r = nullptr, *cg_p = nullptr, *cg_Q = nullptr, *cg_b = nullptr, *M2 = nullptr;

@@ -837,7 +837,7 @@ __device__ void line_search_v(const double *__restrict__ par, double p1, double 
 // updated in place; the arithmetic runs on a register copy (constant indices only).
 // d = the nine dots of the previous gradient stage when `fold`.
 __device__ void ctrl_step(double *csh, const double *__restrict__ par, double lsflag, double lstau, int fold,
-                          const double *d) {
+                          const double *d, bool ph1) {
     double c[C_NCTRL];
 #pragma unroll
     for (int q = 0; q < C_NCTRL; ++q) c[q] = csh[q];
@@ -867,11 +867,28 @@ __device__ void ctrl_step(double *csh, const double *__restrict__ par, double ls
             c[C_DSG] = d[3]; c[C_DYG] = d[4]; c[C_DSOG] = d[5]; c[C_DYOG] = d[6];
             c[C_DSOY] = d[7]; c[C_DYOY] = d[8];
             c[C_PENDING] = 2.0;
-            c[C_RRDONE] = 1.0;
-            // the phase-1 test on the refreshed residual (which takes precedence) runs in S2
-            c[C_RCVAL] = sqrt(c[C_LAG]) / (1.0 + cninf);
-            c[C_INNER] += 1; c[C_LOCAL] += 1; c[C_CLEAR] += 1;
-            if (c[C_LOCAL] > 800) { c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_LOCAL800; }
+            c[C_RCUR] = 1.0 - c[C_RCUR];
+            if (ph1) {
+                // primalInfeasibility (lorads_alg_common.c:393), l_inf and the phase-1 exit
+                // (lorads_alm.c:1359-1364), which takes precedence over the tests below
+                const double pinf1 = sqrt(d[9]) / (1.0 + par[P_BN1]);
+                c[C_PINF1] = pinf1;
+                c[C_PINFINF] = pinf1 * (1.0 + par[P_BN1]) / (1.0 + par[P_BNINF]);
+                c[C_INNER] += 1; c[C_LOCAL] += 1; c[C_CLEAR] += 1;
+                if ((c[C_PINFINF] <= par[P_PH1TOL]) && ((par[P_GAP] <= par[P_PH1TOL]) || (par[P_HIGHACC] == 0.0))) {
+                    c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_PHASE1;
+                } else {
+                    c[C_RCVAL] = sqrt(c[C_LAG]) / (1.0 + cninf);
+                    if (c[C_LOCAL] > 800) { c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_LOCAL800; }
+                }
+            } else {
+                // the phase-1 test on the refreshed residual (which takes precedence) runs in
+                // the global-constraint stage
+                c[C_RRDONE] = 1.0;
+                c[C_RCVAL] = sqrt(c[C_LAG]) / (1.0 + cninf);
+                c[C_INNER] += 1; c[C_LOCAL] += 1; c[C_CLEAR] += 1;
+                if (c[C_LOCAL] > 800) { c[C_ACTIVE] = 0.0; c[C_EXIT] = EXIT_LOCAL800; }
+            }
         }
     } else if (c[C_PENDING] == 0.0) {
         c[C_DSG] = c[C_DYG] = c[C_DSOG] = c[C_DYOG] = c[C_DSOY] = c[C_DYOY] = 0.0;
@@ -919,6 +936,7 @@ __device__ void ctrl_step(double *csh, const double *__restrict__ par, double ls
         c[C_DG] = dg;
         c[C_PENDING] = 1.0;
     }
+    if (ph1) { c[C_ACT2] = c[C_ACTIVE]; c[C_EXIT2] = c[C_EXIT]; }
 #pragma unroll
     for (int q = 0; q < C_NCTRL; ++q) csh[q] = c[q];
 }
@@ -958,39 +976,45 @@ struct DirRow {
 
 constexpr int kRowBlock = 512;   // threads per block of the row kernels S1 / S4
 
-// S1.  Partials written (3): objective part of <C, sym RD^T>, of <C, DD^T>, residual.
+// Rows of the lower pattern carry the single-slot ("local") constraints: whoever
+// computes a slot value also evaluates the local constraints on that slot.
+//
+// A.  Partials written (8): objective part of <C, sym RD^T>, of <C, DD^T>, the five
+//     line-search dots over the local constraints, residual of the global ones.
 template <int G, int E>
-__global__ void __launch_bounds__(kRowBlock) k_it_dir_sddmm(
+__global__ void __launch_bounds__(kRowBlock) k_it_a(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
-    const double *__restrict__ Rall, double *__restrict__ Dall, const double *__restrict__ G0,
-    const double *__restrict__ G1, const double *__restrict__ s0a, const double *__restrict__ y0a,
-    const double *__restrict__ s1a, const double *__restrict__ y1a, double *__restrict__ uRD,
-    double *__restrict__ uDD, int do_rr, int m, int K, const int *__restrict__ con_ptr,
-    const int *__restrict__ con_slot, const double *__restrict__ con_w, const double *__restrict__ uRR,
-    const double *__restrict__ b, double *__restrict__ cvs, const double *__restrict__ par,
+    const double *__restrict__ Rb0, const double *__restrict__ Rb1, double *__restrict__ Dall,
+    const double *__restrict__ G0, const double *__restrict__ G1, const double *__restrict__ s0a,
+    const double *__restrict__ y0a, const double *__restrict__ s1a, const double *__restrict__ y1a,
+    double *__restrict__ uRD, double *__restrict__ uDD, const int *__restrict__ loc_ptr,
+    const int *__restrict__ loc_con, const double *__restrict__ loc_w, const double *__restrict__ b,
+    double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec, int do_glob, int mg,
+    const int *__restrict__ glob, int m, int K, const int *__restrict__ con_ptr, const int *__restrict__ con_slot,
+    const double *__restrict__ con_w, const double *__restrict__ uRR, const double *__restrict__ par,
     const double *__restrict__ ctrl_prev, double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev,
-    const double *__restrict__ partG, int nblkG, double *__restrict__ partA, int pblk_off) {
+    const double *__restrict__ partC, int nblkC, double *__restrict__ partA, int pblk_off) {
     __shared__ double c[C_NCTRL];
-    __shared__ double red[9];
+    __shared__ double red[10];
     __shared__ double lsv[2];
     LRS_TS(0, 0);
     LRS_BLK_BEGIN();
-    // control words, ls result and the gradient-stage partials load together
     if (threadIdx.x < C_NCTRL) c[threadIdx.x] = ctrl_prev[threadIdx.x];
     if (threadIdx.x == 0) { lsv[0] = ls_prev[LS_FLAG]; lsv[1] = ls_prev[LS_TAU]; }
     __syncthreads();
     LRS_TS(0, 1);
     const int fold = (c[C_ACT2] != 0.0 && c[C_PENDING] == 1.0 && lsv[0] == 0.0) ? 1 : 0;
-    if (fold) reduce_partials<9, kRowBlock>(partG, nblkG, red);
+    if (fold) reduce_partials<10, kRowBlock>(partC, nblkC, red);
     else __syncthreads();   // every wave has read c[] before thread 0 rewrites it
     LRS_TS(0, 2);
-    if (threadIdx.x == 0) ctrl_step(c, par, lsv[0], lsv[1], fold, red);
-    double acc[3] = {0.0, 0.0, 0.0};
-    if (fold && do_rr) {
-        // cvs = A(RR^T) from scratch, residual ||b - cvs||^2 (primalInfeasibility);
+    if (threadIdx.x == 0) ctrl_step(c, par, lsv[0], lsv[1], fold, red, mg == 0);
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (fold && do_glob) {
+        // global constraints: A(RR^T) from the slots and their residual (primalInfeasibility);
         // independent of this iteration's control, so it runs beside ctrl_step
-        for (int i = blockIdx.x * kRowBlock + threadIdx.x; i < m; i += gridDim.x * kRowBlock) {
+        for (int g = blockIdx.x * kRowBlock + threadIdx.x; g < mg; g += gridDim.x * kRowBlock) {
+            const int i = glob[g];
             double tot = 0.0;
             for (int k = 0; k < K; ++k) {
                 const long row = (long)k * m + i;
@@ -1000,21 +1024,22 @@ __global__ void __launch_bounds__(kRowBlock) k_it_dir_sddmm(
             }
             cvs[i] = tot;
             const double dd = b[i] - tot;
-            acc[2] += dd * dd;
+            acc[7] += dd * dd;
         }
     }
     __syncthreads();
     LRS_TS(0, 3);
-    if (do_rr && blockIdx.x == 0 && threadIdx.x < C_NCTRL) ctrl_cur[threadIdx.x] = c[threadIdx.x];
+    if (pblk_off == 0 && blockIdx.x == 0 && threadIdx.x < C_NCTRL) ctrl_cur[threadIdx.x] = c[threadIdx.x];
     const bool active = c[C_ACTIVE] != 0.0;
-    if (!fold && !active) return;
+    if (!active && !(fold && mg > 0)) return;
     LRS_TS(0, 4);
     if (active) {
         DirCoef kc;
         kc.cg = c[C_CG]; kc.cs0 = c[C_CS0]; kc.cy0 = c[C_CY0]; kc.cs1 = c[C_CS1]; kc.cy1 = c[C_CY1];
         kc.u0 = (kc.cs0 != 0.0 || kc.cy0 != 0.0);
         kc.u1 = (kc.cs1 != 0.0 || kc.cy1 != 0.0);
-        const double *__restrict__ R = Rall + foff;
+        const double rho = par[P_RHO], rhoInv = 1.0 / rho;
+        const double *__restrict__ R = (c[C_RCUR] == 0.0 ? Rb0 : Rb1) + foff;
         double *__restrict__ D = Dall + foff;
         const double *__restrict__ Gc = (c[C_GCUR] == 0.0 ? G0 : G1) + foff;
         const double *__restrict__ s0 = s0a + foff, *__restrict__ y0 = y0a + foff;
@@ -1074,44 +1099,55 @@ __global__ void __launch_bounds__(kRowBlock) k_it_dir_sddmm(
                         uDD[sl] = d1;
                         acc[0] += cw * d0;
                         acc[1] += cw * d1;
+                        // local constraints on this slot: q1 = 2 A(sym RD^T), q2 = A(DD^T)
+                        // (ALMCalq12p12 lorads_alm.c:714-734) and the line-search dots (:269-277)
+                        for (int e = loc_ptr[sl]; e < loc_ptr[sl + 1]; ++e) {
+                            const int ci = loc_con[e];
+                            const double w = loc_w[e];
+                            const double q1 = 2.0 * (w * d0), q2 = w * d1;
+                            const double bi = b[ci], cv = cvs[ci], li = lam[ci];
+                            const double q0 = (bi - cv) + rhoInv * li;
+                            acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1;
+                            acc[6] += q0 * q1;
+                            double2 *r = reinterpret_cast<double2 *>(rec + 4L * ci);
+                            r[0] = make_double2(cv, q1);
+                            r[1] = make_double2(q2, (-li) + (-rho) * bi);
+                        }
                     }
                 }
             }
         }
     }
     LRS_TS(0, 5);
-    write_partials<3, kRowBlock>(acc, partA, pblk_off + blockIdx.x);
+    write_partials<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x);
     LRS_TS_END(0, 6);
     LRS_BLK_END(0);
 }
 
-// S2.  Partials written (5): q2q2, q1q2, q0q2, q1q1, q0q1.  rec[i] = {A(RR^T)_i, q1_i,
-// q2_i, -lam_i - rho b_i} feeds S3's on-the-fly M1.
-__global__ void __launch_bounds__(kBlock) k_it_q(int m, int K, const int *__restrict__ con_ptr,
-                                                 const int *__restrict__ con_slot, const double *__restrict__ con_w,
-                                                 const double *__restrict__ uRD, const double *__restrict__ uDD,
-                                                 const double *__restrict__ b, const double *__restrict__ cvs,
-                                                 const double *__restrict__ lam, const double *__restrict__ par,
-                                                 double *__restrict__ ctrl_cur, const double *__restrict__ partA,
-                                                 int nblkA, double *__restrict__ rec, double *__restrict__ partB) {
+// G (only with global constraints).  Phase-1 test on the full residual (local part
+// from stage B's partials, global part from stage A's), then q1, q2, the five dots
+// and rec for the global constraints.  Partials written (5).
+__global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__ glob, int m, int K,
+                                                 const int *__restrict__ con_ptr, const int *__restrict__ con_slot,
+                                                 const double *__restrict__ con_w, const double *__restrict__ uRD,
+                                                 const double *__restrict__ uDD, const double *__restrict__ b,
+                                                 const double *__restrict__ cvs, const double *__restrict__ lam,
+                                                 const double *__restrict__ par, double *__restrict__ ctrl_cur,
+                                                 const double *__restrict__ partC, const double *__restrict__ partA,
+                                                 int nblk, double *__restrict__ rec, double *__restrict__ partB) {
     __shared__ double cs[3];
-    __shared__ double red[1];
+    __shared__ double red[2];
     LRS_TS(1, 0);
     LRS_BLK_BEGIN();
     if (threadIdx.x == 0) { cs[0] = ctrl_cur[C_ACTIVE]; cs[1] = ctrl_cur[C_EXIT]; cs[2] = ctrl_cur[C_RRDONE]; }
-    PartialLoad<1, kBlock> pl;
-    pl.load(partA + 2 * kMaxPartialBlocks, nblkA);
-    // this thread's first constraint: loads independent of the control decision
-    const int i0 = blockIdx.x * kBlock + threadIdx.x;
-    double b0 = 0.0, c0 = 0.0, l0 = 0.0;
-    if (i0 < m) { b0 = b[i0]; c0 = cvs[i0]; l0 = lam[i0]; }
     __syncthreads();
     bool act = cs[0] != 0.0;
     double ex = cs[1];
     if (cs[2] != 0.0) {
-        pl.reduce(red);
+        reduce_partials<1>(partC + 9 * kMaxPartialBlocks, nblk, red);
+        reduce_partials<1>(partA + 7 * kMaxPartialBlocks, nblk, red + 1);
         // primalInfeasibility (lorads_alg_common.c:393) and l_inf (lorads_alm.c:1359)
-        const double pinf1 = sqrt(red[0]) / (1.0 + par[P_BN1]);
+        const double pinf1 = sqrt(red[0] + red[1]) / (1.0 + par[P_BN1]);
         const double pinfinf = pinf1 * (1.0 + par[P_BN1]) / (1.0 + par[P_BNINF]);
         if ((pinfinf <= par[P_PH1TOL]) && ((par[P_GAP] <= par[P_PH1TOL]) || (par[P_HIGHACC] == 0.0))) {
             act = false;
@@ -1125,7 +1161,8 @@ __global__ void __launch_bounds__(kBlock) k_it_q(int m, int K, const int *__rest
     const double rho = par[P_RHO];
     const double rhoInv = 1.0 / rho;
     double acc[5] = {0, 0, 0, 0, 0};
-    for (int i = i0; i < m; i += gridDim.x * kBlock) {
+    for (int g = blockIdx.x * kBlock + threadIdx.x; g < mg; g += gridDim.x * kBlock) {
+        const int i = glob[g];
         double v1 = 0.0, v2 = 0.0;
         for (int k = 0; k < K; ++k) {
             const long row = (long)k * m + i;
@@ -1139,7 +1176,7 @@ __global__ void __launch_bounds__(kBlock) k_it_q(int m, int K, const int *__rest
             v1 += a1; v2 += a2;
         }
         v1 *= 2.0;
-        const double bi = i == i0 ? b0 : b[i], ci = i == i0 ? c0 : cvs[i], li = i == i0 ? l0 : lam[i];
+        const double bi = b[i], ci = cvs[i], li = lam[i];
         const double q0 = (bi - ci) + rhoInv * li;
         acc[0] += v2 * v2; acc[1] += v1 * v2; acc[2] += q0 * v2; acc[3] += v1 * v1; acc[4] += q0 * v1;
         double2 *r = reinterpret_cast<double2 *>(rec + 4L * i);
@@ -1152,92 +1189,51 @@ __global__ void __launch_bounds__(kBlock) k_it_q(int m, int K, const int *__rest
     LRS_BLK_END(1);
 }
 
-// S3.  No partials.  ALMupdateVar (lorads_alm.c:826-830), A(RR^T) update (:1351-1353),
-// M1 (ALMSetGrad :45-49) and S = C + A^*(M1) (addObjCoeff + sdpDataWSum).  The
-// first element of each grid-stride loop is loaded before the line search.
-__global__ void __launch_bounds__(kBlock) k_it_update(long NR, int Ptot, const int *__restrict__ slot_ptr,
-                                                      const int *__restrict__ slot_con,
-                                                      const double *__restrict__ slot_a,
-                                                      const double *__restrict__ Craw, const double *__restrict__ rec,
-                                                      double *__restrict__ R, const double *__restrict__ D,
-                                                      const double *__restrict__ par,
-                                                      const double *__restrict__ ctrl_cur,
-                                                      const double *__restrict__ partA, int nblkA,
-                                                      const double *__restrict__ partB, int nblkB,
-                                                      double *__restrict__ ls_cur, double *__restrict__ S) {
-    __shared__ double red[7];
+// B.  Line search (every block, from A's and G's partials), then per row: R_new =
+// R + tau D (written to the other factor buffer; neighbours' rows recomputed), S =
+// C + A^*(M1) per neighbour slot with M1 = -lam - rho b + rho (A(RR^T) + tau q1 +
+// tau^2 q2) from rec (ALMupdateVar lorads_alm.c:826-830, :1351-1353, ALMSetGrad
+// :38-57), G_new = 2 S R_new, A(R_new R_new^T) on the lower slots with the local
+// constraints' values and residual (primalInfeasibility), the L-BFGS pair s = tau D,
+// y = G_new - G_old (setlbfgsHisTwo :842-863) and nine dots.  Partials written (10).
+template <int G, int E>
+__global__ void __launch_bounds__(kRowBlock) k_it_b(
+    int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
+    const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
+    const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0, double *s1, double *y1,
+    double *__restrict__ uRR, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
+    const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double *__restrict__ rec,
+    const int *__restrict__ loc_ptr, const int *__restrict__ loc_con, const double *__restrict__ loc_w,
+    const double *__restrict__ b, double *__restrict__ cvs, const double *__restrict__ par,
+    const double *__restrict__ ctrl, const double *__restrict__ partA, int nblkA, const double *__restrict__ partB,
+    int nblkB, double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off) {
+    __shared__ double red[12];
     __shared__ double ls[LS_N];
-    __shared__ int act;
+    __shared__ double cs[4];
     LRS_TS(2, 0);
     LRS_BLK_BEGIN();
-    if (threadIdx.x == 0) act = ctrl_cur[C_ACT2] != 0.0;
-    // first factor pair and first slot of this thread
-    const long i0 = ((long)blockIdx.x * kBlock + threadIdx.x) * 2;
-    double2 r0 = make_double2(0.0, 0.0), d0 = make_double2(0.0, 0.0);
-    if (i0 < NR) { r0 = *reinterpret_cast<const double2 *>(R + i0); d0 = *reinterpret_cast<const double2 *>(D + i0); }
-    const int s0 = blockIdx.x * kBlock + threadIdx.x;
-    double cr0 = 0.0;
-    int e0 = 0, e1 = 0;
-    if (s0 < Ptot) { cr0 = Craw[s0]; e0 = slot_ptr[s0]; e1 = slot_ptr[s0 + 1]; }
+    if (threadIdx.x == 0) { cs[0] = ctrl[C_ACT2]; cs[1] = ctrl[C_GCUR]; cs[2] = ctrl[C_HEAD]; cs[3] = ctrl[C_RCUR]; }
     __syncthreads();
-    if (!act) return;
-    reduce_partials<2>(partA, nblkA, red);
+    if (cs[0] == 0.0) return;
+    reduce_partials<7, kRowBlock>(partA, nblkA, red);
+    if (nblkB > 0) {
+        reduce_partials<5, kRowBlock>(partB, nblkB, red + 7);
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) red[2 + q] += red[7 + q];
+        }
+        __syncthreads();
+    }
     LRS_TS(2, 1);
-    reduce_partials<5>(partB, nblkB, red + 2);
-    LRS_TS(2, 2);
     if (threadIdx.x < 64) line_search_t<true>(par, red[0], red[1], red + 2, ls);   // wave 0
     __syncthreads();
-    LRS_TS(2, 3);
-    if (blockIdx.x == 0 && threadIdx.x < LS_N) ls_cur[threadIdx.x] = ls[threadIdx.x];
+    LRS_TS(2, 2);
+    if (pblk_off == 0 && blockIdx.x == 0 && threadIdx.x < LS_N) ls_cur[threadIdx.x] = ls[threadIdx.x];
     if (ls[LS_FLAG] != 0.0) return;
     const double tau = ls[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
-    for (long i = i0; i < NR; i += (long)gridDim.x * kBlock * 2) {
-        double2 r = r0, d = d0;
-        if (i != i0) { r = *reinterpret_cast<const double2 *>(R + i); d = *reinterpret_cast<const double2 *>(D + i); }
-        r.x += tau * d.x; r.y += tau * d.y;
-        *reinterpret_cast<double2 *>(R + i) = r;
-    }
-    LRS_TS(2, 4);
-    for (int s = s0; s < Ptot; s += gridDim.x * kBlock) {
-        double v = cr0;
-        int eb = e0, ee = e1;
-        if (s != s0) { v = Craw[s]; eb = slot_ptr[s]; ee = slot_ptr[s + 1]; }
-        for (int e = eb; e < ee; ++e) {
-            const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
-            const double2 ra = r[0], rb = r[1];
-            double cv = ra.x + tau * ra.y;
-            cv = cv + tau2 * rb.x;
-            const double M1 = rb.y + rho * cv;
-            v += M1 * slot_a[e];
-        }
-        S[s] = v;
-    }
-    LRS_TS_END(2, 5);
-    LRS_BLK_END(2);
-}
-
-// S4.  G_new = 2 S R (row-owned), A(RR^T) slots (lower), L-BFGS pair s = tau D,
-// y = G_new - G_old into ring slot `head`, and the nine dots needed by the next
-// direction.  Partials written (9).  (ALMCalGrad :74-87, setlbfgsHisTwo :842-863,
-// primalInfeasibility's LORADSUVt(R,R) lorads_alg_common.c:387)
-template <int G, int E>
-__global__ void __launch_bounds__(kRowBlock) k_it_grad(int n, int ld, long foff, const int *__restrict__ adj_ptr,
-                                                       const int *__restrict__ adj_low,
-                                                       const int *__restrict__ adj_col,
-                                                       const int *__restrict__ adj_slot, const double *__restrict__ S,
-                                                       const double *__restrict__ Rall, const double *__restrict__ Dall,
-                                                       double *G0, double *G1, double *s0, double *y0, double *s1,
-                                                       double *y1, double *__restrict__ uRR,
-                                                       const double *__restrict__ ctrl, const double *__restrict__ ls,
-                                                       int L, double *__restrict__ partC, int pblk_off) {
-    LRS_TS(3, 0);
-    LRS_BLK_BEGIN();
-    if (ctrl[C_ACT2] == 0.0 || ls[LS_FLAG] != 0.0) return;
-    LRS_TS(3, 1);
-    const int gcur = (int)ctrl[C_GCUR];
-    const int h = (int)ctrl[C_HEAD];
-    const double tau = ls[LS_TAU];
-    const double *__restrict__ R = Rall + foff;
+    const int gcur = (int)cs[1], h = (int)cs[2];
+    const double *__restrict__ R = (cs[3] == 0.0 ? Rb0 : Rb1) + foff;
+    double *__restrict__ Rn = (cs[3] == 0.0 ? Rb1 : Rb0) + foff;
     const double *__restrict__ D = Dall + foff;
     double *__restrict__ Gold = (gcur == 0 ? G0 : G1) + foff;
     double *__restrict__ Gnew = (gcur == 0 ? G1 : G0) + foff;
@@ -1249,19 +1245,21 @@ __global__ void __launch_bounds__(kRowBlock) k_it_grad(int n, int ld, long foff,
     const int lane = threadIdx.x & (G - 1);
     const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
     const int ngrp = gridDim.x * kRowBlock / G;
-    // acc: GG, ys, yy, sG, yG, soG, yoG, soy, yoy
-    double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // acc: GG, ys, yy, sG, yG, soG, yoG, soy, yoy, residual
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = grp; i < n; i += ngrp) {
         const long oi = (long)i * ld + lane * E;
-        double ri[E], g[E], go[E], di[E], sov[E], yov[E];
-        // row-local operands first: their loads overlap the neighbour gathers
+        double ri[E], di[E], g[E], go[E], sov[E], yov[E];
         ld_row<E>(R + oi, ri);
-        ld_row<E>(Gold + oi, go);
         ld_row<E>(D + oi, di);
+        ld_row<E>(Gold + oi, go);
         if (two) {
             ld_row<E>(so + oi, sov);
             ld_row<E>(yo + oi, yov);
         }
+#pragma unroll
+        for (int e = 0; e < E; ++e) ri[e] += tau * di[e];
+        st_row<E>(Rn + oi, ri);
 #pragma unroll
         for (int e = 0; e < E; ++e) g[e] = 0.0;
         const int kb = adj_ptr[i], kl = adj_low[i], ke = adj_ptr[i + 1];
@@ -1274,11 +1272,29 @@ __global__ void __launch_bounds__(kRowBlock) k_it_grad(int n, int ld, long foff,
                 jj[u] = adj_col[k];
                 ss[u] = adj_slot[k];
             }
-            double sv[4], rj[4][E];
+            double rj[4][E], dj[4][E], sv[4];
+            int eb[4], ee[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                sv[u] = S[ss[u]];
                 ld_row<E>(R + (long)jj[u] * ld + lane * E, rj[u]);
+                ld_row<E>(D + (long)jj[u] * ld + lane * E, dj[u]);
+                sv[u] = Craw[ss[u]];
+                eb[u] = slot_ptr[ss[u]];
+                ee[u] = slot_ptr[ss[u] + 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                // S[slot] = C + sum_con M1(con) a  (addObjCoeff + sdpDataWSum)
+                for (int e = eb[u]; e < ee[u]; ++e) {
+                    const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
+                    const double2 ra = r[0], rb = r[1];
+                    double cv = ra.x + tau * ra.y;
+                    cv = cv + tau2 * rb.x;
+                    const double M1 = rb.y + rho * cv;
+                    sv[u] += M1 * slot_a[e];
+                }
+#pragma unroll
+                for (int e = 0; e < E; ++e) rj[u][e] += tau * dj[u][e];
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -1292,7 +1308,16 @@ __global__ void __launch_bounds__(kRowBlock) k_it_grad(int n, int ld, long foff,
 #pragma unroll
                     for (int e = 0; e < E; ++e) d += ri[e] * rj[u][e];
                     d = group_sum<G>(d);
-                    if (lane == 0) uRR[ss[u]] = d;
+                    if (lane == 0) {
+                        uRR[ss[u]] = d;
+                        for (int e = loc_ptr[ss[u]]; e < loc_ptr[ss[u] + 1]; ++e) {
+                            const int ci = loc_con[e];
+                            const double tot = loc_w[e] * d;
+                            cvs[ci] = tot;
+                            const double dd = b[ci] - tot;
+                            acc[9] += dd * dd;
+                        }
+                    }
                 }
             }
         }
@@ -1322,10 +1347,10 @@ __global__ void __launch_bounds__(kRowBlock) k_it_grad(int n, int ld, long foff,
             }
         }
     }
-    LRS_TS(3, 2);
-    write_partials<9, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
-    LRS_TS_END(3, 3);
-    LRS_BLK_END(3);
+    LRS_TS(2, 3);
+    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+    LRS_TS_END(2, 4);
+    LRS_BLK_END(2);
 }
 
 // ------------------------------------------------------------------------
@@ -1496,7 +1521,8 @@ static inline int iter_grid(const DevCone &c, int K) {
     return std::min(g, cap);
 }
 
-// One ALM inner iteration = four launches.  Parity selects the control buffers.
+// One ALM inner iteration = two launches (A, B), three with global constraints
+// (A, G, B).  Parity selects the control buffers.
 int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
     const DevProblem &P = *a.P;
     DevWork &W = *a.W;
@@ -1515,48 +1541,48 @@ int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
         return 0;
     };
     if (mark(0)) return -1;
-    // S1: control, A(RR^T) refresh, direction, sym(RD^T) / DD^T
+    // A: control, direction, sym(RD^T) / DD^T, local constraints' q and dots
     int off = 0;
     for (int k = 0; k < P.K; ++k) {
         const DevCone &c = P.cones[k];
         const int grid = iter_grid(c, P.K);
         LRS_LAYOUT_SWITCH(c.G, c.E, {
-            hipLaunchKernelGGL((k_it_dir_sddmm<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
-                               c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.D, W.G[0], W.G[1],
-                               W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, k == 0 ? 1 : 0, P.m, P.K,
-                               P.con_ptr, P.con_slot, P.con_w, W.uvt2, P.b, W.cvs, W.par, ctrl_prev, ctrl_cur,
-                               ls_prev, W.partC, nblk_rows, W.part, off);
+            hipLaunchKernelGGL((k_it_a<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
+                               c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1],
+                               W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,
+                               P.b, W.cvs, W.lam, W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr,
+                               P.con_slot, P.con_w, W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, W.partC,
+                               nblk_rows, W.part, off);
         });
         LRS_CHECK_LAUNCH();
         off += grid;
     }
     if (mark(1)) return -1;
-    // S2: phase-1 test, q1, q2, line-search dots
-    const int gq = std::min(grid_elems(P.m, 1), kMaxPartialBlocks);
-    hipLaunchKernelGGL(k_it_q, dim3(gq), dim3(kBlock), 0, st, P.m, P.K, P.con_ptr, P.con_slot, P.con_w, W.uvt0,
-                       W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.part, nblk_rows, W.rec, W.partB);
-    LRS_CHECK_LAUNCH();
+    // G: phase-1 test and the global constraints' q and dots
+    const int gg = std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
+    if (P.mg > 0) {
+        hipLaunchKernelGGL(k_it_g, dim3(gg), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot,
+                           P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, W.part, nblk_rows,
+                           W.rec, W.partB);
+        LRS_CHECK_LAUNCH();
+    }
     if (mark(2)) return -1;
-    // S3: line search, R update, S = C + A^*(M1)
-    const int gu = std::max(grid_elems(P.NRpad, 2), grid_elems(P.Ptot, 1));
-    hipLaunchKernelGGL(k_it_update, dim3(gu), dim3(kBlock), 0, st, P.NRpad, P.Ptot, P.slot_ptr, P.slot_con,
-                       P.slot_a, P.Craw, W.rec, W.R, W.D, W.par, ctrl_cur, W.part, nblk_rows, W.partB, gq, ls_cur,
-                       W.S);
-    LRS_CHECK_LAUNCH();
-    if (mark(3)) return -1;
-    // S4: gradient, A(RR^T) slots, L-BFGS pair, dots
+    // B: line search, R update, adjoint, gradient, A(RR^T), L-BFGS pair, dots
     off = 0;
     for (int k = 0; k < P.K; ++k) {
         const DevCone &c = P.cones[k];
         const int grid = iter_grid(c, P.K);
         LRS_LAYOUT_SWITCH(c.G, c.E, {
-            hipLaunchKernelGGL((k_it_grad<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr,
-                               c.adj_low, c.adj_col, c.adj_slot, W.S, W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
-                               W.ls[1], W.ly[1], W.uvt2, ctrl_cur, ls_cur, L, W.partC, off);
+            hipLaunchKernelGGL((k_it_b<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr,
+                               c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
+                               W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a, W.rec, P.loc_ptr,
+                               P.loc_con, P.loc_w, P.b, W.cvs, W.par, ctrl_cur, W.part, nblk_rows, W.partB,
+                               P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off);
         });
         LRS_CHECK_LAUNCH();
         off += grid;
     }
+    if (mark(3)) return -1;
     return mark(4);
 }
 

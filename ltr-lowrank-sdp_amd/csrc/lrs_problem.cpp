@@ -281,6 +281,42 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             fp[g]++;
         }
     dp.Z = Z;
+    // Single-slot ("local") constraints: exactly one merged entry over all cones.  Their
+    // A(.) value is one pattern slot, so the row that owns the slot evaluates them inside
+    // the row kernels; every other constraint is "global" (lrs_kernels.hip, split iteration).
+    std::vector<int> nent(m, 0), only_slot(m, -1);
+    std::vector<double> only_w(m, 0.0);
+    for (int k = 0; k < hp.K; ++k)
+        for (int i = 0; i < m; ++i)
+            for (int e = con_ptr[(long)k * m + i]; e < con_ptr[(long)k * m + i + 1]; ++e) {
+                nent[i]++;
+                only_slot[i] = con_slot[e];
+                only_w[i] = con_w[e];
+            }
+    std::vector<int> glob, loc_ptr(Ptot + 1, 0), loc_con;
+    std::vector<double> loc_w;
+    for (int i = 0; i < m; ++i) {
+        if (nent[i] == 1) loc_ptr[only_slot[i] + 1]++;
+        else glob.push_back(i);
+    }
+    for (int t = 0; t < Ptot; ++t) loc_ptr[t + 1] += loc_ptr[t];
+    loc_con.assign(loc_ptr[Ptot], 0);
+    loc_w.assign(loc_ptr[Ptot], 0.0);
+    {
+        std::vector<int> fpl(loc_ptr.begin(), loc_ptr.end() - 1);
+        for (int i = 0; i < m; ++i)
+            if (nent[i] == 1) {
+                const int t = fpl[only_slot[i]]++;
+                loc_con[t] = i;
+                loc_w[t] = only_w[i];
+            }
+    }
+    dp.mg = (int)glob.size();
+    if (glob.empty()) glob.push_back(0);
+    if (loc_con.empty()) { loc_con.push_back(0); loc_w.push_back(0.0); }
+    if (!dput(&dp.glob, glob, err) || !dput(&dp.loc_ptr, loc_ptr, err) || !dput(&dp.loc_con, loc_con, err) ||
+        !dput(&dp.loc_w, loc_w, err))
+        return false;
     if (!dput(&dp.b, hp.b, err) || !dput(&dp.Cw, Cw, err) || !dput(&dp.Craw, Craw, err) ||
         !dput(&dp.con_ptr, con_ptr, err) || !dput(&dp.con_slot, con_slot, err) || !dput(&dp.con_w, con_w, err) ||
         !dput(&dp.slot_ptr, slot_ptr, err) || !dput(&dp.slot_con, slot_con, err) || !dput(&dp.slot_a, slot_a, err))
@@ -303,6 +339,7 @@ void free_problem(DevProblem &dp) {
     auto f = [](void *p) { if (p) (void)hipFree(p); };
     f(dp.b); f(dp.Cw); f(dp.Craw); f(dp.con_ptr); f(dp.con_slot); f(dp.con_w);
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
+    f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); }
     dp = DevProblem();
 }

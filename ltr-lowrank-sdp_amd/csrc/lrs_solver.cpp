@@ -130,7 +130,7 @@ struct lrs_ctx {
     // hipGraph cache of inner-iteration batches (keyed by batch size; the kernels'
     // arguments are the workspace pointers, so a new workspace drops the cache)
     std::map<int, hipGraphExec_t> graphs;
-    bool use_graphs = true;
+    bool use_graphs = false;   // eager launches measured faster than graph replay (LRS_GRAPHS=1)
     // per-stage event profiling (lrs_profile_stages)
     bool prof = false;
     // host-loop statistics (LRS_STATS=1): run_inner calls, batches, iterations, seconds
@@ -166,7 +166,7 @@ static void free_work(lrs_ctx *c) {
     DevWork &W = c->W;
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
-                      W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec};
+                      W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     c->W = DevWork();
@@ -206,7 +206,7 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         A(&W.M1, m) || A(&W.wtmp, m) || A(&W.cvc, (long)m * std::max(1, P.K)) ||
         A(&W.part, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.partB, (long)kMaxPartialVals * kMaxPartialBlocks) ||
         A(&W.partC, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.ctrl, 2 * C_NCTRL) ||
-        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax) || A(&W.rec, 4L * m))
+        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax) || A(&W.rec, 4L * m) || A(&W.R2, NR))
         return -1;
     HIPC(hipStreamSynchronize(c->st));
     c->walloc = true;
@@ -600,7 +600,7 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     par[P_HIGHACC] = p->highAccMode; par[P_BUDGET] = (double)budget; par[P_L] = p->lbfgsListLength; par[P_GAP] = gap;
     double ctl[C_NCTRL] = {0};
     ctl[C_ACTIVE] = 1; ctl[C_EXIT] = EXIT_NONE; ctl[C_INNER] = (double)io.inner; ctl[C_LOCAL] = (double)io.local;
-    ctl[C_ACT2] = 1; ctl[C_EXIT2] = EXIT_NONE; ctl[C_RRDONE] = 0;
+    ctl[C_ACT2] = 1; ctl[C_EXIT2] = EXIT_NONE; ctl[C_RRDONE] = 0; ctl[C_RCUR] = 0;
     ctl[C_CLEAR] = (double)io.clear; ctl[C_HEAD] = c->head; ctl[C_GCUR] = c->gcur; ctl[C_PENDING] = 0;
     ctl[C_RCVAL] = io.rcval; ctl[C_LAG] = io.lag; ctl[C_PINF1] = io.pinf1; ctl[C_PINFINF] = io.pinfinf;
     ctl[C_BETA0] = c->beta[0]; ctl[C_BETA1] = c->beta[1]; ctl[C_YY0] = c->yy[0]; ctl[C_YY1] = c->yy[1];
@@ -654,6 +654,9 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     io.inner = (long)res[C_INNER]; io.local = (long)res[C_LOCAL]; io.clear = (long)res[C_CLEAR];
     io.rcval = res[C_RCVAL]; io.lag = res[C_LAG]; io.pinf1 = res[C_PINF1]; io.pinfinf = res[C_PINFINF];
     io.exitReason = (int)res[C_EXIT2];
+    // the iterate lives in R2 after an odd number of completed iterations
+    if (res[C_RCUR] != 0.0)
+        HIPC(hipMemcpyAsync(c->W.R, c->W.R2, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
     c->head = (int)res[C_HEAD]; c->gcur = (int)res[C_GCUR];
     c->beta[0] = res[C_BETA0]; c->beta[1] = res[C_BETA1]; c->yy[0] = res[C_YY0]; c->yy[1] = res[C_YY1];
     return 0;
@@ -1042,7 +1045,7 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
     c->device = device;
     if (hipSetDevice(device) != hipSuccess) { set_err("hipSetDevice(%d) failed", device); delete c; return -1; }
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); delete c; return -1; }
-    if (const char *ng = getenv("LRS_NO_GRAPHS")) c->use_graphs = (atoi(ng) == 0);
+    if (const char *ug = getenv("LRS_GRAPHS")) c->use_graphs = (atoi(ug) != 0);
     if (const char *sv = getenv("LRS_STATS")) c->stats = (atoi(sv) != 0);
     if (hipHostMalloc((void **)&c->hpin, 4096 * sizeof(double), 0) != hipSuccess) { set_err("pinned alloc failed"); delete c; return -1; }
     *out = c;

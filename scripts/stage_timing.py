@@ -20,8 +20,8 @@ solver.load_library(timing if os.path.exists(timing) else None)
 cache = os.path.join(ROOT, ".bench_instances")
 os.makedirs(cache, exist_ok=True)
 path = bench.instance_for(0, rows, cols, cache)
-for ng in ("0", "1"):
-    os.environ["LRS_NO_GRAPHS"] = ng
+for ng in ("1", "0"):
+    os.environ["LRS_GRAPHS"] = "0" if ng == "1" else "1"
     sv = solver.Solver(path)
     r = rank or sv.determine_rank()[0]
     kw = dict(fixedRank=r, reoptLevel=0)
@@ -29,7 +29,7 @@ for ng in ("0", "1"):
     out = sv.alm_throughput(0, 2000, **kw)
     print(f"graphs={'off' if ng == '1' else 'on'} rank={r}: {out['done'] / out['seconds']:.1f} it/s "
           f"({out['seconds'] * 1e6 / out['done']:.1f} us/it)")
-    for mode in (("throughput", "profile") if ng == "0" else ()):
+    for mode in (("throughput", "profile") if ng == "1" else ()):
         if mode == "profile":
             ms, done = sv.profile_stages(600, **kw)
             print("stage us (events):", [round(x * 1e3, 2) for x in ms], "sum", round(sum(ms) * 1e3, 2),
@@ -38,25 +38,25 @@ for ng in ("0", "1"):
         dbg = sv.debug_phase_times()
         if dbg:
             ph, blk = dbg
-            names = [["entry", "ctrl-load", "reduce9", "ctrl_step", "gather_rr", "rows", "partials"],
+            names = [["entry", "ctrl-load", "reduce10", "ctrl+glob", "start", "rows", "partials"],
                      ["entry", "pinf", "gather_q", "partials"],
-                     ["entry", "reduce2", "reduce5", "linesearch", "R-upd", "wsum"],
-                     ["entry", "guard", "rows", "partials"]]
-            for k in range(4):
+                     ["entry", "reduce", "linesearch", "rows", "partials"]]
+            for k in range(3):
                 t = ph[k]
                 seq = [f"{names[k][p]}:{(t[p] - t[p - 1]) * 0.01:.2f}" for p in range(1, len(names[k]))]
-                print(f"S{k + 1} phases (us):", " ".join(seq))
+                print(f"K{'AGB'[k]} phases (us):", " ".join(seq))
             # per-block spans of the last full iteration (valid blocks: entry != 0)
             spans = []
-            for k in range(4):
+            ks = [k for k in range(3) if any(a != 0 for a, _ in blk[k])]
+            for k in ks:
                 v = [(a, b) for a, b in blk[k] if a != 0 and b >= a]
                 spans.append((min(a for a, _ in v), max(a for a, _ in v), max(b for _, b in v), len(v),
                               sum(b - a for a, b in v) / len(v)))
-            for k in range(4):
-                f, l, e, nb, av = spans[k]
-                line = (f"S{k + 1}: blocks {nb} first-entry->last-entry {(l - f) * 0.01:.2f} us, "
+            for q, k in enumerate(ks):
+                f, l, e, nb, av = spans[q]
+                line = (f"K{'AGB'[k]}: blocks {nb} first-entry->last-entry {(l - f) * 0.01:.2f} us, "
                         f"first-entry->last-exit {(e - f) * 0.01:.2f} us, mean block span {av * 0.01:.2f} us")
-                nxt = spans[(k + 1) % 4][0]
+                nxt = spans[(q + 1) % len(ks)][0]
                 line += f", last-exit->next first-entry {(nxt - e) * 0.01:.2f} us"
                 print(line)
     sv.close()
