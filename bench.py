@@ -10,9 +10,15 @@ the device.  Multi-GPU: one process per GPU, each solving its own instance (the
 reference's instance-level batching, dataset/run_lorads.sh:85-114): weak scaling,
 no data-path collective; barrier + max-over-ranks timing.
 
-Prints one JSON line (rank 0).  Extra fields: wall-clock to eps = 1e-5 (full
-ALM+ADMM solve, Gset flags), the A(UU^T) kernel roofline, and the reference CPU
-path timed on this host (cpu_baseline).
+Prints one JSON line (rank 0).  Besides the contract keys:
+  roofline          dominant split-iteration stage on the workload (HIP-event timed,
+                    algorithmic bytes from lrs_stage_bytes; DESIGN.md "Kernels")
+  roofline_at_scale the same stages on a 2000 x 2000 torus (n = 4e6, r = 16: factors
+                    far beyond the 256 MB Infinity Cache), where HBM bandwidth binds
+  north_star        MaxCut n = 20 000, r = 64 (G81-like): device vs reference CPU it/s
+  wall_clock_to_eps full ALM + ADMM solve to eps = 1e-5 with the Gset flags
+  cpu_baseline      the reference LoRADS C (oracle/_ref, built from /root/reference)
+                    timed on this host, 1 core, on a bounded sample of the workload
 """
 import argparse
 import importlib
@@ -27,14 +33,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 PKG = "ltr-lowrank-sdp_amd"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+STAGES = ("A: k_it_a (control, L-BFGS direction, SDDMM sym(RD^T)/DD^T, local q1/q2)",
+          "G: k_it_g (phase-1 test, multi-slot constraints' q1/q2)",
+          "B: k_it_b (line search, R+tau D, adjoint S=C+A*(M1), G=2SR, A(RR^T), L-BFGS pair)")
 
 
-def instance_for(rank_id, rows, cols, cache):
+def instance_for(rank_id, rows, cols, cache, seed0=67):
     inst = importlib.import_module(PKG + ".instances")
-    path = os.path.join(cache, f"torus{rows}x{cols}_s{67 + rank_id}.dat-s")
+    path = os.path.join(cache, f"torus{rows}x{cols}_s{seed0 + rank_id}.dat-s")
     if not os.path.exists(path):
         tmp = path + f".tmp{os.getpid()}"
-        inst.maxcut_torus(tmp, rows, cols, seed=67 + rank_id)
+        inst.maxcut_torus(tmp, rows, cols, seed=seed0 + rank_id)
         os.replace(tmp, path)
     return path
 
@@ -74,6 +83,24 @@ def cpu_reference_solve(path, flags, timeout):
     return {"solve_time_sec": float(m.group(1)), "process_wall_sec": wall, "alm_pobj": float(p.group(1))}
 
 
+def stage_roofline(sv, reps):
+    """Per-launch ms of the split-iteration stages (back-to-back relaunches between two
+    HIP events on the solver stream) and their algorithmic bytes -> GB/s."""
+    ms = sv.time_stages(reps)
+    by = sv.stage_bytes()
+    out = []
+    for k in range(3):
+        if ms[k] <= 0:
+            continue
+        gbs = by[k] / (ms[k] * 1e-3) / 1e9
+        out.append({"stage": STAGES[k], "avg_launch_us": ms[k] * 1e3, "bytes_per_launch": by[k],
+                    "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS})
+    dom = max(out, key=lambda s: s["avg_launch_us"])
+    return {"bound": "hbm", "kernel": dom["stage"], "achieved": dom["achieved_GBs"], "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": dom["frac"], "traffic": None, "bytes_per_launch": dom["bytes_per_launch"],
+            "avg_launch_us": dom["avg_launch_us"], "stages": out}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +112,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-eps", action="store_true")
+    ap.add_argument("--no-scale", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,21 +125,7 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
-
-    def barrier_sync():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
-            torch.cuda.synchronize()
-
-    def allreduce(v, op):
-        if dist is None:
-            return v
-        import torch
-        t = torch.tensor([float(v)], device=f"cuda:{local}", dtype=torch.float64)
-        dist.all_reduce(t, op=op)
-        return float(t.item())
+    replicas = importlib.import_module(PKG + ".replicas")
 
     solver = importlib.import_module(PKG + ".solver")
     cache = os.path.join(ROOT, ".bench_instances")
@@ -124,22 +139,13 @@ def main():
     # warmup: W untimed inner iterations (same start point as the timed run)
     if args.warmup > 0:
         sv.alm_throughput(0, args.warmup, **kw)
-    barrier_sync()
+    replicas.barrier_sync(dist)
     t0 = time.perf_counter()
     out = sv.alm_throughput(0, args.steps, **kw)
-    barrier_sync()
+    replicas.barrier_sync(dist)
     dt = time.perf_counter() - t0
-    t_max = allreduce(dt, dist.ReduceOp.MAX if dist else None)
     done = out["done"]
-    done_tot = allreduce(done, dist.ReduceOp.SUM if dist else None)
-
-    # A(U U^T) kernel (SDDMM on the pattern + per-constraint gather) on the final iterate,
-    # HIP events on the solver stream; algorithmic bytes (delta = 1):
-    #   8 n r + 16 Z + 4 (m + 1) + 8 m
-    auut_ms = sv.time_auut(200)
-    m, Z = sv.m, sv.nnz
-    bytes_a = 8.0 * n * r + 16.0 * Z + 4.0 * (m + 1) + 8.0 * m
-    achieved = bytes_a / (auut_ms * 1e-3) / 1e9
+    done_tot, t_max = replicas.aggregate(dist, done, dt)
 
     line = {
         "metric": "ALM iters/sec, MaxCut G67 (torus 100x100 +-1, n=m=10000), fixed default rank",
@@ -154,13 +160,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: seeded G67-structured toroidal grid (real Gset file absent), one instance per rank",
-        "config": {"workload": f"MaxCut torus {args.rows}x{args.cols} (G67 structure)", "n": n, "m": m,
-                   "rank": r, "pattern_slots": sv.nslots, "constraint_nnz": Z,
+        "config": {"workload": f"MaxCut torus {args.rows}x{args.cols} (G67 structure)", "n": n, "m": sv.m,
+                   "rank": r, "pattern_slots": sv.nslots, "constraint_nnz": sv.nnz,
                    "flags": "--fixedRank %d --reoptLevel 0, phase-1 exit disabled, budget = steps" % r,
                    "parallelism": f"replicas x{world} (instance-level, weak)"},
-        "roofline": {"bound": "hbm", "kernel": "A(UU^T): k_sddmm<XX^T> + k_gather", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "bytes_per_launch": bytes_a, "avg_launch_us": auut_ms * 1e3},
+        "alm_phase_rate": done / out["seconds"],
+        "roofline": stage_roofline(sv, 300),
     }
     if rank_id == 0 and world == 1 and not args.no_eps:
         eps_flags = dict(reoptLevel=0, heuristicFactor=10.0, phase1Tol=1e-2, phase2Tol=1e-5)
@@ -172,6 +177,7 @@ def main():
                                      "alm_inner": sol["alm_inner"], "admm_iter": sol["admm_iter"],
                                      "primal_obj": sol["pobj"], "alm_primal_obj": sol["alm_pobj"],
                                      "pinf": sol["pinf"], "gap": sol["gap"], "rank": sol["final_rank"]}
+    sv.close()
     if rank_id == 0 and world == 1 and not args.no_cpu:
         it, sec, kind = cpu_reference_rate(path, r, args.cpu_seconds)
         line["cpu_baseline"] = {"value": it / sec, "unit": "ALM inner iterations/s", "cores": 1, "kind": kind,
@@ -182,7 +188,36 @@ def main():
                                       timeout=600)
             if ref:
                 line["cpu_baseline"]["wall_clock_to_eps"] = ref
-    sv.close()
+    if rank_id == 0 and world == 1 and not args.no_north_star:
+        # BASELINE.json target: >= 10x CPU LoRADS it/s on MaxCut n = 20 000, rank 64, 1 GPU
+        p81 = instance_for(0, 100, 200, cache, seed0=81)
+        s81 = solver.Solver(p81, device=local)
+        kw81 = dict(fixedRank=64, reoptLevel=0)
+        s81.alm_throughput(0, 100, **kw81)
+        o81 = s81.alm_throughput(0, 1000, **kw81)
+        ns = {"workload": "MaxCut torus 100x200 (G81 structure), n=m=20000, --fixedRank 64",
+              "gpu_it_s": o81["done"] / o81["seconds"], "roofline": stage_roofline(s81, 100)}
+        s81.close()
+        if not args.no_cpu:
+            it, sec, kind = cpu_reference_rate(p81, 64, min(args.cpu_seconds, 10.0))
+            ns["cpu_it_s"] = it / sec
+            ns["cpu_kind"] = kind
+            ns["speedup"] = ns["gpu_it_s"] / ns["cpu_it_s"]
+        line["north_star"] = ns
+    if rank_id == 0 and world == 1 and not args.no_scale:
+        # roofline at scale: 2000 x 2000 torus built in memory (lrs_load_coo), rank 16
+        inst = importlib.import_module(PKG + ".instances")
+        t1 = time.perf_counter()
+        big = solver.Solver(coo=inst.coo_arrays(inst.maxcut_torus_problem(2000, 2000, 2000)), device=local)
+        load_s = time.perf_counter() - t1
+        kwb = dict(fixedRank=16, reoptLevel=0)
+        ob = big.alm_throughput(0, 60, **kwb)
+        rl = stage_roofline(big, 20)
+        rl["workload"] = "MaxCut torus 2000x2000 (n=m=4e6), --fixedRank 16, in-memory load"
+        rl["it_s"] = ob["done"] / ob["seconds"]
+        rl["load_sec"] = load_s
+        big.close()
+        line["roofline_at_scale"] = rl
     if rank_id == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

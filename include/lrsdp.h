@@ -134,6 +134,23 @@ int lrs_time_auut(lrs_ctx *ctx, int reps, double *avg_ms);
  * adjoint, S4 gradient).  stage_ms[4] = average ms per launch; *done = iterations. */
 int lrs_profile_stages(lrs_ctx *ctx, const lrs_params *p, long steps, double *stage_ms, long *done);
 
+/* In-memory problem in SDPA entry semantics (replaces LReadSDPA for callers that
+ * already hold the data, io/lorads_file_io.c:59-455): nblk blocks of sizes dims
+ * (last may be negative = LP, unsupported), b[m], and nnz entries (con, blk, row,
+ * col, val) with 1-based blk/row/col and con 0 = F0 (C = -F0). */
+int lrs_load_coo(lrs_ctx *ctx, int m, int nblk, const int *dims, const double *b, long nnz, const int *con,
+                 const int *blk, const int *row, const int *col, const double *val);
+
+/* Algorithmic HBM bytes per launch of the split-iteration stages A, G, B at the
+ * current ranks (the roofline numerators, DESIGN.md "Kernels"). */
+int lrs_stage_bytes(lrs_ctx *ctx, double *bytes);
+
+/* Per-launch duration (ms) of the split-iteration stages A, G, B on the current solver
+ * state (call after lrs_alm_throughput): each stage is relaunched `reps` times back to
+ * back between two HIP events on the solver stream (the stages are idempotent for a
+ * fixed control block).  stage_ms[1] = 0 when there are no multi-slot constraints. */
+int lrs_time_stages(lrs_ctx *ctx, int reps, double *stage_ms);
+
 /* Diagnostics: in-kernel phase timestamps of the last split iteration (block 0,
  * 100 MHz wall clock), out[4][16], and (blk, optional) per-block entry/exit stamps
  * blk[4][1024][2].  Returns 64 from the diagnostics build (liblrsdp_timing.so), 0

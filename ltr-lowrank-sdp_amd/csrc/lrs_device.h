@@ -169,6 +169,8 @@ struct AlmIterArgs {
 };
 // Four launches per inner iteration (lrs_kernels.hip "split iteration").
 int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st);
+// a subset of the stages (mask bit 0 = A, 1 = G, 2 = B), for per-stage timing
+int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t st);
 
 const char *last_device_error();
 // diagnostics build only: copies g_phase[4][16] (returns 64), else returns 0

@@ -1524,6 +1524,10 @@ static inline int iter_grid(const DevCone &c, int K) {
 // One ALM inner iteration = two launches (A, B), three with global constraints
 // (A, G, B).  Parity selects the control buffers.
 int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
+    return enqueue_alm_stages(a, parity, 7, st);
+}
+
+int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t st) {
     const DevProblem &P = *a.P;
     DevWork &W = *a.W;
     double *ctrl_prev = W.ctrl + (parity ^ 1) * C_NCTRL;
@@ -1543,7 +1547,7 @@ int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
     if (mark(0)) return -1;
     // A: control, direction, sym(RD^T) / DD^T, local constraints' q and dots
     int off = 0;
-    for (int k = 0; k < P.K; ++k) {
+    for (int k = 0; k < P.K && (mask & 1); ++k) {
         const DevCone &c = P.cones[k];
         const int grid = iter_grid(c, P.K);
         LRS_LAYOUT_SWITCH(c.G, c.E, {
@@ -1560,7 +1564,7 @@ int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
     if (mark(1)) return -1;
     // G: phase-1 test and the global constraints' q and dots
     const int gg = std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
-    if (P.mg > 0) {
+    if (P.mg > 0 && (mask & 2)) {
         hipLaunchKernelGGL(k_it_g, dim3(gg), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot,
                            P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, W.part, nblk_rows,
                            W.rec, W.partB);
@@ -1569,7 +1573,7 @@ int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
     if (mark(2)) return -1;
     // B: line search, R update, adjoint, gradient, A(RR^T), L-BFGS pair, dots
     off = 0;
-    for (int k = 0; k < P.K; ++k) {
+    for (int k = 0; k < P.K && (mask & 4); ++k) {
         const DevCone &c = P.cones[k];
         const int grid = iter_grid(c, P.K);
         LRS_LAYOUT_SWITCH(c.G, c.E, {

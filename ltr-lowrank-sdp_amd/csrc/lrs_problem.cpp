@@ -33,6 +33,9 @@ bool is_sep(char c) {
 
 }  // namespace
 
+static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, bool lpEntries,
+                          std::vector<RawEntry> &raw, HostProblem &hp, std::string &err);
+
 bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err) {
     FILE *f = fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
@@ -104,6 +107,11 @@ bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err) {
         if (ic == 0) v = -v;                                // :317-319 (C = -F0)
         raw.push_back({ib, ic, ij, ii, v});
     }
+    return build_problem(m, K, dims, nLp, lpEntries, raw, hp, err);
+}
+
+static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, bool lpEntries,
+                          std::vector<RawEntry> &raw, HostProblem &hp, std::string &err) {
     if (nLp > 0 || lpEntries) {
         err = "LP blocks are not supported by the device path yet (SURVEY.md §2, out of scope)";
         return false;
@@ -217,6 +225,34 @@ bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err) {
     for (auto &c : hp.cones) { c1 += c.cNrm1; c2 += c.cNrm2sq; ci = std::max(ci, c.cNrmInf); }
     hp.cNrm1 = c1; hp.cNrm2 = std::pow(c2, 0.5); hp.cNrmInf = ci;
     return true;
+}
+
+
+bool build_problem_coo(int m, int nblk, const int *dims_in, const double *b, long nnz, const int *con,
+                       const int *blk, const int *row, const int *col, const double *val, HostProblem &hp,
+                       std::string &err) {
+    // same entry semantics as the file reader (1-based blocks/rows/cols, con 0 = F0)
+    std::vector<int> dims(dims_in, dims_in + nblk);
+    for (int k = 0; k < nblk - 1; ++k)
+        if (dims[k] <= 0) { err = "only the last block may be an LP block"; return false; }
+    int K = nblk, nLp = 0;
+    if (nblk > 0 && dims[nblk - 1] < 0) { nLp = -dims[nblk - 1]; K = nblk - 1; }
+    hp.b.assign(b, b + m);
+    std::vector<RawEntry> raw;
+    raw.reserve(nnz);
+    bool lpEntries = false;
+    for (long t = 0; t < nnz; ++t) {
+        int ic = con[t], ib = blk[t] - 1, ii = row[t] - 1, ij = col[t] - 1;
+        double v = val[t];
+        if (std::fabs(v) < 1e-12) continue;
+        if (ib == K && nLp > 0) { lpEntries = true; continue; }
+        if (ib < 0 || ib >= K || ic < 0 || ic > m) { err = "entry out of range"; return false; }
+        if (ii > ij) std::swap(ii, ij);
+        if (ii < 0 || ij >= dims[ib]) { err = "entry index out of block"; return false; }
+        if (ic == 0) v = -v;
+        raw.push_back({ib, ic, ij, ii, v});
+    }
+    return build_problem(m, K, dims, nLp, lpEntries, raw, hp, err);
 }
 
 template <typename T>

@@ -40,6 +40,11 @@ struct HostProblem {
 // (C = -F0, |v| < 1e-12 dropped, (i,j) swapped into the lower triangle).
 bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err);
 
+// Same presolve from in-memory SDPA-style entries (1-based block/row/col, con 0 = F0).
+bool build_problem_coo(int m, int nblk, const int *dims, const double *b, long nnz, const int *con,
+                       const int *blk, const int *row, const int *col, const double *val, HostProblem &hp,
+                       std::string &err);
+
 // Device upload of everything that does not depend on the rank.
 bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err);
 void free_problem(DevProblem &dp);

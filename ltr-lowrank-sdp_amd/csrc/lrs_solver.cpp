@@ -1087,6 +1087,50 @@ int lrs_load_sdpa(lrs_ctx *c, const char *path, double *read_seconds) {
     return 0;
 }
 
+int lrs_load_coo(lrs_ctx *c, int m, int nblk, const int *dims, const double *b, long nnz, const int *con,
+                 const int *blk, const int *row, const int *col, const double *val) {
+    if (!c) { set_err("null ctx"); return -1; }
+    std::string err;
+    HostProblem hp;
+    if (!build_problem_coo(m, nblk, dims, b, nnz, con, blk, row, col, val, hp, err)) {
+        set_err("load_coo: %s", err.c_str());
+        return -1;
+    }
+    free_work(c);
+    if (c->loaded) free_problem(c->dp);
+    c->hp = std::move(hp);
+    if (!upload_problem(c->hp, c->dp, err)) { set_err("upload: %s", err.c_str()); return -1; }
+    c->loaded = true;
+    c->path = "<memory>";
+    c->cgIterCone.assign(c->hp.K, 0);
+    return 0;
+}
+
+int lrs_stage_bytes(lrs_ctx *c, double *bytes) {
+    // Algorithmic HBM bytes per launch of the split-iteration stages:
+    // every array the stage must touch, once, at its unpadded size; L-BFGS with two
+    // pairs; int32 indices, FP64 values.  n, r per cone; P lower slots; adjacency
+    // entries A = 2P - n_diag; Z constraint entries; m constraints (m_l local).
+    if (!c || !c->loaded || !c->walloc) { set_err("no solver state"); return -1; }
+    double a = 0, g = 0, bb = 0;
+    const DevProblem &P = c->dp;
+    for (int k = 0; k < P.K; ++k) {
+        const HostCone &hc = c->hp.cones[k];
+        const double n = hc.n, r = c->rank[k], Pk = (double)hc.prow.size(), A = (double)hc.adj_col.size();
+        const double nr8 = 8.0 * n * r;
+        a += 7 * nr8 + 8 * (n + 1) + 8 * Pk /*lower adj col+slot*/ + 8 * Pk /*Cw*/ + 16 * Pk /*uRD,uDD*/ + 4 * (Pk + 1);
+        bb += 9 * nr8 + 8 * (n + 1) + 8 * A /*adj col+slot*/ + 8 * Pk /*Craw*/ + 4 * (Pk + 1) /*slot_ptr*/ +
+              8 * Pk /*uRR*/ + 4 * (Pk + 1) /*loc_ptr*/;
+    }
+    const double m = P.m, ml = P.m - P.mg, Z = (double)P.Z;
+    a += 12 * ml /*loc con,w*/ + 24 * ml /*b,cvs,lam*/ + 32 * ml /*rec*/;
+    g = P.mg > 0 ? (12.0 * Z + 4.0 * (P.K * m + 1) + 16.0 * 2 * Z /*uRD,uDD gathers*/ + 24.0 * P.mg + 32.0 * P.mg +
+                    4.0 * P.mg) : 0.0;
+    bb += 12 * Z /*slot_con,a*/ + 32 * m /*rec*/ + 12 * ml /*loc con,w*/ + 16 * ml /*b read, cvs write*/;
+    bytes[0] = a; bytes[1] = g; bytes[2] = bb;
+    return 0;
+}
+
 int lrs_problem_info(lrs_ctx *c, int *m, int *ncones, int *dims, long *nslots, long *nnzc) {
     if (!c->loaded) { set_err("no problem loaded"); return -1; }
     if (m) *m = c->hp.m;
@@ -1440,6 +1484,46 @@ int lrs_profile_stages(lrs_ctx *c, const lrs_params *pin, long steps, double *st
     if (rc) return -1;
     for (int q = 0; q < 4; ++q) stage_ms[q] = c->pn ? c->pacc[q] / c->pn : 0.0;
     if (done) *done = r.alm_inner;
+    return 0;
+}
+
+int lrs_time_stages(lrs_ctx *c, int reps, double *stage_ms) {
+    // Per-launch durations of the split-iteration stages on the current state: each
+    // stage is launched `reps` times back to back between two HIP events on the solver
+    // stream.  The stages are idempotent for a fixed control block (A reads ctrl[1] and
+    // writes ctrl[0]; G and B read ctrl[0]), so the repeats redo identical work.  The
+    // control is set active with every exit test disabled.
+    if (!c || !c->loaded || !c->walloc) { set_err("no solver state"); return -1; }
+    double *h = c->hpin;
+    HIPC(hipMemcpyAsync(h, c->W.ctrl, sizeof(double) * 2 * C_NCTRL, hipMemcpyDeviceToHost, c->st));
+    HIPC(hipMemcpyAsync(h + 2 * C_NCTRL, c->W.par, sizeof(double) * P_NPAR, hipMemcpyDeviceToHost, c->st));
+    HIPC(hipStreamSynchronize(c->st));
+    double *ctl = h + C_NCTRL, *par = h + 2 * C_NCTRL;
+    // previous control = the last one written; A folds it and continues
+    for (int q = 0; q < C_NCTRL; ++q) ctl[q] = h[q];
+    ctl[C_ACT2] = 1; ctl[C_EXIT2] = EXIT_NONE; ctl[C_ACTIVE] = 1; ctl[C_EXIT] = EXIT_NONE;
+    if (ctl[C_PENDING] == 0) ctl[C_PENDING] = 1;
+    par[P_BUDGET] = 0; par[P_RCTOL] = -1e300; par[P_PH1TOL] = -1; par[P_ENDTAU] = 0;
+    HIPC(hipMemcpyAsync(c->W.ctrl + C_NCTRL, ctl, sizeof(double) * C_NCTRL, hipMemcpyHostToDevice, c->st));
+    HIPC(hipMemcpyAsync(c->W.par, par, sizeof(double) * P_NPAR, hipMemcpyHostToDevice, c->st));
+    double zero[LS_N] = {0, 0, 0, 0};
+    HIPC(hipMemcpyAsync(c->W.lsres + LS_N, zero, sizeof(zero), hipMemcpyHostToDevice, c->st));
+    AlmIterArgs a{&c->dp, &c->W, nullptr};
+    // one full iteration first so that every buffer the stages read is populated
+    OPC(enqueue_alm_stages(a, 0, 7, c->st));
+    hipEvent_t e[4];
+    for (auto &x : e) HIPC(hipEventCreate(&x));
+    const int masks[3] = {1, 2, 4};
+    for (int q = 0; q < 3; ++q) {
+        HIPC(hipEventRecord(e[0], c->st));
+        for (int t = 0; t < reps; ++t) OPC(enqueue_alm_stages(a, 0, masks[q], c->st));
+        HIPC(hipEventRecord(e[1], c->st));
+        HIPC(hipEventSynchronize(e[1]));
+        float ms = 0;
+        HIPC(hipEventElapsedTime(&ms, e[0], e[1]));
+        stage_ms[q] = (q == 1 && c->dp.mg == 0) ? 0.0 : ms / reps;
+    }
+    for (auto &x : e) (void)hipEventDestroy(x);
     return 0;
 }
 

@@ -22,6 +22,8 @@ import numpy as np
 __all__ = [
     "maxcut_random",
     "maxcut_torus",
+    "maxcut_torus_problem",
+    "coo_arrays",
     "theta",
     "theta_multiblock",
     "random_sparse",
@@ -49,8 +51,25 @@ def write_sdpa(path, m, dims, b, entries):
     return path
 
 
-def _maxcut_from_edges(path, n, ei, ej, w):
-    """MaxCut SDP from an edge list (0-based, i != j)."""
+def coo_arrays(problem):
+    """(m, dims, b, entries) -> dict of flat arrays for Solver(coo=...) / lrs_load_coo."""
+    m, dims, b, entries = problem
+    con, blk, row, col, val = [], [], [], [], []
+    for c, bk, ii, jj, vv in entries:
+        c = np.asarray(c, dtype=np.int32)
+        con.append(c)
+        blk.append(np.broadcast_to(np.asarray(bk, dtype=np.int32), c.shape))
+        row.append(np.asarray(ii, dtype=np.int32))
+        col.append(np.asarray(jj, dtype=np.int32))
+        val.append(np.asarray(vv, dtype=np.float64))
+    cat = lambda xs, t: np.ascontiguousarray(np.concatenate(xs).astype(t))
+    return dict(m=int(m), dims=np.asarray(dims, dtype=np.int32), b=np.asarray(b, dtype=np.float64),
+                con=cat(con, np.int32), blk=cat(blk, np.int32), row=cat(row, np.int32), col=cat(col, np.int32),
+                val=cat(val, np.float64))
+
+
+def _maxcut_problem(n, ei, ej, w):
+    """MaxCut SDP (m, dims, b, entries) from an edge list (0-based, i != j)."""
     lo = np.minimum(ei, ej)
     hi = np.maximum(ei, ej)
     deg = np.zeros(n)
@@ -66,7 +85,11 @@ def _maxcut_from_edges(path, n, ei, ej, w):
         (np.zeros(int(keep.sum()), dtype=np.int64), 1, obj_i[keep], obj_j[keep], obj_v[keep]),
         (con_i, 1, con_i, con_i, np.ones(n)),
     ]
-    return write_sdpa(path, n, [n], np.ones(n), entries)
+    return n, [n], np.ones(n), entries
+
+
+def _maxcut_from_edges(path, n, ei, ej, w):
+    return write_sdpa(path, *_maxcut_problem(n, ei, ej, w))
 
 
 def maxcut_random(path, n, n_edges, seed, weights="one"):
@@ -83,6 +106,11 @@ def maxcut_random(path, n, n_edges, seed, weights="one"):
 
 def maxcut_torus(path, rows, cols, seed):
     """G67/G81-like: 2-D toroidal grid rows x cols, weights uniform in {-1, +1}."""
+    return write_sdpa(path, *maxcut_torus_problem(rows, cols, seed))
+
+
+def maxcut_torus_problem(rows, cols, seed):
+    """The maxcut_torus instance in memory: (m, dims, b, entries)."""
     rng = np.random.default_rng(seed)
     n = rows * cols
     idx = np.arange(n).reshape(rows, cols)
@@ -91,7 +119,7 @@ def maxcut_torus(path, rows, cols, seed):
     ei = np.concatenate([idx.ravel(), idx.ravel()])
     ej = np.concatenate([right.ravel(), down.ravel()])
     w = rng.choice([-1.0, 1.0], size=ei.size)
-    return _maxcut_from_edges(path, n, ei, ej, w)
+    return _maxcut_problem(n, ei, ej, w)
 
 
 def _theta_entries(n, ei, ej, blk, con0):

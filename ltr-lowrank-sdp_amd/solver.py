@@ -105,6 +105,9 @@ def load_library(path=None):
         "lrs_set_log_path": (C.c_int, [vp, C.c_char_p]),
         "lrs_time_auut": (C.c_int, [vp, C.c_int, dp]),
         "lrs_profile_stages": (C.c_int, [vp, C.POINTER(Params), C.c_long, dp, C.POINTER(C.c_long)]),
+        "lrs_time_stages": (C.c_int, [vp, C.c_int, dp]),
+        "lrs_stage_bytes": (C.c_int, [vp, dp]),
+        "lrs_load_coo": (C.c_int, [vp, C.c_int, C.c_int, ip, dp, C.c_long, ip, ip, ip, ip, dp]),
         "lrs_debug_phase_times": (C.c_int, [vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
     }
     for name, (res, args) in sig.items():
@@ -139,12 +142,24 @@ def _dptr(a):
 class Solver:
     """One device context with a loaded SDPA problem."""
 
-    def __init__(self, path, device=0):
+    def __init__(self, path=None, device=0, coo=None):
+        """path: SDPA .dat-s file; or coo: dict from instances.coo_arrays (lrs_load_coo)."""
         self.lib = load_library()
         self.ctx = C.c_void_p()
         self._check(self.lib.lrs_ctx_create(device, C.byref(self.ctx)), "ctx_create")
         t = C.c_double()
-        self._check(self.lib.lrs_load_sdpa(self.ctx, str(path).encode(), C.byref(t)), "load_sdpa")
+        if coo is not None:
+            import time as _time
+            t0 = _time.perf_counter()
+            a = {k: coo[k] for k in ("dims", "b", "con", "blk", "row", "col", "val")}
+            ip_ = lambda x: x.ctypes.data_as(C.POINTER(C.c_int))
+            dp_ = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))
+            self._check(self.lib.lrs_load_coo(self.ctx, int(coo["m"]), len(a["dims"]), ip_(a["dims"]), dp_(a["b"]),
+                                              len(a["con"]), ip_(a["con"]), ip_(a["blk"]), ip_(a["row"]),
+                                              ip_(a["col"]), dp_(a["val"])), "load_coo")
+            t.value = _time.perf_counter() - t0
+        else:
+            self._check(self.lib.lrs_load_sdpa(self.ctx, str(path).encode(), C.byref(t)), "load_sdpa")
         self.read_time = t.value
         m, k = C.c_int(), C.c_int()
         self._check(self.lib.lrs_problem_info(self.ctx, C.byref(m), C.byref(k), None, None, None), "info")
@@ -273,6 +288,18 @@ class Solver:
         done = C.c_long()
         self._check(self.lib.lrs_profile_stages(self.ctx, C.byref(p), steps, ms, C.byref(done)), "profile_stages")
         return list(ms), done.value
+
+    def stage_bytes(self):
+        """Algorithmic bytes per launch of the stages [A, G, B] at the current ranks."""
+        v = (C.c_double * 3)()
+        self._check(self.lib.lrs_stage_bytes(self.ctx, v), "stage_bytes")
+        return list(v)
+
+    def time_stages(self, reps=200):
+        """Per-launch ms of the split-iteration stages [A, G, B] (back-to-back relaunches)."""
+        ms = (C.c_double * 3)()
+        self._check(self.lib.lrs_time_stages(self.ctx, reps, ms), "time_stages")
+        return list(ms)
 
     def debug_phase_times(self):
         """In-kernel timestamps (diagnostics library only): ([4][16] block-0 phase ticks,

@@ -111,3 +111,26 @@ def test_device_deterministic(solver_mod):
     a = solver_mod.Solver(instance("mc_torus12x10")).solve(reoptLevel=0)
     b = solver_mod.Solver(instance("mc_torus12x10")).solve(reoptLevel=0)
     assert a["alm_inner"] == b["alm_inner"] and a["pobj"] == b["pobj"]
+
+
+@pytest.mark.gpu
+def test_coo_load_matches_file(solver_mod):
+    inst = importlib.import_module("ltr-lowrank-sdp_amd.instances")
+    a = solver_mod.Solver(instance("mc_torus12x10"))
+    b = solver_mod.Solver(coo=inst.coo_arrays(inst.maxcut_torus_problem(12, 10, 5)))
+    assert (a.m, a.dims, a.nslots, a.nnz) == (b.m, b.dims, b.nslots, b.nnz)
+    ra, rb = a.solve(reoptLevel=0), b.solve(reoptLevel=0)
+    assert ra["alm_inner"] == rb["alm_inner"] and ra["pobj"] == rb["pobj"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mc_rand200", "theta25x3"])
+def test_stage_timing(solver_mod, name):
+    sv = solver_mod.Solver(instance(name))
+    r = sv.determine_rank()[0]
+    out = sv.alm_throughput(0, 50, fixedRank=r, reoptLevel=0)
+    assert out["done"] == 50
+    ms = sv.time_stages(5)
+    by = sv.stage_bytes()
+    assert ms[0] > 0 and ms[2] > 0 and by[0] > 0 and by[2] > 0
+    assert (ms[1] > 0) == (name.startswith("theta"))   # theta has the multi-slot trace constraint
