@@ -24,9 +24,8 @@
 namespace lrs {
 
 constexpr int kBlock = 256;          // threads per block (4 waves)
-constexpr int kMaxPartialBlocks = 1024;
+constexpr int kMaxPartialBlocks = 4096;
 constexpr int kMaxPartialVals = 16;
-constexpr int kIterMaxBlocks = 512;   // row-kernel grid cap of the split iteration
 
 // ---- ALM inner-loop control block (double array, double-buffered by iteration parity)
 enum CtrlIdx {

@@ -744,42 +744,6 @@ __device__ __forceinline__ void write_partials(double (&acc)[NV], double *__rest
     }
 }
 
-// Partial loads of the consumer side, split from the reduction so that they are
-// issued together with other independent loads (every thread: kMaxPartialBlocks/NT
-// loads per value, all in flight at once).  Summation order = reduce_partials'.
-template <int NV, int NT>
-struct PartialLoad {
-    static constexpr int NL = kMaxPartialBlocks / NT;
-    double a[NV];
-    __device__ __forceinline__ void load(const double *__restrict__ part, int nblk) {
-        double x[NV][NL];
-#pragma unroll
-        for (int v = 0; v < NV; ++v)
-#pragma unroll
-            for (int l = 0; l < NL; ++l) {
-                const int b = threadIdx.x + l * NT;
-                x[v][l] = b < nblk ? part[v * kMaxPartialBlocks + b] : 0.0;
-            }
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            double t = 0.0;
-#pragma unroll
-            for (int l = 0; l < NL; ++l) t += x[v][l];
-            a[v] = t;
-        }
-    }
-    // all threads; out (shared) receives the NV sums, visible to the block on return
-    __device__ __forceinline__ void reduce(double *out) {
-        double s[NV];
-        block_reduce<NV, NT>(a, s);
-        if (threadIdx.x == 0) {
-#pragma unroll
-            for (int v = 0; v < NV; ++v) out[v] = s[v];
-        }
-        __syncthreads();
-    }
-};
-
 // all threads; generic nblk
 template <int NV, int NT = kBlock>
 __device__ __forceinline__ void reduce_partials(const double *__restrict__ part, int nblk, double *out) {
@@ -834,13 +798,12 @@ __device__ void line_search_v(const double *__restrict__ par, double p1, double 
 }
 
 // Control of one split iteration (thread 0).  c: shared copy of the previous control,
-// updated in place; the arithmetic runs on a register copy (constant indices only).
+// updated in place.
 // d = the nine dots of the previous gradient stage when `fold`.
-__device__ void ctrl_step(double *csh, const double *__restrict__ par, double lsflag, double lstau, int fold,
+__device__ void ctrl_step(double *c, const double *__restrict__ par, double lsflag, double lstau, int fold,
                           const double *d, bool ph1) {
-    double c[C_NCTRL];
-#pragma unroll
-    for (int q = 0; q < C_NCTRL; ++q) c[q] = csh[q];
+    // in place on the shared copy: a register copy of the block would set the VGPR
+    // peak (and so the occupancy) of the whole row kernel
     const int L = (int)par[P_L];
     const double cninf = par[P_CNINF], rctol = par[P_RCTOL], endsub = par[P_ENDSUB], budget = par[P_BUDGET];
     c[C_ACTIVE] = c[C_ACT2];
@@ -937,8 +900,6 @@ __device__ void ctrl_step(double *csh, const double *__restrict__ par, double ls
         c[C_PENDING] = 1.0;
     }
     if (ph1) { c[C_ACT2] = c[C_ACTIVE]; c[C_EXIT2] = c[C_EXIT]; }
-#pragma unroll
-    for (int q = 0; q < C_NCTRL; ++q) csh[q] = c[q];
 }
 
 struct DirCoef {
@@ -981,7 +942,7 @@ constexpr int kRowBlock = 512;   // threads per block of the row kernels S1 / S4
 //
 // A.  Partials written (8): objective part of <C, sym RD^T>, of <C, DD^T>, the five
 //     line-search dots over the local constraints, residual of the global ones.
-template <int G, int E>
+template <int G, int E, int U>
 __global__ void __launch_bounds__(kRowBlock) k_it_a(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
@@ -1058,47 +1019,47 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
                 dr.eval(kc, yi);
             }
             st_row<E>(D + oi, yi);
-            // lower entries two at a time: both neighbours' operand loads in flight together
-            for (int k0 = kb; k0 < ke; k0 += 2) {
-                const int kA = k0, kB = min(k0 + 1, ke - 1);
-                const int jA = adj_col[kA], jB = adj_col[kB];
-                const int sA = adj_slot[kA], sB = adj_slot[kB];
-                const long oA = (long)jA * ld + lane * E, oB = (long)jB * ld + lane * E;
-                double xA[E], xB[E];
-                DirRow<E> dA, dB;
-                ld_row<E>(R + oA, xA);
-                ld_row<E>(R + oB, xB);
-                dA.load(kc, Gc, s0, y0, s1, y1, oA);
-                dB.load(kc, Gc, s0, y0, s1, y1, oB);
-                const double cwA = Cw[sA], cwB = Cw[sB];
-                double yA[E], yB[E];
-                dA.eval(kc, yA);
-                dB.eval(kc, yB);
+            // lower entries U at a time: the neighbours' operand loads in flight together
+            // (indices clamped to the row; the extra lanes' results are not stored)
+            for (int k0 = kb; k0 < ke; k0 += U) {
+                int jj[U], ss[U];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int j = u ? jB : jA;
-                    const double(&xj)[E] = u ? xB : xA;
-                    const double(&yj)[E] = u ? yB : yA;
+                for (int u = 0; u < U; ++u) {
+                    const int k = min(k0 + u, ke - 1);
+                    jj[u] = adj_col[k];
+                    ss[u] = adj_slot[k];
+                }
+                double xj[U][E], yj[U][E], cw[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const long oj = (long)jj[u] * ld + lane * E;
+                    DirRow<E> dj;
+                    ld_row<E>(R + oj, xj[u]);
+                    dj.load(kc, Gc, s0, y0, s1, y1, oj);
+                    cw[u] = Cw[ss[u]];
+                    dj.eval(kc, yj[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
                     double d0 = 0.0, d1 = 0.0;
-                    if (j != i) {
+                    if (jj[u] != i) {
 #pragma unroll
-                        for (int e = 0; e < E; ++e) d0 += xi[e] * yj[e] + xj[e] * yi[e];
+                        for (int e = 0; e < E; ++e) d0 += xi[e] * yj[u][e] + xj[u][e] * yi[e];
                         d0 *= 0.5;
                     } else {
 #pragma unroll
                         for (int e = 0; e < E; ++e) d0 += xi[e] * yi[e];
                     }
 #pragma unroll
-                    for (int e = 0; e < E; ++e) d1 += yi[e] * yj[e];
+                    for (int e = 0; e < E; ++e) d1 += yi[e] * yj[u][e];
                     d0 = group_sum<G>(d0);
                     d1 = group_sum<G>(d1);
-                    if (lane == 0 && (u == 0 || k0 + 1 < ke)) {
-                        const int sl = u ? sB : sA;
-                        const double cw = u ? cwB : cwA;
+                    if (lane == 0 && k0 + u < ke) {
+                        const int sl = ss[u];
                         uRD[sl] = d0;
                         uDD[sl] = d1;
-                        acc[0] += cw * d0;
-                        acc[1] += cw * d1;
+                        acc[0] += cw[u] * d0;
+                        acc[1] += cw[u] * d1;
                         // local constraints on this slot: q1 = 2 A(sym RD^T), q2 = A(DD^T)
                         // (ALMCalq12p12 lorads_alm.c:714-734) and the line-search dots (:269-277)
                         for (int e = loc_ptr[sl]; e < loc_ptr[sl + 1]; ++e) {
@@ -1133,8 +1094,9 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
                                                  const double *__restrict__ uDD, const double *__restrict__ b,
                                                  const double *__restrict__ cvs, const double *__restrict__ lam,
                                                  const double *__restrict__ par, double *__restrict__ ctrl_cur,
-                                                 const double *__restrict__ partC, const double *__restrict__ partA,
-                                                 int nblk, double *__restrict__ rec, double *__restrict__ partB) {
+                                                 const double *__restrict__ partC, int nblkC,
+                                                 const double *__restrict__ partA, int nblkA,
+                                                 double *__restrict__ rec, double *__restrict__ partB) {
     __shared__ double cs[3];
     __shared__ double red[2];
     LRS_TS(1, 0);
@@ -1144,8 +1106,8 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
     bool act = cs[0] != 0.0;
     double ex = cs[1];
     if (cs[2] != 0.0) {
-        reduce_partials<1>(partC + 9 * kMaxPartialBlocks, nblk, red);
-        reduce_partials<1>(partA + 7 * kMaxPartialBlocks, nblk, red + 1);
+        reduce_partials<1>(partC + 9 * kMaxPartialBlocks, nblkC, red);
+        reduce_partials<1>(partA + 7 * kMaxPartialBlocks, nblkA, red + 1);
         // primalInfeasibility (lorads_alg_common.c:393) and l_inf (lorads_alm.c:1359)
         const double pinf1 = sqrt(red[0] + red[1]) / (1.0 + par[P_BN1]);
         const double pinfinf = pinf1 * (1.0 + par[P_BN1]) / (1.0 + par[P_BNINF]);
@@ -1196,7 +1158,7 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
 // :38-57), G_new = 2 S R_new, A(R_new R_new^T) on the lower slots with the local
 // constraints' values and residual (primalInfeasibility), the L-BFGS pair s = tau D,
 // y = G_new - G_old (setlbfgsHisTwo :842-863) and nine dots.  Partials written (10).
-template <int G, int E>
+template <int G, int E, int U>
 __global__ void __launch_bounds__(kRowBlock) k_it_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
@@ -1249,33 +1211,28 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = grp; i < n; i += ngrp) {
         const long oi = (long)i * ld + lane * E;
-        double ri[E], di[E], g[E], go[E], sov[E], yov[E];
+        double ri[E], di[E], g[E];
         ld_row<E>(R + oi, ri);
         ld_row<E>(D + oi, di);
-        ld_row<E>(Gold + oi, go);
-        if (two) {
-            ld_row<E>(so + oi, sov);
-            ld_row<E>(yo + oi, yov);
-        }
 #pragma unroll
         for (int e = 0; e < E; ++e) ri[e] += tau * di[e];
         st_row<E>(Rn + oi, ri);
 #pragma unroll
         for (int e = 0; e < E; ++e) g[e] = 0.0;
         const int kb = adj_ptr[i], kl = adj_low[i], ke = adj_ptr[i + 1];
-        // neighbours four at a time (indices clamped to the row; extra lanes add 0)
-        for (int k0 = kb; k0 < ke; k0 += 4) {
-            int jj[4], ss[4];
+        // neighbours U at a time (indices clamped to the row; extra lanes add 0)
+        for (int k0 = kb; k0 < ke; k0 += U) {
+            int jj[U], ss[U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const int k = min(k0 + u, ke - 1);
                 jj[u] = adj_col[k];
                 ss[u] = adj_slot[k];
             }
-            double rj[4][E], dj[4][E], sv[4];
-            int eb[4], ee[4];
+            double rj[U][E], dj[U][E], sv[U];
+            int eb[U], ee[U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 ld_row<E>(R + (long)jj[u] * ld + lane * E, rj[u]);
                 ld_row<E>(D + (long)jj[u] * ld + lane * E, dj[u]);
                 sv[u] = Craw[ss[u]];
@@ -1283,7 +1240,7 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
                 ee[u] = slot_ptr[ss[u] + 1];
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 // S[slot] = C + sum_con M1(con) a  (addObjCoeff + sdpDataWSum)
                 for (int e = eb[u]; e < ee[u]; ++e) {
                     const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
@@ -1297,7 +1254,7 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
                 for (int e = 0; e < E; ++e) rj[u][e] += tau * dj[u][e];
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const int k = k0 + u;
                 if (k < ke) {
 #pragma unroll
@@ -1321,7 +1278,8 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
                 }
             }
         }
-        double sv[E], yv[E];
+        double sv[E], yv[E], go[E];
+        ld_row<E>(Gold + oi, go);
 #pragma unroll
         for (int e = 0; e < E; ++e) g[e] *= 2.0;
 #pragma unroll
@@ -1338,6 +1296,9 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
             acc[4] += yv[e] * g[e];
         }
         if (two) {
+            double sov[E], yov[E];
+            ld_row<E>(so + oi, sov);
+            ld_row<E>(yo + oi, yov);
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 acc[5] += sov[e] * g[e];
@@ -1512,13 +1473,68 @@ int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y,
     return 0;
 }
 
-// Row-kernel grid of the split iteration: per cone, capped so that the sum over
-// cones fits the partial buffers.
-static inline int iter_grid(const DevCone &c, int K) {
-    long threads = (long)c.n * c.G;
-    int g = (int)std::max(1L, (threads + kRowBlock - 1) / kRowBlock);
-    const int cap = std::max(1, std::min(kIterMaxBlocks, kMaxPartialBlocks / std::max(1, K)));
-    return std::min(g, cap);
+// Row-kernel grids of the split iteration, sized from the occupancy query: a stage
+// launches min(rows' lane groups, blocks resident on the whole chip).  When one
+// resident wave of groups covers every row (latency regime, small n) the neighbour
+// loops are unrolled so that their gathers overlap; otherwise (bandwidth regime) the
+// unroll-1 variant keeps registers low and occupancy high, and groups stride over rows.
+static int num_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (cus[dev] <= 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cus[dev] = v;
+    }
+    return cus[dev];
+}
+template <typename KernelT>
+static int resident_blocks(KernelT kern, int *cache) {
+    if (*cache <= 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), kRowBlock, 0) !=
+                hipSuccess || nb < 1)
+            nb = 1;
+        *cache = nb * num_cus();
+    }
+    return *cache;
+}
+template <int GG, int EE, int UU>
+static int res_a() {
+    static int c = 0;
+    return resident_blocks(k_it_a<GG, EE, UU>, &c);
+}
+template <int GG, int EE, int UU>
+static int res_b() {
+    static int c = 0;
+    return resident_blocks(k_it_b<GG, EE, UU>, &c);
+}
+
+struct StagePlan {
+    int grid = 1;
+    bool small = true;
+};
+static StagePlan plan_stage(int need, int res_small, int res_large, int K) {
+    StagePlan p;
+    const int cap = std::max(1, kMaxPartialBlocks / std::max(1, K));
+    if (need <= res_small) { p.grid = std::min(need, cap); p.small = true; }
+    else { p.grid = std::min(std::min(need, res_large), cap); p.small = false; }
+    p.grid = std::max(1, p.grid);
+    return p;
+}
+static int plan_a(const DevCone &c, int K, StagePlan &p) {
+    const long need = std::max(1L, ((long)c.n * c.G + kRowBlock - 1) / kRowBlock);
+    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((int)std::min(need, 1L << 30), res_a<GG, EE, 2>(),
+                                                 res_a<GG, EE, 1>(), K); });
+    return 0;
+}
+static int plan_b(const DevCone &c, int K, StagePlan &p) {
+    const long need = std::max(1L, ((long)c.n * c.G + kRowBlock - 1) / kRowBlock);
+    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((int)std::min(need, 1L << 30), res_b<GG, EE, 4>(),
+                                                 res_b<GG, EE, 1>(), K); });
+    return 0;
 }
 
 // One ALM inner iteration = two launches (A, B), three with global constraints
@@ -1535,8 +1551,13 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     double *ls_prev = W.lsres + (parity ^ 1) * LS_N;
     double *ls_cur = W.lsres + parity * LS_N;
     const int L = 2;
-    int nblk_rows = 0;
-    for (int k = 0; k < P.K; ++k) nblk_rows += iter_grid(P.cones[k], P.K);
+    StagePlan pa[kMaxCones], pb[kMaxCones];
+    int nblkA = 0, nblkB = 0;
+    for (int k = 0; k < P.K; ++k) {
+        if (plan_a(P.cones[k], P.K, pa[k]) || plan_b(P.cones[k], P.K, pb[k])) return -1;
+        nblkA += pa[k].grid;
+        nblkB += pb[k].grid;
+    }
     auto mark = [&](int q) -> int {
         if (a.ev && hipEventRecord(a.ev[q], st) != hipSuccess) {
             snprintf(g_err, sizeof(g_err), "hipEventRecord failed");
@@ -1549,15 +1570,19 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     int off = 0;
     for (int k = 0; k < P.K && (mask & 1); ++k) {
         const DevCone &c = P.cones[k];
-        const int grid = iter_grid(c, P.K);
+        const int grid = pa[k].grid;
+#define LRS_LAUNCH_A(UU)                                                                                   \
+    hipLaunchKernelGGL((k_it_a<GG, EE, UU>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr, \
+                       c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], \
+                       W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, P.b, W.cvs, W.lam, W.rec, \
+                       k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w, W.uvt2, W.par,      \
+                       ctrl_prev, ctrl_cur, ls_prev, W.partC, nblkB, W.part, off)
+        const bool small = pa[k].small;
         LRS_LAYOUT_SWITCH(c.G, c.E, {
-            hipLaunchKernelGGL((k_it_a<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
-                               c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1],
-                               W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,
-                               P.b, W.cvs, W.lam, W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr,
-                               P.con_slot, P.con_w, W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, W.partC,
-                               nblk_rows, W.part, off);
+            if (small) LRS_LAUNCH_A(2);
+            else LRS_LAUNCH_A(1);
         });
+#undef LRS_LAUNCH_A
         LRS_CHECK_LAUNCH();
         off += grid;
     }
@@ -1566,8 +1591,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     const int gg = std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
     if (P.mg > 0 && (mask & 2)) {
         hipLaunchKernelGGL(k_it_g, dim3(gg), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot,
-                           P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, W.part, nblk_rows,
-                           W.rec, W.partB);
+                           P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, nblkB, W.part,
+                           nblkA, W.rec, W.partB);
         LRS_CHECK_LAUNCH();
     }
     if (mark(2)) return -1;
@@ -1575,14 +1600,19 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     off = 0;
     for (int k = 0; k < P.K && (mask & 4); ++k) {
         const DevCone &c = P.cones[k];
-        const int grid = iter_grid(c, P.K);
+        const int grid = pb[k].grid;
+#define LRS_LAUNCH_B(UU)                                                                                   \
+    hipLaunchKernelGGL((k_it_b<GG, EE, UU>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr, \
+                       c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],        \
+                       W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a, W.rec, P.loc_ptr,       \
+                       P.loc_con, P.loc_w, P.b, W.cvs, W.par, ctrl_cur, W.part, nblkA, W.partB,                    \
+                       P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off)
+        const bool small = pb[k].small;
         LRS_LAYOUT_SWITCH(c.G, c.E, {
-            hipLaunchKernelGGL((k_it_b<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr,
-                               c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
-                               W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a, W.rec, P.loc_ptr,
-                               P.loc_con, P.loc_w, P.b, W.cvs, W.par, ctrl_cur, W.part, nblk_rows, W.partB,
-                               P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off);
+            if (small) LRS_LAUNCH_B(4);
+            else LRS_LAUNCH_B(1);
         });
+#undef LRS_LAUNCH_B
         LRS_CHECK_LAUNCH();
         off += grid;
     }
