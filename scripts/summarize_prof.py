@@ -39,7 +39,7 @@ if pmc:
 for log in ("trace.log",):
     p = os.path.join(src, log)
     if os.path.exists(p):
-        js = [l for l in open(p) if l.startswith("{")]
+        js = [l[l.index("{"):] for l in open(p) if "{\"metric\"" in l]
         if js:
             lines += ["", "## bench line under the profiler", "", "```", js[-1].strip(), "```"]
 open(os.path.join(dst, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
