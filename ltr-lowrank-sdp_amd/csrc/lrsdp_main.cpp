@@ -129,11 +129,11 @@ int main(int argc, char **argv) {
     }
     if (p.lbfgsListLength < 1 || p.lbfgsListLength > 2) {
         fprintf(stderr, "[lrsdp] lbfgsListLength %d not supported on the device path; using 2\n", p.lbfgsListLength);
+        p.lbfgsListLength = 2;
     }
     if (p.reoptLevel >= 1) {
         fprintf(stderr, "[lrsdp] reoptLevel %d: reoptimisation restarts are not on the device path yet; "
                         "running reoptLevel 0 (DESIGN.md section 7)\n", p.reoptLevel);
-        p.lbfgsListLength = 2;
     }
     printf("-----------------------------------------------------------\n");
     printf("  LoRADS-compatible low-rank SDP solver on MI355X (%s)\n", lrs_version());
