@@ -96,9 +96,15 @@ def stage_roofline(sv, reps):
         out.append({"stage": STAGES[k], "avg_launch_us": ms[k] * 1e3, "bytes_per_launch": by[k],
                     "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS})
     dom = max(out, key=lambda s: s["avg_launch_us"])
+    # the north-star's named operator: A(UU^T) straight from the constraint entries
+    ams = sv.time_auut(reps)
+    aby = sv.auut_bytes()
+    agbs = aby / (ams * 1e-3) / 1e9
+    auut = {"kernel": "k_auv_con<XX^T> (A(UU^T) over constraint entries)", "avg_launch_us": ams * 1e3,
+            "bytes_per_launch": aby, "achieved_GBs": agbs, "frac": agbs / HBM_PEAK_GBS}
     return {"bound": "hbm", "kernel": dom["stage"], "achieved": dom["achieved_GBs"], "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": dom["frac"], "traffic": None, "bytes_per_launch": dom["bytes_per_launch"],
-            "avg_launch_us": dom["avg_launch_us"], "stages": out}
+            "avg_launch_us": dom["avg_launch_us"], "stages": out, "a_uut": auut}
 
 
 def main():

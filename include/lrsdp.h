@@ -125,8 +125,11 @@ int lrs_alm_throughput(lrs_ctx *ctx, const lrs_params *p, long warmup, long step
 /* Mirror the iteration log into a file (the reference's --logfile). */
 int lrs_set_log_path(lrs_ctx *ctx, const char *path);
 
-/* Standalone A(UU^T) (SDDMM + gather) timing on R: reps launches, average ms per launch. */
+/* Standalone A(UU^T) on R (the constraint-entry kernel k_auv_con, all cones): reps
+ * launches back to back between two HIP events, average ms per launch; and its
+ * algorithmic bytes (factor rows touched once + entry data + outputs). */
 int lrs_time_auut(lrs_ctx *ctx, int reps, double *avg_ms);
+int lrs_auut_bytes(lrs_ctx *ctx, double *bytes);
 
 /* Per-stage timing of the split ALM inner iteration: runs `steps` inner iterations at
  * the current rank like lrs_alm_throughput, with HIP events on the solver stream

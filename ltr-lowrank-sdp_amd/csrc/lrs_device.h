@@ -105,6 +105,9 @@ struct DevProblem {
     int *glob = nullptr;                                     // [mg]
     int *loc_ptr = nullptr, *loc_con = nullptr;              // [Ptot+1], [m - mg]
     double *loc_w = nullptr;                                 // (2 - delta) a of that one entry
+    int *slot_rc = nullptr;                                  // [Ptot][2] (row, col) in the cone
+    int *con1_pq = nullptr;                                  // [K*m][2] single-entry rows: (p, q) or -1
+    double *con1_w = nullptr;                                // [K*m] their weight
     std::vector<DevCone> cones;
 };
 
@@ -141,6 +144,12 @@ int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const
 // partial sum of (b - out)^2 if vio_part != nullptr (primal residual).
 int launch_gather(const DevProblem &P, const double *uvt, double scale, double *out,
                   const double *b_for_vio, double *vio_part, hipStream_t st, int *nblk_used);
+// Constraint-entry A(.) of one cone without the pattern pass: every constraint's
+// entries of cone `cone` read their two factor rows directly (mode 0: sym(X Y^T),
+// mode 1: X X^T).  out[i] = (accumulate ? out[i] : 0) + scale * value_of_this_cone; optional
+// residual sum (b - out)^2 -> tmpfin TF_GATHER.  Bitwise equal to sddmm + gather_cone.
+int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double scale,
+                   int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st);
 // S[slot] = (withC ? Craw[slot] : 0) + sum_(con,a) w[con] * a
 int launch_wsum(const DevProblem &P, const double *w, int withC, double *S, hipStream_t st);
 // out = scale * S X (+ addX * X) per cone, partial ||out||^2 -> part[0][pblk_off+b]

@@ -337,6 +337,86 @@ __global__ void __launch_bounds__(kBlock) k_gather(int m, int K, int cone, const
     if (part) partials_finalize<1>(acc, part, ticket, fin);
 }
 
+// Constraint-entry A(X Y^T) (LORADSUpdateConstrValCG lorads_admm.c:442-459 /
+// coneAUV data/lorads_sdp_conic.c:378-385 without materialising the pattern): one
+// lane group per constraint, each entry (p, q) of cone k read as two factor rows.
+template <int E, int MODE>
+__device__ __forceinline__ double auv_entry(const double *__restrict__ X, const double *__restrict__ Y, int ld,
+                                            int lane, int p, int q) {
+    double xp[E];
+    ld_row<E>(X + (long)p * ld + lane * E, xp);
+    double d = 0.0;
+    if (p == q) {
+        if constexpr (MODE == 1) {
+#pragma unroll
+            for (int t = 0; t < E; ++t) d += xp[t] * xp[t];
+        } else {
+            double yp[E];
+            ld_row<E>(Y + (long)p * ld + lane * E, yp);
+#pragma unroll
+            for (int t = 0; t < E; ++t) d += xp[t] * yp[t];
+        }
+    } else {
+        double xq[E];
+        ld_row<E>(X + (long)q * ld + lane * E, xq);
+        if constexpr (MODE == 1) {
+#pragma unroll
+            for (int t = 0; t < E; ++t) d += xp[t] * xq[t];
+        } else {
+            double yp[E], yq[E];
+            ld_row<E>(Y + (long)p * ld + lane * E, yp);
+            ld_row<E>(Y + (long)q * ld + lane * E, yq);
+#pragma unroll
+            for (int t = 0; t < E; ++t) d += xp[t] * yq[t] + xq[t] * yp[t];
+            d *= 0.5;
+        }
+    }
+    return d;
+}
+
+template <int G, int E, int MODE>
+__global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int ld, const int *__restrict__ con_ptr,
+                                                    const int *__restrict__ con_slot,
+                                                    const double *__restrict__ con_w, const int *__restrict__ slot_rc,
+                                                    const int *__restrict__ con1_pq, const double *__restrict__ con1_w,
+                                                    const double *__restrict__ X, const double *__restrict__ Y,
+                                                    double scale, int accumulate, double *__restrict__ out,
+                                                    const double *__restrict__ b, double *part, unsigned *ticket,
+                                                    double *fin) {
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kBlock / G;
+    double acc[1] = {0.0};
+    for (int i = grp; i < m; i += ngrp) {
+        const long row = (long)cone * m + i;
+        const int2 pq = reinterpret_cast<const int2 *>(con1_pq)[row];
+        double v = 0.0;
+        if (pq.x >= 0) {
+            // single-entry row: (p, q, w) in one coalesced load, then the factor rows
+            const double w = con1_w[row];
+            double d = auv_entry<E, MODE>(X, Y, ld, lane, pq.x, pq.y);
+            d = group_sum<G>(d);
+            v += w * d;
+        } else {
+            const int e0 = con_ptr[row], e1 = con_ptr[row + 1];
+            for (int e = e0; e < e1; ++e) {
+                const int s = con_slot[e];
+                const int p = slot_rc[2 * s], q = slot_rc[2 * s + 1];
+                double d = auv_entry<E, MODE>(X, Y, ld, lane, p, q);
+                d = group_sum<G>(d);
+                v += con_w[e] * d;
+            }
+        }
+        if (lane == 0) {
+            double tot = v * scale;
+            if (accumulate) tot = out[i] + tot;
+            out[i] = tot;
+            if (b) { const double dd = b[i] - tot; acc[0] += dd * dd; }
+        }
+    }
+    if (part) partials_finalize<1>(acc, part, ticket, fin);
+}
+
 // S[slot] = (withC ? Craw : 0) + sum w[con] a
 __global__ void __launch_bounds__(kBlock) k_wsum(int Ptot, const int *__restrict__ slot_ptr,
                                                  const int *__restrict__ slot_con, const double *__restrict__ slot_a,
@@ -1399,6 +1479,28 @@ int launch_gather_cone(const DevProblem &P, int cone, const double *uvt, double 
     const int grid = grid_elems(P.m, 1);
     hipLaunchKernelGGL(k_gather, dim3(grid), dim3(kBlock), 0, st, P.m, P.K, cone, P.con_ptr, P.con_slot, P.con_w,
                        uvt, 1.0, out, nullptr, nullptr, ticket_ptr(T_GATHER), tmpfin_ptr() + TF_GATHER);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double scale,
+                   int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st) {
+    const DevCone &c = P.cones[cone];
+    const int grid = grid_rows(P.m, c.G);
+    const double *Xc = X + c.foff;
+    const double *Yc = Y ? Y + c.foff : nullptr;
+    unsigned *tk = ticket_ptr(T_GATHER);
+    double *fin = tmpfin_ptr() + TF_GATHER;
+    LRS_LAYOUT_SWITCH(c.G, c.E, {
+        if (mode == 1)
+            hipLaunchKernelGGL((k_auv_con<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
+                               P.con_ptr, P.con_slot, P.con_w, P.slot_rc, P.con1_pq, P.con1_w, Xc, Yc, scale,
+                               accumulate, out, b_for_vio, vio_part, tk, fin);
+        else
+            hipLaunchKernelGGL((k_auv_con<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
+                               P.con_ptr, P.con_slot, P.con_w, P.slot_rc, P.con1_pq, P.con1_w, Xc, Yc, scale,
+                               accumulate, out, b_for_vio, vio_part, tk, fin);
+    });
     LRS_CHECK_LAUNCH();
     return 0;
 }

@@ -317,6 +317,31 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             fp[g]++;
         }
     dp.Z = Z;
+    // slot coordinates (row, col) inside their cone, for the constraint-entry A(UV^T)
+    std::vector<int> slot_rc(2L * std::max(1, Ptot), 0);
+    for (int k = 0; k < hp.K; ++k) {
+        const HostCone &c = hp.cones[k];
+        for (int t = 0; t < (int)c.prow.size(); ++t) {
+            slot_rc[2L * (dp.cones[k].slot_off + t)] = c.prow[t];
+            slot_rc[2L * (dp.cones[k].slot_off + t) + 1] = c.pcol[t];
+        }
+    }
+    if (!dput(&dp.slot_rc, slot_rc, err)) return false;
+    // per (cone, constraint) row with exactly one entry: its (p, q) and weight, so the
+    // constraint-entry kernels read them in one coalesced load; p = -1 otherwise
+    {
+        const long rows = (long)hp.K * m;
+        std::vector<int> c1pq(2 * std::max(1L, rows), -1);
+        std::vector<double> c1w(std::max(1L, rows), 0.0);
+        for (long r = 0; r < rows; ++r) {
+            if (con_ptr[r + 1] - con_ptr[r] != 1) continue;
+            const int e = con_ptr[r];
+            c1pq[2 * r] = slot_rc[2L * con_slot[e]];
+            c1pq[2 * r + 1] = slot_rc[2L * con_slot[e] + 1];
+            c1w[r] = con_w[e];
+        }
+        if (!dput(&dp.con1_pq, c1pq, err) || !dput(&dp.con1_w, c1w, err)) return false;
+    }
     // Single-slot ("local") constraints: exactly one merged entry over all cones.  Their
     // A(.) value is one pattern slot, so the row that owns the slot evaluates them inside
     // the row kernels; every other constraint is "global" (lrs_kernels.hip, split iteration).
@@ -375,7 +400,7 @@ void free_problem(DevProblem &dp) {
     auto f = [](void *p) { if (p) (void)hipFree(p); };
     f(dp.b); f(dp.Cw); f(dp.Craw); f(dp.con_ptr); f(dp.con_slot); f(dp.con_w);
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
-    f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w);
+    f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); }
     dp = DevProblem();
 }

@@ -817,8 +817,8 @@ PRINT_AND_EXIT:
 static int lin_sys_product(lrs_ctx *c, int k, const double *Y, const double *x, double *res) {
     DevProblem &P = c->dp;
     DevWork &W = c->W;
-    OPC(launch_sddmm(P, k, 0, x, Y, W.uvt2, nullptr, W.part, 0, nullptr, c->st));
-    OPC(launch_gather_cone(P, k, W.uvt2, W.wtmp, c->st));
+    // A(sym(x Y^T)) over cone k's constraint entries only (LORADSUpdateConstrValCG)
+    OPC(launch_auv_con(P, k, 0, x, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st));
     OPC(launch_wsum(P, W.wtmp, 0, W.S, c->st));
     OPC(launch_spmm(P, k, W.S, Y, 1.0, x, 1.0, res, nullptr, 0, nullptr, c->st));
     return 0;
@@ -1103,6 +1103,28 @@ int lrs_load_coo(lrs_ctx *c, int m, int nblk, const int *dims, const double *b, 
     c->loaded = true;
     c->path = "<memory>";
     c->cgIterCone.assign(c->hp.K, 0);
+    return 0;
+}
+
+int lrs_auut_bytes(lrs_ctx *c, double *bytes) {
+    // A(U U^T) over constraint entries (SURVEY.md §8(d) B_A with delta = 1): the factor
+    // rows touched (each row once when distinct), per entry con_slot + con_w + slot
+    // coordinates (16 B), con_ptr, and the m outputs.
+    if (!c || !c->loaded || !c->walloc) { set_err("no solver state"); return -1; }
+    double by = 0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        const HostCone &hc = c->hp.cones[k];
+        std::vector<char> touched(hc.n, 0);
+        long rows = 0;
+        for (const HostEntry &e : hc.ent) {
+            const int p = hc.prow[e.slot], q = hc.pcol[e.slot];
+            if (!touched[p]) { touched[p] = 1; rows++; }
+            if (!touched[q]) { touched[q] = 1; rows++; }
+        }
+        by += 8.0 * rows * c->rank[k] + 16.0 * (double)hc.ent.size() + 4.0 * (c->dp.m + 1);
+    }
+    by += 8.0 * c->dp.m;
+    *bytes = by;
     return 0;
 }
 
@@ -1538,11 +1560,10 @@ int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {
     HIPC(hipEventCreate(&e0));
     HIPC(hipEventCreate(&e1));
     HIPC(hipEventRecord(e0, c->st));
-    for (int q = 0; q < reps; ++q) {
+    // A(R R^T): the constraint-entry kernel, cones accumulated in cone order
+    for (int q = 0; q < reps; ++q)
         for (int k = 0; k < c->dp.K; ++k)
-            OPC(launch_sddmm(c->dp, k, 1, c->W.R, nullptr, c->W.uvt2, nullptr, c->W.part, 0, nullptr, c->st));
-        OPC(launch_gather(c->dp, c->W.uvt2, 1.0, c->W.q1, nullptr, nullptr, c->st, nullptr));
-    }
+            OPC(launch_auv_con(c->dp, k, 1, c->W.R, nullptr, 1.0, k > 0, c->W.q1, nullptr, nullptr, c->st));
     HIPC(hipEventRecord(e1, c->st));
     HIPC(hipEventSynchronize(e1));
     float ms = 0;

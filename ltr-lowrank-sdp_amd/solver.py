@@ -107,6 +107,7 @@ def load_library(path=None):
         "lrs_profile_stages": (C.c_int, [vp, C.POINTER(Params), C.c_long, dp, C.POINTER(C.c_long)]),
         "lrs_time_stages": (C.c_int, [vp, C.c_int, dp]),
         "lrs_stage_bytes": (C.c_int, [vp, dp]),
+        "lrs_auut_bytes": (C.c_int, [vp, dp]),
         "lrs_load_coo": (C.c_int, [vp, C.c_int, C.c_int, ip, dp, C.c_long, ip, ip, ip, ip, dp]),
         "lrs_debug_phase_times": (C.c_int, [vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
     }
@@ -288,6 +289,12 @@ class Solver:
         done = C.c_long()
         self._check(self.lib.lrs_profile_stages(self.ctx, C.byref(p), steps, ms, C.byref(done)), "profile_stages")
         return list(ms), done.value
+
+    def auut_bytes(self):
+        """Algorithmic bytes of one A(UU^T) (constraint-entry kernel) launch."""
+        v = C.c_double()
+        self._check(self.lib.lrs_auut_bytes(self.ctx, C.byref(v)), "auut_bytes")
+        return v.value
 
     def stage_bytes(self):
         """Algorithmic bytes per launch of the stages [A, G, B] at the current ranks."""

@@ -134,3 +134,21 @@ def test_stage_timing(solver_mod, name):
     by = sv.stage_bytes()
     assert ms[0] > 0 and ms[2] > 0 and by[0] > 0 and by[2] > 0
     assert (ms[1] > 0) == (name.startswith("theta"))   # theta has the multi-slot trace constraint
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mc_rand200", "theta25x3", "rsparse60"])
+def test_constraint_entry_auut_matches_pattern_path(solver_mod, name):
+    """k_auv_con (A(RR^T) straight from constraint entries) == SDDMM over the pattern + gather."""
+    g = load_kernels(name)
+    s = split_inputs(g)
+    sv = solver_mod.Solver(instance(name))
+    sv.set_rank([s["rank"]] * len(s["dims"]))
+    sv.set_factor(solver_mod.R, s["R"])
+    cvs, _, _ = sv.constr_rr()
+    sv.time_auut(1)
+    q = sv.get_vec(solver_mod.Q1)
+    if len(s["dims"]) == 1:
+        assert np.array_equal(q, cvs)          # same arithmetic, same order
+    assert rel_err(q, g["cvs_rr"]) < TOL
+    assert sv.auut_bytes() > 0
