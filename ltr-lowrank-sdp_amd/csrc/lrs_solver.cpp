@@ -130,6 +130,11 @@ struct lrs_ctx {
     // hipGraph cache of inner-iteration batches (keyed by batch size; the kernels'
     // arguments are the workspace pointers, so a new workspace drops the cache)
     std::map<int, hipGraphExec_t> graphs;
+    // initial point cache (device layout, host copy) for the ranks it was drawn at
+    std::vector<int> init_ranks;
+    std::vector<double> init_cache;
+    // running estimate of inner iterations per run_inner call (first batch size)
+    double inner_est = 8.0;
     bool use_graphs = false;   // eager launches measured faster than graph replay (LRS_GRAPHS=1)
     // per-stage event profiling (lrs_profile_stages)
     bool prof = false;
@@ -173,7 +178,26 @@ static void free_work(lrs_ctx *c) {
     c->walloc = false;
 }
 
+static int zero_work(lrs_ctx *c) {
+    DevWork &W = c->W;
+    const DevProblem &P = c->dp;
+    const long NR = std::max(2L, P.NRpad);
+    const int m = std::max(1, P.m), Pt = std::max(1, P.Ptot);
+    struct Z { double *p; long n; } zs[] = {
+        {W.R, NR}, {W.D, NR}, {W.G[0], NR}, {W.G[1], NR}, {W.ls[0], NR}, {W.ly[0], NR}, {W.ls[1], NR}, {W.ly[1], NR},
+        {W.U, NR}, {W.V, NR}, {W.X, NR}, {W.cg_r, NR}, {W.cg_p, NR}, {W.cg_Q, NR}, {W.cg_b, NR}, {W.M2, NR},
+        {W.R2, NR}, {W.uvt0, Pt}, {W.uvt1, Pt}, {W.uvt2, Pt}, {W.S, Pt}, {W.lam, m}, {W.cvs, m}, {W.q1, m},
+        {W.q2, m}, {W.M1, m}, {W.wtmp, m}, {W.cvc, (long)m * std::max(1, P.K)}, {W.ctrl, 2 * C_NCTRL},
+        {W.lsres, 2 * LS_N}, {W.rec, 4L * m}};
+    for (auto &z : zs) HIPC(hipMemsetAsync(z.p, 0, sizeof(double) * z.n, c->st));
+    c->head = 0; c->gcur = 0;
+    c->beta[0] = c->beta[1] = c->yy[0] = c->yy[1] = 0;
+    return 0;
+}
+
 static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
+    // same ranks as the live workspace: keep the buffers (and the captured graphs), zero them
+    if (c->walloc && ranks == c->rank) return zero_work(c);
     free_work(c);
     DevProblem &P = c->dp;
     c->rank = ranks;
@@ -465,6 +489,11 @@ static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &ra
 
 // random initial point R (LORADS_RANDOM_rk_MAT), cones in order, column-major draw order
 static int init_point(lrs_ctx *c) {
+    if (c->init_ranks == c->rank && !c->init_cache.empty()) {
+        HIPC(hipMemcpyAsync(c->W.R, c->init_cache.data(), sizeof(double) * c->init_cache.size(),
+                            hipMemcpyHostToDevice, c->st));
+        return 0;
+    }
     GlibcRand g(925);
     long NRc = 0;
     for (int k = 0; k < c->dp.K; ++k) NRc += (long)c->dp.cones[k].n * c->rank[k];
@@ -474,7 +503,12 @@ static int init_point(lrs_ctx *c) {
         v -= (double)g.next() / 2147483647.0;
         R[i] = v;
     }
-    return factor_put(c, c->W.R, R.data());
+    if (factor_put(c, c->W.R, R.data())) return -1;
+    // keep the device-layout copy: every solve at these ranks starts from the same point
+    c->init_cache.assign(c->dp.NRpad, 0.0);
+    HIPC(hipMemcpy(c->init_cache.data(), c->W.R, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToHost));
+    c->init_ranks = c->rank;
+    return 0;
 }
 
 // ---- AUG_RANK (data/lorads_solver.c:1154-1254)
@@ -609,11 +643,19 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     memcpy(c->hpin + 64, ctl, sizeof(ctl));
     HIPC(hipMemcpyAsync(c->W.ctrl + C_NCTRL, c->hpin + 64, sizeof(ctl), hipMemcpyHostToDevice, c->st));
     AlmIterArgs a{&c->dp, &c->W, nullptr};
-    int B = 4;
+    // Batch sizes: start near the running estimate of this call's length, double after
+    // each batch, never beyond the iterations to a certain exit (budget, localIter 800)
+    // + 1 (the iteration whose first stage detects it).  B stays even (parity).
+    long certain = 801 - io.local;
+    if (budget > 0) certain = std::min(certain, budget - io.inner);
+    certain = std::max(0L, certain) + 1;
+    auto even_clamp = [](long v) { v = std::max(4L, std::min(64L, v)); return (int)(v + (v & 1)); };
+    int B = even_clamp((long)(c->inner_est * 0.5));
     double *res = c->hpin + 128;
     const double t_in = c->stats ? now_s() : 0.0;
     long enq = 0;
     for (;;) {
+        B = std::min(B, even_clamp(certain - enq));
         enq += B;
         if (c->prof) {
             // two iterations with events around each launch, then read the control
@@ -645,6 +687,7 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
         if (res[C_ACT2] == 0.0) break;
         B = std::min(B * 2, 64);
     }
+    c->inner_est = 0.7 * c->inner_est + 0.3 * (double)std::max(1L, (long)res[C_INNER] - io.inner);
     if (c->stats) {
         c->st_calls++;
         c->st_iters += (long)res[C_INNER] - io.inner;
