@@ -102,6 +102,7 @@ struct DevProblem {
     double *slot_a = nullptr;                                // [Z]
     // single-slot ("local") constraints per slot, and the list of the others
     int mg = 0;                                              // number of global constraints
+    int glob_maxlen = 0;                                     // most entries of one global constraint
     int *glob = nullptr;                                     // [mg]
     int *loc_ptr = nullptr, *loc_con = nullptr;              // [Ptot+1], [m - mg]
     double *loc_w = nullptr;                                 // (2 - delta) a of that one entry

@@ -1035,7 +1035,7 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
     const int *__restrict__ glob, int m, int K, const int *__restrict__ con_ptr, const int *__restrict__ con_slot,
     const double *__restrict__ con_w, const double *__restrict__ uRR, const double *__restrict__ par,
     const double *__restrict__ ctrl_prev, double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev,
-    const double *__restrict__ partC, int nblkC, double *__restrict__ partA, int pblk_off) {
+    const double *__restrict__ partC, int nblkC, double *__restrict__ partA, int pblk_off, int T, int gwide) {
     __shared__ double c[C_NCTRL];
     __shared__ double red[10];
     __shared__ double lsv[2];
@@ -1053,19 +1053,40 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (fold && do_glob) {
         // global constraints: A(RR^T) from the slots and their residual (primalInfeasibility);
-        // independent of this iteration's control, so it runs beside ctrl_step
-        for (int g = blockIdx.x * kRowBlock + threadIdx.x; g < mg; g += gridDim.x * kRowBlock) {
-            const int i = glob[g];
-            double tot = 0.0;
-            for (int k = 0; k < K; ++k) {
-                const long row = (long)k * m + i;
-                double v = 0.0;
-                for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) v += con_w[e] * uRR[con_slot[e]];
-                tot += v;
+        // independent of this iteration's control, so it runs beside ctrl_step.  Long
+        // constraints (gwide) take a whole wave each, lanes striding over the entries.
+        if (gwide) {
+            const int lane64 = threadIdx.x & 63;
+            const int nw = gridDim.x * (kRowBlock / 64);
+            for (int g = blockIdx.x * (kRowBlock / 64) + (threadIdx.x >> 6); g < mg; g += nw) {
+                const int i = glob[g];
+                double tot = 0.0;
+                for (int k = 0; k < K; ++k) {
+                    const long row = (long)k * m + i;
+                    double v = 0.0;
+                    for (int e = con_ptr[row] + lane64; e < con_ptr[row + 1]; e += 64) v += con_w[e] * uRR[con_slot[e]];
+                    tot += wave_sum(v);
+                }
+                if (lane64 == 0) {
+                    cvs[i] = tot;
+                    const double dd = b[i] - tot;
+                    acc[7] += dd * dd;
+                }
             }
-            cvs[i] = tot;
-            const double dd = b[i] - tot;
-            acc[7] += dd * dd;
+        } else {
+            for (int g = blockIdx.x * kRowBlock + threadIdx.x; g < mg; g += gridDim.x * kRowBlock) {
+                const int i = glob[g];
+                double tot = 0.0;
+                for (int k = 0; k < K; ++k) {
+                    const long row = (long)k * m + i;
+                    double v = 0.0;
+                    for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) v += con_w[e] * uRR[con_slot[e]];
+                    tot += v;
+                }
+                cvs[i] = tot;
+                const double dd = b[i] - tot;
+                acc[7] += dd * dd;
+            }
         }
     }
     __syncthreads();
@@ -1085,10 +1106,12 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
         const double *__restrict__ Gc = (c[C_GCUR] == 0.0 ? G0 : G1) + foff;
         const double *__restrict__ s0 = s0a + foff, *__restrict__ y0 = y0a + foff;
         const double *__restrict__ s1 = s1a + foff, *__restrict__ y1 = y1a + foff;
+        // lane groups of G lanes; a team of T groups shares one row (dense rows)
         const int lane = threadIdx.x & (G - 1);
         const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
         const int ngrp = gridDim.x * kRowBlock / G;
-        for (int i = grp; i < n; i += ngrp) {
+        const int team = grp / T, mem = grp % T, nteams = ngrp / T;
+        for (int i = team; i < n; i += nteams) {
             const long oi = (long)i * ld + lane * E;
             const int kb = adj_ptr[i], ke = adj_low[i];
             double xi[E], yi[E];
@@ -1098,10 +1121,11 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
                 dr.load(kc, Gc, s0, y0, s1, y1, oi);
                 dr.eval(kc, yi);
             }
-            st_row<E>(D + oi, yi);
+            if (mem == 0) st_row<E>(D + oi, yi);
             // lower entries U at a time: the neighbours' operand loads in flight together
-            // (indices clamped to the row; the extra lanes' results are not stored)
-            for (int k0 = kb; k0 < ke; k0 += U) {
+            // (indices clamped to the row; the extra lanes' results are not stored); the
+            // team's members take interleaved chunks of U
+            for (int k0 = kb + mem * U; k0 < ke; k0 += T * U) {
                 int jj[U], ss[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -1176,7 +1200,7 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
                                                  const double *__restrict__ par, double *__restrict__ ctrl_cur,
                                                  const double *__restrict__ partC, int nblkC,
                                                  const double *__restrict__ partA, int nblkA,
-                                                 double *__restrict__ rec, double *__restrict__ partB) {
+                                                 double *__restrict__ rec, double *__restrict__ partB, int gwide) {
     __shared__ double cs[3];
     __shared__ double red[2];
     LRS_TS(1, 0);
@@ -1203,20 +1227,27 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
     const double rho = par[P_RHO];
     const double rhoInv = 1.0 / rho;
     double acc[5] = {0, 0, 0, 0, 0};
-    for (int g = blockIdx.x * kBlock + threadIdx.x; g < mg; g += gridDim.x * kBlock) {
+    // gwide: a wave per constraint, lanes striding over its entries
+    const int lanes = gwide ? 64 : 1;
+    const int sub = gwide ? (threadIdx.x & 63) : 0;
+    const int gid = gwide ? blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6) : blockIdx.x * kBlock + threadIdx.x;
+    const int gstride = gwide ? gridDim.x * (kBlock / 64) : gridDim.x * kBlock;
+    for (int g = gid; g < mg; g += gstride) {
         const int i = glob[g];
         double v1 = 0.0, v2 = 0.0;
         for (int k = 0; k < K; ++k) {
             const long row = (long)k * m + i;
             double a1 = 0.0, a2 = 0.0;
-            for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) {
+            for (int e = con_ptr[row] + sub; e < con_ptr[row + 1]; e += lanes) {
                 const double w = con_w[e];
                 const int s = con_slot[e];
                 a1 += w * uRD[s];
                 a2 += w * uDD[s];
             }
+            if (gwide) { a1 = wave_sum(a1); a2 = wave_sum(a2); }
             v1 += a1; v2 += a2;
         }
+        if (sub != 0) continue;
         v1 *= 2.0;
         const double bi = b[i], ci = cvs[i], li = lam[i];
         const double q0 = (bi - ci) + rhoInv * li;
@@ -1248,7 +1279,8 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
     const int *__restrict__ loc_ptr, const int *__restrict__ loc_con, const double *__restrict__ loc_w,
     const double *__restrict__ b, double *__restrict__ cvs, const double *__restrict__ par,
     const double *__restrict__ ctrl, const double *__restrict__ partA, int nblkA, const double *__restrict__ partB,
-    int nblkB, double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off) {
+    int nblkB, double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int T) {
+    __shared__ double gsh[kRowBlock * E];   // team reduction of the row gradient (T > 1)
     __shared__ double red[12];
     __shared__ double ls[LS_N];
     __shared__ double cs[4];
@@ -1284,24 +1316,33 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
     const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
     const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
     const bool two = (L == 2);
+    // lane groups of G lanes; a team of T groups shares one row (dense rows): member m
+    // takes interleaved chunks of U neighbours, the partial gradients meet in LDS.  The
+    // row loop runs the same trip count in every team of a block (barriers inside).
     const int lane = threadIdx.x & (G - 1);
     const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
     const int ngrp = gridDim.x * kRowBlock / G;
+    const int team = grp / T, mem = grp % T, nteams = ngrp / T;
+    const int tpb = (kRowBlock / G) / T;                 // teams per block
+    const int team_local = team - blockIdx.x * tpb;
     // acc: GG, ys, yy, sG, yG, soG, yoG, soy, yoy, residual
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = grp; i < n; i += ngrp) {
-        const long oi = (long)i * ld + lane * E;
-        double ri[E], di[E], g[E];
+    for (int ib = blockIdx.x * tpb; ib < n; ib += nteams) {
+    const int i = ib + team_local;
+    const bool valid = i < n;
+    double ri[E], di[E], g[E];
+    const long oi = (long)(valid ? i : 0) * ld + lane * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e) g[e] = 0.0;
+    if (valid) {
         ld_row<E>(R + oi, ri);
         ld_row<E>(D + oi, di);
 #pragma unroll
         for (int e = 0; e < E; ++e) ri[e] += tau * di[e];
-        st_row<E>(Rn + oi, ri);
-#pragma unroll
-        for (int e = 0; e < E; ++e) g[e] = 0.0;
+        if (mem == 0) st_row<E>(Rn + oi, ri);
         const int kb = adj_ptr[i], kl = adj_low[i], ke = adj_ptr[i + 1];
         // neighbours U at a time (indices clamped to the row; extra lanes add 0)
-        for (int k0 = kb; k0 < ke; k0 += U) {
+        for (int k0 = kb + mem * U; k0 < ke; k0 += T * U) {
             int jj[U], ss[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -1358,6 +1399,23 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
                 }
             }
         }
+    }   // valid
+    if (T > 1) {
+        // team reduction: member 0 of each team sums the members' partials in order
+#pragma unroll
+        for (int e = 0; e < E; ++e) gsh[threadIdx.x * E + e] = g[e];
+        __syncthreads();
+        if (mem == 0 && valid) {
+            const int base = (team_local * T) * G + lane;
+#pragma unroll
+            for (int e = 0; e < E; ++e) g[e] = gsh[base * E + e];
+            for (int t = 1; t < T; ++t)
+#pragma unroll
+                for (int e = 0; e < E; ++e) g[e] += gsh[(base + t * G) * E + e];
+        }
+        __syncthreads();
+    }
+    if (mem == 0 && valid) {
         double sv[E], yv[E], go[E];
         ld_row<E>(Gold + oi, go);
 #pragma unroll
@@ -1387,7 +1445,8 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
                 acc[8] += yov[e] * yv[e];
             }
         }
-    }
+    }   // mem == 0
+    }   // rows
     LRS_TS(2, 3);
     write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
     LRS_TS_END(2, 4);
@@ -1617,25 +1676,37 @@ static int res_b() {
 struct StagePlan {
     int grid = 1;
     bool small = true;
+    int T = 1;         // lane groups per row (team)
 };
-static StagePlan plan_stage(int need, int res_small, int res_large, int K) {
+// Team size for rows of average degree `deg`: split a row's neighbour list over T lane
+// groups while every group still gets two unrolled chunks and the chip is not
+// oversubscribed (dense rows, e.g. the Lovasz theta objective, n ~ 100s).
+static int team_size(const DevCone &c, double deg, int U) {
+    const long cap_threads = 256L * 2048;
+    int T = 1;
+    while (T * 2 <= kRowBlock / c.G && (double)(T * 2 * U * 2) <= deg && (long)c.n * T * 2 * c.G <= cap_threads) T *= 2;
+    return T;
+}
+static StagePlan plan_stage(long rows_threads, int res_small, int res_large, int K, int T) {
     StagePlan p;
+    p.T = T;
+    const long need = std::max(1L, (rows_threads * T + kRowBlock - 1) / kRowBlock);
     const int cap = std::max(1, kMaxPartialBlocks / std::max(1, K));
-    if (need <= res_small) { p.grid = std::min(need, cap); p.small = true; }
-    else { p.grid = std::min(std::min(need, res_large), cap); p.small = false; }
+    if (need <= res_small) { p.grid = (int)std::min<long>(need, cap); p.small = true; }
+    else { p.grid = (int)std::min<long>(std::min<long>(need, res_large), cap); p.small = false; }
     p.grid = std::max(1, p.grid);
     return p;
 }
 static int plan_a(const DevCone &c, int K, StagePlan &p) {
-    const long need = std::max(1L, ((long)c.n * c.G + kRowBlock - 1) / kRowBlock);
-    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((int)std::min(need, 1L << 30), res_a<GG, EE, 2>(),
-                                                 res_a<GG, EE, 1>(), K); });
+    const double deg = c.n > 0 ? (double)c.P / c.n : 0.0;    // lower entries per row
+    const int T = team_size(c, deg, 2);
+    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.n * c.G, res_a<GG, EE, 2>(), res_a<GG, EE, 1>(), K, T); });
     return 0;
 }
 static int plan_b(const DevCone &c, int K, StagePlan &p) {
-    const long need = std::max(1L, ((long)c.n * c.G + kRowBlock - 1) / kRowBlock);
-    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((int)std::min(need, 1L << 30), res_b<GG, EE, 4>(),
-                                                 res_b<GG, EE, 1>(), K); });
+    const double deg = c.n > 0 ? (double)c.adj_nnz / c.n : 0.0;
+    const int T = team_size(c, deg, 4);
+    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.n * c.G, res_b<GG, EE, 4>(), res_b<GG, EE, 1>(), K, T); });
     return 0;
 }
 
@@ -1660,6 +1731,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         nblkA += pa[k].grid;
         nblkB += pb[k].grid;
     }
+    const int gwide = P.glob_maxlen >= 32 ? 1 : 0;   // long global constraints: a wave each
     auto mark = [&](int q) -> int {
         if (a.ev && hipEventRecord(a.ev[q], st) != hipSuccess) {
             snprintf(g_err, sizeof(g_err), "hipEventRecord failed");
@@ -1678,7 +1750,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], \
                        W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, P.b, W.cvs, W.lam, W.rec, \
                        k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w, W.uvt2, W.par,      \
-                       ctrl_prev, ctrl_cur, ls_prev, W.partC, nblkB, W.part, off)
+                       ctrl_prev, ctrl_cur, ls_prev, W.partC, nblkB, W.part, off, pa[k].T, gwide)
         const bool small = pa[k].small;
         LRS_LAYOUT_SWITCH(c.G, c.E, {
             if (small) LRS_LAUNCH_A(2);
@@ -1690,11 +1762,12 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     }
     if (mark(1)) return -1;
     // G: phase-1 test and the global constraints' q and dots
-    const int gg = std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
+    const int gg = gwide ? std::min((std::max(1, P.mg) + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks)
+                         : std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
     if (P.mg > 0 && (mask & 2)) {
         hipLaunchKernelGGL(k_it_g, dim3(gg), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot,
                            P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, nblkB, W.part,
-                           nblkA, W.rec, W.partB);
+                           nblkA, W.rec, W.partB, gwide);
         LRS_CHECK_LAUNCH();
     }
     if (mark(2)) return -1;
@@ -1708,7 +1781,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],        \
                        W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a, W.rec, P.loc_ptr,       \
                        P.loc_con, P.loc_w, P.b, W.cvs, W.par, ctrl_cur, W.part, nblkA, W.partB,                    \
-                       P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off)
+                       P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, pb[k].T)
         const bool small = pb[k].small;
         LRS_LAYOUT_SWITCH(c.G, c.E, {
             if (small) LRS_LAUNCH_B(4);

@@ -373,6 +373,8 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             }
     }
     dp.mg = (int)glob.size();
+    dp.glob_maxlen = 0;
+    for (int i : glob) dp.glob_maxlen = std::max(dp.glob_maxlen, nent[i]);
     if (glob.empty()) glob.push_back(0);
     if (loc_con.empty()) { loc_con.push_back(0); loc_w.push_back(0.0); }
     if (!dput(&dp.glob, glob, err) || !dput(&dp.loc_ptr, loc_ptr, err) || !dput(&dp.loc_con, loc_con, err) ||
