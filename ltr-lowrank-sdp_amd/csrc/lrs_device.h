@@ -75,6 +75,7 @@ enum LsIdx { LS_TAU = 0, LS_ROOTNUM, LS_FLAG, LS_N = 4 };
 // ---- finals of the standalone launchers (g_tmpfin offsets)
 enum TmpFinIdx { TF_SD = 0, TF_GATHER = 128, TF_RESID = 129, TF_DOT = 130, TF_SPMM = 131, TF_N = 256 };
 constexpr int kMaxCones = 64;
+constexpr int kLongRow = 32;         // constraint rows longer than this get a wave each
 
 struct Layout {
     int G = 1, E = 1, ld = 1;
@@ -107,7 +108,9 @@ struct DevProblem {
     int *loc_ptr = nullptr, *loc_con = nullptr;              // [Ptot+1], [m - mg]
     double *loc_w = nullptr;                                 // (2 - delta) a of that one entry
     int *slot_rc = nullptr;                                  // [Ptot][2] (row, col) in the cone
-    int *con1_pq = nullptr;                                  // [K*m][2] single-entry rows: (p, q) or -1
+    int *con1_pq = nullptr;                                  // [K*m][2] single-entry rows: (p, q); -1 other; -2 long
+    int *long_rows = nullptr;                                // constraints with > kLongRow entries in a cone,
+    std::vector<int> long_ptr_h;                             //   grouped by cone: long_ptr_h[k]..[k+1]
     double *con1_w = nullptr;                                // [K*m] their weight
     std::vector<DevCone> cones;
 };
@@ -130,6 +133,7 @@ struct DevWork {
     double *par = nullptr;     // [P_NPAR]
     double *gram = nullptr;    // gram partials
     double *rec = nullptr;     // [m][4] per-constraint {A(RR^T), q1, q2, -lam - rho b}
+    double *cgc = nullptr;     // [8] device CG control (CgIdx)
 };
 
 // ---------------------------- launchers -----------------------------------
@@ -150,7 +154,8 @@ int launch_gather(const DevProblem &P, const double *uvt, double scale, double *
 // mode 1: X X^T).  out[i] = (accumulate ? out[i] : 0) + scale * value_of_this_cone; optional
 // residual sum (b - out)^2 -> tmpfin TF_GATHER.  Bitwise equal to sddmm + gather_cone.
 int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double scale,
-                   int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st);
+                   int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st,
+                   const double *guard = nullptr);
 // S[slot] = (withC ? Craw[slot] : 0) + sum_(con,a) w[con] * a
 int launch_wsum(const DevProblem &P, const double *w, int withC, double *S, hipStream_t st);
 // out = scale * S X (+ addX * X) per cone, partial ||out||^2 -> part[0][pblk_off+b]
@@ -180,6 +185,20 @@ struct AlmIterArgs {
 int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st);
 // a subset of the stages (mask bit 0 = A, 1 = G, 2 = B), for per-stage timing
 int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t st);
+
+// ---- device-resident CG (lrs_kernels.hip "Device-resident CG") ----
+enum CgIdx { CG_ACTIVE = 0, CG_ITERS, CG_BNORM, CG_RR, CG_QTR0, CG_QTR1, CG_N = 8 };
+int launch_cg_mv(const DevProblem &P, int cone, const double *w, const double *V, const double *Xin, double *Q,
+                 double *part, const double *cgc, int guarded, hipStream_t st, int *nblk);
+int launch_cg_nrm1(long nr, const double *b, double *part, hipStream_t st, int *nblk);
+int launch_cg_upd(long nr, double *X, double *r, const double *p, const double *Q, const double *partB, int nblkB,
+                  double *partC, double *cgc, int par, int it, hipStream_t st, int *nblk);
+int launch_cg_conv(long nr, const double *r, double *p, const double *partC, int nblkC, double *cgc, double tol,
+                   int par, int restart, hipStream_t st);
+int launch_cg_resid(long nr, const double *b, const double *Q, double *r, double *p, double *partC, double *cgc,
+                    const double *partA, int nblkA, int init, hipStream_t st, int *nblk);
+int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, int nblkC, double *cgc, double tol,
+                     int par, int init, hipStream_t st);
 
 const char *last_device_error();
 // diagnostics build only: copies g_phase[4][16] (returns 64), else returns 0

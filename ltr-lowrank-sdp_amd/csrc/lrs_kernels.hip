@@ -382,7 +382,8 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
                                                     const double *__restrict__ X, const double *__restrict__ Y,
                                                     double scale, int accumulate, double *__restrict__ out,
                                                     const double *__restrict__ b, double *part, unsigned *ticket,
-                                                    double *fin) {
+                                                    double *fin, const double *__restrict__ guard) {
+    if (guard && guard[0] == 0.0) return;
     const int lane = threadIdx.x & (G - 1);
     const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
     const int ngrp = gridDim.x * kBlock / G;
@@ -390,6 +391,7 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
     for (int i = grp; i < m; i += ngrp) {
         const long row = (long)cone * m + i;
         const int2 pq = reinterpret_cast<const int2 *>(con1_pq)[row];
+        if (pq.x == -2) continue;   // long row: k_auv_con_long
         double v = 0.0;
         if (pq.x >= 0) {
             // single-entry row: (p, q, w) in one coalesced load, then the factor rows
@@ -415,6 +417,42 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
         }
     }
     if (part) partials_finalize<1>(acc, part, ticket, fin);
+}
+
+// Long constraint rows (> kLongRow entries in this cone, e.g. a trace constraint): a
+// wave per constraint, its 64/G lane groups striding over the entries.
+template <int G, int E, int MODE>
+__global__ void __launch_bounds__(kBlock) k_auv_con_long(int nlong, const int *__restrict__ long_rows, int m,
+                                                         int cone, int ld, const int *__restrict__ con_ptr,
+                                                         const int *__restrict__ con_slot,
+                                                         const double *__restrict__ con_w,
+                                                         const int *__restrict__ slot_rc,
+                                                         const double *__restrict__ X, const double *__restrict__ Y,
+                                                         double scale, int accumulate, double *__restrict__ out,
+                                                         const double *__restrict__ guard) {
+    if (guard && guard[0] == 0.0) return;
+    constexpr int NG = 64 / G;
+    const int lane = threadIdx.x & (G - 1);
+    const int gq = (threadIdx.x & 63) / G;
+    const int nw = gridDim.x * (kBlock / 64);
+    for (int t = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t < nlong; t += nw) {
+        const int i = long_rows[t];
+        const long row = (long)cone * m + i;
+        const int e0 = con_ptr[row], e1 = con_ptr[row + 1];
+        double v = 0.0;
+        for (int e = e0 + gq; e < e1; e += NG) {
+            const int s = con_slot[e];
+            double d = auv_entry<E, MODE>(X, Y, ld, lane, slot_rc[2 * s], slot_rc[2 * s + 1]);
+            d = group_sum<G>(d);
+            v += con_w[e] * d;
+        }
+        v = wave_sum(lane == 0 ? v : 0.0);
+        if ((threadIdx.x & 63) == 0) {
+            double tot = v * scale;
+            if (accumulate) tot = out[i] + tot;
+            out[i] = tot;
+        }
+    }
 }
 
 // S[slot] = (withC ? Craw : 0) + sum w[con] a
@@ -1454,6 +1492,210 @@ __global__ void __launch_bounds__(kRowBlock) k_it_b(
 }
 
 // ------------------------------------------------------------------------
+// Device-resident CG (CGSolve, linalg/lorads_cgs.c:128-287) for one cone's ADMM
+// half-step system M X = b, M x = x + A^*(A(sym(x V^T))) V (linSysProduct,
+// lorads_admm.c:471-486).  Scalars live in cgc[] (CgIdx); every kernel after the
+// initial residual is guarded by cgc[CG_ACTIVE], so a batch of iterations enqueued
+// past convergence does nothing.  Same partial-sum scheme as the ALM iteration.
+// ------------------------------------------------------------------------
+// sum |b| over the cone's factor rows (bNorm, lorads_cgs.c: nrm1 of the RHS)
+__global__ void __launch_bounds__(kBlock) k_cg_nrm1(long nr, const double *__restrict__ b, double *__restrict__ part) {
+    double acc[1] = {0.0};
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nr; i += (long)gridDim.x * kBlock) acc[0] += fabs(b[i]);
+    write_partials<1>(acc, part, blockIdx.x);
+}
+
+// Q = A^*(w) V + Xin on the cone's rows (S on the fly from the slot lists), optional
+// partial <Xin, Q>.  Teams of T lane groups per row for dense rows (as k_it_b).
+template <int G, int E, int U>
+__global__ void __launch_bounds__(kRowBlock) k_cg_mv(int n, int ld, const int *__restrict__ adj_ptr,
+                                                     const int *__restrict__ adj_col, const int *__restrict__ adj_slot,
+                                                     const int *__restrict__ slot_ptr,
+                                                     const int *__restrict__ slot_con,
+                                                     const double *__restrict__ slot_a, const double *__restrict__ w,
+                                                     const double *__restrict__ V, const double *__restrict__ Xin,
+                                                     double *__restrict__ Q, double *__restrict__ part,
+                                                     const double *__restrict__ cgc, int guarded, int T) {
+    __shared__ double gsh[kRowBlock * E];
+    if (guarded && cgc[CG_ACTIVE] == 0.0) return;
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kRowBlock / G;
+    const int team = grp / T, mem = grp % T, nteams = ngrp / T;
+    const int tpb = (kRowBlock / G) / T;
+    const int team_local = team - blockIdx.x * tpb;
+    double acc[1] = {0.0};
+    for (int ib = blockIdx.x * tpb; ib < n; ib += nteams) {
+        const int i = ib + team_local;
+        const bool valid = i < n;
+        double g[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[e] = 0.0;
+        if (valid) {
+            const int kb = adj_ptr[i], ke = adj_ptr[i + 1];
+            for (int k0 = kb + mem * U; k0 < ke; k0 += T * U) {
+                int jj[U], ss[U], eb[U], ee[U];
+                double yj[U][E], sv[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = min(k0 + u, ke - 1);
+                    jj[u] = adj_col[k];
+                    ss[u] = adj_slot[k];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    ld_row<E>(V + (long)jj[u] * ld + lane * E, yj[u]);
+                    eb[u] = slot_ptr[ss[u]];
+                    ee[u] = slot_ptr[ss[u] + 1];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    // S[slot] = sum_con w[con] a  (sdpDataWSum without C)
+                    double v = 0.0;
+                    for (int e = eb[u]; e < ee[u]; ++e) v += w[slot_con[e]] * slot_a[e];
+                    sv[u] = v;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (k0 + u < ke) {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) g[e] += sv[u] * yj[u][e];
+                    }
+            }
+        }
+        if (T > 1) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) gsh[threadIdx.x * E + e] = g[e];
+            __syncthreads();
+            if (mem == 0 && valid) {
+                const int base = (team_local * T) * G + lane;
+#pragma unroll
+                for (int e = 0; e < E; ++e) g[e] = gsh[base * E + e];
+                for (int t = 1; t < T; ++t)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) g[e] += gsh[(base + t * G) * E + e];
+            }
+            __syncthreads();
+        }
+        if (mem == 0 && valid) {
+            const long oi = (long)i * ld + lane * E;
+            double x[E];
+            ld_row<E>(Xin + oi, x);
+#pragma unroll
+            for (int e = 0; e < E; ++e) { g[e] *= 1.0; g[e] += 1.0 * x[e]; }
+            st_row<E>(Q + oi, g);
+            if (part) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) acc[0] += x[e] * g[e];
+            }
+        }
+    }
+    if (part) write_partials<1, kRowBlock>(acc, part, blockIdx.x);
+}
+
+// alpha = qTr / <p, Q>; X += alpha p; r -= alpha Q; partial <r, r>; ITERS = it + 1
+__global__ void __launch_bounds__(kBlock) k_cg_upd(long nr, double *__restrict__ X, double *__restrict__ r,
+                                                   const double *__restrict__ p, const double *__restrict__ Q,
+                                                   const double *__restrict__ partB, int nblkB,
+                                                   double *__restrict__ partC, double *__restrict__ cgc, int par,
+                                                   int it) {
+    __shared__ double red[1];
+    __shared__ int act;
+    if (threadIdx.x == 0) act = cgc[CG_ACTIVE] != 0.0;
+    __syncthreads();
+    if (!act) return;
+    reduce_partials<1>(partB, nblkB, red);
+    const double alpha = cgc[CG_QTR0 + par] / red[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cgc[CG_ITERS] = it + 1;
+    double acc[1] = {0.0};
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nr; i += (long)gridDim.x * kBlock) {
+        X[i] = alpha * p[i] + 1.0 * X[i];
+        const double ri = -alpha * Q[i] + 1.0 * r[i];
+        r[i] = ri;
+        acc[0] += ri * ri;
+    }
+    write_partials<1>(acc, partC, blockIdx.x);
+}
+
+// convergence test on ||r||_2 / ||b||_1; unless restarting: beta = rr / qTr,
+// p = r + beta p, qTr <- rr (next parity)
+__global__ void __launch_bounds__(kBlock) k_cg_conv(long nr, const double *__restrict__ r, double *__restrict__ p,
+                                                    const double *__restrict__ partC, int nblkC,
+                                                    double *__restrict__ cgc, double tol, int par, int restart) {
+    __shared__ double red[1];
+    __shared__ int act;
+    if (threadIdx.x == 0) act = cgc[CG_ACTIVE] != 0.0;
+    __syncthreads();
+    if (!act) return;
+    reduce_partials<1>(partC, nblkC, red);
+    const double rr = red[0];
+    const double resi = sqrt(rr);
+    if (resi / cgc[CG_BNORM] < tol || resi != resi) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) { cgc[CG_ACTIVE] = 0.0; cgc[CG_RR] = rr; }
+        return;
+    }
+    if (restart) return;
+    const double beta = rr / cgc[CG_QTR0 + par];
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nr; i += (long)gridDim.x * kBlock)
+        p[i] = 1.0 * r[i] + beta * p[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) { cgc[CG_QTR0 + (par ^ 1)] = rr; cgc[CG_RR] = rr; }
+}
+
+// r = b - Q (Q = M X), p = r, partial <r, r>.  init: also bNorm from the nrm1 partials
+__global__ void __launch_bounds__(kBlock) k_cg_resid(long nr, const double *__restrict__ b,
+                                                     const double *__restrict__ Q, double *__restrict__ r,
+                                                     double *__restrict__ p, double *__restrict__ partC,
+                                                     double *__restrict__ cgc, const double *__restrict__ partA,
+                                                     int nblkA, int init) {
+    __shared__ double red[1];
+    __shared__ int act;
+    if (threadIdx.x == 0) act = init || cgc[CG_ACTIVE] != 0.0;
+    __syncthreads();
+    if (!act) return;
+    if (init) {
+        reduce_partials<1>(partA, nblkA, red);
+        if (blockIdx.x == 0 && threadIdx.x == 0) cgc[CG_BNORM] = red[0];
+    }
+    double acc[1] = {0.0};
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nr; i += (long)gridDim.x * kBlock) {
+        const double ri = 1.0 * b[i] + -1.0 * Q[i];
+        r[i] = ri;
+        p[i] = ri;
+        acc[0] += ri * ri;
+    }
+    write_partials<1>(acc, partC, blockIdx.x);
+}
+
+// init: resi test (ACTIVE), qTr[0] = rr.  restart (lorads_cgs.c restart every 20):
+// qTr = rr, beta = rr / qTr, p = r + beta p, qTr[next] = rr
+__global__ void __launch_bounds__(kBlock) k_cg_resid2(long nr, const double *__restrict__ r, double *__restrict__ p,
+                                                      const double *__restrict__ partC, int nblkC,
+                                                      double *__restrict__ cgc, double tol, int par, int init) {
+    __shared__ double red[1];
+    __shared__ int act;
+    if (threadIdx.x == 0) act = init || cgc[CG_ACTIVE] != 0.0;
+    __syncthreads();
+    if (!act) return;
+    reduce_partials<1>(partC, nblkC, red);
+    const double rr = red[0];
+    if (init) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const double resi = sqrt(rr);
+            cgc[CG_ACTIVE] = (resi / cgc[CG_BNORM] < tol) ? 0.0 : 1.0;
+            cgc[CG_QTR0] = rr;
+            cgc[CG_RR] = rr;
+            cgc[CG_ITERS] = 0;
+        }
+        return;
+    }
+    const double qTr = rr;
+    const double beta = rr / qTr;
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < nr; i += (long)gridDim.x * kBlock)
+        p[i] = 1.0 * r[i] + beta * p[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) { cgc[CG_QTR0 + (par ^ 1)] = rr; cgc[CG_RR] = rr; }
+}
+
+// ------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------
 static unsigned *ticket_ptr(int id) {
@@ -1543,22 +1785,40 @@ int launch_gather_cone(const DevProblem &P, int cone, const double *uvt, double 
 }
 
 int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double scale,
-                   int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st) {
+                   int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st,
+                   const double *guard) {
     const DevCone &c = P.cones[cone];
     const int grid = grid_rows(P.m, c.G);
     const double *Xc = X + c.foff;
     const double *Yc = Y ? Y + c.foff : nullptr;
     unsigned *tk = ticket_ptr(T_GATHER);
     double *fin = tmpfin_ptr() + TF_GATHER;
+    const int l0 = P.long_ptr_h.empty() ? 0 : P.long_ptr_h[cone];
+    const int nlong = P.long_ptr_h.empty() ? 0 : P.long_ptr_h[cone + 1] - l0;
+    if (nlong > 0 && b_for_vio) {
+        snprintf(g_err, sizeof(g_err), "auv_con: residual with long constraint rows is not supported");
+        return -1;
+    }
     LRS_LAYOUT_SWITCH(c.G, c.E, {
         if (mode == 1)
             hipLaunchKernelGGL((k_auv_con<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
                                P.con_ptr, P.con_slot, P.con_w, P.slot_rc, P.con1_pq, P.con1_w, Xc, Yc, scale,
-                               accumulate, out, b_for_vio, vio_part, tk, fin);
+                               accumulate, out, b_for_vio, vio_part, tk, fin, guard);
         else
             hipLaunchKernelGGL((k_auv_con<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
                                P.con_ptr, P.con_slot, P.con_w, P.slot_rc, P.con1_pq, P.con1_w, Xc, Yc, scale,
-                               accumulate, out, b_for_vio, vio_part, tk, fin);
+                               accumulate, out, b_for_vio, vio_part, tk, fin, guard);
+        if (nlong > 0) {
+            const int gl = std::min((nlong + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks);
+            if (mode == 1)
+                hipLaunchKernelGGL((k_auv_con_long<GG, EE, 1>), dim3(gl), dim3(kBlock), 0, st, nlong,
+                                   P.long_rows + l0, P.m, cone, c.ld, P.con_ptr, P.con_slot, P.con_w, P.slot_rc, Xc,
+                                   Yc, scale, accumulate, out, guard);
+            else
+                hipLaunchKernelGGL((k_auv_con_long<GG, EE, 0>), dim3(gl), dim3(kBlock), 0, st, nlong,
+                                   P.long_rows + l0, P.m, cone, c.ld, P.con_ptr, P.con_slot, P.con_w, P.slot_rc, Xc,
+                                   Yc, scale, accumulate, out, guard);
+        }
     });
     LRS_CHECK_LAUNCH();
     return 0;
@@ -1883,6 +2143,69 @@ int launch_alm_dir_only(const DevProblem &P, DevWork &W, hipStream_t st) {
     hipLaunchKernelGGL(k_alm_dir, dim3(grid_elems(P.NRpad, 2)), dim3(kBlock), 0, st, P.NRpad, W.par,
                        W.ctrl + C_NCTRL, W.ctrl, W.lsres + LS_N, P.K, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
                        W.ls[1], W.ly[1]);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+// ---- device CG launchers
+static StagePlan plan_cg_mv(const DevCone &c) {
+    const double deg = c.n > 0 ? (double)c.adj_nnz / c.n : 0.0;
+    const int T = team_size(c, deg, 4);
+    StagePlan p;
+    p.T = T;
+    const long need = std::max(1L, ((long)c.n * c.G * T + kRowBlock - 1) / kRowBlock);
+    p.grid = (int)std::min<long>(need, kMaxPartialBlocks);
+    p.small = true;
+    return p;
+}
+int launch_cg_mv(const DevProblem &P, int cone, const double *w, const double *V, const double *Xin, double *Q,
+                 double *part, const double *cgc, int guarded, hipStream_t st, int *nblk) {
+    const DevCone &c = P.cones[cone];
+    const StagePlan pl = plan_cg_mv(c);
+    LRS_LAYOUT_SWITCH(c.G, c.E, {
+        hipLaunchKernelGGL((k_cg_mv<GG, EE, 4>), dim3(pl.grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.adj_ptr,
+                           c.adj_col, c.adj_slot, P.slot_ptr, P.slot_con, P.slot_a, w, V + c.foff, Xin + c.foff,
+                           Q + c.foff, part, cgc, guarded, pl.T);
+    });
+    LRS_CHECK_LAUNCH();
+    if (nblk) *nblk = pl.grid;
+    return 0;
+}
+static inline int cg_grid(long nr) { return std::min(grid_elems(nr, 2), 1024); }
+int launch_cg_nrm1(long nr, const double *b, double *part, hipStream_t st, int *nblk) {
+    const int g = cg_grid(nr);
+    hipLaunchKernelGGL(k_cg_nrm1, dim3(g), dim3(kBlock), 0, st, nr, b, part);
+    LRS_CHECK_LAUNCH();
+    *nblk = g;
+    return 0;
+}
+int launch_cg_upd(long nr, double *X, double *r, const double *p, const double *Q, const double *partB, int nblkB,
+                  double *partC, double *cgc, int par, int it, hipStream_t st, int *nblk) {
+    const int g = cg_grid(nr);
+    hipLaunchKernelGGL(k_cg_upd, dim3(g), dim3(kBlock), 0, st, nr, X, r, p, Q, partB, nblkB, partC, cgc, par, it);
+    LRS_CHECK_LAUNCH();
+    *nblk = g;
+    return 0;
+}
+int launch_cg_conv(long nr, const double *r, double *p, const double *partC, int nblkC, double *cgc, double tol,
+                   int par, int restart, hipStream_t st) {
+    hipLaunchKernelGGL(k_cg_conv, dim3(cg_grid(nr)), dim3(kBlock), 0, st, nr, r, p, partC, nblkC, cgc, tol, par,
+                       restart);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int launch_cg_resid(long nr, const double *b, const double *Q, double *r, double *p, double *partC, double *cgc,
+                    const double *partA, int nblkA, int init, hipStream_t st, int *nblk) {
+    const int g = cg_grid(nr);
+    hipLaunchKernelGGL(k_cg_resid, dim3(g), dim3(kBlock), 0, st, nr, b, Q, r, p, partC, cgc, partA, nblkA, init);
+    LRS_CHECK_LAUNCH();
+    *nblk = g;
+    return 0;
+}
+int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, int nblkC, double *cgc, double tol,
+                     int par, int init, hipStream_t st) {
+    hipLaunchKernelGGL(k_cg_resid2, dim3(cg_grid(nr)), dim3(kBlock), 0, st, nr, r, p, partC, nblkC, cgc, tol, par,
+                       init);
     LRS_CHECK_LAUNCH();
     return 0;
 }

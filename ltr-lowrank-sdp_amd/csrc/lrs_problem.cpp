@@ -333,6 +333,21 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         const long rows = (long)hp.K * m;
         std::vector<int> c1pq(2 * std::max(1L, rows), -1);
         std::vector<double> c1w(std::max(1L, rows), 0.0);
+        // long rows (> kLongRow entries) go to the wave-per-constraint kernel: p = -2
+        std::vector<int> long_ptr(hp.K + 1, 0), long_rows;
+        for (int k = 0; k < hp.K; ++k) {
+            for (int i = 0; i < m; ++i) {
+                const long r = (long)k * m + i;
+                if (con_ptr[r + 1] - con_ptr[r] > kLongRow) {
+                    long_rows.push_back(i);
+                    c1pq[2 * r] = -2;
+                }
+            }
+            long_ptr[k + 1] = (int)long_rows.size();
+        }
+        dp.long_ptr_h = long_ptr;
+        if (long_rows.empty()) long_rows.push_back(0);
+        if (!dput(&dp.long_rows, long_rows, err)) return false;
         for (long r = 0; r < rows; ++r) {
             if (con_ptr[r + 1] - con_ptr[r] != 1) continue;
             const int e = con_ptr[r];
@@ -402,7 +417,7 @@ void free_problem(DevProblem &dp) {
     auto f = [](void *p) { if (p) (void)hipFree(p); };
     f(dp.b); f(dp.Cw); f(dp.Craw); f(dp.con_ptr); f(dp.con_slot); f(dp.con_w);
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
-    f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w);
+    f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); }
     dp = DevProblem();
 }

@@ -171,7 +171,8 @@ static void free_work(lrs_ctx *c) {
     DevWork &W = c->W;
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
-                      W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2};
+                      W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2,
+                      W.cgc};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     c->W = DevWork();
@@ -230,7 +231,7 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         A(&W.M1, m) || A(&W.wtmp, m) || A(&W.cvc, (long)m * std::max(1, P.K)) ||
         A(&W.part, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.partB, (long)kMaxPartialVals * kMaxPartialBlocks) ||
         A(&W.partC, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.ctrl, 2 * C_NCTRL) ||
-        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax) || A(&W.rec, 4L * m) || A(&W.R2, NR))
+        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax) || A(&W.rec, 4L * m) || A(&W.R2, NR) || A(&W.cgc, 8))
         return -1;
     HIPC(hipStreamSynchronize(c->st));
     c->walloc = true;
@@ -867,64 +868,47 @@ static int lin_sys_product(lrs_ctx *c, int k, const double *Y, const double *x, 
     return 0;
 }
 
-static int cone_dot(lrs_ctx *c, int k, const double *x, const double *y, double *out) {
-    const DevCone &d = c->dp.cones[k];
-    return op_dot(c, (long)d.n * d.ld, x + d.foff, y + d.foff, out);
-}
-static int cone_nrm1(lrs_ctx *c, int k, const double *x, double *out) {
-    const DevCone &d = c->dp.cones[k];
-    std::vector<double> h((long)d.n * d.ld);
-    HIPC(hipStreamSynchronize(c->st));
-    HIPC(hipMemcpy(h.data(), x + d.foff, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
-    double s = 0;
-    for (double v : h) s += std::fabs(v);
-    *out = s;
-    return 0;
-}
-
-// CGSolve, linalg/lorads_cgs.c:128-287
+// CGSolve (linalg/lorads_cgs.c:128-287) on the device: initial residual, then batches of
+// iterations (4 launches each; the restart every 20 iterations adds 4) with all scalars
+// in W.cgc; one poll per batch.
 static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double *b, double tol, int maxit) {
+    DevProblem &P = c->dp;
     DevWork &W = c->W;
-    const DevCone &d = c->dp.cones[k];
+    const DevCone &d = P.cones[k];
     const long nr = (long)d.n * d.ld;
     double *r = W.cg_r + d.foff, *p = W.cg_p + d.foff, *Q = W.cg_Q + d.foff;
     double *xk = X + d.foff;
     const double *bk = b + d.foff;
-    double bNorm;
-    if (cone_nrm1(c, k, b, &bNorm)) return -1;
-    if (lin_sys_product(c, k, Y, X, W.cg_r)) return -1;
-    OPC(launch_axpby(nr, 1.0, bk, -1.0, r, c->st));   // r = b - r
-    double rr;
-    if (op_dot(c, nr, r, r, &rr)) return -1;
-    double resi = std::sqrt(rr);
-    if (resi / bNorm < tol) return 0;
-    HIPC(hipMemcpyAsync(p, r, sizeof(double) * nr, hipMemcpyDeviceToDevice, c->st));
-    double qTr = rr;
-    c->cgIterCone[k] = 0;
-    for (int it = 0; it < maxit; ++it) {
-        c->cgIterCone[k] += 1;
-        if (lin_sys_product(c, k, Y, W.cg_p, W.cg_Q)) return -1;
-        double pTQ;
-        if (op_dot(c, nr, p, Q, &pTQ)) return -1;
-        const double alpha = qTr / pTQ;
-        OPC(launch_axpby(nr, alpha, p, 1.0, xk, c->st));
-        OPC(launch_axpby(nr, -alpha, Q, 1.0, r, c->st));
-        if (op_dot(c, nr, r, r, &rr)) return -1;
-        resi = std::sqrt(rr);
-        if (resi / bNorm < tol) return 0;
-        if (it % 20 == 0) {
-            if (lin_sys_product(c, k, Y, X, W.cg_r)) return -1;
-            OPC(launch_axpby(nr, 1.0, bk, -1.0, r, c->st));
-            HIPC(hipMemcpyAsync(p, r, sizeof(double) * nr, hipMemcpyDeviceToDevice, c->st));
-            if (op_dot(c, nr, r, r, &rr)) return -1;
-            qTr = rr;
+    double *cgc = W.cgc;
+    int nA = 0, nB = 0, nC = 0, nR = 0;
+    OPC(launch_cg_nrm1(nr, bk, W.part, c->st, &nA));
+    OPC(launch_auv_con(P, k, 0, X, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, nullptr));
+    OPC(launch_cg_mv(P, k, W.wtmp, Y, X, W.cg_Q, nullptr, cgc, 0, c->st, &nB));
+    OPC(launch_cg_resid(nr, bk, Q, r, p, W.partC, cgc, W.part, nA, 1, c->st, &nC));
+    OPC(launch_cg_resid2(nr, r, p, W.partC, nC, cgc, tol, 0, 1, c->st));
+    double *h = c->hpin + 256;
+    int it = 0, B = 8;
+    while (it < maxit) {
+        for (int j = 0; j < B && it < maxit; ++j, ++it) {
+            const int par = it & 1;
+            OPC(launch_auv_con(P, k, 0, W.cg_p, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, cgc));
+            OPC(launch_cg_mv(P, k, W.wtmp, Y, W.cg_p, W.cg_Q, W.partB, cgc, 1, c->st, &nB));
+            OPC(launch_cg_upd(nr, xk, r, p, Q, W.partB, nB, W.partC, cgc, par, it, c->st, &nC));
+            const int restart = (it % 20 == 0);
+            OPC(launch_cg_conv(nr, r, p, W.partC, nC, cgc, tol, par, restart, c->st));
+            if (restart) {
+                OPC(launch_auv_con(P, k, 0, X, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, cgc));
+                OPC(launch_cg_mv(P, k, W.wtmp, Y, X, W.cg_Q, nullptr, cgc, 1, c->st, &nB));
+                OPC(launch_cg_resid(nr, bk, Q, r, p, W.partC, cgc, nullptr, 0, 0, c->st, &nR));
+                OPC(launch_cg_resid2(nr, r, p, W.partC, nR, cgc, tol, par, 0, c->st));
+            }
         }
-        const double qTrNew = rr;
-        const double beta = qTrNew / qTr;
-        OPC(launch_axpby(nr, 1.0, r, beta, p, c->st));   // p = beta p + r
-        qTr = qTrNew;
-        if (resi != resi) break;
+        HIPC(hipMemcpyAsync(h, cgc, sizeof(double) * CG_N, hipMemcpyDeviceToHost, c->st));
+        HIPC(hipStreamSynchronize(c->st));
+        if (h[CG_ACTIVE] == 0.0) break;
+        B = std::min(2 * B, 64);
     }
+    c->cgIterCone[k] = (long)h[CG_ITERS];
     return 0;
 }
 
@@ -947,8 +931,7 @@ static int refresh_cone(lrs_ctx *c, int k) {   // lorads_alg_common.c:310-314
     DevWork &W = c->W;
     double *cv = W.cvc + (long)k * P.m;
     OPC(launch_axpby(P.m, -1.0, cv, 1.0, W.cvs, c->st));
-    OPC(launch_sddmm(P, k, 0, W.U, W.V, W.uvt2, nullptr, W.part, 0, nullptr, c->st));
-    OPC(launch_gather_cone(P, k, W.uvt2, cv, c->st));
+    OPC(launch_auv_con(P, k, 0, W.U, W.V, 1.0, 0, cv, nullptr, nullptr, c->st));
     OPC(launch_axpby(P.m, 1.0, cv, 1.0, W.cvs, c->st));
     return 0;
 }
@@ -999,8 +982,7 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
         DevProblem &P = c->dp;
         OPC(launch_fill(P.m, 0.0, c->W.cvs, c->st));
         for (int k = 0; k < P.K; ++k) {
-            OPC(launch_sddmm(P, k, 0, c->W.U, c->W.V, c->W.uvt2, nullptr, c->W.part, 0, nullptr, c->st));
-            OPC(launch_gather_cone(P, k, c->W.uvt2, c->W.cvc + (long)k * P.m, c->st));
+            OPC(launch_auv_con(P, k, 0, c->W.U, c->W.V, 1.0, 0, c->W.cvc + (long)k * P.m, nullptr, nullptr, c->st));
             OPC(launch_axpby(P.m, 1.0, c->W.cvc + (long)k * P.m, 1.0, c->W.cvs, c->st));
         }
     }
