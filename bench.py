@@ -17,6 +17,8 @@ Prints one JSON line (rank 0).  Besides the contract keys:
                     far beyond the 256 MB Infinity Cache), where HBM bandwidth binds
   north_star        MaxCut n = 20 000, r = 64 (G81-like): device vs reference CPU it/s
   wall_clock_to_eps full ALM + ADMM solve to eps = 1e-5 with the Gset flags
+  configs_wall_clock_to_eps  G1, G22, theta3 (and a 3-block theta3) solved to eps, device vs
+                    the reference, with benchmark.py's flags per subtype
   cpu_baseline      the reference LoRADS C (oracle/_ref, built from /root/reference)
                     timed on this host, 1 core, on a bounded sample of the workload
 """
@@ -120,6 +122,7 @@ def main():
     ap.add_argument("--no-eps", action="store_true")
     ap.add_argument("--no-scale", action="store_true")
     ap.add_argument("--no-north-star", action="store_true")
+    ap.add_argument("--no-configs", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -210,6 +213,30 @@ def main():
             ns["cpu_kind"] = kind
             ns["speedup"] = ns["gpu_it_s"] / ns["cpu_it_s"]
         line["north_star"] = ns
+    if rank_id == 0 and world == 1 and not args.no_configs:
+        # the other BASELINE.json configs as whole solves to eps = 1e-5 with benchmark.py's
+        # flags for their subtype (get_lorads_params, benchmark.py:136-200), device vs reference
+        inst = importlib.import_module(PKG + ".instances")
+        gset = {"reoptLevel": 0, "heuristicFactor": 10.0, "phase1Tol": 1e-2, "rhoMax": 5000.0}
+        sdplib = {"reoptLevel": 0, "heuristicFactor": 1.0, "phase1Tol": 1e-3, "rhoMax": 5000.0}
+        rows = []
+        for name, flags in (("G1", gset), ("G22", gset), ("theta3", sdplib), ("theta3x3", sdplib)):
+            pth = inst.config_instance(name, cache)
+            s1 = solver.Solver(pth, device=local)
+            res = s1.solve(**flags)
+            s1.close()
+            row = {"config": name, "gpu_solve_s": res["solve_time"], "alm_inner": res["alm_inner"],
+                   "admm_iter": res["admm_iter"], "primal_obj": res["pobj"], "gap": res["gap"], "pinf": res["pinf"]}
+            if not args.no_cpu:
+                cli = []
+                for k, v in flags.items():
+                    cli += [f"--{k}", str(v)]
+                ref = cpu_reference_solve(pth, cli, timeout=300)
+                if ref:
+                    row["cpu_solve_s"] = ref["solve_time_sec"]
+                    row["speedup"] = ref["solve_time_sec"] / res["solve_time"]
+            rows.append(row)
+        line["configs_wall_clock_to_eps"] = rows
     if rank_id == 0 and world == 1 and not args.no_scale:
         # roofline at scale: 2000 x 2000 torus built in memory (lrs_load_coo), rank 16
         inst = importlib.import_module(PKG + ".instances")

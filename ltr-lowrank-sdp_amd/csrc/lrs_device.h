@@ -113,6 +113,10 @@ struct DevProblem {
     std::vector<int> long_ptr_h;                             //   grouped by cone: long_ptr_h[k]..[k+1]
     double *con1_w = nullptr;                                // [K*m] their weight
     std::vector<DevCone> cones;
+    // K > 1: all cones as one block-diagonal row space (global rows and columns); used by
+    // the split iteration when every cone has the same (G, E) row layout
+    DevCone merged;
+    bool has_merged = false;
 };
 
 // Scratch shared by the kernels of one solve.

@@ -1984,10 +1984,22 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     double *ls_prev = W.lsres + (parity ^ 1) * LS_N;
     double *ls_cur = W.lsres + parity * LS_N;
     const int L = 2;
+    // one launch over the merged row space when every cone has the same row layout
+    bool merge = P.K > 1 && P.has_merged;
+    for (int k = 1; k < P.K && merge; ++k)
+        merge = P.cones[k].G == P.cones[0].G && P.cones[k].E == P.cones[0].E && P.cones[k].ld == P.cones[0].ld;
+    DevCone mc;
+    if (merge) {
+        mc = P.merged;
+        mc.G = P.cones[0].G; mc.E = P.cones[0].E; mc.ld = P.cones[0].ld; mc.r = P.cones[0].r;
+        mc.foff = 0;
+    }
+    const int KL = merge ? 1 : P.K;                       // launches per stage
+    auto cone_of = [&](int k) -> const DevCone & { return merge ? mc : P.cones[k]; };
     StagePlan pa[kMaxCones], pb[kMaxCones];
     int nblkA = 0, nblkB = 0;
-    for (int k = 0; k < P.K; ++k) {
-        if (plan_a(P.cones[k], P.K, pa[k]) || plan_b(P.cones[k], P.K, pb[k])) return -1;
+    for (int k = 0; k < KL; ++k) {
+        if (plan_a(cone_of(k), KL, pa[k]) || plan_b(cone_of(k), KL, pb[k])) return -1;
         nblkA += pa[k].grid;
         nblkB += pb[k].grid;
     }
@@ -2002,8 +2014,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     if (mark(0)) return -1;
     // A: control, direction, sym(RD^T) / DD^T, local constraints' q and dots
     int off = 0;
-    for (int k = 0; k < P.K && (mask & 1); ++k) {
-        const DevCone &c = P.cones[k];
+    for (int k = 0; k < KL && (mask & 1); ++k) {
+        const DevCone &c = cone_of(k);
         const int grid = pa[k].grid;
 #define LRS_LAUNCH_A(UU)                                                                                   \
     hipLaunchKernelGGL((k_it_a<GG, EE, UU>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr, \
@@ -2033,8 +2045,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     if (mark(2)) return -1;
     // B: line search, R update, adjoint, gradient, A(RR^T), L-BFGS pair, dots
     off = 0;
-    for (int k = 0; k < P.K && (mask & 4); ++k) {
-        const DevCone &c = P.cones[k];
+    for (int k = 0; k < KL && (mask & 4); ++k) {
+        const DevCone &c = cone_of(k);
         const int grid = pb[k].grid;
 #define LRS_LAUNCH_B(UU)                                                                                   \
     hipLaunchKernelGGL((k_it_b<GG, EE, UU>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr, \

@@ -399,6 +399,36 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         !dput(&dp.con_ptr, con_ptr, err) || !dput(&dp.con_slot, con_slot, err) || !dput(&dp.con_w, con_w, err) ||
         !dput(&dp.slot_ptr, slot_ptr, err) || !dput(&dp.slot_con, slot_con, err) || !dput(&dp.slot_a, slot_a, err))
         return false;
+    // all cones as one block-diagonal row space (global rows, global columns): the split
+    // iteration launches once over it when every cone has the same row layout
+    if (hp.K > 1) {
+        DevCone &mc = dp.merged;
+        long ntot = 0, nadj = 0, Ptot_l = 0;
+        for (auto &c : hp.cones) { ntot += c.n; nadj += (long)c.adj_col.size(); Ptot_l += (long)c.prow.size(); }
+        std::vector<int> ap(ntot + 1, 0), al(ntot, 0), ac(nadj, 0), as(nadj, 0);
+        long r0 = 0, e0 = 0;
+        for (int k = 0; k < hp.K; ++k) {
+            const HostCone &c = hp.cones[k];
+            for (int i = 0; i < c.n; ++i) {
+                ap[r0 + i] = (int)(e0 + c.adj_ptr[i]);
+                al[r0 + i] = (int)(e0 + c.adj_low[i]);
+            }
+            for (size_t t = 0; t < c.adj_col.size(); ++t) {
+                ac[e0 + t] = (int)(r0 + c.adj_col[t]);
+                as[e0 + t] = dp.cones[k].slot_off + c.adj_slot[t];
+            }
+            r0 += c.n;
+            e0 += (long)c.adj_col.size();
+        }
+        ap[ntot] = (int)e0;
+        mc.n = (int)ntot;
+        mc.P = (int)Ptot_l;
+        mc.adj_nnz = nadj;
+        if (!dput(&mc.adj_ptr, ap, err) || !dput(&mc.adj_low, al, err) || !dput(&mc.adj_col, ac, err) ||
+            !dput(&mc.adj_slot, as, err))
+            return false;
+        dp.has_merged = true;
+    }
     for (int k = 0; k < hp.K; ++k) {
         const HostCone &c = hp.cones[k];
         DevCone &d = dp.cones[k];
@@ -419,6 +449,7 @@ void free_problem(DevProblem &dp) {
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); }
+    if (dp.has_merged) { f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot); }
     dp = DevProblem();
 }
 
