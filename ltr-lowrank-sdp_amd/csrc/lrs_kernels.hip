@@ -1308,7 +1308,7 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
 // constraints' values and residual (primalInfeasibility), the L-BFGS pair s = tau D,
 // y = G_new - G_old (setlbfgsHisTwo :842-863) and nine dots.  Partials written (10).
 template <int G, int E, int U>
-__global__ void __launch_bounds__(kRowBlock) k_it_b(
+__global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
     const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0, double *s1, double *y1,
