@@ -187,6 +187,8 @@ struct AlmIterArgs {
 };
 // Four launches per inner iteration (lrs_kernels.hip "split iteration").
 int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st);
+// whether stage A is split into direction + SDDMM launches (bandwidth regime)
+bool alm_stage_a_split(const DevProblem &P);
 // a subset of the stages (mask bit 0 = A, 1 = G, 2 = B), for per-stage timing
 int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t st);
 

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <algorithm>
 
 #include "lrs_device.h"
@@ -862,6 +863,18 @@ __device__ __forceinline__ void write_partials(double (&acc)[NV], double *__rest
     }
 }
 
+template <int NV, int NT = kBlock>
+__device__ __forceinline__ void write_partials_range(double (&acc)[NV], double *__restrict__ part, int slot, int v0,
+                                                     int v1) {
+    double s[NV];
+    block_reduce<NV, NT>(acc, s);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (v >= v0 && v < v1) part[v * kMaxPartialBlocks + slot] = s[v];
+    }
+}
+
 // all threads; generic nblk
 template <int NV, int NT = kBlock>
 __device__ __forceinline__ void reduce_partials(const double *__restrict__ part, int nblk, double *out) {
@@ -1060,7 +1073,11 @@ constexpr int kRowBlock = 512;   // threads per block of the row kernels S1 / S4
 //
 // A.  Partials written (8): objective part of <C, sym RD^T>, of <C, DD^T>, the five
 //     line-search dots over the local constraints, residual of the global ones.
-template <int G, int E, int U>
+// MODE 0: the whole stage (latency regime).  Bandwidth regime (large n), split in two
+// launches over the same grid: MODE 1 = control + D of the own rows (+ global residual,
+// partial 7), MODE 2 = SDDMM with D read back instead of recomputed per neighbour,
+// local constraints (partials 0..6).
+template <int G, int E, int U, int MODE>
 __global__ void __launch_bounds__(kRowBlock) k_it_a(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
@@ -1079,16 +1096,22 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
     __shared__ double lsv[2];
     LRS_TS(0, 0);
     LRS_BLK_BEGIN();
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int fold = 0;
+    if constexpr (MODE == 2) {
+        // second half of a split stage: the control the first half wrote
+        if (threadIdx.x < C_NCTRL) c[threadIdx.x] = ctrl_cur[threadIdx.x];
+        __syncthreads();
+    } else {
     if (threadIdx.x < C_NCTRL) c[threadIdx.x] = ctrl_prev[threadIdx.x];
     if (threadIdx.x == 0) { lsv[0] = ls_prev[LS_FLAG]; lsv[1] = ls_prev[LS_TAU]; }
     __syncthreads();
     LRS_TS(0, 1);
-    const int fold = (c[C_ACT2] != 0.0 && c[C_PENDING] == 1.0 && lsv[0] == 0.0) ? 1 : 0;
+    fold = (c[C_ACT2] != 0.0 && c[C_PENDING] == 1.0 && lsv[0] == 0.0) ? 1 : 0;
     if (fold) reduce_partials<10, kRowBlock>(partC, nblkC, red);
     else __syncthreads();   // every wave has read c[] before thread 0 rewrites it
     LRS_TS(0, 2);
     if (threadIdx.x == 0) ctrl_step(c, par, lsv[0], lsv[1], fold, red, mg == 0);
-    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (fold && do_glob) {
         // global constraints: A(RR^T) from the slots and their residual (primalInfeasibility);
         // independent of this iteration's control, so it runs beside ctrl_step.  Long
@@ -1130,8 +1153,13 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
     __syncthreads();
     LRS_TS(0, 3);
     if (pblk_off == 0 && blockIdx.x == 0 && threadIdx.x < C_NCTRL) ctrl_cur[threadIdx.x] = c[threadIdx.x];
+    }   // MODE != 2
     const bool active = c[C_ACTIVE] != 0.0;
-    if (!active && !(fold && mg > 0)) return;
+    if constexpr (MODE == 2) {
+        if (!active) return;
+    } else {
+        if (!active && !(fold && mg > 0)) return;
+    }
     LRS_TS(0, 4);
     if (active) {
         DirCoef kc;
@@ -1153,13 +1181,16 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
             const long oi = (long)i * ld + lane * E;
             const int kb = adj_ptr[i], ke = adj_low[i];
             double xi[E], yi[E];
-            ld_row<E>(R + oi, xi);
-            {
+            if constexpr (MODE == 2) {
+                ld_row<E>(D + oi, yi);
+            } else {
                 DirRow<E> dr;
                 dr.load(kc, Gc, s0, y0, s1, y1, oi);
                 dr.eval(kc, yi);
+                if (mem == 0) st_row<E>(D + oi, yi);
+                if constexpr (MODE == 1) continue;   // the direction only
             }
-            if (mem == 0) st_row<E>(D + oi, yi);
+            ld_row<E>(R + oi, xi);
             // lower entries U at a time: the neighbours' operand loads in flight together
             // (indices clamped to the row; the extra lanes' results are not stored); the
             // team's members take interleaved chunks of U
@@ -1175,11 +1206,15 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const long oj = (long)jj[u] * ld + lane * E;
-                    DirRow<E> dj;
                     ld_row<E>(R + oj, xj[u]);
-                    dj.load(kc, Gc, s0, y0, s1, y1, oj);
                     cw[u] = Cw[ss[u]];
-                    dj.eval(kc, yj[u]);
+                    if constexpr (MODE == 2) {
+                        ld_row<E>(D + oj, yj[u]);
+                    } else {
+                        DirRow<E> dj;
+                        dj.load(kc, Gc, s0, y0, s1, y1, oj);
+                        dj.eval(kc, yj[u]);
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -1222,7 +1257,9 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
         }
     }
     LRS_TS(0, 5);
-    write_partials<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x);
+    if constexpr (MODE == 0) write_partials<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x);
+    else if constexpr (MODE == 1) write_partials_range<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x, 7, 8);
+    else write_partials_range<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x, 0, 7);
     LRS_TS_END(0, 6);
     LRS_BLK_END(0);
 }
@@ -1379,6 +1416,9 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
         for (int e = 0; e < E; ++e) ri[e] += tau * di[e];
         if (mem == 0) st_row<E>(Rn + oi, ri);
         const int kb = adj_ptr[i], kl = adj_low[i], ke = adj_ptr[i + 1];
+#ifdef LRS_PHASE_TIMING
+        if (threadIdx.x == 0 && ib == blockIdx.x * tpb && kb >= 0 && ri[0] != 12345.678) LRS_TS(2, 6);
+#endif
         // neighbours U at a time (indices clamped to the row; extra lanes add 0)
         for (int k0 = kb + mem * U; k0 < ke; k0 += T * U) {
             int jj[U], ss[U];
@@ -1412,6 +1452,10 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
 #pragma unroll
                 for (int e = 0; e < E; ++e) rj[u][e] += tau * dj[u][e];
             }
+#ifdef LRS_PHASE_TIMING
+            if (threadIdx.x == 0 && ib == blockIdx.x * tpb && rj[0][0] != 12345.678 && sv[0] != 12345.678)
+                LRS_TS(2, k0 == kb ? 7 : 9);
+#endif
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int k = k0 + u;
@@ -1436,6 +1480,9 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
                     }
                 }
             }
+#ifdef LRS_PHASE_TIMING
+            if (threadIdx.x == 0 && ib == blockIdx.x * tpb && acc[9] != 12345.678) LRS_TS(2, k0 == kb ? 8 : 10);
+#endif
         }
     }   // valid
     if (T > 1) {
@@ -1463,6 +1510,9 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
         st_row<E>(Gnew + oi, g);
         st_row<E>(sh + oi, sv);
         st_row<E>(yh + oi, yv);
+#ifdef LRS_PHASE_TIMING
+        if (threadIdx.x == 0 && ib == blockIdx.x * tpb && go[0] != 12345.678) LRS_TS(2, 11);
+#endif
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             acc[0] += g[e] * g[e];
@@ -1488,6 +1538,10 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     LRS_TS(2, 3);
     write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
     LRS_TS_END(2, 4);
+#ifdef LRS_PHASE_TIMING
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int q_ = 5; q_ < 12; ++q_) g_phase[2][q_] = g_phase_tmp[2][q_];
+#endif
     LRS_BLK_END(2);
 }
 
@@ -1925,7 +1979,7 @@ static int resident_blocks(KernelT kern, int *cache) {
 template <int GG, int EE, int UU>
 static int res_a() {
     static int c = 0;
-    return resident_blocks(k_it_a<GG, EE, UU>, &c);
+    return resident_blocks(k_it_a<GG, EE, UU, UU == 1 ? 2 : 0>, &c);
 }
 template <int GG, int EE, int UU>
 static int res_b() {
@@ -1947,11 +2001,24 @@ static int team_size(const DevCone &c, double deg, int U) {
     while (T * 2 <= kRowBlock / c.G && (double)(T * 2 * U * 2) <= deg && (long)c.n * T * 2 * c.G <= cap_threads) T *= 2;
     return T;
 }
+// LRS_FORCE_REGIME=small|large overrides the choice (tests run the bandwidth-regime code
+// paths on small instances that way)
+static int forced_regime() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("LRS_FORCE_REGIME");
+        v = !e ? 0 : (strcmp(e, "small") == 0 ? 1 : (strcmp(e, "large") == 0 ? 2 : 0));
+    }
+    return v;
+}
 static StagePlan plan_stage(long rows_threads, int res_small, int res_large, int K, int T) {
     StagePlan p;
     p.T = T;
     const long need = std::max(1L, (rows_threads * T + kRowBlock - 1) / kRowBlock);
     const int cap = std::max(1, kMaxPartialBlocks / std::max(1, K));
+    const int fr = forced_regime();
+    if (fr == 2) { p.grid = (int)std::max(1L, std::min<long>(std::min<long>(need, res_large), cap)); p.small = false; return p; }
+    if (fr == 1) { p.grid = (int)std::max(1L, std::min<long>(need, cap)); p.small = true; return p; }
     if (need <= res_small) { p.grid = (int)std::min<long>(need, cap); p.small = true; }
     else { p.grid = (int)std::min<long>(std::min<long>(need, res_large), cap); p.small = false; }
     p.grid = std::max(1, p.grid);
@@ -1968,6 +2035,16 @@ static int plan_b(const DevCone &c, int K, StagePlan &p) {
     const int T = team_size(c, deg, 4);
     LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.n * c.G, res_b<GG, EE, 4>(), res_b<GG, EE, 1>(), K, T); });
     return 0;
+}
+
+// Whether stage A runs as two launches (bandwidth regime) for the current layouts.
+bool alm_stage_a_split(const DevProblem &P) {
+    for (int k = 0; k < P.K; ++k) {
+        StagePlan pa;
+        if (plan_a(P.cones[k], P.K, pa)) return false;
+        if (!pa.small) return true;
+    }
+    return false;
 }
 
 // One ALM inner iteration = two launches (A, B), three with global constraints
@@ -1998,10 +2075,12 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     auto cone_of = [&](int k) -> const DevCone & { return merge ? mc : P.cones[k]; };
     StagePlan pa[kMaxCones], pb[kMaxCones];
     int nblkA = 0, nblkB = 0;
+    bool split = false;   // stage A as two launches (bandwidth regime)
     for (int k = 0; k < KL; ++k) {
         if (plan_a(cone_of(k), KL, pa[k]) || plan_b(cone_of(k), KL, pb[k])) return -1;
         nblkA += pa[k].grid;
         nblkB += pb[k].grid;
+        if (!pa[k].small) split = true;
     }
     const int gwide = P.glob_maxlen >= 32 ? 1 : 0;   // long global constraints: a wave each
     auto mark = [&](int q) -> int {
@@ -2017,21 +2096,28 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     for (int k = 0; k < KL && (mask & 1); ++k) {
         const DevCone &c = cone_of(k);
         const int grid = pa[k].grid;
-#define LRS_LAUNCH_A(UU)                                                                                   \
-    hipLaunchKernelGGL((k_it_a<GG, EE, UU>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr, \
+#define LRS_LAUNCH_A(UU, MM)                                                                               \
+    hipLaunchKernelGGL((k_it_a<GG, EE, UU, MM>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr, \
                        c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], \
                        W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, P.b, W.cvs, W.lam, W.rec, \
                        k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w, W.uvt2, W.par,      \
                        ctrl_prev, ctrl_cur, ls_prev, W.partC, nblkB, W.part, off, pa[k].T, gwide)
-        const bool small = pa[k].small;
         LRS_LAYOUT_SWITCH(c.G, c.E, {
-            if (small) LRS_LAUNCH_A(2);
-            else LRS_LAUNCH_A(1);
+            if (!split) LRS_LAUNCH_A(2, 0);
+            else LRS_LAUNCH_A(1, 1);
         });
-#undef LRS_LAUNCH_A
         LRS_CHECK_LAUNCH();
         off += grid;
     }
+    off = 0;
+    for (int k = 0; k < KL && (mask & 1) && split; ++k) {
+        const DevCone &c = cone_of(k);
+        const int grid = pa[k].grid;
+        LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_A(1, 2); });
+        LRS_CHECK_LAUNCH();
+        off += grid;
+    }
+#undef LRS_LAUNCH_A
     if (mark(1)) return -1;
     // G: phase-1 test and the global constraints' q and dots
     const int gg = gwide ? std::min((std::max(1, P.mg) + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks)

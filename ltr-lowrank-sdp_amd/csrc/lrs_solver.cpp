@@ -1165,7 +1165,9 @@ int lrs_stage_bytes(lrs_ctx *c, double *bytes) {
         const HostCone &hc = c->hp.cones[k];
         const double n = hc.n, r = c->rank[k], Pk = (double)hc.prow.size(), A = (double)hc.adj_col.size();
         const double nr8 = 8.0 * n * r;
-        a += 7 * nr8 + 8 * (n + 1) + 8 * Pk /*lower adj col+slot*/ + 8 * Pk /*Cw*/ + 16 * Pk /*uRD,uDD*/ + 4 * (Pk + 1);
+        // split stage A (bandwidth regime): D is written by the first launch and read back
+        a += (alm_stage_a_split(c->dp) ? 8 : 7) * nr8 + 8 * (n + 1) + 8 * Pk /*lower adj col+slot*/ + 8 * Pk /*Cw*/ +
+             16 * Pk /*uRD,uDD*/ + 4 * (Pk + 1);
         bb += 9 * nr8 + 8 * (n + 1) + 8 * A /*adj col+slot*/ + 8 * Pk /*Craw*/ + 4 * (Pk + 1) /*slot_ptr*/ +
               8 * Pk /*uRR*/ + 4 * (Pk + 1) /*loc_ptr*/;
     }

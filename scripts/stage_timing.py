@@ -45,6 +45,12 @@ for ng in ("1", "0"):
                 t = ph[k]
                 seq = [f"{names[k][p]}:{(t[p] - t[p - 1]) * 0.01:.2f}" for p in range(1, len(names[k]))]
                 print(f"K{'AGB'[k]} phases (us):", " ".join(seq))
+            t = ph[2]
+            if t[6] and t[11]:
+                print("KB rows detail (us from LS end): header", round((t[6] - t[2]) * 0.01, 2), "chunk1 data",
+                      round((t[7] - t[2]) * 0.01, 2), "chunk1 done", round((t[8] - t[2]) * 0.01, 2), "chunk2 data",
+                      round((t[9] - t[2]) * 0.01, 2), "chunk2 done", round((t[10] - t[2]) * 0.01, 2), "epilogue",
+                      round((t[11] - t[2]) * 0.01, 2), "rows end", round((t[3] - t[2]) * 0.01, 2))
             # per-block spans of the last full iteration (valid blocks: entry != 0)
             spans = []
             ks = [k for k in range(3) if any(a != 0 for a, _ in blk[k])]

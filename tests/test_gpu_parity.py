@@ -152,3 +152,39 @@ def test_constraint_entry_auut_matches_pattern_path(solver_mod, name):
         assert np.array_equal(q, cvs)          # same arithmetic, same order
     assert rel_err(q, g["cvs_rr"]) < TOL
     assert sv.auut_bytes() > 0
+
+
+_REGIME_SCRIPT = r"""
+import importlib, json, sys
+sys.path.insert(0, sys.argv[1])
+s = importlib.import_module("ltr-lowrank-sdp_amd.solver")
+out = {}
+for name in sys.argv[2:]:
+    sv = s.Solver(name)
+    r = sv.solve(reoptLevel=0)
+    out[name] = [r["alm_inner"], r["alm_pobj"], r["pobj"], r["admm_iter"]]
+    sv.close()
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_bandwidth_regime_matches_latency_regime(tmp_path):
+    """The large-n code paths (split stage A, unroll-1 B, occupancy grids) forced on small
+    instances give the same solves as the latency-regime kernels (LRS_FORCE_REGIME)."""
+    import sys as _sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = [instance(n) for n in ("mc_torus12x10", "mc_rand300w", "theta25x3")]
+    res = {}
+    for reg in ("small", "large"):
+        env = dict(os.environ, LRS_FORCE_REGIME=reg)
+        p = subprocess.run([_sys.executable, "-c", _REGIME_SCRIPT, root] + names, env=env, capture_output=True,
+                           text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-2000:]
+        res[reg] = json.loads(p.stdout.strip().splitlines()[-1])
+    for nm in names:
+        a, b = res["small"][nm], res["large"][nm]
+        if "mc_" in nm:
+            assert abs(a[0] - b[0]) <= 2, (nm, a, b)
+            assert abs(a[1] - b[1]) <= 1e-8 * abs(a[1]), (nm, a, b)
+        assert abs(a[2] - b[2]) <= 1e-6 * max(1.0, abs(a[2])), (nm, a, b)
