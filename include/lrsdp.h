@@ -131,6 +131,11 @@ int lrs_set_log_path(lrs_ctx *ctx, const char *path);
 int lrs_time_auut(lrs_ctx *ctx, int reps, double *avg_ms);
 int lrs_auut_bytes(lrs_ctx *ctx, double *bytes);
 
+/* Standalone r x r Gram R^T R of one cone (build_gram_from_factor, lorads_logging.c:216-240;
+ * k_gram on the FP64 matrix cores, then the fixed-order partial reduction): avg_ms = ms per
+ * Gram (kernel + reduction), gram_ms = ms of the MFMA kernel alone (may be NULL). */
+int lrs_time_gram(lrs_ctx *ctx, int cone, int reps, double *avg_ms, double *gram_ms);
+
 /* Per-stage timing of the split ALM inner iteration: runs `steps` inner iterations at
  * the current rank like lrs_alm_throughput, with HIP events on the solver stream
  * around each of the four launches (S1 direction+SDDMM, S2 q-gather, S3 update+

@@ -540,41 +540,79 @@ __global__ void __launch_bounds__(kBlock) k_alm_m1(int m, double rho, const doub
 
 // Gram partials: block b accumulates rows [b*chunk, (b+1)*chunk) of X^T X into
 // gram_part[b][r][r] (upper+lower).  avg: rows are (X+Y)/2.
+// r x r Gram X^T X (or of the average (X+Y)/2), build_gram_from_factor / _from_average
+// (lorads_logging.c:216-270), on the FP64 matrix cores: v_mfma_f64_16x16x4_f64 with
+// A = X^T and B = X, K = rows.  Block (bx, by): rows of chunk bx, 16x16 output tiles
+// (ta <= tb) of group by, kGramTPW tiles per wave.  A chunk of kGramRows rows is staged
+// in LDS (zero-padded to 16-column tiles), every wave takes its A/B fragments from there:
+// lane l of k-step s reads row 4s + (l >> 4), column 16t + (l & 15).  D fragment: col
+// = l & 15, row = (l >> 4) + 4q (cdna_hip_programming.md §3, f64 map).  Each block writes
+// its tiles (both orientations) into its r x r partial; k_gram_reduce sums the partials
+// of the bx blocks in order.
+constexpr int kGramRows = 16;
+constexpr int kGramTPW = 4;
+constexpr int kGramTPB = kGramTPW * (kBlock / 64);
+typedef double gram_acc_t __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(kBlock) k_gram(int n, int r, int ld, const double *__restrict__ X,
                                                  const double *__restrict__ Y, int avg,
                                                  double *__restrict__ gram_part) {
-    extern __shared__ double rowbuf[];   // [8][ld]
-    const int chunk = (n + gridDim.x - 1) / gridDim.x;
-    const int i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
-    const int rr = r * r;
-    double acc[16];
+    extern __shared__ double xs[];   // [kGramRows][ldp]
+    const int rt = (r + 15) >> 4;
+    const int ldp = rt * 16 + 1;
+    const int ntiles = rt * (rt + 1) / 2;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int ta[kGramTPW], tb[kGramTPW];
+    bool on[kGramTPW];
+    gram_acc_t acc[kGramTPW];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = 0.0;
-    for (int ib = i0; ib < i1; ib += 8) {
-        const int nr = min(8, i1 - ib);
-        for (int t = threadIdx.x; t < nr * ld; t += kBlock) {
-            const int a = t / ld, c = t % ld;
-            double v = X[(long)(ib + a) * ld + c];
-            if (avg) v = 0.5 * (v + Y[(long)(ib + a) * ld + c]);
-            rowbuf[a * ld + c] = v;
+    for (int t = 0; t < kGramTPW; ++t) {
+        int id = blockIdx.y * kGramTPB + wv + (kBlock / 64) * t;   // id -> (a, b), a <= b, row-major upper
+        on[t] = id < ntiles;
+        int a = 0;
+        while (on[t] && id >= rt - a) { id -= rt - a; ++a; }
+        ta[t] = a;
+        tb[t] = a + id;
+        acc[t] = gram_acc_t{0.0, 0.0, 0.0, 0.0};
+    }
+    const int chunk = ((n + gridDim.x - 1) / gridDim.x + kGramRows - 1) / kGramRows * kGramRows;
+    const int i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+    const int cols = rt * 16;
+    for (int ib = i0; ib < i1; ib += kGramRows) {
+        for (int e = threadIdx.x; e < kGramRows * cols; e += kBlock) {
+            const int a = e / cols, c = e - a * cols;
+            const int row = ib + a;
+            double v = 0.0;
+            if (row < i1 && c < r) {
+                v = X[(long)row * ld + c];
+                if (avg) v = 0.5 * (v + Y[(long)row * ld + c]);
+            }
+            xs[a * ldp + c] = v;
         }
         __syncthreads();
-        for (int a = 0; a < nr; ++a) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int idx = threadIdx.x + q * kBlock;
-                if (idx < rr) {
-                    const int c1 = idx / r, c2 = idx % r;
-                    acc[q] += rowbuf[a * ld + c1] * rowbuf[a * ld + c2];
-                }
-            }
+        for (int t = 0; t < kGramTPW; ++t) {
+            if (!on[t]) continue;   // wave-uniform
+            const double *pa = xs + (lane >> 4) * ldp + ta[t] * 16 + (lane & 15);
+            const double *pb = xs + (lane >> 4) * ldp + tb[t] * 16 + (lane & 15);
+#pragma unroll
+            for (int s = 0; s < kGramRows / 4; ++s)
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[4 * s * ldp], pb[4 * s * ldp], acc[t], 0, 0, 0);
         }
         __syncthreads();
     }
+    double *out = gram_part + (long)blockIdx.x * r * r;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int idx = threadIdx.x + q * kBlock;
-        if (idx < rr) gram_part[(long)blockIdx.x * rr + idx] = acc[q];
+    for (int t = 0; t < kGramTPW; ++t) {
+        if (!on[t]) continue;
+        const int col = tb[t] * 16 + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = ta[t] * 16 + (lane >> 4) + 4 * q;
+            if (row < r && col < r) {
+                out[(long)row * r + col] = acc[t][q];
+                out[(long)col * r + row] = acc[t][q];
+            }
+        }
     }
 }
 
@@ -1931,20 +1969,21 @@ int launch_alm_m1(const DevProblem &P, double rho, const double *lam, const doub
     LRS_CHECK_LAUNCH();
     return 0;
 }
+static int num_cus();
 int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y, int avg, double *gram_part,
                 int *nblk_used, hipStream_t st) {
     const DevCone &c = P.cones[cone];
-    if (c.r * c.r > 16 * kBlock) {
-        snprintf(g_err, sizeof(g_err), "gram: rank %d too large", c.r);
-        return -1;
-    }
-    int grid = (c.n + 255) / 256;
-    if (grid > 64) grid = 64;
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_gram, dim3(grid), dim3(kBlock), 8 * c.ld * sizeof(double), st, c.n, c.r, c.ld,
-                       X + c.foff, Y ? Y + c.foff : nullptr, avg, gram_part);
+    const int rt = (c.r + 15) / 16;
+    const int ntiles = rt * (rt + 1) / 2;
+    const int gy = (ntiles + kGramTPB - 1) / kGramTPB;
+    // at most 64 row chunks (the partial buffer holds 64 r x r partials), >= ~2 blocks per CU
+    int gx = std::max(1, std::min(64, (c.n + kGramRows - 1) / kGramRows));
+    gx = std::min(gx, std::max(1, (2 * num_cus() + gy - 1) / gy));
+    const size_t lds = sizeof(double) * kGramRows * (rt * 16 + 1);
+    hipLaunchKernelGGL(k_gram, dim3(gx, gy), dim3(kBlock), lds, st, c.n, c.r, c.ld, X + c.foff,
+                       Y ? Y + c.foff : nullptr, avg, gram_part);
     LRS_CHECK_LAUNCH();
-    if (nblk_used) *nblk_used = grid;
+    if (nblk_used) *nblk_used = gx;
     return 0;
 }
 

@@ -1601,4 +1601,37 @@ int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {
     return 0;
 }
 
+// Standalone r x r Gram of cone `cone` on R (k_gram on the FP64 matrix cores + the
+// fixed-order partial reduction): reps back to back between two HIP events.
+int lrs_time_gram(lrs_ctx *c, int cone, int reps, double *avg_ms, double *gram_ms) {
+    if (cone < 0 || cone >= c->dp.K) {
+        set_err("time_gram: bad cone %d", cone);
+        return -1;
+    }
+    hipEvent_t e0, e1, e2;
+    HIPC(hipEventCreate(&e0));
+    HIPC(hipEventCreate(&e1));
+    HIPC(hipEventCreate(&e2));
+    const int rr = c->rank[cone] * c->rank[cone];
+    int nblk = 0;
+    HIPC(hipEventRecord(e0, c->st));
+    for (int q = 0; q < reps; ++q) OPC(launch_gram(c->dp, cone, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st));
+    HIPC(hipEventRecord(e1, c->st));
+    for (int q = 0; q < reps; ++q) {
+        OPC(launch_gram(c->dp, cone, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st));
+        OPC(launch_gram_reduce(nblk, rr, c->W.gram, c->W.gram + 64L * rr, c->st));
+    }
+    HIPC(hipEventRecord(e2, c->st));
+    HIPC(hipEventSynchronize(e2));
+    float ms0 = 0, ms1 = 0;
+    HIPC(hipEventElapsedTime(&ms0, e0, e1));
+    HIPC(hipEventElapsedTime(&ms1, e1, e2));
+    if (gram_ms) *gram_ms = ms0 / reps;
+    *avg_ms = ms1 / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    return 0;
+}
+
 }  // extern "C"

@@ -27,6 +27,7 @@ __all__ = [
     "theta",
     "theta_multiblock",
     "random_sparse",
+    "random_sparse_problem",
     "write_sdpa",
     "config_instance",
 ]
@@ -164,9 +165,9 @@ def theta_multiblock(path, n, n_edges, nblocks, seed):
     return write_sdpa(path, len(b), [n] * nblocks, np.array(b), entries)
 
 
-def random_sparse(path, n, m, k, seed, dense_c=False):
-    """C5-like: C = I (or dense), each A_i has k random lower-triangle N(0,1) entries,
-    b_i = <A_i, I> (X = I feasible)."""
+def random_sparse_problem(n, m, k, seed, dense_c=False):
+    """C5-like in memory: C = I (or dense), each A_i has k random lower-triangle N(0,1)
+    entries, b_i = <A_i, I> (X = I feasible).  Returns (m, dims, b, entries)."""
     rng = np.random.default_rng(seed)
     ii = rng.integers(0, n, size=(m, k))
     jj = rng.integers(0, n, size=(m, k))
@@ -185,7 +186,12 @@ def random_sparse(path, n, m, k, seed, dense_c=False):
         d = np.arange(1, n + 1)
         entries.append((np.zeros(n, dtype=np.int64), 1, d, d, -np.ones(n)))
     entries.append((con, 1, lo.ravel() + 1, hi.ravel() + 1, v.ravel()))
-    return write_sdpa(path, m, [n], b, entries)
+    return m, [n], b, entries
+
+
+def random_sparse(path, n, m, k, seed, dense_c=False):
+    """random_sparse_problem written as a .dat-s file."""
+    return write_sdpa(path, *random_sparse_problem(n, m, k, seed, dense_c))
 
 
 # BASELINE.json configs restated (SURVEY.md §8(d)); small = parity-test sizes
@@ -197,6 +203,7 @@ CONFIGS = {
     "theta3": dict(kind="theta", n=150, n_edges=1105, seed=3),
     "theta3x3": dict(kind="theta_multiblock", n=150, n_edges=1105, nblocks=3, seed=3),
     "R2000": dict(kind="maxcut_torus", rows=2000, cols=2000, seed=2000),
+    "C5": dict(kind="random_sparse", n=10000, m=1000000, k=6, seed=5),
 }
 
 

@@ -108,6 +108,7 @@ def load_library(path=None):
         "lrs_time_stages": (C.c_int, [vp, C.c_int, dp]),
         "lrs_stage_bytes": (C.c_int, [vp, dp]),
         "lrs_auut_bytes": (C.c_int, [vp, dp]),
+        "lrs_time_gram": (C.c_int, [vp, C.c_int, C.c_int, dp, dp]),
         "lrs_load_coo": (C.c_int, [vp, C.c_int, C.c_int, ip, dp, C.c_long, ip, ip, ip, ip, dp]),
         "lrs_debug_phase_times": (C.c_int, [vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
     }
@@ -321,6 +322,12 @@ class Solver:
         ph = [list(out[16 * k:16 * k + 16]) for k in range(4)]
         b = [[(blk[(k * 1024 + i) * 2], blk[(k * 1024 + i) * 2 + 1]) for i in range(1024)] for k in range(4)]
         return ph, b
+
+    def time_gram(self, cone=0, reps=20):
+        """(ms per Gram incl. reduction, ms of the MFMA kernel alone) on R of `cone`."""
+        ms, kms = C.c_double(), C.c_double()
+        self._check(self.lib.lrs_time_gram(self.ctx, cone, reps, C.byref(ms), C.byref(kms)), "time_gram")
+        return ms.value, kms.value
 
     def time_auut(self, reps=100):
         ms = C.c_double()

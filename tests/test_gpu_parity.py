@@ -188,3 +188,28 @@ def test_bandwidth_regime_matches_latency_regime(tmp_path):
             assert abs(a[0] - b[0]) <= 2, (nm, a, b)
             assert abs(a[1] - b[1]) <= 1e-8 * abs(a[1]), (nm, a, b)
         assert abs(a[2] - b[2]) <= 1e-6 * max(1.0, abs(a[2])), (nm, a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r", [5, 19, 64, 128, 200])
+def test_gram_mfma_matches_fp64(solver_mod, r):
+    """k_gram (v_mfma_f64_16x16x4_f64) == X^T X / ((U+V)/2)^T ((U+V)/2) in FP64
+    (build_gram_from_factor / _from_average, lorads_logging.c:216-270)."""
+    sv = solver_mod.Solver(instance("mc_rand300w"))
+    n = sv.dims[0]
+    sv.set_rank([r])
+    rng = np.random.default_rng(r)
+    x, y = rng.standard_normal(n * r), rng.standard_normal(n * r)
+    X, Y = x.reshape(r, n).T, y.reshape(r, n).T      # reference layout: column-major n x r
+    sv.set_factor(solver_mod.R, x)
+    g = sv.gram(0, solver_mod.R)
+    ref = X.T @ X
+    assert np.max(np.abs(g - ref)) <= 1e-12 * np.max(np.abs(ref))
+    assert np.array_equal(g, g.T)
+    sv.set_factor(solver_mod.U, x)
+    sv.set_factor(solver_mod.V, y)
+    g2 = sv.gram(0, solver_mod.U)
+    A = 0.5 * (X + Y)
+    ref2 = A.T @ A
+    assert np.max(np.abs(g2 - ref2)) <= 1e-12 * np.max(np.abs(ref2))
+    sv.close()
