@@ -26,6 +26,7 @@ extern "C" {
 #endif
 
 typedef struct lrs_ctx lrs_ctx;
+typedef struct lrs_loopback lrs_loopback;
 
 /* LoRADS flags (main.c:56-86 defaults, main.c:125-154 names) + the three flags
  * benchmark.py passes that the reference never implemented. */
@@ -164,6 +165,29 @@ int lrs_time_stages(lrs_ctx *ctx, int reps, double *stage_ms);
  * blk[4][1024][2].  Returns 64 from the diagnostics build (liblrsdp_timing.so), 0
  * from the product build. */
 int lrs_debug_phase_times(lrs_ctx *ctx, unsigned long long *out, unsigned long long *blk);
+
+/* ---- Sharded solve of one instance over several GPUs.
+ * Replaces the reference's single-process operator slots for one cone split by rows:
+ * every process loads the whole problem (lrs_load_sdpa / lrs_load_coo), then calls one
+ * lrs_shard_* with its rank; the context then owns a contiguous block of rows (+ the
+ * halo of neighbour rows) and the constraints inside it, and lrs_solve /
+ * lrs_alm_throughput run the ALM phase (the unit of the metric) with, per inner
+ * iteration, one halo exchange of direction rows and two all-reduces of the stage
+ * totals (line search; L-BFGS dots + residual).  One SDP cone; every constraint's
+ * entries inside one row block (MaxCut's e_i e_i^T).  The ADMM phase is not sharded
+ * (lrs_solve stops after the ALM phase).  Every shard must make the same calls in the
+ * same order (the collectives are matched by order). */
+/* RCCL: rank 0 creates the id (128 bytes) and broadcasts it; every rank then calls
+ * lrs_shard_rccl on its own GPU (ncclCommInitRank is collective). */
+int lrs_comm_unique_id(char *id_out);
+int lrs_shard_rccl(lrs_ctx *ctx, int world, int rank, const char *id);
+/* One-process loopback transport (tests): `world` contexts on one GPU, one host thread
+ * each; lrs_shard_loopback is collective over the group's threads. */
+int lrs_loopback_create(int world, lrs_loopback **out);
+void lrs_loopback_destroy(lrs_loopback *g);
+int lrs_shard_loopback(lrs_ctx *ctx, lrs_loopback *g, int rank);
+/* world, rank, first global row, owned rows, halo rows of this context (1, 0, 0, n, 0 unsharded) */
+int lrs_shard_info(lrs_ctx *ctx, int *world, int *rank, int *row0, int *nown, int *nhalo);
 
 #ifdef __cplusplus
 }

@@ -75,6 +75,7 @@ enum LsIdx { LS_TAU = 0, LS_ROOTNUM, LS_FLAG, LS_N = 4 };
 // ---- finals of the standalone launchers (g_tmpfin offsets)
 enum TmpFinIdx { TF_SD = 0, TF_GATHER = 128, TF_RESID = 129, TF_DOT = 130, TF_SPMM = 131, TF_N = 256 };
 constexpr int kMaxCones = 64;
+constexpr int kMaxShards = 64;       // processes of one sharded solve
 constexpr int kLongRow = 32;         // constraint rows longer than this get a wave each
 
 struct Layout {
@@ -84,13 +85,28 @@ Layout choose_layout(int r);
 
 struct DevCone {
     int n = 0, r = 0, ld = 0, G = 0, E = 0;
+    // rows the kernels compute: [row0, row0 + nown) -- the whole cone, or in a sharded
+    // solve this process's rows (the others, the halo, are read as neighbours only)
+    int row0 = 0, nown = 0;
     long foff = 0;      // offset (doubles) of this cone in the factor buffer
     int slot_off = 0, P = 0;
     int *adj_ptr = nullptr, *adj_low = nullptr, *adj_col = nullptr, *adj_slot = nullptr;
     long adj_nnz = 0;
 };
 
+// Sharded solve (one process per GPU, rows of the cone split into contiguous blocks):
+// the collectives the split iteration calls between its stages, provided by the host
+// (lrs_solver.cpp: RCCL, or the one-process loopback transport of the tests).
+struct ShardHooks {
+    void *self = nullptr;
+    // direction rows D of this shard's halo from their owners (and its rows to theirs)
+    int (*halo)(void *self, double *D, hipStream_t st) = nullptr;
+    // in-place sum over the shards of n contiguous doubles in device memory
+    int (*allreduce)(void *self, double *buf, int n, hipStream_t st) = nullptr;
+};
+
 struct DevProblem {
+    const ShardHooks *shard = nullptr;   // non-null in a sharded solve
     int m = 0, K = 0;
     long NRpad = 0;     // factor buffer length (doubles)
     int Ptot = 0;
@@ -138,6 +154,7 @@ struct DevWork {
     double *gram = nullptr;    // gram partials
     double *rec = nullptr;     // [m][4] per-constraint {A(RR^T), q1, q2, -lam - rho b}
     double *cgc = nullptr;     // [8] device CG control (CgIdx)
+    double *tot = nullptr;     // [32] sharded solve: summed stage totals (A: 0..7, B: 16..25)
 };
 
 // ---------------------------- launchers -----------------------------------
@@ -205,6 +222,12 @@ int launch_cg_resid(long nr, const double *b, const double *Q, double *r, double
                     const double *partA, int nblkA, int init, hipStream_t st, int *nblk);
 int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, int nblkC, double *cgc, double tol,
                      int par, int init, hipStream_t st);
+
+// per-context scratch of the standalone reductions for the calling thread (nullptr: globals)
+void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart);
+// sharded solve helpers
+int launch_pack_rows(int nrows, int ld, const int *rows, const double *src, double *dst, hipStream_t st);
+int launch_sum_shards(int n, int world, const double *const *src, double *out, hipStream_t st);
 
 const char *last_device_error();
 // diagnostics build only: copies g_phase[4][16] (returns 64), else returns 0

@@ -260,13 +260,13 @@ __global__ void __launch_bounds__(kBlock) k_sddmm(int n, int ld, const int *__re
                                                   const double *__restrict__ Y, double *__restrict__ out0,
                                                   double *__restrict__ out1, const double *__restrict__ Cw,
                                                   double *part, unsigned *ticket, double *fin,
-                                                  const double *__restrict__ guard) {
+                                                  const double *__restrict__ guard, int row0) {
     if (guard && guard[C_ACTIVE] == 0.0) return;
     const int lane = threadIdx.x & (G - 1);
     const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
     const int ngrp = gridDim.x * kBlock / G;
     double acc[2] = {0.0, 0.0};
-    for (int i = grp; i < n; i += ngrp) {
+    for (int i = row0 + grp; i < row0 + n; i += ngrp) {
         double xi[E], yi[E];
         ld_row<E>(X + (long)i * ld + lane * E, xi);
         if constexpr (MODE != 1) ld_row<E>(Y + (long)i * ld + lane * E, yi);
@@ -478,12 +478,12 @@ __global__ void __launch_bounds__(kBlock) k_spmm(int n, int ld, const int *__res
                                                  const double *__restrict__ S, const double *__restrict__ X,
                                                  double scale, const double *__restrict__ addX, double addScale,
                                                  double *__restrict__ out, double *part, unsigned *ticket,
-                                                 double *fin) {
+                                                 double *fin, int row0) {
     const int lane = threadIdx.x & (G - 1);
     const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
     const int ngrp = gridDim.x * kBlock / G;
     double nrm[1] = {0.0};
-    for (int i = grp; i < n; i += ngrp) {
+    for (int i = row0 + grp; i < row0 + n; i += ngrp) {
         double acc[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) acc[e] = 0.0;
@@ -915,13 +915,14 @@ __device__ __forceinline__ void write_partials_range(double (&acc)[NV], double *
 
 // all threads; generic nblk
 template <int NV, int NT = kBlock>
-__device__ __forceinline__ void reduce_partials(const double *__restrict__ part, int nblk, double *out) {
+__device__ __forceinline__ void reduce_partials(const double *__restrict__ part, int nblk, double *out,
+                                                int pstr = kMaxPartialBlocks) {
     double a[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) a[v] = 0.0;
     for (int b = threadIdx.x; b < nblk; b += NT) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) a[v] += part[v * kMaxPartialBlocks + b];
+        for (int v = 0; v < NV; ++v) a[v] += part[v * pstr + b];
     }
     double s[NV];
     block_reduce<NV, NT>(a, s);
@@ -1128,7 +1129,8 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
     const int *__restrict__ glob, int m, int K, const int *__restrict__ con_ptr, const int *__restrict__ con_slot,
     const double *__restrict__ con_w, const double *__restrict__ uRR, const double *__restrict__ par,
     const double *__restrict__ ctrl_prev, double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev,
-    const double *__restrict__ partC, int nblkC, double *__restrict__ partA, int pblk_off, int T, int gwide) {
+    const double *__restrict__ partC, int nblkC, double *__restrict__ partA, int pblk_off, int T, int gwide,
+    int row0, int pstr) {
     __shared__ double c[C_NCTRL];
     __shared__ double red[10];
     __shared__ double lsv[2];
@@ -1146,7 +1148,7 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
     __syncthreads();
     LRS_TS(0, 1);
     fold = (c[C_ACT2] != 0.0 && c[C_PENDING] == 1.0 && lsv[0] == 0.0) ? 1 : 0;
-    if (fold) reduce_partials<10, kRowBlock>(partC, nblkC, red);
+    if (fold) reduce_partials<10, kRowBlock>(partC, nblkC, red, pstr);
     else __syncthreads();   // every wave has read c[] before thread 0 rewrites it
     LRS_TS(0, 2);
     if (threadIdx.x == 0) ctrl_step(c, par, lsv[0], lsv[1], fold, red, mg == 0);
@@ -1215,7 +1217,8 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
         const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
         const int ngrp = gridDim.x * kRowBlock / G;
         const int team = grp / T, mem = grp % T, nteams = ngrp / T;
-        for (int i = team; i < n; i += nteams) {
+        // rows [row0, row0 + n): the whole cone, or this process's shard of it
+        for (int i = row0 + team; i < row0 + n; i += nteams) {
             const long oi = (long)i * ld + lane * E;
             const int kb = adj_ptr[i], ke = adj_low[i];
             double xi[E], yi[E];
@@ -1392,7 +1395,8 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     const int *__restrict__ loc_ptr, const int *__restrict__ loc_con, const double *__restrict__ loc_w,
     const double *__restrict__ b, double *__restrict__ cvs, const double *__restrict__ par,
     const double *__restrict__ ctrl, const double *__restrict__ partA, int nblkA, const double *__restrict__ partB,
-    int nblkB, double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int T) {
+    int nblkB, double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int T, int row0,
+    int nall, int pstr) {
     __shared__ double gsh[kRowBlock * E];   // team reduction of the row gradient (T > 1)
     __shared__ double red[12];
     __shared__ double ls[LS_N];
@@ -1402,7 +1406,7 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     if (threadIdx.x == 0) { cs[0] = ctrl[C_ACT2]; cs[1] = ctrl[C_GCUR]; cs[2] = ctrl[C_HEAD]; cs[3] = ctrl[C_RCUR]; }
     __syncthreads();
     if (cs[0] == 0.0) return;
-    reduce_partials<7, kRowBlock>(partA, nblkA, red);
+    reduce_partials<7, kRowBlock>(partA, nblkA, red, pstr);
     if (nblkB > 0) {
         reduce_partials<5, kRowBlock>(partB, nblkB, red + 7);
         if (threadIdx.x == 0) {
@@ -1441,8 +1445,8 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     // acc: GG, ys, yy, sG, yG, soG, yoG, soy, yoy, residual
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int ib = blockIdx.x * tpb; ib < n; ib += nteams) {
-    const int i = ib + team_local;
-    const bool valid = i < n;
+    const int i = row0 + ib + team_local;   // rows [row0, row0 + n) (a shard: n = owned rows)
+    const bool valid = ib + team_local < n;
     double ri[E], di[E], g[E];
     const long oi = (long)(valid ? i : 0) * ld + lane * E;
 #pragma unroll
@@ -1573,6 +1577,20 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
         }
     }   // mem == 0
     }   // rows
+    // sharded solve: the halo rows (the other shards' rows this one reads) take the same
+    // update R_new = R + tau D, D of the halo received after stage A's first half
+    if (nall > n) {
+        for (int q = grp; q < nall - n; q += ngrp) {
+            const int l = q < row0 ? q : q + n;
+            const long ol = (long)l * ld + lane * E;
+            double rv[E], dv[E];
+            ld_row<E>(R + ol, rv);
+            ld_row<E>(D + ol, dv);
+#pragma unroll
+            for (int e = 0; e < E; ++e) rv[e] += tau * dv[e];
+            st_row<E>(Rn + ol, rv);
+        }
+    }
     LRS_TS(2, 3);
     write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
     LRS_TS_END(2, 4);
@@ -1790,7 +1808,18 @@ __global__ void __launch_bounds__(kBlock) k_cg_resid2(long nr, const double *__r
 // ------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------
+// Per-context scratch of the standalone reductions (tickets, finals, residual partials),
+// bound to the calling thread by the context (several contexts may run concurrently in
+// one process, e.g. the shards of the loopback transport); unbound: the module globals.
+static thread_local unsigned *t_tickets = nullptr;
+static thread_local double *t_tmpfin = nullptr, *t_rpart = nullptr;
+void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart) {
+    t_tickets = tickets;
+    t_tmpfin = tmpfin;
+    t_rpart = rpart;
+}
 static unsigned *ticket_ptr(int id) {
+    if (t_tickets) return t_tickets + id;
     unsigned *p = nullptr;
     (void)hipGetSymbolAddress((void **)&p, HIP_SYMBOL(g_tickets));
     return p + id;
@@ -1801,6 +1830,7 @@ static double *fin_ptr() {
     return p;
 }
 static double *tmpfin_ptr() {
+    if (t_tmpfin) return t_tmpfin;
     double *p = nullptr;
     (void)hipGetSymbolAddress((void **)&p, HIP_SYMBOL(g_tmpfin));
     return p;
@@ -1835,23 +1865,23 @@ int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const
                  double *out1, double *part, int pblk_off, int *nblk_used, hipStream_t st) {
     (void)pblk_off;
     const DevCone &c = P.cones[cone];
-    const int grid = grid_rows(c.n, c.G);
+    const int grid = grid_rows(c.nown, c.G);
     double *fin = tmpfin_ptr() + TF_SD + 2 * cone;
     const double *Xc = X + c.foff;
     const double *Yc = Y ? Y + c.foff : nullptr;
     LRS_LAYOUT_SWITCH(c.G, c.E, {
         if (mode == 0)
-            hipLaunchKernelGGL((k_sddmm<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr,
+            hipLaunchKernelGGL((k_sddmm<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, c.nown, c.ld, c.adj_ptr,
                                c.adj_low, c.adj_col, c.adj_slot, Xc, Yc, out0, out1, P.Cw, part,
-                               ticket_ptr(T_SDDMM), fin, nullptr);
+                               ticket_ptr(T_SDDMM), fin, nullptr, c.row0);
         else if (mode == 1)
-            hipLaunchKernelGGL((k_sddmm<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr,
+            hipLaunchKernelGGL((k_sddmm<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, c.nown, c.ld, c.adj_ptr,
                                c.adj_low, c.adj_col, c.adj_slot, Xc, Yc, out0, out1, P.Cw, part,
-                               ticket_ptr(T_SDDMM), fin, nullptr);
+                               ticket_ptr(T_SDDMM), fin, nullptr, c.row0);
         else
-            hipLaunchKernelGGL((k_sddmm<GG, EE, 2>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr,
+            hipLaunchKernelGGL((k_sddmm<GG, EE, 2>), dim3(grid), dim3(kBlock), 0, st, c.nown, c.ld, c.adj_ptr,
                                c.adj_low, c.adj_col, c.adj_slot, Xc, Yc, out0, out1, P.Cw, part,
-                               ticket_ptr(T_SDDMM), fin, nullptr);
+                               ticket_ptr(T_SDDMM), fin, nullptr, c.row0);
     });
     LRS_CHECK_LAUNCH();
     if (nblk_used) *nblk_used = grid;
@@ -1928,12 +1958,12 @@ int launch_spmm(const DevProblem &P, int cone, const double *S, const double *X,
                 double addScale, double *out, double *part, int pblk_off, int *nblk_used, hipStream_t st) {
     (void)pblk_off;
     const DevCone &c = P.cones[cone];
-    const int grid = grid_rows(c.n, c.G);
+    const int grid = grid_rows(c.nown, c.G);
     double *fin = tmpfin_ptr() + TF_SPMM + cone;
     LRS_LAYOUT_SWITCH(c.G, c.E, {
-        hipLaunchKernelGGL((k_spmm<GG, EE>), dim3(grid), dim3(kBlock), 0, st, c.n, c.ld, c.adj_ptr, c.adj_col,
+        hipLaunchKernelGGL((k_spmm<GG, EE>), dim3(grid), dim3(kBlock), 0, st, c.nown, c.ld, c.adj_ptr, c.adj_col,
                            c.adj_slot, S, X + c.foff, scale, addX ? addX + c.foff : nullptr, addScale,
-                           out + c.foff, part, ticket_ptr(T_SPMM), fin);
+                           out + c.foff, part, ticket_ptr(T_SPMM), fin, c.row0);
     });
     LRS_CHECK_LAUNCH();
     if (nblk_used) *nblk_used = grid;
@@ -1977,11 +2007,12 @@ int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y,
     const int ntiles = rt * (rt + 1) / 2;
     const int gy = (ntiles + kGramTPB - 1) / kGramTPB;
     // at most 64 row chunks (the partial buffer holds 64 r x r partials), >= ~2 blocks per CU
-    int gx = std::max(1, std::min(64, (c.n + kGramRows - 1) / kGramRows));
+    int gx = std::max(1, std::min(64, (c.nown + kGramRows - 1) / kGramRows));
     gx = std::min(gx, std::max(1, (2 * num_cus() + gy - 1) / gy));
     const size_t lds = sizeof(double) * kGramRows * (rt * 16 + 1);
-    hipLaunchKernelGGL(k_gram, dim3(gx, gy), dim3(kBlock), lds, st, c.n, c.r, c.ld, X + c.foff,
-                       Y ? Y + c.foff : nullptr, avg, gram_part);
+    hipLaunchKernelGGL(k_gram, dim3(gx, gy), dim3(kBlock), lds, st, c.nown, c.r, c.ld,
+                       X + c.foff + (long)c.row0 * c.ld, Y ? Y + c.foff + (long)c.row0 * c.ld : nullptr, avg,
+                       gram_part);
     LRS_CHECK_LAUNCH();
     if (nblk_used) *nblk_used = gx;
     return 0;
@@ -2037,7 +2068,7 @@ struct StagePlan {
 static int team_size(const DevCone &c, double deg, int U) {
     const long cap_threads = 256L * 2048;
     int T = 1;
-    while (T * 2 <= kRowBlock / c.G && (double)(T * 2 * U * 2) <= deg && (long)c.n * T * 2 * c.G <= cap_threads) T *= 2;
+    while (T * 2 <= kRowBlock / c.G && (double)(T * 2 * U * 2) <= deg && (long)c.nown * T * 2 * c.G <= cap_threads) T *= 2;
     return T;
 }
 // LRS_FORCE_REGIME=small|large overrides the choice (tests run the bandwidth-regime code
@@ -2064,15 +2095,15 @@ static StagePlan plan_stage(long rows_threads, int res_small, int res_large, int
     return p;
 }
 static int plan_a(const DevCone &c, int K, StagePlan &p) {
-    const double deg = c.n > 0 ? (double)c.P / c.n : 0.0;    // lower entries per row
+    const double deg = c.nown > 0 ? (double)c.P / c.nown : 0.0;    // lower entries per row
     const int T = team_size(c, deg, 2);
-    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.n * c.G, res_a<GG, EE, 2>(), res_a<GG, EE, 1>(), K, T); });
+    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_a<GG, EE, 2>(), res_a<GG, EE, 1>(), K, T); });
     return 0;
 }
 static int plan_b(const DevCone &c, int K, StagePlan &p) {
-    const double deg = c.n > 0 ? (double)c.adj_nnz / c.n : 0.0;
+    const double deg = c.nown > 0 ? (double)c.adj_nnz / c.nown : 0.0;
     const int T = team_size(c, deg, 4);
-    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.n * c.G, res_b<GG, EE, 4>(), res_b<GG, EE, 1>(), K, T); });
+    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_b<GG, EE, 4>(), res_b<GG, EE, 1>(), K, T); });
     return 0;
 }
 
@@ -2092,6 +2123,17 @@ int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
     return enqueue_alm_stages(a, parity, 7, st);
 }
 
+// Sharded solve: one block folds a stage's per-block partials (fixed order) into NV
+// contiguous totals, which the shards then sum (ShardHooks::allreduce); the next stage
+// reads the totals as a single "block" with stride 1.
+template <int NV>
+__global__ void __launch_bounds__(kBlock) k_fold_partials(const double *__restrict__ part, int nblk,
+                                                          double *__restrict__ out) {
+    __shared__ double red[NV];
+    reduce_partials<NV, kBlock>(part, nblk, red);
+    if (threadIdx.x < NV) out[threadIdx.x] = red[threadIdx.x];
+}
+
 int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t st) {
     const DevProblem &P = *a.P;
     DevWork &W = *a.W;
@@ -2100,6 +2142,11 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     double *ls_prev = W.lsres + (parity ^ 1) * LS_N;
     double *ls_cur = W.lsres + parity * LS_N;
     const int L = 2;
+    const ShardHooks *sh = P.shard;
+    if (sh && (P.K != 1 || P.mg > 0 || !W.tot)) {
+        snprintf(g_err, sizeof(g_err), "sharded iteration: one cone, single-slot constraints only");
+        return -1;
+    }
     // one launch over the merged row space when every cone has the same row layout
     bool merge = P.K > 1 && P.has_merged;
     for (int k = 1; k < P.K && merge; ++k)
@@ -2114,13 +2161,19 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     auto cone_of = [&](int k) -> const DevCone & { return merge ? mc : P.cones[k]; };
     StagePlan pa[kMaxCones], pb[kMaxCones];
     int nblkA = 0, nblkB = 0;
-    bool split = false;   // stage A as two launches (bandwidth regime)
+    bool split = sh != nullptr;   // stage A as two launches (bandwidth regime; always when sharded)
     for (int k = 0; k < KL; ++k) {
         if (plan_a(cone_of(k), KL, pa[k]) || plan_b(cone_of(k), KL, pb[k])) return -1;
         nblkA += pa[k].grid;
         nblkB += pb[k].grid;
         if (!pa[k].small) split = true;
     }
+    // what the consumers read: every producer block's partials, or (sharded) the summed totals
+    double *totA = sh ? W.tot : nullptr, *totC = sh ? W.tot + 16 : nullptr;
+    const double *inC = sh ? totC : W.partC;
+    const int nC = sh ? 1 : nblkB, pstr = sh ? 1 : kMaxPartialBlocks;
+    const double *inA = sh ? totA : W.part;
+    const int nA = sh ? 1 : nblkA;
     const int gwide = P.glob_maxlen >= 32 ? 1 : 0;   // long global constraints: a wave each
     auto mark = [&](int q) -> int {
         if (a.ev && hipEventRecord(a.ev[q], st) != hipSuccess) {
@@ -2136,11 +2189,12 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const DevCone &c = cone_of(k);
         const int grid = pa[k].grid;
 #define LRS_LAUNCH_A(UU, MM)                                                                               \
-    hipLaunchKernelGGL((k_it_a<GG, EE, UU, MM>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr, \
-                       c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], \
-                       W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, P.b, W.cvs, W.lam, W.rec, \
-                       k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w, W.uvt2, W.par,      \
-                       ctrl_prev, ctrl_cur, ls_prev, W.partC, nblkB, W.part, off, pa[k].T, gwide)
+    hipLaunchKernelGGL((k_it_a<GG, EE, UU, MM>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,     \
+                       c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], \
+                       W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, P.b, W.cvs,    \
+                       W.lam, W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,      \
+                       W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, pa[k].T, gwide, c.row0, \
+                       pstr)
         LRS_LAYOUT_SWITCH(c.G, c.E, {
             if (!split) LRS_LAUNCH_A(2, 0);
             else LRS_LAUNCH_A(1, 1);
@@ -2148,6 +2202,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         LRS_CHECK_LAUNCH();
         off += grid;
     }
+    // sharded: the direction rows of the halo from their owners before the SDDMM half
+    if (sh && (mask & 1) && sh->halo(sh->self, W.D, st)) return -1;
     off = 0;
     for (int k = 0; k < KL && (mask & 1) && split; ++k) {
         const DevCone &c = cone_of(k);
@@ -2157,6 +2213,11 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         off += grid;
     }
 #undef LRS_LAUNCH_A
+    if (sh && (mask & 1)) {
+        hipLaunchKernelGGL(k_fold_partials<8>, dim3(1), dim3(kBlock), 0, st, W.part, nblkA, totA);
+        LRS_CHECK_LAUNCH();
+        if (sh->allreduce(sh->self, totA, 8, st)) return -1;
+    }
     if (mark(1)) return -1;
     // G: phase-1 test and the global constraints' q and dots
     const int gg = gwide ? std::min((std::max(1, P.mg) + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks)
@@ -2174,11 +2235,11 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const DevCone &c = cone_of(k);
         const int grid = pb[k].grid;
 #define LRS_LAUNCH_B(UU)                                                                                   \
-    hipLaunchKernelGGL((k_it_b<GG, EE, UU>), dim3(grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff, c.adj_ptr, \
+    hipLaunchKernelGGL((k_it_b<GG, EE, UU>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff, c.adj_ptr, \
                        c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],        \
                        W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a, W.rec, P.loc_ptr,       \
-                       P.loc_con, P.loc_w, P.b, W.cvs, W.par, ctrl_cur, W.part, nblkA, W.partB,                    \
-                       P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, pb[k].T)
+                       P.loc_con, P.loc_w, P.b, W.cvs, W.par, ctrl_cur, inA, nA, W.partB,                          \
+                       P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, c.n, pstr)
         const bool small = pb[k].small;
         LRS_LAYOUT_SWITCH(c.G, c.E, {
             if (small) LRS_LAUNCH_B(4);
@@ -2188,8 +2249,48 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         LRS_CHECK_LAUNCH();
         off += grid;
     }
+    if (sh && (mask & 4)) {
+        hipLaunchKernelGGL(k_fold_partials<10>, dim3(1), dim3(kBlock), 0, st, W.partC, nblkB, totC);
+        LRS_CHECK_LAUNCH();
+        if (sh->allreduce(sh->self, totC, 10, st)) return -1;
+    }
     if (mark(3)) return -1;
     return mark(4);
+}
+
+// Sharded solve: pack the listed rows (ld doubles each) into a contiguous buffer.
+__global__ void __launch_bounds__(kBlock) k_pack_rows(int nrows, int ld, const int *__restrict__ rows,
+                                                      const double *__restrict__ src, double *__restrict__ dst) {
+    const long tot = (long)nrows * ld;
+    for (long t = (long)blockIdx.x * kBlock + threadIdx.x; t < tot; t += (long)gridDim.x * kBlock) {
+        const long q = t / ld, e = t - q * ld;
+        dst[t] = src[(long)rows[q] * ld + e];
+    }
+}
+int launch_pack_rows(int nrows, int ld, const int *rows, const double *src, double *dst, hipStream_t st) {
+    if (nrows <= 0) return 0;
+    hipLaunchKernelGGL(k_pack_rows, dim3(grid_elems((long)nrows * ld, 4)), dim3(kBlock), 0, st, nrows, ld, rows,
+                       src, dst);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+// Loopback transport (tests: several shards in one process on one GPU): out = sum of
+// the shards' buffers in rank order.
+struct SumSrc { const double *p[kMaxShards]; };
+__global__ void __launch_bounds__(kBlock) k_sum_shards(int n, int world, SumSrc src, double *__restrict__ out) {
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        double v = 0.0;
+        for (int q = 0; q < world; ++q) v += src.p[q][i];
+        out[i] = v;
+    }
+}
+int launch_sum_shards(int n, int world, const double *const *src, double *out, hipStream_t st) {
+    if (world > kMaxShards) { snprintf(g_err, sizeof(g_err), "sum_shards: world %d", world); return -1; }
+    SumSrc s{};
+    for (int q = 0; q < world; ++q) s.p[q] = src[q];
+    hipLaunchKernelGGL(k_sum_shards, dim3(grid_elems(n, 1)), dim3(kBlock), 0, st, n, world, s, out);
+    LRS_CHECK_LAUNCH();
+    return 0;
 }
 
 // ------------------------------------------------------------------------
@@ -2238,8 +2339,12 @@ __global__ void __launch_bounds__(kBlock) k_gram_reduce(int nblk, int rr, const 
 }
 
 int launch_resid(int m, const double *b, const double *x, hipStream_t st) {
-    static double *part = nullptr;
-    if (!part && hipMalloc((void **)&part, sizeof(double) * kMaxPartialBlocks) != hipSuccess) return -1;
+    static double *gpart = nullptr;
+    double *part = t_rpart;
+    if (!part) {
+        if (!gpart && hipMalloc((void **)&gpart, sizeof(double) * kMaxPartialBlocks) != hipSuccess) return -1;
+        part = gpart;
+    }
     hipLaunchKernelGGL(k_resid, dim3(grid_elems(m, 1)), dim3(kBlock), 0, st, m, b, x, part, ticket_ptr(T_RR + 40),
                        tmpfin_ptr() + TF_RESID);
     LRS_CHECK_LAUNCH();

@@ -255,6 +255,101 @@ bool build_problem_coo(int m, int nblk, const int *dims_in, const double *b, lon
     return build_problem(m, K, dims, nLp, lpEntries, raw, hp, err);
 }
 
+bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, ShardPlan &plan, std::string &err) {
+    if (g.K != 1) { err = "sharded solve: one SDP cone only"; return false; }
+    const HostCone &gc = g.cones[0];
+    const int n = gc.n;
+    if (world < 1 || rank < 0 || rank >= world || n < world) { err = "sharded solve: bad world/rank for n"; return false; }
+    plan = ShardPlan();
+    plan.world = world; plan.rank = rank; plan.n_global = n;
+    // contiguous blocks balanced by (adjacency entries + 1) per row
+    std::vector<long> cum(n + 1, 0);
+    for (int i = 0; i < n; ++i) cum[i + 1] = cum[i] + (gc.adj_ptr[i + 1] - gc.adj_ptr[i]) + 1;
+    plan.bounds.assign(world + 1, 0);
+    for (int q = 1; q < world; ++q) {
+        const long target = cum[n] * q / world;
+        int b = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        b = std::max(b, plan.bounds[q - 1] + 1);
+        b = std::min(b, n - (world - q));
+        plan.bounds[q] = b;
+    }
+    plan.bounds[world] = n;
+    auto owner = [&](int i) { return (int)(std::upper_bound(plan.bounds.begin(), plan.bounds.end(), i) - plan.bounds.begin()) - 1; };
+    const int r0 = plan.bounds[rank], r1 = plan.bounds[rank + 1];
+    // constraint ownership: all entries of a constraint inside one shard's rows
+    std::vector<int> con_owner(g.m, -1);
+    for (const HostEntry &e : gc.ent) {
+        const int oi = owner(gc.prow[e.slot]), oj = owner(gc.pcol[e.slot]);
+        if (oi != oj || (con_owner[e.con] >= 0 && con_owner[e.con] != oi)) {
+            err = "sharded solve: constraint " + std::to_string(e.con + 1) + " spans row blocks";
+            return false;
+        }
+        con_owner[e.con] = oi;
+    }
+    for (int i = 0; i < g.m; ++i)
+        if (con_owner[i] < 0) con_owner[i] = 0;   // constraints without entries: shard 0 (residual b_i)
+    // local rows: owned + halo, in global order
+    std::vector<char> need(n, 0);
+    for (int i = r0; i < r1; ++i) {
+        need[i] = 1;
+        for (int k = gc.adj_ptr[i]; k < gc.adj_ptr[i + 1]; ++k) need[gc.adj_col[k]] = 1;
+    }
+    std::vector<int> lid(n, -1);
+    for (int i = 0; i < n; ++i)
+        if (need[i]) { lid[i] = (int)plan.gid.size(); plan.gid.push_back(i); }
+    const int nl = (int)plan.gid.size();
+    plan.row0 = lid[r0];
+    plan.nown = r1 - r0;
+    // local constraints in global order
+    std::vector<int> clid(g.m, -1);
+    for (int i = 0; i < g.m; ++i)
+        if (con_owner[i] == rank) { clid[i] = (int)plan.con_gid.size(); plan.con_gid.push_back(i); }
+    const int ml = (int)plan.con_gid.size();
+    // entries of the local problem (already merged and sign-converted: build_problem input)
+    std::vector<RawEntry> raw;
+    for (size_t t = 0; t < gc.prow.size(); ++t) {
+        const int i = gc.prow[t], j = gc.pcol[t];
+        if (!gc.Chas[t] || (owner(i) != rank && owner(j) != rank)) continue;
+        raw.push_back({0, 0, lid[i], lid[j], gc.Craw[t]});
+    }
+    for (const HostEntry &e : gc.ent) {
+        if (clid[e.con] < 0) continue;
+        raw.push_back({0, clid[e.con] + 1, lid[gc.prow[e.slot]], lid[gc.pcol[e.slot]], e.a});
+    }
+    out = HostProblem();
+    out.b.resize(ml);
+    for (int q = 0; q < ml; ++q) out.b[q] = g.b[plan.con_gid[q]];
+    if (!build_problem(ml, 1, std::vector<int>{nl}, 0, false, raw, out, err)) return false;
+    // the solve's norms and rank statistics are the whole problem's
+    out.bNrm1 = g.bNrm1; out.bNrm2 = g.bNrm2; out.bNrmInf = g.bNrmInf;
+    out.cNrm1 = g.cNrm1; out.cNrm2 = g.cNrm2; out.cNrmInf = g.cNrmInf;
+    HostCone &oc = out.cones[0];
+    oc.nnzRows = gc.nnzRows; oc.denseCoeff = gc.denseCoeff;
+    oc.cNrm1 = gc.cNrm1; oc.cNrm2sq = gc.cNrm2sq; oc.cNrmInf = gc.cNrmInf;
+    // halo exchange plan: rows of ours adjacent to each peer's rows (both sides derive the
+    // same global-order lists), and the peers' rows in our halo (contiguous locally)
+    plan.send_ptr.assign(world + 1, 0);
+    plan.recv_start.assign(world, 0);
+    plan.recv_cnt.assign(world, 0);
+    for (int q = 0; q < world; ++q) {
+        plan.send_ptr[q] = (int)plan.send_rows.size();
+        if (q == rank) continue;
+        const int q0 = plan.bounds[q], q1 = plan.bounds[q + 1];
+        for (int i = r0; i < r1; ++i) {
+            bool adj = false;
+            for (int k = gc.adj_ptr[i]; k < gc.adj_ptr[i + 1] && !adj; ++k) adj = gc.adj_col[k] >= q0 && gc.adj_col[k] < q1;
+            if (adj) plan.send_rows.push_back(lid[i]);
+        }
+        int first = -1, cnt = 0;
+        for (int l = 0; l < nl; ++l)
+            if (plan.gid[l] >= q0 && plan.gid[l] < q1) { if (first < 0) first = l; cnt++; }
+        plan.recv_start[q] = first < 0 ? 0 : first;
+        plan.recv_cnt[q] = cnt;
+    }
+    plan.send_ptr[world] = (int)plan.send_rows.size();
+    return true;
+}
+
 template <typename T>
 static bool dput(T **dst, const std::vector<T> &v, std::string &err) {
     size_t bytes = std::max<size_t>(1, v.size()) * sizeof(T);
@@ -422,6 +517,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         }
         ap[ntot] = (int)e0;
         mc.n = (int)ntot;
+        mc.nown = (int)ntot;
         mc.P = (int)Ptot_l;
         mc.adj_nnz = nadj;
         if (!dput(&mc.adj_ptr, ap, err) || !dput(&mc.adj_low, al, err) || !dput(&mc.adj_col, ac, err) ||
@@ -433,6 +529,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         const HostCone &c = hp.cones[k];
         DevCone &d = dp.cones[k];
         d.n = c.n;
+        d.nown = c.n;
         std::vector<int> adj_slot_g(c.adj_slot.size());
         for (size_t t = 0; t < c.adj_slot.size(); ++t) adj_slot_g[t] = d.slot_off + c.adj_slot[t];
         d.adj_nnz = (long)c.adj_col.size();

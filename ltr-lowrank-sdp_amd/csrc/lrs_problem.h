@@ -45,6 +45,24 @@ bool build_problem_coo(int m, int nblk, const int *dims, const double *b, long n
                        const int *blk, const int *row, const int *col, const double *val, HostProblem &hp,
                        std::string &err);
 
+// Sharded solve: the rows of the (single) cone split into `world`
+// contiguous blocks balanced by adjacency entries.  Shard `rank` owns rows
+// [bounds[rank], bounds[rank+1]) and every constraint whose entries lie in its rows;
+// its local problem holds the owned rows plus the halo (the other shards' rows its
+// rows are adjacent to), numbered in global order, and the slots with at least one
+// owned endpoint.  Norms and rank statistics stay the global ones.
+struct ShardPlan {
+    int world = 1, rank = 0;
+    int n_global = 0;
+    std::vector<int> bounds;                 // [world + 1] global row partition
+    std::vector<int> gid;                    // local row -> global row
+    int row0 = 0, nown = 0;                  // owned rows: local [row0, row0 + nown)
+    std::vector<int> send_ptr, send_rows;    // rows sent to each peer: local ids, grouped by peer
+    std::vector<int> recv_start, recv_cnt;   // halo rows from each peer: local first row, count
+    std::vector<int> con_gid;                // local constraint -> global constraint
+};
+bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, ShardPlan &plan, std::string &err);
+
 // Device upload of everything that does not depend on the rank.
 bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err);
 void free_problem(DevProblem &dp);

@@ -16,9 +16,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <string>
+#include <condition_variable>
 #include <map>
+#include <mutex>
+#include <string>
 #include <vector>
+
+#include <rccl/rccl.h>
 
 #include "../../include/lrsdp.h"
 #include "lrs_device.h"
@@ -145,7 +149,191 @@ struct lrs_ctx {
     hipEvent_t pev[2][5] = {};
     double pacc[4] = {0, 0, 0, 0};
     long pn = 0;
+    // per-context scratch of the standalone reductions (bound to the calling thread)
+    unsigned *s_tickets = nullptr;
+    double *s_tmpfin = nullptr, *s_rpart = nullptr;
+    // sharded solve (lrs_shard_*): this process's rows, the transport, the stage hooks
+    struct ShardComm *comm = nullptr;
+    ShardPlan plan;
+    ShardHooks hooks;
+    int *d_send_rows = nullptr;
+    double *d_sendbuf = nullptr;
+    long sendbuf_len = 0;
 };
+
+// ------------------------------------------------------------------------
+// sharded solve: transports.  Every collective is called by all shards in the same
+// order (the host control flow is identical on every shard: it only sees summed values).
+// ------------------------------------------------------------------------
+struct ShardComm {
+    virtual ~ShardComm() {}
+    // in-place sum over shards of n device doubles, ordered on stream st
+    virtual int allreduce_dev(lrs_ctx *c, double *buf, int n, hipStream_t st) = 0;
+    // blocking sum over shards of n host doubles
+    virtual int allreduce_host(lrs_ctx *c, double *v, int n) = 0;
+    // direction rows: this shard's send rows to each peer, the halo rows from them
+    virtual int halo(lrs_ctx *c, double *D, hipStream_t st) = 0;
+};
+static bool sharded(const lrs_ctx *c) { return c->comm != nullptr; }
+static int cone_n_global(const lrs_ctx *c, int k) { return sharded(c) ? c->plan.n_global : c->hp.cones[k].n; }
+
+// pack this shard's send rows (all peers) into the send buffer
+static int pack_send_rows(lrs_ctx *c, const double *D, hipStream_t st) {
+    const int ld = c->dp.cones[0].ld;
+    const long need = std::max(1L, (long)c->plan.send_rows.size() * ld);
+    if (need > c->sendbuf_len) {
+        if (c->d_sendbuf) HIPC(hipFree(c->d_sendbuf));
+        HIPC(hipMalloc((void **)&c->d_sendbuf, sizeof(double) * need));
+        c->sendbuf_len = need;
+    }
+    OPC(launch_pack_rows((int)c->plan.send_rows.size(), ld, c->d_send_rows, D, c->d_sendbuf, st));
+    return 0;
+}
+
+#define NCCLC(x)                                                                            \
+    do {                                                                                    \
+        ncclResult_t r_ = (x);                                                              \
+        if (r_ != ncclSuccess) {                                                            \
+            set_err("%s:%d %s: %s", __FILE__, __LINE__, #x, ncclGetErrorString(r_));        \
+            return -1;                                                                      \
+        }                                                                                   \
+    } while (0)
+
+// RCCL over xGMI: one process per GPU
+struct RcclComm : ShardComm {
+    ncclComm_t comm = nullptr;
+    double *dscr = nullptr;   // host all-reduce staging
+    int dscr_len = 0;
+    ~RcclComm() override {
+        if (comm) (void)ncclCommDestroy(comm);
+        if (dscr) (void)hipFree(dscr);
+    }
+    int allreduce_dev(lrs_ctx *, double *buf, int n, hipStream_t st) override {
+        NCCLC(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, comm, st));
+        return 0;
+    }
+    int allreduce_host(lrs_ctx *c, double *v, int n) override {
+        if (n > dscr_len) {
+            if (dscr) HIPC(hipFree(dscr));
+            HIPC(hipMalloc((void **)&dscr, sizeof(double) * n));
+            dscr_len = n;
+        }
+        HIPC(hipMemcpyAsync(dscr, v, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+        NCCLC(ncclAllReduce(dscr, dscr, n, ncclDouble, ncclSum, comm, c->st));
+        HIPC(hipMemcpyAsync(v, dscr, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
+        HIPC(hipStreamSynchronize(c->st));
+        return 0;
+    }
+    int halo(lrs_ctx *c, double *D, hipStream_t st) override {
+        const ShardPlan &pl = c->plan;
+        const int ld = c->dp.cones[0].ld;
+        if (pack_send_rows(c, D, st)) return -1;
+        NCCLC(ncclGroupStart());
+        for (int q = 0; q < pl.world; ++q) {
+            const int ns = pl.send_ptr[q + 1] - pl.send_ptr[q];
+            if (ns > 0) NCCLC(ncclSend(c->d_sendbuf + (long)pl.send_ptr[q] * ld, (size_t)ns * ld, ncclDouble, q, comm, st));
+            if (pl.recv_cnt[q] > 0)
+                NCCLC(ncclRecv(D + (long)pl.recv_start[q] * ld, (size_t)pl.recv_cnt[q] * ld, ncclDouble, q, comm, st));
+        }
+        NCCLC(ncclGroupEnd());
+        return 0;
+    }
+};
+
+// One-process loopback transport for tests: the shards are contexts on one GPU driven by
+// one host thread each; collectives meet at host barriers and order the shards' streams
+// with events (every shard waits for all shards' work before reading their buffers, and
+// again before anyone reuses them).
+struct lrs_loopback {
+    int world = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    long gen = 0;
+    std::vector<hipEvent_t> ev_pre, ev_post;
+    std::vector<const double *> bufs;
+    std::vector<const double *> sendbufs;
+    std::vector<const ShardPlan *> plans;
+    std::vector<std::vector<double>> hv;
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const long g = gen;
+        if (++arrived == world) { arrived = 0; gen++; cv.notify_all(); }
+        else cv.wait(lk, [&] { return gen != g; });
+    }
+};
+struct LoopComm : ShardComm {
+    lrs_loopback *g = nullptr;
+    int rank = 0;
+    double *dsum = nullptr;
+    int dsum_len = 0;
+    ~LoopComm() override { if (dsum) (void)hipFree(dsum); }
+    int pre(hipStream_t st) {
+        HIPC(hipEventRecord(g->ev_pre[rank], st));
+        g->barrier();
+        for (int q = 0; q < g->world; ++q) HIPC(hipStreamWaitEvent(st, g->ev_pre[q], 0));
+        return 0;
+    }
+    int post(hipStream_t st) {
+        HIPC(hipEventRecord(g->ev_post[rank], st));
+        g->barrier();
+        for (int q = 0; q < g->world; ++q) HIPC(hipStreamWaitEvent(st, g->ev_post[q], 0));
+        return 0;
+    }
+    int allreduce_dev(lrs_ctx *, double *buf, int n, hipStream_t st) override {
+        if (n > dsum_len) {
+            if (dsum) HIPC(hipFree(dsum));
+            HIPC(hipMalloc((void **)&dsum, sizeof(double) * n));
+            dsum_len = n;
+        }
+        g->bufs[rank] = buf;
+        if (pre(st)) return -1;
+        OPC(launch_sum_shards(n, g->world, g->bufs.data(), dsum, st));
+        if (post(st)) return -1;
+        HIPC(hipMemcpyAsync(buf, dsum, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+        return 0;
+    }
+    int allreduce_host(lrs_ctx *, double *v, int n) override {
+        g->hv[rank].assign(v, v + n);
+        g->barrier();
+        for (int i = 0; i < n; ++i) {
+            double t = 0.0;
+            for (int q = 0; q < g->world; ++q) t += g->hv[q][i];
+            v[i] = t;
+        }
+        g->barrier();
+        return 0;
+    }
+    int halo(lrs_ctx *c, double *D, hipStream_t st) override {
+        const int ld = c->dp.cones[0].ld;
+        if (pack_send_rows(c, D, st)) return -1;
+        g->sendbufs[rank] = c->d_sendbuf;
+        if (pre(st)) return -1;
+        for (int q = 0; q < g->world; ++q) {
+            const int cnt = c->plan.recv_cnt[q];
+            if (q == rank || cnt == 0) continue;
+            const ShardPlan &pq = *g->plans[q];
+            if (pq.send_ptr[rank + 1] - pq.send_ptr[rank] != cnt) { set_err("loopback halo: plan mismatch"); return -1; }
+            HIPC(hipMemcpyAsync(D + (long)c->plan.recv_start[q] * ld, g->sendbufs[q] + (long)pq.send_ptr[rank] * ld,
+                                sizeof(double) * cnt * ld, hipMemcpyDeviceToDevice, st));
+        }
+        return post(st);
+    }
+};
+
+static int hook_halo(void *self, double *D, hipStream_t st) {
+    lrs_ctx *c = static_cast<lrs_ctx *>(self);
+    return c->comm->halo(c, D, st);
+}
+static int hook_allreduce(void *self, double *buf, int n, hipStream_t st) {
+    lrs_ctx *c = static_cast<lrs_ctx *>(self);
+    return c->comm->allreduce_dev(c, buf, n, st);
+}
+// this context's device, stream-free scratch bound to the calling thread
+static void bind(lrs_ctx *c) {
+    (void)hipSetDevice(c->device);
+    bind_scratch(c->s_tickets, c->s_tmpfin, c->s_rpart);
+}
 
 static void drop_graphs(lrs_ctx *c) {
     for (auto &kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
@@ -172,7 +360,7 @@ static void free_work(lrs_ctx *c) {
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
                       W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2,
-                      W.cgc};
+                      W.cgc, W.tot};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     c->W = DevWork();
@@ -189,7 +377,7 @@ static int zero_work(lrs_ctx *c) {
         {W.U, NR}, {W.V, NR}, {W.X, NR}, {W.cg_r, NR}, {W.cg_p, NR}, {W.cg_Q, NR}, {W.cg_b, NR}, {W.M2, NR},
         {W.R2, NR}, {W.uvt0, Pt}, {W.uvt1, Pt}, {W.uvt2, Pt}, {W.S, Pt}, {W.lam, m}, {W.cvs, m}, {W.q1, m},
         {W.q2, m}, {W.M1, m}, {W.wtmp, m}, {W.cvc, (long)m * std::max(1, P.K)}, {W.ctrl, 2 * C_NCTRL},
-        {W.lsres, 2 * LS_N}, {W.rec, 4L * m}};
+        {W.lsres, 2 * LS_N}, {W.rec, 4L * m}, {W.tot, 32}};
     for (auto &z : zs) HIPC(hipMemsetAsync(z.p, 0, sizeof(double) * z.n, c->st));
     c->head = 0; c->gcur = 0;
     c->beta[0] = c->beta[1] = c->yy[0] = c->yy[1] = 0;
@@ -231,7 +419,8 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         A(&W.M1, m) || A(&W.wtmp, m) || A(&W.cvc, (long)m * std::max(1, P.K)) ||
         A(&W.part, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.partB, (long)kMaxPartialVals * kMaxPartialBlocks) ||
         A(&W.partC, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.ctrl, 2 * C_NCTRL) ||
-        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax) || A(&W.rec, 4L * m) || A(&W.R2, NR) || A(&W.cgc, 8))
+        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax) || A(&W.rec, 4L * m) || A(&W.R2, NR) || A(&W.cgc, 8) ||
+        A(&W.tot, 32))
         return -1;
     HIPC(hipStreamSynchronize(c->st));
     c->walloc = true;
@@ -297,6 +486,8 @@ static int read_tmpfin(lrs_ctx *c, int idx, int n, double *out) {
     HIPC(hipMemcpyAsync(c->hpin, device_tmpfin() + idx, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
     HIPC(hipStreamSynchronize(c->st));
     for (int i = 0; i < n; ++i) out[i] = c->hpin[i];
+    // sharded: every standalone reduction is a sum over the shard's rows / constraints
+    if (sharded(c)) return c->comm->allreduce_host(c, out, n);
     return 0;
 }
 
@@ -419,6 +610,7 @@ static int gram_of(lrs_ctx *c, int k, const double *X, const double *Y, int avg,
     g.resize(rr);
     HIPC(hipMemcpyAsync(g.data(), c->W.gram + 64L * rr, sizeof(double) * rr, hipMemcpyDeviceToHost, c->st));
     HIPC(hipStreamSynchronize(c->st));
+    if (sharded(c)) return c->comm->allreduce_host(c, g.data(), rr);
     return 0;
 }
 
@@ -458,10 +650,11 @@ static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &ra
     std::vector<int> dflt(K);
     for (int k = 0; k < K; ++k) {
         const HostCone &hc = c->hp.cones[k];
+        const int hn = cone_n_global(c, k);
         int nnzRows = hc.nnzRows;
-        int calc = std::min((int)std::sqrt(2.0 * nnzRows) + 1, hc.n);
+        int calc = std::min((int)std::sqrt(2.0 * nnzRows) + 1, hn);
         if (p->fixedRank > 0) {
-            rank[k] = std::max(1, std::min(p->fixedRank, hc.n));
+            rank[k] = std::max(1, std::min(p->fixedRank, hn));
             rmax[k] = rank[k];
             dflt[k] = rank[k];
             tot_default += rank[k];
@@ -469,10 +662,10 @@ static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &ra
         }
         rmax[k] = calc;
         int rk;
-        if (p->initRank > 0) rk = std::min(p->initRank, hc.n);
+        if (p->initRank > 0) rk = std::min(p->initRank, hn);
         else if (p->timesLogRank <= 1e-6) rk = calc;
-        else if (nnzRows / hc.n >= 20 && hc.n <= 400 && K <= 3) rk = calc;
-        else rk = (int)std::min(std::ceil(p->timesLogRank * std::log((double)hc.n)), (double)calc);
+        else if (nnzRows / hn >= 20 && hn <= 400 && K <= 3) rk = calc;
+        else rk = (int)std::min(std::ceil(p->timesLogRank * std::log((double)hn)), (double)calc);
         rank[k] = std::max(1, rk);
         dflt[k] = rank[k];
         tot_default += rank[k];
@@ -482,7 +675,7 @@ static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &ra
         int tot = std::max(1, p->rankSchedule[0]);
         for (int k = 0; k < K; ++k) {
             int rk = (int)std::lround((double)tot * dflt[k] / std::max(1, tot_default));
-            rank[k] = std::max(1, std::min(rk, c->hp.cones[k].n));
+            rank[k] = std::max(1, std::min(rk, cone_n_global(c, k)));
             rmax[k] = std::max(rmax[k], rank[k]);
         }
     }
@@ -497,12 +690,20 @@ static int init_point(lrs_ctx *c) {
     }
     GlibcRand g(925);
     long NRc = 0;
-    for (int k = 0; k < c->dp.K; ++k) NRc += (long)c->dp.cones[k].n * c->rank[k];
+    for (int k = 0; k < c->dp.K; ++k) NRc += (long)cone_n_global(c, k) * c->rank[k];
     std::vector<double> R(NRc);
     for (long i = 0; i < NRc; ++i) {
         double v = (double)g.next() / 2147483647.0;
         v -= (double)g.next() / 2147483647.0;
         R[i] = v;
+    }
+    if (sharded(c)) {
+        // the whole problem's draw, then this shard's rows (owned + halo)
+        const int ng = c->plan.n_global, nl = c->dp.cones[0].n, r = c->rank[0];
+        std::vector<double> Rl((long)nl * r);
+        for (int q = 0; q < r; ++q)
+            for (int l = 0; l < nl; ++l) Rl[l + (long)q * nl] = R[c->plan.gid[l] + (long)q * ng];
+        R.swap(Rl);
     }
     if (factor_put(c, c->W.R, R.data())) return -1;
     // keep the device-layout copy: every solve at these ranks starts from the same point
@@ -541,8 +742,15 @@ static int regrow(lrs_ctx *c, const std::vector<int> &nr) {
         const int n = c->dp.cones[k].n, ro = c->rank[k], rn = nr[k];
         auto grow = [&](const std::vector<double> &src, std::vector<double> &dst) {
             std::copy(src.begin() + so, src.begin() + so + (long)n * ro, dst.begin() + dn);
-            const int aug = rn - ro, r = std::min(n, aug);   // lpRandomDiag :1096-1106
-            for (int i = 0; i < r; ++i) dst[dn + (long)n * ro + (long)i * n + i] = 1 / std::sqrt((double)r);
+            const int aug = rn - ro, r = std::min(cone_n_global(c, k), aug);   // lpRandomDiag :1096-1106
+            if (sharded(c)) {   // global row i of new column i, on the shard's local rows
+                for (int l = 0; l < n; ++l) {
+                    const int gi = c->plan.gid[l];
+                    if (gi < r) dst[dn + (long)n * ro + (long)gi * n + l] = 1 / std::sqrt((double)r);
+                }
+            } else {
+                for (int i = 0; i < r; ++i) dst[dn + (long)n * ro + (long)i * n + i] = 1 / std::sqrt((double)r);
+            }
         };
         grow(R, Rn); grow(U, Un); grow(V, Vn); grow(G, Gn);
         so += (long)n * ro;
@@ -570,7 +778,7 @@ static int aug_rank(lrs_ctx *c, double f, const lrs_params *p, int *sched_pos, i
         int tot = std::max(1, p->rankSchedule[pos]), cur = sum_rank(c);
         for (int k = 0; k < c->dp.K; ++k) {
             int rk = (int)std::lround((double)tot * c->rank[k] / std::max(1, cur));
-            nr[k] = std::max(c->rank[k], std::min(rk, c->hp.cones[k].n));
+            nr[k] = std::max(c->rank[k], std::min(rk, cone_n_global(c, k)));
             c->rank_max[k] = std::max(c->rank_max[k], nr[k]);
         }
     } else {
@@ -823,7 +1031,9 @@ ALG_START:
             if (st.gap <= p->phase1Tol * 1e-3 && st.pinf1 <= p->phase1Tol * 1e-3) goto PRINT_AND_EXIT;
             record_state(c, p, 1);
             alm_log(c, p, st, now_s() - ori);
-            if (now_s() - tss >= p->timeSecLimit) goto PRINT_AND_EXIT;
+            double tout = now_s() - tss >= p->timeSecLimit ? 1.0 : 0.0;
+            if (sharded(c) && c->comm->allreduce_host(c, &tout, 1)) return -1;   // every shard stops together
+            if (tout > 0) goto PRINT_AND_EXIT;
         }
         if (rank_flag >= thres && !is_rank_max) {
             rank_flag = 0;
@@ -1073,11 +1283,21 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
     if (const char *ug = getenv("LRS_GRAPHS")) c->use_graphs = (atoi(ug) != 0);
     if (const char *sv = getenv("LRS_STATS")) c->stats = (atoi(sv) != 0);
     if (hipHostMalloc((void **)&c->hpin, 4096 * sizeof(double), 0) != hipSuccess) { set_err("pinned alloc failed"); delete c; return -1; }
+    if (hipMalloc((void **)&c->s_tickets, 64 * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(c->s_tickets, 0, 64 * sizeof(unsigned)) != hipSuccess ||
+        hipMalloc((void **)&c->s_tmpfin, TF_N * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&c->s_rpart, kMaxPartialBlocks * sizeof(double)) != hipSuccess) {
+        set_err("scratch alloc failed");
+        lrs_ctx_destroy(c);
+        return -1;
+    }
+    bind(c);
     *out = c;
     return 0;
 }
 
 int lrs_set_log_path(lrs_ctx *c, const char *path) {
+    if (c) bind(c);
     if (c->logfp) fclose(c->logfp);
     c->logfp = fopen(path, "w");
     if (!c->logfp) { set_err("cannot open log %s", path); return -1; }
@@ -1092,11 +1312,17 @@ void lrs_ctx_destroy(lrs_ctx *c) {
     free_work(c);
     if (c->loaded) free_problem(c->dp);
     if (c->hpin) (void)hipHostFree(c->hpin);
+    delete c->comm;
+    for (void *q : {(void *)c->s_tickets, (void *)c->s_tmpfin, (void *)c->s_rpart, (void *)c->d_send_rows,
+                    (void *)c->d_sendbuf})
+        if (q) (void)hipFree(q);
+    bind_scratch(nullptr, nullptr, nullptr);
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
 }
 
 int lrs_load_sdpa(lrs_ctx *c, const char *path, double *read_seconds) {
+    if (c) bind(c);
     const double t0 = now_s();
     std::string err;
     HostProblem hp;
@@ -1114,6 +1340,7 @@ int lrs_load_sdpa(lrs_ctx *c, const char *path, double *read_seconds) {
 
 int lrs_load_coo(lrs_ctx *c, int m, int nblk, const int *dims, const double *b, long nnz, const int *con,
                  const int *blk, const int *row, const int *col, const double *val) {
+    if (c) bind(c);
     if (!c) { set_err("null ctx"); return -1; }
     std::string err;
     HostProblem hp;
@@ -1132,6 +1359,7 @@ int lrs_load_coo(lrs_ctx *c, int m, int nblk, const int *dims, const double *b, 
 }
 
 int lrs_auut_bytes(lrs_ctx *c, double *bytes) {
+    if (c) bind(c);
     // A(U U^T) over constraint entries (SURVEY.md §8(d) B_A with delta = 1): the factor
     // rows touched (each row once when distinct), per entry con_slot + con_w + slot
     // coordinates (16 B), con_ptr, and the m outputs.
@@ -1154,6 +1382,7 @@ int lrs_auut_bytes(lrs_ctx *c, double *bytes) {
 }
 
 int lrs_stage_bytes(lrs_ctx *c, double *bytes) {
+    if (c) bind(c);
     // Algorithmic HBM bytes per launch of the split-iteration stages:
     // every array the stage must touch, once, at its unpadded size; L-BFGS with two
     // pairs; int32 indices, FP64 values.  n, r per cone; P lower slots; adjacency
@@ -1181,6 +1410,7 @@ int lrs_stage_bytes(lrs_ctx *c, double *bytes) {
 }
 
 int lrs_problem_info(lrs_ctx *c, int *m, int *ncones, int *dims, long *nslots, long *nnzc) {
+    if (c) bind(c);
     if (!c->loaded) { set_err("no problem loaded"); return -1; }
     if (m) *m = c->hp.m;
     if (ncones) *ncones = c->hp.K;
@@ -1191,6 +1421,7 @@ int lrs_problem_info(lrs_ctx *c, int *m, int *ncones, int *dims, long *nslots, l
 }
 
 int lrs_determine_rank(lrs_ctx *c, const lrs_params *p, int *ranks_out) {
+    if (c) bind(c);
     if (!c->loaded) { set_err("no problem loaded"); return -1; }
     std::vector<int> r, rm;
     determine_rank(c, p, r, rm);
@@ -1199,29 +1430,34 @@ int lrs_determine_rank(lrs_ctx *c, const lrs_params *p, int *ranks_out) {
 }
 
 int lrs_set_rank(lrs_ctx *c, const int *ranks) {
+    if (c) bind(c);
     if (!c->loaded) { set_err("no problem loaded"); return -1; }
     std::vector<int> r(ranks, ranks + c->hp.K);
     c->rank_max = r;
     return alloc_work(c, r);
 }
 int lrs_get_rank(lrs_ctx *c, int *ranks) {
+    if (c) bind(c);
     for (size_t k = 0; k < c->rank.size(); ++k) ranks[k] = c->rank[k];
     return 0;
 }
 
 int lrs_factor_set(lrs_ctx *c, int which, const double *colmajor) {
+    if (c) bind(c);
     if (!c->walloc) { set_err("ranks not set"); return -1; }
     double *d = factor_ptr(c, which);
     if (!d) { set_err("bad factor id"); return -1; }
     return factor_put(c, d, colmajor);
 }
 int lrs_factor_get(lrs_ctx *c, int which, double *colmajor) {
+    if (c) bind(c);
     if (!c->walloc) { set_err("ranks not set"); return -1; }
     double *d = factor_ptr(c, which);
     if (!d) { set_err("bad factor id"); return -1; }
     return factor_fetch(c, d, colmajor);
 }
 int lrs_vec_set(lrs_ctx *c, int which, const double *v) {
+    if (c) bind(c);
     if (!c->walloc) { set_err("ranks not set"); return -1; }
     double *d = vec_ptr(c, which);
     if (!d) { set_err("bad vector id"); return -1; }
@@ -1229,6 +1465,7 @@ int lrs_vec_set(lrs_ctx *c, int which, const double *v) {
     return 0;
 }
 int lrs_vec_get(lrs_ctx *c, int which, double *v) {
+    if (c) bind(c);
     if (!c->walloc) { set_err("ranks not set"); return -1; }
     double *d = vec_ptr(c, which);
     if (!d) { set_err("bad vector id"); return -1; }
@@ -1238,6 +1475,7 @@ int lrs_vec_get(lrs_ctx *c, int which, double *v) {
 }
 
 int lrs_op_q12(lrs_ctx *c, double *q1, double *p1, double *q2, double *p2) {
+    if (c) bind(c);
     DevProblem &P = c->dp;
     DevWork &W = c->W;
     double a = 0, b = 0;
@@ -1263,6 +1501,7 @@ int lrs_op_q12(lrs_ctx *c, double *q1, double *p1, double *q2, double *p2) {
 }
 
 int lrs_op_constr_rr(lrs_ctx *c, double *cvs, double *pinf, double *pobj) {
+    if (c) bind(c);
     double pi, ob;
     if (op_constr_xx(c, c->W.R, nullptr, &pi, &ob)) return -1;
     if (pinf) *pinf = pi;
@@ -1275,6 +1514,7 @@ int lrs_op_constr_rr(lrs_ctx *c, double *cvs, double *pinf, double *pobj) {
 }
 
 int lrs_op_grad(lrs_ctx *c, double rho, double *lag) {
+    if (c) bind(c);
     double l;
     if (op_grad(c, rho, &l)) return -1;
     if (lag) *lag = l;
@@ -1282,6 +1522,7 @@ int lrs_op_grad(lrs_ctx *c, double rho, double *lag) {
 }
 
 int lrs_op_line_search(lrs_ctx *c, double rho, double *tau, int *root_num) {
+    if (c) bind(c);
     double par[P_NPAR] = {0};
     par[P_RHO] = rho;
     par[P_ENDTAU] = 1e-16;
@@ -1296,6 +1537,7 @@ int lrs_op_line_search(lrs_ctx *c, double rho, double *tau, int *root_num) {
 }
 
 int lrs_op_lbfgs(lrs_ctx *c, int node_num, double beta_new, double beta_old) {
+    if (c) bind(c);
     // White-box test of the fused direction kernel: ring slot 0 = newest pair
     // (S0, Y0, beta_new), slot 1 = older pair (S1, Y1, beta_old), gradient G[gcur].
     if (node_num < 0 || node_num > 2) { set_err("node_num must be 0..2"); return -1; }
@@ -1325,6 +1567,7 @@ int lrs_op_lbfgs(lrs_ctx *c, int node_num, double beta_new, double beta_old) {
 }
 
 int lrs_op_admm_half(lrs_ctx *c, double rho, double cg_tol, int cg_maxit, int *cg_iters, double *rhs) {
+    if (c) bind(c);
     DevProblem &P = c->dp;
     OPC(launch_fill(P.m, 0.0, c->W.cvs, c->st));
     for (int k = 0; k < P.K; ++k) {
@@ -1347,6 +1590,7 @@ int lrs_op_admm_half(lrs_ctx *c, double rho, double cg_tol, int cg_maxit, int *c
 }
 
 int lrs_op_gram(lrs_ctx *c, int cone, int which, double *gram) {
+    if (c) bind(c);
     std::vector<double> g;
     if (which == LRS_R) { if (gram_of(c, cone, c->W.R, nullptr, 0, g)) return -1; }
     else { if (gram_of(c, cone, c->W.U, c->W.V, 1, g)) return -1; }
@@ -1358,6 +1602,7 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     lrs_params prm = *pin;
     lrs_params *p = &prm;
     p->rhoCellingADMM = p->rhoMax * 200;   // main.c:350
+    if (sharded(c)) p->skipADMM = 1;       // the sharded solve covers the ALM phase
     memset(res, 0, sizeof(*res));
     const double tss = now_s();
     std::vector<int> r, rm;
@@ -1373,7 +1618,7 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     double rho = p->initRho;
     if (rho == 0) {   // initial_solver_state, data/lorads_solver.c:1599-1606
         long sd = 0;
-        for (auto &hc : c->hp.cones) sd += hc.n;
+        for (int k = 0; k < c->hp.K; ++k) sd += cone_n_global(c, k);
         rho = 1 / std::sqrt((double)sd);
     }
     alm.rho = rho; admm.rho = rho;
@@ -1426,11 +1671,13 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
 }
 
 int lrs_solve(lrs_ctx *c, const lrs_params *p, lrs_result *res) {
+    if (c) bind(c);
     if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
     return solve_impl(c, p, res);
 }
 
 int lrs_trajectory(lrs_ctx *c, int phase, int *curr, int *orc, int cap) {
+    if (c) bind(c);
     const std::vector<int> &a = phase == 1 ? c->t1c : c->t2c, &b = phase == 1 ? c->t1o : c->t2o;
     int n = std::min(cap, (int)a.size());
     for (int i = 0; i < n; ++i) { if (curr) curr[i] = a[i]; if (orc) orc[i] = b[i]; }
@@ -1439,6 +1686,7 @@ int lrs_trajectory(lrs_ctx *c, int phase, int *curr, int *orc, int cap) {
 
 int lrs_write_json(lrs_ctx *c, const char *path, const char *pid, const char *fpath, const lrs_result *r,
                    const lrs_params *p) {
+    if (c) bind(c);
     FILE *f = fopen(path, "w");
     if (!f) { set_err("cannot open %s", path); return -1; }
     fprintf(f, "{\n");
@@ -1471,6 +1719,7 @@ int lrs_write_json(lrs_ctx *c, const char *path, const char *pid, const char *fp
 
 int lrs_alm_throughput(lrs_ctx *c, const lrs_params *pin, long warmup, long steps, double *seconds, long *done,
                        double *sddmm_avg_ms, double *iter_avg_ms) {
+    if (c) bind(c);
     // ALM iters/s: the real phase-1 control flow (lorads_alm.c:1220)
     // at fixed rank with the phase-1 exit disabled, stopped after a budget of inner
     // iterations.  Warmup = an untimed run of `warmup` iterations from the same start;
@@ -1490,7 +1739,7 @@ int lrs_alm_throughput(lrs_ctx *c, const lrs_params *pin, long warmup, long step
     hipEvent_t e0, e1;
     HIPC(hipEventCreate(&e0));
     HIPC(hipEventCreate(&e1));
-    HIPC(hipDeviceSynchronize());
+    HIPC(hipStreamSynchronize(c->st));
     const double h0 = now_s();
     HIPC(hipEventRecord(e0, c->st));
     if (solve_impl(c, &prm, &r)) return -1;
@@ -1513,6 +1762,7 @@ int lrs_alm_throughput(lrs_ctx *c, const lrs_params *pin, long warmup, long step
 }
 
 int lrs_profile_stages(lrs_ctx *c, const lrs_params *pin, long steps, double *stage_ms, long *done) {
+    if (c) bind(c);
     if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
     lrs_params prm = *pin;
     prm.phase1Tol = 1e-300;
@@ -1537,6 +1787,7 @@ int lrs_profile_stages(lrs_ctx *c, const lrs_params *pin, long steps, double *st
 }
 
 int lrs_time_stages(lrs_ctx *c, int reps, double *stage_ms) {
+    if (c) bind(c);
     // Per-launch durations of the split-iteration stages on the current state: each
     // stage is launched `reps` times back to back between two HIP events on the solver
     // stream.  The stages are idempotent for a fixed control block (A reads ctrl[1] and
@@ -1577,12 +1828,14 @@ int lrs_time_stages(lrs_ctx *c, int reps, double *stage_ms) {
 }
 
 int lrs_debug_phase_times(lrs_ctx *c, unsigned long long *out, unsigned long long *blk) {
+    if (c) bind(c);
     if (!c) { set_err("null ctx"); return -1; }
-    HIPC(hipDeviceSynchronize());
+    HIPC(hipStreamSynchronize(c->st));
     return read_phase_times(out, blk);
 }
 
 int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {
+    if (c) bind(c);
     hipEvent_t e0, e1;
     HIPC(hipEventCreate(&e0));
     HIPC(hipEventCreate(&e1));
@@ -1604,6 +1857,7 @@ int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {
 // Standalone r x r Gram of cone `cone` on R (k_gram on the FP64 matrix cores + the
 // fixed-order partial reduction): reps back to back between two HIP events.
 int lrs_time_gram(lrs_ctx *c, int cone, int reps, double *avg_ms, double *gram_ms) {
+    if (c) bind(c);
     if (cone < 0 || cone >= c->dp.K) {
         set_err("time_gram: bad cone %d", cone);
         return -1;
@@ -1631,6 +1885,117 @@ int lrs_time_gram(lrs_ctx *c, int cone, int reps, double *avg_ms, double *gram_m
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipEventDestroy(e2);
+    return 0;
+}
+
+// ---- sharded solve
+int lrs_comm_unique_id(char *id_out) {
+    ncclUniqueId id;
+    NCCLC(ncclGetUniqueId(&id));
+    memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return 0;
+}
+
+static int shard_setup(lrs_ctx *c, int world, int rank) {
+    if (!c->loaded) { set_err("shard: no problem loaded"); return -1; }
+    if (sharded(c)) { set_err("shard: context is already sharded"); return -1; }
+    HostProblem sh;
+    ShardPlan pl;
+    std::string err;
+    if (!shard_problem(c->hp, world, rank, sh, pl, err)) { set_err("shard: %s", err.c_str()); return -1; }
+    free_work(c);
+    free_problem(c->dp);
+    c->loaded = false;
+    c->hp = std::move(sh);
+    c->plan = std::move(pl);
+    if (!upload_problem(c->hp, c->dp, err)) { set_err("shard upload: %s", err.c_str()); return -1; }
+    if (c->dp.mg > 0) { set_err("shard: constraints with several entries are not supported by the sharded solve"); return -1; }
+    DevCone &dc = c->dp.cones[0];
+    dc.row0 = c->plan.row0;
+    dc.nown = c->plan.nown;
+    c->hooks.self = c;
+    c->hooks.halo = hook_halo;
+    c->hooks.allreduce = hook_allreduce;
+    c->dp.shard = &c->hooks;
+    const size_t ns = std::max<size_t>(1, c->plan.send_rows.size());
+    HIPC(hipMalloc((void **)&c->d_send_rows, sizeof(int) * ns));
+    if (!c->plan.send_rows.empty())
+        HIPC(hipMemcpy(c->d_send_rows, c->plan.send_rows.data(), sizeof(int) * c->plan.send_rows.size(),
+                       hipMemcpyHostToDevice));
+    c->init_cache.clear();
+    c->init_ranks.clear();
+    c->cgIterCone.assign(c->hp.K, 0);
+    c->loaded = true;
+    return 0;
+}
+
+int lrs_shard_rccl(lrs_ctx *c, int world, int rank, const char *id) {
+    if (!c) { set_err("null ctx"); return -1; }
+    bind(c);
+    if (shard_setup(c, world, rank)) return -1;
+    RcclComm *rc = new RcclComm();
+    ncclUniqueId uid;
+    memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    const ncclResult_t r = ncclCommInitRank(&rc->comm, world, uid, rank);
+    if (r != ncclSuccess) {
+        rc->comm = nullptr;
+        delete rc;
+        set_err("ncclCommInitRank: %s", ncclGetErrorString(r));
+        return -1;
+    }
+    c->comm = rc;
+    return 0;
+}
+
+int lrs_loopback_create(int world, lrs_loopback **out) {
+    if (world < 1 || world > kMaxShards) { set_err("loopback: world %d", world); return -1; }
+    lrs_loopback *g = new lrs_loopback();
+    g->world = world;
+    g->ev_pre.assign(world, nullptr);
+    g->ev_post.assign(world, nullptr);
+    g->bufs.assign(world, nullptr);
+    g->sendbufs.assign(world, nullptr);
+    g->plans.assign(world, nullptr);
+    g->hv.assign(world, {});
+    *out = g;
+    return 0;
+}
+
+void lrs_loopback_destroy(lrs_loopback *g) {
+    if (!g) return;
+    for (auto e : g->ev_pre) if (e) (void)hipEventDestroy(e);
+    for (auto e : g->ev_post) if (e) (void)hipEventDestroy(e);
+    delete g;
+}
+
+int lrs_shard_loopback(lrs_ctx *c, lrs_loopback *g, int rank) {
+    if (!c || !g || rank < 0 || rank >= g->world) { set_err("loopback: bad arguments"); return -1; }
+    bind(c);
+    int rc = shard_setup(c, g->world, rank);
+    if (rc == 0 && (hipEventCreateWithFlags(&g->ev_pre[rank], hipEventDisableTiming) != hipSuccess ||
+                    hipEventCreateWithFlags(&g->ev_post[rank], hipEventDisableTiming) != hipSuccess)) {
+        set_err("loopback: event create failed");
+        rc = -1;
+    }
+    if (rc == 0) {
+        g->plans[rank] = &c->plan;
+        LoopComm *lc = new LoopComm();
+        lc->g = g;
+        lc->rank = rank;
+        c->comm = lc;
+    }
+    g->barrier();   // every shard's plan is registered before the first exchange
+    return rc;
+}
+
+int lrs_shard_info(lrs_ctx *c, int *world, int *rank, int *row0, int *nown, int *nhalo) {
+    if (!c) { set_err("null ctx"); return -1; }
+    const bool s = sharded(c);
+    if (world) *world = s ? c->plan.world : 1;
+    if (rank) *rank = s ? c->plan.rank : 0;
+    if (row0) *row0 = s ? c->plan.bounds[c->plan.rank] : 0;
+    if (nown) *nown = s ? c->plan.nown : (c->loaded ? c->hp.cones[0].n : 0);
+    if (nhalo) *nhalo = s ? c->dp.cones[0].n - c->plan.nown : 0;
     return 0;
 }
 

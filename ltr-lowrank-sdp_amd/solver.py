@@ -111,6 +111,12 @@ def load_library(path=None):
         "lrs_time_gram": (C.c_int, [vp, C.c_int, C.c_int, dp, dp]),
         "lrs_load_coo": (C.c_int, [vp, C.c_int, C.c_int, ip, dp, C.c_long, ip, ip, ip, ip, dp]),
         "lrs_debug_phase_times": (C.c_int, [vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
+        "lrs_comm_unique_id": (C.c_int, [C.c_char_p]),
+        "lrs_shard_rccl": (C.c_int, [vp, C.c_int, C.c_int, C.c_char_p]),
+        "lrs_loopback_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "lrs_loopback_destroy": (None, [vp]),
+        "lrs_shard_loopback": (C.c_int, [vp, vp, C.c_int]),
+        "lrs_shard_info": (C.c_int, [vp, ip, ip, ip, ip, ip]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -139,6 +145,32 @@ def default_params(**kw):
 
 def _dptr(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def comm_unique_id():
+    """RCCL unique id (128 bytes) for lrs_shard_rccl; made on rank 0 and broadcast."""
+    lib = load_library()
+    buf = C.create_string_buffer(128)
+    if lib.lrs_comm_unique_id(buf) != 0:
+        raise RuntimeError(f"comm_unique_id: {lib.lrs_last_error().decode()}")
+    return buf.raw
+
+
+class LoopbackGroup:
+    """One-process loopback transport of a sharded solve (tests): `world` Solvers on one
+    GPU, each driven by its own thread, call Solver.shard_loopback(group, rank)."""
+
+    def __init__(self, world):
+        self.lib = load_library()
+        self.h = C.c_void_p()
+        if self.lib.lrs_loopback_create(world, C.byref(self.h)) != 0:
+            raise RuntimeError(f"loopback_create: {self.lib.lrs_last_error().decode()}")
+        self.world = world
+
+    def close(self):
+        if self.h:
+            self.lib.lrs_loopback_destroy(self.h)
+            self.h = C.c_void_p()
 
 
 class Solver:
@@ -187,6 +219,27 @@ class Solver:
             self.close()
         except Exception:
             pass
+
+    # ---- sharded solve (include/lrsdp.h lrs_shard_*): call after loading, before solving
+    def shard_rccl(self, world, rank, uid):
+        self._check(self.lib.lrs_shard_rccl(self.ctx, world, rank, uid), "shard_rccl")
+        self._after_shard()
+
+    def shard_loopback(self, group, rank):
+        self._check(self.lib.lrs_shard_loopback(self.ctx, group.h, rank), "shard_loopback")
+        self._after_shard()
+
+    def _after_shard(self):
+        m, k = C.c_int(), C.c_int()
+        dims = (C.c_int * 1)()
+        self._check(self.lib.lrs_problem_info(self.ctx, C.byref(m), C.byref(k), dims, None, None), "info")
+        self.m, self.dims = m.value, list(dims)
+
+    def shard_info(self):
+        """(world, rank, first global row, owned rows, halo rows)."""
+        v = [C.c_int() for _ in range(5)]
+        self._check(self.lib.lrs_shard_info(self.ctx, *[C.byref(x) for x in v]), "shard_info")
+        return tuple(x.value for x in v)
 
     # ---- ranks / state
     def determine_rank(self, **kw):
