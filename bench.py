@@ -21,6 +21,11 @@ Prints one JSON line (rank 0).  Besides the contract keys:
                     the reference, with benchmark.py's flags per subtype
   cpu_baseline      the reference LoRADS C (oracle/_ref, built from /root/reference)
                     timed on this host, 1 core, on a bounded sample of the workload
+  config_c5         BASELINE config C5 (random sparse SDP n = 1e4, m = 1e6, r = 128): ALM it/s
+                    and the r x r Gram on the FP64 matrix cores (TFLOP/s vs the MFMA peak)
+  sharded           ONE G81-like instance (n = 20 000, r = 64) row-sharded over all N ranks
+                    (RCCL: halo exchange of direction rows + all-reduced stage totals per
+                    inner iteration): strong-scaling it/s of the single instance
 """
 import argparse
 import importlib
@@ -35,6 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 PKG = "ltr-lowrank-sdp_amd"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec)
 STAGES = ("A: k_it_a (control, L-BFGS direction, SDDMM sym(RD^T)/DD^T, local q1/q2)",
           "G: k_it_g (phase-1 test, multi-slot constraints' q1/q2)",
           "B: k_it_b (line search, R+tau D, adjoint S=C+A*(M1), G=2SR, A(RR^T), L-BFGS pair)")
@@ -109,6 +115,56 @@ def stage_roofline(sv, reps):
             "avg_launch_us": dom["avg_launch_us"], "stages": out, "a_uut": auut}
 
 
+def config_c5(solver, local, iters=20):
+    """BASELINE config C5 in memory: ALM it/s at r = 128, stage roofline, MFMA Gram."""
+    inst = importlib.import_module(PKG + ".instances")
+    t0 = time.perf_counter()
+    sv = solver.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(10000, 1000000, 6, 5)), device=local)
+    load_s = time.perf_counter() - t0
+    kw = dict(fixedRank=128, reoptLevel=0)
+    sv.alm_throughput(0, 4, **kw)
+    o = sv.alm_throughput(0, iters, **kw)
+    rl = stage_roofline(sv, 3)
+    ms, kms = sv.time_gram(0, 20)
+    n = sv.dims[0]
+    fl = n * 128 * 129   # the symmetric product (dsyrk count)
+    sv.close()
+    return {"workload": "random sparse SDP n=1e4, m=1e6, 6 entries/constraint, C=I, --fixedRank 128 (in memory)",
+            "gpu_it_s": o["done"] / o["seconds"], "load_sec": load_s, "roofline": rl,
+            "gram_mfma": {"kernel": "k_gram (v_mfma_f64_16x16x4_f64), R^T R, n=1e4, r=128", "bound": "mfma",
+                          "avg_launch_us": kms * 1e3, "with_reduction_us": ms * 1e3, "flop_per_launch": fl,
+                          "achieved": fl / (kms * 1e-3) / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                          "frac": fl / (kms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS},
+            "cpu_baseline": "not run: the reference's presolve alone takes ~1600 s on C5 (SURVEY.md §8(d))"}
+
+
+def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=500):
+    """ONE G81-like instance (torus 100 x 200, n = 20 000, r = 64) row-sharded over the
+    `world` ranks through RCCL (lrs_shard_rccl): whole-instance ALM it/s, strong scaling."""
+    p81 = instance_for(0, 100, 200, cache, seed0=81)
+    sv = solver.Solver(p81, device=local)
+    uid = solver.comm_unique_id() if rank_id == 0 else None
+    if dist is not None:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    sv.shard_rccl(world, rank_id, uid)
+    info = sv.shard_info()
+    kw = dict(fixedRank=64, reoptLevel=0)
+    sv.alm_throughput(0, 50, **kw)
+    replicas.barrier_sync(dist)
+    t0 = time.perf_counter()
+    out = sv.alm_throughput(0, steps, **kw)
+    replicas.barrier_sync(dist)
+    dt = time.perf_counter() - t0
+    sv.close()
+    _, t_max = replicas.aggregate(dist, out["done"], dt)
+    return {"workload": "MaxCut torus 100x200 (G81 structure), n=m=20000, --fixedRank 64, ONE instance "
+                        f"row-sharded over {world} GPU(s)", "it_s": out["done"] / t_max, "steps": out["done"],
+            "n_gpus": world, "scaling": "strong", "transport": "RCCL (ncclSend/Recv halo, ncclAllReduce totals)",
+            "rank0_rows": info[3], "rank0_halo_rows": info[4]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +179,9 @@ def main():
     ap.add_argument("--no-scale", action="store_true")
     ap.add_argument("--no-north-star", action="store_true")
     ap.add_argument("--no-configs", action="store_true")
+    ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--no-sharded", action="store_true")
+    ap.add_argument("--sharded-timeout", type=float, default=300.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -251,6 +310,25 @@ def main():
         rl["load_sec"] = load_s
         big.close()
         line["roofline_at_scale"] = rl
+    if rank_id == 0 and world == 1 and not args.no_c5:
+        line["config_c5"] = config_c5(solver, local)
+    if not args.no_sharded:
+        # a watchdog keeps a stuck collective from swallowing the result line
+        import threading
+
+        def fire():
+            if rank_id == 0:
+                line["sharded"] = {"error": f"no result within {args.sharded_timeout:.0f} s"}
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+        wd = threading.Timer(args.sharded_timeout, fire)
+        wd.daemon = True
+        wd.start()
+        try:
+            line["sharded"] = sharded_strong(solver, dist, world, rank_id, local, cache, replicas)
+        except Exception as e:   # reported in the line, the headline stands
+            line["sharded"] = {"error": repr(e)[:300]}
+        wd.cancel()
     if rank_id == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

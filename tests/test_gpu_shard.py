@@ -80,3 +80,21 @@ def test_sharded_deterministic(solver_mod):
     a = run_sharded(solver_mod, instance("mc_rand200"), 2, lambda sv: sv.solve(**kw))
     b = run_sharded(solver_mod, instance("mc_rand200"), 2, lambda sv: sv.solve(**kw))
     assert a[0][1]["alm_pobj"] == b[0][1]["alm_pobj"] and a[0][1]["alm_inner"] == b[0][1]["alm_inner"]
+
+
+def test_rccl_transport_world1(solver_mod):
+    """The RCCL transport's plumbing on one GPU (a communicator of one rank: all-reduces,
+    no halo peers); bench.py drives the same calls on N GPUs under torch.distributed.run."""
+    kw = dict(reoptLevel=0, skipADMM=1)
+    single = solver_mod.Solver(instance("mc_torus12x10"))
+    ref = single.solve(**kw)
+    single.close()
+    sv = solver_mod.Solver(instance("mc_torus12x10"))
+    sv.shard_rccl(1, 0, solver_mod.comm_unique_id())
+    assert sv.shard_info() == (1, 0, 0, 120, 0)
+    r = sv.solve(**kw)
+    out = sv.alm_throughput(0, 40, fixedRank=6, reoptLevel=0)
+    sv.close()
+    assert abs(r["alm_inner"] - ref["alm_inner"]) <= 2
+    assert abs(r["alm_pobj"] - ref["alm_pobj"]) <= 1e-6 * abs(ref["alm_pobj"])
+    assert out["done"] == 40
