@@ -149,6 +149,11 @@ struct lrs_ctx {
     hipEvent_t pev[2][5] = {};
     double pacc[4] = {0, 0, 0, 0};
     long pn = 0;
+    // MAX_ALM_SUB_ITER (lorads_alm.c:20): reset by the ALM phase, carried into reopt
+    int max_sub = 5000;
+    // objective scaling of reopt (objScale_dualvar): the unscaled C, restored per solve
+    double *Cw0 = nullptr, *Craw0 = nullptr;
+    bool c_scaled = false;
     // per-context scratch of the standalone reductions (bound to the calling thread)
     unsigned *s_tickets = nullptr;
     double *s_tmpfin = nullptr, *s_rpart = nullptr;
@@ -836,10 +841,11 @@ struct InnerIo {
     int exitReason;
 };
 
-static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, double gap, long budget, InnerIo &io) {
+static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, double gap, long budget, InnerIo &io,
+                     bool ph1_exit = true) {
     double par[P_NPAR] = {0};
     par[P_RHO] = rho; par[P_RCTOL] = rctol; par[P_ENDSUB] = p->endALMSubTol; par[P_ENDTAU] = p->endTauTol;
-    par[P_PH1TOL] = p->phase1Tol; par[P_BN1] = c->hp.bNrm1; par[P_BNINF] = c->hp.bNrmInf; par[P_CNINF] = c->hp.cNrmInf;
+    par[P_PH1TOL] = ph1_exit ? p->phase1Tol : -1.0; par[P_BN1] = c->hp.bNrm1; par[P_BNINF] = c->hp.bNrmInf; par[P_CNINF] = c->hp.cNrmInf;
     par[P_HIGHACC] = p->highAccMode; par[P_BUDGET] = (double)budget; par[P_L] = p->lbfgsListLength; par[P_GAP] = gap;
     double ctl[C_NCTRL] = {0};
     ctl[C_ACTIVE] = 1; ctl[C_EXIT] = EXIT_NONE; ctl[C_INNER] = (double)io.inner; ctl[C_LOCAL] = (double)io.local;
@@ -938,7 +944,7 @@ static int alm_optimize(lrs_ctx *c, const lrs_params *p, AlmState &st, double ts
 }
 static int alm_optimize_body(lrs_ctx *c, const lrs_params *p, AlmState &st, double tss) {
     const double ori = now_s();
-    int MAX_SUB = 5000;
+    c->max_sub = 5000;   // lorads_alm.c:1222
     int is_rank_max = check_all_rank_max(c, 1.0);
     int retcode = 0, last_outer_start = 1, sched_pos = 0;
     double rc, rc_tol, rc_val = 0, lag = 0;
@@ -970,12 +976,12 @@ ALG_START:
         double ema_cur = 0, ema_old = 0;
         int ema_cnt = 1;
         long cur_iter_counter = 1;
-        if (upd_cnt >= 2) { upd_cnt = 0; MAX_SUB = std::min(MAX_SUB + max_inc, max_ceil); }
+        if (upd_cnt >= 2) { upd_cnt = 0; c->max_sub = std::min(c->max_sub + max_inc, max_ceil); }
         while (difficulty != 'e') {
             localIter = 0;
             int if_break = update_check_ema(&ema_cur, &ema_old, rc_val, 0.1, 0.005, 5, &ema_cnt);
             if (!if_break && !p->highAccMode) break;
-            if (cur_iter_counter >= MAX_SUB) { upd_cnt += 1; break; }
+            if (cur_iter_counter >= c->max_sub) { upd_cnt += 1; break; }
             if (rank_flag >= thres && !is_rank_max && (k - last_outer_start >= 3)) break;
             if (rc_val <= rc_tol) break;
             // ---- inner L-BFGS loop on the device (lorads_alm.c:1302-1379)
@@ -1181,7 +1187,10 @@ static void admm_log(lrs_ctx *c, const lrs_params *p, const AdmmState &st, doubl
            c->t2o.empty() ? 0 : c->t2o.back(), t);
 }
 
-static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling, double tss) {
+// LORADSADMMOptimize (lorads_admm.c:84-209); reopt = LORADSADMMOptimize_reopt (:222-363):
+// CG tolerance 1e-4 pinf, bad-gap budget 200, exit on l_1 pinf only with the gap met,
+// rho schedule on iter instead of iter + 1.
+static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling, double tss, bool reopt = false) {
     if (st.gap <= p->phase2Tol && st.pinf1 <= p->phase2Tol) return 0;
     const int maxCG = 800;
     const double orig = now_s();
@@ -1204,8 +1213,11 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
     double cur_rho_max = p->rhoMax, old_mean = 1e30, buf[10] = {0};
     int bad_pd = 0, count = 0;
     while (st.iter <= p->maxADMMIter || st.gap >= p->phase2Tol || st.pinf1 >= p->phase2Tol) {
-        if (st.iter >= ceiling) break;
-        const double cgtol = std::min(st.pinf1 * 1e-2, 1e-8);
+        if (st.iter >= ceiling) {
+            if (reopt) record_state(c, p, 2);
+            break;
+        }
+        const double cgtol = std::min(st.pinf1 * (reopt ? 1e-4 : 1e-2), 1e-8);
         if (admm_update_var(c, st.rho, cgtol, maxCG)) return -1;
         st.cg_iter = c->cgIterTotal;
         if (cal_obj_admm(c)) return -1;
@@ -1220,19 +1232,20 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
         if (st.gap <= p->phase2Tol * 5) { bad_pd -= 5; bad_pd = std::max(0, bad_pd); }
         else if (st.gap <= p->phase2Tol) { bad_pd -= 10; bad_pd = std::max(0, bad_pd); }
         if (st.gap >= p->phase1Tol * 1e2) bad_pd += 2;
-        if (bad_pd >= 800) return 0;
+        if (bad_pd >= (reopt ? 200 : 800)) return 0;
         buf[count % 10] = st.pinfinf;
-        if (st.pinfinf <= p->phase2Tol) {
+        if ((reopt ? st.pinf1 : st.pinfinf) <= p->phase2Tol) {
             if (update_dimacs_admm(c)) return -1;
             st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.gap = c->dimGap; st.pinf1 = c->dimPinf;
-            return 0;
+            if (!reopt || st.gap <= p->phase2Tol) return 0;
         }
         OPC(launch_dual_update(c->dp, st.rho, c->W.lam, c->W.cvs, c->st));
-        if ((st.iter + 1) % p->rhoFreq == 0) {
+        const long rit = reopt ? st.iter : st.iter + 1;
+        if (rit % p->rhoFreq == 0) {
             st.rho *= p->rhoFactor;
             if (st.rho >= cur_rho_max) {
                 st.rho = cur_rho_max;
-                if ((st.iter + 1) % (p->rhoFreq * 100) == 0) {
+                if (rit % (p->rhoFreq * 100) == 0) {
                     double mean = 0;
                     for (double v : buf) mean += std::fabs(v);
                     mean /= 10.0;
@@ -1253,6 +1266,196 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
         if (st.gap <= p->phase2Tol * 1e-3 && st.pinf1 <= p->phase2Tol * 1e-3) return 0;
         st.iter++;
     }
+    return 0;
+}
+
+// ------------------------------------------------------------------------
+// reopt (reoptLevel >= 1): main.c:491-513 / :527-580, reopt() data/lorads_solver.c:1497-1539
+// ------------------------------------------------------------------------
+// LORADS_ALMOptimize_reopt (lorads_alm.c:959-1218) with early_stop = true, as reopt() calls it:
+// no phase-1 exit inside the inner loop, outer loop until maxALMIter (shifted by reopt) and
+// the phase-1 tolerances, difficulty without the "super" class, rank growth only with <= 10 cones.
+static int alm_optimize_reopt(lrs_ctx *c, lrs_params *p, AlmState &st, double rho_update_factor, double tss) {
+    const double ori = now_s();
+    int is_rank_max = check_all_rank_max(c, 1.0);
+    int retcode = 0, sched_pos = 0;
+    long last_outer_start = 1, k = 0, k0 = 0, localIter = 0, clearL = 0;
+    double rc = 0.1, rc_tol = 0, rc_val = 0, lag = 0;
+    char difficulty = 'h';
+    int rank_flag = 0, rho_factor_flag = 0, upd_cnt = 0;
+    const double rank_update_factor = p->rankUpdateFactor;
+    double thres = 15;
+    const int max_inc = 10000, max_ceil = 25000;
+ALG_START:
+    rc = 0.1;
+    rc_tol = rc / st.rho;
+    if (op_constr_xx(c, c->W.R, nullptr, nullptr, nullptr)) return -1;
+    if (op_grad(c, st.rho, &lag)) return -1;
+    rc_val = std::sqrt(lag) / (1 + c->hp.cNrmInf);
+    difficulty = 'h';
+    localIter = 0; clearL = 0; rank_flag = 0;
+    k = st.outerIter; k0 = st.outerIter;
+    rho_factor_flag = 0;
+    if (p->dyrankLevel == 0) thres = 1e8;
+    else if (p->dyrankLevel == 1) thres = 150;
+    else if (p->dyrankLevel == 2) thres = 15;
+    else if (p->dyrankLevel == 3) thres = 5;
+    upd_cnt = 0;
+    for (;;) {
+        if (k > p->maxALMIter && st.pinfinf <= p->phase1Tol &&
+            (st.gap <= std::max(p->phase1Tol, p->phase2Tol * 5) || !p->highAccMode))
+            break;
+        double ema_cur = 0, ema_old = 0;
+        int ema_cnt = 1;
+        long cur_iter_counter = 1;
+        if (upd_cnt >= 2) { upd_cnt = 0; c->max_sub = std::min(c->max_sub + max_inc, max_ceil); }
+        while (difficulty != 'e') {
+            localIter = 0;
+            int if_break = update_check_ema(&ema_cur, &ema_old, rc_val, 0.1, 0.005, 5, &ema_cnt);
+            if (!if_break && !p->highAccMode) break;
+            if (cur_iter_counter >= c->max_sub) { upd_cnt += 1; break; }
+            if (rank_flag >= thres && !is_rank_max && (k - last_outer_start >= 3)) break;
+            if (rc_val <= rc_tol) break;
+            InnerIo io;
+            io.inner = st.innerIter; io.local = localIter; io.clear = clearL; io.rcval = rc_val; io.lag = lag;
+            io.pinf1 = st.pinf1; io.pinfinf = st.pinfinf;
+            const long before = st.innerIter;
+            if (run_inner(c, p, st.rho, rc_tol, st.gap, p->almInnerBudget, io, false)) return -1;
+            st.innerIter = io.inner; localIter = io.local; clearL = io.clear;
+            cur_iter_counter += io.inner - before;
+            rc_val = io.rcval; lag = io.lag; st.pinf1 = io.pinf1; st.pinfinf = io.pinfinf;
+            if (io.exitReason == EXIT_NUMERR) { retcode = 4; goto END_ALM; }
+            if (io.exitReason == EXIT_BUDGET) goto PRINT_AND_EXIT;
+            if (io.exitReason == EXIT_TINYTAU) goto UpdateRho;
+            OPC(launch_dual_update(c->dp, st.rho, c->W.lam, c->W.cvs, c->st));
+            if (op_grad(c, st.rho, &lag)) return -1;
+            rc_val = std::sqrt(lag) / (1 + c->hp.cNrmInf);
+            if (localIter <= 20) difficulty = 'e';
+            else if (localIter <= 100) { difficulty = 'm'; rank_flag += 2; }
+            else { difficulty = 'h'; rank_flag += 3; }
+            if (difficulty == 'e') rank_flag = 0;
+        }
+    UpdateRho:
+        do {
+            st.rho *= rho_update_factor;
+            if (op_grad(c, st.rho, &lag)) return -1;
+            rc_val = std::sqrt(lag) / (1 + c->hp.cNrmInf);
+            rc_tol = rc / st.rho;
+        } while (rc_tol >= rc_val);
+        if (st.rho >= 5e4 && rho_factor_flag < 4) { rho_update_factor = std::sqrt(std::sqrt(rho_update_factor)); rho_factor_flag = 4; }
+        else if (st.rho >= 5e6 && rho_factor_flag < 6) { rho_update_factor = std::sqrt(std::sqrt(rho_update_factor)); rho_factor_flag = 6; }
+        else if (st.rho >= 5e8 && rho_factor_flag < 8) { rho_update_factor = std::sqrt(std::sqrt(rho_update_factor)); rho_factor_flag = 8; }
+        difficulty = 'h';
+        clearL = 0;
+        k += 1;
+        st.outerIter = k;
+        {
+            double pinf, obj;
+            if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj)) return -1;
+            c->pObjVal = obj / c->scaleObjHis;
+            cal_dual_obj(c);
+            c->dimPinf = pinf;
+            c->dimGap = std::fabs(c->pObjVal - c->dObjVal) / (1 + std::fabs(c->pObjVal) + std::fabs(c->dObjVal));
+            st.gap = c->dimGap; st.pobj = c->pObjVal; st.dobj = c->dObjVal;
+            st.pinf1 = c->dimPinf;
+            st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+            if (st.pinf1 <= p->phase1Tol && st.gap <= std::max(p->phase1Tol, p->phase2Tol * 5) && (k - k0) > 1)
+                goto PRINT_AND_EXIT;
+            record_state(c, p, 1);
+            alm_log(c, p, st, now_s() - ori);
+            if (now_s() - tss >= p->timeSecLimit) goto PRINT_AND_EXIT;
+        }
+        if (rank_flag >= thres && !is_rank_max && c->dp.K <= 10) {
+            rank_flag = 0;
+            if (k - last_outer_start >= 2) {
+                if (aug_rank(c, rank_update_factor, p, &sched_pos, &is_rank_max)) return -1;
+                st.outerIter = k;
+                last_outer_start = st.outerIter;
+                goto ALG_START;
+            }
+        }
+    }
+END_ALM: {
+        double pinf, obj;
+        if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj)) return -1;
+        c->pObjVal = obj / c->scaleObjHis;
+        cal_dual_obj(c);
+        c->dimPinf = pinf;
+        c->dimGap = std::fabs(c->pObjVal - c->dObjVal) / (1 + std::fabs(c->pObjVal) + std::fabs(c->dObjVal));
+        st.gap = c->dimGap;
+        // lorads_alm.c:1208 derives l_1 back from the last l_inf
+        st.pinf1 = st.pinfinf * (1 + c->hp.bNrmInf) / (1 + c->hp.bNrm1);
+    }
+PRINT_AND_EXIT:
+    logf_(c, p, "-----------------------------------------------------------------------\nExit ALM:\n");
+    record_state(c, p, 1);
+    alm_log(c, p, st, now_s() - ori);
+    return retcode;
+}
+
+// objScale_dualvar (data/lorads_solver.c:1438-1450): C *= f, lambda *= f, scaleObjHis *= f
+static int obj_scale(lrs_ctx *c, double f) {
+    DevProblem &P = c->dp;
+    const long Pt = std::max(1, P.Ptot);
+    if (!c->c_scaled) {
+        if (!c->Cw0) {
+            HIPC(hipMalloc((void **)&c->Cw0, sizeof(double) * Pt));
+            HIPC(hipMalloc((void **)&c->Craw0, sizeof(double) * Pt));
+        }
+        HIPC(hipMemcpyAsync(c->Cw0, P.Cw, sizeof(double) * Pt, hipMemcpyDeviceToDevice, c->st));
+        HIPC(hipMemcpyAsync(c->Craw0, P.Craw, sizeof(double) * Pt, hipMemcpyDeviceToDevice, c->st));
+        c->c_scaled = true;
+    }
+    c->scaleObjHis *= f;
+    OPC(launch_axpby(Pt, 0.0, P.Cw, f, P.Cw, c->st));
+    OPC(launch_axpby(Pt, 0.0, P.Craw, f, P.Craw, c->st));
+    OPC(launch_axpby(P.m, 0.0, c->W.lam, f, c->W.lam, c->st));
+    return 0;
+}
+static int obj_unscale(lrs_ctx *c) {
+    if (!c->c_scaled) return 0;
+    DevProblem &P = c->dp;
+    const long Pt = std::max(1, P.Ptot);
+    HIPC(hipMemcpyAsync(P.Cw, c->Cw0, sizeof(double) * Pt, hipMemcpyDeviceToDevice, c->st));
+    HIPC(hipMemcpyAsync(P.Craw, c->Craw0, sizeof(double) * Pt, hipMemcpyDeviceToDevice, c->st));
+    HIPC(hipStreamSynchronize(c->st));
+    c->c_scaled = false;
+    return 0;
+}
+
+// LORADS_ALMtoADMM (data/lorads_solver.c:1351-1387)
+static int alm_to_admm(lrs_ctx *c, lrs_params *p, const AlmState &alm, AdmmState &admm) {
+    HIPC(hipMemcpyAsync(c->W.V, c->W.R, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
+    HIPC(hipMemcpyAsync(c->W.U, c->W.V, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
+    admm.pinf1 = alm.pinf1; admm.pinfinf = alm.pinfinf; admm.gap = alm.gap;
+    admm.rho = alm.rho * p->heuristicFactor;
+    if (alm.rho > p->rhoMax) {
+        admm.rho = std::min(std::sqrt(std::max(p->rhoMax, alm.rho) / p->rhoMax) * p->rhoMax, alm.rho);
+        p->rhoMax = admm.rho;
+    }
+    return 0;
+}
+
+// reopt() (data/lorads_solver.c:1497-1539)
+static int reopt(lrs_ctx *c, lrs_params *p, AlmState &alm, AdmmState &admm, double reopt_param, long alm_iter,
+                 long admm_iter, double tss, int *bad, int level) {
+    const long old_maxALM = p->maxALMIter, old_maxADMM = p->maxADMMIter;
+    const double old_rhoMax = p->rhoMax;
+    p->maxALMIter = alm_iter - 1 + alm.outerIter;
+    p->maxADMMIter = admm_iter;
+    if (obj_scale(c, reopt_param)) return -1;
+    if (admm.rho <= p->rhoMax) alm.rho = std::max(admm.rho, alm.rho);
+    if (alm_optimize_reopt(c, p, alm, std::sqrt(p->ALMRhoFactor), tss) < 0) return -1;
+    p->rhoMax = std::max(std::sqrt(std::max(admm.rho, alm.rho) / admm.rho) * admm.rho, p->rhoMax);
+    if (alm_to_admm(c, p, alm, admm)) return -1;
+    if (*bad == 0 || level < 2) {
+        const int rc = admm_optimize(c, p, admm, std::min(admm.iter * 4, admm.iter + old_maxADMM), tss, true);
+        if (rc < 0) return -1;
+        *bad = 0;   // LORADSADMMOptimize_reopt never returns RET_CODE_BAD_ITER
+    }
+    p->maxALMIter = old_maxALM;
+    p->maxADMMIter = old_maxADMM;
+    p->rhoMax = old_rhoMax;
     return 0;
 }
 
@@ -1314,7 +1517,7 @@ void lrs_ctx_destroy(lrs_ctx *c) {
     if (c->hpin) (void)hipHostFree(c->hpin);
     delete c->comm;
     for (void *q : {(void *)c->s_tickets, (void *)c->s_tmpfin, (void *)c->s_rpart, (void *)c->d_send_rows,
-                    (void *)c->d_sendbuf})
+                    (void *)c->d_sendbuf, (void *)c->Cw0, (void *)c->Craw0})
         if (q) (void)hipFree(q);
     bind_scratch(nullptr, nullptr, nullptr);
     if (c->st) (void)hipStreamDestroy(c->st);
@@ -1605,6 +1808,7 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     if (sharded(c)) p->skipADMM = 1;       // the sharded solve covers the ALM phase
     memset(res, 0, sizeof(*res));
     const double tss = now_s();
+    if (obj_unscale(c)) return -1;   // a previous solve's reopt scaled C on the device
     std::vector<int> r, rm;
     determine_rank(c, p, r, rm);
     if (alloc_work(c, r)) return -1;
@@ -1634,19 +1838,47 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     bool timeout = now_s() - tss > p->timeSecLimit;
     double t_admm = 0;
     if (!timeout && !p->skipADMM) {
-        // LORADS_ALMtoADMM (data/lorads_solver.c:1351-1387)
-        HIPC(hipMemcpyAsync(c->W.V, c->W.R, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
-        HIPC(hipMemcpyAsync(c->W.U, c->W.V, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
-        admm.pinf1 = alm.pinf1; admm.pinfinf = alm.pinfinf; admm.gap = alm.gap;
-        admm.rho = alm.rho * p->heuristicFactor;
-        if (alm.rho > p->rhoMax) {
-            admm.rho = std::min(std::sqrt(std::max(p->rhoMax, alm.rho) / p->rhoMax) * p->rhoMax, alm.rho);
-            p->rhoMax = admm.rho;
-        }
+        if (alm_to_admm(c, p, alm, admm)) return -1;
         const double ta = now_s();
         int arc = admm_optimize(c, p, admm, p->maxADMMIter, tss);
         if (arc < 0) return -1;
         t_admm = now_s() - ta;
+        // reoptLevel >= 1 (main.c:491-513): one reopt round while neither phase met phase2Tol
+        const double reopt_param = 5;
+        const long alm_min = 3, admm_min = p->highAccMode ? 1000 : 50;   // main.c:436-443
+        int bad = 0, cnt = 0;
+        if (p->reoptLevel >= 1) {
+            while ((alm.gap > p->phase2Tol || alm.pinf1 > p->phase2Tol) &&
+                   (admm.gap > p->phase2Tol || admm.pinf1 > p->phase2Tol)) {
+                if (cnt >= 1) break;
+                if (reopt(c, p, alm, admm, reopt_param, alm_min, admm_min, tss, &bad, 1)) return -1;
+                cnt++;
+                if (now_s() - tss > p->timeSecLimit) { timeout = true; break; }
+            }
+        }
+        // reoptLevel >= 2 (main.c:527-580): up to two more rounds, each followed by the
+        // U/V average; the dual infeasibility that also drives this loop in the reference
+        // (ARPACK, main.c:515) is not computed here and enters as 0
+        if (p->reoptLevel >= 2 && !timeout) {
+            int dual_cnt = 0;
+            while (admm.gap > p->phase2Tol || admm.pinf1 > p->phase2Tol) {
+                if (dual_cnt >= 2) break;
+                if (!p->highAccMode && admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol) break;
+                if (reopt(c, p, alm, admm, reopt_param, 3, 50, tss, &bad, 2)) return -1;
+                OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
+                HIPC(hipMemcpyAsync(c->W.V, c->W.R, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
+                admm.gap = c->dimGap;
+                admm.pinf1 = c->dimPinf;
+                admm.pinfinf = c->dimPinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+                dual_cnt++;
+                if (now_s() - tss > p->timeSecLimit) { timeout = true; break; }
+            }
+        }
+        t_admm = now_s() - ta;
+        // the ALM state after the reopt rounds (alm_inner / alm_time stay the first phase's)
+        res->alm_outer = alm.outerIter;
+        res->alm_pobj = alm.pobj; res->alm_dobj = alm.dobj; res->alm_pinf = alm.pinf1; res->alm_gap = alm.gap;
+        res->alm_rho = alm.rho;
     }
     HIPC(hipStreamSynchronize(c->st));
     const double all_time = now_s() - t0;

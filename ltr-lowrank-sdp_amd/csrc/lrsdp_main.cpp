@@ -131,10 +131,10 @@ int main(int argc, char **argv) {
         fprintf(stderr, "[lrsdp] lbfgsListLength %d not supported on the device path; using 2\n", p.lbfgsListLength);
         p.lbfgsListLength = 2;
     }
-    if (p.reoptLevel >= 1) {
-        fprintf(stderr, "[lrsdp] reoptLevel %d: reoptimisation restarts are not on the device path yet; "
-                        "running reoptLevel 0 (DESIGN.md section 7)\n", p.reoptLevel);
-    }
+    if (p.reoptLevel >= 2)
+        fprintf(stderr, "[lrsdp] reoptLevel %d: the dual infeasibility (ARPACK in the reference) is not computed; "
+                        "its reopt rounds are driven by the gap and primal infeasibility (DESIGN.md section 7)\n",
+                p.reoptLevel);
     printf("-----------------------------------------------------------\n");
     printf("  LoRADS-compatible low-rank SDP solver on MI355X (%s)\n", lrs_version());
     printf("-----------------------------------------------------------\n");
