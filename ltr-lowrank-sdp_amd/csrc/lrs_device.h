@@ -124,6 +124,9 @@ struct DevProblem {
     int *loc_ptr = nullptr, *loc_con = nullptr;              // [Ptot+1], [m - mg]
     double *loc_w = nullptr;                                 // (2 - delta) a of that one entry
     int *slot_rc = nullptr;                                  // [Ptot][2] (row, col) in the cone
+    double *slot1 = nullptr;                                 // [Ptot][2] {a, con} of a slot's single
+                                                             //   constraint entry (con -1 none, -2 several)
+    double *loc1 = nullptr;                                  // [Ptot][2] {w, con} of its single local constraint
     int *con1_pq = nullptr;                                  // [K*m][2] single-entry rows: (p, q); -1 other; -2 long
     int *long_rows = nullptr;                                // constraints with > kLongRow entries in a cone,
     std::vector<int> long_ptr_h;                             //   grouped by cone: long_ptr_h[k]..[k+1]
@@ -206,6 +209,7 @@ struct AlmIterArgs {
 int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st);
 // whether stage A is split into direction + SDDMM launches (bandwidth regime)
 bool alm_stage_a_split(const DevProblem &P);
+bool alm_stage_b_split(const DevProblem &P);   // stage B likewise (line search + update, gradient)
 // a subset of the stages (mask bit 0 = A, 1 = G, 2 = B), for per-stage timing
 int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t st);
 

@@ -1124,7 +1124,8 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
     const double *__restrict__ G0, const double *__restrict__ G1, const double *__restrict__ s0a,
     const double *__restrict__ y0a, const double *__restrict__ s1a, const double *__restrict__ y1a,
     double *__restrict__ uRD, double *__restrict__ uDD, const int *__restrict__ loc_ptr,
-    const int *__restrict__ loc_con, const double *__restrict__ loc_w, const double *__restrict__ b,
+    const int *__restrict__ loc_con, const double *__restrict__ loc_w, const double2 *__restrict__ loc1,
+    const double *__restrict__ b,
     double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec, int do_glob, int mg,
     const int *__restrict__ glob, int m, int K, const int *__restrict__ con_ptr, const int *__restrict__ con_slot,
     const double *__restrict__ con_w, const double *__restrict__ uRR, const double *__restrict__ par,
@@ -1279,10 +1280,14 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
                         acc[0] += cw[u] * d0;
                         acc[1] += cw[u] * d1;
                         // local constraints on this slot: q1 = 2 A(sym RD^T), q2 = A(DD^T)
-                        // (ALMCalq12p12 lorads_alm.c:714-734) and the line-search dots (:269-277)
-                        for (int e = loc_ptr[sl]; e < loc_ptr[sl + 1]; ++e) {
-                            const int ci = loc_con[e];
-                            const double w = loc_w[e];
+                        // (ALMCalq12p12 lorads_alm.c:714-734) and the line-search dots (:269-277);
+                        // a single one comes with the slot's record, several from the lists
+                        const double2 l1u = loc1[sl];
+                        const int c1 = (int)l1u.y;
+                        const int e0 = c1 == -2 ? loc_ptr[sl] : 0, e1 = c1 == -2 ? loc_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
+                        for (int e = e0; e < e1; ++e) {
+                            const int ci = c1 >= 0 ? c1 : loc_con[e];
+                            const double w = c1 >= 0 ? l1u.x : loc_w[e];
                             const double q1 = 2.0 * (w * d0), q2 = w * d1;
                             const double bi = b[ci], cv = cvs[ci], li = lam[ci];
                             const double q0 = (bi - cv) + rhoInv * li;
@@ -1385,14 +1390,19 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
 // :38-57), G_new = 2 S R_new, A(R_new R_new^T) on the lower slots with the local
 // constraints' values and residual (primalInfeasibility), the L-BFGS pair s = tau D,
 // y = G_new - G_old (setlbfgsHisTwo :842-863) and nine dots.  Partials written (10).
-template <int G, int E, int U>
-__global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
+// MODE 0: the whole stage.  Bandwidth regime, split in two launches: MODE 1 = line search
+// + R_new = R + tau D of every row (own and halo), MODE 2 = the rest with the neighbours'
+// R_new read back (one row per neighbour instead of R and D) and tau from MODE 1.
+template <int G, int E, int U, int MODE>
+__global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_it_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
     const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0, double *s1, double *y1,
     double *__restrict__ uRR, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
-    const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double *__restrict__ rec,
+    const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double2 *__restrict__ slot1,
+    const double *__restrict__ rec,
     const int *__restrict__ loc_ptr, const int *__restrict__ loc_con, const double *__restrict__ loc_w,
+    const double2 *__restrict__ loc1,
     const double *__restrict__ b, double *__restrict__ cvs, const double *__restrict__ par,
     const double *__restrict__ ctrl, const double *__restrict__ partA, int nblkA, const double *__restrict__ partB,
     int nblkB, double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int T, int row0,
@@ -1406,6 +1416,11 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     if (threadIdx.x == 0) { cs[0] = ctrl[C_ACT2]; cs[1] = ctrl[C_GCUR]; cs[2] = ctrl[C_HEAD]; cs[3] = ctrl[C_RCUR]; }
     __syncthreads();
     if (cs[0] == 0.0) return;
+    if constexpr (MODE == 2) {
+        // second half of a split stage: the line search the first half wrote
+        if (threadIdx.x < LS_N) ls[threadIdx.x] = ls_cur[threadIdx.x];
+        __syncthreads();
+    } else {
     reduce_partials<7, kRowBlock>(partA, nblkA, red, pstr);
     if (nblkB > 0) {
         reduce_partials<5, kRowBlock>(partB, nblkB, red + 7);
@@ -1420,6 +1435,7 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     __syncthreads();
     LRS_TS(2, 2);
     if (pblk_off == 0 && blockIdx.x == 0 && threadIdx.x < LS_N) ls_cur[threadIdx.x] = ls[threadIdx.x];
+    }   // MODE != 2
     if (ls[LS_FLAG] != 0.0) return;
     const double tau = ls[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
     const int gcur = (int)cs[1], h = (int)cs[2];
@@ -1433,6 +1449,22 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
     const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
     const bool two = (L == 2);
+    if constexpr (MODE == 1) {
+        // R_new = R + tau D for every local row (the shard's halo included)
+        const int lane1 = threadIdx.x & (G - 1);
+        const int grp1 = (blockIdx.x * kRowBlock + threadIdx.x) / G;
+        const int ngrp1 = gridDim.x * kRowBlock / G;
+        for (int l = grp1; l < nall; l += ngrp1) {
+            const long ol = (long)l * ld + lane1 * E;
+            double rv[E], dv[E];
+            ld_row<E>(R + ol, rv);
+            ld_row<E>(D + ol, dv);
+#pragma unroll
+            for (int e = 0; e < E; ++e) rv[e] += tau * dv[e];
+            st_row<E>(Rn + ol, rv);
+        }
+        return;
+    }
     // lane groups of G lanes; a team of T groups shares one row (dense rows): member m
     // takes interleaved chunks of U neighbours, the partial gradients meet in LDS.  The
     // row loop runs the same trip count in every team of a block (barriers inside).
@@ -1452,11 +1484,15 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
 #pragma unroll
     for (int e = 0; e < E; ++e) g[e] = 0.0;
     if (valid) {
-        ld_row<E>(R + oi, ri);
-        ld_row<E>(D + oi, di);
+        if constexpr (MODE == 2) {
+            ld_row<E>(Rn + oi, ri);   // D of the row is read at the end (s = tau D): fewer live registers
+        } else {
+            ld_row<E>(D + oi, di);
+            ld_row<E>(R + oi, ri);
 #pragma unroll
-        for (int e = 0; e < E; ++e) ri[e] += tau * di[e];
-        if (mem == 0) st_row<E>(Rn + oi, ri);
+            for (int e = 0; e < E; ++e) ri[e] += tau * di[e];
+            if (mem == 0) st_row<E>(Rn + oi, ri);
+        }
         const int kb = adj_ptr[i], kl = adj_low[i], ke = adj_ptr[i + 1];
 #ifdef LRS_PHASE_TIMING
         if (threadIdx.x == 0 && ib == blockIdx.x * tpb && kb >= 0 && ri[0] != 12345.678) LRS_TS(2, 6);
@@ -1471,28 +1507,38 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
                 ss[u] = adj_slot[k];
             }
             double rj[U][E], dj[U][E], sv[U];
-            int eb[U], ee[U];
+            double2 s1[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                ld_row<E>(R + (long)jj[u] * ld + lane * E, rj[u]);
-                ld_row<E>(D + (long)jj[u] * ld + lane * E, dj[u]);
+                if constexpr (MODE == 2) {
+                    ld_row<E>(Rn + (long)jj[u] * ld + lane * E, rj[u]);
+                } else {
+                    ld_row<E>(R + (long)jj[u] * ld + lane * E, rj[u]);
+                    ld_row<E>(D + (long)jj[u] * ld + lane * E, dj[u]);
+                }
                 sv[u] = Craw[ss[u]];
-                eb[u] = slot_ptr[ss[u]];
-                ee[u] = slot_ptr[ss[u] + 1];
+                s1[u] = slot1[ss[u]];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                // S[slot] = C + sum_con M1(con) a  (addObjCoeff + sdpDataWSum)
-                for (int e = eb[u]; e < ee[u]; ++e) {
-                    const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
+                // S[slot] = C + sum_con M1(con) a  (addObjCoeff + sdpDataWSum); a single entry
+                // comes with the slot's record, several from the slot lists
+                const int c1 = (int)s1[u].y;
+                const int e0 = c1 == -2 ? slot_ptr[ss[u]] : 0;
+                const int e1 = c1 == -2 ? slot_ptr[ss[u] + 1] : (c1 >= 0 ? 1 : 0);
+                for (int e = e0; e < e1; ++e) {
+                    const int con = c1 >= 0 ? c1 : slot_con[e];
+                    const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * con);
                     const double2 ra = r[0], rb = r[1];
                     double cv = ra.x + tau * ra.y;
                     cv = cv + tau2 * rb.x;
                     const double M1 = rb.y + rho * cv;
-                    sv[u] += M1 * slot_a[e];
+                    sv[u] += M1 * (c1 >= 0 ? s1[u].x : slot_a[e]);
                 }
+                if constexpr (MODE != 2) {
 #pragma unroll
-                for (int e = 0; e < E; ++e) rj[u][e] += tau * dj[u][e];
+                    for (int e = 0; e < E; ++e) rj[u][e] += tau * dj[u][e];
+                }
             }
 #ifdef LRS_PHASE_TIMING
             if (threadIdx.x == 0 && ib == blockIdx.x * tpb && rj[0][0] != 12345.678 && sv[0] != 12345.678)
@@ -1512,9 +1558,13 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
                     d = group_sum<G>(d);
                     if (lane == 0) {
                         uRR[ss[u]] = d;
-                        for (int e = loc_ptr[ss[u]]; e < loc_ptr[ss[u] + 1]; ++e) {
-                            const int ci = loc_con[e];
-                            const double tot = loc_w[e] * d;
+                        const double2 l1u = loc1[ss[u]];
+                        const int c1 = (int)l1u.y;
+                        const int e0 = c1 == -2 ? loc_ptr[ss[u]] : 0;
+                        const int e1 = c1 == -2 ? loc_ptr[ss[u] + 1] : (c1 >= 0 ? 1 : 0);
+                        for (int e = e0; e < e1; ++e) {
+                            const int ci = c1 >= 0 ? c1 : loc_con[e];
+                            const double tot = (c1 >= 0 ? l1u.x : loc_w[e]) * d;
                             cvs[ci] = tot;
                             const double dd = b[ci] - tot;
                             acc[9] += dd * dd;
@@ -1544,6 +1594,7 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     }
     if (mem == 0 && valid) {
         double sv[E], yv[E], go[E];
+        if constexpr (MODE == 2) ld_row<E>(D + oi, di);
         ld_row<E>(Gold + oi, go);
 #pragma unroll
         for (int e = 0; e < E; ++e) g[e] *= 2.0;
@@ -1579,7 +1630,7 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? 6 : 1)) k_it_b(
     }   // rows
     // sharded solve: the halo rows (the other shards' rows this one reads) take the same
     // update R_new = R + tau D, D of the halo received after stage A's first half
-    if (nall > n) {
+    if (MODE == 0 && nall > n) {
         for (int q = grp; q < nall - n; q += ngrp) {
             const int l = q < row0 ? q : q + n;
             const long ol = (long)l * ld + lane * E;
@@ -2054,7 +2105,7 @@ static int res_a() {
 template <int GG, int EE, int UU>
 static int res_b() {
     static int c = 0;
-    return resident_blocks(k_it_b<GG, EE, UU>, &c);
+    return resident_blocks(k_it_b<GG, EE, UU, (UU == 1 ? 2 : 0)>, &c);
 }
 
 struct StagePlan {
@@ -2113,6 +2164,16 @@ bool alm_stage_a_split(const DevProblem &P) {
         StagePlan pa;
         if (plan_a(P.cones[k], P.K, pa)) return false;
         if (!pa.small) return true;
+    }
+    return false;
+}
+
+// Whether stage B runs as two launches (bandwidth regime).
+bool alm_stage_b_split(const DevProblem &P) {
+    for (int k = 0; k < P.K; ++k) {
+        StagePlan pb;
+        if (plan_b(P.cones[k], P.K, pb)) return false;
+        if (!pb.small) return true;
     }
     return false;
 }
@@ -2191,7 +2252,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
 #define LRS_LAUNCH_A(UU, MM)                                                                               \
     hipLaunchKernelGGL((k_it_a<GG, EE, UU, MM>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,     \
                        c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], \
-                       W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, P.b, W.cvs,    \
+                       W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,                \
+                       reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs,                                     \
                        W.lam, W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,      \
                        W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, pa[k].T, gwide, c.row0, \
                        pstr)
@@ -2234,21 +2296,32 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     for (int k = 0; k < KL && (mask & 4); ++k) {
         const DevCone &c = cone_of(k);
         const int grid = pb[k].grid;
-#define LRS_LAUNCH_B(UU)                                                                                   \
-    hipLaunchKernelGGL((k_it_b<GG, EE, UU>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff, c.adj_ptr, \
+#define LRS_LAUNCH_B(UU, MM)                                                                               \
+    hipLaunchKernelGGL((k_it_b<GG, EE, UU, MM>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff, c.adj_ptr, \
                        c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],        \
-                       W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a, W.rec, P.loc_ptr,       \
-                       P.loc_con, P.loc_w, P.b, W.cvs, W.par, ctrl_cur, inA, nA, W.partB,                          \
+                       W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,                        \
+                       reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,           \
+                       reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, inA, nA, W.partB,   \
                        P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, c.n, pstr)
         const bool small = pb[k].small;
         LRS_LAYOUT_SWITCH(c.G, c.E, {
-            if (small) LRS_LAUNCH_B(4);
-            else LRS_LAUNCH_B(1);
+            if (small) LRS_LAUNCH_B(4, 0);
+            else LRS_LAUNCH_B(1, 1);
         });
-#undef LRS_LAUNCH_B
         LRS_CHECK_LAUNCH();
         off += grid;
     }
+    // bandwidth regime: the gradient half over the updated factor
+    off = 0;
+    for (int k = 0; k < KL && (mask & 4); ++k) {
+        const DevCone &c = cone_of(k);
+        const int grid = pb[k].grid;
+        if (pb[k].small) { off += grid; continue; }
+        LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_B(1, 2); });
+        LRS_CHECK_LAUNCH();
+        off += grid;
+    }
+#undef LRS_LAUNCH_B
     if (sh && (mask & 4)) {
         hipLaunchKernelGGL(k_fold_partials<10>, dim3(1), dim3(kBlock), 0, st, W.partC, nblkB, totC);
         LRS_CHECK_LAUNCH();

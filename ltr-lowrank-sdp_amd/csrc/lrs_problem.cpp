@@ -482,6 +482,21 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 loc_w[t] = only_w[i];
             }
     }
+    // per slot, its single constraint entry / single local constraint as one 16-byte record
+    // {a or w, con} (con = -1: none, -2: several -> the lists): one dependent load less per
+    // neighbour in the row kernels (slot -> record -> rec[con] instead of slot -> ptr -> con -> rec)
+    {
+        std::vector<double> s1(2L * std::max(1, Ptot), 0.0), l1(2L * std::max(1, Ptot), 0.0);
+        for (int t = 0; t < Ptot; ++t) {
+            const int ns = slot_ptr[t + 1] - slot_ptr[t];
+            s1[2L * t] = ns == 1 ? slot_a[slot_ptr[t]] : 0.0;
+            s1[2L * t + 1] = ns == 0 ? -1.0 : (ns == 1 ? (double)slot_con[slot_ptr[t]] : -2.0);
+            const int nl = loc_ptr[t + 1] - loc_ptr[t];
+            l1[2L * t] = nl == 1 ? loc_w[loc_ptr[t]] : 0.0;
+            l1[2L * t + 1] = nl == 0 ? -1.0 : (nl == 1 ? (double)loc_con[loc_ptr[t]] : -2.0);
+        }
+        if (!dput(&dp.slot1, s1, err) || !dput(&dp.loc1, l1, err)) return false;
+    }
     dp.mg = (int)glob.size();
     dp.glob_maxlen = 0;
     for (int i : glob) dp.glob_maxlen = std::max(dp.glob_maxlen, nent[i]);
@@ -544,7 +559,7 @@ void free_problem(DevProblem &dp) {
     auto f = [](void *p) { if (p) (void)hipFree(p); };
     f(dp.b); f(dp.Cw); f(dp.Craw); f(dp.con_ptr); f(dp.con_slot); f(dp.con_w);
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
-    f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
+    f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); }
     if (dp.has_merged) { f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot); }
     dp = DevProblem();

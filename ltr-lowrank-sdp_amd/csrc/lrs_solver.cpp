@@ -1600,7 +1600,8 @@ int lrs_stage_bytes(lrs_ctx *c, double *bytes) {
         // split stage A (bandwidth regime): D is written by the first launch and read back
         a += (alm_stage_a_split(c->dp) ? 8 : 7) * nr8 + 8 * (n + 1) + 8 * Pk /*lower adj col+slot*/ + 8 * Pk /*Cw*/ +
              16 * Pk /*uRD,uDD*/ + 4 * (Pk + 1);
-        bb += 9 * nr8 + 8 * (n + 1) + 8 * A /*adj col+slot*/ + 8 * Pk /*Craw*/ + 4 * (Pk + 1) /*slot_ptr*/ +
+        // split stage B: R_new is written by the first launch and read back by the second
+        bb += (alm_stage_b_split(c->dp) ? 11 : 9) * nr8 + 8 * (n + 1) + 8 * A /*adj col+slot*/ + 8 * Pk /*Craw*/ + 4 * (Pk + 1) /*slot_ptr*/ +
               8 * Pk /*uRR*/ + 4 * (Pk + 1) /*loc_ptr*/;
     }
     const double m = P.m, ml = P.m - P.mg, Z = (double)P.Z;
