@@ -126,6 +126,15 @@ int lrs_alm_throughput(lrs_ctx *ctx, const lrs_params *p, long warmup, long step
 /* Mirror the iteration log into a file (the reference's --logfile). */
 int lrs_set_log_path(lrs_ctx *ctx, const char *path);
 
+/* Kernel selection of the ALM inner iteration (same arithmetic either way):
+ * 0 = automatic (the latency-regime kernels k_lat_a/k_lat_b when every row's lane group is
+ * resident at once, else the general row kernels), 1 = general row kernels only.
+ * The environment variable LRS_NO_LAT=1 forces 1 for every context. */
+int lrs_set_kernel_path(lrs_ctx *ctx, int path);
+/* The path the last enqueued ALM inner iteration of this context took (0 latency-regime
+ * kernels, 1 general row kernels; -1 none enqueued yet). */
+int lrs_get_kernel_path(lrs_ctx *ctx, int *used);
+
 /* Standalone A(UU^T) on R (the constraint-entry kernel k_auv_con, all cones): reps
  * launches back to back between two HIP events, average ms per launch; and its
  * algorithmic bytes (factor rows touched once + entry data + outputs). */

@@ -92,6 +92,8 @@ struct DevCone {
     int slot_off = 0, P = 0;
     int *adj_ptr = nullptr, *adj_low = nullptr, *adj_col = nullptr, *adj_slot = nullptr;
     long adj_nnz = 0;
+    // most adjacency entries of one row (all, and lower incl. the diagonal); 0 = unknown
+    int maxdeg = 0, maxlow = 0;
 };
 
 // Sharded solve (one process per GPU, rows of the cone split into contiguous blocks):
@@ -107,6 +109,8 @@ struct ShardHooks {
 
 struct DevProblem {
     const ShardHooks *shard = nullptr;   // non-null in a sharded solve
+    int no_lat = 0;                      // 1: never the latency-regime iteration kernels
+    mutable int last_path = -1;          // path of the last enqueued iteration (0 lat, 1 general)
     int m = 0, K = 0;
     long NRpad = 0;     // factor buffer length (doubles)
     int Ptot = 0;

@@ -957,7 +957,7 @@ __device__ void line_search_t(const double *__restrict__ par, double p1, double 
     if (fabs(mn - fr1) < 1e-10) tau = roots[0];
     if (fabs(mn - fr2) < 1e-10) tau = roots[1];
     if (fabs(mn - fr3) < 1e-10) tau = roots[2];
-    if (!WAVE || threadIdx.x == 0) {
+    if (!WAVE || (threadIdx.x & 63) == 0) {
         ls[LS_TAU] = tau;
         ls[LS_ROOTNUM] = rn;
         ls[LS_FLAG] = rn == 0 ? 1.0 : (fabs(tau) < par[P_ENDTAU] ? 2.0 : 0.0);
@@ -1653,6 +1653,514 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_
 }
 
 // ------------------------------------------------------------------------
+// Latency regime (small n: every row's lane group resident at once).  Same work and
+// arithmetic as k_it_a<.,.,.,0> / k_it_b<.,.,.,0>, restructured around the critical path
+// of one launch: the last wave of each block is a CONTROL wave (the cross-block reduction
+// of the previous stage's partials, then ctrl_step, resp. the line search); the other
+// seven are ROW waves, one row per lane group.  Every load that does not depend on this
+// iteration's control -- the row header, the first NB adjacency entries, the own row
+// operands, the slot and constraint records -- is issued by the row waves before the
+// block barrier, so its latency runs beside the reduction and the serial control instead
+// of after them.  Only the neighbours' factor rows (U at a time) are loaded afterwards.
+// ------------------------------------------------------------------------
+constexpr int kLatRowWaves = kRowBlock / 64 - 1;
+constexpr int kLatRows = kLatRowWaves * 64;      // row-wave threads per block
+constexpr int kLatMaxPartials = 256;             // producer blocks one control wave reduces
+
+// control wave: NV partial vectors summed over 1 <= nblk <= kLatMaxPartials producer blocks
+// (lane l takes blocks l, l+64, ...).  Every load is issued before the first sum (loads
+// clamped, not branched), so the wave waits for one memory trip; wave-uniform result.
+template <int NV>
+__device__ __forceinline__ void wave_reduce_partials(const double *__restrict__ part, int nblk, double (&out)[NV]) {
+    constexpr int Q = kLatMaxPartials / 64;
+    const int lane = threadIdx.x & 63;
+    double x[Q][NV];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int bc = min(lane + 64 * q, nblk - 1);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) x[q][v] = part[v * kMaxPartialBlocks + bc];
+    }
+#ifndef LRS_LAT_SERIAL_RED
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        double a = 0.0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) a += (lane + 64 * q < nblk) ? x[q][v] : 0.0;
+        out[v] = wave_sum(a);
+    }
+}
+
+// A in the latency regime (k_it_a MODE 0).  NB: lower entries prefetched per row;
+// U: neighbour rows loaded at a time.
+template <int G, int E, int NB, int U>
+__global__ void __launch_bounds__(kRowBlock) k_lat_a(
+    int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
+    const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
+    const double *__restrict__ Rb0, const double *__restrict__ Rb1, double *__restrict__ Dall,
+    const double *__restrict__ G0, const double *__restrict__ G1, const double *__restrict__ s0a,
+    const double *__restrict__ y0a, const double *__restrict__ s1a, const double *__restrict__ y1a,
+    double *__restrict__ uRD, double *__restrict__ uDD, const int *__restrict__ loc_ptr,
+    const int *__restrict__ loc_con, const double *__restrict__ loc_w, const double2 *__restrict__ loc1,
+    const double *__restrict__ b, double *__restrict__ cvs, const double *__restrict__ lam,
+    double *__restrict__ rec, int do_glob, int mg, const int *__restrict__ glob, int m, int K,
+    const int *__restrict__ con_ptr, const int *__restrict__ con_slot, const double *__restrict__ con_w,
+    const double *__restrict__ uRR, const double *__restrict__ par, const double *__restrict__ ctrl_prev,
+    double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev, const double *__restrict__ partC, int nblkC,
+    double *__restrict__ partA, int pblk_off, int gwide) {
+    __shared__ double c[C_NCTRL];
+    __shared__ double red[10];
+    LRS_TS(0, 0);
+    LRS_BLK_BEGIN();
+    const bool ctrl_wave = (int)(threadIdx.x >> 6) == kLatRowWaves;
+    // this iteration's operands: ctrl_step folds the previous stage (and flips the G and R
+    // buffers) exactly when `fold` holds
+    const double lsflag = ls_prev[LS_FLAG];
+    const int fold = (ctrl_prev[C_ACT2] != 0.0 && ctrl_prev[C_PENDING] == 1.0 && lsflag == 0.0) ? 1 : 0;
+    const bool r1 = (ctrl_prev[C_RCUR] != 0.0) != (fold != 0);
+    const bool g1 = (ctrl_prev[C_GCUR] != 0.0) != (fold != 0);
+    const double *__restrict__ R = (r1 ? Rb1 : Rb0) + foff;
+    const double *__restrict__ Gc = (g1 ? G1 : G0) + foff;
+    const double *__restrict__ s0 = s0a + foff, *__restrict__ y0 = y0a + foff;
+    const double *__restrict__ s1 = s1a + foff, *__restrict__ y1 = y1a + foff;
+    double *__restrict__ D = Dall + foff;
+    const int lane = threadIdx.x & (G - 1);
+    const int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G;
+    const bool valid = !ctrl_wave && i < n;
+    const int ic = valid ? i : 0;
+    const long oi = (long)ic * ld + lane * E;
+    DirRow<E> own;
+    double xi[E];
+    int kb = 0, ke = 0, np = 0;
+    int jj[NB], ss[NB];
+    double cw[NB], bq[NB], cq[NB], lq[NB];
+    double2 l1[NB];
+    if (ctrl_wave) {
+        // ---- control wave: the previous stage's dots, then the control of this iteration
+        const int l64 = threadIdx.x & 63;
+        if (l64 < C_NCTRL) c[l64] = ctrl_prev[l64];
+        double s[10];
+        if (fold) {
+            wave_reduce_partials<10>(partC, nblkC, s);
+        } else {
+#pragma unroll
+            for (int v = 0; v < 10; ++v) s[v] = 0.0;
+        }
+        if (l64 == 0) {
+#pragma unroll
+            for (int v = 0; v < 10; ++v) red[v] = s[v];
+            ctrl_step(c, par, lsflag, ls_prev[LS_TAU], fold, red, mg == 0);
+        }
+#ifdef LRS_PHASE_TIMING
+        if (blockIdx.x == 0 && l64 == 0) g_phase_tmp[0][7] = wall_clock64();
+#endif
+    } else {
+        // ---- row waves: every load the control does not decide, one memory trip per
+        // dependency level; loads clamped to valid addresses instead of branched
+        kb = adj_ptr[ic];
+        ke = adj_low[ic];
+        ld_row<E>(Gc + oi, own.g);
+        ld_row<E>(s0 + oi, own.a0); ld_row<E>(y0 + oi, own.b0);
+        ld_row<E>(s1 + oi, own.a1); ld_row<E>(y1 + oi, own.b1);
+        ld_row<E>(R + oi, xi);
+        np = valid ? min(ke - kb, NB) : 0;
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int k = np > 0 ? kb + min(u, np - 1) : 0;
+            jj[u] = adj_col[k];
+            ss[u] = adj_slot[k];
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            cw[u] = Cw[ss[u]];
+            l1[u] = loc1[ss[u]];
+        }
+        // slots without a single local constraint read the row's own (spread, cached) index
+        // instead of a common one: no hot line shared by every lane
+        const int ispare = min(ic, m - 1);
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int ci = (int)l1[u].y >= 0 ? (int)l1[u].y : ispare;
+            bq[u] = b[ci];
+            cq[u] = cvs[ci];
+            lq[u] = lam[ci];
+        }
+#ifdef LRS_PHASE_TIMING
+        if (blockIdx.x == 0 && threadIdx.x == 0 && xi[0] != 12345.678) g_phase_tmp[0][1] = wall_clock64();
+        if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && cw[0] != 12345.678)
+            g_phase_tmp[0][2] = wall_clock64();
+#endif
+    }
+    __syncthreads();
+    LRS_TS(0, 3);
+    if (pblk_off == 0 && blockIdx.x == 0 && threadIdx.x < C_NCTRL) ctrl_cur[threadIdx.x] = c[threadIdx.x];
+    const bool active = c[C_ACTIVE] != 0.0;
+    if (!active && !(fold && mg > 0)) return;
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (fold && do_glob) {
+        // global constraints: A(RR^T) from the slots and their residual (as k_it_a)
+        if (gwide) {
+            const int lane64 = threadIdx.x & 63;
+            const int nw = gridDim.x * (kRowBlock / 64);
+            for (int g = blockIdx.x * (kRowBlock / 64) + (threadIdx.x >> 6); g < mg; g += nw) {
+                const int ig = glob[g];
+                double tot = 0.0;
+                for (int k = 0; k < K; ++k) {
+                    const long row = (long)k * m + ig;
+                    double v = 0.0;
+                    for (int e = con_ptr[row] + lane64; e < con_ptr[row + 1]; e += 64) v += con_w[e] * uRR[con_slot[e]];
+                    tot += wave_sum(v);
+                }
+                if (lane64 == 0) {
+                    cvs[ig] = tot;
+                    const double dd = b[ig] - tot;
+                    acc[7] += dd * dd;
+                }
+            }
+        } else {
+            for (int g = blockIdx.x * kRowBlock + threadIdx.x; g < mg; g += gridDim.x * kRowBlock) {
+                const int ig = glob[g];
+                double tot = 0.0;
+                for (int k = 0; k < K; ++k) {
+                    const long row = (long)k * m + ig;
+                    double v = 0.0;
+                    for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) v += con_w[e] * uRR[con_slot[e]];
+                    tot += v;
+                }
+                cvs[ig] = tot;
+                const double dd = b[ig] - tot;
+                acc[7] += dd * dd;
+            }
+        }
+    }
+    if (active && valid) {
+        DirCoef kc;
+        kc.cg = c[C_CG]; kc.cs0 = c[C_CS0]; kc.cy0 = c[C_CY0]; kc.cs1 = c[C_CS1]; kc.cy1 = c[C_CY1];
+        kc.u0 = (kc.cs0 != 0.0 || kc.cy0 != 0.0);
+        kc.u1 = (kc.cs1 != 0.0 || kc.cy1 != 0.0);
+        const double rho = par[P_RHO], rhoInv = 1.0 / rho;
+        double yi[E];
+        own.eval(kc, yi);
+        st_row<E>(D + oi, yi);
+        // one lower entry (j, slot): sym(R D^T), D D^T, objective parts, local constraints
+        auto entry = [&](int j, int sl, const double (&xj)[E], const double (&yj)[E], double cwv, double2 l1v,
+                         double bv, double cv, double lv) {
+            double d0 = 0.0, d1 = 0.0;
+            if (j != i) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) d0 += xi[e] * yj[e] + xj[e] * yi[e];
+                d0 *= 0.5;
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e) d0 += xi[e] * yi[e];
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) d1 += yi[e] * yj[e];
+            d0 = group_sum<G>(d0);
+            d1 = group_sum<G>(d1);
+            if (lane != 0) return;
+            uRD[sl] = d0;
+            uDD[sl] = d1;
+            acc[0] += cwv * d0;
+            acc[1] += cwv * d1;
+            // local constraints on this slot (ALMCalq12p12 lorads_alm.c:714-734, dots :269-277)
+            const int c1 = (int)l1v.y;
+            const int e0 = c1 == -2 ? loc_ptr[sl] : 0, e1 = c1 == -2 ? loc_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
+            for (int e = e0; e < e1; ++e) {
+                const int ci = c1 >= 0 ? c1 : loc_con[e];
+                const double w = c1 >= 0 ? l1v.x : loc_w[e];
+                const double bi = c1 >= 0 ? bv : b[ci], cvi = c1 >= 0 ? cv : cvs[ci], li = c1 >= 0 ? lv : lam[ci];
+                const double q1 = 2.0 * (w * d0), q2 = w * d1;
+                const double q0 = (bi - cvi) + rhoInv * li;
+                acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1;
+                acc[6] += q0 * q1;
+                double2 *r = reinterpret_cast<double2 *>(rec + 4L * ci);
+                r[0] = make_double2(cvi, q1);
+                r[1] = make_double2(q2, (-li) + (-rho) * bi);
+            }
+        };
+        // prefetched entries, U neighbour rows in flight at a time
+#pragma unroll
+        for (int u0 = 0; u0 < NB; u0 += U) {
+            if (u0 < np) {
+                double xj[U][E], yj[U][E];
+#pragma unroll
+                for (int v = 0; v < U; ++v) {
+                    // entries past np repeat the chunk's first (static indices only: a
+                    // runtime index would move jj[] to LDS)
+                    const long oj = (long)(u0 + v < np ? jj[u0 + v] : jj[u0]) * ld + lane * E;
+                    ld_row<E>(R + oj, xj[v]);
+                    DirRow<E> dj;
+                    dj.load(kc, Gc, s0, y0, s1, y1, oj);
+                    dj.eval(kc, yj[v]);
+                }
+#pragma unroll
+                for (int v = 0; v < U; ++v)
+                    if (u0 + v < np) entry(jj[u0 + v], ss[u0 + v], xj[v], yj[v], cw[u0 + v], l1[u0 + v], bq[u0 + v],
+                                           cq[u0 + v], lq[u0 + v]);
+            }
+        }
+        // entries beyond the prefetched ones
+        for (int k = kb + NB; k < ke; ++k) {
+            const int j = adj_col[k], sl = adj_slot[k];
+            const long oj = (long)j * ld + lane * E;
+            double xj[E], yj[E];
+            ld_row<E>(R + oj, xj);
+            DirRow<E> dj;
+            dj.load(kc, Gc, s0, y0, s1, y1, oj);
+            dj.eval(kc, yj);
+            const double2 l1v = loc1[sl];
+            const int ci = (int)l1v.y;
+            double bv = 0.0, cv = 0.0, lv = 0.0;
+            if (ci >= 0) { bv = b[ci]; cv = cvs[ci]; lv = lam[ci]; }
+            entry(j, sl, xj, yj, Cw[sl], l1v, bv, cv, lv);
+        }
+    }
+    LRS_TS(0, 5);
+    write_partials<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x);
+    LRS_TS_END(0, 6);
+#ifdef LRS_PHASE_TIMING
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int q_ = 7; q_ < 12; ++q_) g_phase[0][q_] = g_phase_tmp[0][q_];
+#endif
+    LRS_BLK_END(0);
+}
+
+// B in the latency regime (k_it_b MODE 0): the control wave reduces A's (and G's)
+// partials and solves the line search while the row waves prefetch.
+template <int G, int E, int NB, int U>
+__global__ void __launch_bounds__(kRowBlock) k_lat_b(
+    int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
+    const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
+    const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0, double *s1, double *y1,
+    double *__restrict__ uRR, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
+    const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double2 *__restrict__ slot1,
+    const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
+    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
+    double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
+    const double *__restrict__ partA, int nblkA, const double *__restrict__ partB, int nblkB,
+    double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m) {
+    __shared__ double red[12];
+    __shared__ double ls[LS_N];
+    LRS_TS(2, 0);
+    LRS_BLK_BEGIN();
+    if (ctrl[C_ACT2] == 0.0) return;
+    const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
+    const bool r1 = ctrl[C_RCUR] != 0.0;
+    const double *__restrict__ R = (r1 ? Rb1 : Rb0) + foff;
+    double *__restrict__ Rn = (r1 ? Rb0 : Rb1) + foff;
+    const double *__restrict__ D = Dall + foff;
+    double *__restrict__ Gold = (gcur == 0 ? G0 : G1) + foff;
+    double *__restrict__ Gnew = (gcur == 0 ? G1 : G0) + foff;
+    double *__restrict__ sh = (h == 0 ? s0 : s1) + foff;
+    double *__restrict__ yh = (h == 0 ? y0 : y1) + foff;
+    const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
+    const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
+    const bool two = (L == 2);
+    const bool ctrl_wave = (int)(threadIdx.x >> 6) == kLatRowWaves;
+    const int lane = threadIdx.x & (G - 1);
+    const int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G;
+    const bool valid = !ctrl_wave && i < n;
+    const int ic = valid ? i : 0;
+    const long oi = (long)ic * ld + lane * E;
+    int kb = 0, kl = 0, ke = 0, np = 0;
+    double ri[E], di[E], go[E], sov[E], yov[E];
+    int jj[NB], ss[NB];
+    double sv[NB], bq[NB];
+    double2 s1v[NB], l1v[NB], ra[NB], rb[NB];
+    if (ctrl_wave) {
+        // ---- control wave: line search (ALMLineSearch lorads_alm.c:266-333)
+        double sA[7];
+        wave_reduce_partials<7>(partA, nblkA, sA);
+        if (nblkB > 0) {
+            double sB[5];
+            wave_reduce_partials<5>(partB, nblkB, sB);
+#pragma unroll
+            for (int q = 0; q < 5; ++q) sA[2 + q] += sB[q];
+        }
+        if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+            for (int v = 0; v < 7; ++v) red[v] = sA[v];
+        }
+        __builtin_amdgcn_wave_barrier();
+        line_search_t<true>(par, red[0], red[1], red + 2, ls);
+#ifdef LRS_PHASE_TIMING
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_phase_tmp[2][7] = wall_clock64();
+#endif
+    } else {
+        // ---- row waves: prefetch, one memory trip per dependency level, clamped loads
+        kb = adj_ptr[ic];
+        kl = adj_low[ic];
+        ke = adj_ptr[ic + 1];
+        ld_row<E>(R + oi, ri);
+        ld_row<E>(D + oi, di);
+        ld_row<E>(Gold + oi, go);
+        if (two) { ld_row<E>(so + oi, sov); ld_row<E>(yo + oi, yov); }
+        np = valid ? min(ke - kb, NB) : 0;
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int k = np > 0 ? kb + min(u, np - 1) : 0;
+            jj[u] = adj_col[k];
+            ss[u] = adj_slot[k];
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            sv[u] = Craw[ss[u]];
+            s1v[u] = slot1[ss[u]];
+            l1v[u] = loc1[ss[u]];
+        }
+        // slots without a single constraint read the row's own (spread, cached) index instead
+        // of a common one: no hot line shared by every lane
+        const int ispare = min(ic, m - 1);
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int c1 = (int)s1v[u].y >= 0 ? (int)s1v[u].y : ispare;
+            const int cl = (int)l1v[u].y >= 0 ? (int)l1v[u].y : ispare;
+            const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
+            ra[u] = r[0];
+            rb[u] = r[1];
+            bq[u] = b[cl];
+        }
+#ifdef LRS_PHASE_TIMING
+        if (blockIdx.x == 0 && threadIdx.x == 0 && ri[0] != 12345.678 && sv[0] != 12345.678)
+            g_phase_tmp[2][5] = wall_clock64();
+        if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && ra[0].x != 12345.678)
+            g_phase_tmp[2][6] = wall_clock64();
+#endif
+    }
+    __syncthreads();
+    LRS_TS(2, 2);
+    if (pblk_off == 0 && blockIdx.x == 0 && threadIdx.x < LS_N) ls_cur[threadIdx.x] = ls[threadIdx.x];
+    if (ls[LS_FLAG] != 0.0) return;
+    const double tau = ls[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (valid) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) ri[e] += tau * di[e];
+        st_row<E>(Rn + oi, ri);
+        double g[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[e] = 0.0;
+        // one entry (j, slot) with R_new,j: S_ij = C + A^*(M1) (ALMSetGrad lorads_alm.c:38-57),
+        // the gradient, and on lower slots A(R_new R_new^T) with the local constraints
+        auto entry = [&](int sl, bool lower, const double (&rj)[E], double svv, double2 s1u, double2 ra_, double2 rb_,
+                         double2 l1u, double bv) {
+            const int c1 = (int)s1u.y;
+            const int e0 = c1 == -2 ? slot_ptr[sl] : 0;
+            const int e1 = c1 == -2 ? slot_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
+            for (int e = e0; e < e1; ++e) {
+                double2 x = ra_, y = rb_;
+                if (c1 < 0) {
+                    const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
+                    x = r[0];
+                    y = r[1];
+                }
+                double cv = x.x + tau * x.y;
+                cv = cv + tau2 * y.x;
+                const double M1 = y.y + rho * cv;
+                svv += M1 * (c1 >= 0 ? s1u.x : slot_a[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) g[e] += svv * rj[e];
+            if (!lower) return;
+            double d = 0.0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) d += ri[e] * rj[e];
+            d = group_sum<G>(d);
+            if (lane != 0) return;
+            uRR[sl] = d;
+            const int cl = (int)l1u.y;
+            const int f0 = cl == -2 ? loc_ptr[sl] : 0;
+            const int f1 = cl == -2 ? loc_ptr[sl + 1] : (cl >= 0 ? 1 : 0);
+            for (int e = f0; e < f1; ++e) {
+                const int ci = cl >= 0 ? cl : loc_con[e];
+                const double tot = (cl >= 0 ? l1u.x : loc_w[e]) * d;
+                cvs[ci] = tot;
+                const double dd = (cl >= 0 ? bv : b[ci]) - tot;
+                acc[9] += dd * dd;
+            }
+        };
+#pragma unroll
+        for (int u0 = 0; u0 < NB; u0 += U) {
+            if (u0 < np) {
+                double rj[U][E];
+#pragma unroll
+                for (int v = 0; v < U; ++v) {
+                    const long oj = (long)(u0 + v < np ? jj[u0 + v] : jj[u0]) * ld + lane * E;
+                    double dj[E];
+                    ld_row<E>(R + oj, rj[v]);
+                    ld_row<E>(D + oj, dj);
+#pragma unroll
+                    for (int e = 0; e < E; ++e) rj[v][e] += tau * dj[e];
+                }
+#pragma unroll
+                for (int v = 0; v < U; ++v) {
+                    const int u = u0 + v;
+                    if (u < np) entry(ss[u], kb + u < kl, rj[v], sv[u], s1v[u], ra[u], rb[u], l1v[u], bq[u]);
+                }
+            }
+        }
+        for (int k = kb + NB; k < ke; ++k) {
+            const int j = adj_col[k], sl = adj_slot[k];
+            const long oj = (long)j * ld + lane * E;
+            double rj[E], dj[E];
+            ld_row<E>(R + oj, rj);
+            ld_row<E>(D + oj, dj);
+#pragma unroll
+            for (int e = 0; e < E; ++e) rj[e] += tau * dj[e];
+            const double2 s1u = slot1[sl];
+            const int c1 = (int)s1u.y;
+            double2 x = make_double2(0.0, 0.0), y = x;
+            if (c1 >= 0) {
+                const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
+                x = r[0];
+                y = r[1];
+            }
+            const bool lower = k < kl;
+            const double2 l1u = lower ? loc1[sl] : make_double2(0.0, -1.0);
+            const int cl = (int)l1u.y;
+            entry(sl, lower, rj, Craw[sl], s1u, x, y, l1u, cl >= 0 ? b[cl] : 0.0);
+        }
+        // gradient G_new = 2 S R_new, L-BFGS pair s = tau D, y = G_new - G_old, dots
+        double sv2[E], yv[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[e] *= 2.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { sv2[e] = tau * di[e]; yv[e] = g[e] - go[e]; }
+        st_row<E>(Gnew + oi, g);
+        st_row<E>(sh + oi, sv2);
+        st_row<E>(yh + oi, yv);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            acc[0] += g[e] * g[e];
+            acc[1] += yv[e] * sv2[e];
+            acc[2] += yv[e] * yv[e];
+            acc[3] += sv2[e] * g[e];
+            acc[4] += yv[e] * g[e];
+        }
+        if (two) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                acc[5] += sov[e] * g[e];
+                acc[6] += yov[e] * g[e];
+                acc[7] += sov[e] * yv[e];
+                acc[8] += yov[e] * yv[e];
+            }
+        }
+    }
+    LRS_TS(2, 3);
+    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+    LRS_TS_END(2, 4);
+#ifdef LRS_PHASE_TIMING
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int q_ = 5; q_ < 12; ++q_) g_phase[2][q_] = g_phase_tmp[2][q_];
+#endif
+    LRS_BLK_END(2);
+}
+
+// ------------------------------------------------------------------------
 // Device-resident CG (CGSolve, linalg/lorads_cgs.c:128-287) for one cone's ADMM
 // half-step system M X = b, M x = x + A^*(A(sym(x V^T))) V (linSysProduct,
 // lorads_admm.c:471-486).  Scalars live in cgc[] (CgIdx); every kernel after the
@@ -2158,6 +2666,39 @@ static int plan_b(const DevCone &c, int K, StagePlan &p) {
     return 0;
 }
 
+// Latency-regime kernels (k_lat_a / k_lat_b): one row per lane group, every group
+// resident, no teams (T == 1), and each stage's producer partials within one control
+// wave's reach.  NB (prefetched entries) from the most entries of one row.
+constexpr int kLatNbA = 4, kLatUA = 2, kLatNbB = 6, kLatUB = 3;
+template <int GG, int EE>
+static int res_la() {
+    static int c = 0;
+    return resident_blocks(k_lat_a<GG, EE, kLatNbA, kLatUA>, &c);
+}
+template <int GG, int EE>
+static int res_lb() {
+    static int c = 0;
+    return resident_blocks(k_lat_b<GG, EE, kLatNbB, kLatUB>, &c);
+}
+static bool lat_disabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("LRS_NO_LAT");
+        v = (e && atoi(e) != 0) ? 1 : 0;
+    }
+    return v != 0;
+}
+// grid of the latency kernels for cone c, or 0 when they do not apply
+static int lat_grid(const DevCone &c, const StagePlan &pa, const StagePlan &pb) {
+    if (lat_disabled() || forced_regime() == 2 || c.maxdeg <= 0 || !pa.small || !pb.small || pa.T != 1 || pb.T != 1)
+        return 0;
+    const long need = ((long)c.nown * c.G + kLatRows - 1) / kLatRows;
+    int ra = 0, rb = 0;
+    LRS_LAYOUT_SWITCH(c.G, c.E, { ra = (res_la<GG, EE>)(); rb = (res_lb<GG, EE>)(); });
+    if (need > std::min(ra, rb) || need > kLatMaxPartials) return 0;
+    return (int)std::max(1L, need);
+}
+
 // Whether stage A runs as two launches (bandwidth regime) for the current layouts.
 bool alm_stage_a_split(const DevProblem &P) {
     for (int k = 0; k < P.K; ++k) {
@@ -2229,13 +2770,30 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         nblkB += pb[k].grid;
         if (!pa[k].small) split = true;
     }
+    const int gwide = P.glob_maxlen >= 32 ? 1 : 0;   // long global constraints: a wave each
+    const int gg = gwide ? std::min((std::max(1, P.mg) + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks)
+                         : std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
+    // latency regime: every launch of both stages on the k_lat kernels, or none
+    int lg[kMaxCones] = {0};
+    bool lat = !sh && !split && !P.no_lat;
+    int nlat = 0;
+    for (int k = 0; k < KL && lat; ++k) {
+        lg[k] = lat_grid(cone_of(k), pa[k], pb[k]);
+        if (lg[k] <= 0) lat = false;
+        nlat += lg[k];
+    }
+    if (lat && (nlat > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials))) lat = false;
+    P.last_path = lat ? 0 : 1;
+    if (lat) {
+        nblkA = nblkB = nlat;
+        for (int k = 0; k < KL; ++k) pa[k].grid = pb[k].grid = lg[k];
+    }
     // what the consumers read: every producer block's partials, or (sharded) the summed totals
     double *totA = sh ? W.tot : nullptr, *totC = sh ? W.tot + 16 : nullptr;
     const double *inC = sh ? totC : W.partC;
     const int nC = sh ? 1 : nblkB, pstr = sh ? 1 : kMaxPartialBlocks;
     const double *inA = sh ? totA : W.part;
     const int nA = sh ? 1 : nblkA;
-    const int gwide = P.glob_maxlen >= 32 ? 1 : 0;   // long global constraints: a wave each
     auto mark = [&](int q) -> int {
         if (a.ev && hipEventRecord(a.ev[q], st) != hipSuccess) {
             snprintf(g_err, sizeof(g_err), "hipEventRecord failed");
@@ -2257,10 +2815,21 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        W.lam, W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,      \
                        W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, pa[k].T, gwide, c.row0, \
                        pstr)
-        LRS_LAYOUT_SWITCH(c.G, c.E, {
-            if (!split) LRS_LAUNCH_A(2, 0);
-            else LRS_LAUNCH_A(1, 1);
-        });
+        if (lat) {
+            LRS_LAYOUT_SWITCH(c.G, c.E, {
+                hipLaunchKernelGGL((k_lat_a<GG, EE, kLatNbA, kLatUA>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
+                                   c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D,
+                                   W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr,
+                                   P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam,
+                                   W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,
+                                   W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, gwide);
+            });
+        } else {
+            LRS_LAYOUT_SWITCH(c.G, c.E, {
+                if (!split) LRS_LAUNCH_A(2, 0);
+                else LRS_LAUNCH_A(1, 1);
+            });
+        }
         LRS_CHECK_LAUNCH();
         off += grid;
     }
@@ -2282,8 +2851,6 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     }
     if (mark(1)) return -1;
     // G: phase-1 test and the global constraints' q and dots
-    const int gg = gwide ? std::min((std::max(1, P.mg) + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks)
-                         : std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
     if (P.mg > 0 && (mask & 2)) {
         hipLaunchKernelGGL(k_it_g, dim3(gg), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot,
                            P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, nblkB, W.part,
@@ -2304,10 +2871,21 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, inA, nA, W.partB,   \
                        P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, c.n, pstr)
         const bool small = pb[k].small;
-        LRS_LAYOUT_SWITCH(c.G, c.E, {
-            if (small) LRS_LAUNCH_B(4, 0);
-            else LRS_LAUNCH_B(1, 1);
-        });
+        if (lat) {
+            LRS_LAYOUT_SWITCH(c.G, c.E, {
+                hipLaunchKernelGGL((k_lat_b<GG, EE, kLatNbB, kLatUB>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
+                                   c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0],
+                                   W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
+                                   P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con,
+                                   P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur,
+                                   inA, nA, W.partB, P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, P.m);
+            });
+        } else {
+            LRS_LAYOUT_SWITCH(c.G, c.E, {
+                if (small) LRS_LAUNCH_B(4, 0);
+                else LRS_LAUNCH_B(1, 1);
+            });
+        }
         LRS_CHECK_LAUNCH();
         off += grid;
     }

@@ -535,6 +535,10 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         mc.nown = (int)ntot;
         mc.P = (int)Ptot_l;
         mc.adj_nnz = nadj;
+        for (long q = 0; q < ntot; ++q) {
+            mc.maxdeg = std::max(mc.maxdeg, ap[q + 1] - ap[q]);
+            mc.maxlow = std::max(mc.maxlow, al[q] - ap[q]);
+        }
         if (!dput(&mc.adj_ptr, ap, err) || !dput(&mc.adj_low, al, err) || !dput(&mc.adj_col, ac, err) ||
             !dput(&mc.adj_slot, as, err))
             return false;
@@ -548,6 +552,10 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         std::vector<int> adj_slot_g(c.adj_slot.size());
         for (size_t t = 0; t < c.adj_slot.size(); ++t) adj_slot_g[t] = d.slot_off + c.adj_slot[t];
         d.adj_nnz = (long)c.adj_col.size();
+        for (int q = 0; q < c.n; ++q) {
+            d.maxdeg = std::max(d.maxdeg, c.adj_ptr[q + 1] - c.adj_ptr[q]);
+            d.maxlow = std::max(d.maxlow, c.adj_low[q] - c.adj_ptr[q]);
+        }
         if (!dput(&d.adj_ptr, c.adj_ptr, err) || !dput(&d.adj_low, c.adj_low, err) ||
             !dput(&d.adj_col, c.adj_col, err) || !dput(&d.adj_slot, adj_slot_g, err))
             return false;

@@ -1499,6 +1499,24 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
     return 0;
 }
 
+int lrs_set_kernel_path(lrs_ctx *c, int path) {
+    if (c) bind(c);
+    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    if (path != 0 && path != 1) { set_err("kernel path %d: expected 0 (auto) or 1 (general)", path); return -1; }
+    if (c->dp.no_lat != path) {
+        drop_graphs(c);   // captured batches hold the previous kernels
+        c->dp.no_lat = path;
+    }
+    return 0;
+}
+
+int lrs_get_kernel_path(lrs_ctx *c, int *used) {
+    if (c) bind(c);
+    if (!c || !used) { set_err("null argument"); return -1; }
+    *used = c->loaded ? c->dp.last_path : -1;
+    return 0;
+}
+
 int lrs_set_log_path(lrs_ctx *c, const char *path) {
     if (c) bind(c);
     if (c->logfp) fclose(c->logfp);

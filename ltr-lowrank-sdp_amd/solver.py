@@ -106,6 +106,8 @@ def load_library(path=None):
         "lrs_time_auut": (C.c_int, [vp, C.c_int, dp]),
         "lrs_profile_stages": (C.c_int, [vp, C.POINTER(Params), C.c_long, dp, C.POINTER(C.c_long)]),
         "lrs_time_stages": (C.c_int, [vp, C.c_int, dp]),
+        "lrs_set_kernel_path": (C.c_int, [vp, C.c_int]),
+        "lrs_get_kernel_path": (C.c_int, [vp, ip]),
         "lrs_stage_bytes": (C.c_int, [vp, dp]),
         "lrs_auut_bytes": (C.c_int, [vp, dp]),
         "lrs_time_gram": (C.c_int, [vp, C.c_int, C.c_int, dp, dp]),
@@ -355,6 +357,16 @@ class Solver:
         v = (C.c_double * 3)()
         self._check(self.lib.lrs_stage_bytes(self.ctx, v), "stage_bytes")
         return list(v)
+
+    def set_kernel_path(self, path):
+        """0 = automatic (latency-regime kernels where they apply), 1 = general row kernels."""
+        self._check(self.lib.lrs_set_kernel_path(self.ctx, int(path)), "set_kernel_path")
+
+    def kernel_path(self):
+        """Path of the last enqueued ALM iteration: 0 latency-regime kernels, 1 general, -1 none."""
+        v = C.c_int(-1)
+        self._check(self.lib.lrs_get_kernel_path(self.ctx, C.byref(v)), "get_kernel_path")
+        return v.value
 
     def time_stages(self, reps=200):
         """Per-launch ms of the split-iteration stages [A, G, B] (back-to-back relaunches)."""

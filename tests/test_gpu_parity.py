@@ -249,3 +249,42 @@ def test_device_reopt_level1_matches_reference(solver_mod, case):
     if due:   # both ran the round: its ALM phase ends near the same point
         assert abs(res["alm_pobj"] - r["alm_pobj"]) <= tol * (1 + abs(r["alm_pobj"]))
     assert res["pinf"] <= 1e-4 and res["gap"] <= max(1e-4, 10 * r["admm_gap"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mc_torus12x10", "mc_rand200", "mc_rand300w", "rsparse60", "theta40"])
+def test_latency_kernels_match_general(solver_mod, name):
+    """k_lat_a / k_lat_b (control wave + prefetching row waves) solve like the general row
+    kernels k_it_a / k_it_b: same per-entry arithmetic, partial sums over other block
+    partitions (MaxCut: inner iterations +-2, ALM objective 1e-8; all: final 1e-6)."""
+    out = []
+    for path in (0, 1):
+        sv = solver_mod.Solver(instance(name))
+        sv.set_kernel_path(path)
+        r = sv.solve(reoptLevel=0)
+        out.append((r, sv.kernel_path()))
+        sv.close()
+    (a, pa), (b, pb) = out
+    assert pb == 1
+    if name == "mc_torus12x10":   # sparse rows, 120 of them: every lane group resident, no teams
+        assert pa == 0, "latency kernels not taken on a small sparse instance"
+    if name.startswith("mc_"):
+        assert abs(a["alm_inner"] - b["alm_inner"]) <= 2, (a["alm_inner"], b["alm_inner"])
+        assert abs(a["alm_pobj"] - b["alm_pobj"]) <= 1e-8 * abs(b["alm_pobj"])
+    tol = 1e-6 if name.startswith("mc_") else 10 * (a["gap"] + b["gap"]) + 1e-6
+    assert abs(a["pobj"] - b["pobj"]) <= tol * max(1.0, abs(b["pobj"])), (a["pobj"], b["pobj"])
+
+
+@pytest.mark.gpu
+def test_latency_kernels_throughput_budget(solver_mod):
+    """The bench's fixed-budget ALM run (phase-1 exit off) does exactly `steps` iterations
+    on the latency kernels, deterministically."""
+    sv = solver_mod.Solver(instance("mc_torus12x10"))
+    r = sv.determine_rank()[0]
+    outs = []
+    for _ in range(2):
+        o = sv.alm_throughput(0, 300, fixedRank=r, reoptLevel=0)
+        outs.append(o["done"])
+    assert sv.kernel_path() == 0
+    assert outs == [300, 300]
+    sv.close()
