@@ -891,13 +891,25 @@ __device__ void line_search(const double *__restrict__ par, int K, double *ls) {
 // consuming launch reduces them in the same fixed order.  No in-launch hand-off, no
 // fences; the launch boundary is the only synchronisation.  Bitwise reproducible.
 // ------------------------------------------------------------------------
+// Block sums of NV accumulators into part[v][slot]: wave sums meet in LDS, then thread v
+// adds value v over the waves in wave order (the order of block_reduce) and stores it --
+// one barrier, the NV sums in parallel.
 template <int NV, int NT = kBlock>
 __device__ __forceinline__ void write_partials(double (&acc)[NV], double *__restrict__ part, int slot) {
-    double s[NV];
-    block_reduce<NV, NT>(acc, s);
-    if (threadIdx.x == 0) {
+    __shared__ double sh[NV][NT / 64];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-        for (int v = 0; v < NV; ++v) part[v * kMaxPartialBlocks + slot] = s[v];
+    for (int v = 0; v < NV; ++v) {
+        const double t = wave_sum(acc[v]);
+        if (lane == 0) sh[v][wid] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        const int v = threadIdx.x;
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) t += sh[v][w];
+        part[v * kMaxPartialBlocks + slot] = t;
     }
 }
 
@@ -970,8 +982,8 @@ __device__ void line_search_v(const double *__restrict__ par, double p1, double 
 // Control of one split iteration (thread 0).  c: shared copy of the previous control,
 // updated in place.
 // d = the nine dots of the previous gradient stage when `fold`.
-__device__ void ctrl_step(double *c, const double *__restrict__ par, double lsflag, double lstau, int fold,
-                          const double *d, bool ph1) {
+__device__ __forceinline__ void ctrl_step(double *c, const double *__restrict__ par, double lsflag, double lstau,
+                                          int fold, const double *d, bool ph1) {
     // in place on the shared copy: a register copy of the block would set the VGPR
     // peak (and so the occupancy) of the whole row kernel
     const int L = (int)par[P_L];
@@ -1693,9 +1705,10 @@ __device__ __forceinline__ void wave_reduce_partials(const double *__restrict__ 
     }
 }
 
-// A in the latency regime (k_it_a MODE 0).  NB: lower entries prefetched per row;
-// U: neighbour rows loaded at a time.
-template <int G, int E, int NB, int U>
+// A in the latency regime (k_it_a MODE 0).  NO: off-diagonal lower entries whose operand
+// rows are prefetched before the barrier (the diagonal entry, the last lower one in the
+// column-sorted adjacency, uses the row's own operands); further ones are loaded after it.
+template <int G, int E, int NO>
 __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
@@ -1711,7 +1724,6 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev, const double *__restrict__ partC, int nblkC,
     double *__restrict__ partA, int pblk_off, int gwide) {
     __shared__ double c[C_NCTRL];
-    __shared__ double red[10];
     LRS_TS(0, 0);
     LRS_BLK_BEGIN();
     const bool ctrl_wave = (int)(threadIdx.x >> 6) == kLatRowWaves;
@@ -1731,16 +1743,27 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     const bool valid = !ctrl_wave && i < n;
     const int ic = valid ? i : 0;
     const long oi = (long)ic * ld + lane * E;
+    // row-wave prefetch state: own operands, the NO off-diagonal entries (records and the
+    // neighbours' direction operands), the diagonal entry's records
     DirRow<E> own;
     double xi[E];
-    int kb = 0, ke = 0, np = 0;
-    int jj[NB], ss[NB];
-    double cw[NB], bq[NB], cq[NB], lq[NB];
-    double2 l1[NB];
+    int kb = 0, no = 0;
+    bool dg = false;
+    int jj[NO], ss[NO];
+    double cw[NO], bq[NO], cq[NO], lq[NO];
+    double2 l1[NO];
+    DirRow<E> nbr[NO];
+    double xj[NO][E];
+    int sd = 0;
+    double cwd = 0.0, bd = 0.0, cd = 0.0, lmd = 0.0;
+    double2 l1d = make_double2(0.0, -1.0);
     if (ctrl_wave) {
-        // ---- control wave: the previous stage's dots, then the control of this iteration
+        // ---- control wave: the previous stage's dots, then the control of this iteration;
+        // every lane runs ctrl_step on a register copy (uniform values), lane 0 publishes it
         const int l64 = threadIdx.x & 63;
-        if (l64 < C_NCTRL) c[l64] = ctrl_prev[l64];
+        double cc[C_NCTRL];
+#pragma unroll
+        for (int q = 0; q < C_NCTRL; ++q) cc[q] = ctrl_prev[q];
         double s[10];
         if (fold) {
             wave_reduce_partials<10>(partC, nblkC, s);
@@ -1748,10 +1771,13 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
 #pragma unroll
             for (int v = 0; v < 10; ++v) s[v] = 0.0;
         }
+#ifdef LRS_PHASE_TIMING
+        if (blockIdx.x == 0 && l64 == 0 && s[9] != 12345.678 && cc[5] != 12345.678) g_phase_tmp[0][8] = wall_clock64();
+#endif
+        ctrl_step(cc, par, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
         if (l64 == 0) {
 #pragma unroll
-            for (int v = 0; v < 10; ++v) red[v] = s[v];
-            ctrl_step(c, par, lsflag, ls_prev[LS_TAU], fold, red, mg == 0);
+            for (int q = 0; q < C_NCTRL; ++q) c[q] = cc[q];
         }
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && l64 == 0) g_phase_tmp[0][7] = wall_clock64();
@@ -1760,36 +1786,55 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         // ---- row waves: every load the control does not decide, one memory trip per
         // dependency level; loads clamped to valid addresses instead of branched
         kb = adj_ptr[ic];
-        ke = adj_low[ic];
+        const int ke = adj_low[ic];
         ld_row<E>(Gc + oi, own.g);
         ld_row<E>(s0 + oi, own.a0); ld_row<E>(y0 + oi, own.b0);
         ld_row<E>(s1 + oi, own.a1); ld_row<E>(y1 + oi, own.b1);
         ld_row<E>(R + oi, xi);
-        np = valid ? min(ke - kb, NB) : 0;
+        const int nl = valid ? ke - kb : 0;
+        const int kd = nl > 0 ? ke - 1 : 0;
+        const int jd = adj_col[kd];
+        sd = adj_slot[kd];
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int k = np > 0 ? kb + min(u, np - 1) : 0;
+        for (int u = 0; u < NO; ++u) {
+            const int k = nl > 0 ? kb + min(u, nl - 1) : 0;
             jj[u] = adj_col[k];
             ss[u] = adj_slot[k];
         }
+        dg = nl > 0 && jd == i;
+        no = nl - (dg ? 1 : 0);
+        cwd = Cw[sd];
+        l1d = loc1[sd];
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
+        for (int u = 0; u < NO; ++u) {
             cw[u] = Cw[ss[u]];
             l1[u] = loc1[ss[u]];
+            // entries past `no` read the own row again (cached) instead of another
+            const long oj = (long)(u < no ? jj[u] : ic) * ld + lane * E;
+            ld_row<E>(R + oj, xj[u]);
+            ld_row<E>(Gc + oj, nbr[u].g);
+            ld_row<E>(s0 + oj, nbr[u].a0); ld_row<E>(y0 + oj, nbr[u].b0);
+            ld_row<E>(s1 + oj, nbr[u].a1); ld_row<E>(y1 + oj, nbr[u].b1);
         }
         // slots without a single local constraint read the row's own (spread, cached) index
         // instead of a common one: no hot line shared by every lane
         const int ispare = min(ic, m - 1);
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
+        for (int u = 0; u < NO; ++u) {
             const int ci = (int)l1[u].y >= 0 ? (int)l1[u].y : ispare;
             bq[u] = b[ci];
             cq[u] = cvs[ci];
             lq[u] = lam[ci];
         }
+        {
+            const int ci = (int)l1d.y >= 0 ? (int)l1d.y : ispare;
+            bd = b[ci];
+            cd = cvs[ci];
+            lmd = lam[ci];
+        }
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && threadIdx.x == 0 && xi[0] != 12345.678) g_phase_tmp[0][1] = wall_clock64();
-        if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && cw[0] != 12345.678)
+        if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && xj[0][0] != 12345.678 && bd != 12345.678)
             g_phase_tmp[0][2] = wall_clock64();
 #endif
     }
@@ -1845,12 +1890,12 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         own.eval(kc, yi);
         st_row<E>(D + oi, yi);
         // one lower entry (j, slot): sym(R D^T), D D^T, objective parts, local constraints
-        auto entry = [&](int j, int sl, const double (&xj)[E], const double (&yj)[E], double cwv, double2 l1v,
+        auto entry = [&](int j, int sl, const double (&xjv)[E], const double (&yj)[E], double cwv, double2 l1v,
                          double bv, double cv, double lv) {
             double d0 = 0.0, d1 = 0.0;
             if (j != i) {
 #pragma unroll
-                for (int e = 0; e < E; ++e) d0 += xi[e] * yj[e] + xj[e] * yi[e];
+                for (int e = 0; e < E; ++e) d0 += xi[e] * yj[e] + xjv[e] * yi[e];
                 d0 *= 0.5;
             } else {
 #pragma unroll
@@ -1881,33 +1926,20 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
                 r[1] = make_double2(q2, (-li) + (-rho) * bi);
             }
         };
-        // prefetched entries, U neighbour rows in flight at a time
+        // adjacency order: the off-diagonal lower entries, then the diagonal (the last)
 #pragma unroll
-        for (int u0 = 0; u0 < NB; u0 += U) {
-            if (u0 < np) {
-                double xj[U][E], yj[U][E];
-#pragma unroll
-                for (int v = 0; v < U; ++v) {
-                    // entries past np repeat the chunk's first (static indices only: a
-                    // runtime index would move jj[] to LDS)
-                    const long oj = (long)(u0 + v < np ? jj[u0 + v] : jj[u0]) * ld + lane * E;
-                    ld_row<E>(R + oj, xj[v]);
-                    DirRow<E> dj;
-                    dj.load(kc, Gc, s0, y0, s1, y1, oj);
-                    dj.eval(kc, yj[v]);
-                }
-#pragma unroll
-                for (int v = 0; v < U; ++v)
-                    if (u0 + v < np) entry(jj[u0 + v], ss[u0 + v], xj[v], yj[v], cw[u0 + v], l1[u0 + v], bq[u0 + v],
-                                           cq[u0 + v], lq[u0 + v]);
+        for (int u = 0; u < NO; ++u) {
+            if (u < no) {
+                double yj[E];
+                nbr[u].eval(kc, yj);
+                entry(jj[u], ss[u], xj[u], yj, cw[u], l1[u], bq[u], cq[u], lq[u]);
             }
         }
-        // entries beyond the prefetched ones
-        for (int k = kb + NB; k < ke; ++k) {
+        for (int k = kb + NO; k < kb + no; ++k) {
             const int j = adj_col[k], sl = adj_slot[k];
             const long oj = (long)j * ld + lane * E;
-            double xj[E], yj[E];
-            ld_row<E>(R + oj, xj);
+            double xjv[E], yj[E];
+            ld_row<E>(R + oj, xjv);
             DirRow<E> dj;
             dj.load(kc, Gc, s0, y0, s1, y1, oj);
             dj.eval(kc, yj);
@@ -1915,8 +1947,9 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
             const int ci = (int)l1v.y;
             double bv = 0.0, cv = 0.0, lv = 0.0;
             if (ci >= 0) { bv = b[ci]; cv = cvs[ci]; lv = lam[ci]; }
-            entry(j, sl, xj, yj, Cw[sl], l1v, bv, cv, lv);
+            entry(j, sl, xjv, yj, Cw[sl], l1v, bv, cv, lv);
         }
+        if (dg) entry(i, sd, xi, yi, cwd, l1d, bd, cd, lmd);
     }
     LRS_TS(0, 5);
     write_partials<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x);
@@ -1929,8 +1962,10 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
 }
 
 // B in the latency regime (k_it_b MODE 0): the control wave reduces A's (and G's)
-// partials and solves the line search while the row waves prefetch.
-template <int G, int E, int NB, int U>
+// partials and solves the line search while the row waves prefetch the row header, the
+// first NO off-diagonal entries (records and neighbour rows R_j, D_j) and the diagonal
+// entry's records; after the barrier only the tau-dependent arithmetic and the stores run.
+template <int G, int E, int NO>
 __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
@@ -1965,11 +2000,18 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     const bool valid = !ctrl_wave && i < n;
     const int ic = valid ? i : 0;
     const long oi = (long)ic * ld + lane * E;
-    int kb = 0, kl = 0, ke = 0, np = 0;
+    // row-wave prefetch state
+    int kb = 0, kl = 0, ke = 0, no = 0;
+    bool dg = false;
     double ri[E], di[E], go[E], sov[E], yov[E];
-    int jj[NB], ss[NB];
-    double sv[NB], bq[NB];
-    double2 s1v[NB], l1v[NB], ra[NB], rb[NB];
+    int ss[NO];
+    bool lw[NO];
+    double rjp[NO][E], djp[NO][E];
+    double sv[NO], bq[NO];
+    double2 s1v[NO], l1v[NO], ra[NO], rb[NO];
+    int sd = 0;
+    double svd = 0.0, bqd = 0.0;
+    double2 s1d = make_double2(0.0, -1.0), l1d = s1d, rad = make_double2(0.0, 0.0), rbd = rad;
     if (ctrl_wave) {
         // ---- control wave: line search (ALMLineSearch lorads_alm.c:266-333)
         double sA[7];
@@ -1985,6 +2027,9 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
             for (int v = 0; v < 7; ++v) red[v] = sA[v];
         }
         __builtin_amdgcn_wave_barrier();
+#ifdef LRS_PHASE_TIMING
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && sA[6] != 12345.678) g_phase_tmp[2][8] = wall_clock64();
+#endif
         line_search_t<true>(par, red[0], red[1], red + 2, ls);
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_phase_tmp[2][7] = wall_clock64();
@@ -1998,24 +2043,43 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
         ld_row<E>(D + oi, di);
         ld_row<E>(Gold + oi, go);
         if (two) { ld_row<E>(so + oi, sov); ld_row<E>(yo + oi, yov); }
-        np = valid ? min(ke - kb, NB) : 0;
+        const int nt = valid ? ke - kb : 0;
+        // the diagonal is the last lower entry (columns ascending); positions of the first
+        // NO + 1 entries, the off-diagonal ones picked after the diagonal test
+        const int kd = (valid && kl > kb) ? kl - 1 : 0;
+        const int jd = adj_col[kd];
+        sd = adj_slot[kd];
+        int ja[NO + 1], sa[NO + 1];
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int k = np > 0 ? kb + min(u, np - 1) : 0;
-            jj[u] = adj_col[k];
-            ss[u] = adj_slot[k];
+        for (int u = 0; u <= NO; ++u) {
+            const int k = nt > 0 ? kb + min(u, nt - 1) : 0;
+            ja[u] = adj_col[k];
+            sa[u] = adj_slot[k];
         }
+        dg = valid && kl > kb && jd == i;
+        no = nt - (dg ? 1 : 0);
+        const int pd = dg ? kl - 1 - kb : NO + 1;    // the diagonal's position among the first
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
+        for (int u = 0; u < NO; ++u) {
+            const bool past = u >= pd;
+            const int j = past ? ja[u + 1] : ja[u];
+            ss[u] = past ? sa[u + 1] : sa[u];
+            lw[u] = kb + u + (past ? 1 : 0) < kl;
+            const long oj = (long)(u < no ? j : ic) * ld + lane * E;
+            ld_row<E>(R + oj, rjp[u]);
+            ld_row<E>(D + oj, djp[u]);
             sv[u] = Craw[ss[u]];
             s1v[u] = slot1[ss[u]];
             l1v[u] = loc1[ss[u]];
         }
+        svd = Craw[sd];
+        s1d = slot1[sd];
+        l1d = loc1[sd];
         // slots without a single constraint read the row's own (spread, cached) index instead
         // of a common one: no hot line shared by every lane
         const int ispare = min(ic, m - 1);
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
+        for (int u = 0; u < NO; ++u) {
             const int c1 = (int)s1v[u].y >= 0 ? (int)s1v[u].y : ispare;
             const int cl = (int)l1v[u].y >= 0 ? (int)l1v[u].y : ispare;
             const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
@@ -2023,10 +2087,18 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
             rb[u] = r[1];
             bq[u] = b[cl];
         }
+        {
+            const int c1 = (int)s1d.y >= 0 ? (int)s1d.y : ispare;
+            const int cl = (int)l1d.y >= 0 ? (int)l1d.y : ispare;
+            const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
+            rad = r[0];
+            rbd = r[1];
+            bqd = b[cl];
+        }
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && threadIdx.x == 0 && ri[0] != 12345.678 && sv[0] != 12345.678)
             g_phase_tmp[2][5] = wall_clock64();
-        if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && ra[0].x != 12345.678)
+        if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && ra[0].x != 12345.678 && rjp[0][0] != 12345.678)
             g_phase_tmp[2][6] = wall_clock64();
 #endif
     }
@@ -2082,47 +2154,43 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
                 acc[9] += dd * dd;
             }
         };
+        // the off-diagonal entries in adjacency order (prefetched, then the rest), the diagonal last
 #pragma unroll
-        for (int u0 = 0; u0 < NB; u0 += U) {
-            if (u0 < np) {
-                double rj[U][E];
+        for (int u = 0; u < NO; ++u) {
+            if (u < no) {
+                double rj[E];
 #pragma unroll
-                for (int v = 0; v < U; ++v) {
-                    const long oj = (long)(u0 + v < np ? jj[u0 + v] : jj[u0]) * ld + lane * E;
-                    double dj[E];
-                    ld_row<E>(R + oj, rj[v]);
-                    ld_row<E>(D + oj, dj);
-#pragma unroll
-                    for (int e = 0; e < E; ++e) rj[v][e] += tau * dj[e];
-                }
-#pragma unroll
-                for (int v = 0; v < U; ++v) {
-                    const int u = u0 + v;
-                    if (u < np) entry(ss[u], kb + u < kl, rj[v], sv[u], s1v[u], ra[u], rb[u], l1v[u], bq[u]);
-                }
+                for (int e = 0; e < E; ++e) rj[e] = rjp[u][e] + tau * djp[u][e];
+                entry(ss[u], lw[u], rj, sv[u], s1v[u], ra[u], rb[u], l1v[u], bq[u]);
             }
         }
-        for (int k = kb + NB; k < ke; ++k) {
-            const int j = adj_col[k], sl = adj_slot[k];
-            const long oj = (long)j * ld + lane * E;
-            double rj[E], dj[E];
-            ld_row<E>(R + oj, rj);
-            ld_row<E>(D + oj, dj);
+        if (no > NO) {
+            int cnt = 0;
+            for (int k = kb; k < ke; ++k) {
+                if (dg && k == kl - 1) continue;
+                if (cnt++ < NO) continue;
+                const int j = adj_col[k], sl = adj_slot[k];
+                const long oj = (long)j * ld + lane * E;
+                double rj[E], dj[E];
+                ld_row<E>(R + oj, rj);
+                ld_row<E>(D + oj, dj);
 #pragma unroll
-            for (int e = 0; e < E; ++e) rj[e] += tau * dj[e];
-            const double2 s1u = slot1[sl];
-            const int c1 = (int)s1u.y;
-            double2 x = make_double2(0.0, 0.0), y = x;
-            if (c1 >= 0) {
-                const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
-                x = r[0];
-                y = r[1];
+                for (int e = 0; e < E; ++e) rj[e] += tau * dj[e];
+                const double2 s1u = slot1[sl];
+                const int c1 = (int)s1u.y;
+                double2 x = make_double2(0.0, 0.0), y = x;
+                if (c1 >= 0) {
+                    const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
+                    x = r[0];
+                    y = r[1];
+                }
+                const bool lower = k < kl;
+                const double2 l1u = lower ? loc1[sl] : make_double2(0.0, -1.0);
+                const int cl = (int)l1u.y;
+                entry(sl, lower, rj, Craw[sl], s1u, x, y, l1u, cl >= 0 ? b[cl] : 0.0);
             }
-            const bool lower = k < kl;
-            const double2 l1u = lower ? loc1[sl] : make_double2(0.0, -1.0);
-            const int cl = (int)l1u.y;
-            entry(sl, lower, rj, Craw[sl], s1u, x, y, l1u, cl >= 0 ? b[cl] : 0.0);
         }
+        if (dg) entry(sd, true, ri, svd, s1d, rad, rbd, l1d, bqd);
         // gradient G_new = 2 S R_new, L-BFGS pair s = tau D, y = G_new - G_old, dots
         double sv2[E], yv[E];
 #pragma unroll
@@ -2669,16 +2737,16 @@ static int plan_b(const DevCone &c, int K, StagePlan &p) {
 // Latency-regime kernels (k_lat_a / k_lat_b): one row per lane group, every group
 // resident, no teams (T == 1), and each stage's producer partials within one control
 // wave's reach.  NB (prefetched entries) from the most entries of one row.
-constexpr int kLatNbA = 4, kLatUA = 2, kLatNbB = 6, kLatUB = 3;
+constexpr int kLatNoA = 2, kLatNoB = 4;   // off-diagonal entries prefetched (A: lower, B: all)
 template <int GG, int EE>
 static int res_la() {
     static int c = 0;
-    return resident_blocks(k_lat_a<GG, EE, kLatNbA, kLatUA>, &c);
+    return resident_blocks(k_lat_a<GG, EE, kLatNoA>, &c);
 }
 template <int GG, int EE>
 static int res_lb() {
     static int c = 0;
-    return resident_blocks(k_lat_b<GG, EE, kLatNbB, kLatUB>, &c);
+    return resident_blocks(k_lat_b<GG, EE, kLatNoB>, &c);
 }
 static bool lat_disabled() {
     static int v = -1;
@@ -2817,7 +2885,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        pstr)
         if (lat) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                hipLaunchKernelGGL((k_lat_a<GG, EE, kLatNbA, kLatUA>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
+                hipLaunchKernelGGL((k_lat_a<GG, EE, kLatNoA>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
                                    c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D,
                                    W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr,
                                    P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam,
@@ -2873,7 +2941,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const bool small = pb[k].small;
         if (lat) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                hipLaunchKernelGGL((k_lat_b<GG, EE, kLatNbB, kLatUB>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
+                hipLaunchKernelGGL((k_lat_b<GG, EE, kLatNoB>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
                                    c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0],
                                    W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
                                    P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con,
