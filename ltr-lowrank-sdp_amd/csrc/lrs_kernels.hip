@@ -1680,29 +1680,37 @@ constexpr int kLatRows = kLatRowWaves * 64;      // row-wave threads per block
 constexpr int kLatMaxPartials = 256;             // producer blocks one control wave reduces
 
 // control wave: NV partial vectors summed over 1 <= nblk <= kLatMaxPartials producer blocks
-// (lane l takes blocks l, l+64, ...).  Every load is issued before the first sum (loads
-// clamped, not branched), so the wave waits for one memory trip; wave-uniform result.
+// (lane l takes blocks l, l+64, ...).  Split in two so that the loads can be issued first
+// thing in the kernel (clamped, not branched): the wave then waits for one memory trip.
+constexpr int kLatQ = kLatMaxPartials / 64;
 template <int NV>
-__device__ __forceinline__ void wave_reduce_partials(const double *__restrict__ part, int nblk, double (&out)[NV]) {
-    constexpr int Q = kLatMaxPartials / 64;
+__device__ __forceinline__ void load_partials(const double *__restrict__ part, int nblk, double (&x)[kLatQ][NV]) {
     const int lane = threadIdx.x & 63;
-    double x[Q][NV];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
+    for (int q = 0; q < kLatQ; ++q) {
         const int bc = min(lane + 64 * q, nblk - 1);
 #pragma unroll
         for (int v = 0; v < NV; ++v) x[q][v] = part[v * kMaxPartialBlocks + bc];
     }
-#ifndef LRS_LAT_SERIAL_RED
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+}
+// wave-uniform sums of what load_partials fetched
+template <int NV>
+__device__ __forceinline__ void sum_partials(const double (&x)[kLatQ][NV], int nblk, double (&out)[NV]) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         double a = 0.0;
 #pragma unroll
-        for (int q = 0; q < Q; ++q) a += (lane + 64 * q < nblk) ? x[q][v] : 0.0;
+        for (int q = 0; q < kLatQ; ++q) a += (lane + 64 * q < nblk) ? x[q][v] : 0.0;
         out[v] = wave_sum(a);
     }
+}
+template <int NV>
+__device__ __forceinline__ void wave_reduce_partials(const double *__restrict__ part, int nblk, double (&out)[NV]) {
+    double x[kLatQ][NV];
+    load_partials<NV>(part, nblk, x);
+    __builtin_amdgcn_sched_barrier(0);
+    sum_partials<NV>(x, nblk, out);
 }
 
 // A in the latency regime (k_it_a MODE 0).  NO: off-diagonal lower entries whose operand
@@ -1727,6 +1735,10 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     LRS_TS(0, 0);
     LRS_BLK_BEGIN();
     const bool ctrl_wave = (int)(threadIdx.x >> 6) == kLatRowWaves;
+    // control wave: the previous stage's partials first of all (used only when folding), so
+    // that their memory trip overlaps the one of the control words
+    double px[kLatQ][10];
+    if (ctrl_wave) load_partials<10>(partC, nblkC, px);
     // this iteration's operands: ctrl_step folds the previous stage (and flips the G and R
     // buffers) exactly when `fold` holds
     const double lsflag = ls_prev[LS_FLAG];
@@ -1766,7 +1778,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         for (int q = 0; q < C_NCTRL; ++q) cc[q] = ctrl_prev[q];
         double s[10];
         if (fold) {
-            wave_reduce_partials<10>(partC, nblkC, s);
+            sum_partials<10>(px, nblkC, s);
         } else {
 #pragma unroll
             for (int v = 0; v < 10; ++v) s[v] = 0.0;
@@ -1981,6 +1993,13 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     __shared__ double ls[LS_N];
     LRS_TS(2, 0);
     LRS_BLK_BEGIN();
+    const bool ctrl_wave = (int)(threadIdx.x >> 6) == kLatRowWaves;
+    // control wave: A's (and G's) partials first of all
+    double pa[kLatQ][7], pb[kLatQ][5];
+    if (ctrl_wave) {
+        load_partials<7>(partA, nblkA, pa);
+        if (nblkB > 0) load_partials<5>(partB, nblkB, pb);
+    }
     if (ctrl[C_ACT2] == 0.0) return;
     const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
     const bool r1 = ctrl[C_RCUR] != 0.0;
@@ -1994,7 +2013,6 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
     const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
     const bool two = (L == 2);
-    const bool ctrl_wave = (int)(threadIdx.x >> 6) == kLatRowWaves;
     const int lane = threadIdx.x & (G - 1);
     const int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G;
     const bool valid = !ctrl_wave && i < n;
@@ -2015,10 +2033,10 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     if (ctrl_wave) {
         // ---- control wave: line search (ALMLineSearch lorads_alm.c:266-333)
         double sA[7];
-        wave_reduce_partials<7>(partA, nblkA, sA);
+        sum_partials<7>(pa, nblkA, sA);
         if (nblkB > 0) {
             double sB[5];
-            wave_reduce_partials<5>(partB, nblkB, sB);
+            sum_partials<5>(pb, nblkB, sB);
 #pragma unroll
             for (int q = 0; q < 5; ++q) sA[2 + q] += sB[q];
         }
