@@ -208,6 +208,8 @@ struct AlmIterArgs {
     const DevProblem *P;
     DevWork *W;
     hipEvent_t *ev;    // optional: 5 events recorded before S1..S4 and after S4
+    double *hmirror = nullptr;   // optional: device pointer of a pinned host slot; stage B
+    double seq = 0;              // mirrors the control block there, then writes seq after it
 };
 // Four launches per inner iteration (lrs_kernels.hip "split iteration").
 int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st);

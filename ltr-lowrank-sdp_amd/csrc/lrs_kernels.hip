@@ -823,7 +823,7 @@ __device__ int dev_cubic(double a, double b, double c, double d, double *res) {
 
 // Same as dev_cubic, executed by a whole wave (uniform result): the two independent
 // cube roots of the delta > 0 branch run on lanes 0 and 1 at once.
-__device__ int dev_cubic_wave(double a, double b, double c, double d, double *res) {
+__device__ __forceinline__ int dev_cubic_wave(double a, double b, double c, double d, double *res) {
     const double A = b * b - 3 * a * c, B = b * c - 9 * a * d, C = c * c - 3 * b * d;
     const double delta = B * B - 4 * A * C;
     res[0] = res[1] = res[2] = 0.0;
@@ -948,7 +948,7 @@ __device__ __forceinline__ void reduce_partials(const double *__restrict__ part,
 // ALMLineSearch (lorads_alm.c:266-333) from reduced values: p1, p2 objective parts
 // (p1 before its factor 2), dots = {q2q2, q1q2, q0q2, q1q1, q0q1}.
 template <bool WAVE>
-__device__ void line_search_t(const double *__restrict__ par, double p1, double p2, const double *dots, double *ls) {
+__device__ __forceinline__ void line_search_t(const double *__restrict__ par, double p1, double p2, const double *dots, double *ls) {
     p1 *= 2.0;
     const double rho = par[P_RHO];
     const double a = rho * dots[0] / 2;
@@ -1005,7 +1005,7 @@ __device__ __forceinline__ void ctrl_step(double *c, const double *__restrict__ 
             const double beta = 1.0 / d[1];
             if (h == 0) { c[C_BETA0] = beta; c[C_YY0] = d[2]; }
             else { c[C_BETA1] = beta; c[C_YY1] = d[2]; }
-            c[C_HEAD] = (double)((h + 1) % L);
+            c[C_HEAD] = (double)(h + 1 >= L ? 0 : h + 1);
             c[C_GCUR] = 1.0 - c[C_GCUR];
             c[C_LAG] = d[0];
             c[C_LASTTAU] = lstau;
@@ -1044,14 +1044,14 @@ __device__ __forceinline__ void ctrl_step(double *c, const double *__restrict__ 
     }
     if (c[C_ACTIVE] != 0.0) {
         // LBFGSDirection (lorads_alm.c:468-505) in coefficient space
-        if (((long)c[C_LOCAL]) % 300 == 0) c[C_CLEAR] = 0;
+        if (((int)c[C_LOCAL]) % 300 == 0) c[C_CLEAR] = 0;   // localIter <= 801
         const int clear = (int)c[C_CLEAR];
         const int nodeNum = clear == 0 ? 0 : (clear <= L - 1 ? clear : L);
         c[C_NODENUM] = nodeNum;
         const double GG = c[C_LAG];
         const double sG = c[C_DSG], yG = c[C_DYG], soG = c[C_DSOG], yoG = c[C_DYOG], soy = c[C_DSOY],
                      yoy = c[C_DYOY];
-        const int hn = ((int)c[C_HEAD] - 1 + L) % L;     // newest slot
+        const int hn = (int)c[C_HEAD] == 0 ? L - 1 : (int)c[C_HEAD] - 1;     // newest slot
         double cs0 = 0, cs1 = 0, cy0 = 0, cy1 = 0;
         double dg;
         if (nodeNum == 0) {
@@ -1082,6 +1082,15 @@ __device__ __forceinline__ void ctrl_step(double *c, const double *__restrict__ 
         c[C_PENDING] = 1.0;
     }
     if (ph1) { c[C_ACT2] = c[C_ACTIVE]; c[C_EXIT2] = c[C_EXIT]; }
+}
+
+// Batch-end mirror of the control block into pinned host memory (run_inner polls it
+// instead of a device-to-host copy and a stream synchronisation): the first wave of block 0
+// stores the NCTRL words, then the sequence number with a system-scope release.
+__device__ __forceinline__ void mirror_ctrl(const double *__restrict__ ctrl, double *hm, double seq) {
+    if (hm == nullptr || blockIdx.x != 0 || threadIdx.x >= 64) return;
+    if (threadIdx.x < C_NCTRL) hm[threadIdx.x] = ctrl[threadIdx.x];
+    if (threadIdx.x == 0) __hip_atomic_store(hm + C_NCTRL, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 struct DirCoef {
@@ -1418,13 +1427,14 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_
     const double *__restrict__ b, double *__restrict__ cvs, const double *__restrict__ par,
     const double *__restrict__ ctrl, const double *__restrict__ partA, int nblkA, const double *__restrict__ partB,
     int nblkB, double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int T, int row0,
-    int nall, int pstr) {
+    int nall, int pstr, double *hmirror, double seq) {
     __shared__ double gsh[kRowBlock * E];   // team reduction of the row gradient (T > 1)
     __shared__ double red[12];
     __shared__ double ls[LS_N];
     __shared__ double cs[4];
     LRS_TS(2, 0);
     LRS_BLK_BEGIN();
+    if constexpr (MODE != 2) mirror_ctrl(ctrl, hmirror, seq);
     if (threadIdx.x == 0) { cs[0] = ctrl[C_ACT2]; cs[1] = ctrl[C_GCUR]; cs[2] = ctrl[C_HEAD]; cs[3] = ctrl[C_RCUR]; }
     __syncthreads();
     if (cs[0] == 0.0) return;
@@ -1732,13 +1742,30 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev, const double *__restrict__ partC, int nblkC,
     double *__restrict__ partA, int pblk_off, int gwide) {
     __shared__ double c[C_NCTRL];
+    __shared__ double pl[P_NPAR];
     LRS_TS(0, 0);
     LRS_BLK_BEGIN();
-    const bool ctrl_wave = (int)(threadIdx.x >> 6) == kLatRowWaves;
-    // control wave: the previous stage's partials first of all (used only when folding), so
-    // that their memory trip overlaps the one of the control words
-    double px[kLatQ][10];
-    if (ctrl_wave) load_partials<10>(partC, nblkC, px);
+    const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == kLatRowWaves;   // wave-uniform
+    const int lane = threadIdx.x & (G - 1);
+    const int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G;
+    const bool valid = !ctrl_wave && i < n;
+    const int ic = valid ? i : 0;
+    // every load that needs nothing else goes out first, so that its memory trip overlaps
+    // the one of the control words: the control wave's partials (used only when folding),
+    // control block and parameters; the row waves' row header
+    // (control block and parameters one word per lane: two vector loads, broadcast later)
+    double px[kLatQ][10], ccv = 0.0, pvv = 0.0;
+    int kb = 0, ke = 0;
+    if (ctrl_wave) {
+        load_partials<10>(partC, nblkC, px);
+        const int l64 = threadIdx.x & 63;
+        ccv = ctrl_prev[min(l64, C_NCTRL - 1)];
+        pvv = par[min(l64, P_NPAR - 1)];
+    } else {
+        kb = adj_ptr[ic];
+        ke = adj_low[ic];
+    }
+    __builtin_amdgcn_sched_barrier(0);
     // this iteration's operands: ctrl_step folds the previous stage (and flips the G and R
     // buffers) exactly when `fold` holds
     const double lsflag = ls_prev[LS_FLAG];
@@ -1750,16 +1777,12 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     const double *__restrict__ s0 = s0a + foff, *__restrict__ y0 = y0a + foff;
     const double *__restrict__ s1 = s1a + foff, *__restrict__ y1 = y1a + foff;
     double *__restrict__ D = Dall + foff;
-    const int lane = threadIdx.x & (G - 1);
-    const int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G;
-    const bool valid = !ctrl_wave && i < n;
-    const int ic = valid ? i : 0;
     const long oi = (long)ic * ld + lane * E;
     // row-wave prefetch state: own operands, the NO off-diagonal entries (records and the
     // neighbours' direction operands), the diagonal entry's records
     DirRow<E> own;
     double xi[E];
-    int kb = 0, no = 0;
+    int no = 0;
     bool dg = false;
     int jj[NO], ss[NO];
     double cw[NO], bq[NO], cq[NO], lq[NO];
@@ -1773,9 +1796,8 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         // ---- control wave: the previous stage's dots, then the control of this iteration;
         // every lane runs ctrl_step on a register copy (uniform values), lane 0 publishes it
         const int l64 = threadIdx.x & 63;
-        double cc[C_NCTRL];
-#pragma unroll
-        for (int q = 0; q < C_NCTRL; ++q) cc[q] = ctrl_prev[q];
+        if (l64 < C_NCTRL) c[l64] = ccv;
+        if (l64 < P_NPAR) pl[l64] = pvv;
         double s[10];
         if (fold) {
             sum_partials<10>(px, nblkC, s);
@@ -1784,21 +1806,15 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
             for (int v = 0; v < 10; ++v) s[v] = 0.0;
         }
 #ifdef LRS_PHASE_TIMING
-        if (blockIdx.x == 0 && l64 == 0 && s[9] != 12345.678 && cc[5] != 12345.678) g_phase_tmp[0][8] = wall_clock64();
+        if (blockIdx.x == 0 && l64 == 0 && s[9] != 12345.678 && ccv != 12345.678) g_phase_tmp[0][8] = wall_clock64();
 #endif
-        ctrl_step(cc, par, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
-        if (l64 == 0) {
-#pragma unroll
-            for (int q = 0; q < C_NCTRL; ++q) c[q] = cc[q];
-        }
+        if (l64 == 0) ctrl_step(c, pl, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && l64 == 0) g_phase_tmp[0][7] = wall_clock64();
 #endif
     } else {
         // ---- row waves: every load the control does not decide, one memory trip per
         // dependency level; loads clamped to valid addresses instead of branched
-        kb = adj_ptr[ic];
-        const int ke = adj_low[ic];
         ld_row<E>(Gc + oi, own.g);
         ld_row<E>(s0 + oi, own.a0); ld_row<E>(y0 + oi, own.b0);
         ld_row<E>(s1 + oi, own.a1); ld_row<E>(y1 + oi, own.b1);
@@ -1988,18 +2004,33 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
     const double *__restrict__ partA, int nblkA, const double *__restrict__ partB, int nblkB,
-    double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m) {
+    double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m, double *hmirror,
+    double seq) {
     __shared__ double red[12];
     __shared__ double ls[LS_N];
+    __shared__ double pl[P_NPAR];
     LRS_TS(2, 0);
     LRS_BLK_BEGIN();
-    const bool ctrl_wave = (int)(threadIdx.x >> 6) == kLatRowWaves;
-    // control wave: A's (and G's) partials first of all
-    double pa[kLatQ][7], pb[kLatQ][5];
+    mirror_ctrl(ctrl, hmirror, seq);
+    const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == kLatRowWaves;   // wave-uniform
+    const int lane = threadIdx.x & (G - 1);
+    const int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G;
+    const bool valid = !ctrl_wave && i < n;
+    const int ic = valid ? i : 0;
+    // loads that need nothing else first: the control wave's partials (A's, and G's) and
+    // parameters, the row waves' row header
+    double pa[kLatQ][7], pb[kLatQ][5], pvv = 0.0;
+    int kb = 0, kl = 0, ke = 0;
     if (ctrl_wave) {
         load_partials<7>(partA, nblkA, pa);
         if (nblkB > 0) load_partials<5>(partB, nblkB, pb);
+        pvv = par[min((int)(threadIdx.x & 63), P_NPAR - 1)];
+    } else {
+        kb = adj_ptr[ic];
+        kl = adj_low[ic];
+        ke = adj_ptr[ic + 1];
     }
+    __builtin_amdgcn_sched_barrier(0);
     if (ctrl[C_ACT2] == 0.0) return;
     const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
     const bool r1 = ctrl[C_RCUR] != 0.0;
@@ -2013,13 +2044,9 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
     const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
     const bool two = (L == 2);
-    const int lane = threadIdx.x & (G - 1);
-    const int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G;
-    const bool valid = !ctrl_wave && i < n;
-    const int ic = valid ? i : 0;
     const long oi = (long)ic * ld + lane * E;
     // row-wave prefetch state
-    int kb = 0, kl = 0, ke = 0, no = 0;
+    int no = 0;
     bool dg = false;
     double ri[E], di[E], go[E], sov[E], yov[E];
     int ss[NO];
@@ -2048,15 +2075,14 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && sA[6] != 12345.678) g_phase_tmp[2][8] = wall_clock64();
 #endif
-        line_search_t<true>(par, red[0], red[1], red + 2, ls);
+        if ((threadIdx.x & 63) < P_NPAR) pl[threadIdx.x & 63] = pvv;
+        __builtin_amdgcn_wave_barrier();
+        line_search_t<true>(pl, red[0], red[1], red + 2, ls);
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_phase_tmp[2][7] = wall_clock64();
 #endif
     } else {
         // ---- row waves: prefetch, one memory trip per dependency level, clamped loads
-        kb = adj_ptr[ic];
-        kl = adj_low[ic];
-        ke = adj_ptr[ic + 1];
         ld_row<E>(R + oi, ri);
         ld_row<E>(D + oi, di);
         ld_row<E>(Gold + oi, go);
@@ -2955,7 +2981,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,                        \
                        reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,           \
                        reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, inA, nA, W.partB,   \
-                       P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, c.n, pstr)
+                       P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, c.n, pstr,                \
+                       (MM) != 2 && k == 0 ? a.hmirror : nullptr, a.seq)
         const bool small = pb[k].small;
         if (lat) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
@@ -2964,7 +2991,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
                                    P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con,
                                    P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur,
-                                   inA, nA, W.partB, P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, P.m);
+                                   inA, nA, W.partB, P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, P.m,
+                                   k == 0 ? a.hmirror : nullptr, a.seq);
             });
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -147,6 +148,10 @@ struct lrs_ctx {
     long st_calls = 0, st_batches = 0, st_iters = 0, st_nop = 0;
     double st_inner_s = 0;
     hipEvent_t pev[2][5] = {};
+    hipEvent_t bev[2] = {nullptr, nullptr};   // completion of the two batches in flight (run_inner)
+    int pipe_batch = 8;                         // iterations per pipelined batch (LRS_PIPE_BATCH)
+    double *hmir = nullptr, *dmir = nullptr;    // pinned control mirror [2][64] (host / device view)
+    double mseq = 0;                            // last sequence number handed to a batch
     double pacc[4] = {0, 0, 0, 0};
     long pn = 0;
     // MAX_ALM_SUB_ITER (lorads_alm.c:20): reset by the ALM phase, carried into reopt
@@ -869,7 +874,82 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     double *res = c->hpin + 128;
     const double t_in = c->stats ? now_s() : 0.0;
     long enq = 0;
-    for (;;) {
+    if (!c->prof) {
+        // Two batches in flight: batch k+1 is enqueued before the host waits for batch k, so
+        // the GPU never idles on the host's submission or on the wait's wake-up.  Each batch
+        // ends with a copy of the control block into its own pinned slot.  At the loop's exit
+        // the batch still in flight runs as no-op iterations (the kernels' fast exits) and
+        // leaves the state unchanged; later work on the stream is ordered after it.
+        // Eager launches: the batch's last stage B writes the control block and a sequence
+        // number into a pinned slot and the host spins on the number (no copy kernel, no
+        // stream synchronisation).  Graph replay: a copy into the slot and an event.
+        for (auto &e : c->bev)
+            if (!e) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        if (!c->hmir) {
+            HIPC(hipHostMalloc((void **)&c->hmir, 128 * sizeof(double), hipHostMallocCoherent));
+            HIPC(hipHostGetDevicePointer((void **)&c->dmir, c->hmir, 0));
+            for (int q = 0; q < 128; ++q) c->hmir[q] = -1.0;
+        }
+        const bool mirror = !c->use_graphs;
+        long k = 0, kw = 0;
+        double bseq[2] = {0, 0};
+        auto enqueue = [&](int Bk) -> int {
+            if (c->use_graphs) {
+                hipGraphExec_t ge;
+                if (get_batch_graph(c, Bk, &ge)) return -1;
+                HIPC(hipGraphLaunch(ge, c->st));
+                HIPC(hipMemcpyAsync(c->hpin + 128 + 64 * (k & 1), c->W.ctrl + C_NCTRL, sizeof(double) * C_NCTRL,
+                                    hipMemcpyDeviceToHost, c->st));
+                HIPC(hipEventRecord(c->bev[k & 1], c->st));
+            } else {
+                bseq[k & 1] = (c->mseq += 1.0);
+                for (int j = 0; j < Bk; ++j) {
+                    a.hmirror = (j == Bk - 1) ? c->dmir + 64 * (k & 1) : nullptr;
+                    a.seq = bseq[k & 1];
+                    OPC(enqueue_alm_iteration(a, j & 1, c->st));
+                }
+                a.hmirror = nullptr;
+            }
+            ++k;
+            enq += Bk;
+            if (c->stats) c->st_batches++;
+            return 0;
+        };
+        // small fixed batches: the batch in flight at the exit bounds the no-op iterations,
+        // and one batch of GPU work outlasts the host's submission of the next
+        const int Bp = c->pipe_batch;
+        if (enqueue(std::min(Bp, even_clamp(certain - enq)))) return -1;
+        for (;;) {
+            if (enq < certain) {
+                if (enqueue(std::min(Bp, even_clamp(certain - enq)))) return -1;
+            }
+            if (mirror) {
+                volatile double *slot = c->hmir + 64 * (kw & 1);
+                const double t_w = now_s();
+                long spins = 0;
+                while (slot[C_NCTRL] != bseq[kw & 1]) {
+                    if ((++spins & 0xFFFF) == 0) {
+                        if (hipStreamQuery(c->st) == hipSuccess && slot[C_NCTRL] != bseq[kw & 1]) {
+                            set_err("control mirror not written by the batch");
+                            return -1;
+                        }
+                        if (now_s() - t_w > 600.0) { set_err("inner-loop batch timed out"); return -1; }
+                    }
+                }
+                std::atomic_thread_fence(std::memory_order_acquire);
+                for (int q = 0; q < C_NCTRL; ++q) c->hpin[128 + 64 * (kw & 1) + q] = slot[q];
+            } else {
+                HIPC(hipEventSynchronize(c->bev[kw & 1]));
+            }
+            res = c->hpin + 128 + 64 * (kw & 1);
+            ++kw;
+            if (res[C_ACT2] == 0.0) break;
+            if (kw == k) {   // still active past the certain exits (cannot happen): keep going
+                if (enqueue(even_clamp(8))) return -1;
+            }
+        }
+    }
+    for (; c->prof;) {
         B = std::min(B, even_clamp(certain - enq));
         enq += B;
         if (c->prof) {
@@ -1485,6 +1565,7 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); delete c; return -1; }
     if (const char *ug = getenv("LRS_GRAPHS")) c->use_graphs = (atoi(ug) != 0);
     if (const char *sv = getenv("LRS_STATS")) c->stats = (atoi(sv) != 0);
+    if (const char *pb = getenv("LRS_PIPE_BATCH")) c->pipe_batch = std::max(2, std::min(64, (atoi(pb) + 1) & ~1));
     if (hipHostMalloc((void **)&c->hpin, 4096 * sizeof(double), 0) != hipSuccess) { set_err("pinned alloc failed"); delete c; return -1; }
     if (hipMalloc((void **)&c->s_tickets, 64 * sizeof(unsigned)) != hipSuccess ||
         hipMemset(c->s_tickets, 0, 64 * sizeof(unsigned)) != hipSuccess ||
@@ -1533,6 +1614,9 @@ void lrs_ctx_destroy(lrs_ctx *c) {
     free_work(c);
     if (c->loaded) free_problem(c->dp);
     if (c->hpin) (void)hipHostFree(c->hpin);
+    if (c->hmir) (void)hipHostFree(c->hmir);
+    for (auto &e : c->bev)
+        if (e) (void)hipEventDestroy(e);
     delete c->comm;
     for (void *q : {(void *)c->s_tickets, (void *)c->s_tmpfin, (void *)c->s_rpart, (void *)c->d_send_rows,
                     (void *)c->d_sendbuf, (void *)c->Cw0, (void *)c->Craw0})

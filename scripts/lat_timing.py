@@ -41,3 +41,23 @@ for kp in (0, 1):
             print(f"  K{name}: blocks {len(v)}, first entry -> last exit {(e - f) * 0.01:.2f} us, "
                   f"entry spread {(max(a for a, _ in v) - f) * 0.01:.2f} us, mean span {sum(b - a for a, b in v) / len(v) * 0.01:.2f} us")
     sv.close()
+
+# per-block span by XCD (blockIdx % 8) of the last real-loop iteration
+sv = solver.Solver(path)
+r = sv.determine_rank()[0]
+sv.alm_throughput(0, 300, fixedRank=r, reoptLevel=0)
+dbg = sv.debug_phase_times()
+if dbg:
+    ph, blk = dbg
+    for k, name in ((0, "A"), (2, "B")):
+        v = [(q, a, b) for q, (a, b) in enumerate(blk[k]) if a != 0 and b >= a]
+        if not v:
+            continue
+        f = min(a for _, a, _ in v)
+        by = {}
+        for q, a, b in v:
+            by.setdefault(q % 8, []).append(((a - f) * 0.01, (b - f) * 0.01))
+        print(f"K{name} per XCD: " + "  ".join(f"x{x}: exit mean {sum(e for _, e in l) / len(l):.2f} max {max(e for _, e in l):.2f}" for x, l in sorted(by.items())))
+        worst = sorted(v, key=lambda t: -t[2])[:8]
+        print(f"K{name} slowest blocks:", [(q, round((b - f) * 0.01, 2)) for q, a, b in worst])
+sv.close()
