@@ -10,11 +10,11 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-dst = os.path.join(ROOT, "profiles")
+dst = os.environ.get("PROF_DST") or os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
 
-lines = [f"# rocprofv3 summary `{tag}`", "", "## kernel trace (--kernel-trace --stats)", "",
+lines = [f"# rocprofv3 summary `{tag}`", "", "Command: `scripts/profile_r01.sh` (bench.py headline run; separate --pmc passes).", "", "## kernel trace (--kernel-trace --stats)", "",
          "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
     lines.append(f"| `{r['Name'][:60]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | "
@@ -31,11 +31,12 @@ for f, cname in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         pmc.setdefault(k, {})[cname] = (len(v), sum(v) / len(v))
 if pmc:
     lines += ["", "## HBM-side bytes per dispatch (separate --pmc passes; KB as reported, FETCH_SIZE uncorrected)", "",
-              "| kernel | dispatches | FETCH_SIZE KB | WRITE_SIZE KB |", "|---|---|---|---|"]
+              "| kernel | dispatches | FETCH_SIZE KB | x2 (gfx950 wide-read correction) KB | WRITE_SIZE KB |",
+              "|---|---|---|---|---|"]
     for k, d in sorted(pmc.items(), key=lambda kv: -kv[1].get("FETCH_SIZE", (0, 0))[1]):
         fz = d.get("FETCH_SIZE", (0, float("nan")))
         wz = d.get("WRITE_SIZE", (0, float("nan")))
-        lines.append(f"| `{k[:60]}` | {fz[0]} | {fz[1]:.1f} | {wz[1]:.1f} |")
+        lines.append(f"| `{k[:60]}` | {fz[0]} | {fz[1]:.1f} | {2 * fz[1]:.1f} | {wz[1]:.1f} |")
 for log in ("trace.log",):
     p = os.path.join(src, log)
     if os.path.exists(p):
