@@ -41,9 +41,28 @@ sys.path.insert(0, ROOT)
 PKG = "ltr-lowrank-sdp_amd"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec)
-STAGES = ("A: k_it_a (control, L-BFGS direction, SDDMM sym(RD^T)/DD^T, local q1/q2)",
+STAGES = ("A: {a} (control, L-BFGS direction, SDDMM sym(RD^T)/DD^T, local q1/q2)",
           "G: k_it_g (phase-1 test, multi-slot constraints' q1/q2)",
-          "B: k_it_b (line search, R+tau D, adjoint S=C+A*(M1), G=2SR, A(RR^T), L-BFGS pair)")
+          "B: {b} (line search, R+tau D, adjoint S=C+A*(M1), G=2SR, A(RR^T), L-BFGS pair)")
+# kernels per path (lrs_get_kernel_path): 0 latency-regime kernels, 1 general row kernels
+STAGE_KERNELS = {0: ("k_lat_a", "k_lat_b"), 1: ("k_it_a", "k_it_b")}
+
+
+def pmc_traffic(kernel):
+    """HBM-side bytes per dispatch of `kernel` from the newest committed rocprofv3 PMC
+    summary of this same bench run (profiles/<tag>_pmc.json, scripts/profile_r01.sh:
+    separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per MI355X_MICROARCH.md)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for k, v in d.items():
+            if k.split("<")[0].endswith(kernel):
+                return v["fetch_bytes"] + v["write_bytes"], v["source"]
+    return None, None
 
 
 def instance_for(rank_id, rows, cols, cache, seed0=67):
@@ -91,28 +110,35 @@ def cpu_reference_solve(path, flags, timeout):
     return {"solve_time_sec": float(m.group(1)), "process_wall_sec": wall, "alm_pobj": float(p.group(1))}
 
 
-def stage_roofline(sv, reps):
+def stage_roofline(sv, reps, with_traffic=False):
     """Per-launch ms of the split-iteration stages (back-to-back relaunches between two
     HIP events on the solver stream) and their algorithmic bytes -> GB/s."""
     ms = sv.time_stages(reps)
     by = sv.stage_bytes()
+    ka, kb = STAGE_KERNELS.get(sv.kernel_path(), STAGE_KERNELS[1])
     out = []
     for k in range(3):
         if ms[k] <= 0:
             continue
         gbs = by[k] / (ms[k] * 1e-3) / 1e9
-        out.append({"stage": STAGES[k], "avg_launch_us": ms[k] * 1e3, "bytes_per_launch": by[k],
-                    "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS})
+        out.append({"stage": STAGES[k].format(a=ka, b=kb), "kernel": (ka, "k_it_g", kb)[k],
+                    "avg_launch_us": ms[k] * 1e3, "bytes_per_launch": by[k], "achieved_GBs": gbs,
+                    "frac": gbs / HBM_PEAK_GBS})
     dom = max(out, key=lambda s: s["avg_launch_us"])
+    traffic, tsrc = pmc_traffic(dom["kernel"]) if with_traffic else (None, None)
     # the north-star's named operator: A(UU^T) straight from the constraint entries
     ams = sv.time_auut(reps)
     aby = sv.auut_bytes()
     agbs = aby / (ams * 1e-3) / 1e9
     auut = {"kernel": "k_auv_con<XX^T> (A(UU^T) over constraint entries)", "avg_launch_us": ams * 1e3,
             "bytes_per_launch": aby, "achieved_GBs": agbs, "frac": agbs / HBM_PEAK_GBS}
-    return {"bound": "hbm", "kernel": dom["stage"], "achieved": dom["achieved_GBs"], "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": dom["frac"], "traffic": None, "bytes_per_launch": dom["bytes_per_launch"],
-            "avg_launch_us": dom["avg_launch_us"], "stages": out, "a_uut": auut}
+    res = {"bound": "hbm", "kernel": dom["stage"], "achieved": dom["achieved_GBs"], "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": dom["frac"], "traffic": traffic, "bytes_per_launch": dom["bytes_per_launch"],
+           "avg_launch_us": dom["avg_launch_us"], "stages": out, "a_uut": auut}
+    if traffic is not None:
+        res["traffic_source"] = (f"{tsrc}: FETCH_SIZE x2 + WRITE_SIZE per dispatch (bytes); the x2 correction is "
+                                 "calibrated for 16-B/lane reads, these rows mix 16-B and 8-B loads")
+    return res
 
 
 def config_c5(solver, local, iters=20):
@@ -233,7 +259,7 @@ def main():
                    "flags": "--fixedRank %d --reoptLevel 0, phase-1 exit disabled, budget = steps" % r,
                    "parallelism": f"replicas x{world} (instance-level, weak)"},
         "alm_phase_rate": done / out["seconds"],
-        "roofline": stage_roofline(sv, 300),
+        "roofline": stage_roofline(sv, 300, with_traffic=True),
     }
     if rank_id == 0 and world == 1 and not args.no_eps:
         eps_flags = dict(reoptLevel=0, heuristicFactor=10.0, phase1Tol=1e-2, phase2Tol=1e-5)
