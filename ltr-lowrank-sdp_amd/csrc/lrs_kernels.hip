@@ -2273,6 +2273,254 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
 }
 
 // ------------------------------------------------------------------------
+// Bandwidth regime, long rows (a random sparse SDP has ~10^3 pattern entries per row): the
+// neighbour halves of stages A and B (k_it_a / k_it_b MODE 2) with the per-entry metadata
+// fetched lane-parallel -- a lane group takes G entries of its row at a time and every lane
+// gathers one entry's column, slot and records (three memory trips for G entries instead
+// of three per entry) -- then the entries' factor rows U at a time, the column broadcast
+// from the lane that fetched it, which also stores the entry's results.
+// ------------------------------------------------------------------------
+template <int G>
+__device__ __forceinline__ int bcast_i(int v, int u) {
+    if constexpr (G == 64) return __builtin_amdgcn_readlane(v, u);
+    else return __shfl(v, (int)(threadIdx.x & 63 & ~(G - 1)) + u, 64);
+}
+template <int G>
+__device__ __forceinline__ double bcast_d(double v, int u) {
+    if constexpr (G == 64) return read_lane(v, u);
+    else return __shfl(v, (int)(threadIdx.x & 63 & ~(G - 1)) + u, 64);
+}
+
+// A, second half (SDDMM sym(RD^T), DD^T on the lower slots, local constraints' q1/q2 and
+// dots), D read back; partials 0..6 as k_it_a MODE 2
+template <int G, int E, int U>
+__global__ void __launch_bounds__(kRowBlock) k_wide_a(
+    int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
+    const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
+    const double *__restrict__ Rb0, const double *__restrict__ Rb1, const double *__restrict__ Dall,
+    double *__restrict__ uRD, double *__restrict__ uDD, const int *__restrict__ loc_ptr,
+    const int *__restrict__ loc_con, const double *__restrict__ loc_w, const double2 *__restrict__ loc1,
+    const double *__restrict__ b, const double *__restrict__ cvs, const double *__restrict__ lam,
+    double *__restrict__ rec, const double *__restrict__ par, const double *__restrict__ ctrl_cur,
+    double *__restrict__ partA, int pblk_off, int row0, int m) {
+    if (ctrl_cur[C_ACTIVE] == 0.0) return;
+    const double *__restrict__ R = (ctrl_cur[C_RCUR] == 0.0 ? Rb0 : Rb1) + foff;
+    const double *__restrict__ D = Dall + foff;
+    const double rho = par[P_RHO], rhoInv = 1.0 / rho;
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kRowBlock / G;
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = row0 + grp; i < row0 + n; i += ngrp) {
+        const long oi = (long)i * ld + lane * E;
+        double xi[E], yi[E];
+        ld_row<E>(R + oi, xi);
+        ld_row<E>(D + oi, yi);
+        const int kb = adj_ptr[i], ke = adj_low[i];
+        const int ispare = min(i, m - 1);
+        for (int c0 = kb; c0 < ke; c0 += G) {
+            // this lane's entry of the chunk: column, slot, records
+            const int kc = c0 + lane < ke ? c0 + lane : c0;
+            const int jl = adj_col[kc], sl = adj_slot[kc];
+            const double cwl = Cw[sl];
+            const double2 l1l = loc1[sl];
+            const int cil = (int)l1l.y >= 0 ? (int)l1l.y : ispare;
+            const double bl = b[cil], cvl = cvs[cil], lml = lam[cil];
+            const int nc = min(G, ke - c0);
+            for (int u0 = 0; u0 < nc; u0 += U) {
+                double xj[U][E], yj[U][E];
+#pragma unroll
+                for (int v = 0; v < U; ++v) {
+                    const int j = bcast_i<G>(jl, min(u0 + v, nc - 1));
+                    const long oj = (long)j * ld + lane * E;
+                    ld_row<E>(R + oj, xj[v]);
+                    ld_row<E>(D + oj, yj[v]);
+                }
+#pragma unroll
+                for (int v = 0; v < U; ++v) {
+                    const int u = u0 + v;
+                    if (u >= nc) break;
+                    const int j = bcast_i<G>(jl, u);
+                    double d0 = 0.0, d1 = 0.0;
+                    if (j != i) {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) d0 += xi[e] * yj[v][e] + xj[v][e] * yi[e];
+                        d0 *= 0.5;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) d0 += xi[e] * yi[e];
+                    }
+#pragma unroll
+                    for (int e = 0; e < E; ++e) d1 += yi[e] * yj[v][e];
+                    d0 = group_sum<G>(d0);
+                    d1 = group_sum<G>(d1);
+                    if (lane == u) {
+                        uRD[sl] = d0;
+                        uDD[sl] = d1;
+                        acc[0] += cwl * d0;
+                        acc[1] += cwl * d1;
+                        // local constraints on this slot (ALMCalq12p12 lorads_alm.c:714-734)
+                        const int c1 = (int)l1l.y;
+                        const int e0 = c1 == -2 ? loc_ptr[sl] : 0, e1 = c1 == -2 ? loc_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
+                        for (int e = e0; e < e1; ++e) {
+                            const int ci = c1 >= 0 ? c1 : loc_con[e];
+                            const double w = c1 >= 0 ? l1l.x : loc_w[e];
+                            const double bi = c1 >= 0 ? bl : b[ci], cvi = c1 >= 0 ? cvl : cvs[ci];
+                            const double li = c1 >= 0 ? lml : lam[ci];
+                            const double q1 = 2.0 * (w * d0), q2 = w * d1;
+                            const double q0 = (bi - cvi) + rhoInv * li;
+                            acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1;
+                            acc[6] += q0 * q1;
+                            double2 *r = reinterpret_cast<double2 *>(rec + 4L * ci);
+                            r[0] = make_double2(cvi, q1);
+                            r[1] = make_double2(q2, (-li) + (-rho) * bi);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    write_partials_range<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x, 0, 7);
+}
+
+// B, second half (adjoint S = C + A^*(M1), G = 2 S R_new, A(R_new R_new^T) on the lower
+// slots, L-BFGS pair, nine dots + residual) over the updated factor; as k_it_b MODE 2
+template <int G, int E, int U>
+__global__ void __launch_bounds__(kRowBlock) k_wide_b(
+    int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
+    const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *Rb0, const double *Rb1,
+    const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0, double *s1, double *y1,
+    double *__restrict__ uRR, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
+    const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double2 *__restrict__ slot1,
+    const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
+    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
+    double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
+    const double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int row0, int m) {
+    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
+    const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
+    const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
+    const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
+    const double *__restrict__ D = Dall + foff;
+    const double *__restrict__ Gold = (gcur == 0 ? G0 : G1) + foff;
+    double *__restrict__ Gnew = (gcur == 0 ? G1 : G0) + foff;
+    double *__restrict__ sh = (h == 0 ? s0 : s1) + foff;
+    double *__restrict__ yh = (h == 0 ? y0 : y1) + foff;
+    const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
+    const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
+    const bool two = (L == 2);
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kRowBlock / G;
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = row0 + grp; i < row0 + n; i += ngrp) {
+        const long oi = (long)i * ld + lane * E;
+        double ri[E], g[E];
+        ld_row<E>(Rn + oi, ri);
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[e] = 0.0;
+        const int kb = adj_ptr[i], kl = adj_low[i], ke = adj_ptr[i + 1];
+        const int ispare = min(i, m - 1);
+        for (int c0 = kb; c0 < ke; c0 += G) {
+            // this lane's entry: column, slot, S = C + A^*(M1) on the slot (ALMSetGrad
+            // lorads_alm.c:38-57 with M1 formed from rec), its local constraint records
+            const int kc = c0 + lane < ke ? c0 + lane : c0;
+            const int jl = adj_col[kc], sl = adj_slot[kc];
+            double svl = Craw[sl];
+            const double2 s1l = slot1[sl];
+            const int c1 = (int)s1l.y;
+            {
+                const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * (c1 >= 0 ? c1 : ispare));
+                const double2 ra = r[0], rb = r[1];
+                if (c1 >= 0) {
+                    double cv = ra.x + tau * ra.y;
+                    cv = cv + tau2 * rb.x;
+                    svl += (rb.y + rho * cv) * s1l.x;
+                } else if (c1 == -2) {
+                    for (int e = slot_ptr[sl]; e < slot_ptr[sl + 1]; ++e) {
+                        const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
+                        const double2 x = q[0], y = q[1];
+                        double cv = x.x + tau * x.y;
+                        cv = cv + tau2 * y.x;
+                        svl += (y.y + rho * cv) * slot_a[e];
+                    }
+                }
+            }
+            const bool lowl = kc < kl;
+            const double2 l1l = lowl ? loc1[sl] : make_double2(0.0, -1.0);
+            const double bl = b[(int)l1l.y >= 0 ? (int)l1l.y : ispare];
+            const int nc = min(G, ke - c0);
+            for (int u0 = 0; u0 < nc; u0 += U) {
+                double rj[U][E];
+#pragma unroll
+                for (int v = 0; v < U; ++v) {
+                    const int j = bcast_i<G>(jl, min(u0 + v, nc - 1));
+                    ld_row<E>(Rn + (long)j * ld + lane * E, rj[v]);
+                }
+#pragma unroll
+                for (int v = 0; v < U; ++v) {
+                    const int u = u0 + v;
+                    if (u >= nc) break;
+                    const double sv = bcast_d<G>(svl, u);
+#pragma unroll
+                    for (int e = 0; e < E; ++e) g[e] += sv * rj[v][e];
+                    if (c0 + u < kl) {   // lower entry: A(R_new R_new^T) slot owned by this row
+                        double d = 0.0;
+#pragma unroll
+                        for (int e = 0; e < E; ++e) d += ri[e] * rj[v][e];
+                        d = group_sum<G>(d);
+                        if (lane == u) {
+                            uRR[sl] = d;
+                            const int cl = (int)l1l.y;
+                            const int f0 = cl == -2 ? loc_ptr[sl] : 0;
+                            const int f1 = cl == -2 ? loc_ptr[sl + 1] : (cl >= 0 ? 1 : 0);
+                            for (int e = f0; e < f1; ++e) {
+                                const int ci = cl >= 0 ? cl : loc_con[e];
+                                const double tot = (cl >= 0 ? l1l.x : loc_w[e]) * d;
+                                cvs[ci] = tot;
+                                const double dd = (cl >= 0 ? bl : b[ci]) - tot;
+                                acc[9] += dd * dd;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        // G_new = 2 S R_new, s = tau D, y = G_new - G_old (setlbfgsHisTwo lorads_alm.c:842-863)
+        double di[E], go[E], sv2[E], yv[E];
+        ld_row<E>(D + oi, di);
+        ld_row<E>(Gold + oi, go);
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[e] *= 2.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { sv2[e] = tau * di[e]; yv[e] = g[e] - go[e]; }
+        st_row<E>(Gnew + oi, g);
+        st_row<E>(sh + oi, sv2);
+        st_row<E>(yh + oi, yv);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            acc[0] += g[e] * g[e];
+            acc[1] += yv[e] * sv2[e];
+            acc[2] += yv[e] * yv[e];
+            acc[3] += sv2[e] * g[e];
+            acc[4] += yv[e] * g[e];
+        }
+        if (two) {
+            double sov[E], yov[E];
+            ld_row<E>(so + oi, sov);
+            ld_row<E>(yo + oi, yov);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                acc[5] += sov[e] * g[e];
+                acc[6] += yov[e] * g[e];
+                acc[7] += sov[e] * yv[e];
+                acc[8] += yov[e] * yv[e];
+            }
+        }
+    }
+    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+}
+
+// ------------------------------------------------------------------------
 // Device-resident CG (CGSolve, linalg/lorads_cgs.c:128-287) for one cone's ADMM
 // half-step system M X = b, M x = x + A^*(A(sym(x V^T))) V (linSysProduct,
 // lorads_admm.c:471-486).  Scalars live in cgc[] (CgIdx); every kernel after the
@@ -2728,10 +2976,13 @@ static int res_b() {
     return resident_blocks(k_it_b<GG, EE, UU, (UU == 1 ? 2 : 0)>, &c);
 }
 
+constexpr int kWideU = 8;   // factor rows in flight per lane group in k_wide_a / k_wide_b
 struct StagePlan {
     int grid = 1;
     bool small = true;
     int T = 1;         // lane groups per row (team)
+    bool wide = false; // bandwidth regime, long rows: the neighbour half unrolled by 4 (more
+                       // gathers in flight per lane group; E <= 2 keeps the registers low)
 };
 // Team size for rows of average degree `deg`: split a row's neighbour list over T lane
 // groups while every group still gets two unrolled chunks and the chip is not
@@ -2769,12 +3020,14 @@ static int plan_a(const DevCone &c, int K, StagePlan &p) {
     const double deg = c.nown > 0 ? (double)c.P / c.nown : 0.0;    // lower entries per row
     const int T = team_size(c, deg, 2);
     LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_a<GG, EE, 2>(), res_a<GG, EE, 1>(), K, T); });
+    p.wide = !p.small && deg / T >= 32.0 && c.E <= 2;
     return 0;
 }
 static int plan_b(const DevCone &c, int K, StagePlan &p) {
     const double deg = c.nown > 0 ? (double)c.adj_nnz / c.nown : 0.0;
     const int T = team_size(c, deg, 4);
     LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_b<GG, EE, 4>(), res_b<GG, EE, 1>(), K, T); });
+    p.wide = !p.small && deg / T >= 64.0 && c.E <= 2;
     return 0;
 }
 
@@ -2951,7 +3204,16 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     for (int k = 0; k < KL && (mask & 1) && split; ++k) {
         const DevCone &c = cone_of(k);
         const int grid = pa[k].grid;
-        LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_A(1, 2); });
+        if (pa[k].wide) {
+            LRS_LAYOUT_SWITCH(c.G, c.E, {
+                hipLaunchKernelGGL((k_wide_a<GG, EE, kWideU>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,
+                                   c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.uvt0,
+                                   W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1),
+                                   P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, c.row0, P.m);
+            });
+        } else {
+            LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_A(1, 2); });
+        }
         LRS_CHECK_LAUNCH();
         off += grid;
     }
@@ -3009,7 +3271,18 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const DevCone &c = cone_of(k);
         const int grid = pb[k].grid;
         if (pb[k].small) { off += grid; continue; }
-        LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_B(1, 2); });
+        if (pb[k].wide) {
+            LRS_LAYOUT_SWITCH(c.G, c.E, {
+                hipLaunchKernelGGL((k_wide_b<GG, EE, kWideU>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,
+                                   c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1],
+                                   W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
+                                   P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr,
+                                   P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par,
+                                   ctrl_cur, ls_cur, L, W.partC, off, c.row0, P.m);
+            });
+        } else {
+            LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_B(1, 2); });
+        }
         LRS_CHECK_LAUNCH();
         off += grid;
     }

@@ -158,11 +158,19 @@ _REGIME_SCRIPT = r"""
 import importlib, json, sys
 sys.path.insert(0, sys.argv[1])
 s = importlib.import_module("ltr-lowrank-sdp_amd.solver")
+inst = importlib.import_module("ltr-lowrank-sdp_amd.instances")
 out = {}
 for name in sys.argv[2:]:
-    sv = s.Solver(name)
-    r = sv.solve(reoptLevel=0)
-    out[name] = [r["alm_inner"], r["alm_pobj"], r["pobj"], r["admm_iter"]]
+    if name.startswith("rsparse:"):   # in-memory random sparse SDP n:m (long rows: the wide path)
+        n, m, r = map(int, name.split(":")[1:4])
+        sv = s.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(n, m, 6, 7)))
+        # a bounded ALM phase (150 inner iterations): the long-row kernels' arithmetic
+        res = sv.solve(fixedRank=r, reoptLevel=0, skipADMM=1, almInnerBudget=150)
+        out[name] = [res["alm_inner"], res["alm_pobj"], res["pobj"], res["admm_iter"]]
+    else:
+        sv = s.Solver(name)
+        r = sv.solve(reoptLevel=0)
+        out[name] = [r["alm_inner"], r["alm_pobj"], r["pobj"], r["admm_iter"]]
     sv.close()
 print(json.dumps(out))
 """
@@ -174,7 +182,7 @@ def test_bandwidth_regime_matches_latency_regime(tmp_path):
     instances give the same solves as the latency-regime kernels (LRS_FORCE_REGIME)."""
     import sys as _sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    names = [instance(n) for n in ("mc_torus12x10", "mc_rand300w", "theta25x3")]
+    names = [instance(n) for n in ("mc_torus12x10", "mc_rand300w", "theta25x3")] + ["rsparse:400:8000:16", "rsparse:4000:100000:128"]
     res = {}
     for reg in ("small", "large"):
         env = dict(os.environ, LRS_FORCE_REGIME=reg)
@@ -187,7 +195,11 @@ def test_bandwidth_regime_matches_latency_regime(tmp_path):
         if "mc_" in nm:
             assert abs(a[0] - b[0]) <= 2, (nm, a, b)
             assert abs(a[1] - b[1]) <= 1e-8 * abs(a[1]), (nm, a, b)
-        assert abs(a[2] - b[2]) <= 1e-6 * max(1.0, abs(a[2])), (nm, a, b)
+        if "rsparse" in nm:
+            assert a[0] == b[0] == 150, (nm, a, b)
+            assert abs(a[1] - b[1]) <= 1e-8 * max(1.0, abs(a[1])), (nm, a, b)
+        else:
+            assert abs(a[2] - b[2]) <= 1e-6 * max(1.0, abs(a[2])), (nm, a, b)
 
 
 @pytest.mark.gpu
