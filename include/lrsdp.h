@@ -59,6 +59,7 @@ typedef struct {
     int final_rank, oracle_rank;
     int traj1_len, traj2_len;
     double rho_max;      /* params.rhoMax after LORADS_ALMtoADMM (written to the JSON) */
+    double dinf, dinf_inf, dinf_2;   /* dual infeasibility l_1 / l_inf / l_2 (main.c:515-521); -1 if not evaluated */
 } lrs_result;
 
 /* factor / vector selectors */
@@ -106,6 +107,11 @@ int lrs_op_lbfgs(lrs_ctx *ctx, int node_num, double beta_new, double beta_old);
 int lrs_op_admm_half(lrs_ctx *ctx, double rho, double cg_tol, int cg_maxit, int *cg_iters, double *rhs);
 /* Gram R^T R of cone k (r x r, row-major) */
 int lrs_op_gram(lrs_ctx *ctx, int cone, int which, double *gram);
+/* Dual infeasibility of the current multipliers (calculate_dual_infeasibility_solver,
+ * data/lorads_solver.c:1396-1426): l1 = sum_k |min(lambda_min(S_k), 0)| / scaleObjHis /
+ * (||C||_1 + 1) with S = C - sum_i lambda_i A_i; lam_min[k] per cone (may be NULL).  The
+ * reference's ARPACK dsaupd is replaced by a device Lanczos with full reorthogonalisation. */
+int lrs_op_dual_infeasibility(lrs_ctx *ctx, double *l1, double *lam_min);
 
 /* ---- whole solves ---- */
 /* main.c:380-610 flow (reoptLevel>=1 restarts not yet on the device path: see DESIGN.md). */

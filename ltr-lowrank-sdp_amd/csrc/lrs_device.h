@@ -233,6 +233,12 @@ int launch_cg_resid(long nr, const double *b, const double *Q, double *r, double
 int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, int nblkC, double *cgc, double tol,
                      int par, int init, hipStream_t st);
 
+// ---- dual infeasibility (Lanczos for lambda_min of S per cone) ----
+// y = S x over one cone's adjacency (S on the global slots, x / y cone-local vectors)
+int launch_symv(const DevProblem &P, int cone, const double *S, const double *x, double *y, hipStream_t st);
+// w -= Q (Q^T w): Q column-major n x k (leading dimension ldq); part >= 64 k doubles, h >= k
+int launch_reorth(int n, int k, const double *Q, long ldq, double *w, double *part, double *h, hipStream_t st);
+
 // per-context scratch of the standalone reductions for the calling thread (nullptr: globals)
 void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart);
 // sharded solve helpers

@@ -2521,6 +2521,90 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
 }
 
 // ------------------------------------------------------------------------
+// Dual infeasibility (calculate_dual_infeasibility_solver, data/lorads_solver.c:1396-1426):
+// lambda_min of S = C - sum_i lambda_i A_i per cone.  The reference runs ARPACK dsaupd
+// ("SA", ncv 40, tol 1e-2; dual_infeasible, data/lorads_sdp_conic.c:1636-1699).  Here: a
+// Lanczos process with full reorthogonalisation on the device -- S x over the cone's
+// symmetric adjacency, Q^T w and w - Q h as row-blocked kernels -- the host keeps the
+// tridiagonal and its smallest eigenvalue (lrs_solver.cpp lanczos_min).
+// ------------------------------------------------------------------------
+// y = S x on one cone (S on the pattern slots): a thread per row, or a wave per row (WAVE)
+template <bool WAVE>
+__global__ void __launch_bounds__(kBlock) k_symv(int n, const int *__restrict__ adj_ptr, const int *__restrict__ adj_col,
+                                                 const int *__restrict__ adj_slot, const double *__restrict__ S,
+                                                 const double *__restrict__ x, double *__restrict__ y) {
+    if constexpr (WAVE) {
+        const int lane = threadIdx.x & 63;
+        const int nw = gridDim.x * (kBlock / 64);
+        for (int i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < n; i += nw) {
+            double acc = 0.0;
+            for (int k = adj_ptr[i] + lane; k < adj_ptr[i + 1]; k += 64) acc += S[adj_slot[k]] * x[adj_col[k]];
+            acc = wave_sum(acc);
+            if (lane == 0) y[i] = acc;
+        }
+    } else {
+        for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+            double acc = 0.0;
+            for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) acc += S[adj_slot[k]] * x[adj_col[k]];
+            y[i] = acc;
+        }
+    }
+}
+// part[c][blockIdx.x] = sum over this block's rows of Q[c][i] w[i]   (grid.y = column c)
+__global__ void __launch_bounds__(kBlock) k_gemvt_part(int n, const double *__restrict__ Q, long ldq,
+                                                       const double *__restrict__ w, double *__restrict__ part) {
+    const int c = blockIdx.y;
+    double a[1] = {0.0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) a[0] += Q[c * ldq + i] * w[i];
+    double s[1];
+    block_reduce<1>(a, s);
+    if (threadIdx.x == 0) part[(long)c * gridDim.x + blockIdx.x] = s[0];
+}
+// h[c] = sum over the blocks' partials in block order
+__global__ void __launch_bounds__(kBlock) k_gemvt_fin(int k, int nb, const double *__restrict__ part,
+                                                      double *__restrict__ h) {
+    for (int c = blockIdx.x * kBlock + threadIdx.x; c < k; c += gridDim.x * kBlock) {
+        double t = 0.0;
+        for (int b = 0; b < nb; ++b) t += part[(long)c * nb + b];
+        h[c] = t;
+    }
+}
+// w -= Q h (k columns)
+__global__ void __launch_bounds__(kBlock) k_gemv_sub(int n, int k, const double *__restrict__ Q, long ldq,
+                                                     const double *__restrict__ h, double *__restrict__ w) {
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        double t = 0.0;
+        for (int c = 0; c < k; ++c) t += Q[c * ldq + i] * h[c];
+        w[i] -= t;
+    }
+}
+
+int launch_symv(const DevProblem &P, int cone, const double *S, const double *x, double *y, hipStream_t st) {
+    const DevCone &c = P.cones[cone];
+    const double deg = c.n > 0 ? (double)c.adj_nnz / c.n : 0.0;
+    if (deg > 32.0) {
+        const int grid = std::max(1, std::min(4096, (c.n + kBlock / 64 - 1) / (kBlock / 64)));
+        hipLaunchKernelGGL(k_symv<true>, dim3(grid), dim3(kBlock), 0, st, c.n, c.adj_ptr, c.adj_col, c.adj_slot, S, x, y);
+    } else {
+        hipLaunchKernelGGL(k_symv<false>, dim3(grid_elems(c.n, 1)), dim3(kBlock), 0, st, c.n, c.adj_ptr, c.adj_col,
+                           c.adj_slot, S, x, y);
+    }
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int launch_reorth(int n, int k, const double *Q, long ldq, double *w, double *part, double *h, hipStream_t st) {
+    if (k <= 0) return 0;
+    const int nb = std::max(1, std::min(64, (n + kBlock * 8 - 1) / (kBlock * 8)));
+    hipLaunchKernelGGL(k_gemvt_part, dim3(nb, k), dim3(kBlock), 0, st, n, Q, ldq, w, part);
+    LRS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_gemvt_fin, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, st, k, nb, part, h);
+    LRS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_gemv_sub, dim3(grid_elems(n, 1)), dim3(kBlock), 0, st, n, k, Q, ldq, h, w);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+// ------------------------------------------------------------------------
 // Device-resident CG (CGSolve, linalg/lorads_cgs.c:128-287) for one cone's ADMM
 // half-step system M X = b, M x = x + A^*(A(sym(x V^T))) V (linSysProduct,
 // lorads_admm.c:471-486).  Scalars live in cgc[] (CgIdx); every kernel after the

@@ -560,6 +560,144 @@ static int op_dot(lrs_ctx *c, long n, const double *x, const double *y, double *
     return read_tmpfin(c, TF_DOT, 1, out);
 }
 
+// ------------------------------------------------------------------------
+// Dual infeasibility (calculate_dual_infeasibility_solver, data/lorads_solver.c:1396-1426):
+// S = C + A^*(-lambda) on the pattern, lambda_min(S) per cone, and
+// err = sum_k |min(lambda_min,k, 0)| / scaleObjHis / (||C||_1 + 1).  The reference's
+// eigensolver is ARPACK dsaupd "SA" (ncv 40, tol 1e-2, data/lorads_sdp_conic.c:1636-1699);
+// here a Lanczos process with full reorthogonalisation (device kernels launch_symv /
+// launch_reorth), run to a 1e-10 relative Ritz residual or its step cap.
+// ------------------------------------------------------------------------
+// smallest eigenvalue of the symmetric tridiagonal T = tridiag(b, a, b) (k x k): bisection
+// on the Sturm count, then the last component of its unit eigenvector by inverse iteration
+static double tridiag_min(const std::vector<double> &a, const std::vector<double> &b, int k, double *last) {
+    double lo = 1e300, hi = -1e300;
+    for (int i = 0; i < k; ++i) {
+        const double r = (i > 0 ? std::fabs(b[i - 1]) : 0.0) + (i < k - 1 ? std::fabs(b[i]) : 0.0);
+        lo = std::min(lo, a[i] - r);
+        hi = std::max(hi, a[i] + r);
+    }
+    auto below = [&](double x) {   // eigenvalues of T smaller than x
+        int cnt = 0;
+        double d = 1.0;
+        for (int i = 0; i < k; ++i) {
+            d = (a[i] - x) - (i > 0 ? b[i - 1] * b[i - 1] / d : 0.0);
+            if (d == 0.0) d = -1e-300;
+            if (d < 0) ++cnt;
+        }
+        return cnt;
+    };
+    for (int it = 0; it < 2000 && hi - lo > 1e-15 * std::max(std::fabs(lo), std::fabs(hi)) + 1e-300; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (mid <= lo || mid >= hi) break;
+        if (below(mid) >= 1) hi = mid;
+        else lo = mid;
+    }
+    const double theta = 0.5 * (lo + hi);
+    // inverse iteration on T - theta I (Thomas algorithm; exact singularity nudged)
+    std::vector<double> x(k, 1.0 / std::sqrt((double)k)), cp(k), dp(k);
+    for (int sweep = 0; sweep < 3; ++sweep) {
+        double piv = a[0] - theta;
+        if (piv == 0.0) piv = 1e-300;
+        cp[0] = k > 1 ? b[0] / piv : 0.0;
+        dp[0] = x[0] / piv;
+        for (int i = 1; i < k; ++i) {
+            piv = (a[i] - theta) - b[i - 1] * cp[i - 1];
+            if (piv == 0.0) piv = 1e-300;
+            cp[i] = i < k - 1 ? b[i] / piv : 0.0;
+            dp[i] = (x[i] - b[i - 1] * dp[i - 1]) / piv;
+        }
+        x[k - 1] = dp[k - 1];
+        for (int i = k - 2; i >= 0; --i) x[i] = dp[i] - cp[i] * x[i + 1];
+        double nr = 0.0;
+        for (double v : x) nr += v * v;
+        nr = std::sqrt(nr);
+        if (!(nr > 0.0) || !std::isfinite(nr)) break;
+        for (double &v : x) v /= nr;
+    }
+    *last = std::fabs(x[k - 1]);
+    return theta;
+}
+
+static int op_dot(lrs_ctx *c, long n, const double *x, const double *y, double *out);
+// lambda_min of S on cone k (S: device slot values)
+static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int *steps) {
+    const int n = c->dp.cones[k].n;
+    const int kmax = (int)std::max(1L, std::min<long>(std::min<long>(n, 300), (long)(2e9 / (8.0 * n))));
+    double *Q = nullptr, *w = nullptr, *part = nullptr, *h = nullptr;
+    HIPC(hipMalloc((void **)&Q, sizeof(double) * (size_t)n * kmax));
+    HIPC(hipMalloc((void **)&w, sizeof(double) * n));
+    HIPC(hipMalloc((void **)&part, sizeof(double) * 64 * kmax));
+    HIPC(hipMalloc((void **)&h, sizeof(double) * kmax));
+    int rc = 0;
+    auto fail = [&](void) { rc = -1; };
+    HIPC(hipMemsetAsync(Q, 0, sizeof(double) * (size_t)n * kmax, c->st));
+    {   // deterministic start vector (the reference's ARPACK draws its own random residual)
+        std::vector<double> q0(n);
+        unsigned long long st = 0x9E3779B97F4A7C15ULL;
+        double nr = 0.0;
+        for (int i = 0; i < n; ++i) {
+            st = st * 6364136223846793005ULL + 1442695040888963407ULL;
+            q0[i] = ((double)(st >> 11) / 9007199254740992.0) - 0.5;
+            nr += q0[i] * q0[i];
+        }
+        nr = std::sqrt(nr);
+        for (double &v : q0) v /= nr;
+        HIPC(hipMemcpy(Q, q0.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+    }
+    std::vector<double> al, be;
+    double beta = 0.0, theta = 0.0;
+    int j = 0;
+    for (; j < kmax && rc == 0; ++j) {
+        const double *qj = Q + (size_t)j * n;
+        if (launch_symv(c->dp, k, S, qj, w, c->st)) { fail(); break; }
+        double alpha = 0.0;
+        if (op_dot(c, n, qj, w, &alpha)) { fail(); break; }
+        if (launch_axpby(n, -alpha, qj, 1.0, w, c->st)) { fail(); break; }
+        if (j > 0 && launch_axpby(n, -beta, Q + (size_t)(j - 1) * n, 1.0, w, c->st)) { fail(); break; }
+        // full reorthogonalisation against q_0..q_j, twice (classical Gram-Schmidt)
+        for (int t = 0; t < 2; ++t)
+            if (launch_reorth(n, j + 1, Q, n, w, part, h, c->st)) { fail(); break; }
+        double ww = 0.0;
+        if (rc || op_dot(c, n, w, w, &ww)) { fail(); break; }
+        const double bnew = std::sqrt(std::max(ww, 0.0));
+        al.push_back(alpha);
+        double last = 1.0;
+        theta = tridiag_min(al, be, j + 1, &last);
+        const double scale = std::max(1.0, std::fabs(theta));
+        if (bnew * last <= 1e-10 * scale || bnew <= 1e-14 * scale || j + 1 == kmax) { ++j; break; }
+        be.push_back(bnew);
+        beta = bnew;
+        if (launch_axpby(n, 1.0 / bnew, w, 0.0, Q + (size_t)(j + 1) * n, c->st)) { fail(); break; }
+    }
+    if (rc) set_err("lanczos: %s", last_device_error());
+    (void)hipFree(Q); (void)hipFree(w); (void)hipFree(part); (void)hipFree(h);
+    *lam_min = theta;
+    if (steps) *steps = j;
+    return rc;
+}
+
+// l_1 dual infeasibility of the current lambda (data/lorads_solver.c:1396-1426); lam_min per
+// cone into lmin (may be null)
+static int dual_infeasibility(lrs_ctx *c, double *l1, double *lmin) {
+    DevWork &W = c->W;
+    const int m = c->dp.m;
+    HIPC(hipMemsetAsync(W.wtmp, 0, sizeof(double) * m, c->st));
+    OPC(launch_axpby(m, -1.0, W.lam, 1.0, W.wtmp, c->st));          // negLambd = -dualVar
+    OPC(launch_wsum(c->dp, W.wtmp, 1, W.S, c->st));                 // S = C + A^*(negLambd)
+    double err = 0.0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        double lk = 0.0;
+        if (lanczos_min(c, k, W.S, &lk, nullptr)) return -1;
+        if (lmin) lmin[k] = lk;
+        err += std::fabs(std::min(lk, 0.0));
+    }
+    err /= c->scaleObjHis;
+    err /= (c->hp.cNrm1 + 1);
+    *l1 = err;
+    return 0;
+}
+
 static void cal_dual_obj(lrs_ctx *c) {   // LORADSCalDualObj lorads_alg_common.c:531
     double v = 0;
     op_dot(c, c->dp.m, c->dp.b, c->W.lam, &v);
@@ -1591,6 +1729,13 @@ int lrs_set_kernel_path(lrs_ctx *c, int path) {
     return 0;
 }
 
+int lrs_op_dual_infeasibility(lrs_ctx *c, double *l1, double *lam_min) {
+    if (c) bind(c);
+    if (!c || !c->loaded || !c->walloc) { set_err("no solver state"); return -1; }
+    if (!l1) { set_err("null argument"); return -1; }
+    return dual_infeasibility(c, l1, lam_min);
+}
+
 int lrs_get_kernel_path(lrs_ctx *c, int *used) {
     if (c) bind(c);
     if (!c || !used) { set_err("null argument"); return -1; }
@@ -1940,6 +2085,7 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     res->alm_time = t_alm;
     bool timeout = now_s() - tss > p->timeSecLimit;
     double t_admm = 0;
+    double dinf = -1.0;   // not evaluated (phase 2 skipped)
     if (!timeout && !p->skipADMM) {
         if (alm_to_admm(c, p, alm, admm)) return -1;
         const double ta = now_s();
@@ -1959,20 +2105,32 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
                 if (now_s() - tss > p->timeSecLimit) { timeout = true; break; }
             }
         }
+        // dual infeasibility of the phase-2 multipliers (main.c:515-527)
+        if (dual_infeasibility(c, &dinf, nullptr)) return -1;
+        admm.gap = c->dimGap;
+        admm.pinf1 = c->dimPinf;
+        logf_(c, p, "-----------------------------------------------------------------------\n"
+                    "Dual infeasibility: l_1 = %f, l_inf = %f, l_2 = %f\n"
+                    "-----------------------------------------------------------------------\n",
+              dinf, dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrmInf), dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrm2));
         // reoptLevel >= 2 (main.c:527-580): up to two more rounds, each followed by the
-        // U/V average; the dual infeasibility that also drives this loop in the reference
-        // (ARPACK, main.c:515) is not computed here and enters as 0
+        // U/V average and a new dual infeasibility
         if (p->reoptLevel >= 2 && !timeout) {
             int dual_cnt = 0;
-            while (admm.gap > p->phase2Tol || admm.pinf1 > p->phase2Tol) {
+            while (dinf > p->phase2Tol || admm.gap > p->phase2Tol || admm.pinf1 > p->phase2Tol) {
                 if (dual_cnt >= 2) break;
-                if (!p->highAccMode && admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol) break;
+                if (!p->highAccMode && dinf <= 5 * p->phase2Tol && admm.gap <= 5 * p->phase2Tol &&
+                    admm.pinf1 <= p->phase2Tol)
+                    break;
                 if (reopt(c, p, alm, admm, reopt_param, 3, 50, tss, &bad, 2)) return -1;
                 OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
                 HIPC(hipMemcpyAsync(c->W.V, c->W.R, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
+                if (dual_infeasibility(c, &dinf, nullptr)) return -1;
                 admm.gap = c->dimGap;
                 admm.pinf1 = c->dimPinf;
                 admm.pinfinf = c->dimPinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+                logf_(c, p, "reopt %d:Dual infeasibility: l_1 = %f, l_inf = %f, l_2 = %f\n", dual_cnt, dinf,
+                      dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrmInf), dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrm2));
                 dual_cnt++;
                 if (now_s() - tss > p->timeSecLimit) { timeout = true; break; }
             }
@@ -1994,8 +2152,14 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     res->gap = admm.gap; res->rho = admm.rho;
     res->solve_time = all_time; res->admm_time = t_admm;
     res->rho_max = p->rhoMax;
+    // main.c:592-604
+    res->dinf = dinf;
+    res->dinf_inf = dinf < 0 ? dinf : dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrmInf);
+    res->dinf_2 = dinf < 0 ? dinf : dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrm2);
     if (timeout) res->status = 4;
-    else if (admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol) res->status = 2;   // dual infeasibility not evaluated
+    else if (dinf >= 0 && dinf <= 5 * p->phase2Tol && admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol)
+        res->status = 1;
+    else if (admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol) res->status = 2;
     else res->status = 3;
     res->final_rank = sum_rank(c);
     int orc = (p->disableOracle || p->skipADMM) ? res->final_rank : oracle_rank(c, 2);

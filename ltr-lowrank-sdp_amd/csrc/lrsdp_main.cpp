@@ -131,10 +131,6 @@ int main(int argc, char **argv) {
         fprintf(stderr, "[lrsdp] lbfgsListLength %d not supported on the device path; using 2\n", p.lbfgsListLength);
         p.lbfgsListLength = 2;
     }
-    if (p.reoptLevel >= 2)
-        fprintf(stderr, "[lrsdp] reoptLevel %d: the dual infeasibility (ARPACK in the reference) is not computed; "
-                        "its reopt rounds are driven by the gap and primal infeasibility (DESIGN.md section 7)\n",
-                p.reoptLevel);
     printf("-----------------------------------------------------------\n");
     printf("  LoRADS-compatible low-rank SDP solver on MI355X (%s)\n", lrs_version());
     printf("-----------------------------------------------------------\n");
@@ -161,13 +157,23 @@ int main(int argc, char **argv) {
         return 0;
     }
     printf("-----------------------------------------------------------------------\n");
+    // LORADSEndProgram, data/lorads_solver.c:1307-1333
+    if (r.status == 3) printf("End Program due to reaching `the maximum number of iterations`:\n");
+    else if (r.status == 1) printf("End Program due to reaching `Official terminate criteria`:\n");
+    else if (r.status == 2) printf("End Program due to reaching `final terminate criteria`:\n");
+    else if (r.status == 4) printf("End Program since time limit.\n");
+    else printf("End Program but the status is unknown, please notify the authors\n");
+    const double dinf = r.dinf < 0 ? 0.0 : r.dinf, dinf_inf = r.dinf_inf < 0 ? 0.0 : r.dinf_inf;
     printf("Objective function Value are:\n");
     printf("\t 1.Primal Objective:            : %10.6e\n", r.pobj);
     printf("\t 2.Dual Objective:              : %10.6e\n", r.dobj);
     printf("Dimacs Error are:\n");
     printf("\t 1.Constraint Violation(1)      : %10.6e\n", r.pinf);
+    printf("\t 2.Dual Infeasibility(1)        : %10.6e\n", dinf);
     printf("\t 3.Primal Dual Gap              : %10.6e\n", r.gap);
+    printf("\t 4.Primal Variable Semidefinite : %10.6e\n", 0.0);
     printf("\t 5.Constraint Violation(Inf)    : %10.6e\n", r.pinf_inf);
+    printf("\t 6.Dual Infeasibility(Inf)      : %10.6e\n", dinf_inf);
     printf("-----------------------------------------------------------------------\n");
     printf("ALM inner iterations: %ld, ALM time: %f s, ADMM iterations: %ld\n", r.alm_inner, r.alm_time, r.admm_iter);
     printf("all_time: %f\n", r.solve_time);

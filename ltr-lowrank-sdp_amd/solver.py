@@ -52,7 +52,8 @@ class Result(C.Structure):
         ("pinf_inf", C.c_double), ("gap", C.c_double), ("rho", C.c_double), ("solve_time", C.c_double),
         ("alm_time", C.c_double), ("admm_time", C.c_double), ("read_time", C.c_double), ("status", C.c_int),
         ("retcode", C.c_int), ("final_rank", C.c_int), ("oracle_rank", C.c_int), ("traj1_len", C.c_int),
-        ("traj2_len", C.c_int), ("rho_max", C.c_double),
+        ("traj2_len", C.c_int), ("rho_max", C.c_double), ("dinf", C.c_double), ("dinf_inf", C.c_double),
+        ("dinf_2", C.c_double),
     ]
 
     def as_dict(self):
@@ -107,6 +108,7 @@ def load_library(path=None):
         "lrs_profile_stages": (C.c_int, [vp, C.POINTER(Params), C.c_long, dp, C.POINTER(C.c_long)]),
         "lrs_time_stages": (C.c_int, [vp, C.c_int, dp]),
         "lrs_set_kernel_path": (C.c_int, [vp, C.c_int]),
+        "lrs_op_dual_infeasibility": (C.c_int, [vp, dp, dp]),
         "lrs_get_kernel_path": (C.c_int, [vp, ip]),
         "lrs_stage_bytes": (C.c_int, [vp, dp]),
         "lrs_auut_bytes": (C.c_int, [vp, dp]),
@@ -361,6 +363,13 @@ class Solver:
     def set_kernel_path(self, path):
         """0 = automatic (latency-regime kernels where they apply), 1 = general row kernels."""
         self._check(self.lib.lrs_set_kernel_path(self.ctx, int(path)), "set_kernel_path")
+
+    def dual_infeasibility(self):
+        """(l1 dual infeasibility, [lambda_min(S_k)] per cone) of the current multipliers."""
+        l1 = C.c_double()
+        lm = np.zeros(max(1, len(self.dims)))
+        self._check(self.lib.lrs_op_dual_infeasibility(self.ctx, C.byref(l1), _dptr(lm)), "dual_infeasibility")
+        return l1.value, lm[:len(self.dims)]
 
     def kernel_path(self):
         """Path of the last enqueued ALM iteration: 0 latency-regime kernels, 1 general, -1 none."""

@@ -85,3 +85,37 @@ def oracle_solve(lib, name, flags):
     keys = ["alm_inner", "alm_outer", "alm_pobj", "alm_dobj", "alm_pinf", "alm_gap", "alm_rho", "admm_iter",
             "admm_pobj", "admm_dobj", "admm_pinf", "admm_gap", "admm_rho", "solve_time", "rank", "alm_time"]
     return dict(zip(keys, list(res)))
+
+
+def read_sdpa_dense(path):
+    """Test-side SDPA reader (the contract of LReadSDPA, io/lorads_file_io.c:59-455: '*' / '"'
+    comment lines, '{ ( ' ,' as separators, C = -F0, A_i = F_i, |v| < 1e-12 dropped, entries
+    symmetric).  Returns m, block dims, b, dense C per block, A as {(i, blk): [(r, c, v)]}.
+    LP blocks (negative dims) are not supported (as the device reader)."""
+    toks = []
+    with open(path) as f:
+        for line in f:
+            s = line.strip()
+            if not s or s[0] in '*"':
+                continue
+            for ch in "{}(),'":
+                s = s.replace(ch, " ")
+            toks.append(s.split())
+    m = int(toks[0][0])
+    nb = int(toks[1][0])
+    dims = [abs(int(x)) for x in toks[2][:nb]]
+    b = np.array([float(x) for x in toks[3][:m]])
+    C = [np.zeros((d, d)) for d in dims]
+    A = {}
+    for t in toks[4:]:
+        if len(t) < 5:
+            continue
+        i, blk, r, c, v = int(t[0]), int(t[1]) - 1, int(t[2]) - 1, int(t[3]) - 1, float(t[4])
+        if abs(v) < 1e-12:
+            continue
+        if i == 0:
+            C[blk][r, c] = -v
+            C[blk][c, r] = -v
+        else:
+            A.setdefault((i - 1, blk), []).append((r, c, v))
+    return m, dims, b, C, A

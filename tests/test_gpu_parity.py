@@ -300,3 +300,42 @@ def test_latency_kernels_throughput_budget(solver_mod):
     assert sv.kernel_path() == 0
     assert outs == [300, 300]
     sv.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mc_torus12x10", "mc_rand200", "theta40", "theta25x3", "rsparse60"])
+def test_dual_infeasibility_matches_dense_eig(solver_mod, name):
+    """Dual infeasibility (calculate_dual_infeasibility_solver, data/lorads_solver.c:1396-1426)
+    of the solve's multipliers: the device Lanczos' lambda_min(S_k), S = C - sum lambda_i A_i,
+    against numpy's dense eigvalsh (1e-8 of ||S||), and the reference's ARPACK call
+    (dsaupd "SA", ncv 40, tol 1e-2, data/lorads_sdp_conic.c:1636-1699) emulated with scipy's
+    ARPACK within that tolerance; the l1 error as the reference forms it."""
+    from golden_util import read_sdpa_dense
+    import scipy.sparse.linalg as sla
+    sv = solver_mod.Solver(instance(name))
+    res = sv.solve(reoptLevel=0)
+    lam = sv.get_vec(solver_mod.LAMBDA)
+    l1, lmin = sv.dual_infeasibility()
+    sv.close()
+    m, dims, b, Cb, A = read_sdpa_dense(instance(name))
+    err, cn1 = 0.0, sum(np.abs(Ck).sum() for Ck in Cb)
+    for k, d in enumerate(dims):
+        S = Cb[k].copy()
+        for (i, blk), ents in A.items():
+            if blk != k:
+                continue
+            for r, c, v in ents:
+                S[r, c] -= lam[i] * v
+                if r != c:
+                    S[c, r] -= lam[i] * v
+        ev = np.linalg.eigvalsh(S)[0]
+        nS = max(1.0, np.abs(S).max() * d)
+        assert abs(lmin[k] - ev) <= 1e-8 * nS, (k, lmin[k], ev)
+        if d >= 40:
+            w = sla.eigsh(S, k=1, which="SA", ncv=40, tol=1e-2, maxiter=600, return_eigenvectors=False)[0]
+            assert abs(lmin[k] - w) <= 1e-2 * max(1.0, abs(w)) + 1e-8 * nS, (k, lmin[k], w)
+        err += abs(min(ev, 0.0))
+    assert abs(l1 - err / (cn1 + 1)) <= 1e-8 * max(1.0, err / (cn1 + 1)) + 1e-12
+    # the solve evaluated it too (main.c:515) and reports l_inf = l_1 (1 + ||C||_1) / (1 + ||C||_inf)
+    assert res["dinf"] >= 0
+    assert abs(res["dinf"] - l1) <= 1e-8 * max(1.0, l1) + 1e-12
