@@ -8,6 +8,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 solver = importlib.import_module("ltr-lowrank-sdp_amd.solver")
+if os.environ.get("LRS_LIB"):
+    solver.load_library(os.environ["LRS_LIB"])
 inst = importlib.import_module("ltr-lowrank-sdp_amd.instances")
 side = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
 rank = int(sys.argv[2]) if len(sys.argv) > 2 else 16
