@@ -94,7 +94,17 @@ struct DevCone {
     long adj_nnz = 0;
     // most adjacency entries of one row (all, and lower incl. the diagonal); 0 = unknown
     int maxdeg = 0, maxlow = 0;
+    // dense rows (far more entries than the rest, e.g. a hub vertex): the latency kernels
+    // spread their entries over extra slice blocks.  A: rows whose lower part has more than
+    // kDenseRow entries; B: rows whose adjacency has.  Host ids (for the grids) and device copies.
+    std::vector<int> dra_h, drb_h;
+    std::vector<int> dra_n, drb_n;       // their entry counts (A: lower incl. diagonal, B: all)
+    int *dra = nullptr, *drb = nullptr;
+    long gl_need = 0;                    // doubles of slice gradients the B slices can need (any layout)
 };
+constexpr int kDenseRow = 64;        // entries of a row past which the latency kernels slice it
+constexpr int kSliceMinB = 28;       // fewest entries of one B slice block (G = 64: 7 groups x 4)
+constexpr int kMaxDenseRows = 32;    // more dense rows than this: the general row kernels
 
 // Sharded solve (one process per GPU, rows of the cone split into contiguous blocks):
 // the collectives the split iteration calls between its stages, provided by the host
@@ -162,6 +172,8 @@ struct DevWork {
     double *rec = nullptr;     // [m][4] per-constraint {A(RR^T), q1, q2, -lam - rho b}
     double *cgc = nullptr;     // [8] device CG control (CgIdx)
     double *tot = nullptr;     // [32] sharded solve: summed stage totals (A: 0..7, B: 16..25)
+    double *gl = nullptr;      // latency kernels: partial gradients of the dense rows' slices [slices][ld]
+    long gl_len = 0;
 };
 
 // ---------------------------- launchers -----------------------------------

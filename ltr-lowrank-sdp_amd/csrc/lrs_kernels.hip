@@ -1688,6 +1688,8 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_
 constexpr int kLatRowWaves = kRowBlock / 64 - 1;
 constexpr int kLatRows = kLatRowWaves * 64;      // row-wave threads per block
 constexpr int kLatMaxPartials = 256;             // producer blocks one control wave reduces
+constexpr int kSliceA = 2;                       // lower entries per lane group in a dense-row slice of A
+constexpr int kSliceB = 4;                       // entries per lane group in a dense-row slice of B
 
 // control wave: NV partial vectors summed over 1 <= nblk <= kLatMaxPartials producer blocks
 // (lane l takes blocks l, l+64, ...).  Split in two so that the loads can be issued first
@@ -1740,14 +1742,29 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     const int *__restrict__ con_ptr, const int *__restrict__ con_slot, const double *__restrict__ con_w,
     const double *__restrict__ uRR, const double *__restrict__ par, const double *__restrict__ ctrl_prev,
     double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev, const double *__restrict__ partC, int nblkC,
-    double *__restrict__ partA, int pblk_off, int gwide) {
+    double *__restrict__ partA, int pblk_off, int gwide, int nrb, int nda, const int *__restrict__ dra) {
     __shared__ double c[C_NCTRL];
     __shared__ double pl[P_NPAR];
     LRS_TS(0, 0);
     LRS_BLK_BEGIN();
     const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == kLatRowWaves;   // wave-uniform
     const int lane = threadIdx.x & (G - 1);
-    const int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G;
+    // blocks [0, nrb): one row per lane group.  Blocks past nrb: slices of the dense rows --
+    // every lane group of the block takes kSliceA consecutive lower entries of one dense row
+    // (the rows' own groups skip those entries; A's results are per slot, nothing to combine)
+    const bool slice = (int)blockIdx.x >= nrb;
+    int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G, sq = 0;
+    if (slice) {
+        constexpr int per = (kLatRows / G) * kSliceA;
+        int q = (int)blockIdx.x - nrb, L = 0;
+        for (; L < nda - 1; ++L) {
+            const int r = dra[L], ns = (adj_low[r] - adj_ptr[r] + per - 1) / per;
+            if (q < ns) break;
+            q -= ns;
+        }
+        i = dra[L];
+        sq = q * per + ((int)threadIdx.x / G) * kSliceA;   // this group's first entry (offset in the row)
+    }
     const bool valid = !ctrl_wave && i < n;
     const int ic = valid ? i : 0;
     // every load that needs nothing else goes out first, so that its memory trip overlaps
@@ -1819,17 +1836,22 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         ld_row<E>(s0 + oi, own.a0); ld_row<E>(y0 + oi, own.b0);
         ld_row<E>(s1 + oi, own.a1); ld_row<E>(y1 + oi, own.b1);
         ld_row<E>(R + oi, xi);
-        const int nl = valid ? ke - kb : 0;
-        const int kd = nl > 0 ? ke - 1 : 0;
+        // entries of this group: the row's lower part (a dense row's own group: none), or its
+        // slice of a dense row (no diagonal special case there)
+        int eb = kb, nl = valid ? ke - kb : 0;
+        if (slice) { eb = kb + sq; nl = valid ? max(0, min(kSliceA, ke - eb)) : 0; }
+        else if (nl > kDenseRow) nl = 0;
+        const int kd = nl > 0 ? eb + nl - 1 : 0;
         const int jd = adj_col[kd];
         sd = adj_slot[kd];
 #pragma unroll
         for (int u = 0; u < NO; ++u) {
-            const int k = nl > 0 ? kb + min(u, nl - 1) : 0;
+            const int k = nl > 0 ? eb + min(u, nl - 1) : 0;
             jj[u] = adj_col[k];
             ss[u] = adj_slot[k];
         }
-        dg = nl > 0 && jd == i;
+        kb = eb;
+        dg = !slice && nl > 0 && jd == i;
         no = nl - (dg ? 1 : 0);
         cwd = Cw[sd];
         l1d = loc1[sd];
@@ -1916,7 +1938,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         const double rho = par[P_RHO], rhoInv = 1.0 / rho;
         double yi[E];
         own.eval(kc, yi);
-        st_row<E>(D + oi, yi);
+        if (!slice) st_row<E>(D + oi, yi);
         // one lower entry (j, slot): sym(R D^T), D D^T, objective parts, local constraints
         auto entry = [&](int j, int sl, const double (&xjv)[E], const double (&yj)[E], double cwv, double2 l1v,
                          double bv, double cv, double lv) {
@@ -2005,16 +2027,32 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
     const double *__restrict__ partA, int nblkA, const double *__restrict__ partB, int nblkB,
     double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m, double *hmirror,
-    double seq) {
+    double seq, int nrb, int ndb, const int *__restrict__ drb, double *__restrict__ gl) {
     __shared__ double red[12];
     __shared__ double ls[LS_N];
     __shared__ double pl[P_NPAR];
+    __shared__ double gsh[kLatRows * 4];   // slice blocks: the lane groups' partial gradients
     LRS_TS(2, 0);
     LRS_BLK_BEGIN();
     mirror_ctrl(ctrl, hmirror, seq);
     const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == kLatRowWaves;   // wave-uniform
     const int lane = threadIdx.x & (G - 1);
-    const int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G;
+    // blocks [0, nrb): one row per lane group.  Blocks past nrb: slices of the dense rows --
+    // every lane group takes kSliceB consecutive entries of one dense row, the block's partial
+    // gradient goes to gl[slice] and k_lat_f finishes the row (its own group skips the entries)
+    const bool slice = (int)blockIdx.x >= nrb;
+    int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G, sq = 0;
+    if (slice) {
+        constexpr int per = (kLatRows / G) * kSliceB;
+        int q = (int)blockIdx.x - nrb, Ld = 0;
+        for (; Ld < ndb - 1; ++Ld) {
+            const int r = drb[Ld], ns = (adj_ptr[r + 1] - adj_ptr[r] + per - 1) / per;
+            if (q < ns) break;
+            q -= ns;
+        }
+        i = drb[Ld];
+        sq = q * per + ((int)threadIdx.x / G) * kSliceB;
+    }
     const bool valid = !ctrl_wave && i < n;
     const int ic = valid ? i : 0;
     // loads that need nothing else first: the control wave's partials (A's, and G's) and
@@ -2047,7 +2085,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     const long oi = (long)ic * ld + lane * E;
     // row-wave prefetch state
     int no = 0;
-    bool dg = false;
+    bool dg = false, dense = false;
     double ri[E], di[E], go[E], sov[E], yov[E];
     int ss[NO];
     bool lw[NO];
@@ -2087,20 +2125,24 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
         ld_row<E>(D + oi, di);
         ld_row<E>(Gold + oi, go);
         if (two) { ld_row<E>(so + oi, sov); ld_row<E>(yo + oi, yov); }
-        const int nt = valid ? ke - kb : 0;
+        // entries of this group: the row's adjacency (a dense row's own group: none, it only
+        // updates R), or its slice of a dense row (no diagonal special case there)
+        int eb = kb, nt = valid ? ke - kb : 0;
+        if (slice) { eb = kb + sq; nt = valid ? max(0, min(kSliceB, ke - eb)) : 0; }
+        else if (nt > kDenseRow) { nt = 0; dense = true; }
         // the diagonal is the last lower entry (columns ascending); positions of the first
         // NO + 1 entries, the off-diagonal ones picked after the diagonal test
-        const int kd = (valid && kl > kb) ? kl - 1 : 0;
+        const int kd = (!slice && nt > 0 && kl > kb) ? kl - 1 : 0;
         const int jd = adj_col[kd];
         sd = adj_slot[kd];
         int ja[NO + 1], sa[NO + 1];
 #pragma unroll
         for (int u = 0; u <= NO; ++u) {
-            const int k = nt > 0 ? kb + min(u, nt - 1) : 0;
+            const int k = nt > 0 ? eb + min(u, nt - 1) : 0;
             ja[u] = adj_col[k];
             sa[u] = adj_slot[k];
         }
-        dg = valid && kl > kb && jd == i;
+        dg = !slice && nt > 0 && kl > kb && jd == i;
         no = nt - (dg ? 1 : 0);
         const int pd = dg ? kl - 1 - kb : NO + 1;    // the diagonal's position among the first
 #pragma unroll
@@ -2108,7 +2150,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
             const bool past = u >= pd;
             const int j = past ? ja[u + 1] : ja[u];
             ss[u] = past ? sa[u + 1] : sa[u];
-            lw[u] = kb + u + (past ? 1 : 0) < kl;
+            lw[u] = eb + u + (past ? 1 : 0) < kl;
             const long oj = (long)(u < no ? j : ic) * ld + lane * E;
             ld_row<E>(R + oj, rjp[u]);
             ld_row<E>(D + oj, djp[u]);
@@ -2152,13 +2194,13 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     if (ls[LS_FLAG] != 0.0) return;
     const double tau = ls[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    double g[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) g[e] = 0.0;
     if (valid) {
 #pragma unroll
         for (int e = 0; e < E; ++e) ri[e] += tau * di[e];
-        st_row<E>(Rn + oi, ri);
-        double g[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) g[e] = 0.0;
+        if (!slice) st_row<E>(Rn + oi, ri);
         // one entry (j, slot) with R_new,j: S_ij = C + A^*(M1) (ALMSetGrad lorads_alm.c:38-57),
         // the gradient, and on lower slots A(R_new R_new^T) with the local constraints
         auto entry = [&](int sl, bool lower, const double (&rj)[E], double svv, double2 s1u, double2 ra_, double2 rb_,
@@ -2208,7 +2250,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
                 entry(ss[u], lw[u], rj, sv[u], s1v[u], ra[u], rb[u], l1v[u], bq[u]);
             }
         }
-        if (no > NO) {
+        if (!slice && no > NO) {
             int cnt = 0;
             for (int k = kb; k < ke; ++k) {
                 if (dg && k == kl - 1) continue;
@@ -2235,31 +2277,47 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
             }
         }
         if (dg) entry(sd, true, ri, svd, s1d, rad, rbd, l1d, bqd);
-        // gradient G_new = 2 S R_new, L-BFGS pair s = tau D, y = G_new - G_old, dots
-        double sv2[E], yv[E];
+        if (!slice && !dense) {
+            // gradient G_new = 2 S R_new, L-BFGS pair s = tau D, y = G_new - G_old, dots
+            double sv2[E], yv[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) g[e] *= 2.0;
+            for (int e = 0; e < E; ++e) g[e] *= 2.0;
 #pragma unroll
-        for (int e = 0; e < E; ++e) { sv2[e] = tau * di[e]; yv[e] = g[e] - go[e]; }
-        st_row<E>(Gnew + oi, g);
-        st_row<E>(sh + oi, sv2);
-        st_row<E>(yh + oi, yv);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            acc[0] += g[e] * g[e];
-            acc[1] += yv[e] * sv2[e];
-            acc[2] += yv[e] * yv[e];
-            acc[3] += sv2[e] * g[e];
-            acc[4] += yv[e] * g[e];
-        }
-        if (two) {
+            for (int e = 0; e < E; ++e) { sv2[e] = tau * di[e]; yv[e] = g[e] - go[e]; }
+            st_row<E>(Gnew + oi, g);
+            st_row<E>(sh + oi, sv2);
+            st_row<E>(yh + oi, yv);
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                acc[5] += sov[e] * g[e];
-                acc[6] += yov[e] * g[e];
-                acc[7] += sov[e] * yv[e];
-                acc[8] += yov[e] * yv[e];
+                acc[0] += g[e] * g[e];
+                acc[1] += yv[e] * sv2[e];
+                acc[2] += yv[e] * yv[e];
+                acc[3] += sv2[e] * g[e];
+                acc[4] += yv[e] * g[e];
             }
+            if (two) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    acc[5] += sov[e] * g[e];
+                    acc[6] += yov[e] * g[e];
+                    acc[7] += sov[e] * yv[e];
+                    acc[8] += yov[e] * yv[e];
+                }
+            }
+        }
+    }
+    if (slice) {
+        // the block's partial gradient of its dense row: groups summed in group order
+        if (!ctrl_wave) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) gsh[threadIdx.x * E + e] = g[e];
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < G * E) {
+            const int ln = threadIdx.x / E, e = threadIdx.x % E;
+            double t = 0.0;
+            for (int q = 0; q < kLatRows / G; ++q) t += gsh[(q * G + ln) * E + e];
+            gl[(long)((int)blockIdx.x - nrb) * ld + threadIdx.x] = t;
         }
     }
     LRS_TS(2, 3);
@@ -2270,6 +2328,57 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
         for (int q_ = 5; q_ < 12; ++q_) g_phase[2][q_] = g_phase_tmp[2][q_];
 #endif
     LRS_BLK_END(2);
+}
+
+// Dense rows of stage B after the slice blocks: one block per row sums the row's slice
+// gradients (slice order), then the epilogue of k_lat_b (gradient G_new = 2 S R_new, the
+// L-BFGS pair, the dots); the block's partials go to slot pblk_off + blockIdx.x.
+__global__ void __launch_bounds__(kRowBlock) k_lat_f(
+    int ld, int w, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ drb, int per,
+    const double *__restrict__ gl, const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0,
+    double *s1, double *y1, const double *__restrict__ ctrl, const double *__restrict__ ls_cur, int L,
+    double *__restrict__ partC, int pblk_off) {
+    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
+    const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
+    const double *__restrict__ D = Dall + foff;
+    const double *__restrict__ Gold = (gcur == 0 ? G0 : G1) + foff;
+    double *__restrict__ Gnew = (gcur == 0 ? G1 : G0) + foff;
+    double *__restrict__ sh = (h == 0 ? s0 : s1) + foff;
+    double *__restrict__ yh = (h == 0 ? y0 : y1) + foff;
+    const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
+    const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
+    const double tau = ls_cur[LS_TAU];
+    int sl0 = 0;
+    for (int q = 0; q < (int)blockIdx.x; ++q) {
+        const int r = drb[q];
+        sl0 += (adj_ptr[r + 1] - adj_ptr[r] + per - 1) / per;
+    }
+    const int i = drb[blockIdx.x], ns = (adj_ptr[i + 1] - adj_ptr[i] + per - 1) / per;
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const int t = threadIdx.x;
+    if (t < w) {
+        const long oi = (long)i * ld + t;
+        double g = 0.0;
+        for (int q = 0; q < ns; ++q) g += gl[(long)(sl0 + q) * ld + t];
+        g *= 2.0;
+        const double sv2 = tau * D[oi], yv = g - Gold[oi];
+        Gnew[oi] = g;
+        sh[oi] = sv2;
+        yh[oi] = yv;
+        acc[0] = g * g;
+        acc[1] = yv * sv2;
+        acc[2] = yv * yv;
+        acc[3] = sv2 * g;
+        acc[4] = yv * g;
+        if (L == 2) {
+            const double sov = so[oi], yov = yo[oi];
+            acc[5] = sov * g;
+            acc[6] = yov * g;
+            acc[7] = sov * yv;
+            acc[8] = yov * yv;
+        }
+    }
+    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
 }
 
 // ------------------------------------------------------------------------
@@ -3137,15 +3246,38 @@ static bool lat_disabled() {
     }
     return v != 0;
 }
-// grid of the latency kernels for cone c, or 0 when they do not apply
-static int lat_grid(const DevCone &c, const StagePlan &pa, const StagePlan &pb) {
-    if (lat_disabled() || forced_regime() == 2 || c.maxdeg <= 0 || !pa.small || !pb.small || pa.T != 1 || pb.T != 1)
-        return 0;
-    const long need = ((long)c.nown * c.G + kLatRows - 1) / kLatRows;
-    int ra = 0, rb = 0;
+// Launch plan of the latency kernels for one cone: nrb row blocks (one row per lane group),
+// then sa / sb slice blocks over the dense rows' entries (A: lower, B: all) and nf k_lat_f
+// blocks.  nrb == 0: they do not apply.
+struct LatPlan {
+    int nrb = 0, sa = 0, sb = 0, nf = 0;
+};
+static int lat_slices(const std::vector<int> &cnt, int per) {
+    int s = 0;
+    for (int x : cnt) s += (x + per - 1) / per;
+    return s;
+}
+static int lat_resident(const DevCone &c, int &ra, int &rb) {
     LRS_LAYOUT_SWITCH(c.G, c.E, { ra = (res_la<GG, EE>)(); rb = (res_lb<GG, EE>)(); });
-    if (need > std::min(ra, rb) || need > kLatMaxPartials) return 0;
-    return (int)std::max(1L, need);
+    return 0;
+}
+static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &pb) {
+    LatPlan lp;
+    if (lat_disabled() || forced_regime() == 2 || c.maxdeg <= 0 || !pa.small || !pb.small || pa.T != 1 || pb.T != 1)
+        return lp;
+    if ((int)c.dra_h.size() > kMaxDenseRows || (int)c.drb_h.size() > kMaxDenseRows) return lp;
+    const long need = std::max(1L, ((long)c.nown * c.G + kLatRows - 1) / kLatRows);
+    const int sa = lat_slices(c.dra_n, (kLatRows / c.G) * kSliceA);
+    const int sb = lat_slices(c.drb_n, (kLatRows / c.G) * kSliceB);
+    int ra = 0, rb = 0;
+    if (lat_resident(c, ra, rb)) return lp;
+    if (need + sa > ra || need + sb > rb || need + sa > kLatMaxPartials) return lp;
+    if (need + sb + (long)c.drb_h.size() > kLatMaxPartials) return lp;
+    lp.nrb = (int)need;
+    lp.sa = sa;
+    lp.sb = sb;
+    lp.nf = (int)c.drb_h.size();
+    return lp;
 }
 
 // Whether stage A runs as two launches (bandwidth regime) for the current layouts.
@@ -3223,19 +3355,26 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     const int gg = gwide ? std::min((std::max(1, P.mg) + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks)
                          : std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
     // latency regime: every launch of both stages on the k_lat kernels, or none
-    int lg[kMaxCones] = {0};
+    LatPlan lg[kMaxCones];
     bool lat = !sh && !split && !P.no_lat;
-    int nlat = 0;
+    int nla = 0, nlb = 0, nlf = 0;
     for (int k = 0; k < KL && lat; ++k) {
-        lg[k] = lat_grid(cone_of(k), pa[k], pb[k]);
-        if (lg[k] <= 0) lat = false;
-        nlat += lg[k];
+        lg[k] = lat_plan(cone_of(k), pa[k], pb[k]);
+        if (lg[k].nrb <= 0) lat = false;
+        nla += lg[k].nrb + lg[k].sa;
+        nlb += lg[k].nrb + lg[k].sb;
+        nlf += lg[k].nf;
     }
-    if (lat && (nlat > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials))) lat = false;
+    if (lat && (nla > kLatMaxPartials || nlb + nlf > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials)))
+        lat = false;
     P.last_path = lat ? 0 : 1;
     if (lat) {
-        nblkA = nblkB = nlat;
-        for (int k = 0; k < KL; ++k) pa[k].grid = pb[k].grid = lg[k];
+        nblkA = nla;
+        nblkB = nlb + nlf;   // the C partials: B's blocks, then k_lat_f's
+        for (int k = 0; k < KL; ++k) {
+            pa[k].grid = lg[k].nrb + lg[k].sa;
+            pb[k].grid = lg[k].nrb + lg[k].sb;
+        }
     }
     // what the consumers read: every producer block's partials, or (sharded) the summed totals
     double *totA = sh ? W.tot : nullptr, *totC = sh ? W.tot + 16 : nullptr;
@@ -3271,7 +3410,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr,
                                    P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam,
                                    W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,
-                                   W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, gwide);
+                                   W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, gwide,
+                                   lg[k].nrb, (int)c.dra_h.size(), c.dra);
             });
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
@@ -3318,6 +3458,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     if (mark(2)) return -1;
     // B: line search, R update, adjoint, gradient, A(RR^T), L-BFGS pair, dots
     off = 0;
+    long glo = 0;   // latency kernels: this launch's slice gradients in W.gl
     for (int k = 0; k < KL && (mask & 4); ++k) {
         const DevCone &c = cone_of(k);
         const int grid = pb[k].grid;
@@ -3338,8 +3479,10 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con,
                                    P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur,
                                    inA, nA, W.partB, P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, P.m,
-                                   k == 0 ? a.hmirror : nullptr, a.seq);
+                                   k == 0 ? a.hmirror : nullptr, a.seq, lg[k].nrb, (int)c.drb_h.size(), c.drb,
+                                   W.gl + glo);
             });
+            glo += (long)lg[k].sb * c.ld;
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
                 if (small) LRS_LAUNCH_B(4, 0);
@@ -3348,6 +3491,19 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         }
         LRS_CHECK_LAUNCH();
         off += grid;
+    }
+    // latency regime: the dense rows' epilogues after their slices
+    glo = 0;
+    for (int k = 0; k < KL && (mask & 4) && lat; ++k) {
+        const DevCone &c = cone_of(k);
+        if (lg[k].nf > 0) {
+            hipLaunchKernelGGL(k_lat_f, dim3(lg[k].nf), dim3(kRowBlock), 0, st, c.ld, c.G * c.E, c.foff, c.adj_ptr,
+                               c.drb, (kLatRows / c.G) * kSliceB, W.gl + glo, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
+                               W.ls[1], W.ly[1], ctrl_cur, ls_cur, L, W.partC, off);
+            LRS_CHECK_LAUNCH();
+        }
+        glo += (long)lg[k].sb * c.ld;
+        off += lg[k].nf;
     }
     // bandwidth regime: the gradient half over the updated factor
     off = 0;

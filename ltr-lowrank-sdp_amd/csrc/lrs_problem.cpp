@@ -538,7 +538,14 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         for (long q = 0; q < ntot; ++q) {
             mc.maxdeg = std::max(mc.maxdeg, ap[q + 1] - ap[q]);
             mc.maxlow = std::max(mc.maxlow, al[q] - ap[q]);
+            if (al[q] - ap[q] > kDenseRow) { mc.dra_h.push_back((int)q); mc.dra_n.push_back(al[q] - ap[q]); }
+            if (ap[q + 1] - ap[q] > kDenseRow) {
+                mc.drb_h.push_back((int)q);
+                mc.drb_n.push_back(ap[q + 1] - ap[q]);
+                mc.gl_need += (long)((ap[q + 1] - ap[q] + kSliceMinB - 1) / kSliceMinB) * 256;
+            }
         }
+        if (!dput(&mc.dra, mc.dra_h, err) || !dput(&mc.drb, mc.drb_h, err)) return false;
         if (!dput(&mc.adj_ptr, ap, err) || !dput(&mc.adj_low, al, err) || !dput(&mc.adj_col, ac, err) ||
             !dput(&mc.adj_slot, as, err))
             return false;
@@ -555,7 +562,17 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         for (int q = 0; q < c.n; ++q) {
             d.maxdeg = std::max(d.maxdeg, c.adj_ptr[q + 1] - c.adj_ptr[q]);
             d.maxlow = std::max(d.maxlow, c.adj_low[q] - c.adj_ptr[q]);
+            if (c.adj_low[q] - c.adj_ptr[q] > kDenseRow) {
+                d.dra_h.push_back(q);
+                d.dra_n.push_back(c.adj_low[q] - c.adj_ptr[q]);
+            }
+            if (c.adj_ptr[q + 1] - c.adj_ptr[q] > kDenseRow) {
+                d.drb_h.push_back(q);
+                d.drb_n.push_back(c.adj_ptr[q + 1] - c.adj_ptr[q]);
+                d.gl_need += (long)((c.adj_ptr[q + 1] - c.adj_ptr[q] + kSliceMinB - 1) / kSliceMinB) * 256;
+            }
         }
+        if (!dput(&d.dra, d.dra_h, err) || !dput(&d.drb, d.drb_h, err)) return false;
         if (!dput(&d.adj_ptr, c.adj_ptr, err) || !dput(&d.adj_low, c.adj_low, err) ||
             !dput(&d.adj_col, c.adj_col, err) || !dput(&d.adj_slot, adj_slot_g, err))
             return false;
@@ -568,8 +585,11 @@ void free_problem(DevProblem &dp) {
     f(dp.b); f(dp.Cw); f(dp.Craw); f(dp.con_ptr); f(dp.con_slot); f(dp.con_w);
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
-    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); }
-    if (dp.has_merged) { f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot); }
+    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); }
+    if (dp.has_merged) {
+        f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
+        f(dp.merged.dra); f(dp.merged.drb);
+    }
     dp = DevProblem();
 }
 

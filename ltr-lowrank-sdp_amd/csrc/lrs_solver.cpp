@@ -370,7 +370,7 @@ static void free_work(lrs_ctx *c) {
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
                       W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2,
-                      W.cgc, W.tot};
+                      W.cgc, W.tot, W.gl};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     c->W = DevWork();
@@ -432,6 +432,14 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax) || A(&W.rec, 4L * m) || A(&W.R2, NR) || A(&W.cgc, 8) ||
         A(&W.tot, 32))
         return -1;
+    {   // slice gradients of the latency kernels' dense rows
+        long gl = 1, sum = 0;
+        for (const auto &dc : P.cones) sum += dc.gl_need;   // per-cone launches: disjoint ranges
+        gl = std::max(gl, sum);
+        if (P.has_merged) gl = std::max(gl, P.merged.gl_need);
+        if (A(&W.gl, gl)) return -1;
+        W.gl_len = gl;
+    }
     HIPC(hipStreamSynchronize(c->st));
     c->walloc = true;
     c->head = 0; c->gcur = 0;

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Golden solves of the reference on the instances it ships itself (lorads/data/General_SDP,
+lorads/data/Max_cut_SDP; copied as data into data/bundled/): the reference LoRADS C code built
+by oracle/Makefile.ref (oracle/_ref/lorads_ref_harness) solves each with the flags below and
+the REF_RESULT line + JSON go to tests/golden/solves_bundled.json.  reoptLevel 0 / 1 only: the
+reference built here has no ARPACK, so its level-2 rounds (driven by the dual infeasibility)
+are not the reference's.  CPU only; needs /root/reference.
+Run:  python scripts/make_golden_bundled.py [name ...]"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "lorads_ref_harness")
+DATA = os.path.join(ROOT, "data", "bundled")
+OUT = os.path.join(ROOT, "tests", "golden", "solves_bundled.json")
+GSET = ["--reoptLevel", "0", "--heuristicFactor", "10", "--phase1Tol", "1e-2"]   # lorads/README.md:166
+CASES = [("G11", GSET), ("G12", GSET), ("G13", GSET),
+         ("cphil12", ["--reoptLevel", "0"]), ("checker_1.5", ["--reoptLevel", "0"]),
+         ("ice_2.0", ["--reoptLevel", "0"]), ("p_auss2_3.0", ["--reoptLevel", "0"]),
+         ("theta102", ["--reoptLevel", "0"])]
+
+
+def main():
+    want = set(sys.argv[1:])
+    old = json.load(open(OUT)) if os.path.exists(OUT) else []
+    keep = [o for o in old if want and o["instance"] not in want]
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1")
+    with tempfile.TemporaryDirectory() as td:
+        for name, flags in CASES:
+            if want and name not in want:
+                continue
+            path = os.path.join(DATA, f"{name}.dat-s")
+            js = os.path.join(td, "o.json")
+            t0 = time.time()
+            r = subprocess.run([HARNESS, "solve", path, *flags, "--timeSecLimit", "1800", "--jsonfile", js],
+                               capture_output=True, text=True, cwd=td, env=env)
+            wall = time.time() - t0
+            res = {}
+            for line in r.stdout.splitlines():
+                if line.startswith("REF_RESULT"):
+                    for kv in line.split()[1:]:
+                        k, v = kv.split("=")
+                        res[k] = float(v)
+            if not res:
+                print("no result", name, r.stdout[-2000:], r.stderr[-2000:])
+                continue
+            ref_json = json.load(open(js)) if os.path.exists(js) else None
+            keep.append({"instance": name, "flags": flags, "result": res, "wall_sec": wall, "json": ref_json})
+            print(name, flags, {k: res.get(k) for k in ("alm_inner", "admm_pobj", "admm_dobj", "solve_time")},
+                  f"wall {wall:.1f}s", flush=True)
+            json.dump(keep, open(OUT, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
