@@ -218,9 +218,21 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
             fillp[j]++;
         }
     }
-    double bn1 = 0, bn2 = 0, bni = 0;
-    for (double v : hp.b) { bn1 += std::fabs(v); bn2 += v * v; bni = std::max(bni, std::fabs(v)); }
-    hp.bNrm1 = bn1; hp.bNrm2 = std::sqrt(bn2); hp.bNrmInf = bni;
+    double bn1 = 0, bn2 = 0, bmax = -1.0;
+    size_t imax = 0;
+    for (size_t i = 0; i < hp.b.size(); ++i) {
+        const double v = hp.b[i];
+        bn1 += std::fabs(v);
+        bn2 += v * v;
+        if (std::fabs(v) > bmax) { bmax = std::fabs(v); imax = i; }
+    }
+    // ||b||_inf as the reference forms it (cal_sdp_const, data/lorads_solver.c:1469, the Linux
+    // build's UNDER_BLAS branch): Fortran idamax_ returns the 1-based position of the first
+    // largest |b_i|, used there as a 0-based index -- so the entry AFTER the largest.  (It
+    // scales l_inf_primal_infeasibility and thereby the ALM exit test.)  Largest entry last:
+    // the reference reads past b; here the largest itself.
+    const size_t inext = imax + 1 < hp.b.size() ? imax + 1 : imax;
+    hp.bNrm1 = bn1; hp.bNrm2 = std::sqrt(bn2); hp.bNrmInf = hp.b.empty() ? 0.0 : std::fabs(hp.b[inext]);
     double c1 = 0, c2 = 0, ci = 0;
     for (auto &c : hp.cones) { c1 += c.cNrm1; c2 += c.cNrm2sq; ci = std::max(ci, c.cNrmInf); }
     hp.cNrm1 = c1; hp.cNrm2 = std::pow(c2, 0.5); hp.cNrmInf = ci;

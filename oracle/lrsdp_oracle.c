@@ -476,10 +476,15 @@ static void nrm_consts(osolver *s) {   /* cal_sdp_const, data/lorads_solver.c:14
     }
     s->cObjNrm2 = pow(s->cObjNrm2, 0.5);
     s->bNrm1 = 0; s->bNrm2 = 0; s->bNrmInf = 0;
+    int imax = 0;
+    double bmax = -1.0;
     for (int i = 0; i < s->m; ++i) {
         s->bNrm1 += fabs(p->b[i]); s->bNrm2 += p->b[i] * p->b[i];
-        s->bNrmInf = OMAX(s->bNrmInf, fabs(p->b[i]));
+        if (fabs(p->b[i]) > bmax) { bmax = fabs(p->b[i]); imax = i; }
     }
+    /* data/lorads_solver.c:1469 (UNDER_BLAS): b[idamax_(b)] with Fortran's 1-based idamax_
+       as a C index -- the entry after the first largest |b_i| (the largest itself if last) */
+    if (s->m > 0) s->bNrmInf = fabs(p->b[imax + 1 < s->m ? imax + 1 : imax]);
     s->bNrm2 = sqrt(s->bNrm2);
 }
 

@@ -20,7 +20,8 @@ CASES = [("G11", GSET, GSET), ("G12", GSET, GSET), ("G13", GSET, GSET),
          ("checker_1.5", dict(reoptLevel=0), GENERAL_PUBLISHED),
          ("ice_2.0", dict(reoptLevel=0), GENERAL_PUBLISHED),
          ("p_auss2_3.0", dict(reoptLevel=0), GENERAL_PUBLISHED),
-         ("theta102", dict(reoptLevel=0), GENERAL_PUBLISHED)]
+         ("theta102", dict(reoptLevel=0), GENERAL_PUBLISHED),
+         ("MC_500", dict(reoptLevel=0), GENERAL_PUBLISHED)]
 want = set(sys.argv[1:])
 for name, gflags, pflags in CASES:
     if want and name not in want:

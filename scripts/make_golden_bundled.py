@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Golden solves of the reference on the instances it ships itself (lorads/data/General_SDP,
-lorads/data/Max_cut_SDP; copied as data into data/bundled/): the reference LoRADS C code built
+lorads/data/Max_cut_SDP,
+lorads/data/Matrix_Completion_SDP; copied as data into data/bundled/): the reference LoRADS C code built
 by oracle/Makefile.ref (oracle/_ref/lorads_ref_harness) solves each with the flags below and
 the REF_RESULT line + JSON go to tests/golden/solves_bundled.json.  reoptLevel 0 / 1 only: the
 reference built here has no ARPACK, so its level-2 rounds (driven by the dual infeasibility)
@@ -21,7 +22,7 @@ GSET = ["--reoptLevel", "0", "--heuristicFactor", "10", "--phase1Tol", "1e-2"]  
 CASES = [("G11", GSET), ("G12", GSET), ("G13", GSET),
          ("cphil12", ["--reoptLevel", "0"]), ("checker_1.5", ["--reoptLevel", "0"]),
          ("ice_2.0", ["--reoptLevel", "0"]), ("p_auss2_3.0", ["--reoptLevel", "0"]),
-         ("theta102", ["--reoptLevel", "0"])]
+         ("theta102", ["--reoptLevel", "0"]), ("MC_500", ["--reoptLevel", "0"])]
 
 
 def main():

@@ -36,7 +36,7 @@ def flags_of(g):
 
 def test_bundled_fixtures_complete():
     g = golden()
-    for name in ["G11", "G12", "G13", "cphil12", *HUBS, "theta102"]:
+    for name in ["G11", "G12", "G13", "cphil12", *HUBS, "theta102", "MC_500"]:
         assert name in g and os.path.exists(os.path.join(DATA, f"{name}.dat-s"))
         r = g[name]["result"]
         assert r["admm_pinf"] < 1e-4 and r["alm_inner"] > 0
@@ -93,7 +93,7 @@ def test_dense_row_slices_match_general(solver_mod, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["G11", "G12", "G13", "cphil12", *HUBS])
+@pytest.mark.parametrize("name", ["G11", "G12", "G13", "cphil12", *HUBS, "MC_500"])
 def test_bundled_matches_reference(solver_mod, name):
     """Device solve with the golden run's flags against the reference's final result: the
     primal objective within OBJ_TOL (MaxCut, where both stop at a gap of ~1e-7: 1e-6),
