@@ -250,6 +250,9 @@ int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, i
 int launch_symv(const DevProblem &P, int cone, const double *S, const double *x, double *y, hipStream_t st);
 // w -= Q (Q^T w): Q column-major n x k (leading dimension ldq); part >= 64 k doubles, h >= k
 int launch_reorth(int n, int k, const double *Q, long ldq, double *w, double *part, double *h, hipStream_t st);
+int launch_lanczos_step(const DevProblem &P, int cone, const double *S, int kmax, double *Q, long ldq, double *w0,
+                        double *w1, int *jp, double *al, double *bw2, double *part, hipStream_t st);
+constexpr int kLzStepCap = 300;   // Lanczos steps at most (the device step kernels take up to 512)
 
 // per-context scratch of the standalone reductions for the calling thread (nullptr: globals)
 void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart);
