@@ -776,38 +776,70 @@ static int update_dimacs(lrs_ctx *c, const double *X, const double *Y, bool with
 }
 
 // ---- oracle rank: device Gram + host Jacobi eigenvalues (lorads_logging.c:216-366)
+// Number of eigenvalues of the symmetric r x r matrix A above eps * lambda_max
+// (count_significant_from_matrix, lorads_logging.c:272-366, which takes all eigenvalues from
+// dsyevr): Householder reduction to tridiagonal form, lambda_max by Sturm bisection, then one
+// Sturm count at eps * lambda_max -- O(r^3) once instead of a Jacobi sweep loop (the oracle
+// rank runs every ADMM iteration, lorads_admm.c:60).
 static int sym_count(int r, std::vector<double> A, double eps) {
-    for (int sweep = 0; sweep < 100; ++sweep) {
-        double off = 0.0;
-        for (int i = 0; i < r; ++i)
-            for (int j = i + 1; j < r; ++j) off += A[i * r + j] * A[i * r + j];
-        if (off < 1e-30) break;
-        for (int p = 0; p < r; ++p)
-            for (int q = p + 1; q < r; ++q) {
-                double apq = A[p * r + q];
-                if (std::fabs(apq) < 1e-300) continue;
-                double th = 0.5 * (A[q * r + q] - A[p * r + p]) / apq;
-                double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
-                double cs = 1.0 / std::sqrt(t * t + 1.0), sn = t * cs;
-                for (int k = 0; k < r; ++k) {
-                    double akp = A[k * r + p], akq = A[k * r + q];
-                    A[k * r + p] = cs * akp - sn * akq;
-                    A[k * r + q] = sn * akp + cs * akq;
-                }
-                for (int k = 0; k < r; ++k) {
-                    double apk = A[p * r + k], aqk = A[q * r + k];
-                    A[p * r + k] = cs * apk - sn * aqk;
-                    A[q * r + k] = sn * apk + cs * aqk;
-                }
-            }
+    if (r <= 0) return 0;
+    std::vector<double> d(r), e(r, 0.0), v(r), w(r);
+    for (int k = 0; k < r - 2; ++k) {
+        // Householder vector for column k below the diagonal
+        double alpha = 0.0;
+        for (int i = k + 1; i < r; ++i) alpha += A[i * r + k] * A[i * r + k];
+        alpha = std::sqrt(alpha);
+        if (alpha == 0.0) { e[k] = 0.0; continue; }
+        const double x0 = A[(k + 1) * r + k];
+        if (x0 > 0) alpha = -alpha;
+        e[k] = alpha;
+        double vn = 0.0;
+        for (int i = k + 1; i < r; ++i) v[i] = A[i * r + k];
+        v[k + 1] -= alpha;
+        for (int i = k + 1; i < r; ++i) vn += v[i] * v[i];
+        if (vn == 0.0) continue;
+        // A <- H A H on the trailing block, H = I - 2 v v^T / (v^T v)
+        const double beta = 2.0 / vn;
+        double vw = 0.0;
+        for (int i = k + 1; i < r; ++i) {
+            double t = 0.0;
+            for (int j = k + 1; j < r; ++j) t += A[i * r + j] * v[j];
+            w[i] = beta * t;
+            vw += v[i] * w[i];
+        }
+        const double hk = 0.5 * beta * vw;
+        for (int i = k + 1; i < r; ++i) w[i] -= hk * v[i];
+        for (int i = k + 1; i < r; ++i)
+            for (int j = k + 1; j < r; ++j) A[i * r + j] -= v[i] * w[j] + w[i] * v[j];
     }
-    double mx = -1e300;
-    for (int i = 0; i < r; ++i) mx = std::max(mx, A[i * r + i]);
-    int cnt = 0;
-    if (mx > 0)
-        for (int i = 0; i < r; ++i)
-            if (A[i * r + i] > eps * mx) cnt++;
-    return cnt;
+    for (int i = 0; i < r; ++i) d[i] = A[i * r + i];
+    if (r >= 2) e[r - 2] = A[(r - 1) * r + (r - 2)];
+    // Sturm count of eigenvalues below x for tridiag(e, d, e)
+    auto below = [&](double x) {
+        int cnt = 0;
+        double q = 1.0;
+        for (int i = 0; i < r; ++i) {
+            q = (d[i] - x) - (i > 0 ? e[i - 1] * e[i - 1] / q : 0.0);
+            if (q == 0.0) q = -1e-300;
+            if (q < 0) ++cnt;
+        }
+        return cnt;
+    };
+    double lo = 1e300, hi = -1e300;
+    for (int i = 0; i < r; ++i) {
+        const double rad = (i > 0 ? std::fabs(e[i - 1]) : 0.0) + (i < r - 1 ? std::fabs(e[i]) : 0.0);
+        lo = std::min(lo, d[i] - rad);
+        hi = std::max(hi, d[i] + rad);
+    }
+    for (int it = 0; it < 200 && hi - lo > 1e-14 * std::max(std::fabs(lo), std::fabs(hi)) + 1e-300; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (mid <= lo || mid >= hi) break;
+        if (below(mid) >= r) hi = mid;   // every eigenvalue below mid: lambda_max < mid
+        else lo = mid;
+    }
+    const double mx = 0.5 * (lo + hi);
+    if (!(mx > 0)) return 0;
+    return r - below(eps * mx);
 }
 
 static int gram_of(lrs_ctx *c, int k, const double *X, const double *Y, int avg, std::vector<double> &g) {
@@ -1381,7 +1413,10 @@ static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double 
     OPC(launch_cg_resid(nr, bk, Q, r, p, W.partC, cgc, W.part, nA, 1, c->st, &nC));
     OPC(launch_cg_resid2(nr, r, p, W.partC, nC, cgc, tol, 0, 1, c->st));
     double *h = c->hpin + 256;
-    int it = 0, B = 8;
+    // first batch sized from this cone's previous solve (ADMM's CG solves take a handful of
+    // iterations each; the batch past convergence runs guarded no-op launches), then doubling
+    const long prev = c->cgIterCone[k];
+    int it = 0, B = prev > 0 ? (int)std::max(2L, std::min(8L, prev + 1)) : 8;
     while (it < maxit) {
         for (int j = 0; j < B && it < maxit; ++j, ++it) {
             const int par = it & 1;
