@@ -53,7 +53,8 @@ def pmc_traffic(kernel):
     summary of this same bench run (profiles/<tag>_pmc.json, scripts/profile_r01.sh:
     separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per MI355X_MICROARCH.md)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    # newest round tag last (r01f < r01h ...): file names, not mtimes, which a checkout resets
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
