@@ -261,18 +261,20 @@ __global__ void __launch_bounds__(kBlock) k_sddmm(int n, int ld, const int *__re
                                                   const double *__restrict__ Y, double *__restrict__ out0,
                                                   double *__restrict__ out1, const double *__restrict__ Cw,
                                                   double *part, unsigned *ticket, double *fin,
-                                                  const double *__restrict__ guard, int row0) {
+                                                  const double *__restrict__ guard, int row0, int T) {
     if (guard && guard[C_ACTIVE] == 0.0) return;
+    // teams of T lane groups per row (dense rows): member `mem` takes entries mem, mem + T, ...
     const int lane = threadIdx.x & (G - 1);
     const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
     const int ngrp = gridDim.x * kBlock / G;
+    const int mem = grp % T;
     double acc[2] = {0.0, 0.0};
-    for (int i = row0 + grp; i < row0 + n; i += ngrp) {
+    for (int i = row0 + grp / T; i < row0 + n; i += ngrp / T) {
         double xi[E], yi[E];
         ld_row<E>(X + (long)i * ld + lane * E, xi);
         if constexpr (MODE != 1) ld_row<E>(Y + (long)i * ld + lane * E, yi);
         const int kb = adj_ptr[i], ke = adj_low[i];
-        for (int k = kb; k < ke; ++k) {
+        for (int k = kb + mem; k < ke; k += T) {
             const int j = adj_col[k];
             const int s = adj_slot[k];
             double xj[E];
@@ -433,11 +435,11 @@ __global__ void __launch_bounds__(kBlock) k_auv_con_long(int nlong, const int *_
                                                          double scale, int accumulate, double *__restrict__ out,
                                                          const double *__restrict__ guard) {
     if (guard && guard[0] == 0.0) return;
-    constexpr int NG = 64 / G;
+    __shared__ double wsum4[kBlock / 64];
+    constexpr int NG = kBlock / G;   // lane groups of the block, striding over the entries
     const int lane = threadIdx.x & (G - 1);
-    const int gq = (threadIdx.x & 63) / G;
-    const int nw = gridDim.x * (kBlock / 64);
-    for (int t = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t < nlong; t += nw) {
+    const int gq = threadIdx.x / G;
+    for (int t = blockIdx.x; t < nlong; t += gridDim.x) {   // block-uniform
         const int i = long_rows[t];
         const long row = (long)cone * m + i;
         const int e0 = con_ptr[row], e1 = con_ptr[row + 1];
@@ -449,11 +451,16 @@ __global__ void __launch_bounds__(kBlock) k_auv_con_long(int nlong, const int *_
             v += con_w[e] * d;
         }
         v = wave_sum(lane == 0 ? v : 0.0);
-        if ((threadIdx.x & 63) == 0) {
-            double tot = v * scale;
+        if ((threadIdx.x & 63) == 0) wsum4[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double w = 0.0;
+            for (int q = 0; q < kBlock / 64; ++q) w += wsum4[q];
+            double tot = w * scale;
             if (accumulate) tot = out[i] + tot;
             out[i] = tot;
         }
+        __syncthreads();
     }
 }
 
@@ -479,22 +486,44 @@ __global__ void __launch_bounds__(kBlock) k_spmm(int n, int ld, const int *__res
                                                  const double *__restrict__ S, const double *__restrict__ X,
                                                  double scale, const double *__restrict__ addX, double addScale,
                                                  double *__restrict__ out, double *part, unsigned *ticket,
-                                                 double *fin, int row0) {
+                                                 double *fin, int row0, int T) {
+    // teams of T lane groups per row (dense rows): members take interleaved entries, their
+    // partial rows meet in LDS and member 0 sums them in member order (T = 1: no LDS step)
+    __shared__ double gsh[kBlock * 4];
     const int lane = threadIdx.x & (G - 1);
-    const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
-    const int ngrp = gridDim.x * kBlock / G;
+    const int gib = threadIdx.x / G;
+    const int tpb = (kBlock / G) / T;
+    const int tl = gib / T, mem = gib % T;
     double nrm[1] = {0.0};
-    for (int i = row0 + grp; i < row0 + n; i += ngrp) {
+    for (int ib = row0 + blockIdx.x * tpb; ib < row0 + n; ib += gridDim.x * tpb) {   // block-uniform
+        const int i = ib + tl;
+        const bool valid = i < row0 + n;
         double acc[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) acc[e] = 0.0;
-        for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) {
-            const double sv = S[adj_slot[k]];
-            double xj[E];
-            ld_row<E>(X + (long)adj_col[k] * ld + lane * E, xj);
+        if (valid)
+            for (int k = adj_ptr[i] + mem; k < adj_ptr[i + 1]; k += T) {
+                const double sv = S[adj_slot[k]];
+                double xj[E];
+                ld_row<E>(X + (long)adj_col[k] * ld + lane * E, xj);
 #pragma unroll
-            for (int e = 0; e < E; ++e) acc[e] += sv * xj[e];
+                for (int e = 0; e < E; ++e) acc[e] += sv * xj[e];
+            }
+        if (T > 1) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) gsh[threadIdx.x * E + e] = acc[e];
+            __syncthreads();
+            if (mem == 0) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    double t = 0.0;
+                    for (int q = 0; q < T; ++q) t += gsh[((tl * T + q) * G + lane) * E + e];
+                    acc[e] = t;
+                }
+            }
+            __syncthreads();
         }
+        if (!valid || mem != 0) continue;
 #pragma unroll
         for (int e = 0; e < E; ++e) acc[e] *= scale;
         if (addX) {
@@ -3142,11 +3171,23 @@ double *device_fin() { return fin_ptr(); }
         return -1;                                                                             \
     }
 
+// Team size (lane groups per row) of the standalone SDDMM / SpMM on cone c: 1 for sparse
+// rows (the row loop unchanged); for dense rows up to the block's groups, about 8 entries
+// per member (lower entries for the SDDMM).
+static int small_team(const DevCone &c, bool lower) {
+    const double deg = c.nown > 0 ? (double)c.adj_nnz / c.n : 0.0;
+    const double ent = lower ? 0.5 * deg : deg;
+    int T = 1;
+    while (T * 2 <= kBlock / c.G && T * 2 * 8 <= ent && (long)c.nown * T * 2 * c.G <= 256L * 2048) T *= 2;
+    return T;
+}
+
 int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double *out0,
                  double *out1, double *part, int pblk_off, int *nblk_used, hipStream_t st) {
     (void)pblk_off;
     const DevCone &c = P.cones[cone];
-    const int grid = grid_rows(c.nown, c.G);
+    const int T = small_team(c, true);
+    const int grid = grid_rows((long)c.nown * T, c.G);
     double *fin = tmpfin_ptr() + TF_SD + 2 * cone;
     const double *Xc = X + c.foff;
     const double *Yc = Y ? Y + c.foff : nullptr;
@@ -3154,15 +3195,15 @@ int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const
         if (mode == 0)
             hipLaunchKernelGGL((k_sddmm<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, c.nown, c.ld, c.adj_ptr,
                                c.adj_low, c.adj_col, c.adj_slot, Xc, Yc, out0, out1, P.Cw, part,
-                               ticket_ptr(T_SDDMM), fin, nullptr, c.row0);
+                               ticket_ptr(T_SDDMM), fin, nullptr, c.row0, T);
         else if (mode == 1)
             hipLaunchKernelGGL((k_sddmm<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, c.nown, c.ld, c.adj_ptr,
                                c.adj_low, c.adj_col, c.adj_slot, Xc, Yc, out0, out1, P.Cw, part,
-                               ticket_ptr(T_SDDMM), fin, nullptr, c.row0);
+                               ticket_ptr(T_SDDMM), fin, nullptr, c.row0, T);
         else
             hipLaunchKernelGGL((k_sddmm<GG, EE, 2>), dim3(grid), dim3(kBlock), 0, st, c.nown, c.ld, c.adj_ptr,
                                c.adj_low, c.adj_col, c.adj_slot, Xc, Yc, out0, out1, P.Cw, part,
-                               ticket_ptr(T_SDDMM), fin, nullptr, c.row0);
+                               ticket_ptr(T_SDDMM), fin, nullptr, c.row0, T);
     });
     LRS_CHECK_LAUNCH();
     if (nblk_used) *nblk_used = grid;
@@ -3212,7 +3253,7 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
                                P.con_ptr, P.con_slot, P.con_w, P.slot_rc, P.con1_pq, P.con1_w, Xc, Yc, scale,
                                accumulate, out, b_for_vio, vio_part, tk, fin, guard);
         if (nlong > 0) {
-            const int gl = std::min((nlong + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks);
+            const int gl = std::min(nlong, kMaxPartialBlocks);
             if (mode == 1)
                 hipLaunchKernelGGL((k_auv_con_long<GG, EE, 1>), dim3(gl), dim3(kBlock), 0, st, nlong,
                                    P.long_rows + l0, P.m, cone, c.ld, P.con_ptr, P.con_slot, P.con_w, P.slot_rc, Xc,
@@ -3239,12 +3280,13 @@ int launch_spmm(const DevProblem &P, int cone, const double *S, const double *X,
                 double addScale, double *out, double *part, int pblk_off, int *nblk_used, hipStream_t st) {
     (void)pblk_off;
     const DevCone &c = P.cones[cone];
-    const int grid = grid_rows(c.nown, c.G);
+    const int T = small_team(c, false);
+    const int grid = grid_rows((long)c.nown * T, c.G);
     double *fin = tmpfin_ptr() + TF_SPMM + cone;
     LRS_LAYOUT_SWITCH(c.G, c.E, {
         hipLaunchKernelGGL((k_spmm<GG, EE>), dim3(grid), dim3(kBlock), 0, st, c.nown, c.ld, c.adj_ptr, c.adj_col,
                            c.adj_slot, S, X + c.foff, scale, addX ? addX + c.foff : nullptr, addScale,
-                           out + c.foff, part, ticket_ptr(T_SPMM), fin, c.row0);
+                           out + c.foff, part, ticket_ptr(T_SPMM), fin, c.row0, T);
     });
     LRS_CHECK_LAUNCH();
     if (nblk_used) *nblk_used = grid;
