@@ -655,15 +655,33 @@ static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int 
     HIPC(hipMemsetAsync(jp, 0, sizeof(int), c->st));
     int rc = 0;
     HIPC(hipMemsetAsync(Q, 0, sizeof(double) * (size_t)n * kmax, c->st));
-    {   // deterministic start vector (the reference's ARPACK draws its own random residual)
-        std::vector<double> q0(n);
+    {   // Deterministic start vector (the reference's ARPACK draws its own random residual):
+        // a pseudo-random combination of the factor's columns plus 1 % pseudo-random noise.
+        // Near optimality S R ~ 0 (complementarity), so lambda_min sits in the near-null
+        // cluster spanned by R, and a start there reaches it in far fewer steps than a
+        // plain random vector; the noise keeps every eigendirection in the Krylov space.
+        const DevCone &dc = c->dp.cones[k];
+        std::vector<double> Rh((size_t)n * dc.ld, 0.0), q0(n), g(dc.ld, 0.0);
+        HIPC(hipMemcpyAsync(Rh.data(), c->W.R + dc.foff, sizeof(double) * Rh.size(), hipMemcpyDeviceToHost, c->st));
+        HIPC(hipStreamSynchronize(c->st));
         unsigned long long st = 0x9E3779B97F4A7C15ULL;
-        double nr = 0.0;
-        for (int i = 0; i < n; ++i) {
+        auto rnd = [&]() {
             st = st * 6364136223846793005ULL + 1442695040888963407ULL;
-            q0[i] = ((double)(st >> 11) / 9007199254740992.0) - 0.5;
-            nr += q0[i] * q0[i];
+            return ((double)(st >> 11) / 9007199254740992.0) - 0.5;
+        };
+        for (int q = 0; q < dc.r; ++q) g[q] = rnd();
+        double nr = 0.0, nn = 0.0;
+        for (int i = 0; i < n; ++i) {
+            double t = 0.0;
+            for (int q = 0; q < dc.r; ++q) t += Rh[(size_t)i * dc.ld + q] * g[q];
+            q0[i] = t;
+            nr += t * t;
         }
+        std::vector<double> z(n);
+        for (int i = 0; i < n; ++i) { z[i] = rnd(); nn += z[i] * z[i]; }
+        const double zs = (nr > 0 ? 1e-2 * std::sqrt(nr) : 1.0) / std::sqrt(nn);
+        nr = 0.0;
+        for (int i = 0; i < n; ++i) { q0[i] += zs * z[i]; nr += q0[i] * q0[i]; }
         nr = std::sqrt(nr);
         for (double &v : q0) v /= nr;
         // on the solver stream, after the zero fill above (a null-stream copy can overtake it)

@@ -30,4 +30,6 @@ for name in sys.argv[1:] or ["theta3"]:
     print("  fixed-rank %d ALM: %.1f it/s (%.1f us/it), path %d" % (rk, o["done"] / o["seconds"],
                                                                    o["seconds"] / max(1, o["done"]) * 1e6,
                                                                    sv.kernel_path()), flush=True)
+    ms = sv.time_stages(200)
+    print("  stages (A, G, B) us per launch:", [round(x * 1e3, 2) for x in ms], flush=True)
     sv.close()
