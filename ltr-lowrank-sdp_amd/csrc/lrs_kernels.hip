@@ -2727,13 +2727,15 @@ __device__ __forceinline__ void lz_bufs(int j, const double *Q, double *w0, doub
     *win = j == 0 ? Q : ((j & 1) ? w0 : w1);
     *wout = (j & 1) ? w1 : w0;
 }
-// q_j = w / beta_{j-1} into Q[j], y = S q_j, partials of alpha_j = q_j . y
+// q_j = w / beta_{j-1} into Q[j]; y = S q_j - beta_{j-1} q_{j-1}.  alpha_j is not formed here:
+// the reorthogonalisation against Q[0..j] removes the q_j component, and alpha_j is the sum of
+// its two passes' j-th coefficients (the entries of Q^T S Q, as in Arnoldi).
 template <bool WAVE>
 __global__ void __launch_bounds__(kBlock) k_lz_symv(int n, const int *__restrict__ adj_ptr,
                                                     const int *__restrict__ adj_col, const int *__restrict__ adj_slot,
                                                     const double *__restrict__ S, double *w0, double *w1,
                                                     const double *__restrict__ bw2, const int *__restrict__ jp,
-                                                    double *Q, long ldq, double *__restrict__ apart) {
+                                                    double *Q, long ldq) {
     const int j = *jp;
     const double *w;
     double *y;
@@ -2741,7 +2743,8 @@ __global__ void __launch_bounds__(kBlock) k_lz_symv(int n, const int *__restrict
     const double beta = j > 0 ? sqrt(fmax(bw2[j - 1], 0.0)) : 1.0;
     const double inv = 1.0 / beta;
     double *qj = Q + (long)j * ldq;
-    double acc[1] = {0.0};
+    const double *qp = Q + (long)(j > 0 ? j - 1 : 0) * ldq;
+    const double bp = j > 0 ? beta : 0.0;
     if constexpr (WAVE) {
         const int lane = threadIdx.x & 63;
         const int nw = gridDim.x * (kBlock / 64);
@@ -2750,43 +2753,17 @@ __global__ void __launch_bounds__(kBlock) k_lz_symv(int n, const int *__restrict
             for (int k = adj_ptr[i] + lane; k < adj_ptr[i + 1]; k += 64) t += S[adj_slot[k]] * (w[adj_col[k]] * inv);
             t = wave_sum(t);
             if (lane == 0) {
-                const double qi = w[i] * inv;
-                if (j > 0) qj[i] = qi;
-                y[i] = t;
-                acc[0] += qi * t;
+                if (j > 0) qj[i] = w[i] * inv;
+                y[i] = -bp * qp[i] + t;
             }
         }
     } else {
         for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
             double t = 0.0;
             for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) t += S[adj_slot[k]] * (w[adj_col[k]] * inv);
-            const double qi = w[i] * inv;
-            if (j > 0) qj[i] = qi;
-            y[i] = t;
-            acc[0] += qi * t;
+            if (j > 0) qj[i] = w[i] * inv;
+            y[i] = -bp * qp[i] + t;
         }
-    }
-    write_partials<1>(acc, apart, blockIdx.x);
-}
-// alpha_j from the partials (block order); y -= alpha_j q_j + beta_{j-1} q_{j-1}
-__global__ void __launch_bounds__(kBlock) k_lz_update(int n, double *w0, double *w1, const double *Q, long ldq,
-                                                      const int *__restrict__ jp, const double *__restrict__ apart,
-                                                      int nba, double *__restrict__ al,
-                                                      const double *__restrict__ bw2) {
-    const int j = *jp;
-    const double *w;
-    double *y;
-    lz_bufs(j, Q, w0, w1, &w, &y);
-    double a = 0.0;
-    for (int b = 0; b < nba; ++b) a += apart[b];
-    if (blockIdx.x == 0 && threadIdx.x == 0) al[j] = a;
-    const double bp = j > 0 ? sqrt(fmax(bw2[j - 1], 0.0)) : 0.0;
-    const double *qj = Q + (long)j * ldq;
-    const double *qp = Q + (long)(j > 0 ? j - 1 : 0) * ldq;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        double v = -a * qj[i] + y[i];
-        if (j > 0) v = -bp * qp[i] + v;
-        y[i] = v;
     }
 }
 // part[c][blockIdx.x] = sum over this block's rows of Q[c][i] y[i], c = blockIdx.y <= j
@@ -2806,11 +2783,12 @@ __global__ void __launch_bounds__(kBlock) k_lz_gemvt_part(int n, const double *Q
 }
 // y -= Q h with h[c] = sum of the partials (block order), c <= j < kLzMaxSteps.  A block takes
 // 64 rows; its four waves split the columns (wave w: c = w, w + 4, ...), a lane per row, and
-// the waves' sums meet in LDS in wave order.
+// the waves' sums meet in LDS in wave order.  Pass 0 records alpha_j = h[j], pass 1 adds its
+// h[j], forms ||y||^2 (the last block sums the block partials in order) and advances j.
 constexpr int kLzMaxSteps = 512;
 __global__ void __launch_bounds__(kBlock) k_lz_gemv_sub(int n, const double *Q, long ldq, double *w0, double *w1,
-                                                        const int *__restrict__ jp, const double *__restrict__ part,
-                                                        int nb) {
+                                                        int *jp, const double *__restrict__ part, int nb, int pass,
+                                                        double *al, double *npart, unsigned *ticket, double *bw2) {
     static_assert(kBlock == 256, "four waves per block");
     __shared__ double h[kLzMaxSteps];
     __shared__ double ws[4][64];
@@ -2824,25 +2802,24 @@ __global__ void __launch_bounds__(kBlock) k_lz_gemv_sub(int n, const double *Q, 
         h[c] = t;
     }
     __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) al[j] = pass == 0 ? h[j] : al[j] + h[j];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i = blockIdx.x * 64 + lane;
-    double t = 0.0;
-    if (i < n)
-        for (int c = wv; c < k; c += 4) t += Q[c * ldq + i] * h[c];
-    ws[wv][lane] = t;
-    __syncthreads();
-    if (wv == 0 && i < n) y[i] -= ((ws[0][lane] + ws[1][lane]) + ws[2][lane]) + ws[3][lane];
-}
-// bw2[j] = ||y||^2 (the last block sums the partials in block order and advances j)
-__global__ void __launch_bounds__(kBlock) k_lz_norm(int n, const double *Q, double *w0, double *w1, int *jp,
-                                                    double *part, unsigned *ticket, double *bw2) {
-    const int j = *jp;
-    const double *w;
-    double *y;
-    lz_bufs(j, Q, w0, w1, &w, &y);
     double acc[1] = {0.0};
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) acc[0] += y[i] * y[i];
-    partials_finalize<1>(acc, part, ticket, bw2 + j, jp);
+    for (int i0 = blockIdx.x * 64; i0 < n; i0 += gridDim.x * 64) {   // block-uniform
+        const int i = i0 + lane;
+        double t = 0.0;
+        if (i < n)
+            for (int c = wv; c < k; c += 4) t += Q[c * ldq + i] * h[c];
+        ws[wv][lane] = t;
+        __syncthreads();
+        if (wv == 0 && i < n) {
+            const double v = y[i] - (((ws[0][lane] + ws[1][lane]) + ws[2][lane]) + ws[3][lane]);
+            y[i] = v;
+            acc[0] += v * v;
+        }
+        __syncthreads();
+    }
+    if (pass == 1) partials_finalize<1>(acc, npart, ticket, bw2 + j, jp);
 }
 
 static unsigned *ticket_ptr(int id);
@@ -2857,32 +2834,25 @@ int launch_lanczos_step(const DevProblem &P, int cone, const double *S, int kmax
         return -1;
     }
     const double deg = c.n > 0 ? (double)c.adj_nnz / c.n : 0.0;
-    int ga;
     if (deg > 32.0) {
-        ga = std::max(1, std::min(256, (n + kBlock / 64 - 1) / (kBlock / 64)));
+        const int ga = std::max(1, std::min(256, (n + kBlock / 64 - 1) / (kBlock / 64)));
         hipLaunchKernelGGL(k_lz_symv<true>, dim3(ga), dim3(kBlock), 0, st, n, c.adj_ptr, c.adj_col, c.adj_slot, S, w0,
-                           w1, bw2, jp, Q, ldq, part);
+                           w1, bw2, jp, Q, ldq);
     } else {
-        ga = std::max(1, std::min(256, (n + kBlock - 1) / kBlock));
+        const int ga = std::max(1, std::min(256, (n + kBlock - 1) / kBlock));
         hipLaunchKernelGGL(k_lz_symv<false>, dim3(ga), dim3(kBlock), 0, st, n, c.adj_ptr, c.adj_col, c.adj_slot, S, w0,
-                           w1, bw2, jp, Q, ldq, part);
+                           w1, bw2, jp, Q, ldq);
     }
     LRS_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_lz_update, dim3(grid_elems(n, 1)), dim3(kBlock), 0, st, n, w0, w1, Q, ldq, jp, part, ga, al,
-                       bw2);
-    LRS_CHECK_LAUNCH();
     const int nb = std::max(1, std::min(64, (n + kBlock * 8 - 1) / (kBlock * 8)));
-    double *gpart = part + kMaxPartialBlocks;   // past the alpha partials
+    double *gpart = part + kMaxPartialBlocks;   // past the norm partials
     for (int t = 0; t < 2; ++t) {
         hipLaunchKernelGGL(k_lz_gemvt_part, dim3(nb, kmax), dim3(kBlock), 0, st, n, Q, ldq, w0, w1, jp, gpart);
         LRS_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_lz_gemv_sub, dim3((n + 63) / 64), dim3(kBlock), 0, st, n, Q, ldq, w0, w1, jp, gpart,
-                           nb);
+        hipLaunchKernelGGL(k_lz_gemv_sub, dim3(std::min((n + 63) / 64, kMaxPartialBlocks)), dim3(kBlock), 0, st, n,
+                           Q, ldq, w0, w1, jp, gpart, nb, t, al, part, ticket_ptr(T_DOT), bw2);
         LRS_CHECK_LAUNCH();
     }
-    hipLaunchKernelGGL(k_lz_norm, dim3(grid_elems(n, 8)), dim3(kBlock), 0, st, n, Q, w0, w1, jp, part,
-                       ticket_ptr(T_DOT), bw2);
-    LRS_CHECK_LAUNCH();
     return 0;
 }
 

@@ -688,30 +688,37 @@ static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int 
         HIPC(hipMemcpyAsync(Q, q0.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->st));
         HIPC(hipStreamSynchronize(c->st));
     }
-    // one step's launches, captured once and replayed (the step index lives on the device)
-    hipGraph_t g = nullptr;
-    hipGraphExec_t ge = nullptr;
-    if (hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal) != hipSuccess) rc = -1;
-    if (rc == 0) {
-        const int lr = launch_lanczos_step(c->dp, k, S, kmax, Q, n, w0, w1, jp, al_d, bw2_d, part, c->st);
-        if (hipStreamEndCapture(c->st, &g) != hipSuccess || lr) rc = -1;
+    // one step's launches and a chunk of kChunk steps, each captured once and replayed (the
+    // step index lives on the device, so every step's launches are the same)
+    constexpr int kChunk = 16, kLzTestEvery = 4;
+    hipGraph_t g[2] = {nullptr, nullptr};
+    hipGraphExec_t ge[2] = {nullptr, nullptr};
+    for (int q = 0; q < 2 && rc == 0; ++q) {
+        if (hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal) != hipSuccess) { rc = -1; break; }
+        int lr = 0;
+        for (int t = 0; t < (q == 0 ? 1 : kChunk) && lr == 0; ++t)
+            lr = launch_lanczos_step(c->dp, k, S, kmax, Q, n, w0, w1, jp, al_d, bw2_d, part, c->st);
+        if (hipStreamEndCapture(c->st, &g[q]) != hipSuccess || lr) rc = -1;
+        if (rc == 0 && hipGraphInstantiate(&ge[q], g[q], nullptr, nullptr, 0) != hipSuccess) rc = -1;
     }
-    if (rc == 0 && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) != hipSuccess) rc = -1;
     // Steps run on the device in chunks (alpha_j, ||w_j||^2 stay in device memory); the host
     // fetches a chunk's coefficients and applies the stopping test step by step (every
     // kLzTestEvery steps: the Sturm bisection is the host's cost).  Converged: Ritz residual
     // beta_j |e_j^T y| <= 1e-4 max(|theta|, 1e-10 ||T||) -- the reference's ARPACK test
     // (|r| <= tol |theta|, dsaupd tol 1e-2, data/lorads_sdp_conic.c:1636-1699) 100x tighter --;
     // breakdown beta_j <= 1e-14 ||T||; or the step cap.
-    constexpr int kChunk = 16, kLzTestEvery = 4;
     std::vector<double> al, be, alc(kChunk), bwc(kChunk);
     double theta = 0.0, tnorm = 0.0;   // tnorm: Gershgorin bound of T (~ ||S||)
     int j = 0;
     bool done = false;
     while (!done && rc == 0) {
         const int j0 = j, j1 = std::min(kmax, j0 + kChunk);
-        for (int t = j0; t < j1 && rc == 0; ++t)
-            if (hipGraphLaunch(ge, c->st) != hipSuccess) rc = -1;
+        if (j1 - j0 == kChunk) {
+            if (hipGraphLaunch(ge[1], c->st) != hipSuccess) rc = -1;
+        } else {
+            for (int t = j0; t < j1 && rc == 0; ++t)
+                if (hipGraphLaunch(ge[0], c->st) != hipSuccess) rc = -1;
+        }
         if (rc) break;
         if (hipMemcpyAsync(alc.data(), al_d + j0, sizeof(double) * (j1 - j0), hipMemcpyDeviceToHost, c->st) !=
                 hipSuccess ||
@@ -744,8 +751,10 @@ static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int 
         if (!done) j = j1;
     }
     if (rc) set_err("lanczos: %s", last_device_error());
-    if (ge) (void)hipGraphExecDestroy(ge);
-    if (g) (void)hipGraphDestroy(g);
+    for (int q = 0; q < 2; ++q) {
+        if (ge[q]) (void)hipGraphExecDestroy(ge[q]);
+        if (g[q]) (void)hipGraphDestroy(g[q]);
+    }
     (void)hipStreamSynchronize(c->st);
     (void)hipFree(Q); (void)hipFree(w0); (void)hipFree(w1); (void)hipFree(part); (void)hipFree(coef);
     (void)hipFree(jp);
