@@ -3362,9 +3362,12 @@ struct StagePlan {
 // groups while every group still gets two unrolled chunks and the chip is not
 // oversubscribed (dense rows, e.g. the Lovasz theta objective, n ~ 100s).
 static int team_size(const DevCone &c, double deg, int U) {
+    // largest power of two with at least one full U-unrolled round of entries per member
+    // (theta3's 150-entry rows: T = 16, stages A/B 13.6/17.1 -> 12.0/13.7 us against T = 8)
     const long cap_threads = 256L * 2048;
     int T = 1;
-    while (T * 2 <= kRowBlock / c.G && (double)(T * 2 * U * 2) <= deg && (long)c.nown * T * 2 * c.G <= cap_threads) T *= 2;
+    while (T * 2 <= kRowBlock / c.G && (double)(T * 2 * U) <= deg && (long)c.nown * T * 2 * c.G <= cap_threads)
+        T *= 2;
     return T;
 }
 // LRS_FORCE_REGIME=small|large overrides the choice (tests run the bandwidth-regime code
