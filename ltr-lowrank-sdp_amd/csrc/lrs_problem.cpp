@@ -96,7 +96,12 @@ bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err) {
             bool blank = true;
             for (char c : line) if (c != ' ' && c != '\t' && c != '\r') blank = false;
             if (blank) continue;
-            break;
+            // the reference stops at the 'BEGIN.COMMENT' trailer or at end of file (a last line
+            // without a newline), and rejects any other line that is not an entry
+            // (io/lorads_file_io.c:264-279)
+            if (line.compare(0, 13, "BEGIN.COMMENT") == 0 || pos > s.size()) break;
+            err = "bad entry line: " + line.substr(0, 80);
+            return false;
         }
         ib -= 1; ii -= 1; ij -= 1;
         if (std::fabs(v) < 1e-12) continue;                 // :288-294

@@ -302,7 +302,11 @@ oproblem *oracle_read(const char *path) {
             int blank = 1;
             for (char *q = line; *q; ++q) if (*q != ' ' && *q != '\t' && *q != '\r') blank = 0;
             if (blank) continue;
-            break;
+            /* :264-279: stop at the 'BEGIN.COMMENT' trailer or at end of file (a last line
+               without a newline: next_line leaves it unterminated), else reject */
+            if (strncmp(line, "BEGIN.COMMENT", 13) == 0 || (t.pos >= t.len && t.s[t.len - 1] != '\0')) break;
+            free(t.s); free(dims); free(b); free(ent); free(blk);
+            return NULL;
         }
         ib -= 1; ii -= 1; ij -= 1;
         if (fabs(v) < 1e-12) continue;                        /* :288-294 */

@@ -78,9 +78,13 @@ def oracle_kernels(lib, name):
 
 
 def oracle_solve(lib, name, flags):
+    return oracle_solve_path(lib, instance(name), flags)
+
+
+def oracle_solve_path(lib, path, flags):
     arr = (C.c_char_p * len(flags))(*[f.encode() for f in flags])
     res = (C.c_double * 16)()
-    rc = lib.oracle_solve(instance(name).encode(), len(flags), arr, res)
+    rc = lib.oracle_solve(str(path).encode(), len(flags), arr, res)
     assert rc == 0
     keys = ["alm_inner", "alm_outer", "alm_pobj", "alm_dobj", "alm_pinf", "alm_gap", "alm_rho", "admm_iter",
             "admm_pobj", "admm_dobj", "admm_pinf", "admm_gap", "admm_rho", "solve_time", "rank", "alm_time"]
