@@ -520,27 +520,37 @@ static int read_tmpfin(lrs_ctx *c, int idx, int n, double *out) {
     return 0;
 }
 
+// several tmpfin ranges behind one stream sync (staged at hpin + 1024, clear of the
+// ALM mirror slots and the CG poll): out = [idx1, idx1 + n1) ++ [idx2, idx2 + n2)
+static int read_tmpfin2(lrs_ctx *c, int idx1, int n1, int idx2, int n2, double *out) {
+    double *h = c->hpin + 1024;
+    HIPC(hipMemcpyAsync(h, device_tmpfin() + idx1, sizeof(double) * n1, hipMemcpyDeviceToHost, c->st));
+    if (n2 > 0)
+        HIPC(hipMemcpyAsync(h + n1, device_tmpfin() + idx2, sizeof(double) * n2, hipMemcpyDeviceToHost, c->st));
+    HIPC(hipStreamSynchronize(c->st));
+    for (int i = 0; i < n1 + n2; ++i) out[i] = h[i];
+    if (sharded(c)) return c->comm->allreduce_host(c, out, n1 + n2);
+    return 0;
+}
+
 // ------------------------------------------------------------------------
 // host-driven operators
 // ------------------------------------------------------------------------
 // A(X X^T) for every cone -> cvc[k], cvs = sum_k, returns pinf (primalInfeasibility)
 // and the objective <C, X X^T> (unscaled), with X given per-cone rows in factor buffer.
-static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pinf, double *obj) {
+// blam != nullptr: also b^T lambda (tmpfin TF_DOT), read behind the same sync
+static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pinf, double *obj,
+                        double *blam = nullptr) {
     DevProblem &P = c->dp;
     DevWork &W = c->W;
-    double o = 0.0;
-    for (int k = 0; k < P.K; ++k) {
+    // every cone's <C, X Y^T> (tmpfin TF_SD + 2k) and the residual norm in one read
+    for (int k = 0; k < P.K; ++k)
         OPC(launch_sddmm(P, k, Y ? 0 : 1, X, Y, W.uvt2, nullptr, W.part, 0, nullptr, c->st));
-        double t[2];
-        if (read_tmpfin(c, TF_SD + 2 * k, 1, t)) return -1;
-        o += t[0];
-    }
+    int fin;
     if (P.K == 1) {
         OPC(launch_gather(P, W.uvt2, 1.0, W.cvs, P.b, W.part, c->st, nullptr));
         HIPC(hipMemcpyAsync(W.cvc, W.cvs, sizeof(double) * P.m, hipMemcpyDeviceToDevice, c->st));
-        double v;
-        if (read_tmpfin(c, TF_GATHER, 1, &v)) return -1;
-        if (pinf) *pinf = std::sqrt(v) / (1 + c->hp.bNrm1);
+        fin = TF_GATHER;
     } else {
         OPC(launch_fill(P.m, 0.0, W.cvs, c->st));
         for (int k = 0; k < P.K; ++k) {
@@ -548,10 +558,15 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
             OPC(launch_axpby(P.m, 1.0, W.cvc + (long)k * P.m, 1.0, W.cvs, c->st));
         }
         OPC(launch_resid(P.m, P.b, W.cvs, c->st));
-        double v;
-        if (read_tmpfin(c, TF_RESID, 1, &v)) return -1;
-        if (pinf) *pinf = std::sqrt(v) / (1 + c->hp.bNrm1);
+        fin = TF_RESID;
     }
+    if (blam) OPC(launch_dot(P.m, P.b, W.lam, W.part, c->st, nullptr));
+    double t[2 * 64 + 3];
+    if (read_tmpfin2(c, TF_SD, 2 * P.K, TF_GATHER, 3, t)) return -1;   // GATHER, RESID, DOT
+    double o = 0.0;
+    for (int k = 0; k < P.K; ++k) o += t[2 * k];
+    if (pinf) *pinf = std::sqrt(t[2 * P.K + (fin - TF_GATHER)]) / (1 + c->hp.bNrm1);
+    if (blam) *blam = t[2 * P.K + (TF_DOT - TF_GATHER)];
     if (obj) *obj = o;
     return 0;
 }
@@ -562,12 +577,13 @@ static int op_grad(lrs_ctx *c, double rho, double *lag) {
     DevWork &W = c->W;
     OPC(launch_alm_m1(P, rho, W.lam, W.cvs, W.M1, c->st));
     OPC(launch_wsum(P, W.M1, 1, W.S, c->st));
+    for (int k = 0; k < P.K; ++k)
+        OPC(launch_spmm(P, k, W.S, W.R, 2.0, nullptr, 0.0, W.G[c->gcur], W.part, 0, nullptr, c->st));
+    double v[TF_N - TF_SPMM];
+    if (read_tmpfin2(c, TF_SPMM, P.K, 0, 0, v)) return -1;
     double tot = 0.0;
     for (int k = 0; k < P.K; ++k) {
-        OPC(launch_spmm(P, k, W.S, W.R, 2.0, nullptr, 0.0, W.G[c->gcur], W.part, 0, nullptr, c->st));
-        double v;
-        if (read_tmpfin(c, TF_SPMM + k, 1, &v)) return -1;
-        double nrm = std::sqrt(v);
+        double nrm = std::sqrt(v[k]);
         tot += nrm * nrm;
     }
     *lag = tot;
@@ -1502,21 +1518,23 @@ static int admm_update_var(lrs_ctx *c, double rho, double tol, int maxit) {
     return 0;
 }
 
-static int cal_obj_admm(lrs_ctx *c) {   // LORADSCalObjUV_ADMM lorads_admm.c:398-410
-    OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
-    double o = 0;
-    for (int k = 0; k < c->dp.K; ++k) {
-        OPC(launch_sddmm(c->dp, k, 1, c->W.R, nullptr, c->W.uvt0, nullptr, c->W.part, 0, nullptr, c->st));
-        double t;
-        if (read_tmpfin(c, TF_SD + 2 * k, 1, &t)) return -1;
-        o += t;
-    }
-    c->pObjVal = o / c->scaleObjHis;
-    return 0;
-}
 static int update_dimacs_admm(lrs_ctx *c) {   // lorads_alg_common.c:454-462
     OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
     return update_dimacs(c, c->W.R, nullptr, false);
+}
+// LORADSCalObjUV_ADMM (lorads_admm.c:398-410) + cal_dual_obj + update_dimacs_admm (lorads_admm.c:155-157) in one pass: the
+// objective <C, R R^T> of R = (U + V) / 2 comes out of the same SDDMM as A(R R^T), so the
+// three evaluations share one set of launches and one host read
+static int admm_eval(lrs_ctx *c) {
+    OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
+    double pinf, obj, blam;
+    if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj, &blam)) return -1;
+    c->pObjVal = obj / c->scaleObjHis;
+    c->dObjVal = blam / c->scaleObjHis;
+    c->dimPinf = pinf;
+    const double gap = c->pObjVal - c->dObjVal;
+    c->dimGap = std::fabs(gap) / (1 + std::fabs(c->pObjVal) + std::fabs(c->dObjVal));
+    return 0;
 }
 
 static void admm_log(lrs_ctx *c, const lrs_params *p, const AdmmState &st, double t) {
@@ -1545,9 +1563,7 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
             OPC(launch_axpby(P.m, 1.0, c->W.cvc + (long)k * P.m, 1.0, c->W.cvs, c->st));
         }
     }
-    if (cal_obj_admm(c)) return -1;
-    cal_dual_obj(c);
-    if (update_dimacs_admm(c)) return -1;
+    if (admm_eval(c)) return -1;
     st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.gap = c->dimGap; st.pinf1 = c->dimPinf;
     st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
     double cur_rho_max = p->rhoMax, old_mean = 1e30, buf[10] = {0};
@@ -1560,9 +1576,7 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
         const double cgtol = std::min(st.pinf1 * (reopt ? 1e-4 : 1e-2), 1e-8);
         if (admm_update_var(c, st.rho, cgtol, maxCG)) return -1;
         st.cg_iter = c->cgIterTotal;
-        if (cal_obj_admm(c)) return -1;
-        cal_dual_obj(c);
-        if (update_dimacs_admm(c)) return -1;
+        if (admm_eval(c)) return -1;
         st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.pinf1 = c->dimPinf;
         st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
         st.gap = c->dimGap;
