@@ -378,6 +378,50 @@ __device__ __forceinline__ double auv_entry(const double *__restrict__ X, const 
     return d;
 }
 
+// Long constraint rows (> kLongRow entries in this cone, e.g. a trace constraint): a
+// block per constraint, its kBlock/G lane groups striding over the entries (two entries'
+// loads in flight per group; the sum keeps the entry order).
+template <int G, int E, int MODE>
+__device__ __forceinline__ void auv_long_rows(int blk, int nblk, int nlong, const int *__restrict__ long_rows,
+                                              int m, int cone, int ld, const int *__restrict__ con_ptr,
+                                              const int *__restrict__ con_slot, const double *__restrict__ con_w,
+                                              const int *__restrict__ slot_rc, const double *__restrict__ X,
+                                              const double *__restrict__ Y, double scale, int accumulate,
+                                              double *__restrict__ out) {
+    __shared__ double wsum4[kBlock / 64];
+    constexpr int NG = kBlock / G;   // lane groups of the block, striding over the entries
+    const int lane = threadIdx.x & (G - 1);
+    const int gq = threadIdx.x / G;
+    for (int t = blk; t < nlong; t += nblk) {   // block-uniform
+        const int i = long_rows[t];
+        const long row = (long)cone * m + i;
+        const int e0 = con_ptr[row], e1 = con_ptr[row + 1];
+        double v = 0.0;
+        for (int e = e0 + gq; e < e1; e += 2 * NG) {
+            // two entries' loads in flight, summed in entry order (group-uniform has1)
+            const bool has1 = e + NG < e1;
+            const int s0 = con_slot[e], s1 = has1 ? con_slot[e + NG] : s0;
+            double d0 = auv_entry<E, MODE>(X, Y, ld, lane, slot_rc[2 * s0], slot_rc[2 * s0 + 1]);
+            double d1 = auv_entry<E, MODE>(X, Y, ld, lane, slot_rc[2 * s1], slot_rc[2 * s1 + 1]);
+            d0 = group_sum<G>(d0);
+            d1 = group_sum<G>(d1);
+            v += con_w[e] * d0;
+            if (has1) v += con_w[e + NG] * d1;
+        }
+        v = wave_sum(lane == 0 ? v : 0.0);
+        if ((threadIdx.x & 63) == 0) wsum4[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double w = 0.0;
+            for (int q = 0; q < kBlock / 64; ++q) w += wsum4[q];
+            double tot = w * scale;
+            if (accumulate) tot = out[i] + tot;
+            out[i] = tot;
+        }
+        __syncthreads();
+    }
+}
+
 template <int G, int E, int MODE>
 __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int ld, const int *__restrict__ con_ptr,
                                                     const int *__restrict__ con_slot,
@@ -386,16 +430,24 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
                                                     const double *__restrict__ X, const double *__restrict__ Y,
                                                     double scale, int accumulate, double *__restrict__ out,
                                                     const double *__restrict__ b, double *part, unsigned *ticket,
-                                                    double *fin, const double *__restrict__ guard) {
+                                                    double *fin, const double *__restrict__ guard, int nrowblk,
+                                                    int nlong, const int *__restrict__ long_rows) {
     if (guard && guard[0] == 0.0) return;
+    double acc[1] = {0.0};
+    if ((int)blockIdx.x >= nrowblk) {
+        // the blocks past the row blocks take the long rows (one launch for both)
+        auv_long_rows<G, E, MODE>(blockIdx.x - nrowblk, gridDim.x - nrowblk, nlong, long_rows, m, cone, ld, con_ptr,
+                                  con_slot, con_w, slot_rc, X, Y, scale, accumulate, out);
+        if (part) partials_finalize<1>(acc, part, ticket, fin);
+        return;
+    }
     const int lane = threadIdx.x & (G - 1);
     const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
-    const int ngrp = gridDim.x * kBlock / G;
-    double acc[1] = {0.0};
+    const int ngrp = nrowblk * kBlock / G;
     for (int i = grp; i < m; i += ngrp) {
         const long row = (long)cone * m + i;
         const int2 pq = reinterpret_cast<const int2 *>(con1_pq)[row];
-        if (pq.x == -2) continue;   // long row: k_auv_con_long
+        if (pq.x == -2) continue;   // long row: the blocks past nrowblk
         double v = 0.0;
         if (pq.x >= 0) {
             // single-entry row: (p, q, w) in one coalesced load, then the factor rows
@@ -421,47 +473,6 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
         }
     }
     if (part) partials_finalize<1>(acc, part, ticket, fin);
-}
-
-// Long constraint rows (> kLongRow entries in this cone, e.g. a trace constraint): a
-// wave per constraint, its 64/G lane groups striding over the entries.
-template <int G, int E, int MODE>
-__global__ void __launch_bounds__(kBlock) k_auv_con_long(int nlong, const int *__restrict__ long_rows, int m,
-                                                         int cone, int ld, const int *__restrict__ con_ptr,
-                                                         const int *__restrict__ con_slot,
-                                                         const double *__restrict__ con_w,
-                                                         const int *__restrict__ slot_rc,
-                                                         const double *__restrict__ X, const double *__restrict__ Y,
-                                                         double scale, int accumulate, double *__restrict__ out,
-                                                         const double *__restrict__ guard) {
-    if (guard && guard[0] == 0.0) return;
-    __shared__ double wsum4[kBlock / 64];
-    constexpr int NG = kBlock / G;   // lane groups of the block, striding over the entries
-    const int lane = threadIdx.x & (G - 1);
-    const int gq = threadIdx.x / G;
-    for (int t = blockIdx.x; t < nlong; t += gridDim.x) {   // block-uniform
-        const int i = long_rows[t];
-        const long row = (long)cone * m + i;
-        const int e0 = con_ptr[row], e1 = con_ptr[row + 1];
-        double v = 0.0;
-        for (int e = e0 + gq; e < e1; e += NG) {
-            const int s = con_slot[e];
-            double d = auv_entry<E, MODE>(X, Y, ld, lane, slot_rc[2 * s], slot_rc[2 * s + 1]);
-            d = group_sum<G>(d);
-            v += con_w[e] * d;
-        }
-        v = wave_sum(lane == 0 ? v : 0.0);
-        if ((threadIdx.x & 63) == 0) wsum4[threadIdx.x >> 6] = v;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double w = 0.0;
-            for (int q = 0; q < kBlock / 64; ++q) w += wsum4[q];
-            double tot = w * scale;
-            if (accumulate) tot = out[i] + tot;
-            out[i] = tot;
-        }
-        __syncthreads();
-    }
 }
 
 // S[slot] = (withC ? Craw : 0) + sum w[con] a
@@ -3202,7 +3213,6 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
                    int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st,
                    const double *guard) {
     const DevCone &c = P.cones[cone];
-    const int grid = grid_rows(P.m, c.G);
     const double *Xc = X + c.foff;
     const double *Yc = Y ? Y + c.foff : nullptr;
     unsigned *tk = ticket_ptr(T_GATHER);
@@ -3213,26 +3223,19 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
         snprintf(g_err, sizeof(g_err), "auv_con: residual with long constraint rows is not supported");
         return -1;
     }
+    // row blocks, then a block per long row (at most 64 of them, striding past that)
+    const int nlb = std::min(nlong, 64);
+    const int grid = std::min(grid_rows(P.m, c.G), kMaxPartialBlocks - nlb);
+    const int *lrows = nlong > 0 ? P.long_rows + l0 : nullptr;
     LRS_LAYOUT_SWITCH(c.G, c.E, {
         if (mode == 1)
-            hipLaunchKernelGGL((k_auv_con<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
+            hipLaunchKernelGGL((k_auv_con<GG, EE, 1>), dim3(grid + nlb), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
                                P.con_ptr, P.con_slot, P.con_w, P.slot_rc, P.con1_pq, P.con1_w, Xc, Yc, scale,
-                               accumulate, out, b_for_vio, vio_part, tk, fin, guard);
+                               accumulate, out, b_for_vio, vio_part, tk, fin, guard, grid, nlong, lrows);
         else
-            hipLaunchKernelGGL((k_auv_con<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
+            hipLaunchKernelGGL((k_auv_con<GG, EE, 0>), dim3(grid + nlb), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
                                P.con_ptr, P.con_slot, P.con_w, P.slot_rc, P.con1_pq, P.con1_w, Xc, Yc, scale,
-                               accumulate, out, b_for_vio, vio_part, tk, fin, guard);
-        if (nlong > 0) {
-            const int gl = std::min(nlong, kMaxPartialBlocks);
-            if (mode == 1)
-                hipLaunchKernelGGL((k_auv_con_long<GG, EE, 1>), dim3(gl), dim3(kBlock), 0, st, nlong,
-                                   P.long_rows + l0, P.m, cone, c.ld, P.con_ptr, P.con_slot, P.con_w, P.slot_rc, Xc,
-                                   Yc, scale, accumulate, out, guard);
-            else
-                hipLaunchKernelGGL((k_auv_con_long<GG, EE, 0>), dim3(gl), dim3(kBlock), 0, st, nlong,
-                                   P.long_rows + l0, P.m, cone, c.ld, P.con_ptr, P.con_slot, P.con_w, P.slot_rc, Xc,
-                                   Yc, scale, accumulate, out, guard);
-        }
+                               accumulate, out, b_for_vio, vio_part, tk, fin, guard, grid, nlong, lrows);
     });
     LRS_CHECK_LAUNCH();
     return 0;
