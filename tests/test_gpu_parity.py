@@ -339,3 +339,20 @@ def test_dual_infeasibility_matches_dense_eig(solver_mod, name):
     # the solve evaluated it too (main.c:515) and reports l_inf = l_1 (1 + ||C||_1) / (1 + ||C||_inf)
     assert res["dinf"] >= 0
     assert abs(res["dinf"] - l1) <= 1e-8 * max(1.0, l1) + 1e-12
+
+
+def test_more_than_64_cones_rejected(solver_mod, tmp_path):
+    """The per-cone scalars live in fixed device slots (lrs_device.h TmpFinIdx): at most 64
+    SDP cones, refused at load with a message instead of overrunning those slots."""
+    def write(nb):
+        lines = ["1", str(nb), " ".join(["2"] * nb), "1.0"]
+        for k in range(1, nb + 1):
+            lines += [f"0 {k} 1 1 1.0", f"1 {k} 1 1 1.0", f"1 {k} 2 2 1.0"]
+        p = tmp_path / f"blocks{nb}.dat-s"
+        p.write_text("\n".join(lines) + "\n")
+        return str(p)
+    sv = solver_mod.Solver(write(64))
+    assert len(sv.dims) == 64
+    sv.close()
+    with pytest.raises(RuntimeError, match="64 SDP cones"):
+        solver_mod.Solver(write(65))
