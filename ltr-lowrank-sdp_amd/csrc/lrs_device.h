@@ -195,7 +195,7 @@ int launch_gather(const DevProblem &P, const double *uvt, double scale, double *
 // residual sum (b - out)^2 -> tmpfin TF_GATHER.  Bitwise equal to sddmm + gather_cone.
 int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double scale,
                    int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st,
-                   const double *guard = nullptr);
+                   const double *guard = nullptr, double *sum_upd = nullptr);   // sum_upd[i] += new - old out[i]
 // S[slot] = (withC ? Craw[slot] : 0) + sum_(con,a) w[con] * a
 int launch_wsum(const DevProblem &P, const double *w, int withC, double *S, hipStream_t st);
 // out = scale * S X (+ addX * X) per cone, partial ||out||^2 -> part[0][pblk_off+b]

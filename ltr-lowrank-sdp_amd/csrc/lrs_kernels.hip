@@ -387,7 +387,7 @@ __device__ __forceinline__ void auv_long_rows(int blk, int nblk, int nlong, cons
                                               const int *__restrict__ con_slot, const double *__restrict__ con_w,
                                               const int *__restrict__ slot_rc, const double *__restrict__ X,
                                               const double *__restrict__ Y, double scale, int accumulate,
-                                              double *__restrict__ out) {
+                                              double *__restrict__ out, double *__restrict__ sum_upd) {
     __shared__ double wsum4[kBlock / 64];
     constexpr int NG = kBlock / G;   // lane groups of the block, striding over the entries
     const int lane = threadIdx.x & (G - 1);
@@ -416,6 +416,7 @@ __device__ __forceinline__ void auv_long_rows(int blk, int nblk, int nlong, cons
             for (int q = 0; q < kBlock / 64; ++q) w += wsum4[q];
             double tot = w * scale;
             if (accumulate) tot = out[i] + tot;
+            if (sum_upd) sum_upd[i] = (sum_upd[i] - out[i]) + tot;
             out[i] = tot;
         }
         __syncthreads();
@@ -431,13 +432,14 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
                                                     double scale, int accumulate, double *__restrict__ out,
                                                     const double *__restrict__ b, double *part, unsigned *ticket,
                                                     double *fin, const double *__restrict__ guard, int nrowblk,
-                                                    int nlong, const int *__restrict__ long_rows) {
+                                                    int nlong, const int *__restrict__ long_rows,
+                                                    double *__restrict__ sum_upd) {
     if (guard && guard[0] == 0.0) return;
     double acc[1] = {0.0};
     if ((int)blockIdx.x >= nrowblk) {
         // the blocks past the row blocks take the long rows (one launch for both)
         auv_long_rows<G, E, MODE>(blockIdx.x - nrowblk, gridDim.x - nrowblk, nlong, long_rows, m, cone, ld, con_ptr,
-                                  con_slot, con_w, slot_rc, X, Y, scale, accumulate, out);
+                                  con_slot, con_w, slot_rc, X, Y, scale, accumulate, out, sum_upd);
         if (part) partials_finalize<1>(acc, part, ticket, fin);
         return;
     }
@@ -468,6 +470,7 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
         if (lane == 0) {
             double tot = v * scale;
             if (accumulate) tot = out[i] + tot;
+            if (sum_upd) sum_upd[i] = (sum_upd[i] - out[i]) + tot;   // sum += new - old
             out[i] = tot;
             if (b) { const double dd = b[i] - tot; acc[0] += dd * dd; }
         }
@@ -3211,7 +3214,7 @@ int launch_gather_cone(const DevProblem &P, int cone, const double *uvt, double 
 
 int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double scale,
                    int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st,
-                   const double *guard) {
+                   const double *guard, double *sum_upd) {
     const DevCone &c = P.cones[cone];
     const double *Xc = X + c.foff;
     const double *Yc = Y ? Y + c.foff : nullptr;
@@ -3231,11 +3234,11 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
         if (mode == 1)
             hipLaunchKernelGGL((k_auv_con<GG, EE, 1>), dim3(grid + nlb), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
                                P.con_ptr, P.con_slot, P.con_w, P.slot_rc, P.con1_pq, P.con1_w, Xc, Yc, scale,
-                               accumulate, out, b_for_vio, vio_part, tk, fin, guard, grid, nlong, lrows);
+                               accumulate, out, b_for_vio, vio_part, tk, fin, guard, grid, nlong, lrows, sum_upd);
         else
             hipLaunchKernelGGL((k_auv_con<GG, EE, 0>), dim3(grid + nlb), dim3(kBlock), 0, st, P.m, P.K, cone, c.ld,
                                P.con_ptr, P.con_slot, P.con_w, P.slot_rc, P.con1_pq, P.con1_w, Xc, Yc, scale,
-                               accumulate, out, b_for_vio, vio_part, tk, fin, guard, grid, nlong, lrows);
+                               accumulate, out, b_for_vio, vio_part, tk, fin, guard, grid, nlong, lrows, sum_upd);
     });
     LRS_CHECK_LAUNCH();
     return 0;

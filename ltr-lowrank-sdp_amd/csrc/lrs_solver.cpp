@@ -1502,9 +1502,9 @@ static int refresh_cone(lrs_ctx *c, int k) {   // lorads_alg_common.c:310-314
     DevProblem &P = c->dp;
     DevWork &W = c->W;
     double *cv = W.cvc + (long)k * P.m;
-    OPC(launch_axpby(P.m, -1.0, cv, 1.0, W.cvs, c->st));
-    OPC(launch_auv_con(P, k, 0, W.U, W.V, 1.0, 0, cv, nullptr, nullptr, c->st));
-    OPC(launch_axpby(P.m, 1.0, cv, 1.0, W.cvs, c->st));
+    // cvs = (cvs - cvc[k]) + A_k(U V^T) in the pass that rewrites cvc[k] (the same two
+    // roundings as the reference's two axpys)
+    OPC(launch_auv_con(P, k, 0, W.U, W.V, 1.0, 0, cv, nullptr, nullptr, c->st, nullptr, W.cvs));
     return 0;
 }
 
