@@ -150,6 +150,7 @@ struct lrs_ctx {
     hipEvent_t pev[2][5] = {};
     hipEvent_t bev[2] = {nullptr, nullptr};   // completion of the two batches in flight (run_inner)
     int pipe_batch = 8;                         // iterations per pipelined batch (LRS_PIPE_BATCH)
+    int cg_slack = 1;                           // CG first batch = previous count + slack (LRS_CG_SLACK)
     double *hmir = nullptr, *dmir = nullptr;    // pinned control mirror [2][64] (host / device view)
     double mseq = 0;                            // last sequence number handed to a batch
     double pacc[4] = {0, 0, 0, 0};
@@ -1459,7 +1460,7 @@ static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double 
     // first batch sized from this cone's previous solve (ADMM's CG solves take a handful of
     // iterations each; the batch past convergence runs guarded no-op launches), then doubling
     const long prev = c->cgIterCone[k];
-    int it = 0, B = prev > 0 ? (int)std::max(2L, std::min(8L, prev + 1)) : 8;
+    int it = 0, B = prev > 0 ? (int)std::max(2L, std::min(8L, prev + c->cg_slack)) : 8;
     while (it < maxit) {
         for (int j = 0; j < B && it < maxit; ++j, ++it) {
             const int par = it & 1;
@@ -1839,6 +1840,7 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); delete c; return -1; }
     if (const char *ug = getenv("LRS_GRAPHS")) c->use_graphs = (atoi(ug) != 0);
     if (const char *sv = getenv("LRS_STATS")) c->stats = (atoi(sv) != 0);
+    if (const char *cs = getenv("LRS_CG_SLACK")) c->cg_slack = std::max(0, std::min(8, atoi(cs)));
     if (const char *pb = getenv("LRS_PIPE_BATCH")) c->pipe_batch = std::max(2, std::min(64, (atoi(pb) + 1) & ~1));
     if (hipHostMalloc((void **)&c->hpin, 4096 * sizeof(double), 0) != hipSuccess) { set_err("pinned alloc failed"); delete c; return -1; }
     if (hipMalloc((void **)&c->s_tickets, 64 * sizeof(unsigned)) != hipSuccess ||
