@@ -231,14 +231,23 @@ def main():
     n = sv.dims[0]
     kw = dict(fixedRank=r, reoptLevel=0)
 
-    # warmup: W untimed inner iterations (same start point as the timed run)
-    if args.warmup > 0:
-        sv.alm_throughput(0, args.warmup, **kw)
-    replicas.barrier_sync(dist)
-    t0 = time.perf_counter()
-    out = sv.alm_throughput(0, args.steps, **kw)
-    replicas.barrier_sync(dist)
-    dt = time.perf_counter() - t0
+    # ONE phase-1 solve: W untimed warmup inner iterations (solver setup, initial point and
+    # first gradient included), then exactly K inner iterations of the same solve timed
+    # between barrier + device synchronisation on both sides (lrs_set_budget_hook)
+    clock = {}
+
+    def on_start():
+        sv.sync()
+        replicas.barrier_sync(dist)
+        clock["t0"] = time.perf_counter()
+
+    def on_stop():
+        sv.sync()
+        replicas.barrier_sync(dist)
+        clock["t1"] = time.perf_counter()
+
+    out = sv.alm_timed(max(1, args.warmup), args.steps, on_start, on_stop, **kw)
+    dt = clock["t1"] - clock["t0"]
     done = out["done"]
     done_tot, t_max = replicas.aggregate(dist, done, dt)
 
@@ -344,10 +353,13 @@ def main():
         import threading
 
         def fire():
+            # a stuck collective: print what was measured, then fail loudly (exit 3)
             if rank_id == 0:
                 line["sharded"] = {"error": f"no result within {args.sharded_timeout:.0f} s"}
                 print(json.dumps(line), flush=True)
-            os._exit(0)
+            print(f"bench.py rank {rank_id}: sharded section hung for {args.sharded_timeout:.0f} s", file=sys.stderr,
+                  flush=True)
+            os._exit(3)
         wd = threading.Timer(args.sharded_timeout, fire)
         wd.daemon = True
         wd.start()

@@ -114,7 +114,7 @@ int lrs_op_gram(lrs_ctx *ctx, int cone, int which, double *gram);
 int lrs_op_dual_infeasibility(lrs_ctx *ctx, double *l1, double *lam_min);
 
 /* ---- whole solves ---- */
-/* main.c:380-610 flow (reoptLevel>=1 restarts not yet on the device path: see DESIGN.md). */
+/* main.c:380-610 flow: ALM phase, ADMM phase, reoptLevel 1/2 rounds, dual infeasibility. */
 int lrs_solve(lrs_ctx *ctx, const lrs_params *p, lrs_result *res);
 /* trajectory (phase 1 then phase 2) after lrs_solve: curr and oracle ranks */
 int lrs_trajectory(lrs_ctx *ctx, int phase, int *curr_rank, int *oracle_rank, int cap);
@@ -129,12 +129,32 @@ int lrs_write_json(lrs_ctx *ctx, const char *path, const char *problem_id, const
 int lrs_alm_throughput(lrs_ctx *ctx, const lrs_params *p, long warmup, long steps, double *seconds,
                        long *done, double *sddmm_avg_ms, double *iter_avg_ms);
 
+/* Benchmark hook on the phase-1 budget (lrs_params.almInnerBudget): when the ALM inner
+ * loop reaches the budget, the solve synchronises its stream and calls
+ * hook(user, inner_iterations_done).  A return value larger than the count continues the
+ * SAME solve (same iterate, L-BFGS ring and control block) up to that new absolute budget;
+ * anything else ends phase 1 as without a hook.  This lets a caller time exactly K inner
+ * iterations after W warmup iterations with no solver setup inside the timed region.
+ * NULL removes the hook.  (No reference counterpart: benchmarking only.) */
+typedef long (*lrs_budget_hook)(void *user, long inner_done);
+int lrs_set_budget_hook(lrs_ctx *ctx, lrs_budget_hook hook, void *user);
+/* The last completed ALM inner iteration of the last solve (after a budget stop: trip
+ * almInnerBudget): out4 = {tau, ||G||^2, l_1 primal infeasibility, beta of the newest
+ * L-BFGS pair}; newest_pair = 0 if that pair is (LRS_S0, LRS_Y0), 1 if (LRS_S1, LRS_Y1).
+ * (Test hook for the per-iteration parity against the reference's inner loop,
+ * lorads_alm.c:1302-1379.) */
+int lrs_alm_last_step(lrs_ctx *ctx, double *out4, int *newest_pair);
+/* Wait for every operation enqueued on the context's stream. */
+int lrs_sync(lrs_ctx *ctx);
+
 /* Mirror the iteration log into a file (the reference's --logfile). */
 int lrs_set_log_path(lrs_ctx *ctx, const char *path);
 
 /* Kernel selection of the ALM inner iteration (same arithmetic either way):
  * 0 = automatic (the latency-regime kernels k_lat_a/k_lat_b when every row's lane group is
- * resident at once, else the general row kernels), 1 = general row kernels only.
+ * resident at once, else the general row kernels), 1 = general row kernels only,
+ * 2 = general row kernels in their bandwidth-regime form (stages split in two launches),
+ * 3 = as 2 with the long-row neighbour kernels k_wide_a/k_wide_b wherever the layout allows.
  * The environment variable LRS_NO_LAT=1 forces 1 for every context. */
 int lrs_set_kernel_path(lrs_ctx *ctx, int path);
 /* The path the last enqueued ALM inner iteration of this context took (0 latency-regime

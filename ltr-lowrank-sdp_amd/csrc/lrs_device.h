@@ -119,7 +119,7 @@ struct ShardHooks {
 
 struct DevProblem {
     const ShardHooks *shard = nullptr;   // non-null in a sharded solve
-    int no_lat = 0;                      // 1: never the latency-regime iteration kernels
+    int no_lat = 0;                      // kernel path (lrs_set_kernel_path): 1 never the latency kernels, 2 + bandwidth regime, 3 + long-row kernels
     mutable int last_path = -1;          // path of the last enqueued iteration (0 lat, 1 general)
     int m = 0, K = 0;
     long NRpad = 0;     // factor buffer length (doubles)

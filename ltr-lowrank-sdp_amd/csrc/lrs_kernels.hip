@@ -3386,12 +3386,13 @@ static int forced_regime() {
     }
     return v;
 }
-static StagePlan plan_stage(long rows_threads, int res_small, int res_large, int K, int T) {
+// force: the context's kernel path (lrs_set_kernel_path): >= 2 forces the bandwidth regime
+static StagePlan plan_stage(long rows_threads, int res_small, int res_large, int K, int T, int force) {
     StagePlan p;
     p.T = T;
     const long need = std::max(1L, (rows_threads * T + kRowBlock - 1) / kRowBlock);
     const int cap = std::max(1, kMaxPartialBlocks / std::max(1, K));
-    const int fr = forced_regime();
+    const int fr = force >= 2 ? 2 : forced_regime();
     if (fr == 2) { p.grid = (int)std::max(1L, std::min<long>(std::min<long>(need, res_large), cap)); p.small = false; return p; }
     if (fr == 1) { p.grid = (int)std::max(1L, std::min<long>(need, cap)); p.small = true; return p; }
     if (need <= res_small) { p.grid = (int)std::min<long>(need, cap); p.small = true; }
@@ -3399,18 +3400,20 @@ static StagePlan plan_stage(long rows_threads, int res_small, int res_large, int
     p.grid = std::max(1, p.grid);
     return p;
 }
-static int plan_a(const DevCone &c, int K, StagePlan &p) {
+// force == 3 (lrs_set_kernel_path): the long-row neighbour kernels k_wide_a / k_wide_b on
+// every row the layout allows (tests run them on short rows that way)
+static int plan_a(const DevCone &c, int K, StagePlan &p, int force) {
     const double deg = c.nown > 0 ? (double)c.P / c.nown : 0.0;    // lower entries per row
     const int T = team_size(c, deg, 2);
-    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_a<GG, EE, 2>(), res_a<GG, EE, 1>(), K, T); });
-    p.wide = !p.small && deg / T >= 32.0 && c.E <= 2;
+    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_a<GG, EE, 2>(), res_a<GG, EE, 1>(), K, T, force); });
+    p.wide = !p.small && (deg / T >= 32.0 || force == 3) && c.E <= 2;
     return 0;
 }
-static int plan_b(const DevCone &c, int K, StagePlan &p) {
+static int plan_b(const DevCone &c, int K, StagePlan &p, int force) {
     const double deg = c.nown > 0 ? (double)c.adj_nnz / c.nown : 0.0;
     const int T = team_size(c, deg, 4);
-    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_b<GG, EE, 4>(), res_b<GG, EE, 1>(), K, T); });
-    p.wide = !p.small && deg / T >= 64.0 && c.E <= 2;
+    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_b<GG, EE, 4>(), res_b<GG, EE, 1>(), K, T, force); });
+    p.wide = !p.small && (deg / T >= 64.0 || force == 3) && c.E <= 2;
     return 0;
 }
 
@@ -3474,7 +3477,7 @@ static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &
 bool alm_stage_a_split(const DevProblem &P) {
     for (int k = 0; k < P.K; ++k) {
         StagePlan pa;
-        if (plan_a(P.cones[k], P.K, pa)) return false;
+        if (plan_a(P.cones[k], P.K, pa, P.no_lat)) return false;
         if (!pa.small) return true;
     }
     return false;
@@ -3484,7 +3487,7 @@ bool alm_stage_a_split(const DevProblem &P) {
 bool alm_stage_b_split(const DevProblem &P) {
     for (int k = 0; k < P.K; ++k) {
         StagePlan pb;
-        if (plan_b(P.cones[k], P.K, pb)) return false;
+        if (plan_b(P.cones[k], P.K, pb, P.no_lat)) return false;
         if (!pb.small) return true;
     }
     return false;
@@ -3536,7 +3539,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     int nblkA = 0, nblkB = 0;
     bool split = sh != nullptr;   // stage A as two launches (bandwidth regime; always when sharded)
     for (int k = 0; k < KL; ++k) {
-        if (plan_a(cone_of(k), KL, pa[k]) || plan_b(cone_of(k), KL, pb[k])) return -1;
+        if (plan_a(cone_of(k), KL, pa[k], P.no_lat) || plan_b(cone_of(k), KL, pb[k], P.no_lat)) return -1;
         nblkA += pa[k].grid;
         nblkB += pb[k].grid;
         if (!pa[k].small) split = true;

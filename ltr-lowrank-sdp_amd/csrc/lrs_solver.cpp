@@ -170,6 +170,11 @@ struct lrs_ctx {
     int *d_send_rows = nullptr;
     double *d_sendbuf = nullptr;
     long sendbuf_len = 0;
+    // phase-1 budget hook (lrs_set_budget_hook): called when almInnerBudget is reached;
+    // a larger absolute budget continues the same solve from the saved control block
+    lrs_budget_hook bhook = nullptr;
+    void *buser = nullptr;
+    double last_ctl[C_NCTRL] = {0};
 };
 
 // ------------------------------------------------------------------------
@@ -1118,6 +1123,7 @@ struct InnerIo {
     long inner, local, clear;
     double rcval, lag, pinf1, pinfinf;
     int exitReason;
+    bool resume = false;   // continue from the control block the last call stopped on (budget exit)
 };
 
 static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, double gap, long budget, InnerIo &io,
@@ -1132,6 +1138,13 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     ctl[C_CLEAR] = (double)io.clear; ctl[C_HEAD] = c->head; ctl[C_GCUR] = c->gcur; ctl[C_PENDING] = 0;
     ctl[C_RCVAL] = io.rcval; ctl[C_LAG] = io.lag; ctl[C_PINF1] = io.pinf1; ctl[C_PINFINF] = io.pinfinf;
     ctl[C_BETA0] = c->beta[0]; ctl[C_BETA1] = c->beta[1]; ctl[C_YY0] = c->yy[0]; ctl[C_YY1] = c->yy[1];
+    if (io.resume) {
+        // a budget exit stops an iteration after its fold (PENDING = 2, the L-BFGS dots of
+        // the new gradient kept) and before its direction: restart exactly there.  R was
+        // moved back into W.R by the previous call, so RCUR restarts at 0.
+        memcpy(ctl, c->last_ctl, sizeof(ctl));
+        ctl[C_ACTIVE] = 1; ctl[C_EXIT] = EXIT_NONE; ctl[C_ACT2] = 1; ctl[C_EXIT2] = EXIT_NONE; ctl[C_RCUR] = 0;
+    }
     memcpy(c->hpin, par, sizeof(par));
     HIPC(hipMemcpyAsync(c->W.par, c->hpin, sizeof(par), hipMemcpyHostToDevice, c->st));
     memcpy(c->hpin + 64, ctl, sizeof(ctl));
@@ -1266,6 +1279,7 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     io.inner = (long)res[C_INNER]; io.local = (long)res[C_LOCAL]; io.clear = (long)res[C_CLEAR];
     io.rcval = res[C_RCVAL]; io.lag = res[C_LAG]; io.pinf1 = res[C_PINF1]; io.pinfinf = res[C_PINFINF];
     io.exitReason = (int)res[C_EXIT2];
+    memcpy(c->last_ctl, res, sizeof(double) * C_NCTRL);
     // the iterate lives in R2 after an odd number of completed iterations
     if (res[C_RCUR] != 0.0)
         HIPC(hipMemcpyAsync(c->W.R, c->W.R2, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
@@ -1309,6 +1323,7 @@ static int alm_optimize_body(lrs_ctx *c, const lrs_params *p, AlmState &st, doub
     const int max_inc = 10000, max_ceil = 25000;
     const bool sched = p->rankSchedule && p->rankScheduleLen > 0 && p->fixedRank <= 0;
     if (sched && p->rankScheduleLen <= 1) is_rank_max = 1;
+    long budget = p->almInnerBudget;
 ALG_START:
     upd_cnt = 0;
     rc = 0.1;
@@ -1342,11 +1357,20 @@ ALG_START:
             InnerIo io;
             io.inner = st.innerIter; io.local = localIter; io.clear = clearL; io.rcval = rc_val; io.lag = lag;
             io.pinf1 = st.pinf1; io.pinfinf = st.pinfinf;
-            const long before = st.innerIter;
-            if (run_inner(c, p, st.rho, rc_tol, st.gap, p->almInnerBudget, io)) return -1;
-            st.innerIter = io.inner; localIter = io.local; clearL = io.clear;
-            cur_iter_counter += io.inner - before;
-            rc_val = io.rcval; lag = io.lag; st.pinf1 = io.pinf1; st.pinfinf = io.pinfinf;
+            for (;;) {
+                const long before = st.innerIter;
+                if (run_inner(c, p, st.rho, rc_tol, st.gap, budget, io)) return -1;
+                st.innerIter = io.inner; localIter = io.local; clearL = io.clear;
+                cur_iter_counter += io.inner - before;
+                rc_val = io.rcval; lag = io.lag; st.pinf1 = io.pinf1; st.pinfinf = io.pinfinf;
+                if (io.exitReason != EXIT_BUDGET || !c->bhook) break;
+                // benchmark hook: a larger budget continues this inner loop where it stopped
+                HIPC(hipStreamSynchronize(c->st));
+                const long nb = c->bhook(c->buser, st.innerIter);
+                if (nb <= st.innerIter) break;
+                budget = nb;
+                io.resume = true;
+            }
             if (io.exitReason == EXIT_PHASE1) { st.outerIter = k; goto END_ALM; }
             if (io.exitReason == EXIT_NUMERR) { retcode = 4; goto END_ALM; }
             if (io.exitReason == EXIT_BUDGET) goto PRINT_AND_EXIT;
@@ -1859,7 +1883,10 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
 int lrs_set_kernel_path(lrs_ctx *c, int path) {
     if (c) bind(c);
     if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
-    if (path != 0 && path != 1) { set_err("kernel path %d: expected 0 (auto) or 1 (general)", path); return -1; }
+    if (path < 0 || path > 3) {
+        set_err("kernel path %d: expected 0 (auto), 1 (general), 2 (general, bandwidth regime) or 3 (+ long-row kernels)", path);
+        return -1;
+    }
     if (c->dp.no_lat != path) {
         drop_graphs(c);   // captured batches hold the previous kernels
         c->dp.no_lat = path;
@@ -2395,6 +2422,33 @@ int lrs_alm_throughput(lrs_ctx *c, const lrs_params *pin, long warmup, long step
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    return 0;
+}
+
+int lrs_set_budget_hook(lrs_ctx *c, lrs_budget_hook hook, void *user) {
+    if (!c) { set_err("null ctx"); return -1; }
+    c->bhook = hook;
+    c->buser = user;
+    return 0;
+}
+
+int lrs_alm_last_step(lrs_ctx *c, double *out4, int *newest_pair) {
+    if (!c || !out4) { set_err("null argument"); return -1; }
+    // the control block the last inner loop stopped on: its fold is the last completed trip
+    const int L = 2;
+    const int hn = c->head == 0 ? L - 1 : c->head - 1;
+    out4[0] = c->last_ctl[C_LASTTAU];
+    out4[1] = c->last_ctl[C_LAG];
+    out4[2] = c->last_ctl[C_PINF1];
+    out4[3] = c->beta[hn];
+    if (newest_pair) *newest_pair = hn;
+    return 0;
+}
+
+int lrs_sync(lrs_ctx *c) {
+    if (!c) { set_err("null ctx"); return -1; }
+    bind(c);
+    HIPC(hipStreamSynchronize(c->st));
     return 0;
 }
 

@@ -61,6 +61,7 @@ class Result(C.Structure):
 
 
 _lib = None
+_HOOK = C.CFUNCTYPE(C.c_long, C.c_void_p, C.c_long)
 
 
 def load_library(path=None):
@@ -104,6 +105,9 @@ def load_library(path=None):
         "lrs_alm_throughput": (C.c_int, [vp, C.POINTER(Params), C.c_long, C.c_long, dp, C.POINTER(C.c_long),
                                          dp, dp]),
         "lrs_set_log_path": (C.c_int, [vp, C.c_char_p]),
+        "lrs_set_budget_hook": (C.c_int, [vp, _HOOK, vp]),
+        "lrs_sync": (C.c_int, [vp]),
+        "lrs_alm_last_step": (C.c_int, [vp, dp, ip]),
         "lrs_time_auut": (C.c_int, [vp, C.c_int, dp]),
         "lrs_profile_stages": (C.c_int, [vp, C.POINTER(Params), C.c_long, dp, C.POINTER(C.c_long)]),
         "lrs_time_stages": (C.c_int, [vp, C.c_int, dp]),
@@ -340,6 +344,74 @@ class Solver:
         return {"seconds": sec.value, "done": done.value, "auut_ms": kms.value if auut else None,
                 "iter_ms": ims.value}
 
+    def alm_timed(self, warmup, steps, on_start=None, on_stop=None, **kw):
+        """ONE phase-1 solve: `warmup` inner iterations, then exactly `steps` more of the same
+        solve (lrs_set_budget_hook), with no solver setup between them.  on_start() runs when
+        the warmup iterations are done and the stream is idle, on_stop() after the timed ones
+        (the caller's barrier + clock); returns {"done": timed iterations, "seconds": host
+        time between the two callbacks (the callbacks' own work excluded), "inner": total}."""
+        import time as _time
+        kw = dict(kw)
+        p = default_params(**kw)
+        p.phase1Tol = 1e-300
+        p.maxALMIter = 1000000000
+        p.skipADMM = 1
+        p.timeSecLimit = 1e30
+        p.almInnerBudget = max(1, int(warmup))
+        st = {"t0": None, "t1": None, "i0": 0, "i1": 0}
+
+        def hook(_user, inner):
+            if st["t0"] is None:
+                if on_start:
+                    on_start()
+                st["i0"] = inner
+                st["t0"] = _time.perf_counter()
+                return inner + int(steps)
+            st["t1"] = _time.perf_counter()
+            st["i1"] = inner
+            if on_stop:
+                on_stop()
+            return 0
+
+        cb = _HOOK(hook)
+        self._check(self.lib.lrs_set_budget_hook(self.ctx, cb, None), "set_budget_hook")
+        try:
+            res = Result()
+            self._check(self.lib.lrs_solve(self.ctx, C.byref(p), C.byref(res)), "solve")
+        finally:
+            self.lib.lrs_set_budget_hook(self.ctx, _HOOK(), None)
+        if st["t0"] is None or st["t1"] is None:
+            raise RuntimeError("alm_timed: the phase-1 budget was not reached")
+        return {"done": st["i1"] - st["i0"], "seconds": st["t1"] - st["t0"], "inner": res.alm_inner}
+
+    def alm_steps(self, K, **kw):
+        """Exactly K ALM inner iterations of a fresh phase-1 solve (budget stop), then
+        (tau, ||G||^2, pinf, beta) of trip K, the newest pair's index and the state."""
+        kw = dict(kw)
+        p = default_params(**kw)
+        p.maxALMIter = 1000000000
+        p.skipADMM = 1
+        p.timeSecLimit = 1e30
+        p.almInnerBudget = int(K)
+        res = Result()
+        self._check(self.lib.lrs_solve(self.ctx, C.byref(p), C.byref(res)), "solve")
+        out = (C.c_double * 4)()
+        nw = C.c_int()
+        self._check(self.lib.lrs_alm_last_step(self.ctx, out, C.byref(nw)), "alm_last_step")
+        self.ranks = self.get_rank()
+        pair = (S0, Y0) if nw.value == 0 else (S1, Y1)
+        return {"inner": res.alm_inner, "tau": out[0], "lag": out[1], "pinf": out[2], "beta": out[3],
+                "R": self.get_factor(R), "G": self.get_factor(G), "cvs": self.get_vec(CVS),
+                "lam": self.get_vec(LAMBDA), "s": self.get_factor(pair[0]), "y": self.get_factor(pair[1])}
+
+    def get_rank(self):
+        out = (C.c_int * self.K)()
+        self._check(self.lib.lrs_get_rank(self.ctx, out), "get_rank")
+        return list(out)
+
+    def sync(self):
+        self._check(self.lib.lrs_sync(self.ctx), "sync")
+
     def profile_stages(self, steps, **kw):
         """Average ms per launch of the four split-iteration stages (HIP events)."""
         p = default_params(**kw)
@@ -426,9 +498,21 @@ def run_lorads(instance_path, json_output_path, params, fixed_rank=None, rank_sc
         cmd += ["--rankSchedule", str(rank_schedule_path), "--nearStallFactor", str(near_stall_factor)]
     elif fixed_rank is not None:
         cmd += ["--fixedRank", str(fixed_rank)]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
-    if r.returncode != 0 or not json_output_path.exists():
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0:
+            print(f"  [error] lorads failed: {r.stderr[:200]}")
+            return False, None, None
+        if not json_output_path.exists():
+            return False, None, None
+        with open(json_output_path) as f:
+            out = json.load(f)
+        # same key fallbacks as benchmark.py:270-274
+        m = out.get("final_metrics", out.get("metrics", {}))
+        return True, m.get("solve_time_sec"), m.get("primal_obj", m.get("primal_objective"))
+    except subprocess.TimeoutExpired:
+        print("  [error] lorads timed out")
         return False, None, None
-    with open(json_output_path) as f:
-        m = json.load(f)["metrics"]
-    return True, m.get("solve_time_sec"), m.get("primal_obj")
+    except Exception as e:   # benchmark.py:283-285
+        print(f"  [error] unexpected error: {e}")
+        return False, None, None

@@ -1335,6 +1335,37 @@ long oracle_alm_rate(const char *path, int rank, double seconds, double *elapsed
     return it;
 }
 
+/* Exactly K ALM inner iterations from the reference's initial point (phase 1 with an inner
+ * budget, lorads_alm.c:1302-1379 between the budget checks); out = R, G (col-major per cone,
+ * cones concatenated), A(RR^T), lambda.  Returns NR (doubles per factor) or -1. */
+long oracle_alm_steps(const char *path, int rank, long K, double *out, long cap) {
+    oparams prm;
+    default_oparams(&prm);
+    prm.fixedRank = rank;
+    prm.reoptLevel = 0;
+    prm.disableOracle = 1;
+    oproblem *p = oracle_read(path);
+    if (!p) return -1;
+    osolver *s = osolver_new(p, &prm);
+    ostate alm = {0};
+    long sd = 0;
+    for (int k = 0; k < s->K; ++k) sd += p->cones[k].n;
+    alm.rho = 1 / sqrt((double)sd);
+    alm.pobj = alm.dobj = alm.pinf1 = alm.pinfinf = 1e30;
+    alm_optimize(s, &alm, o_now(), K);
+    long NR = s->NR, need = 2 * NR + 2 * s->m;
+    if (need <= cap) {
+        memcpy(out, s->R, 8 * NR);
+        memcpy(out + NR, s->G, 8 * NR);
+        memcpy(out + 2 * NR, s->cvs, 8 * s->m);
+        memcpy(out + 2 * NR + s->m, s->lam, 8 * s->m);
+    }
+    long inner = alm.innerIter;
+    osolver_free(s);
+    oracle_free(p);
+    return inner == K && need <= cap ? NR : -1;
+}
+
 /* Same layout as oracle/ref_harness.c mode_kernels. */
 int oracle_kernels(oproblem *p, int rank, const double *in, double *out) {
     oparams prm;

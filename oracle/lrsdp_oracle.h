@@ -37,6 +37,11 @@ int oracle_solve(const char *path, int nflags, char **flags, double *res);
  * `seconds` of wall time; *elapsed receives the phase-1 time. */
 long oracle_alm_rate(const char *path, int rank, double seconds, double *elapsed);
 
+/* Exactly K phase-1 inner iterations from the reference's initial point (rank <= 0: the
+ * default rank); out = R, G, A(RR^T), lambda (R, G col-major per cone).  Returns the
+ * doubles per factor, or -1 (read error, fewer than K iterations, or cap too small). */
+long oracle_alm_steps(const char *path, int rank, long K, double *out, long cap);
+
 /* First n outputs of the restated glibc rand() after srand(seed). */
 int oracle_rand_seq(unsigned seed, int n, int *out);
 

@@ -19,6 +19,13 @@
  *   kernels <file.dat-s> <rank> <in.bin> <out.bin>
  *       One call of each hot-path operator on caller-provided iterates (see
  *       scripts/make_golden.py for the exact binary layout).
+ *   alm_steps <file.dat-s> <rank> <K> <out.bin>
+ *       From the reference's own initial point (srand(925), data/lorads_solver.c:625)
+ *       the preamble of LORADS_ALMOptimize (lorads_alm.c:1233-1243) and exactly K
+ *       trips of its inner L-BFGS loop (lorads_alm.c:1302-1379), through the same
+ *       lorads_func slots in the same order; dumps per trip (tau, rootNum,
+ *       ||G||^2, pinf) and after the last one R, G, A(RR^T), lambda and the newest
+ *       L-BFGS pair (s, y, beta).  Layout in scripts/make_golden_steps.py.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -327,10 +334,124 @@ static int mode_kernels(int argc, char **argv) {
     return 0;
 }
 
+/* ---------------- alm_steps mode: K inner iterations, per-iteration dump ---------------- */
+static int mode_alm_steps(int argc, char **argv) {
+    if (argc < 6) return 2;
+    lorads_params p; default_params(&p);
+    p.fname = argv[2];
+    p.fixedRank = atoi(argv[3]);
+    const long K = atol(argv[4]);
+    ref_ctx c; memset(&c, 0, sizeof(c));
+    double t_read, tss;
+    if (ref_setup(&c, &p, &t_read, &tss)) { fprintf(stderr, "read failed\n"); return 1; }
+    lorads_solver *S = c.S;
+    lorads_alm_state *st = &c.alm;
+    lorads_func *aFunc;
+    LORADSInitFuncSet(&aFunc, S->nLpCols);
+    lorads_int incx = 1, m = S->nRows;
+    double minusOne = -1.0, tau = 0.0, lagNormSquare = 0.0;
+    /* lorads_alm.c:1233-1243 */
+    double rc_tol = 0.1 / st->rho;
+    aFunc->InitConstrValAll(S, S->var->rLp, S->var->rLp, S->var->R, S->var->R);
+    aFunc->InitConstrValSum(S);
+    aFunc->ALMCalGrad(S, S->var->rLp, S->var->gradLp, S->var->R, S->var->Grad, &lagNormSquare, st->rho);
+    double rc_val = sqrt(lagNormSquare) / (1 + S->cObjNrmInf);
+    lorads_int localIter = 0, clearLBFGS = 0;
+    double *trips = calloc(4 * (K + 1), sizeof(double));
+    long done = 0;
+    int stop = K <= 0;
+    /* the inner loops of the first outer iterations (lorads_alm.c:1285-1409), trip by trip */
+    /* the state is dumped where trip K + 1 would start (after the dual / rho updates that
+       follow an inner loop ending at trip K), as a phase-1 budget of K stops there */
+    while (!stop) {
+        /* UpdateRho (lorads_alm.c:1403-1409) whenever the certificate is already met
+           (:1297-1300), then a fresh inner loop (localIter = 0, :1285) */
+        while (rc_val <= rc_tol) {
+            do {
+                st->rho *= p.ALMRhoFactor;
+                aFunc->ALMCalGrad(S, S->var->rLp, S->var->gradLp, S->var->R, S->var->Grad, &lagNormSquare, st->rho);
+                rc_val = sqrt(lagNormSquare) / (1 + S->cObjNrmInf);
+                rc_tol = 0.1 / st->rho;
+            } while (rc_tol >= rc_val);
+            if (st->l_inf_primal_infeasibility <= p.phase1Tol) { stop = 1; break; }   /* :1423-1426 */
+        }
+        if (stop) break;
+        localIter = 0;
+        while (rc_val - rc_tol > p.endALMSubTol) {   /* lorads_alm.c:1302-1379 */
+            if (done >= K) { stop = 1; break; }
+            if (localIter % 300 == 0) clearLBFGS = 0;
+            aFunc->LBFGSDirection(&p, S, S->lbfgsHis, S->var->gradLp, S->var->uLp, S->var->Grad, S->var->U, clearLBFGS);
+            aFunc->LBFGSDirUseGrad(S, S->var->uLp, S->var->gradLp, S->var->U, S->var->Grad);
+            double *q0 = S->var->M1temp;
+            memcpy(q0, S->rowRHS, sizeof(double) * m);
+            axpy(&m, &minusOne, S->var->constrValSum, &incx, q0, &incx);
+            double p12[2];
+            aFunc->ALMCalq12p12(S, S->var->rLp, S->var->uLp, S->var->R, S->var->U, S->var->ARDSum, S->var->ADDSum, p12);
+            lorads_int rn = ALMLineSearch(st->rho, m, S->var->dualVar, p12[0], p12[1], q0, S->var->ARDSum,
+                                          S->var->ADDSum, &tau);
+            trips[4 * done] = tau; trips[4 * done + 1] = (double)rn;
+            if (rn == 0 || fabs(tau) < p.endTauTol) { done++; stop = 1; break; }
+            aFunc->setAsNegGrad(S, S->var->gradLp, S->var->Grad);
+            aFunc->ALMupdateVar(S, S->var->rLp, S->var->uLp, S->var->R, S->var->U, tau);
+            double tau2 = tau * tau;
+            axpy(&m, &tau, S->var->ARDSum, &incx, S->var->constrValSum, &incx);
+            axpy(&m, &tau2, S->var->ADDSum, &incx, S->var->constrValSum, &incx);
+            lagNormSquare = 0.0;
+            aFunc->ALMCalGrad(S, S->var->rLp, S->var->gradLp, S->var->R, S->var->Grad, &lagNormSquare, st->rho);
+            aFunc->setlbfgsHisTwo(S, S->var->gradLp, S->var->uLp, S->var->Grad, S->var->U, tau);
+            aFunc->updateDimacsALM(S, S->var->R, S->var->R, S->var->rLp, S->var->rLp);
+            st->l_1_primal_infeasibility = S->dimacError[LORADS_DIMAC_ERROR_CONSTRVIO_L1];
+            st->l_inf_primal_infeasibility = st->l_1_primal_infeasibility * (1 + S->bRHSNrm1) / (1 + S->bRHSNrmInf);
+            trips[4 * done + 2] = lagNormSquare;
+            trips[4 * done + 3] = S->dimacError[LORADS_DIMAC_ERROR_CONSTRVIO_L1];
+            localIter++; clearLBFGS++; done++;
+            if (st->l_inf_primal_infeasibility <= p.phase1Tol &&
+                (st->primal_dual_gap <= p.phase1Tol || !p.highAccMode)) { stop = 1; break; }
+            rc_val = sqrt(lagNormSquare) / (1 + S->cObjNrmInf);
+            if (localIter > 800) break;
+        }
+        if (stop) break;
+        /* lorads_alm.c:1380-1383: dual update, gradient, certificate; the difficulty only
+           decides between another inner loop and UpdateRho, both of which start from here */
+        LORADSUpdateDualVar(S, st->rho);
+        aFunc->ALMCalGrad(S, S->var->rLp, S->var->gradLp, S->var->R, S->var->Grad, &lagNormSquare, st->rho);
+        rc_val = sqrt(lagNormSquare) / (1 + S->cObjNrmInf);
+        if (localIter <= 20) {   /* EASY: leave the outer iteration through UpdateRho */
+            do {
+                st->rho *= p.ALMRhoFactor;
+                aFunc->ALMCalGrad(S, S->var->rLp, S->var->gradLp, S->var->R, S->var->Grad, &lagNormSquare, st->rho);
+                rc_val = sqrt(lagNormSquare) / (1 + S->cObjNrmInf);
+                rc_tol = 0.1 / st->rho;
+            } while (rc_tol >= rc_val);
+            if (st->l_inf_primal_infeasibility <= p.phase1Tol) break;
+        }
+    }
+    FILE *fo = fopen(argv[5], "wb");
+    if (!fo) return 1;
+    double dd = (double)done;
+    fwrite(&dd, 8, 1, fo);
+    fwrite(trips, 8, 4 * done, fo);
+    for (lorads_int k = 0; k < S->nCones; ++k)
+        fwrite(S->var->R[k]->matElem, 8, S->var->R[k]->nRows * S->var->R[k]->rank, fo);
+    for (lorads_int k = 0; k < S->nCones; ++k)
+        fwrite(S->var->Grad[k]->matElem, 8, S->var->Grad[k]->nRows * S->var->Grad[k]->rank, fo);
+    fwrite(S->var->constrValSum, 8, m, fo);
+    fwrite(S->var->dualVar, 8, m, fo);
+    lbfgs_node *newest = S->lbfgsHis->prev;
+    fwrite(newest->s, 8, newest->allElem, fo);
+    fwrite(newest->y, 8, newest->allElem, fo);
+    fwrite(&newest->beta, 8, 1, fo);
+    fclose(fo);
+    free(trips);
+    printf("REF_STEPS done=%ld\n", done);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 3) { fprintf(stderr, "usage: %s solve|alm_rate|kernels file ...\n", argv[0]); return 2; }
     if (!strcmp(argv[1], "solve")) return mode_solve(argc, argv);
     if (!strcmp(argv[1], "alm_rate")) return mode_alm_rate(argc, argv);
     if (!strcmp(argv[1], "kernels")) return mode_kernels(argc, argv);
+    if (!strcmp(argv[1], "alm_steps")) return mode_alm_steps(argc, argv);
     return 2;
 }

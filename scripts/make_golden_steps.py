@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Per-iteration golden fixtures of the ALM inner loop, from the REFERENCE itself.
+
+Runs `oracle/_ref/lorads_ref_harness alm_steps` (our driver over the reference
+LoRADS objects built by oracle/Makefile.ref): from the reference's own initial
+point (srand(925), data/lorads_solver.c:625) the preamble of LORADS_ALMOptimize
+(lorads_alm.c:1233-1243) and exactly K trips of the inner L-BFGS loop
+(lorads_alm.c:1302-1379).  For every K in KS it stores
+
+  trips[K, 4]  per trip: tau, rootNum, ||G||^2 after the trip, pinf after the trip
+  R, G         the factor and gradient after trip K (col-major per cone, cones concatenated)
+  cvs, lam     A(RR^T) and lambda after trip K
+  s, y, beta   the newest L-BFGS pair (s = tau D, y = G_new - G_old, 1/<y,s>)
+
+into tests/golden/steps_<name>.npz (data only; the instances are ours).
+Run:  python scripts/make_golden_steps.py   (needs /root/reference; CPU only)
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "lorads_ref_harness")
+
+# (name, instance path, rank (-1 = the reference's default), Ks)
+CASES = [
+    ("mc_rand200", os.path.join(GOLD, "instances", "mc_rand200.dat-s"), -1, [1, 2, 3, 4, 5]),
+    ("mc_torus12x10", os.path.join(GOLD, "instances", "mc_torus12x10.dat-s"), -1, [1, 2, 3, 4, 5]),
+    ("mc_rand300w", os.path.join(GOLD, "instances", "mc_rand300w.dat-s"), 12, [1, 2, 3, 4, 5]),
+    ("theta40", os.path.join(GOLD, "instances", "theta40.dat-s"), -1, [1, 2, 3, 4, 5]),
+    ("theta25x3", os.path.join(GOLD, "instances", "theta25x3.dat-s"), -1, [1, 2, 3, 4, 5]),
+    ("rsparse60", os.path.join(GOLD, "instances", "rsparse60.dat-s"), -1, [1, 2, 3, 4, 5]),
+    # the reference's own bundled instance with hub rows (the latency kernels' slice blocks)
+    ("checker_1.5", os.path.join(ROOT, "data", "bundled", "checker_1.5.dat-s"), -1, [1, 3, 5]),
+]
+
+
+def run_steps(path, rank, K, m, nr):
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "s.bin")
+        r = subprocess.run([HARNESS, "alm_steps", path, str(rank), str(K), out], capture_output=True, text=True,
+                           env=dict(os.environ, OPENBLAS_NUM_THREADS="1"), timeout=600)
+        if r.returncode != 0 or "REF_STEPS" not in r.stdout:
+            raise RuntimeError(r.stdout[-2000:] + r.stderr[-2000:])
+        a = np.fromfile(out)
+    done = int(a[0])
+    p = 1
+    trips = a[p:p + 4 * done].reshape(done, 4); p += 4 * done
+    d = {"trips": trips}
+    for key, ln in (("R", nr), ("G", nr), ("cvs", m), ("lam", m), ("s", nr), ("y", nr), ("beta", 1)):
+        d[key] = a[p:p + ln]; p += ln
+    assert p == a.size, (p, a.size)
+    return d
+
+
+def dims_of(path):
+    """(m, block sizes) from the SDPA header."""
+    with open(path) as f:
+        lines = [ln for ln in f if ln.strip() and ln.lstrip()[0] not in '*"']
+    m = int(lines[0].split()[0])
+    nb = int(lines[1].split()[0])
+    dims = [abs(int(x)) for x in lines[2].replace(",", " ").replace("{", " ").replace("}", " ")
+            .replace("(", " ").replace(")", " ").split()[:nb]]
+    return m, dims
+
+
+def main():
+    if not os.path.exists(HARNESS):
+        sys.exit("build the reference harness first: make -C oracle -f Makefile.ref")
+    for name, path, rank, ks in CASES:
+        m, dims = dims_of(path)
+        # the reference's rank per cone is only known after presolve: read it back from R's size
+        probe = None
+        out = {}
+        for K in ks:
+            if probe is None:
+                # first call with a generous nr guess; the dump's tail fixes the real size
+                with tempfile.TemporaryDirectory() as td:
+                    o = os.path.join(td, "s.bin")
+                    subprocess.run([HARNESS, "alm_steps", path, str(rank), "1", o], capture_output=True, check=True,
+                                   env=dict(os.environ, OPENBLAS_NUM_THREADS="1"), timeout=600)
+                    a = np.fromfile(o)
+                done = int(a[0])
+                rest = a.size - 1 - 4 * done - 2 * m - 1
+                assert rest % 4 == 0
+                probe = rest // 4
+            d = run_steps(path, rank, K, m, probe)
+            for k, v in d.items():
+                out[f"K{K}_{k}"] = v
+        out["ks"] = np.array(ks)
+        out["m"] = np.array(m)
+        out["dims"] = np.array(dims)
+        out["nr"] = np.array(probe)
+        out["rank_flag"] = np.array(rank)
+        np.savez_compressed(os.path.join(GOLD, f"steps_{name}.npz"), **out)
+        t = out[f"K{ks[-1]}_trips"]
+        print(f"{name}: m={m} dims={dims} nr={probe} taus={np.round(t[:, 0], 6).tolist()}")
+
+
+if __name__ == "__main__":
+    main()

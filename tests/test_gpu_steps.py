@@ -1,0 +1,99 @@
+"""Per-iteration parity of the FUSED ALM inner iteration against the reference.
+
+tests/golden/steps_<name>.npz come from the reference LoRADS C code itself
+(scripts/make_golden_steps.py -> oracle/ref_harness.c `alm_steps`): from the reference's
+initial point, exactly K trips of the inner L-BFGS loop (lorads_alm.c:1302-1379, with the
+dual / rho updates between inner loops of lorads_alm.c:1380-1409).  The device runs the
+same K trips through its product kernels (Solver.alm_steps = lrs_solve with a phase-1
+budget of K) on every kernel family:
+
+  path 0  latency-regime kernels k_lat_a / k_lat_b (+ slice blocks and k_lat_f on hub rows)
+  path 1  general row kernels k_it_a / (k_it_g) / k_it_b, fused (small-n regime)
+  path 2  general row kernels in their bandwidth-regime form (split launches)
+  path 3  path 2 with the long-row neighbour kernels k_wide_a / k_wide_b
+
+Tolerances: tau_k to 1e-9 relative with the same root count; R_K, G_K, A(R_K R_K^T),
+the newest L-BFGS pair to 1e-9 relative (norm-wise; FP64 summation-order rounding grows
+through K dependent trips); ||G||^2 and pinf to 1e-9.
+"""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN, ROOT, rel_err
+
+pytestmark = pytest.mark.gpu
+STEP_CASES = ["mc_rand200", "mc_torus12x10", "mc_rand300w", "theta40", "theta25x3", "rsparse60", "checker_1.5"]
+TOL = 1e-9
+
+
+def _path(name):
+    if name == "checker_1.5":
+        return os.path.join(ROOT, "data", "bundled", "checker_1.5.dat-s")
+    return os.path.join(GOLDEN, "instances", f"{name}.dat-s")
+
+
+@pytest.fixture(scope="module")
+def solver_mod():
+    return importlib.import_module("ltr-lowrank-sdp_amd.solver")
+
+
+def _cases():
+    out = []
+    for name in STEP_CASES:
+        for path in (0, 1, 2, 3):
+            out.append((name, path))
+    return out
+
+
+@pytest.mark.parametrize("name,kpath", _cases())
+def test_fused_iterations_match_reference(solver_mod, name, kpath):
+    z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
+    rank = int(z["rank_flag"])
+    kw = {"reoptLevel": 0}
+    if rank > 0:
+        kw["fixedRank"] = rank
+    sv = solver_mod.Solver(_path(name))
+    sv.set_kernel_path(kpath)
+    worst = {}
+    for K in [int(k) for k in z["ks"]]:
+        trips = z[f"K{K}_trips"]
+        if trips.shape[0] < K:
+            continue
+        d = sv.alm_steps(K, **kw)
+        assert d["inner"] == K, (K, d["inner"])
+        tau, rn, lag, pinf = trips[K - 1]
+        assert abs(d["tau"] - tau) <= TOL * abs(tau), (K, d["tau"], tau)
+        assert abs(d["lag"] - lag) <= TOL * abs(lag), (K, d["lag"], lag)
+        assert abs(d["pinf"] - pinf) <= TOL * max(abs(pinf), 1e-300), (K, d["pinf"], pinf)
+        assert abs(d["beta"] - z[f"K{K}_beta"][0]) <= TOL * abs(z[f"K{K}_beta"][0])
+        for key, ref in (("R", "R"), ("G", "G"), ("cvs", "cvs"), ("s", "s"), ("y", "y")):
+            e = rel_err(d[key], z[f"K{K}_{ref}"])
+            worst[key] = max(worst.get(key, 0.0), e)
+            assert e < TOL, (K, key, e)
+        assert rel_err(d["lam"], z[f"K{K}_lam"]) < TOL or np.linalg.norm(z[f"K{K}_lam"]) == 0
+        if kpath == 0 and name != "rsparse60":
+            # the latency kernels are the ones that ran (rsparse60's multi-slot rows may not fit them)
+            assert sv.kernel_path() in (0, 1)
+        if kpath >= 1:
+            assert sv.kernel_path() == 1
+    print(f"{name} path {kpath}: worst rel errors {worst}")
+    sv.close()
+
+
+def test_budget_hook_resumes_same_solve(solver_mod):
+    """W warmup trips + K timed trips through lrs_set_budget_hook == W + K trips in one go
+    (bit for bit): the bench's timed region continues the same solve."""
+    name = "mc_torus12x10"
+    sv = solver_mod.Solver(_path(name))
+    calls = []
+    out = sv.alm_timed(7, 23, on_start=lambda: calls.append("start"), on_stop=lambda: calls.append("stop"),
+                       reoptLevel=0)
+    assert calls == ["start", "stop"] and out["done"] == 23 and out["inner"] == 30
+    sv.ranks = sv.get_rank()
+    R1 = sv.get_factor(solver_mod.R)
+    d = sv.alm_steps(30, reoptLevel=0, phase1Tol=1e-300)
+    assert np.array_equal(R1, d["R"])
+    sv.close()

@@ -51,3 +51,35 @@ def test_oracle_solve_matches_reference(oracle_lib, case):
         for k in ("admm_pobj", "admm_dobj"):
             assert abs(o[k] - r[k]) <= tol * (1 + abs(r[k])), (k, o[k], r[k], tol)
         assert o["admm_pinf"] <= 1e-4 and r["admm_pinf"] <= 1e-4
+
+
+STEP_CASES = ["mc_rand200", "mc_torus12x10", "mc_rand300w", "theta40", "theta25x3", "rsparse60", "checker_1.5"]
+
+
+@pytest.mark.parametrize("name", STEP_CASES)
+def test_oracle_alm_steps_match_reference(oracle_lib, name):
+    """K inner iterations of the restatement vs the reference's own K trips
+    (tests/golden/steps_*.npz, scripts/make_golden_steps.py)."""
+    import ctypes as C
+    import os
+    from golden_util import GOLDEN, ROOT
+    z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
+    path = (os.path.join(ROOT, "data", "bundled", "checker_1.5.dat-s") if name == "checker_1.5"
+            else os.path.join(GOLDEN, "instances", f"{name}.dat-s"))
+    lib = oracle_lib
+    lib.oracle_alm_steps.restype = C.c_long
+    lib.oracle_alm_steps.argtypes = [C.c_char_p, C.c_int, C.c_long, C.POINTER(C.c_double), C.c_long]
+    nr, m = int(z["nr"]), int(z["m"])
+    for K in [int(k) for k in z["ks"]]:
+        if z[f"K{K}_trips"].shape[0] < K:
+            continue
+        out = np.zeros(2 * nr + 2 * m)
+        got = lib.oracle_alm_steps(path.encode(), int(z["rank_flag"]), K, out.ctypes.data_as(C.POINTER(C.c_double)),
+                                   out.size)
+        assert got == nr, (K, got)
+        assert rel_err(out[:nr], z[f"K{K}_R"]) < 1e-9, K
+        assert rel_err(out[nr:2 * nr], z[f"K{K}_G"]) < 1e-9, K
+        assert rel_err(out[2 * nr:2 * nr + m], z[f"K{K}_cvs"]) < 1e-9, K
+        lam = z[f"K{K}_lam"]
+        if np.linalg.norm(lam) > 0:
+            assert rel_err(out[2 * nr + m:], lam) < 1e-9, K
