@@ -175,6 +175,7 @@ struct lrs_ctx {
     lrs_budget_hook bhook = nullptr;
     void *buser = nullptr;
     double last_ctl[C_NCTRL] = {0};
+    double last_trip[3] = {0, 0, 0};   // tau, ||G||^2, pinf of the last completed inner trip
 };
 
 // ------------------------------------------------------------------------
@@ -1275,6 +1276,10 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
         c->st_iters += (long)res[C_INNER] - io.inner;
         c->st_nop += enq - ((long)res[C_INNER] - io.inner);
         c->st_inner_s += now_s() - t_in;
+    }
+    if ((long)res[C_INNER] > io.inner) {
+        // a later inner loop that stops before its first trip (budget) keeps this record
+        c->last_trip[0] = res[C_LASTTAU]; c->last_trip[1] = res[C_LAG]; c->last_trip[2] = res[C_PINF1];
     }
     io.inner = (long)res[C_INNER]; io.local = (long)res[C_LOCAL]; io.clear = (long)res[C_CLEAR];
     io.rcval = res[C_RCVAL]; io.lag = res[C_LAG]; io.pinf1 = res[C_PINF1]; io.pinfinf = res[C_PINFINF];
@@ -2437,9 +2442,9 @@ int lrs_alm_last_step(lrs_ctx *c, double *out4, int *newest_pair) {
     // the control block the last inner loop stopped on: its fold is the last completed trip
     const int L = 2;
     const int hn = c->head == 0 ? L - 1 : c->head - 1;
-    out4[0] = c->last_ctl[C_LASTTAU];
-    out4[1] = c->last_ctl[C_LAG];
-    out4[2] = c->last_ctl[C_PINF1];
+    out4[0] = c->last_trip[0];
+    out4[1] = c->last_trip[1];
+    out4[2] = c->last_trip[2];
     out4[3] = c->beta[hn];
     if (newest_pair) *newest_pair = hn;
     return 0;
