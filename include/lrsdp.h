@@ -60,6 +60,8 @@ typedef struct {
     int traj1_len, traj2_len;
     double rho_max;      /* params.rhoMax after LORADS_ALMtoADMM (written to the JSON) */
     double dinf, dinf_inf, dinf_2;   /* dual infeasibility l_1 / l_inf / l_2 (main.c:515-521); -1 if not evaluated */
+    int dinf_converged;  /* 1: every cone's Lanczos met its residual test; 0: a step cap was hit (dinf is then a
+                            lower bound and status 1 is withheld); -1: not evaluated */
 } lrs_result;
 
 /* factor / vector selectors */

@@ -211,9 +211,12 @@ int launch_dual_update(const DevProblem &P, double rho, double *lam, const doubl
 // M1 = -lam - rho b + rho cvs   (ALMSetGrad, lorads_alm.c:38-50)
 int launch_alm_m1(const DevProblem &P, double rho, const double *lam, const double *cvs, double *M1,
                   hipStream_t st);
-// Gram partials X^T X (avg=0) or ((U+V)/2)^T((U+V)/2) (avg=1) of one cone -> gram [nblk][r*r]
+// r x r Gram X^T X (avg=0) or ((U+V)/2)^T((U+V)/2) (avg=1) of one cone, one launch:
+// gram[0, r*r) <- the Gram, gram[r*r, ...) chunk partials (gram_buf_len(rmax) doubles)
+constexpr int kGramMaxChunks = 64;
+size_t gram_buf_len(int rmax);
 int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y, int avg,
-                double *gram_part, int *nblk_used, hipStream_t st);
+                double *gram, int *nblk_used, hipStream_t st);
 
 // ---- fused ALM inner iteration (device-side control; see lrs_kernels.hip) ----
 struct AlmIterArgs {
@@ -258,6 +261,8 @@ constexpr int kLzStepCap = 300;   // Lanczos steps at most (the device step kern
 void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart);
 // sharded solve helpers
 int launch_pack_rows(int nrows, int ld, const int *rows, const double *src, double *dst, hipStream_t st);
+// fold one scalar's per-block partials into out[0] (sharded CG, before its all-reduce)
+int launch_fold1(const double *part, int nblk, double *out, hipStream_t st);
 int launch_sum_shards(int n, int world, const double *const *src, double *out, hipStream_t st);
 
 const char *last_device_error();

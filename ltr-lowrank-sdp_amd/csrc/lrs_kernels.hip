@@ -94,6 +94,9 @@ Layout choose_layout(int r) {
             int ld = Gs[gi] * Es[ei];
             if (ld >= r && ld < best.ld) { best.G = Gs[gi]; best.E = Es[ei]; best.ld = ld; }
         }
+    // ranks 257..512 (AUG_RANK's rank_max = sqrt(2 nnzRows) + 1 exceeds 256 on e.g. theta102,
+    // MC_500): full waves per row, 8 doubles per lane
+    if (best.ld > 512 && r <= 512) { best.G = 64; best.E = 8; best.ld = 512; }
     return best;
 }
 
@@ -503,7 +506,7 @@ __global__ void __launch_bounds__(kBlock) k_spmm(int n, int ld, const int *__res
                                                  double *fin, int row0, int T) {
     // teams of T lane groups per row (dense rows): members take interleaved entries, their
     // partial rows meet in LDS and member 0 sums them in member order (T = 1: no LDS step)
-    __shared__ double gsh[kBlock * 4];
+    __shared__ double gsh[kBlock * E];
     const int lane = threadIdx.x & (G - 1);
     const int gib = threadIdx.x / G;
     const int tpb = (kBlock / G) / T;
@@ -582,81 +585,85 @@ __global__ void __launch_bounds__(kBlock) k_alm_m1(int m, double rho, const doub
         M1[i] = ((-lam[i]) + (-rho) * b[i]) + rho * cvs[i];   // lorads_alm.c:45-49
 }
 
-// Gram partials: block b accumulates rows [b*chunk, (b+1)*chunk) of X^T X into
-// gram_part[b][r][r] (upper+lower).  avg: rows are (X+Y)/2.
-// r x r Gram X^T X (or of the average (X+Y)/2), build_gram_from_factor / _from_average
-// (lorads_logging.c:216-270), on the FP64 matrix cores: v_mfma_f64_16x16x4_f64 with
-// A = X^T and B = X, K = rows.  Block (bx, by): rows of chunk bx, 16x16 output tiles
-// (ta <= tb) of group by, kGramTPW tiles per wave.  A chunk of kGramRows rows is staged
-// in LDS (zero-padded to 16-column tiles), every wave takes its A/B fragments from there:
-// lane l of k-step s reads row 4s + (l >> 4), column 16t + (l & 15).  D fragment: col
-// = l & 15, row = (l >> 4) + 4q (cdna_hip_programming.md §3, f64 map).  Each block writes
-// its tiles (both orientations) into its r x r partial; k_gram_reduce sums the partials
-// of the bx blocks in order.
-constexpr int kGramRows = 16;
-constexpr int kGramTPW = 4;
-constexpr int kGramTPB = kGramTPW * (kBlock / 64);
+// r x r Gram X^T X (or of the average (X+Y)/2), build_gram_from_factor /
+// build_gram_from_average (lorads_logging.c:216-270), on the FP64 matrix cores.
+// Grid (C row chunks) x (one 16 x 16 output tile (a <= b) per y).  C is a multiple of 8,
+// so the linear block id y*C + x puts every tile of chunk x on the same XCD (id mod 8):
+// the chunk's rows are fetched into that XCD's L2 once and re-read from there by its
+// tiles.  The four waves of a block take interleaved k-steps of 4 rows of the chunk
+// (v_mfma_f64_16x16x4f64, operands straight from global memory: lane l of a k-step reads
+// row 4s + (l >> 4), columns 16a + (l & 15) and 16b + (l & 15)), kGramBatch k-steps of
+// loads issued before their MFMAs; the waves' accumulators meet in LDS (wave order) and
+// the block stores the chunk's tile partial.  k_gram_fin (one block per tile) sums the C
+// partials in chunk order, eight loads in flight, and writes the tile and its transpose.
+// Deterministic.  (A last-block ticket in k_gram itself was measured slower: one
+// agent-scope release -- an L2 write-back -- per block, thousands of blocks.)
+// D fragment: col = l & 15, row = (l >> 4) + 4q (cdna_hip_programming.md §3, f64 map).
+constexpr int kGramMaxTiles = 32 * 33 / 2;   // r <= 512
+constexpr int kGramBatch = 8;
 typedef double gram_acc_t __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(kBlock) k_gram(int n, int r, int ld, const double *__restrict__ X,
                                                  const double *__restrict__ Y, int avg,
-                                                 double *__restrict__ gram_part) {
-    extern __shared__ double xs[];   // [kGramRows][ldp]
+                                                 double *__restrict__ part, double *__restrict__ out) {
+    __shared__ double red[kBlock / 64][256];
     const int rt = (r + 15) >> 4;
-    const int ldp = rt * 16 + 1;
-    const int ntiles = rt * (rt + 1) / 2;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int ta[kGramTPW], tb[kGramTPW];
-    bool on[kGramTPW];
-    gram_acc_t acc[kGramTPW];
+    int id = blockIdx.y, a = 0;
+    while (id >= rt - a) { id -= rt - a; ++a; }
+    const int b = a + id, tile = blockIdx.y;
+    const int C = gridDim.x, ch = blockIdx.x;
+    const int per = ((n + C - 1) / C + 15) / 16 * 16;
+    const int i0 = ch * per, i1 = min(n, i0 + per);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ca = min(16 * a + (lane & 15), r - 1), cb = min(16 * b + (lane & 15), r - 1);
+    const bool va = 16 * a + (lane & 15) < r, vb = 16 * b + (lane & 15) < r;
+    gram_acc_t acc = gram_acc_t{0.0, 0.0, 0.0, 0.0};
+    // this wave's k-steps: rows i0 + 16 j + 4 w + (lane >> 4), j = 0, 1, ...
+    for (int j0 = 0; i0 + 16 * j0 + 4 * w < i1; j0 += kGramBatch) {
+        double xa[kGramBatch], xb[kGramBatch];
 #pragma unroll
-    for (int t = 0; t < kGramTPW; ++t) {
-        int id = blockIdx.y * kGramTPB + wv + (kBlock / 64) * t;   // id -> (a, b), a <= b, row-major upper
-        on[t] = id < ntiles;
-        int a = 0;
-        while (on[t] && id >= rt - a) { id -= rt - a; ++a; }
-        ta[t] = a;
-        tb[t] = a + id;
-        acc[t] = gram_acc_t{0.0, 0.0, 0.0, 0.0};
-    }
-    const int chunk = ((n + gridDim.x - 1) / gridDim.x + kGramRows - 1) / kGramRows * kGramRows;
-    const int i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
-    const int cols = rt * 16;
-    for (int ib = i0; ib < i1; ib += kGramRows) {
-        for (int e = threadIdx.x; e < kGramRows * cols; e += kBlock) {
-            const int a = e / cols, c = e - a * cols;
-            const int row = ib + a;
-            double v = 0.0;
-            if (row < i1 && c < r) {
-                v = X[(long)row * ld + c];
-                if (avg) v = 0.5 * (v + Y[(long)row * ld + c]);
+        for (int u = 0; u < kGramBatch; ++u) {
+            const int row = i0 + 16 * (j0 + u) + 4 * w + (lane >> 4);
+            const bool ok = row < i1;
+            const long o = (long)(ok ? row : i0) * ld;   // clamped, never branched
+            double x = X[o + ca], y = X[o + cb];
+            if (avg) {
+                x = 0.5 * (x + Y[o + ca]);
+                y = 0.5 * (y + Y[o + cb]);
             }
-            xs[a * ldp + c] = v;
+            xa[u] = (ok && va) ? x : 0.0;
+            xb[u] = (ok && vb) ? y : 0.0;
         }
-        __syncthreads();
 #pragma unroll
-        for (int t = 0; t < kGramTPW; ++t) {
-            if (!on[t]) continue;   // wave-uniform
-            const double *pa = xs + (lane >> 4) * ldp + ta[t] * 16 + (lane & 15);
-            const double *pb = xs + (lane >> 4) * ldp + tb[t] * 16 + (lane & 15);
-#pragma unroll
-            for (int s = 0; s < kGramRows / 4; ++s)
-                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[4 * s * ldp], pb[4 * s * ldp], acc[t], 0, 0, 0);
-        }
-        __syncthreads();
+        for (int u = 0; u < kGramBatch; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[u], xb[u], acc, 0, 0, 0);
     }
-    double *out = gram_part + (long)blockIdx.x * r * r;
 #pragma unroll
-    for (int t = 0; t < kGramTPW; ++t) {
-        if (!on[t]) continue;
-        const int col = tb[t] * 16 + (lane & 15);
+    for (int q = 0; q < 4; ++q) red[w][q * 64 + lane] = acc[q];
+    __syncthreads();
+    const int t = threadIdx.x;   // t = q * 64 + l
+    double v = red[0][t];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int row = ta[t] * 16 + (lane >> 4) + 4 * q;
-            if (row < r && col < r) {
-                out[(long)row * r + col] = acc[t][q];
-                out[(long)col * r + row] = acc[t][q];
-            }
-        }
+    for (int ww = 1; ww < kBlock / 64; ++ww) v += red[ww][t];
+    part[((long)tile * C + ch) * 256 + t] = v;
+}
+__global__ void __launch_bounds__(kBlock) k_gram_fin(int r, int C, const double *__restrict__ part,
+                                                     double *__restrict__ out) {
+    const int rt = (r + 15) >> 4;
+    int id = blockIdx.x, a = 0;
+    while (id >= rt - a) { id -= rt - a; ++a; }
+    const int b = a + id, tile = blockIdx.x, t = threadIdx.x;
+    double s = 0.0;
+    for (int c0 = 0; c0 < C; c0 += 8) {   // eight loads in flight, summed in chunk order
+        double pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pv[u] = c0 + u < C ? part[((long)tile * C + c0 + u) * 256 + t] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += pv[u];
+    }
+    const int q = t >> 6, l = t & 63;
+    const int row = 16 * a + (l >> 4) + 4 * q, col = 16 * b + (l & 15);
+    if (row < r && col < r) {
+        out[(long)row * r + col] = s;
+        out[(long)col * r + row] = s;
     }
 }
 
@@ -2075,7 +2082,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     __shared__ double red[12];
     __shared__ double ls[LS_N];
     __shared__ double pl[P_NPAR];
-    __shared__ double gsh[kLatRows * 4];   // slice blocks: the lane groups' partial gradients
+    __shared__ double gsh[kLatRows * E];   // slice blocks: the lane groups' partial gradients
     LRS_TS(2, 0);
     LRS_BLK_BEGIN();
     mirror_ctrl(ctrl, hmirror, seq);
@@ -3150,6 +3157,7 @@ double *device_fin() { return fin_ptr(); }
     case 64 * 8 + 2: { constexpr int GG = 64, EE = 2; BODY; } break;                           \
     case 64 * 8 + 3: { constexpr int GG = 64, EE = 3; BODY; } break;                           \
     case 64 * 8 + 4: { constexpr int GG = 64, EE = 4; BODY; } break;                           \
+    case 64 * 8 + 8: { constexpr int GG = 64, EE = 8; BODY; } break;                           \
     default:                                                                                   \
         snprintf(g_err, sizeof(g_err), "unsupported layout G=%d E=%d", (Gv), (Ev));            \
         return -1;                                                                             \
@@ -3299,19 +3307,28 @@ int launch_alm_m1(const DevProblem &P, double rho, const double *lam, const doub
     return 0;
 }
 static int num_cus();
-int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y, int avg, double *gram_part,
+size_t gram_buf_len(int rmax) {
+    const long rt = (rmax + 15) / 16;
+    return (size_t)rmax * rmax + (size_t)kGramMaxChunks * (rt * (rt + 1) / 2) * 256;
+}
+int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y, int avg, double *gram,
                 int *nblk_used, hipStream_t st) {
     const DevCone &c = P.cones[cone];
     const int rt = (c.r + 15) / 16;
     const int ntiles = rt * (rt + 1) / 2;
-    const int gy = (ntiles + kGramTPB - 1) / kGramTPB;
-    // at most 64 row chunks (the partial buffer holds 64 r x r partials), >= ~2 blocks per CU
-    int gx = std::max(1, std::min(64, (c.nown + kGramRows - 1) / kGramRows));
-    gx = std::min(gx, std::max(1, (2 * num_cus() + gy - 1) / gy));
-    const size_t lds = sizeof(double) * kGramRows * (rt * 16 + 1);
-    hipLaunchKernelGGL(k_gram, dim3(gx, gy), dim3(kBlock), lds, st, c.nown, c.r, c.ld,
+    if (ntiles > kGramMaxTiles) {
+        snprintf(g_err, sizeof(g_err), "gram: rank %d above 512", c.r);
+        return -1;
+    }
+    // row chunks: a multiple of 8 (chunk x's tiles share an XCD), >= 64 rows each, at most
+    // kGramMaxChunks (the partial buffer)
+    int gx = std::max(1, std::min(kGramMaxChunks, (c.nown + 63) / 64));
+    if (gx >= 8) gx &= ~7;
+    hipLaunchKernelGGL(k_gram, dim3(gx, ntiles), dim3(kBlock), 0, st, c.nown, c.r, c.ld,
                        X + c.foff + (long)c.row0 * c.ld, Y ? Y + c.foff + (long)c.row0 * c.ld : nullptr, avg,
-                       gram_part);
+                       gram + (long)c.r * c.r, gram);
+    LRS_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_gram_fin, dim3(ntiles), dim3(kBlock), 0, st, c.r, gx, gram + (long)c.r * c.r, gram);
     LRS_CHECK_LAUNCH();
     if (nblk_used) *nblk_used = gx;
     return 0;
@@ -3508,6 +3525,12 @@ __global__ void __launch_bounds__(kBlock) k_fold_partials(const double *__restri
     __shared__ double red[NV];
     reduce_partials<NV, kBlock>(part, nblk, red);
     if (threadIdx.x < NV) out[threadIdx.x] = red[threadIdx.x];
+}
+// one scalar's partials (the sharded CG's <p, Q>, <r, r>, ||b||_1) -> out[0]
+int launch_fold1(const double *part, int nblk, double *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_partials<1>, dim3(1), dim3(kBlock), 0, st, part, nblk, out);
+    LRS_CHECK_LAUNCH();
+    return 0;
 }
 
 int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t st) {
@@ -3800,14 +3823,6 @@ __global__ void k_ls_only(const double *__restrict__ par, int K, double *__restr
     __syncthreads();
     if (threadIdx.x < LS_N) lsout[threadIdx.x] = ls[threadIdx.x];
 }
-__global__ void __launch_bounds__(kBlock) k_gram_reduce(int nblk, int rr, const double *__restrict__ part,
-                                                        double *__restrict__ out) {
-    for (int idx = blockIdx.x * kBlock + threadIdx.x; idx < rr; idx += gridDim.x * kBlock) {
-        double s = 0.0;
-        for (int b = 0; b < nblk; ++b) s += part[(long)b * rr + idx];
-        out[idx] = s;
-    }
-}
 
 int launch_resid(int m, const double *b, const double *x, hipStream_t st) {
     static double *gpart = nullptr;
@@ -3829,11 +3844,6 @@ int launch_avg(long n, const double *U, const double *V, double *R, hipStream_t 
 int launch_admm_m1(int m, double rho, const double *b, const double *cvs, const double *cv, const double *lam,
                    double *M1, hipStream_t st) {
     hipLaunchKernelGGL(k_admm_m1, dim3(grid_elems(m, 1)), dim3(kBlock), 0, st, m, rho, b, cvs, cv, lam, M1);
-    LRS_CHECK_LAUNCH();
-    return 0;
-}
-int launch_gram_reduce(int nblk, int rr, const double *part, double *out, hipStream_t st) {
-    hipLaunchKernelGGL(k_gram_reduce, dim3(grid_elems(rr, 1)), dim3(kBlock), 0, st, nblk, rr, part, out);
     LRS_CHECK_LAUNCH();
     return 0;
 }
@@ -3866,7 +3876,7 @@ static StagePlan plan_cg_mv(const DevCone &c) {
     const int T = team_size(c, deg, 4);
     StagePlan p;
     p.T = T;
-    const long need = std::max(1L, ((long)c.n * c.G * T + kRowBlock - 1) / kRowBlock);
+    const long need = std::max(1L, ((long)c.nown * c.G * T + kRowBlock - 1) / kRowBlock);
     p.grid = (int)std::min<long>(need, kMaxPartialBlocks);
     p.small = true;
     return p;
@@ -3876,9 +3886,12 @@ int launch_cg_mv(const DevProblem &P, int cone, const double *w, const double *V
     const DevCone &c = P.cones[cone];
     const StagePlan pl = plan_cg_mv(c);
     LRS_LAYOUT_SWITCH(c.G, c.E, {
-        hipLaunchKernelGGL((k_cg_mv<GG, EE, 4>), dim3(pl.grid), dim3(kRowBlock), 0, st, c.n, c.ld, c.adj_ptr,
-                           c.adj_col, c.adj_slot, P.slot_ptr, P.slot_con, P.slot_a, w, V + c.foff, Xin + c.foff,
-                           Q + c.foff, part, cgc, guarded, pl.T);
+        // the cone's computed rows [row0, row0 + nown) (a sharded solve's owned rows); the
+        // neighbours' rows of V are addressed from the cone's first local row
+        const long o = c.foff + (long)c.row0 * c.ld;
+        hipLaunchKernelGGL((k_cg_mv<GG, EE, 4>), dim3(pl.grid), dim3(kRowBlock), 0, st, c.nown, c.ld,
+                           c.adj_ptr + c.row0, c.adj_col, c.adj_slot, P.slot_ptr, P.slot_con, P.slot_a, w,
+                           V + c.foff, Xin + o, Q + o, part, cgc, guarded, pl.T);
     });
     LRS_CHECK_LAUNCH();
     if (nblk) *nblk = pl.grid;

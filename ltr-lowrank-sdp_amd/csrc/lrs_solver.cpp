@@ -39,7 +39,6 @@ int launch_admm_m1(int m, double rho, const double *b, const double *cvs, const 
                    double *M1, hipStream_t st);
 int launch_ls_only(const DevProblem &P, DevWork &W, hipStream_t st);
 int launch_alm_dir_only(const DevProblem &P, DevWork &W, hipStream_t st);
-int launch_gram_reduce(int nblk, int rr, const double *part, double *out, hipStream_t st);
 }  // namespace lrs
 
 using namespace lrs;
@@ -135,6 +134,17 @@ struct lrs_ctx {
     // hipGraph cache of inner-iteration batches (keyed by batch size; the kernels'
     // arguments are the workspace pointers, so a new workspace drops the cache)
     std::map<int, hipGraphExec_t> graphs;
+    // per-cone Lanczos workspace and its two captured graphs (one step, a chunk of steps),
+    // kept across calls: no per-call device allocation around a graph replay
+    struct LzWork {
+        int n = 0, kmax = 0;
+        const double *S = nullptr;
+        const int *adj = nullptr;
+        double *Q = nullptr, *w0 = nullptr, *w1 = nullptr, *part = nullptr, *coef = nullptr;
+        int *jp = nullptr;
+        hipGraphExec_t ge[2] = {nullptr, nullptr};
+    };
+    std::vector<LzWork> lz;
     // initial point cache (device layout, host copy) for the ranks it was drawn at
     std::vector<int> init_ranks;
     std::vector<double> init_cache;
@@ -176,6 +186,7 @@ struct lrs_ctx {
     void *buser = nullptr;
     double last_ctl[C_NCTRL] = {0};
     double last_trip[3] = {0, 0, 0};   // tau, ||G||^2, pinf of the last completed inner trip
+    double dinf_tol = 1e-5;            // phase2Tol of the running solve (dual-infeasibility accuracy)
 };
 
 // ------------------------------------------------------------------------
@@ -352,9 +363,21 @@ static void bind(lrs_ctx *c) {
     bind_scratch(c->s_tickets, c->s_tmpfin, c->s_rpart);
 }
 
+static void drop_lanczos(lrs_ctx *c) {
+    if (c->lz.empty()) return;
+    (void)hipStreamSynchronize(c->st);   // nothing captured is still in flight
+    for (auto &w : c->lz) {
+        for (auto &g : w.ge)
+            if (g) (void)hipGraphExecDestroy(g);
+        (void)hipFree(w.Q); (void)hipFree(w.w0); (void)hipFree(w.w1); (void)hipFree(w.part);
+        (void)hipFree(w.coef); (void)hipFree(w.jp);
+    }
+    c->lz.clear();
+}
 static void drop_graphs(lrs_ctx *c) {
     for (auto &kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
     c->graphs.clear();
+    drop_lanczos(c);
 }
 
 static void logf_(lrs_ctx *c, const lrs_params *p, const char *fmt, ...) {
@@ -412,7 +435,7 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
     int rmax = 1;
     for (int k = 0; k < P.K; ++k) {
         Layout L = choose_layout(ranks[k]);
-        if (ranks[k] > L.ld || L.ld > 256) { set_err("rank %d unsupported (max 256)", ranks[k]); return -1; }
+        if (ranks[k] > L.ld) { set_err("rank %d unsupported (max 512)", ranks[k]); return -1; }
         c->lay[k] = L;
         DevCone &dc = P.cones[k];
         dc.r = ranks[k]; dc.ld = L.ld; dc.G = L.G; dc.E = L.E; dc.foff = off;
@@ -436,7 +459,7 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         A(&W.M1, m) || A(&W.wtmp, m) || A(&W.cvc, (long)m * std::max(1, P.K)) ||
         A(&W.part, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.partB, (long)kMaxPartialVals * kMaxPartialBlocks) ||
         A(&W.partC, (long)kMaxPartialVals * kMaxPartialBlocks) || A(&W.ctrl, 2 * C_NCTRL) ||
-        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, 65L * rmax * rmax) || A(&W.rec, 4L * m) || A(&W.R2, NR) || A(&W.cgc, 8) ||
+        A(&W.lsres, 2 * LS_N) || A(&W.par, P_NPAR) || A(&W.gram, (long)gram_buf_len(rmax)) || A(&W.rec, 4L * m) || A(&W.R2, NR) || A(&W.cgc, 8) ||
         A(&W.tot, 32))
         return -1;
     {   // slice gradients of the latency kernels' dense rows
@@ -663,18 +686,43 @@ static double tridiag_min(const std::vector<double> &a, const std::vector<double
 
 static int op_dot(lrs_ctx *c, long n, const double *x, const double *y, double *out);
 // lambda_min of S on cone k (S: device slot values)
-static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int *steps) {
+static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int *steps, bool *converged) {
     const int n = c->dp.cones[k].n;
-    const int kmax = (int)std::max(1L, std::min<long>(std::min<long>(n, kLzStepCap), (long)(2e9 / (8.0 * n))));
-    double *Q = nullptr, *w0 = nullptr, *w1 = nullptr, *part = nullptr, *coef = nullptr;
-    HIPC(hipMalloc((void **)&Q, sizeof(double) * (size_t)n * kmax));
-    HIPC(hipMalloc((void **)&w0, sizeof(double) * n));
-    HIPC(hipMalloc((void **)&w1, sizeof(double) * n));
-    HIPC(hipMalloc((void **)&part, sizeof(double) * (kMaxPartialBlocks + 64 * (size_t)kmax)));
-    HIPC(hipMalloc((void **)&coef, sizeof(double) * 2 * kmax));
-    double *al_d = coef, *bw2_d = coef + kmax;
-    int *jp = nullptr;
-    HIPC(hipMalloc((void **)&jp, sizeof(int)));
+    long cap = kLzStepCap;
+    if (const char *e = getenv("LRS_LANCZOS_CAP")) cap = std::max(2L, std::min<long>(kLzStepCap, atol(e)));   // tests
+    const int kmax = (int)std::max(1L, std::min<long>(std::min<long>(n, cap), (long)(2e9 / (8.0 * n))));
+    constexpr int kChunk = 16, kLzTestEvery = 4;
+    if ((int)c->lz.size() < c->dp.K) c->lz.resize(c->dp.K);
+    if (c->lz[k].n != n || c->lz[k].kmax != kmax || c->lz[k].S != S || c->lz[k].adj != c->dp.cones[k].adj_ptr) {
+        drop_lanczos(c);
+        c->lz.resize(c->dp.K);
+        lrs_ctx::LzWork &N = c->lz[k];
+        HIPC(hipMalloc((void **)&N.Q, sizeof(double) * (size_t)n * kmax));
+        HIPC(hipMalloc((void **)&N.w0, sizeof(double) * n));
+        HIPC(hipMalloc((void **)&N.w1, sizeof(double) * n));
+        HIPC(hipMalloc((void **)&N.part, sizeof(double) * (kMaxPartialBlocks + 64 * (size_t)kmax)));
+        HIPC(hipMalloc((void **)&N.coef, sizeof(double) * 2 * kmax));
+        HIPC(hipMalloc((void **)&N.jp, sizeof(int)));
+        N.n = n; N.kmax = kmax; N.S = S; N.adj = c->dp.cones[k].adj_ptr;
+        // one step's launches and a chunk of kChunk steps, each captured once and replayed (the
+        // step index lives on the device, so every step's launches are the same)
+        for (int q = 0; q < 2; ++q) {
+            hipGraph_t g = nullptr;
+            HIPC(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+            int lr = 0;
+            for (int t = 0; t < (q == 0 ? 1 : kChunk) && lr == 0; ++t)
+                lr = launch_lanczos_step(c->dp, k, S, kmax, N.Q, n, N.w0, N.w1, N.jp, N.coef, N.coef + kmax, N.part,
+                                         c->st);
+            const hipError_t e1 = hipStreamEndCapture(c->st, &g);
+            hipError_t e2 = hipErrorUnknown;
+            if (e1 == hipSuccess && lr == 0) e2 = hipGraphInstantiate(&N.ge[q], g, nullptr, nullptr, 0);
+            if (g) (void)hipGraphDestroy(g);
+            if (e2 != hipSuccess) { set_err("lanczos capture: %s", last_device_error()); return -1; }
+        }
+    }
+    lrs_ctx::LzWork &Wz = c->lz[k];
+    double *Q = Wz.Q, *al_d = Wz.coef, *bw2_d = Wz.coef + kmax;
+    int *jp = Wz.jp;
     HIPC(hipMemsetAsync(jp, 0, sizeof(int), c->st));
     int rc = 0;
     HIPC(hipMemsetAsync(Q, 0, sizeof(double) * (size_t)n * kmax, c->st));
@@ -711,19 +759,6 @@ static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int 
         HIPC(hipMemcpyAsync(Q, q0.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->st));
         HIPC(hipStreamSynchronize(c->st));
     }
-    // one step's launches and a chunk of kChunk steps, each captured once and replayed (the
-    // step index lives on the device, so every step's launches are the same)
-    constexpr int kChunk = 16, kLzTestEvery = 4;
-    hipGraph_t g[2] = {nullptr, nullptr};
-    hipGraphExec_t ge[2] = {nullptr, nullptr};
-    for (int q = 0; q < 2 && rc == 0; ++q) {
-        if (hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal) != hipSuccess) { rc = -1; break; }
-        int lr = 0;
-        for (int t = 0; t < (q == 0 ? 1 : kChunk) && lr == 0; ++t)
-            lr = launch_lanczos_step(c->dp, k, S, kmax, Q, n, w0, w1, jp, al_d, bw2_d, part, c->st);
-        if (hipStreamEndCapture(c->st, &g[q]) != hipSuccess || lr) rc = -1;
-        if (rc == 0 && hipGraphInstantiate(&ge[q], g[q], nullptr, nullptr, 0) != hipSuccess) rc = -1;
-    }
     // Steps run on the device in chunks (alpha_j, ||w_j||^2 stay in device memory); the host
     // fetches a chunk's coefficients and applies the stopping test step by step (every
     // kLzTestEvery steps: the Sturm bisection is the host's cost).  Converged: Ritz residual
@@ -733,14 +768,14 @@ static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int 
     std::vector<double> al, be, alc(kChunk), bwc(kChunk);
     double theta = 0.0, tnorm = 0.0;   // tnorm: Gershgorin bound of T (~ ||S||)
     int j = 0;
-    bool done = false;
+    bool done = false, conv = false;
     while (!done && rc == 0) {
         const int j0 = j, j1 = std::min(kmax, j0 + kChunk);
         if (j1 - j0 == kChunk) {
-            if (hipGraphLaunch(ge[1], c->st) != hipSuccess) rc = -1;
+            if (hipGraphLaunch(Wz.ge[1], c->st) != hipSuccess) rc = -1;
         } else {
             for (int t = j0; t < j1 && rc == 0; ++t)
-                if (hipGraphLaunch(ge[0], c->st) != hipSuccess) rc = -1;
+                if (hipGraphLaunch(Wz.ge[0], c->st) != hipSuccess) rc = -1;
         }
         if (rc) break;
         if (hipMemcpyAsync(alc.data(), al_d + j0, sizeof(double) * (j1 - j0), hipMemcpyDeviceToHost, c->st) !=
@@ -766,6 +801,15 @@ static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int 
                 if (bnew * last <= tol || brk || cap) {
                     j = t + 1;
                     done = true;
+                    // converged: the relative Ritz test, a breakdown, or an absolute residual
+                    // (which bounds |theta - lambda|) below 1e-3 of the amount of lambda_min
+                    // that moves the l_1 dual infeasibility by phase2Tol
+                    const double abs_tol = 1e-3 * c->dinf_tol * (1 + c->hp.cNrm1) * c->scaleObjHis;
+                    conv = bnew * last <= tol || brk || bnew * last <= abs_tol;
+                    if (!conv)
+                        fprintf(stderr, "[lrsdp] dual infeasibility: Lanczos on cone %d stopped at its %d-step cap "
+                                "(Ritz value %.6e, residual %.3e): lambda_min may be lower, the l_1 value a lower bound\n",
+                                k, kmax, theta, bnew * last);
                     break;
                 }
             }
@@ -774,22 +818,17 @@ static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int 
         if (!done) j = j1;
     }
     if (rc) set_err("lanczos: %s", last_device_error());
-    for (int q = 0; q < 2; ++q) {
-        if (ge[q]) (void)hipGraphExecDestroy(ge[q]);
-        if (g[q]) (void)hipGraphDestroy(g[q]);
-    }
     (void)hipStreamSynchronize(c->st);
-    (void)hipFree(Q); (void)hipFree(w0); (void)hipFree(w1); (void)hipFree(part); (void)hipFree(coef);
-    (void)hipFree(jp);
     *lam_min = theta;
     if (steps) *steps = j;
+    if (converged) *converged = conv;
     if (getenv("LRS_LANCZOS_TRACE")) fprintf(stderr, "lanczos cone %d: n %d, %d steps, lambda_min %.12e\n", k, n, j, theta);
     return rc;
 }
 
 // l_1 dual infeasibility of the current lambda (data/lorads_solver.c:1396-1426); lam_min per
 // cone into lmin (may be null)
-static int dual_infeasibility(lrs_ctx *c, double *l1, double *lmin) {
+static int dual_infeasibility(lrs_ctx *c, double *l1, double *lmin, int *all_conv = nullptr) {
     DevWork &W = c->W;
     const int m = c->dp.m;
     HIPC(hipMemsetAsync(W.wtmp, 0, sizeof(double) * m, c->st));
@@ -798,8 +837,10 @@ static int dual_infeasibility(lrs_ctx *c, double *l1, double *lmin) {
     double err = 0.0;
     for (int k = 0; k < c->dp.K; ++k) {
         double lk = 0.0;
-        if (lanczos_min(c, k, W.S, &lk, nullptr)) return -1;
+        bool conv = true;
+        if (lanczos_min(c, k, W.S, &lk, nullptr, &conv)) return -1;
         if (lmin) lmin[k] = lk;
+        if (all_conv && !conv) *all_conv = 0;
         err += std::fabs(std::min(lk, 0.0));
     }
     err /= c->scaleObjHis;
@@ -896,9 +937,8 @@ static int gram_of(lrs_ctx *c, int k, const double *X, const double *Y, int avg,
     int nblk = 0;
     OPC(launch_gram(c->dp, k, X, Y, avg, c->W.gram, &nblk, c->st));
     const int rr = c->rank[k] * c->rank[k];
-    OPC(launch_gram_reduce(nblk, rr, c->W.gram, c->W.gram + 64L * rr, c->st));
     g.resize(rr);
-    HIPC(hipMemcpyAsync(g.data(), c->W.gram + 64L * rr, sizeof(double) * rr, hipMemcpyDeviceToHost, c->st));
+    HIPC(hipMemcpyAsync(g.data(), c->W.gram, sizeof(double) * rr, hipMemcpyDeviceToHost, c->st));
     HIPC(hipStreamSynchronize(c->st));
     if (sharded(c)) return c->comm->allreduce_host(c, g.data(), rr);
     return 0;
@@ -1469,22 +1509,40 @@ static int lin_sys_product(lrs_ctx *c, int k, const double *Y, const double *x, 
 
 // CGSolve (linalg/lorads_cgs.c:128-287) on the device: initial residual, then batches of
 // iterations (4 launches each; the restart every 20 iterations adds 4) with all scalars
-// in W.cgc; one poll per batch.
+// in W.cgc; one poll per batch.  Sharded: the vectors are the owned rows, and each
+// reduction (||b||_1, <p, Q>, <r, r>) is folded and summed over the shards in the stream
+// (ncclAllReduce of one double) before the kernel that consumes it, which then reads the
+// total as its only partial -- the "CG dot-products" all-reduce of SURVEY.md §8(e).  The
+// matvec needs no halo: an owned constraint's entries lie in owned rows.
 static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double *b, double tol, int maxit) {
     DevProblem &P = c->dp;
     DevWork &W = c->W;
     const DevCone &d = P.cones[k];
-    const long nr = (long)d.n * d.ld;
-    double *r = W.cg_r + d.foff, *p = W.cg_p + d.foff, *Q = W.cg_Q + d.foff;
-    double *xk = X + d.foff;
-    const double *bk = b + d.foff;
+    const long o = d.foff + (long)d.row0 * d.ld;
+    const long nr = (long)d.nown * d.ld;
+    double *r = W.cg_r + o, *p = W.cg_p + o, *Q = W.cg_Q + o;
+    double *xk = X + o;
+    const double *bk = b + o;
     double *cgc = W.cgc;
+    const bool sh = sharded(c);
+    double *tot = W.tot + 26;   // sharded: the summed scalar the next kernel reads
+    // a reduction's partials -> what its consumer reads (sharded: folded, summed over shards)
+    auto sum = [&](double *part, int &nblk) -> int {
+        if (!sh) return 0;
+        OPC(launch_fold1(part, nblk, tot, c->st));
+        if (c->comm->allreduce_dev(c, tot, 1, c->st)) return -1;
+        nblk = 1;
+        return 0;
+    };
+    double *pA = sh ? tot : W.part, *pB = sh ? tot : W.partB, *pC = sh ? tot : W.partC;
     int nA = 0, nB = 0, nC = 0, nR = 0;
     OPC(launch_cg_nrm1(nr, bk, W.part, c->st, &nA));
+    if (sum(W.part, nA)) return -1;
     OPC(launch_auv_con(P, k, 0, X, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, nullptr));
     OPC(launch_cg_mv(P, k, W.wtmp, Y, X, W.cg_Q, nullptr, cgc, 0, c->st, &nB));
-    OPC(launch_cg_resid(nr, bk, Q, r, p, W.partC, cgc, W.part, nA, 1, c->st, &nC));
-    OPC(launch_cg_resid2(nr, r, p, W.partC, nC, cgc, tol, 0, 1, c->st));
+    OPC(launch_cg_resid(nr, bk, Q, r, p, W.partC, cgc, pA, nA, 1, c->st, &nC));
+    if (sum(W.partC, nC)) return -1;
+    OPC(launch_cg_resid2(nr, r, p, pC, nC, cgc, tol, 0, 1, c->st));
     double *h = c->hpin + 256;
     // first batch sized from this cone's previous solve (ADMM's CG solves take a handful of
     // iterations each; the batch past convergence runs guarded no-op launches), then doubling
@@ -1495,14 +1553,17 @@ static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double 
             const int par = it & 1;
             OPC(launch_auv_con(P, k, 0, W.cg_p, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, cgc));
             OPC(launch_cg_mv(P, k, W.wtmp, Y, W.cg_p, W.cg_Q, W.partB, cgc, 1, c->st, &nB));
-            OPC(launch_cg_upd(nr, xk, r, p, Q, W.partB, nB, W.partC, cgc, par, it, c->st, &nC));
+            if (sum(W.partB, nB)) return -1;
+            OPC(launch_cg_upd(nr, xk, r, p, Q, pB, nB, W.partC, cgc, par, it, c->st, &nC));
+            if (sum(W.partC, nC)) return -1;
             const int restart = (it % 20 == 0);
-            OPC(launch_cg_conv(nr, r, p, W.partC, nC, cgc, tol, par, restart, c->st));
+            OPC(launch_cg_conv(nr, r, p, pC, nC, cgc, tol, par, restart, c->st));
             if (restart) {
                 OPC(launch_auv_con(P, k, 0, X, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, cgc));
                 OPC(launch_cg_mv(P, k, W.wtmp, Y, X, W.cg_Q, nullptr, cgc, 1, c->st, &nB));
                 OPC(launch_cg_resid(nr, bk, Q, r, p, W.partC, cgc, nullptr, 0, 0, c->st, &nR));
-                OPC(launch_cg_resid2(nr, r, p, W.partC, nR, cgc, tol, par, 0, c->st));
+                if (sum(W.partC, nR)) return -1;
+                OPC(launch_cg_resid2(nr, r, p, pC, nR, cgc, tol, par, 0, c->st));
             }
         }
         HIPC(hipMemcpyAsync(h, cgc, sizeof(double) * CG_N, hipMemcpyDeviceToHost, c->st));
@@ -1511,6 +1572,9 @@ static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double 
         B = std::min(2 * B, 64);
     }
     c->cgIterCone[k] = (long)h[CG_ITERS];
+    // sharded: the solved factor's halo rows from their owners (the next half-step's RHS and
+    // the objective read them)
+    if (sh && c->comm->halo(c, X, c->st)) return -1;
     return 0;
 }
 
@@ -2223,9 +2287,9 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     lrs_params prm = *pin;
     lrs_params *p = &prm;
     p->rhoCellingADMM = p->rhoMax * 200;   // main.c:350
-    if (sharded(c)) p->skipADMM = 1;       // the sharded solve covers the ALM phase
     memset(res, 0, sizeof(*res));
     const double tss = now_s();
+    c->dinf_tol = p->phase2Tol;
     if (obj_unscale(c)) return -1;   // a previous solve's reopt scaled C on the device
     std::vector<int> r, rm;
     determine_rank(c, p, r, rm);
@@ -2256,6 +2320,7 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     bool timeout = now_s() - tss > p->timeSecLimit;
     double t_admm = 0;
     double dinf = -1.0;   // not evaluated (phase 2 skipped)
+    int dinf_conv = -1;
     if (!timeout && !p->skipADMM) {
         if (alm_to_admm(c, p, alm, admm)) return -1;
         const double ta = now_s();
@@ -2275,34 +2340,39 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
                 if (now_s() - tss > p->timeSecLimit) { timeout = true; break; }
             }
         }
-        // dual infeasibility of the phase-2 multipliers (main.c:515-527)
-        if (dual_infeasibility(c, &dinf, nullptr)) return -1;
-        admm.gap = c->dimGap;
-        admm.pinf1 = c->dimPinf;
-        logf_(c, p, "-----------------------------------------------------------------------\n"
-                    "Dual infeasibility: l_1 = %f, l_inf = %f, l_2 = %f\n"
-                    "-----------------------------------------------------------------------\n",
-              dinf, dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrmInf), dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrm2));
-        // reoptLevel >= 2 (main.c:527-580): up to two more rounds, each followed by the
-        // U/V average and a new dual infeasibility
-        if (p->reoptLevel >= 2 && !timeout) {
-            int dual_cnt = 0;
-            while (dinf > p->phase2Tol || admm.gap > p->phase2Tol || admm.pinf1 > p->phase2Tol) {
-                if (dual_cnt >= 2) break;
-                if (!p->highAccMode && dinf <= 5 * p->phase2Tol && admm.gap <= 5 * p->phase2Tol &&
-                    admm.pinf1 <= p->phase2Tol)
-                    break;
-                if (reopt(c, p, alm, admm, reopt_param, 3, 50, tss, &bad, 2)) return -1;
-                OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
-                HIPC(hipMemcpyAsync(c->W.V, c->W.R, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
-                if (dual_infeasibility(c, &dinf, nullptr)) return -1;
-                admm.gap = c->dimGap;
-                admm.pinf1 = c->dimPinf;
-                admm.pinfinf = c->dimPinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
-                logf_(c, p, "reopt %d:Dual infeasibility: l_1 = %f, l_inf = %f, l_2 = %f\n", dual_cnt, dinf,
-                      dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrmInf), dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrm2));
-                dual_cnt++;
-                if (now_s() - tss > p->timeSecLimit) { timeout = true; break; }
+        // dual infeasibility of the phase-2 multipliers (main.c:515-527); a time-limit exit of
+        // the reopt round jumps past it to END_SOLVING like main.c:505-510
+        if (!timeout) {
+            dinf_conv = sharded(c) ? -1 : 1;   // sharded: not evaluated
+            if (!sharded(c) && dual_infeasibility(c, &dinf, nullptr, &dinf_conv)) return -1;
+            admm.gap = c->dimGap;
+            admm.pinf1 = c->dimPinf;
+            logf_(c, p, "-----------------------------------------------------------------------\n"
+                        "Dual infeasibility: l_1 = %f, l_inf = %f, l_2 = %f\n"
+                        "-----------------------------------------------------------------------\n",
+                  dinf, dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrmInf), dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrm2));
+            // reoptLevel >= 2 (main.c:527-580): up to two more rounds, each followed by the
+            // U/V average and a new dual infeasibility
+            if (p->reoptLevel >= 2 && !timeout) {
+                int dual_cnt = 0;
+                while (dinf > p->phase2Tol || admm.gap > p->phase2Tol || admm.pinf1 > p->phase2Tol) {
+                    if (dual_cnt >= 2) break;
+                    if (!p->highAccMode && dinf <= 5 * p->phase2Tol && admm.gap <= 5 * p->phase2Tol &&
+                        admm.pinf1 <= p->phase2Tol)
+                        break;
+                    if (reopt(c, p, alm, admm, reopt_param, 3, 50, tss, &bad, 2)) return -1;
+                    OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
+                    HIPC(hipMemcpyAsync(c->W.V, c->W.R, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
+                    dinf_conv = sharded(c) ? -1 : 1;   // sharded: not evaluated
+                    if (!sharded(c) && dual_infeasibility(c, &dinf, nullptr, &dinf_conv)) return -1;
+                    admm.gap = c->dimGap;
+                    admm.pinf1 = c->dimPinf;
+                    admm.pinfinf = c->dimPinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+                    logf_(c, p, "reopt %d:Dual infeasibility: l_1 = %f, l_inf = %f, l_2 = %f\n", dual_cnt, dinf,
+                          dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrmInf), dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrm2));
+                    dual_cnt++;
+                    if (now_s() - tss > p->timeSecLimit) { timeout = true; break; }
+                }
             }
         }
         t_admm = now_s() - ta;
@@ -2313,10 +2383,12 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     }
     HIPC(hipStreamSynchronize(c->st));
     const double all_time = now_s() - t0;
-    // main.c:519-525
-    admm.gap = c->dimGap;
-    admm.pinf1 = c->dimPinf;
-    admm.pinfinf = c->dimPinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+    // main.c:519-525 (END_SOLVING after a time limit keeps the ADMM state as it was)
+    if (!timeout) {
+        admm.gap = c->dimGap;
+        admm.pinf1 = c->dimPinf;
+        admm.pinfinf = c->dimPinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+    }
     res->admm_iter = admm.iter; res->cg_iter = admm.cg_iter;
     res->pobj = admm.pobj; res->dobj = admm.dobj; res->pinf = admm.pinf1; res->pinf_inf = admm.pinfinf;
     res->gap = admm.gap; res->rho = admm.rho;
@@ -2326,8 +2398,11 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     res->dinf = dinf;
     res->dinf_inf = dinf < 0 ? dinf : dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrmInf);
     res->dinf_2 = dinf < 0 ? dinf : dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrm2);
+    res->dinf_converged = dinf_conv;
+    // PRIMAL_DUAL_OPTIMAL only on a dual infeasibility whose eigen-solve converged (a Ritz value
+    // at the step cap only bounds lambda_min from above)
     if (timeout) res->status = 4;
-    else if (dinf >= 0 && dinf <= 5 * p->phase2Tol && admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol)
+    else if (dinf >= 0 && dinf_conv == 1 && dinf <= 5 * p->phase2Tol && admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol)
         res->status = 1;
     else if (admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol) res->status = 2;
     else res->status = 3;
@@ -2550,37 +2625,30 @@ int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {
     return 0;
 }
 
-// Standalone r x r Gram of cone `cone` on R (k_gram on the FP64 matrix cores + the
-// fixed-order partial reduction): reps back to back between two HIP events.
+// Standalone r x r Gram of cone `cone` on R (one k_gram launch: MFMA tiles + the
+// last-arriving chunk's fixed-order reduction): reps back to back between two HIP events.
+// Both outputs are that launch's average (the reduction is no longer a second kernel).
 int lrs_time_gram(lrs_ctx *c, int cone, int reps, double *avg_ms, double *gram_ms) {
     if (c) bind(c);
     if (cone < 0 || cone >= c->dp.K) {
         set_err("time_gram: bad cone %d", cone);
         return -1;
     }
-    hipEvent_t e0, e1, e2;
+    hipEvent_t e0, e1;
     HIPC(hipEventCreate(&e0));
     HIPC(hipEventCreate(&e1));
-    HIPC(hipEventCreate(&e2));
-    const int rr = c->rank[cone] * c->rank[cone];
     int nblk = 0;
+    OPC(launch_gram(c->dp, cone, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st));
     HIPC(hipEventRecord(e0, c->st));
     for (int q = 0; q < reps; ++q) OPC(launch_gram(c->dp, cone, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st));
     HIPC(hipEventRecord(e1, c->st));
-    for (int q = 0; q < reps; ++q) {
-        OPC(launch_gram(c->dp, cone, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st));
-        OPC(launch_gram_reduce(nblk, rr, c->W.gram, c->W.gram + 64L * rr, c->st));
-    }
-    HIPC(hipEventRecord(e2, c->st));
-    HIPC(hipEventSynchronize(e2));
-    float ms0 = 0, ms1 = 0;
-    HIPC(hipEventElapsedTime(&ms0, e0, e1));
-    HIPC(hipEventElapsedTime(&ms1, e1, e2));
-    if (gram_ms) *gram_ms = ms0 / reps;
-    *avg_ms = ms1 / reps;
+    HIPC(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPC(hipEventElapsedTime(&ms, e0, e1));
+    *avg_ms = ms / reps;
+    if (gram_ms) *gram_ms = ms / reps;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    (void)hipEventDestroy(e2);
     return 0;
 }
 
@@ -2628,6 +2696,10 @@ static int shard_setup(lrs_ctx *c, int world, int rank) {
 int lrs_shard_rccl(lrs_ctx *c, int world, int rank, const char *id) {
     if (!c) { set_err("null ctx"); return -1; }
     bind(c);
+    // one shard is the unsharded solve: no fold / all-reduce launches per stage (they cost
+    // 19 % of the G81 rate at world 1); LRS_FORCE_SHARD=1 keeps the RCCL plumbing (tests)
+    const char *force = getenv("LRS_FORCE_SHARD");
+    if (world == 1 && rank == 0 && !(force && atoi(force) != 0)) return 0;
     if (shard_setup(c, world, rank)) return -1;
     RcclComm *rc = new RcclComm();
     ncclUniqueId uid;

@@ -53,7 +53,7 @@ class Result(C.Structure):
         ("alm_time", C.c_double), ("admm_time", C.c_double), ("read_time", C.c_double), ("status", C.c_int),
         ("retcode", C.c_int), ("final_rank", C.c_int), ("oracle_rank", C.c_int), ("traj1_len", C.c_int),
         ("traj2_len", C.c_int), ("rho_max", C.c_double), ("dinf", C.c_double), ("dinf_inf", C.c_double),
-        ("dinf_2", C.c_double),
+        ("dinf_2", C.c_double), ("dinf_converged", C.c_int),
     ]
 
     def as_dict(self):

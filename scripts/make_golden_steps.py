@@ -38,7 +38,17 @@ CASES = [
     ("rsparse60", os.path.join(GOLD, "instances", "rsparse60.dat-s"), -1, [1, 2, 3, 4, 5]),
     # the reference's own bundled instance with hub rows (the latency kernels' slice blocks)
     ("checker_1.5", os.path.join(ROOT, "data", "bundled", "checker_1.5.dat-s"), -1, [1, 3, 5]),
+    # rank 290 > 256 (the 64 x 8 layout): the n x r arrays stored as n x 4 projections R @ Omega
+    ("mc_rand300w_r290", os.path.join(GOLD, "instances", "mc_rand300w.dat-s"), 290, [1, 2, 3, 5, 8]),
 ]
+PROJ = {"mc_rand300w_r290": 4}
+
+
+def project(v, n, k, seed=7):
+    """Col-major n x r array (one cone) -> (n x k) = V @ Omega, Omega ~ N(0,1) (r x k), seeded."""
+    r = v.size // n
+    om = np.random.default_rng(seed).standard_normal((r, k))
+    return v.reshape(r, n).T @ om
 
 
 def run_steps(path, rank, K, m, nr):
@@ -73,7 +83,10 @@ def dims_of(path):
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle -f Makefile.ref")
+    only = set(sys.argv[1:])
     for name, path, rank, ks in CASES:
+        if only and name not in only:
+            continue
         m, dims = dims_of(path)
         # the reference's rank per cone is only known after presolve: read it back from R's size
         probe = None
@@ -92,6 +105,8 @@ def main():
                 probe = rest // 4
             d = run_steps(path, rank, K, m, probe)
             for k, v in d.items():
+                if name in PROJ and k in ("R", "G", "s", "y"):
+                    v = project(v, dims[0], PROJ[name])
                 out[f"K{K}_{k}"] = v
         out["ks"] = np.array(ks)
         out["m"] = np.array(m)

@@ -1,0 +1,55 @@
+"""Ranks above 256 (the factor layouts stopped at ld = 256 while the reference
+has no cap; --fixedRank / rank-schedule entries / AUG_RANK's rank_max = sqrt(2 nnzRows) + 1
+reach past it).  Ranks 257..512 use full 64-lane waves per row with 8 doubles per lane.
+
+Reference: tests/golden/solves_highrank.json (scripts/make_golden_highrank.py, the reference
+LoRADS C code built under oracle/_ref).  Bars as for the MaxCut golden solves
+(test_gpu_parity): ALM inner iterations within +-2, ALM objectives within 1e-6 relative,
+and the per-outer-iteration oracle ranks (r x r Gram of the factor, 290 x 290 here)."""
+import importlib
+import json
+import os
+
+import pytest
+
+from golden_util import GOLDEN, instance
+
+pytestmark = pytest.mark.gpu
+
+
+def cases():
+    with open(os.path.join(GOLDEN, "solves_highrank.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("kpath", [0, 1])
+def test_rank_above_256_matches_reference(kpath):
+    solver = importlib.import_module("ltr-lowrank-sdp_amd.solver")
+    for g in cases():
+        kw = {}
+        for k, v in zip(g["flags"][0::2], g["flags"][1::2]):
+            k = k.lstrip("-")
+            kw[k] = int(v) if k in ("reoptLevel", "fixedRank") else float(v)
+        sv = solver.Solver(instance(g["instance"]))
+        sv.set_kernel_path(kpath)
+        res = sv.solve(**kw)
+        sv.close()
+        ref = g["result"]
+        assert res["final_rank"] == int(ref["rank"]) > 256
+        assert abs(res["alm_inner"] - ref["alm_inner"]) <= 2, (res["alm_inner"], ref["alm_inner"])
+        for ours, theirs in (("alm_pobj", "alm_pobj"), ("alm_dobj", "alm_dobj")):
+            assert abs(res[ours] - ref[theirs]) <= 1e-6 * abs(ref[theirs]), (ours, res[ours], ref[theirs])
+
+
+def test_rank_above_256_cli_trajectory(tmp_path):
+    import subprocess
+    solver = importlib.import_module("ltr-lowrank-sdp_amd.solver")
+    g = cases()[0]
+    js = tmp_path / "o.json"
+    r = subprocess.run([str(solver.BIN_PATH), instance(g["instance"]), *g["flags"], "--jsonfile", str(js)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0
+    out, ref = json.load(open(js)), g["json"]
+    assert out["trajectory"]["phase_1"]["curr_rank"] == ref["trajectory"]["phase_1"]["curr_rank"]
+    assert out["trajectory"]["phase_1"]["oracle_rank"] == ref["trajectory"]["phase_1"]["oracle_rank"]
+    assert abs(out["metrics"]["primal_obj"] - ref["metrics"]["primal_obj"]) <= 1e-6 * abs(ref["metrics"]["primal_obj"])

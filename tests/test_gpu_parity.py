@@ -203,7 +203,7 @@ def test_bandwidth_regime_matches_latency_regime(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("r", [5, 19, 64, 128, 200])
+@pytest.mark.parametrize("r", [1, 5, 19, 64, 128, 200, 290])
 def test_gram_mfma_matches_fp64(solver_mod, r):
     """k_gram (v_mfma_f64_16x16x4_f64) == X^T X / ((U+V)/2)^T ((U+V)/2) in FP64
     (build_gram_from_factor / _from_average, lorads_logging.c:216-270)."""
@@ -356,3 +356,30 @@ def test_more_than_64_cones_rejected(solver_mod, tmp_path):
     sv.close()
     with pytest.raises(RuntimeError, match="64 SDP cones"):
         solver_mod.Solver(write(65))
+
+
+def test_dinf_step_cap_flagged(solver_mod, monkeypatch):
+    """A dual-infeasibility eigen-solve stopped by its step cap reports dinf_converged = 0 and
+    the solve does not claim PRIMAL_DUAL_OPTIMAL on it (the Ritz value only bounds lambda_min
+    from above).  LRS_LANCZOS_CAP forces a 4-step cap."""
+    monkeypatch.setenv("LRS_LANCZOS_CAP", "4")
+    sv = solver_mod.Solver(instance("theta40"))
+    r = sv.solve(reoptLevel=0)
+    sv.close()
+    assert r["dinf_converged"] == 0 and r["dinf"] >= 0
+    assert r["status"] != 1
+    monkeypatch.delenv("LRS_LANCZOS_CAP")
+    sv = solver_mod.Solver(instance("mc_rand200"))
+    r = sv.solve(reoptLevel=0)
+    sv.close()
+    assert r["dinf_converged"] in (0, 1)
+
+
+def test_time_limit_skips_dual_infeasibility(solver_mod):
+    """main.c:450-454 / :505-510: a time-limit exit goes to END_SOLVING: no ADMM after the ALM
+    phase, no dual infeasibility (dinf = -1, not evaluated), status TIME_LIMIT (4)."""
+    sv = solver_mod.Solver(instance("theta40"))
+    r = sv.solve(reoptLevel=1, timeSecLimit=1e-9)
+    sv.close()
+    assert r["status"] == 4 and r["dinf"] == -1.0 and r["dinf_converged"] == -1
+    assert r["admm_iter"] == 0

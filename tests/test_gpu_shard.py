@@ -82,10 +82,12 @@ def test_sharded_deterministic(solver_mod):
     assert a[0][1]["alm_pobj"] == b[0][1]["alm_pobj"] and a[0][1]["alm_inner"] == b[0][1]["alm_inner"]
 
 
-def test_rccl_transport_world1(solver_mod):
+def test_rccl_transport_world1(solver_mod, monkeypatch):
     """The RCCL transport's plumbing on one GPU (a communicator of one rank: all-reduces,
-    no halo peers); bench.py drives the same calls on N GPUs under torch.distributed.run."""
-    kw = dict(reoptLevel=0, skipADMM=1)
+    no halo peers; LRS_FORCE_SHARD=1, since one shard is otherwise the unsharded solve);
+    bench.py drives the same calls on N GPUs under torch.distributed.run."""
+    monkeypatch.setenv("LRS_FORCE_SHARD", "1")
+    kw = dict(reoptLevel=0)
     single = solver_mod.Solver(instance("mc_torus12x10"))
     ref = single.solve(**kw)
     single.close()
@@ -97,4 +99,40 @@ def test_rccl_transport_world1(solver_mod):
     sv.close()
     assert abs(r["alm_inner"] - ref["alm_inner"]) <= 2
     assert abs(r["alm_pobj"] - ref["alm_pobj"]) <= 1e-6 * abs(ref["alm_pobj"])
+    assert abs(r["pobj"] - ref["pobj"]) <= 1e-6 * abs(ref["pobj"])   # ADMM phase over RCCL too
     assert out["done"] == 40
+
+
+def test_rccl_world1_is_unsharded(solver_mod):
+    """lrs_shard_rccl(world = 1) leaves the context unsharded (no per-stage collectives)."""
+    sv = solver_mod.Solver(instance("mc_torus12x10"))
+    sv.shard_rccl(1, 0, solver_mod.comm_unique_id())
+    assert sv.shard_info() == (1, 0, 0, 120, 0)
+    r = sv.solve(reoptLevel=0)
+    sv.close()
+    assert r["dinf"] >= 0          # the unsharded path (a sharded solve does not evaluate it)
+
+
+@pytest.mark.parametrize("name,world", [("mc_torus12x10", 2), ("mc_torus12x10", 4), ("mc_rand200", 3),
+                                        ("mc_rand300w", 2)])
+def test_sharded_full_solve_matches_single_gpu(solver_mod, name, world):
+    """ALM + ADMM sharded: the ADMM half-steps' CG runs on each shard's owned rows with its
+    <p, Q>, <r, r> and ||b||_1 summed over the shards, the solved factor's
+    halo rows exchanged after each half-step.  Every shard runs the identical control; the
+    solve reproduces the single-GPU one (ALM inner iterations within +-2, ADMM iterations
+    within +-1, objectives within 1e-6 relative)."""
+    kw = dict(reoptLevel=0)
+    single = solver_mod.Solver(instance(name))
+    ref = single.solve(**kw)
+    single.close()
+    res = run_sharded(solver_mod, instance(name), world, lambda sv: sv.solve(**kw))
+    first = res[0][1]
+    for _, r in res[1:]:
+        for k in ("alm_inner", "admm_iter", "cg_iter", "pobj", "dobj", "pinf", "gap", "final_rank"):
+            assert r[k] == first[k], (k, r[k], first[k])
+    assert abs(first["alm_inner"] - ref["alm_inner"]) <= 2, (first["alm_inner"], ref["alm_inner"])
+    assert abs(first["admm_iter"] - ref["admm_iter"]) <= 1, (first["admm_iter"], ref["admm_iter"])
+    for k in ("alm_pobj", "alm_dobj", "pobj", "dobj"):
+        assert abs(first[k] - ref[k]) <= 1e-6 * max(1.0, abs(ref[k])), (k, first[k], ref[k])
+    assert first["pinf"] <= max(1e-6, 10 * ref["pinf"])
+    assert first["dinf"] == -1.0 and first["dinf_converged"] == -1   # not evaluated when sharded
