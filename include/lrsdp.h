@@ -225,6 +225,15 @@ void lrs_loopback_destroy(lrs_loopback *g);
 int lrs_shard_loopback(lrs_ctx *ctx, lrs_loopback *g, int rank);
 /* world, rank, first global row, owned rows, halo rows of this context (1, 0, 0, n, 0 unsharded) */
 int lrs_shard_info(lrs_ctx *ctx, int *world, int *rank, int *row0, int *nown, int *nhalo);
+/* Host-only (no device, no context) view of the row partition of a sharded solve of the
+   instance at `path`: counts[8] = {n_global, first owned global row, owned rows, local rows
+   (owned + halo), send rows (all peers), shared constraints, local constraints, world}, then
+   (arrays may be null) bounds[world+1], local_gid[local rows], send_ptr[world+1],
+   send_gid[send rows] (global ids, grouped by peer), shared_gid[shared], con_gid[local
+   constraints], primary[local constraints] (1: this shard counts it in sums).  Replaces the
+   reference's nothing: LoRADS has no multi-process path. */
+int lrs_shard_plan(const char *path, int world, int rank, long *counts, int *bounds, int *local_gid,
+                   int *send_ptr, int *send_gid, int *shared_gid, int *con_gid, int *primary);
 
 #ifdef __cplusplus
 }

@@ -145,6 +145,14 @@ struct DevProblem {
     int *long_rows = nullptr;                                // constraints with > kLongRow entries in a cone,
     std::vector<int> long_ptr_h;                             //   grouped by cone: long_ptr_h[k]..[k+1]
     double *con1_w = nullptr;                                // [K*m] their weight
+    // sharded solve: constraints held by several shards ("shared", lrs_problem.h ShardPlan)
+    int nsh = 0;                                             // shared constraints (same on every shard)
+    int *sh_idx = nullptr;                                   // [m] local constraint -> shared index, -1
+    double *cmask = nullptr;                                 // [m] 1 where this shard counts the constraint
+    double *bprim = nullptr;                                 // [m] b * cmask (b^T lambda counted once)
+    double *g3 = nullptr;                                    // [3][m] owned-slot sums RR, RD, DD (global cons)
+    double *gpack = nullptr;                                 // [nsh][3] the shared ones, all-reduced
+    double *spack = nullptr;                                 // [nsh] one m-vector's shared entries
     std::vector<DevCone> cones;
     // K > 1: all cones as one block-diagonal row space (global rows and columns); used by
     // the split iteration when every cone has the same (G, E) row layout
@@ -261,6 +269,8 @@ constexpr int kLzStepCap = 300;   // Lanczos steps at most (the device step kern
 void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart);
 // sharded solve helpers
 int launch_pack_rows(int nrows, int ld, const int *rows, const double *src, double *dst, hipStream_t st);
+// sharded: sum an m-vector's shared-constraint entries over the shards (no-op otherwise)
+int sync_shared(const DevProblem &P, double *v, hipStream_t st);
 // fold one scalar's per-block partials into out[0] (sharded CG, before its all-reduce)
 int launch_fold1(const double *part, int nblk, double *out, hipStream_t st);
 int launch_sum_shards(int n, int world, const double *const *src, double *out, hipStream_t st);

@@ -1455,6 +1455,112 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
     LRS_BLK_END(1);
 }
 
+// ---- sharded solve, global constraints (lrs_problem.h ShardPlan: shared constraints) ----
+// G1: this shard's share of every global constraint: sums over its owned-slot entries (the
+// others carry weight 0) of RR (the last stage B's slots), RD and DD (this stage A's) ->
+// g3[3][m], or for a shared constraint its row of gpack[nsh][3] (zero-filled before; the
+// holders' rows meet in an all-reduce).
+__global__ void __launch_bounds__(kBlock) k_g_part(int mg, const int *__restrict__ glob, int m,
+                                                   const int *__restrict__ con_ptr, const int *__restrict__ con_slot,
+                                                   const double *__restrict__ con_w, const double *__restrict__ uRR,
+                                                   const double *__restrict__ uRD, const double *__restrict__ uDD,
+                                                   const int *__restrict__ sh_idx, double *__restrict__ g3,
+                                                   double *__restrict__ gpack, int gwide) {
+    const int lanes = gwide ? 64 : 1;
+    const int sub = gwide ? (threadIdx.x & 63) : 0;
+    const int gid = gwide ? blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6) : blockIdx.x * kBlock + threadIdx.x;
+    const int gstride = gwide ? gridDim.x * (kBlock / 64) : gridDim.x * kBlock;
+    for (int g = gid; g < mg; g += gstride) {
+        const int i = glob[g];
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+        for (int e = con_ptr[i] + sub; e < con_ptr[i + 1]; e += lanes) {
+            const double w = con_w[e];
+            const int s = con_slot[e];
+            a0 += w * uRR[s];
+            a1 += w * uRD[s];
+            a2 += w * uDD[s];
+        }
+        if (gwide) { a0 = wave_sum(a0); a1 = wave_sum(a1); a2 = wave_sum(a2); }
+        if (sub != 0) continue;
+        const int q = sh_idx[i];
+        if (q >= 0) {
+            gpack[3L * q] = a0; gpack[3L * q + 1] = a1; gpack[3L * q + 2] = a2;
+        } else {
+            g3[i] = a0; g3[m + i] = a1; g3[2L * m + i] = a2;
+        }
+    }
+}
+
+// G2: from the totals, per global constraint: A(RR^T) and its residual (after a fold), q0,
+// q1 = 2 A(sym RD^T), q2 = A(DD^T) and rec -- on every holder --, the line-search dots and
+// the residual counted by the primary holder only (cmask).  Six partials.
+__global__ void __launch_bounds__(kBlock) k_it_g_sh(int mg, const int *__restrict__ glob, int m,
+                                                    const int *__restrict__ sh_idx, const double *__restrict__ g3,
+                                                    const double *__restrict__ gpack,
+                                                    const double *__restrict__ cmask, const double *__restrict__ b,
+                                                    double *__restrict__ cvs, const double *__restrict__ lam,
+                                                    const double *__restrict__ par, const double *__restrict__ ctrl_cur,
+                                                    double *__restrict__ rec, double *__restrict__ partB) {
+    const bool act = ctrl_cur[C_ACTIVE] != 0.0, rr = ctrl_cur[C_RRDONE] != 0.0;
+    const double rho = par[P_RHO], rhoInv = 1.0 / rho;
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int g = blockIdx.x * kBlock + threadIdx.x; g < mg; g += gridDim.x * kBlock) {
+        const int i = glob[g];
+        const int q = sh_idx[i];
+        const double t0 = q >= 0 ? gpack[3L * q] : g3[i];
+        const double t1 = q >= 0 ? gpack[3L * q + 1] : g3[m + i];
+        const double t2 = q >= 0 ? gpack[3L * q + 2] : g3[2L * m + i];
+        const double pm = cmask[i], bi = b[i];
+        if (rr) {
+            cvs[i] = t0;
+            const double dd = bi - t0;
+            acc[5] += pm * (dd * dd);
+        }
+        if (!act) continue;
+        const double v1 = 2.0 * t1, v2 = t2;
+        const double ci = cvs[i], li = lam[i];
+        const double q0 = (bi - ci) + rhoInv * li;
+        acc[0] += pm * (v2 * v2); acc[1] += pm * (v1 * v2); acc[2] += pm * (q0 * v2);
+        acc[3] += pm * (v1 * v1); acc[4] += pm * (q0 * v1);
+        double2 *r = reinterpret_cast<double2 *>(rec + 4L * i);
+        r[0] = make_double2(ci, v1);
+        r[1] = make_double2(v2, (-li) + (-rho) * bi);
+    }
+    write_partials<6>(acc, partB, blockIdx.x);
+}
+
+// G3 (one thread): the phase-1 test of k_it_g on the summed residuals (stage B's local
+// constraints, totC[9], and G2's global ones, totB[5]), then the stage-B activity.
+__global__ void k_g_ph1(const double *__restrict__ par, double *__restrict__ ctrl_cur,
+                        const double *__restrict__ totC, const double *__restrict__ totB) {
+    if (threadIdx.x != 0) return;
+    bool act = ctrl_cur[C_ACTIVE] != 0.0;
+    double ex = ctrl_cur[C_EXIT];
+    if (ctrl_cur[C_RRDONE] != 0.0) {
+        const double pinf1 = sqrt(totC[9] + totB[5]) / (1.0 + par[P_BN1]);
+        const double pinfinf = pinf1 * (1.0 + par[P_BN1]) / (1.0 + par[P_BNINF]);
+        if ((pinfinf <= par[P_PH1TOL]) && ((par[P_GAP] <= par[P_PH1TOL]) || (par[P_HIGHACC] == 0.0))) {
+            act = false;
+            ex = EXIT_PHASE1;
+        }
+        ctrl_cur[C_PINF1] = pinf1;
+        ctrl_cur[C_PINFINF] = pinfinf;
+    }
+    ctrl_cur[C_ACT2] = act ? 1.0 : 0.0;
+    ctrl_cur[C_EXIT2] = ex;
+}
+
+// an m-vector's shared entries <-> the packed buffer (sum over shards in between)
+__global__ void __launch_bounds__(kBlock) k_pack_shared(int m, const int *__restrict__ sh_idx, double *__restrict__ v,
+                                                        double *__restrict__ pk, int unpack) {
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        const int q = sh_idx[i];
+        if (q < 0) continue;
+        if (unpack) v[i] = pk[q];
+        else pk[q] = v[i];
+    }
+}
+
 // B.  Line search (every block, from A's and G's partials), then per row: R_new =
 // R + tau D (written to the other factor buffer; neighbours' rows recomputed), S =
 // C + A^*(M1) per neighbour slot with M1 = -lam - rho b + rho (A(RR^T) + tau q1 +
@@ -1496,7 +1602,7 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_
     } else {
     reduce_partials<7, kRowBlock>(partA, nblkA, red, pstr);
     if (nblkB > 0) {
-        reduce_partials<5, kRowBlock>(partB, nblkB, red + 7);
+        reduce_partials<5, kRowBlock>(partB, nblkB, red + 7, pstr);
         if (threadIdx.x == 0) {
 #pragma unroll
             for (int q = 0; q < 5; ++q) red[2 + q] += red[7 + q];
@@ -3526,6 +3632,19 @@ __global__ void __launch_bounds__(kBlock) k_fold_partials(const double *__restri
     reduce_partials<NV, kBlock>(part, nblk, red);
     if (threadIdx.x < NV) out[threadIdx.x] = red[threadIdx.x];
 }
+// sharded: an m-vector's shared entries summed over the shards (the holders' partial sums of
+// A(.) over their owned entries)
+int sync_shared(const DevProblem &P, double *v, hipStream_t st) {
+    if (!P.shard || P.nsh == 0) return 0;
+    const ShardHooks *sh = P.shard;
+    hipLaunchKernelGGL(k_fill, dim3(grid_elems(P.nsh, 4)), dim3(kBlock), 0, st, (long)P.nsh, 0.0, P.spack);
+    hipLaunchKernelGGL(k_pack_shared, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, P.sh_idx, v, P.spack, 0);
+    LRS_CHECK_LAUNCH();
+    if (sh->allreduce(sh->self, P.spack, P.nsh, st)) return -1;
+    hipLaunchKernelGGL(k_pack_shared, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, P.sh_idx, v, P.spack, 1);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
 // one scalar's partials (the sharded CG's <p, Q>, <r, r>, ||b||_1) -> out[0]
 int launch_fold1(const double *part, int nblk, double *out, hipStream_t st) {
     hipLaunchKernelGGL(k_fold_partials<1>, dim3(1), dim3(kBlock), 0, st, part, nblk, out);
@@ -3542,8 +3661,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     double *ls_cur = W.lsres + parity * LS_N;
     const int L = 2;
     const ShardHooks *sh = P.shard;
-    if (sh && (P.K != 1 || P.mg > 0 || !W.tot)) {
-        snprintf(g_err, sizeof(g_err), "sharded iteration: one cone, single-slot constraints only");
+    if (sh && (P.K != 1 || !W.tot)) {
+        snprintf(g_err, sizeof(g_err), "sharded iteration: one cone only");
         return -1;
     }
     // one launch over the merged row space when every cone has the same row layout
@@ -3616,7 +3735,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], \
                        W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,                \
                        reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs,                                     \
-                       W.lam, W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,      \
+                       W.lam, W.rec, (k == 0 && !sh) ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot,       \
+                       P.con_w,                                                                                   \
                        W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, pa[k].T, gwide, c.row0, \
                        pstr)
         if (lat) {
@@ -3665,7 +3785,30 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     }
     if (mark(1)) return -1;
     // G: phase-1 test and the global constraints' q and dots
-    if (P.mg > 0 && (mask & 2)) {
+    double *totB = sh ? W.tot + 8 : nullptr;
+    if (sh && P.mg > 0 && (mask & 2)) {
+        // sharded: each holder's owned-entry sums, the shared constraints' summed over the
+        // shards, then q / rec / dots from the totals, the dots and residual summed, the
+        // phase-1 test on the summed residual
+        const int g1 = gwide ? gg : std::min(grid_elems(P.mg, 1), kMaxPartialBlocks);
+        if (P.nsh > 0) {
+            hipLaunchKernelGGL(k_fill, dim3(grid_elems(3L * P.nsh, 4)), dim3(kBlock), 0, st, 3L * P.nsh, 0.0, P.gpack);
+            LRS_CHECK_LAUNCH();
+        }
+        hipLaunchKernelGGL(k_g_part, dim3(g1), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.con_ptr, P.con_slot, P.con_w,
+                           W.uvt2, W.uvt0, W.uvt1, P.sh_idx, P.g3, P.gpack, gwide);
+        LRS_CHECK_LAUNCH();
+        if (P.nsh > 0 && sh->allreduce(sh->self, P.gpack, 3 * P.nsh, st)) return -1;
+        const int g2 = std::min(grid_elems(P.mg, 1), kMaxPartialBlocks);
+        hipLaunchKernelGGL(k_it_g_sh, dim3(g2), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.sh_idx, P.g3, P.gpack, P.cmask,
+                           P.b, W.cvs, W.lam, W.par, ctrl_cur, W.rec, W.partB);
+        LRS_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_fold_partials<6>, dim3(1), dim3(kBlock), 0, st, W.partB, g2, totB);
+        LRS_CHECK_LAUNCH();
+        if (sh->allreduce(sh->self, totB, 6, st)) return -1;
+        hipLaunchKernelGGL(k_g_ph1, dim3(1), dim3(64), 0, st, W.par, ctrl_cur, totC, totB);
+        LRS_CHECK_LAUNCH();
+    } else if (P.mg > 0 && (mask & 2)) {
         hipLaunchKernelGGL(k_it_g, dim3(gg), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot,
                            P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, nblkB, W.part,
                            nblkA, W.rec, W.partB, gwide);
@@ -3683,8 +3826,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],        \
                        W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,                        \
                        reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,           \
-                       reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, inA, nA, W.partB,   \
-                       P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, c.n, pstr,                \
+                       reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, inA, nA,            \
+                       sh ? totB : W.partB, P.mg > 0 ? (sh ? 1 : gg) : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, \
+                       c.n, pstr,                                                                                 \
                        (MM) != 2 && k == 0 ? a.hmirror : nullptr, a.seq)
         const bool small = pb[k].small;
         if (lat) {
@@ -3791,11 +3935,12 @@ int launch_sum_shards(int n, int world, const double *const *src, double *out, h
 // small helper kernels used by the host-driven phases
 // ------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) k_resid(int m, const double *__restrict__ b, const double *__restrict__ x,
-                                                  double *part, unsigned *ticket, double *fin) {
+                                                  const double *__restrict__ mask, double *part, unsigned *ticket,
+                                                  double *fin) {
     double acc[1] = {0.0};
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
         const double d = b[i] - x[i];
-        acc[0] += d * d;
+        acc[0] += mask ? mask[i] * (d * d) : d * d;
     }
     partials_finalize<1>(acc, part, ticket, fin);
 }
@@ -3824,14 +3969,14 @@ __global__ void k_ls_only(const double *__restrict__ par, int K, double *__restr
     if (threadIdx.x < LS_N) lsout[threadIdx.x] = ls[threadIdx.x];
 }
 
-int launch_resid(int m, const double *b, const double *x, hipStream_t st) {
+int launch_resid(int m, const double *b, const double *x, hipStream_t st, const double *mask) {
     static double *gpart = nullptr;
     double *part = t_rpart;
     if (!part) {
         if (!gpart && hipMalloc((void **)&gpart, sizeof(double) * kMaxPartialBlocks) != hipSuccess) return -1;
         part = gpart;
     }
-    hipLaunchKernelGGL(k_resid, dim3(grid_elems(m, 1)), dim3(kBlock), 0, st, m, b, x, part, ticket_ptr(T_RR + 40),
+    hipLaunchKernelGGL(k_resid, dim3(grid_elems(m, 1)), dim3(kBlock), 0, st, m, b, x, mask, part, ticket_ptr(T_RR + 40),
                        tmpfin_ptr() + TF_RESID);
     LRS_CHECK_LAUNCH();
     return 0;

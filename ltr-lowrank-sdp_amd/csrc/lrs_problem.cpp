@@ -276,7 +276,10 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
     if (g.K != 1) { err = "sharded solve: one SDP cone only"; return false; }
     const HostCone &gc = g.cones[0];
     const int n = gc.n;
-    if (world < 1 || rank < 0 || rank >= world || n < world) { err = "sharded solve: bad world/rank for n"; return false; }
+    if (world < 1 || world > kMaxShards || rank < 0 || rank >= world || n < world) {
+        err = "sharded solve: bad world/rank for n";
+        return false;
+    }
     plan = ShardPlan();
     plan.world = world; plan.rank = rank; plan.n_global = n;
     // contiguous blocks balanced by (adjacency entries + 1) per row
@@ -293,18 +296,16 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
     plan.bounds[world] = n;
     auto owner = [&](int i) { return (int)(std::upper_bound(plan.bounds.begin(), plan.bounds.end(), i) - plan.bounds.begin()) - 1; };
     const int r0 = plan.bounds[rank], r1 = plan.bounds[rank + 1];
-    // constraint ownership: all entries of a constraint inside one shard's rows
-    std::vector<int> con_owner(g.m, -1);
-    for (const HostEntry &e : gc.ent) {
-        const int oi = owner(gc.prow[e.slot]), oj = owner(gc.pcol[e.slot]);
-        if (oi != oj || (con_owner[e.con] >= 0 && con_owner[e.con] != oi)) {
-            err = "sharded solve: constraint " + std::to_string(e.con + 1) + " spans row blocks";
-            return false;
-        }
-        con_owner[e.con] = oi;
-    }
+    // the shards holding each constraint: those owning an endpoint of one of its entries' slots
+    // (constraints without entries: shard 0, for the residual b_i)
+    std::vector<unsigned long long> holders(g.m, 0ull);
+    for (const HostEntry &e : gc.ent)
+        holders[e.con] |= (1ull << owner(gc.prow[e.slot])) | (1ull << owner(gc.pcol[e.slot]));
     for (int i = 0; i < g.m; ++i)
-        if (con_owner[i] < 0) con_owner[i] = 0;   // constraints without entries: shard 0 (residual b_i)
+        if (holders[i] == 0) holders[i] = 1ull;
+    auto holds = [&](int i) { return ((holders[i] >> rank) & 1ull) != 0; };
+    for (int i = 0; i < g.m; ++i)
+        if (__builtin_popcountll(holders[i]) > 1) plan.shared_gid.push_back(i);
     // local rows: owned + halo, in global order
     std::vector<char> need(n, 0);
     for (int i = r0; i < r1; ++i) {
@@ -320,7 +321,12 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
     // local constraints in global order
     std::vector<int> clid(g.m, -1);
     for (int i = 0; i < g.m; ++i)
-        if (con_owner[i] == rank) { clid[i] = (int)plan.con_gid.size(); plan.con_gid.push_back(i); }
+        if (holds(i)) {
+            clid[i] = (int)plan.con_gid.size();
+            plan.con_gid.push_back(i);
+            plan.primary.push_back(__builtin_ctzll(holders[i]) == rank ? 1 : 0);
+        }
+    for (int gi : plan.shared_gid) plan.shared_lid.push_back(clid[gi]);
     const int ml = (int)plan.con_gid.size();
     // entries of the local problem (already merged and sign-converted: build_problem input)
     std::vector<RawEntry> raw;
@@ -330,13 +336,24 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
         raw.push_back({0, 0, lid[i], lid[j], gc.Craw[t]});
     }
     for (const HostEntry &e : gc.ent) {
-        if (clid[e.con] < 0) continue;
-        raw.push_back({0, clid[e.con] + 1, lid[gc.prow[e.slot]], lid[gc.pcol[e.slot]], e.a});
+        const int i = gc.prow[e.slot], j = gc.pcol[e.slot];
+        if (owner(i) != rank && owner(j) != rank) continue;   // slot not present here
+        raw.push_back({0, clid[e.con] + 1, lid[i], lid[j], e.a});
     }
     out = HostProblem();
     out.b.resize(ml);
     for (int q = 0; q < ml; ++q) out.b[q] = g.b[plan.con_gid[q]];
     if (!build_problem(ml, 1, std::vector<int>{nl}, 0, false, raw, out, err)) return false;
+    // entries count in A(.) on the shard owning their slot's lower row; shared constraints stay
+    // on the multi-slot path on every holder
+    {
+        HostCone &lc = out.cones[0];
+        const int o0 = lid[r0], o1 = o0 + (r1 - r0);
+        for (HostEntry &e : lc.ent) e.owned = lc.prow[e.slot] >= o0 && lc.prow[e.slot] < o1;
+        out.force_glob.assign(ml, 0);
+        for (int l : plan.shared_lid)
+            if (l >= 0) out.force_glob[l] = 1;
+    }
     // the solve's norms and rank statistics are the whole problem's
     out.bNrm1 = g.bNrm1; out.bNrm2 = g.bNrm2; out.bNrmInf = g.bNrmInf;
     out.cNrm1 = g.cNrm1; out.cNrm2 = g.cNrm2; out.cNrmInf = g.cNrmInf;
@@ -410,7 +427,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         for (int i = 0; i < m; ++i) {
             while (e < c.ent.size() && c.ent[e].con == i) {
                 con_slot.push_back(dp.cones[k].slot_off + c.ent[e].slot);
-                con_w.push_back((c.ent[e].diag ? 1.0 : 2.0) * c.ent[e].a);
+                con_w.push_back(c.ent[e].owned ? (c.ent[e].diag ? 1.0 : 2.0) * c.ent[e].a : 0.0);
                 e++;
             }
             con_ptr[(long)k * m + i + 1] = (int)con_slot.size();
@@ -485,8 +502,9 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             }
     std::vector<int> glob, loc_ptr(Ptot + 1, 0), loc_con;
     std::vector<double> loc_w;
+    auto is_loc = [&](int i) { return nent[i] == 1 && (hp.force_glob.empty() || !hp.force_glob[i]); };
     for (int i = 0; i < m; ++i) {
-        if (nent[i] == 1) loc_ptr[only_slot[i] + 1]++;
+        if (is_loc(i)) loc_ptr[only_slot[i] + 1]++;
         else glob.push_back(i);
     }
     for (int t = 0; t < Ptot; ++t) loc_ptr[t + 1] += loc_ptr[t];
@@ -495,7 +513,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
     {
         std::vector<int> fpl(loc_ptr.begin(), loc_ptr.end() - 1);
         for (int i = 0; i < m; ++i)
-            if (nent[i] == 1) {
+            if (is_loc(i)) {
                 const int t = fpl[only_slot[i]]++;
                 loc_con[t] = i;
                 loc_w[t] = only_w[i];
@@ -604,6 +622,7 @@ void free_problem(DevProblem &dp) {
     f(dp.b); f(dp.Cw); f(dp.Craw); f(dp.con_ptr); f(dp.con_slot); f(dp.con_w);
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
+    f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);

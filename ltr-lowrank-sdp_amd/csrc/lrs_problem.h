@@ -13,6 +13,7 @@ struct HostEntry {      // one merged coefficient entry of constraint `con` in a
     int slot;           // local slot in the cone pattern
     double a;           // raw value (lower triangle)
     bool diag;
+    bool owned = true;  // sharded solve: the slot's lower row is this shard's (the entry counts in A(.))
 };
 
 struct HostCone {
@@ -32,6 +33,7 @@ struct HostProblem {
     std::vector<double> b;
     std::vector<HostCone> cones;
     long nEntries = 0;
+    std::vector<char> force_glob;        // sharded solve: constraints kept on the multi-slot path
     double bNrm1 = 0, bNrm2 = 0, bNrmInf = 0;
     double cNrm1 = 0, cNrm2 = 0, cNrmInf = 0;
 };
@@ -47,10 +49,15 @@ bool build_problem_coo(int m, int nblk, const int *dims, const double *b, long n
 
 // Sharded solve: the rows of the (single) cone split into `world`
 // contiguous blocks balanced by adjacency entries.  Shard `rank` owns rows
-// [bounds[rank], bounds[rank+1]) and every constraint whose entries lie in its rows;
-// its local problem holds the owned rows plus the halo (the other shards' rows its
-// rows are adjacent to), numbered in global order, and the slots with at least one
-// owned endpoint.  Norms and rank statistics stay the global ones.
+// [bounds[rank], bounds[rank+1]); its local problem holds the owned rows plus the halo
+// (the other shards' rows its rows are adjacent to), numbered in global order, the slots
+// with at least one owned endpoint, and every constraint with an entry on such a slot.
+// A slot -- and each constraint entry on it -- belongs to the shard owning its lower row
+// (the row whose kernels evaluate it).  A constraint present on several shards is
+// "shared": every holder keeps it on the multi-slot path, sums its owned entries, and the
+// partial sums meet in an all-reduce of the shared constraints (primary holder: the
+// lowest rank, which alone counts it in sums over constraints).  Norms and rank
+// statistics stay the global ones.
 struct ShardPlan {
     int world = 1, rank = 0;
     int n_global = 0;
@@ -60,6 +67,9 @@ struct ShardPlan {
     std::vector<int> send_ptr, send_rows;    // rows sent to each peer: local ids, grouped by peer
     std::vector<int> recv_start, recv_cnt;   // halo rows from each peer: local first row, count
     std::vector<int> con_gid;                // local constraint -> global constraint
+    std::vector<int> shared_gid;             // shared constraints, ascending global id (same on every shard)
+    std::vector<int> shared_lid;             // per shared constraint: its local id here, or -1
+    std::vector<char> primary;               // per local constraint: this shard counts it in sums
 };
 bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, ShardPlan &plan, std::string &err);
 

@@ -33,7 +33,7 @@ namespace lrs {
 double *device_fin();
 double *device_tmpfin();
 int launch_gather_cone(const DevProblem &P, int cone, const double *uvt, double *out, hipStream_t st);
-int launch_resid(int m, const double *b, const double *x, hipStream_t st);
+int launch_resid(int m, const double *b, const double *x, hipStream_t st, const double *mask = nullptr);
 int launch_avg(long n, const double *U, const double *V, double *R, hipStream_t st);
 int launch_admm_m1(int m, double rho, const double *b, const double *cvs, const double *cv, const double *lam,
                    double *M1, hipStream_t st);
@@ -577,7 +577,15 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
     for (int k = 0; k < P.K; ++k)
         OPC(launch_sddmm(P, k, Y ? 0 : 1, X, Y, W.uvt2, nullptr, W.part, 0, nullptr, c->st));
     int fin;
-    if (P.K == 1) {
+    if (P.K == 1 && P.nsh > 0) {
+        // sharded, shared constraints: the holders' owned-entry sums summed over the shards,
+        // then the residual with each constraint counted once (its primary holder)
+        OPC(launch_gather(P, W.uvt2, 1.0, W.cvs, nullptr, nullptr, c->st, nullptr));
+        OPC(sync_shared(P, W.cvs, c->st));
+        HIPC(hipMemcpyAsync(W.cvc, W.cvs, sizeof(double) * P.m, hipMemcpyDeviceToDevice, c->st));
+        OPC(launch_resid(P.m, P.b, W.cvs, c->st, P.cmask));
+        fin = TF_RESID;
+    } else if (P.K == 1) {
         OPC(launch_gather(P, W.uvt2, 1.0, W.cvs, P.b, W.part, c->st, nullptr));
         HIPC(hipMemcpyAsync(W.cvc, W.cvs, sizeof(double) * P.m, hipMemcpyDeviceToDevice, c->st));
         fin = TF_GATHER;
@@ -590,7 +598,7 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
         OPC(launch_resid(P.m, P.b, W.cvs, c->st));
         fin = TF_RESID;
     }
-    if (blam) OPC(launch_dot(P.m, P.b, W.lam, W.part, c->st, nullptr));
+    if (blam) OPC(launch_dot(P.m, P.bprim ? P.bprim : P.b, W.lam, W.part, c->st, nullptr));
     double t[2 * 64 + 3];
     if (read_tmpfin2(c, TF_SD, 2 * P.K, TF_GATHER, 3, t)) return -1;   // GATHER, RESID, DOT
     double o = 0.0;
@@ -851,7 +859,7 @@ static int dual_infeasibility(lrs_ctx *c, double *l1, double *lmin, int *all_con
 
 static void cal_dual_obj(lrs_ctx *c) {   // LORADSCalDualObj lorads_alg_common.c:531
     double v = 0;
-    op_dot(c, c->dp.m, c->dp.b, c->W.lam, &v);
+    op_dot(c, c->dp.m, c->dp.bprim ? c->dp.bprim : c->dp.b, c->W.lam, &v);   // sharded: once per constraint
     c->dObjVal = v / c->scaleObjHis;
 }
 
@@ -1536,9 +1544,19 @@ static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double 
     };
     double *pA = sh ? tot : W.part, *pB = sh ? tot : W.partB, *pC = sh ? tot : W.partC;
     int nA = 0, nB = 0, nC = 0, nR = 0;
+    // shared constraints: entries on owned slots with a halo endpoint read the halo rows of
+    // the CG direction (exchanged before every matvec), and A(.)'s holders' partial sums meet
+    // in the shared all-reduce
+    const bool shx = sh && P.nsh > 0;
+    auto auv = [&](const double *x, const double *guard) -> int {
+        if (shx && c->comm->halo(c, const_cast<double *>(x), c->st)) return -1;
+        OPC(launch_auv_con(P, k, 0, x, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, guard));
+        OPC(sync_shared(P, W.wtmp, c->st));
+        return 0;
+    };
     OPC(launch_cg_nrm1(nr, bk, W.part, c->st, &nA));
     if (sum(W.part, nA)) return -1;
-    OPC(launch_auv_con(P, k, 0, X, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, nullptr));
+    if (auv(X, nullptr)) return -1;
     OPC(launch_cg_mv(P, k, W.wtmp, Y, X, W.cg_Q, nullptr, cgc, 0, c->st, &nB));
     OPC(launch_cg_resid(nr, bk, Q, r, p, W.partC, cgc, pA, nA, 1, c->st, &nC));
     if (sum(W.partC, nC)) return -1;
@@ -1551,7 +1569,7 @@ static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double 
     while (it < maxit) {
         for (int j = 0; j < B && it < maxit; ++j, ++it) {
             const int par = it & 1;
-            OPC(launch_auv_con(P, k, 0, W.cg_p, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, cgc));
+            if (auv(W.cg_p, cgc)) return -1;
             OPC(launch_cg_mv(P, k, W.wtmp, Y, W.cg_p, W.cg_Q, W.partB, cgc, 1, c->st, &nB));
             if (sum(W.partB, nB)) return -1;
             OPC(launch_cg_upd(nr, xk, r, p, Q, pB, nB, W.partC, cgc, par, it, c->st, &nC));
@@ -1559,7 +1577,7 @@ static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double 
             const int restart = (it % 20 == 0);
             OPC(launch_cg_conv(nr, r, p, pC, nC, cgc, tol, par, restart, c->st));
             if (restart) {
-                OPC(launch_auv_con(P, k, 0, X, Y, 1.0, 0, W.wtmp, nullptr, nullptr, c->st, cgc));
+                if (auv(X, cgc)) return -1;
                 OPC(launch_cg_mv(P, k, W.wtmp, Y, X, W.cg_Q, nullptr, cgc, 1, c->st, &nB));
                 OPC(launch_cg_resid(nr, bk, Q, r, p, W.partC, cgc, nullptr, 0, 0, c->st, &nR));
                 if (sum(W.partC, nR)) return -1;
@@ -1598,6 +1616,14 @@ static int refresh_cone(lrs_ctx *c, int k) {   // lorads_alg_common.c:310-314
     double *cv = W.cvc + (long)k * P.m;
     // cvs = (cvs - cvc[k]) + A_k(U V^T) in the pass that rewrites cvc[k] (the same two
     // roundings as the reference's two axpys)
+    if (P.nsh > 0) {
+        // sharded, shared constraints: the summed A_k(U V^T) first (one cone: cvs = cvc, as
+        // (cvs - cvc_old) + cvc_new is with cvs = cvc_old)
+        OPC(launch_auv_con(P, k, 0, W.U, W.V, 1.0, 0, cv, nullptr, nullptr, c->st, nullptr));
+        OPC(sync_shared(P, cv, c->st));
+        HIPC(hipMemcpyAsync(W.cvs, cv, sizeof(double) * P.m, hipMemcpyDeviceToDevice, c->st));
+        return 0;
+    }
     OPC(launch_auv_con(P, k, 0, W.U, W.V, 1.0, 0, cv, nullptr, nullptr, c->st, nullptr, W.cvs));
     return 0;
 }
@@ -1654,6 +1680,7 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
         OPC(launch_fill(P.m, 0.0, c->W.cvs, c->st));
         for (int k = 0; k < P.K; ++k) {
             OPC(launch_auv_con(P, k, 0, c->W.U, c->W.V, 1.0, 0, c->W.cvc + (long)k * P.m, nullptr, nullptr, c->st));
+            OPC(sync_shared(P, c->W.cvc + (long)k * P.m, c->st));
             OPC(launch_axpby(P.m, 1.0, c->W.cvc + (long)k * P.m, 1.0, c->W.cvs, c->st));
         }
     }
@@ -2673,7 +2700,27 @@ static int shard_setup(lrs_ctx *c, int world, int rank) {
     c->hp = std::move(sh);
     c->plan = std::move(pl);
     if (!upload_problem(c->hp, c->dp, err)) { set_err("shard upload: %s", err.c_str()); return -1; }
-    if (c->dp.mg > 0) { set_err("shard: constraints with several entries are not supported by the sharded solve"); return -1; }
+    {   // shared constraints (lrs_problem.h ShardPlan): index map, primary mask, b counted once
+        DevProblem &P = c->dp;
+        const int m = P.m;
+        std::vector<int> idx(std::max(1, m), -1);
+        for (size_t q = 0; q < c->plan.shared_lid.size(); ++q)
+            if (c->plan.shared_lid[q] >= 0) idx[c->plan.shared_lid[q]] = (int)q;
+        std::vector<double> mk(std::max(1, m), 0.0), bp(std::max(1, m), 0.0);
+        for (int i = 0; i < m; ++i) { mk[i] = c->plan.primary[i] ? 1.0 : 0.0; bp[i] = mk[i] * c->hp.b[i]; }
+        P.nsh = (int)c->plan.shared_gid.size();
+        const size_t ns = std::max<size_t>(1, P.nsh);
+        HIPC(hipMalloc((void **)&P.sh_idx, sizeof(int) * idx.size()));
+        HIPC(hipMalloc((void **)&P.cmask, sizeof(double) * mk.size()));
+        HIPC(hipMalloc((void **)&P.bprim, sizeof(double) * bp.size()));
+        HIPC(hipMalloc((void **)&P.g3, sizeof(double) * 3 * mk.size()));
+        HIPC(hipMalloc((void **)&P.gpack, sizeof(double) * 3 * ns));
+        HIPC(hipMalloc((void **)&P.spack, sizeof(double) * ns));
+        HIPC(hipMemcpy(P.sh_idx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(P.cmask, mk.data(), sizeof(double) * mk.size(), hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(P.bprim, bp.data(), sizeof(double) * bp.size(), hipMemcpyHostToDevice));
+        HIPC(hipMemset(P.g3, 0, sizeof(double) * 3 * mk.size()));
+    }
     DevCone &dc = c->dp.cones[0];
     dc.row0 = c->plan.row0;
     dc.nown = c->plan.nown;
@@ -2764,6 +2811,33 @@ int lrs_shard_info(lrs_ctx *c, int *world, int *rank, int *row0, int *nown, int 
     if (row0) *row0 = s ? c->plan.bounds[c->plan.rank] : 0;
     if (nown) *nown = s ? c->plan.nown : (c->loaded ? c->hp.cones[0].n : 0);
     if (nhalo) *nhalo = s ? c->dp.cones[0].n - c->plan.nown : 0;
+    return 0;
+}
+
+// Host-only view of shard_problem's partition (no device, no context): the row blocks, this
+// shard's local rows, its send lists per peer, the shared constraints and its local ones.
+// counts[8] = {n_global, first owned global row, owned rows, local rows, send rows, shared
+// constraints, local constraints, world}; any array may be null (counts first, then arrays).
+int lrs_shard_plan(const char *path, int world, int rank, long *counts, int *bounds, int *local_gid,
+                   int *send_ptr, int *send_gid, int *shared_gid, int *con_gid, int *primary) {
+    if (!path || !counts) { set_err("null argument"); return -1; }
+    HostProblem g, out;
+    ShardPlan pl;
+    std::string err;
+    if (!read_sdpa(path, g, err)) { set_err("read_sdpa: %s", err.c_str()); return -1; }
+    if (!shard_problem(g, world, rank, out, pl, err)) { set_err("shard: %s", err.c_str()); return -1; }
+    counts[0] = pl.n_global; counts[1] = pl.bounds[rank]; counts[2] = pl.nown; counts[3] = (long)pl.gid.size();
+    counts[4] = (long)pl.send_rows.size(); counts[5] = (long)pl.shared_gid.size(); counts[6] = (long)pl.con_gid.size();
+    counts[7] = world;
+    if (bounds) std::copy(pl.bounds.begin(), pl.bounds.end(), bounds);
+    if (local_gid) std::copy(pl.gid.begin(), pl.gid.end(), local_gid);
+    if (send_ptr) std::copy(pl.send_ptr.begin(), pl.send_ptr.end(), send_ptr);
+    if (send_gid)
+        for (size_t q = 0; q < pl.send_rows.size(); ++q) send_gid[q] = pl.gid[pl.send_rows[q]];
+    if (shared_gid) std::copy(pl.shared_gid.begin(), pl.shared_gid.end(), shared_gid);
+    if (con_gid) std::copy(pl.con_gid.begin(), pl.con_gid.end(), con_gid);
+    if (primary)
+        for (size_t q = 0; q < pl.primary.size(); ++q) primary[q] = pl.primary[q];
     return 0;
 }
 

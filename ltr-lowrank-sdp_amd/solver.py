@@ -125,6 +125,7 @@ def load_library(path=None):
         "lrs_loopback_destroy": (None, [vp]),
         "lrs_shard_loopback": (C.c_int, [vp, vp, C.c_int]),
         "lrs_shard_info": (C.c_int, [vp, ip, ip, ip, ip, ip]),
+        "lrs_shard_plan": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_long), ip, ip, ip, ip, ip, ip, ip]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -479,6 +480,29 @@ class Solver:
         ms = C.c_double()
         self._check(self.lib.lrs_time_auut(self.ctx, reps, C.byref(ms)), "time_auut")
         return ms.value
+
+
+def shard_plan(path, world, rank):
+    """Host-only row partition of a sharded solve (lrs_shard_plan; no device needed)."""
+    lib = load_library()
+    cnt = (C.c_long * 8)()
+    nul = C.POINTER(C.c_int)()
+    rc = lib.lrs_shard_plan(str(path).encode(), world, rank, cnt, nul, nul, nul, nul, nul, nul, nul)
+    if rc != 0:
+        raise RuntimeError(lib.lrs_last_error().decode())
+    n, r0, nown, nl, ns, nsh, ml, w = list(cnt)
+    arr = {k: np.zeros(max(1, v), dtype=np.int32) for k, v in
+           (("bounds", world + 1), ("local_gid", nl), ("send_ptr", world + 1), ("send_gid", ns),
+            ("shared_gid", nsh), ("con_gid", ml), ("primary", ml))}
+    ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+    rc = lib.lrs_shard_plan(str(path).encode(), world, rank, cnt, ip(arr["bounds"]), ip(arr["local_gid"]),
+                            ip(arr["send_ptr"]), ip(arr["send_gid"]), ip(arr["shared_gid"]), ip(arr["con_gid"]),
+                            ip(arr["primary"]))
+    if rc != 0:
+        raise RuntimeError(lib.lrs_last_error().decode())
+    out = {k: v[:n_] for (k, v), n_ in zip(arr.items(), (world + 1, nl, world + 1, ns, nsh, ml, ml))}
+    out.update(n=n, row0=r0, nown=nown)
+    return out
 
 
 def run_lorads(instance_path, json_output_path, params, fixed_rank=None, rank_schedule_path=None,
