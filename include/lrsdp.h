@@ -116,7 +116,8 @@ int lrs_op_gram(lrs_ctx *ctx, int cone, int which, double *gram);
 int lrs_op_dual_infeasibility(lrs_ctx *ctx, double *l1, double *lam_min);
 
 /* ---- whole solves ---- */
-/* main.c:380-610 flow: ALM phase, ADMM phase, reoptLevel 1/2 rounds, dual infeasibility. */
+/* main.c:380-610 flow: ALM phase, ADMM phase, reoptLevel 1/2 rounds (all on the device), dual
+ * infeasibility (skipped after a time-limit exit, as main.c:505-510 jumps to END_SOLVING). */
 int lrs_solve(lrs_ctx *ctx, const lrs_params *p, lrs_result *res);
 /* trajectory (phase 1 then phase 2) after lrs_solve: curr and oracle ranks */
 int lrs_trajectory(lrs_ctx *ctx, int phase, int *curr_rank, int *oracle_rank, int cap);

@@ -60,3 +60,38 @@ def test_params_default_matches_reference_defaults(built, pkg):
 def test_cli_binary_built_for_benchmark_py(built):
     # benchmark.py:25 resolves this executable name
     assert os.path.exists(BIN) and os.access(BIN, os.X_OK)
+
+
+def build_c_caller(tmpdir):
+    """gcc (plain C11) against include/lrsdp.h, linked to liblrsdp.so."""
+    exe = os.path.join(str(tmpdir), "capi_solve")
+    src = os.path.join(ROOT, "tests", "c", "capi_solve.c")
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), src, "-o", exe,
+                        "-L", os.path.dirname(LIB), "-llrsdp", "-Wl,-rpath," + os.path.dirname(LIB)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_c_caller_compiles_and_links(built, tmp_path):
+    exe = build_c_caller(tmp_path)
+    assert os.access(exe, os.X_OK)
+
+
+@pytest.mark.gpu
+def test_c_caller_solves_like_reference(built, tmp_path):
+    """The C caller solves the golden MaxCut instance through the C-ABI: objective against the
+    reference's solve (tests/golden/solves.json) within 1e-6, and the JSON it writes has the
+    reference's key set."""
+    import json
+    exe = build_c_caller(tmp_path)
+    inst = os.path.join(ROOT, "tests", "golden", "instances", "mc_rand200.dat-s")
+    js = tmp_path / "o.json"
+    r = subprocess.run([exe, inst, str(js), "0"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    m = re.search(r"pobj=(\S+)", r.stdout)
+    ref = [s for s in json.load(open(os.path.join(ROOT, "tests", "golden", "solves.json")))
+           if s["instance"] == "mc_rand200" and s["flags"] == ["--reoptLevel", "0"]][0]
+    assert abs(float(m.group(1)) - ref["result"]["admm_pobj"]) <= 1e-6 * abs(ref["result"]["admm_pobj"])
+    out = json.load(open(js))
+    assert set(out["metrics"]) == set(ref["json"]["metrics"])
