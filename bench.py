@@ -76,11 +76,30 @@ def instance_for(rank_id, rows, cols, cache, seed0=67):
     return path
 
 
-def cpu_reference_rate(path, rank, seconds):
+def host_cpu():
+    """(threads this process may use, CPU model) of the host running the bench."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return n, model
+
+
+def cpu_reference_rate(path, rank, seconds, threads=1):
     """Reference LoRADS (oracle/_ref, built from /root/reference sources) phase-1
-    rate on the host; falls back to the CPU restatement if the reference build is absent."""
+    rate on the host (its BLAS on `threads` threads); falls back to the CPU restatement if
+    the reference build is absent."""
     harness = os.path.join(ROOT, "oracle", "_ref", "lorads_ref_harness")
-    env = dict(os.environ, OPENBLAS_NUM_THREADS="1")
+    env = dict(os.environ, OPENBLAS_NUM_THREADS=str(threads), OMP_NUM_THREADS=str(threads))
     if os.path.exists(harness):
         r = subprocess.run([harness, "alm_rate", path, str(rank), "0", str(seconds)], capture_output=True,
                            text=True, env=env, timeout=seconds * 6 + 120)
@@ -142,8 +161,9 @@ def stage_roofline(sv, reps, with_traffic=False):
     return res
 
 
-def config_c5(solver, local, iters=20):
-    """BASELINE config C5 in memory: ALM it/s at r = 128, stage roofline, MFMA Gram."""
+def config_c5(solver, local, iters=20, cpu_seconds=0.0, cache=None):
+    """BASELINE config C5 in memory: ALM it/s at r = 128, stage roofline, MFMA Gram; with
+    cpu_seconds > 0 also the reference CPU rate on a C5-structured sample (m = 1e5)."""
     inst = importlib.import_module(PKG + ".instances")
     t0 = time.perf_counter()
     sv = solver.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(10000, 1000000, 6, 5)), device=local)
@@ -162,7 +182,32 @@ def config_c5(solver, local, iters=20):
                           "avg_launch_us": kms * 1e3, "with_reduction_us": ms * 1e3, "flop_per_launch": fl,
                           "achieved": fl / (kms * 1e-3) / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                           "frac": fl / (kms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS},
-            "cpu_baseline": "not run: the reference's presolve alone takes ~1600 s on C5 (SURVEY.md §8(d))"}
+            "cpu_baseline": c5_cpu_sample(solver, local, cpu_seconds, cache) if cpu_seconds > 0 else
+            "not run (--no-cpu)"}
+
+
+def c5_cpu_sample(solver, local, seconds, cache):
+    """The reference's rate on the C5 structure with m = 1e5 (a bounded sample: at m = 1e6 its
+    hash-chain presolve alone takes ~1600 s; its iteration cost is the dense
+    n^2 path it takes at > 10 % pattern fill, independent of m), the device's rate on the same
+    file beside it."""
+    inst = importlib.import_module(PKG + ".instances")
+    path = os.path.join(cache, "c5_m1e5.dat-s")
+    if not os.path.exists(path):
+        tmp = path + f".tmp{os.getpid()}"
+        inst.random_sparse(tmp, 10000, 100000, 6, 5)
+        os.replace(tmp, path)
+    it, sec, kind = cpu_reference_rate(path, 128, seconds)
+    sv = solver.Solver(path, device=local)
+    kw = dict(fixedRank=128, reoptLevel=0)
+    sv.alm_throughput(0, 4, **kw)
+    o = sv.alm_throughput(0, 20, **kw)
+    sv.close()
+    gpu = o["done"] / o["seconds"]
+    return {"value": it / sec, "unit": "ALM inner iterations/s", "cores": 1, "kind": kind,
+            "sample": f"C5 structure with m = 1e5 (n = 1e4, 6 entries/constraint, --fixedRank 128): {it} inner "
+                      f"iterations in {sec:.1f} s wall, presolve excluded (OPENBLAS_NUM_THREADS=1)",
+            "gpu_it_s_same_file": gpu, "speedup_same_file": gpu / (it / sec) if it else None}
 
 
 def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=500):
@@ -284,9 +329,18 @@ def main():
     sv.close()
     if rank_id == 0 and world == 1 and not args.no_cpu:
         it, sec, kind = cpu_reference_rate(path, r, args.cpu_seconds)
+        nthr, model = host_cpu()
         line["cpu_baseline"] = {"value": it / sec, "unit": "ALM inner iterations/s", "cores": 1, "kind": kind,
                                 "sample": f"phase-1 ALM on the same instance at rank {r}, {it} inner iterations "
-                                          f"in {sec:.1f} s wall (OPENBLAS_NUM_THREADS=1)"}
+                                          f"in {sec:.1f} s wall (OPENBLAS_NUM_THREADS=1)",
+                                "host": {"cpu_model": model, "threads_available": nthr}}
+        # the reference's BLAS on every thread this process may use (its loop is single-threaded C;
+        # only BLAS calls can spread)
+        ta = min(nthr, 16)
+        it2, sec2, _ = cpu_reference_rate(path, r, min(args.cpu_seconds, 10.0), threads=ta)
+        line["cpu_baseline"]["all_cores"] = {"value": it2 / sec2, "threads": ta,
+                                             "sample": f"{it2} inner iterations in {sec2:.1f} s wall "
+                                                       f"(OPENBLAS_NUM_THREADS={ta})"}
         if not args.no_eps:
             ref = cpu_reference_solve(path, ["--reoptLevel", "0", "--heuristicFactor", "10", "--phase1Tol", "1e-2"],
                                       timeout=600)
@@ -347,7 +401,7 @@ def main():
         big.close()
         line["roofline_at_scale"] = rl
     if rank_id == 0 and world == 1 and not args.no_c5:
-        line["config_c5"] = config_c5(solver, local)
+        line["config_c5"] = config_c5(solver, local, cpu_seconds=0.0 if args.no_cpu else 20.0, cache=cache)
     if not args.no_sharded:
         # a watchdog keeps a stuck collective from swallowing the result line
         import threading

@@ -1179,6 +1179,26 @@ struct DirRow {
 
 constexpr int kRowBlock = 512;   // threads per block of the row kernels S1 / S4
 
+// Row order of the row kernels' team loops.  Large grids (the bandwidth regime): blocks b and
+// b + 8 share an XCD under the round-robin dispatch (MI355X_MICROARCH.md, for speed only), so
+// the blocks of XCD group x = b % 8 take the contiguous rows [x n / 8, (x + 1) n / 8) and
+// stride over them together: a row's neighbours (i +- 1, and i +- w on a w-wide grid) are then
+// read by the same XCD and re-read from its L2 instead of fetched again from HBM through
+// another XCD's misses.  Small grids: every team strides over all rows.  Either way each row
+// is visited exactly once; only the rows' grouping into blocks (their partial sums) changes.
+struct RowRange { int first, end, stride; };
+__device__ __forceinline__ RowRange row_range(int n, int tpb, int team_local) {
+#ifndef LRS_NO_XCD_ROWS
+    if (gridDim.x >= 64) {
+        const int x = blockIdx.x & 7, q = blockIdx.x >> 3;
+        const int nbx = ((int)gridDim.x - x + 7) >> 3;
+        const int r0 = (int)((long)n * x / 8), r1 = (int)((long)n * (x + 1) / 8);
+        return {r0 + q * tpb + team_local, r1, nbx * tpb};
+    }
+#endif
+    return {(int)blockIdx.x * tpb + team_local, n, (int)gridDim.x * tpb};
+}
+
 // Rows of the lower pattern carry the single-slot ("local") constraints: whoever
 // computes a slot value also evaluates the local constraints on that slot.
 //
@@ -1288,10 +1308,11 @@ __global__ void __launch_bounds__(kRowBlock) k_it_a(
         // lane groups of G lanes; a team of T groups shares one row (dense rows)
         const int lane = threadIdx.x & (G - 1);
         const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
-        const int ngrp = gridDim.x * kRowBlock / G;
-        const int team = grp / T, mem = grp % T, nteams = ngrp / T;
+        const int team = grp / T, mem = grp % T;
+        const int tpb = (kRowBlock / G) / T;
+        const RowRange rr = row_range(n, tpb, team - blockIdx.x * tpb);
         // rows [row0, row0 + n): the whole cone, or this process's shard of it
-        for (int i = row0 + team; i < row0 + n; i += nteams) {
+        for (int i = row0 + rr.first; i < row0 + rr.end; i += rr.stride) {
             const long oi = (long)i * ld + lane * E;
             const int kb = adj_ptr[i], ke = adj_low[i];
             double xi[E], yi[E];
@@ -1650,14 +1671,16 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_
     const int lane = threadIdx.x & (G - 1);
     const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
     const int ngrp = gridDim.x * kRowBlock / G;
-    const int team = grp / T, mem = grp % T, nteams = ngrp / T;
+    const int team = grp / T, mem = grp % T;
     const int tpb = (kRowBlock / G) / T;                 // teams per block
     const int team_local = team - blockIdx.x * tpb;
+    // block-uniform trip count (the team reduction has barriers inside the loop)
+    const RowRange rr = row_range(n, tpb, 0);
     // acc: GG, ys, yy, sG, yG, soG, yoG, soy, yoy, residual
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int ib = blockIdx.x * tpb; ib < n; ib += nteams) {
+    for (int ib = rr.first; ib < rr.end; ib += rr.stride) {
     const int i = row0 + ib + team_local;   // rows [row0, row0 + n) (a shard: n = owned rows)
-    const bool valid = ib + team_local < n;
+    const bool valid = ib + team_local < rr.end;
     double ri[E], di[E], g[E];
     const long oi = (long)(valid ? i : 0) * ld + lane * E;
 #pragma unroll

@@ -15,6 +15,8 @@ side = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
 rank = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 iters = int(sys.argv[3]) if len(sys.argv) > 3 else 40
 sv = solver.Solver(coo=inst.coo_arrays(inst.maxcut_torus_problem(side, side, 2000)))
+if os.environ.get("LRS_PATH"):
+    sv.set_kernel_path(int(os.environ["LRS_PATH"]))
 out = sv.alm_throughput(0, iters, fixedRank=rank, reoptLevel=0)
 ms = sv.time_stages(5)
 by = sv.stage_bytes()
