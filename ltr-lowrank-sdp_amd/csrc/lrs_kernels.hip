@@ -1184,12 +1184,13 @@ constexpr int kRowBlock = 512;   // threads per block of the row kernels S1 / S4
 // the blocks of XCD group x = b % 8 take the contiguous rows [x n / 8, (x + 1) n / 8) and
 // stride over them together: a row's neighbours (i +- 1, and i +- w on a w-wide grid) are then
 // read by the same XCD and re-read from its L2 instead of fetched again from HBM through
-// another XCD's misses.  Small grids: every team strides over all rows.  Either way each row
-// is visited exactly once; only the rows' grouping into blocks (their partial sums) changes.
+// another XCD's misses.  Small problems (n < 16384; the dense small cones run their teams on a
+// few dozen rows) and small grids: every team strides over all rows.  Either way each row is
+// visited exactly once; only the rows' grouping into blocks (their partial sums) changes.
 struct RowRange { int first, end, stride; };
 __device__ __forceinline__ RowRange row_range(int n, int tpb, int team_local) {
 #ifndef LRS_NO_XCD_ROWS
-    if (gridDim.x >= 64) {
+    if (gridDim.x >= 64 && n >= 16384) {
         const int x = blockIdx.x & 7, q = blockIdx.x >> 3;
         const int nbx = ((int)gridDim.x - x + 7) >> 3;
         const int r0 = (int)((long)n * x / 8), r1 = (int)((long)n * (x + 1) / 8);
