@@ -1482,7 +1482,7 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
 // others carry weight 0) of RR (the last stage B's slots), RD and DD (this stage A's) ->
 // g3[3][m], or for a shared constraint its row of gpack[nsh][3] (zero-filled before; the
 // holders' rows meet in an all-reduce).
-__global__ void __launch_bounds__(kBlock) k_g_part(int mg, const int *__restrict__ glob, int m,
+__global__ void __launch_bounds__(kBlock) k_g_part(int mg, const int *__restrict__ glob, int m, int K,
                                                    const int *__restrict__ con_ptr, const int *__restrict__ con_slot,
                                                    const double *__restrict__ con_w, const double *__restrict__ uRR,
                                                    const double *__restrict__ uRD, const double *__restrict__ uDD,
@@ -1495,12 +1495,15 @@ __global__ void __launch_bounds__(kBlock) k_g_part(int mg, const int *__restrict
     for (int g = gid; g < mg; g += gstride) {
         const int i = glob[g];
         double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-        for (int e = con_ptr[i] + sub; e < con_ptr[i + 1]; e += lanes) {
-            const double w = con_w[e];
-            const int s = con_slot[e];
-            a0 += w * uRR[s];
-            a1 += w * uRD[s];
-            a2 += w * uDD[s];
+        for (int k = 0; k < K; ++k) {   // cone-major constraint rows k m + i
+            const long row = (long)k * m + i;
+            for (int e = con_ptr[row] + sub; e < con_ptr[row + 1]; e += lanes) {
+                const double w = con_w[e];
+                const int s = con_slot[e];
+                a0 += w * uRR[s];
+                a1 += w * uRD[s];
+                a2 += w * uDD[s];
+            }
         }
         if (gwide) { a0 = wave_sum(a0); a1 = wave_sum(a1); a2 = wave_sum(a2); }
         if (sub != 0) continue;
@@ -3685,12 +3688,13 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     double *ls_cur = W.lsres + parity * LS_N;
     const int L = 2;
     const ShardHooks *sh = P.shard;
-    if (sh && (P.K != 1 || !W.tot)) {
-        snprintf(g_err, sizeof(g_err), "sharded iteration: one cone only");
+    if (sh && !W.tot) {
+        snprintf(g_err, sizeof(g_err), "sharded iteration: no totals buffer");
         return -1;
     }
-    // one launch over the merged row space when every cone has the same row layout
-    bool merge = P.K > 1 && P.has_merged;
+    // one launch over the merged row space when every cone has the same row layout (not in a
+    // sharded solve: a shard's owned rows are a range per cone)
+    bool merge = P.K > 1 && P.has_merged && !sh;
     for (int k = 1; k < P.K && merge; ++k)
         merge = P.cones[k].G == P.cones[0].G && P.cones[k].E == P.cones[0].E && P.cones[k].ld == P.cones[0].ld;
     DevCone mc;
@@ -3819,7 +3823,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
             hipLaunchKernelGGL(k_fill, dim3(grid_elems(3L * P.nsh, 4)), dim3(kBlock), 0, st, 3L * P.nsh, 0.0, P.gpack);
             LRS_CHECK_LAUNCH();
         }
-        hipLaunchKernelGGL(k_g_part, dim3(g1), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.con_ptr, P.con_slot, P.con_w,
+        hipLaunchKernelGGL(k_g_part, dim3(g1), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,
                            W.uvt2, W.uvt0, W.uvt1, P.sh_idx, P.g3, P.gpack, gwide);
         LRS_CHECK_LAUNCH();
         if (P.nsh > 0 && sh->allreduce(sh->self, P.gpack, 3 * P.nsh, st)) return -1;

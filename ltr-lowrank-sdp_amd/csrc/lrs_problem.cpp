@@ -273,51 +273,70 @@ bool build_problem_coo(int m, int nblk, const int *dims_in, const double *b, lon
 }
 
 bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, ShardPlan &plan, std::string &err) {
-    if (g.K != 1) { err = "sharded solve: one SDP cone only"; return false; }
-    const HostCone &gc = g.cones[0];
-    const int n = gc.n;
-    if (world < 1 || world > kMaxShards || rank < 0 || rank >= world || n < world) {
-        err = "sharded solve: bad world/rank for n";
+    const int K = g.K;
+    if (world < 1 || world > kMaxShards || rank < 0 || rank >= world) {
+        err = "sharded solve: bad world/rank";
         return false;
     }
+    for (int k = 0; k < K; ++k)
+        if (g.cones[k].n < world) { err = "sharded solve: a cone has fewer rows than shards"; return false; }
     plan = ShardPlan();
-    plan.world = world; plan.rank = rank; plan.n_global = n;
-    // contiguous blocks balanced by (adjacency entries + 1) per row
-    std::vector<long> cum(n + 1, 0);
-    for (int i = 0; i < n; ++i) cum[i + 1] = cum[i] + (gc.adj_ptr[i + 1] - gc.adj_ptr[i]) + 1;
-    plan.bounds.assign(world + 1, 0);
-    for (int q = 1; q < world; ++q) {
-        const long target = cum[n] * q / world;
-        int b = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
-        b = std::max(b, plan.bounds[q - 1] + 1);
-        b = std::min(b, n - (world - q));
-        plan.bounds[q] = b;
+    plan.world = world; plan.rank = rank;
+    plan.cones.assign(K, ShardConePlan());
+    // per cone: contiguous blocks balanced by (adjacency entries + 1) per row
+    std::vector<std::vector<int>> lid(K);
+    for (int k = 0; k < K; ++k) {
+        const HostCone &gc = g.cones[k];
+        ShardConePlan &cp = plan.cones[k];
+        const int n = gc.n;
+        cp.n_global = n;
+        std::vector<long> cum(n + 1, 0);
+        for (int i = 0; i < n; ++i) cum[i + 1] = cum[i] + (gc.adj_ptr[i + 1] - gc.adj_ptr[i]) + 1;
+        cp.bounds.assign(world + 1, 0);
+        for (int q = 1; q < world; ++q) {
+            const long target = cum[n] * q / world;
+            int b = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+            b = std::max(b, cp.bounds[q - 1] + 1);
+            b = std::min(b, n - (world - q));
+            cp.bounds[q] = b;
+        }
+        cp.bounds[world] = n;
     }
-    plan.bounds[world] = n;
-    auto owner = [&](int i) { return (int)(std::upper_bound(plan.bounds.begin(), plan.bounds.end(), i) - plan.bounds.begin()) - 1; };
-    const int r0 = plan.bounds[rank], r1 = plan.bounds[rank + 1];
+    auto owner = [&](int k, int i) {
+        const std::vector<int> &b = plan.cones[k].bounds;
+        return (int)(std::upper_bound(b.begin(), b.end(), i) - b.begin()) - 1;
+    };
     // the shards holding each constraint: those owning an endpoint of one of its entries' slots
     // (constraints without entries: shard 0, for the residual b_i)
     std::vector<unsigned long long> holders(g.m, 0ull);
-    for (const HostEntry &e : gc.ent)
-        holders[e.con] |= (1ull << owner(gc.prow[e.slot])) | (1ull << owner(gc.pcol[e.slot]));
+    for (int k = 0; k < K; ++k) {
+        const HostCone &gc = g.cones[k];
+        for (const HostEntry &e : gc.ent)
+            holders[e.con] |= (1ull << owner(k, gc.prow[e.slot])) | (1ull << owner(k, gc.pcol[e.slot]));
+    }
     for (int i = 0; i < g.m; ++i)
         if (holders[i] == 0) holders[i] = 1ull;
     auto holds = [&](int i) { return ((holders[i] >> rank) & 1ull) != 0; };
     for (int i = 0; i < g.m; ++i)
         if (__builtin_popcountll(holders[i]) > 1) plan.shared_gid.push_back(i);
-    // local rows: owned + halo, in global order
-    std::vector<char> need(n, 0);
-    for (int i = r0; i < r1; ++i) {
-        need[i] = 1;
-        for (int k = gc.adj_ptr[i]; k < gc.adj_ptr[i + 1]; ++k) need[gc.adj_col[k]] = 1;
+    // local rows per cone: owned + halo, in global order
+    std::vector<int> dims(K);
+    for (int k = 0; k < K; ++k) {
+        const HostCone &gc = g.cones[k];
+        ShardConePlan &cp = plan.cones[k];
+        const int n = gc.n, r0 = cp.bounds[rank], r1 = cp.bounds[rank + 1];
+        std::vector<char> need(n, 0);
+        for (int i = r0; i < r1; ++i) {
+            need[i] = 1;
+            for (int q = gc.adj_ptr[i]; q < gc.adj_ptr[i + 1]; ++q) need[gc.adj_col[q]] = 1;
+        }
+        lid[k].assign(n, -1);
+        for (int i = 0; i < n; ++i)
+            if (need[i]) { lid[k][i] = (int)cp.gid.size(); cp.gid.push_back(i); }
+        cp.row0 = lid[k][r0];
+        cp.nown = r1 - r0;
+        dims[k] = (int)cp.gid.size();
     }
-    std::vector<int> lid(n, -1);
-    for (int i = 0; i < n; ++i)
-        if (need[i]) { lid[i] = (int)plan.gid.size(); plan.gid.push_back(i); }
-    const int nl = (int)plan.gid.size();
-    plan.row0 = lid[r0];
-    plan.nown = r1 - r0;
     // local constraints in global order
     std::vector<int> clid(g.m, -1);
     for (int i = 0; i < g.m; ++i)
@@ -328,59 +347,70 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
         }
     for (int gi : plan.shared_gid) plan.shared_lid.push_back(clid[gi]);
     const int ml = (int)plan.con_gid.size();
-    // entries of the local problem (already merged and sign-converted: build_problem input)
+    // entries of the local problem (already merged and sign-converted: build_problem input):
+    // the slots with an owned endpoint
     std::vector<RawEntry> raw;
-    for (size_t t = 0; t < gc.prow.size(); ++t) {
-        const int i = gc.prow[t], j = gc.pcol[t];
-        if (!gc.Chas[t] || (owner(i) != rank && owner(j) != rank)) continue;
-        raw.push_back({0, 0, lid[i], lid[j], gc.Craw[t]});
-    }
-    for (const HostEntry &e : gc.ent) {
-        const int i = gc.prow[e.slot], j = gc.pcol[e.slot];
-        if (owner(i) != rank && owner(j) != rank) continue;   // slot not present here
-        raw.push_back({0, clid[e.con] + 1, lid[i], lid[j], e.a});
+    for (int k = 0; k < K; ++k) {
+        const HostCone &gc = g.cones[k];
+        for (size_t t = 0; t < gc.prow.size(); ++t) {
+            const int i = gc.prow[t], j = gc.pcol[t];
+            if (!gc.Chas[t] || (owner(k, i) != rank && owner(k, j) != rank)) continue;
+            raw.push_back({k, 0, lid[k][i], lid[k][j], gc.Craw[t]});
+        }
+        for (const HostEntry &e : gc.ent) {
+            const int i = gc.prow[e.slot], j = gc.pcol[e.slot];
+            if (owner(k, i) != rank && owner(k, j) != rank) continue;   // slot not present here
+            raw.push_back({k, clid[e.con] + 1, lid[k][i], lid[k][j], e.a});
+        }
     }
     out = HostProblem();
     out.b.resize(ml);
     for (int q = 0; q < ml; ++q) out.b[q] = g.b[plan.con_gid[q]];
-    if (!build_problem(ml, 1, std::vector<int>{nl}, 0, false, raw, out, err)) return false;
-    // entries count in A(.) on the shard owning their slot's lower row; shared constraints stay
-    // on the multi-slot path on every holder
-    {
-        HostCone &lc = out.cones[0];
-        const int o0 = lid[r0], o1 = o0 + (r1 - r0);
-        for (HostEntry &e : lc.ent) e.owned = lc.prow[e.slot] >= o0 && lc.prow[e.slot] < o1;
-        out.force_glob.assign(ml, 0);
-        for (int l : plan.shared_lid)
-            if (l >= 0) out.force_glob[l] = 1;
-    }
+    if (!build_problem(ml, K, dims, 0, false, raw, out, err)) return false;
     // the solve's norms and rank statistics are the whole problem's
     out.bNrm1 = g.bNrm1; out.bNrm2 = g.bNrm2; out.bNrmInf = g.bNrmInf;
     out.cNrm1 = g.cNrm1; out.cNrm2 = g.cNrm2; out.cNrmInf = g.cNrmInf;
-    HostCone &oc = out.cones[0];
-    oc.nnzRows = gc.nnzRows; oc.denseCoeff = gc.denseCoeff;
-    oc.cNrm1 = gc.cNrm1; oc.cNrm2sq = gc.cNrm2sq; oc.cNrmInf = gc.cNrmInf;
-    // halo exchange plan: rows of ours adjacent to each peer's rows (both sides derive the
-    // same global-order lists), and the peers' rows in our halo (contiguous locally)
-    plan.send_ptr.assign(world + 1, 0);
-    plan.recv_start.assign(world, 0);
-    plan.recv_cnt.assign(world, 0);
-    for (int q = 0; q < world; ++q) {
-        plan.send_ptr[q] = (int)plan.send_rows.size();
-        if (q == rank) continue;
-        const int q0 = plan.bounds[q], q1 = plan.bounds[q + 1];
-        for (int i = r0; i < r1; ++i) {
-            bool adj = false;
-            for (int k = gc.adj_ptr[i]; k < gc.adj_ptr[i + 1] && !adj; ++k) adj = gc.adj_col[k] >= q0 && gc.adj_col[k] < q1;
-            if (adj) plan.send_rows.push_back(lid[i]);
-        }
-        int first = -1, cnt = 0;
-        for (int l = 0; l < nl; ++l)
-            if (plan.gid[l] >= q0 && plan.gid[l] < q1) { if (first < 0) first = l; cnt++; }
-        plan.recv_start[q] = first < 0 ? 0 : first;
-        plan.recv_cnt[q] = cnt;
+    for (int k = 0; k < K; ++k) {
+        const HostCone &gc = g.cones[k];
+        HostCone &oc = out.cones[k];
+        const ShardConePlan &cp = plan.cones[k];
+        oc.nnzRows = gc.nnzRows; oc.denseCoeff = gc.denseCoeff;
+        oc.cNrm1 = gc.cNrm1; oc.cNrm2sq = gc.cNrm2sq; oc.cNrmInf = gc.cNrmInf;
+        // entries count in A(.) on the shard owning their slot's lower row
+        const int o0 = cp.row0, o1 = cp.row0 + cp.nown;
+        for (HostEntry &e : oc.ent) e.owned = oc.prow[e.slot] >= o0 && oc.prow[e.slot] < o1;
     }
-    plan.send_ptr[world] = (int)plan.send_rows.size();
+    // shared constraints stay on the multi-slot path on every holder
+    out.force_glob.assign(ml, 0);
+    for (int l : plan.shared_lid)
+        if (l >= 0) out.force_glob[l] = 1;
+    // halo exchange plan per cone: rows of ours adjacent to each peer's rows (both sides derive
+    // the same global-order lists), and the peers' rows in our halo (contiguous locally)
+    for (int k = 0; k < K; ++k) {
+        const HostCone &gc = g.cones[k];
+        ShardConePlan &cp = plan.cones[k];
+        const int r0 = cp.bounds[rank], r1 = cp.bounds[rank + 1], nl = (int)cp.gid.size();
+        cp.send_ptr.assign(world + 1, 0);
+        cp.recv_start.assign(world, 0);
+        cp.recv_cnt.assign(world, 0);
+        for (int q = 0; q < world; ++q) {
+            cp.send_ptr[q] = (int)cp.send_rows.size();
+            if (q == rank) continue;
+            const int q0 = cp.bounds[q], q1 = cp.bounds[q + 1];
+            for (int i = r0; i < r1; ++i) {
+                bool adj = false;
+                for (int t = gc.adj_ptr[i]; t < gc.adj_ptr[i + 1] && !adj; ++t)
+                    adj = gc.adj_col[t] >= q0 && gc.adj_col[t] < q1;
+                if (adj) cp.send_rows.push_back(lid[k][i]);
+            }
+            int first = -1, cnt = 0;
+            for (int l = 0; l < nl; ++l)
+                if (cp.gid[l] >= q0 && cp.gid[l] < q1) { if (first < 0) first = l; cnt++; }
+            cp.recv_start[q] = first < 0 ? 0 : first;
+            cp.recv_cnt[q] = cnt;
+        }
+        cp.send_ptr[world] = (int)cp.send_rows.size();
+    }
     return true;
 }
 

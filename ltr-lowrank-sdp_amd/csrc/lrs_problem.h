@@ -47,8 +47,8 @@ bool build_problem_coo(int m, int nblk, const int *dims, const double *b, long n
                        const int *blk, const int *row, const int *col, const double *val, HostProblem &hp,
                        std::string &err);
 
-// Sharded solve: the rows of the (single) cone split into `world`
-// contiguous blocks balanced by adjacency entries.  Shard `rank` owns rows
+// Sharded solve: the rows of every cone split into `world` contiguous
+// blocks balanced by adjacency entries (a multi-block problem: each block split alike).  Shard `rank` owns rows
 // [bounds[rank], bounds[rank+1]); its local problem holds the owned rows plus the halo
 // (the other shards' rows its rows are adjacent to), numbered in global order, the slots
 // with at least one owned endpoint, and every constraint with an entry on such a slot.
@@ -58,14 +58,17 @@ bool build_problem_coo(int m, int nblk, const int *dims, const double *b, long n
 // partial sums meet in an all-reduce of the shared constraints (primary holder: the
 // lowest rank, which alone counts it in sums over constraints).  Norms and rank
 // statistics stay the global ones.
-struct ShardPlan {
-    int world = 1, rank = 0;
+struct ShardConePlan {
     int n_global = 0;
-    std::vector<int> bounds;                 // [world + 1] global row partition
+    std::vector<int> bounds;                 // [world + 1] global row partition of this cone
     std::vector<int> gid;                    // local row -> global row
     int row0 = 0, nown = 0;                  // owned rows: local [row0, row0 + nown)
     std::vector<int> send_ptr, send_rows;    // rows sent to each peer: local ids, grouped by peer
     std::vector<int> recv_start, recv_cnt;   // halo rows from each peer: local first row, count
+};
+struct ShardPlan {
+    int world = 1, rank = 0;
+    std::vector<ShardConePlan> cones;        // every cone's rows split the same way
     std::vector<int> con_gid;                // local constraint -> global constraint
     std::vector<int> shared_gid;             // shared constraints, ascending global id (same on every shard)
     std::vector<int> shared_lid;             // per shared constraint: its local id here, or -1

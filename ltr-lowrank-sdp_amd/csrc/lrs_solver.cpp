@@ -177,7 +177,7 @@ struct lrs_ctx {
     struct ShardComm *comm = nullptr;
     ShardPlan plan;
     ShardHooks hooks;
-    int *d_send_rows = nullptr;
+    std::vector<int *> d_send_rows;   // per cone: its send rows (local ids, grouped by peer)
     double *d_sendbuf = nullptr;
     long sendbuf_len = 0;
     // phase-1 budget hook (lrs_set_budget_hook): called when almInnerBudget is reached;
@@ -203,18 +203,31 @@ struct ShardComm {
     virtual int halo(lrs_ctx *c, double *D, hipStream_t st) = 0;
 };
 static bool sharded(const lrs_ctx *c) { return c->comm != nullptr; }
-static int cone_n_global(const lrs_ctx *c, int k) { return sharded(c) ? c->plan.n_global : c->hp.cones[k].n; }
+static int cone_n_global(const lrs_ctx *c, int k) {
+    return sharded(c) ? c->plan.cones[k].n_global : c->hp.cones[k].n;
+}
 
-// pack this shard's send rows (all peers) into the send buffer
-static int pack_send_rows(lrs_ctx *c, const double *D, hipStream_t st) {
-    const int ld = c->dp.cones[0].ld;
-    const long need = std::max(1L, (long)c->plan.send_rows.size() * ld);
+// send-buffer offset (doubles) of cone k's segment: cone-major, each cone's rows grouped by peer
+static long send_base(const ShardPlan &pl, const DevProblem &dp, int k) {
+    long b = 0;
+    for (int q = 0; q < k; ++q) b += (long)pl.cones[q].send_rows.size() * dp.cones[q].ld;
+    return b;
+}
+
+// pack this shard's send rows (every cone, all peers) of the factor buffer X into the send buffer
+static int pack_send_rows(lrs_ctx *c, const double *X, hipStream_t st) {
+    const int K = c->dp.K;
+    const long need = std::max(1L, send_base(c->plan, c->dp, K));
     if (need > c->sendbuf_len) {
         if (c->d_sendbuf) HIPC(hipFree(c->d_sendbuf));
         HIPC(hipMalloc((void **)&c->d_sendbuf, sizeof(double) * need));
         c->sendbuf_len = need;
     }
-    OPC(launch_pack_rows((int)c->plan.send_rows.size(), ld, c->d_send_rows, D, c->d_sendbuf, st));
+    for (int k = 0; k < K; ++k) {
+        const DevCone &dc = c->dp.cones[k];
+        OPC(launch_pack_rows((int)c->plan.cones[k].send_rows.size(), dc.ld, c->d_send_rows[k], X + dc.foff,
+                             c->d_sendbuf + send_base(c->plan, c->dp, k), st));
+    }
     return 0;
 }
 
@@ -254,15 +267,22 @@ struct RcclComm : ShardComm {
     }
     int halo(lrs_ctx *c, double *D, hipStream_t st) override {
         const ShardPlan &pl = c->plan;
-        const int ld = c->dp.cones[0].ld;
         if (pack_send_rows(c, D, st)) return -1;
+        // per peer, one send and one receive per cone, in cone order on both sides
         NCCLC(ncclGroupStart());
-        for (int q = 0; q < pl.world; ++q) {
-            const int ns = pl.send_ptr[q + 1] - pl.send_ptr[q];
-            if (ns > 0) NCCLC(ncclSend(c->d_sendbuf + (long)pl.send_ptr[q] * ld, (size_t)ns * ld, ncclDouble, q, comm, st));
-            if (pl.recv_cnt[q] > 0)
-                NCCLC(ncclRecv(D + (long)pl.recv_start[q] * ld, (size_t)pl.recv_cnt[q] * ld, ncclDouble, q, comm, st));
-        }
+        for (int q = 0; q < pl.world; ++q)
+            for (int k = 0; k < c->dp.K; ++k) {
+                const ShardConePlan &cp = pl.cones[k];
+                const DevCone &dc = c->dp.cones[k];
+                const int ld = dc.ld;
+                const int ns = cp.send_ptr[q + 1] - cp.send_ptr[q];
+                if (ns > 0)
+                    NCCLC(ncclSend(c->d_sendbuf + send_base(pl, c->dp, k) + (long)cp.send_ptr[q] * ld, (size_t)ns * ld,
+                                   ncclDouble, q, comm, st));
+                if (cp.recv_cnt[q] > 0)
+                    NCCLC(ncclRecv(D + dc.foff + (long)cp.recv_start[q] * ld, (size_t)cp.recv_cnt[q] * ld, ncclDouble, q,
+                                   comm, st));
+            }
         NCCLC(ncclGroupEnd());
         return 0;
     }
@@ -333,18 +353,22 @@ struct LoopComm : ShardComm {
         return 0;
     }
     int halo(lrs_ctx *c, double *D, hipStream_t st) override {
-        const int ld = c->dp.cones[0].ld;
         if (pack_send_rows(c, D, st)) return -1;
         g->sendbufs[rank] = c->d_sendbuf;
         if (pre(st)) return -1;
-        for (int q = 0; q < g->world; ++q) {
-            const int cnt = c->plan.recv_cnt[q];
-            if (q == rank || cnt == 0) continue;
-            const ShardPlan &pq = *g->plans[q];
-            if (pq.send_ptr[rank + 1] - pq.send_ptr[rank] != cnt) { set_err("loopback halo: plan mismatch"); return -1; }
-            HIPC(hipMemcpyAsync(D + (long)c->plan.recv_start[q] * ld, g->sendbufs[q] + (long)pq.send_ptr[rank] * ld,
-                                sizeof(double) * cnt * ld, hipMemcpyDeviceToDevice, st));
-        }
+        for (int q = 0; q < g->world; ++q)
+            for (int k = 0; k < c->dp.K; ++k) {
+                const ShardConePlan &cp = c->plan.cones[k];
+                const int cnt = cp.recv_cnt[q], ld = c->dp.cones[k].ld;
+                if (q == rank || cnt == 0) continue;
+                const ShardPlan &pq = *g->plans[q];
+                const ShardConePlan &qc = pq.cones[k];
+                if (qc.send_ptr[rank + 1] - qc.send_ptr[rank] != cnt) { set_err("loopback halo: plan mismatch"); return -1; }
+                // the peer's segment offset (same ranks, so the same layouts on every shard)
+                HIPC(hipMemcpyAsync(D + c->dp.cones[k].foff + (long)cp.recv_start[q] * ld,
+                                    g->sendbufs[q] + send_base(pq, c->dp, k) + (long)qc.send_ptr[rank] * ld,
+                                    sizeof(double) * cnt * ld, hipMemcpyDeviceToDevice, st));
+            }
         return post(st);
     }
 };
@@ -593,9 +617,10 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
         OPC(launch_fill(P.m, 0.0, W.cvs, c->st));
         for (int k = 0; k < P.K; ++k) {
             OPC(launch_gather_cone(P, k, W.uvt2, W.cvc + (long)k * P.m, c->st));
+            OPC(sync_shared(P, W.cvc + (long)k * P.m, c->st));   // sharded: the holders' sums
             OPC(launch_axpby(P.m, 1.0, W.cvc + (long)k * P.m, 1.0, W.cvs, c->st));
         }
-        OPC(launch_resid(P.m, P.b, W.cvs, c->st));
+        OPC(launch_resid(P.m, P.b, W.cvs, c->st, P.cmask));   // sharded: each constraint once
         fin = TF_RESID;
     }
     if (blam) OPC(launch_dot(P.m, P.bprim ? P.bprim : P.b, W.lam, W.part, c->st, nullptr));
@@ -1036,11 +1061,19 @@ static int init_point(lrs_ctx *c) {
         R[i] = v;
     }
     if (sharded(c)) {
-        // the whole problem's draw, then this shard's rows (owned + halo)
-        const int ng = c->plan.n_global, nl = c->dp.cones[0].n, r = c->rank[0];
-        std::vector<double> Rl((long)nl * r);
-        for (int q = 0; q < r; ++q)
-            for (int l = 0; l < nl; ++l) Rl[l + (long)q * nl] = R[c->plan.gid[l] + (long)q * ng];
+        // the whole problem's draw (cones in order, each column-major), then this shard's rows
+        // (owned + halo) of every cone
+        long NRl = 0, og = 0, ol = 0;
+        for (int k = 0; k < c->dp.K; ++k) NRl += (long)c->dp.cones[k].n * c->rank[k];
+        std::vector<double> Rl(NRl);
+        for (int k = 0; k < c->dp.K; ++k) {
+            const ShardConePlan &cp = c->plan.cones[k];
+            const int ng = cp.n_global, nl = c->dp.cones[k].n, r = c->rank[k];
+            for (int q = 0; q < r; ++q)
+                for (int l = 0; l < nl; ++l) Rl[ol + l + (long)q * nl] = R[og + cp.gid[l] + (long)q * ng];
+            og += (long)ng * r;
+            ol += (long)nl * r;
+        }
         R.swap(Rl);
     }
     if (factor_put(c, c->W.R, R.data())) return -1;
@@ -1083,7 +1116,7 @@ static int regrow(lrs_ctx *c, const std::vector<int> &nr) {
             const int aug = rn - ro, r = std::min(cone_n_global(c, k), aug);   // lpRandomDiag :1096-1106
             if (sharded(c)) {   // global row i of new column i, on the shard's local rows
                 for (int l = 0; l < n; ++l) {
-                    const int gi = c->plan.gid[l];
+                    const int gi = c->plan.cones[k].gid[l];
                     if (gi < r) dst[dn + (long)n * ro + (long)gi * n + l] = 1 / std::sqrt((double)r);
                 }
             } else {
@@ -1617,11 +1650,12 @@ static int refresh_cone(lrs_ctx *c, int k) {   // lorads_alg_common.c:310-314
     // cvs = (cvs - cvc[k]) + A_k(U V^T) in the pass that rewrites cvc[k] (the same two
     // roundings as the reference's two axpys)
     if (P.nsh > 0) {
-        // sharded, shared constraints: the summed A_k(U V^T) first (one cone: cvs = cvc, as
-        // (cvs - cvc_old) + cvc_new is with cvs = cvc_old)
+        // sharded, shared constraints: the holders' sums of A_k(U V^T) meet first, then the two
+        // axpys of the reference (cvs - cvc_old, + cvc_new)
+        OPC(launch_axpby(P.m, -1.0, cv, 1.0, W.cvs, c->st));
         OPC(launch_auv_con(P, k, 0, W.U, W.V, 1.0, 0, cv, nullptr, nullptr, c->st, nullptr));
         OPC(sync_shared(P, cv, c->st));
-        HIPC(hipMemcpyAsync(W.cvs, cv, sizeof(double) * P.m, hipMemcpyDeviceToDevice, c->st));
+        OPC(launch_axpby(P.m, 1.0, cv, 1.0, W.cvs, c->st));
         return 0;
     }
     OPC(launch_auv_con(P, k, 0, W.U, W.V, 1.0, 0, cv, nullptr, nullptr, c->st, nullptr, W.cvs));
@@ -2024,8 +2058,10 @@ void lrs_ctx_destroy(lrs_ctx *c) {
     for (auto &e : c->bev)
         if (e) (void)hipEventDestroy(e);
     delete c->comm;
-    for (void *q : {(void *)c->s_tickets, (void *)c->s_tmpfin, (void *)c->s_rpart, (void *)c->d_send_rows,
-                    (void *)c->d_sendbuf, (void *)c->Cw0, (void *)c->Craw0})
+    for (void *q : {(void *)c->s_tickets, (void *)c->s_tmpfin, (void *)c->s_rpart, (void *)c->d_sendbuf,
+                    (void *)c->Cw0, (void *)c->Craw0})
+        if (q) (void)hipFree(q);
+    for (int *q : c->d_send_rows)
         if (q) (void)hipFree(q);
     bind_scratch(nullptr, nullptr, nullptr);
     if (c->st) (void)hipStreamDestroy(c->st);
@@ -2721,18 +2757,20 @@ static int shard_setup(lrs_ctx *c, int world, int rank) {
         HIPC(hipMemcpy(P.bprim, bp.data(), sizeof(double) * bp.size(), hipMemcpyHostToDevice));
         HIPC(hipMemset(P.g3, 0, sizeof(double) * 3 * mk.size()));
     }
-    DevCone &dc = c->dp.cones[0];
-    dc.row0 = c->plan.row0;
-    dc.nown = c->plan.nown;
+    for (int k = 0; k < c->dp.K; ++k) {
+        c->dp.cones[k].row0 = c->plan.cones[k].row0;
+        c->dp.cones[k].nown = c->plan.cones[k].nown;
+    }
     c->hooks.self = c;
     c->hooks.halo = hook_halo;
     c->hooks.allreduce = hook_allreduce;
     c->dp.shard = &c->hooks;
-    const size_t ns = std::max<size_t>(1, c->plan.send_rows.size());
-    HIPC(hipMalloc((void **)&c->d_send_rows, sizeof(int) * ns));
-    if (!c->plan.send_rows.empty())
-        HIPC(hipMemcpy(c->d_send_rows, c->plan.send_rows.data(), sizeof(int) * c->plan.send_rows.size(),
-                       hipMemcpyHostToDevice));
+    c->d_send_rows.assign(c->dp.K, nullptr);
+    for (int k = 0; k < c->dp.K; ++k) {
+        const std::vector<int> &sr = c->plan.cones[k].send_rows;
+        HIPC(hipMalloc((void **)&c->d_send_rows[k], sizeof(int) * std::max<size_t>(1, sr.size())));
+        if (!sr.empty()) HIPC(hipMemcpy(c->d_send_rows[k], sr.data(), sizeof(int) * sr.size(), hipMemcpyHostToDevice));
+    }
     c->init_cache.clear();
     c->init_ranks.clear();
     c->cgIterCone.assign(c->hp.K, 0);
@@ -2808,9 +2846,9 @@ int lrs_shard_info(lrs_ctx *c, int *world, int *rank, int *row0, int *nown, int 
     const bool s = sharded(c);
     if (world) *world = s ? c->plan.world : 1;
     if (rank) *rank = s ? c->plan.rank : 0;
-    if (row0) *row0 = s ? c->plan.bounds[c->plan.rank] : 0;
-    if (nown) *nown = s ? c->plan.nown : (c->loaded ? c->hp.cones[0].n : 0);
-    if (nhalo) *nhalo = s ? c->dp.cones[0].n - c->plan.nown : 0;
+    if (row0) *row0 = s ? c->plan.cones[0].bounds[c->plan.rank] : 0;
+    if (nown) *nown = s ? c->plan.cones[0].nown : (c->loaded ? c->hp.cones[0].n : 0);
+    if (nhalo) *nhalo = s ? c->dp.cones[0].n - c->plan.cones[0].nown : 0;
     return 0;
 }
 
@@ -2826,14 +2864,15 @@ int lrs_shard_plan(const char *path, int world, int rank, long *counts, int *bou
     std::string err;
     if (!read_sdpa(path, g, err)) { set_err("read_sdpa: %s", err.c_str()); return -1; }
     if (!shard_problem(g, world, rank, out, pl, err)) { set_err("shard: %s", err.c_str()); return -1; }
-    counts[0] = pl.n_global; counts[1] = pl.bounds[rank]; counts[2] = pl.nown; counts[3] = (long)pl.gid.size();
-    counts[4] = (long)pl.send_rows.size(); counts[5] = (long)pl.shared_gid.size(); counts[6] = (long)pl.con_gid.size();
+    const ShardConePlan &c0 = pl.cones[0];   // the row partition of cone 0 (every cone is split alike)
+    counts[0] = c0.n_global; counts[1] = c0.bounds[rank]; counts[2] = c0.nown; counts[3] = (long)c0.gid.size();
+    counts[4] = (long)c0.send_rows.size(); counts[5] = (long)pl.shared_gid.size(); counts[6] = (long)pl.con_gid.size();
     counts[7] = world;
-    if (bounds) std::copy(pl.bounds.begin(), pl.bounds.end(), bounds);
-    if (local_gid) std::copy(pl.gid.begin(), pl.gid.end(), local_gid);
-    if (send_ptr) std::copy(pl.send_ptr.begin(), pl.send_ptr.end(), send_ptr);
+    if (bounds) std::copy(c0.bounds.begin(), c0.bounds.end(), bounds);
+    if (local_gid) std::copy(c0.gid.begin(), c0.gid.end(), local_gid);
+    if (send_ptr) std::copy(c0.send_ptr.begin(), c0.send_ptr.end(), send_ptr);
     if (send_gid)
-        for (size_t q = 0; q < pl.send_rows.size(); ++q) send_gid[q] = pl.gid[pl.send_rows[q]];
+        for (size_t q = 0; q < c0.send_rows.size(); ++q) send_gid[q] = c0.gid[c0.send_rows[q]];
     if (shared_gid) std::copy(pl.shared_gid.begin(), pl.shared_gid.end(), shared_gid);
     if (con_gid) std::copy(pl.con_gid.begin(), pl.con_gid.end(), con_gid);
     if (primary)

@@ -239,10 +239,12 @@ class Solver:
         self._after_shard()
 
     def _after_shard(self):
+        """The shard's local sizes (every cone: owned + halo rows; the local constraints)."""
         m, k = C.c_int(), C.c_int()
-        dims = (C.c_int * 1)()
+        self._check(self.lib.lrs_problem_info(self.ctx, C.byref(m), C.byref(k), None, None, None), "info")
+        dims = (C.c_int * max(1, k.value))()
         self._check(self.lib.lrs_problem_info(self.ctx, C.byref(m), C.byref(k), dims, None, None), "info")
-        self.m, self.dims = m.value, list(dims)
+        self.m, self.dims = m.value, list(dims)[:k.value]
 
     def shard_info(self):
         """(world, rank, first global row, owned rows, halo rows)."""

@@ -139,10 +139,11 @@ def test_sharded_full_solve_matches_single_gpu(solver_mod, name, world):
 
 
 @pytest.mark.parametrize("name,world", [("theta40", 2), ("theta40", 3), ("rsparse60", 2), ("rsparse60", 4),
-                                        ("mc_torus12x10", 3)])
+                                        ("mc_torus12x10", 3), ("theta25x3", 2), ("theta25x3", 3)])
 def test_sharded_steps_match_reference(solver_mod, name, world):
     """Constraints spanning row blocks (theta's trace and cross-block edges, rsparse's random
-    multi-entry rows): every holder sums its owned-slot entries, the shared constraints'
+    multi-entry rows; theta25x3: three cones, each split across the shards): every holder sums
+    its owned-slot entries, the shared constraints'
     sums meet in an all-reduce, and the primary holder alone counts them in the line-search
     dots and residuals.  K fused ALM trips on every shard against the reference's own K trips
     (tests/golden/steps_<name>.npz): tau, ||G||^2 and pinf to 1e-9 relative."""
@@ -167,7 +168,7 @@ def test_sharded_steps_match_reference(solver_mod, name, world):
             assert abs(d["pinf"] - pinf) <= 1e-9 * max(abs(pinf), 1e-300), (K, d["pinf"], pinf)
 
 
-@pytest.mark.parametrize("name,world", [("theta40", 2), ("rsparse60", 3)])
+@pytest.mark.parametrize("name,world", [("theta40", 2), ("rsparse60", 3), ("theta25x3", 2)])
 def test_sharded_full_solve_shared_constraints(solver_mod, name, world):
     """Whole ALM + ADMM solves with shared constraints (the CG direction's halo rows exchanged
     before every matvec, A(.) of shared constraints summed over the holders): every shard

@@ -82,7 +82,7 @@ def test_shard_plan_multiprocess(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    names = ["mc_torus12x10", "mc_rand200", "theta40", "rsparse60"]
+    names = ["mc_torus12x10", "mc_rand200", "theta40", "rsparse60", "theta25x3"]
     procs = [ctx.Process(target=_worker, args=(r, world, port, names, q)) for r in range(world)]
     for p in procs:
         p.start()
