@@ -175,6 +175,11 @@ int lrs_auut_bytes(lrs_ctx *ctx, double *bytes);
  * Gram (kernel + reduction), gram_ms = ms of the MFMA kernel alone (may be NULL). */
 int lrs_time_gram(lrs_ctx *ctx, int cone, int reps, double *avg_ms, double *gram_ms);
 
+/* The FP64 matrix-core ceiling on this device, measured: TFLOP/s of back-to-back
+ * v_mfma_f64_16x16x4f64 on every CU (8 independent accumulators a wave, 2 waves a SIMD).
+ * Diagnostics for the Gram's roofline; no reference counterpart. */
+int lrs_mfma_f64_peak(lrs_ctx *ctx, double *tflops);
+
 /* Per-stage timing of the split ALM inner iteration: runs `steps` inner iterations at
  * the current rank like lrs_alm_throughput, with HIP events on the solver stream
  * around each of the four launches (S1 direction+SDDMM, S2 q-gather, S3 update+

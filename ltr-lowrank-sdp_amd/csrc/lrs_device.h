@@ -224,7 +224,9 @@ int launch_alm_m1(const DevProblem &P, double rho, const double *lam, const doub
 constexpr int kGramMaxChunks = 64;
 size_t gram_buf_len(int rmax);
 int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y, int avg,
-                double *gram, int *nblk_used, hipStream_t st);
+                double *gram, int *nblk_used, hipStream_t st, bool reduce = true);
+// sustained v_mfma_f64_16x16x4f64 rate: every CU, 2 waves a SIMD, 8 accumulators a wave
+int mfma_f64_peak(hipStream_t st, double *tflops);
 
 // ---- fused ALM inner iteration (device-side control; see lrs_kernels.hip) ----
 struct AlmIterArgs {

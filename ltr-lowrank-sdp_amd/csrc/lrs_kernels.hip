@@ -586,82 +586,165 @@ __global__ void __launch_bounds__(kBlock) k_alm_m1(int m, double rho, const doub
 }
 
 // r x r Gram X^T X (or of the average (X+Y)/2), build_gram_from_factor /
-// build_gram_from_average (lorads_logging.c:216-270), on the FP64 matrix cores.
-// Grid (C row chunks) x (one 16 x 16 output tile (a <= b) per y).  C is a multiple of 8,
-// so the linear block id y*C + x puts every tile of chunk x on the same XCD (id mod 8):
-// the chunk's rows are fetched into that XCD's L2 once and re-read from there by its
-// tiles.  The four waves of a block take interleaved k-steps of 4 rows of the chunk
-// (v_mfma_f64_16x16x4f64, operands straight from global memory: lane l of a k-step reads
-// row 4s + (l >> 4), columns 16a + (l & 15) and 16b + (l & 15)), kGramBatch k-steps of
-// loads issued before their MFMAs; the waves' accumulators meet in LDS (wave order) and
-// the block stores the chunk's tile partial.  k_gram_fin (one block per tile) sums the C
-// partials in chunk order, eight loads in flight, and writes the tile and its transpose.
-// Deterministic.  (A last-block ticket in k_gram itself was measured slower: one
-// agent-scope release -- an L2 write-back -- per block, thousands of blocks.)
+// build_gram_from_average (lorads_logging.c:216-270), on the FP64 matrix cores
+// (v_mfma_f64_16x16x4f64).  Register-blocked: a wave owns an NB x NB block of 16 x 16
+// tiles -- column block A (16 NB columns) against column block B >= A -- and its lane l
+// reads, per k-step of 4 rows, NB consecutive doubles of row 4s + (l >> 4) at column
+// 16 NB A + NB (l & 15) (one vector load), so sub-tile t of a block holds the columns
+// 16 NB A + NB m + t, m = 0..15: NB^2 MFMAs per 2 NB doubles loaded per lane (a diagonal
+// block loads once).  Grid (C row chunks) x (block pairs A <= B); C is a multiple of 8,
+// so the linear block id y*C + x puts every pair of chunk x on the same XCD (id mod 8)
+// and the chunk's rows are fetched into that XCD's L2 once.  The four waves of a
+// workgroup take interleaved k-steps of the chunk (unmasked batches, one masked tail),
+// their accumulators meet in LDS (wave order, four sub-tiles a round) and the workgroup
+// stores the chunk's partial sub-tiles.  k_gram_fin (one workgroup per sub-tile) sums the
+// C partials (four interleaved quarters, every load in one trip) and scatters the
+// sub-tile and its transpose.  Deterministic.  Columns in [r, 16 NB nbc) are never
+// stored: they only reach output entries of their own column, so they are read as they
+// lie (padding below the row pitch ld) or from the row's last NB columns (past ld).
 // D fragment: col = l & 15, row = (l >> 4) + 4q (cdna_hip_programming.md §3, f64 map).
-constexpr int kGramMaxTiles = 32 * 33 / 2;   // r <= 512
-constexpr int kGramBatch = 8;
 typedef double gram_acc_t __attribute__((ext_vector_type(4)));
-__global__ void __launch_bounds__(kBlock) k_gram(int n, int r, int ld, const double *__restrict__ X,
-                                                 const double *__restrict__ Y, int avg,
-                                                 double *__restrict__ part, double *__restrict__ out) {
-    __shared__ double red[kBlock / 64][256];
-    const int rt = (r + 15) >> 4;
-    int id = blockIdx.y, a = 0;
-    while (id >= rt - a) { id -= rt - a; ++a; }
-    const int b = a + id, tile = blockIdx.y;
+template <int NB>
+struct GramVec;
+template <>
+struct GramVec<1> { typedef double T; };
+template <>
+struct GramVec<2> { typedef double T __attribute__((ext_vector_type(2))); };
+template <>
+struct GramVec<4> { typedef double T __attribute__((ext_vector_type(4))); };
+
+template <int NB>
+__device__ __forceinline__ void gram_ld(const double *__restrict__ p, double *o) {
+    typedef typename GramVec<NB>::T V;
+    const V v = *reinterpret_cast<const V *>(p);
+    if constexpr (NB == 1) o[0] = v;
+    else {
+#pragma unroll
+        for (int t = 0; t < NB; ++t) o[t] = v[t];
+    }
+}
+
+// one wave's k-steps of an (A, B) block pair; branch-free so that a batch's U loads are all
+// in flight before its MFMAs (the row test is a select; a lane whose NB columns start at or
+// past ld reads the row's last NB columns instead -- they lie at or past r, never stored)
+template <int NB, int U, bool AVG, bool DIAG>
+__device__ __forceinline__ void gram_loop(int nk, int i0, int i1, int w, int lane, long base, long step,
+                                          long clamp0, const double *__restrict__ X, const double *__restrict__ Y,
+                                          int colA, int colB, gram_acc_t (&acc)[NB][NB]) {
+    for (int j0 = 0; j0 < nk; j0 += U) {
+        double xa[U][NB], xb[U][NB];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = i0 + 16 * (j0 + u) + 4 * w + (lane >> 4);
+            const bool ok = row < i1;
+            const long o = ok ? base + (j0 + u) * step : clamp0;
+            gram_ld<NB>(X + o + colA, xa[u]);
+            if constexpr (!DIAG) gram_ld<NB>(X + o + colB, xb[u]);
+            if constexpr (AVG) {
+                double ya[NB], yb[NB];
+                gram_ld<NB>(Y + o + colA, ya);
+                if constexpr (!DIAG) gram_ld<NB>(Y + o + colB, yb);
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {
+                    xa[u][t] = 0.5 * (xa[u][t] + ya[t]);
+                    if constexpr (!DIAG) xb[u][t] = 0.5 * (xb[u][t] + yb[t]);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < NB; ++t) {
+                xa[u][t] = ok ? xa[u][t] : 0.0;
+                if constexpr (DIAG) xb[u][t] = xa[u][t];
+                else xb[u][t] = ok ? xb[u][t] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int p = 0; p < NB; ++p)
+#pragma unroll
+                for (int q = 0; q < NB; ++q)
+                    acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[u][p], xb[u][q], acc[p][q], 0, 0, 0);
+    }
+}
+
+template <int NB, int U, bool AVG>
+__global__ void __launch_bounds__(kBlock) k_gram(int n, int r, int ld, int nbc, const double *__restrict__ X,
+                                                 const double *__restrict__ Y, double *__restrict__ part) {
+    constexpr int W = 16 * NB;
+    __shared__ double red[kBlock / 64][4][256];
+    int id = blockIdx.y, A = 0;
+    while (id >= nbc - A) { id -= nbc - A; ++A; }
+    const int B = A + id, pair = blockIdx.y;
     const int C = gridDim.x, ch = blockIdx.x;
     const int per = ((n + C - 1) / C + 15) / 16 * 16;
     const int i0 = ch * per, i1 = min(n, i0 + per);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int ca = min(16 * a + (lane & 15), r - 1), cb = min(16 * b + (lane & 15), r - 1);
-    const bool va = 16 * a + (lane & 15) < r, vb = 16 * b + (lane & 15) < r;
-    gram_acc_t acc = gram_acc_t{0.0, 0.0, 0.0, 0.0};
+    const int colA = min(W * A + NB * (lane & 15), ld - NB), colB = min(W * B + NB * (lane & 15), ld - NB);
+    gram_acc_t acc[NB][NB];
+#pragma unroll
+    for (int p = 0; p < NB; ++p)
+#pragma unroll
+        for (int q = 0; q < NB; ++q) acc[p][q] = gram_acc_t{0.0, 0.0, 0.0, 0.0};
     // this wave's k-steps: rows i0 + 16 j + 4 w + (lane >> 4), j = 0, 1, ...
-    for (int j0 = 0; i0 + 16 * j0 + 4 * w < i1; j0 += kGramBatch) {
-        double xa[kGramBatch], xb[kGramBatch];
-#pragma unroll
-        for (int u = 0; u < kGramBatch; ++u) {
-            const int row = i0 + 16 * (j0 + u) + 4 * w + (lane >> 4);
-            const bool ok = row < i1;
-            const long o = (long)(ok ? row : i0) * ld;   // clamped, never branched
-            double x = X[o + ca], y = X[o + cb];
-            if (avg) {
-                x = 0.5 * (x + Y[o + ca]);
-                y = 0.5 * (y + Y[o + cb]);
-            }
-            xa[u] = (ok && va) ? x : 0.0;
-            xb[u] = (ok && vb) ? y : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < kGramBatch; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[u], xb[u], acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) red[w][q * 64 + lane] = acc[q];
-    __syncthreads();
+    const int nk = i1 > i0 + 4 * w ? (i1 - i0 - 4 * w + 15) / 16 : 0;
+    const long step = 16L * ld, base = (long)(i0 + 4 * w + (lane >> 4)) * ld, clamp0 = (long)i0 * ld;
+    if (A == B) gram_loop<NB, U, AVG, true>(nk, i0, i1, w, lane, base, step, clamp0, X, Y, colA, colB, acc);
+    else gram_loop<NB, U, AVG, false>(nk, i0, i1, w, lane, base, step, clamp0, X, Y, colA, colB, acc);
+    // wave partials -> LDS, four sub-tiles a round, summed in wave order
     const int t = threadIdx.x;   // t = q * 64 + l
-    double v = red[0][t];
 #pragma unroll
-    for (int ww = 1; ww < kBlock / 64; ++ww) v += red[ww][t];
-    part[((long)tile * C + ch) * 256 + t] = v;
-}
-__global__ void __launch_bounds__(kBlock) k_gram_fin(int r, int C, const double *__restrict__ part,
-                                                     double *__restrict__ out) {
-    const int rt = (r + 15) >> 4;
-    int id = blockIdx.x, a = 0;
-    while (id >= rt - a) { id -= rt - a; ++a; }
-    const int b = a + id, tile = blockIdx.x, t = threadIdx.x;
-    double s = 0.0;
-    for (int c0 = 0; c0 < C; c0 += 8) {   // eight loads in flight, summed in chunk order
-        double pv[8];
+    for (int g = 0; g < (NB * NB + 3) / 4; ++g) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) pv[u] = c0 + u < C ? part[((long)tile * C + c0 + u) * 256 + t] : 0.0;
+        for (int k = 0; k < 4; ++k) {
+            const int st = 4 * g + k;
+            if (st < NB * NB)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s += pv[u];
+                for (int q = 0; q < 4; ++q) red[w][k][q * 64 + lane] = acc[st / NB][st % NB][q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int st = 4 * g + k;
+            if (st < NB * NB) {
+                double v = red[0][k][t];
+#pragma unroll
+                for (int ww = 1; ww < kBlock / 64; ++ww) v += red[ww][k][t];
+                part[(((long)pair * NB * NB + st) * C + ch) * 256 + t] = v;
+            }
+        }
+        __syncthreads();
     }
+}
+// k_gram_fin: four workgroups per sub-tile, 64 of its elements each; thread (p, e) of a
+// workgroup sums the chunks c = p (mod 16) of element e (every load in one memory trip:
+// C <= 64), the sixteen partial sums meet in LDS in order
+constexpr int kGramFinThreads = 1024;
+__global__ void __launch_bounds__(kGramFinThreads) k_gram_fin(int r, int NB, int nbc, int C,
+                                                              const double *__restrict__ part,
+                                                              double *__restrict__ out) {
+    static_assert(kGramMaxChunks <= 64, "4 chunks per thread");
+    __shared__ double q16[16][64];
+    const int sub = blockIdx.x >> 2, st = sub % (NB * NB);
+    int id = sub / (NB * NB), A = 0;
+    while (id >= nbc - A) { id -= nbc - A; ++A; }
+    const int B = A + id, e = threadIdx.x & 63, pq = threadIdx.x >> 6;
+    const int t = (blockIdx.x & 3) * 64 + e;   // element of the sub-tile, t = q * 64 + l
+    double pv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int ch = pq + 16 * u;
+        pv[u] = ch < C ? part[((long)sub * C + ch) * 256 + t] : 0.0;
+    }
+    q16[pq][e] = (pv[0] + pv[1]) + (pv[2] + pv[3]);
+    __syncthreads();
+    if (pq != 0) return;
+    double s = q16[0][e];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) s += q16[k][e];
     const int q = t >> 6, l = t & 63;
-    const int row = 16 * a + (l >> 4) + 4 * q, col = 16 * b + (l & 15);
-    if (row < r && col < r) {
+    const int W = 16 * NB;
+    const int row = W * A + NB * ((l >> 4) + 4 * q) + st / NB, col = W * B + NB * (l & 15) + st % NB;
+    if (row < r && col < r && (A != B || row <= col)) {
         out[(long)row * r + col] = s;
         out[(long)col * r + row] = s;
     }
@@ -3440,28 +3523,104 @@ int launch_alm_m1(const DevProblem &P, double rho, const double *lam, const doub
     return 0;
 }
 static int num_cus();
+// the FP64 matrix-core ceiling the Gram is measured against (bench.py): back-to-back
+// v_mfma_f64_16x16x4f64 on 8 independent accumulators, 2 waves a SIMD on every CU
+__global__ void __launch_bounds__(kBlock) k_mfma_peak(int iters, double *out) {
+    gram_acc_t acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = gram_acc_t{0.0, 0.0, 0.0, 0.0};
+    const double a = 1.0 + 1e-9 * threadIdx.x, b = 1.0 - 1e-9 * threadIdx.x;
+    for (int i = 0; i < iters; ++i)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += (acc[k][0] + acc[k][1]) + (acc[k][2] + acc[k][3]);
+    out[(long)blockIdx.x * kBlock + threadIdx.x] = s;
+}
+int mfma_f64_peak(hipStream_t st, double *tflops) {
+    const int blocks = 2 * num_cus(), iters = 2000;
+    double *out = nullptr;
+    hipEvent_t e0, e1;
+    if (hipMalloc((void **)&out, sizeof(double) * blocks * kBlock) != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "mfma_f64_peak: hipMalloc");
+        return -1;
+    }
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kBlock), 0, st, iters, out);   // warm (clocks up)
+    (void)hipEventRecord(e0, st);
+    hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kBlock), 0, st, iters, out);
+    (void)hipEventRecord(e1, st);
+    const hipError_t e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(out);
+    if (e != hipSuccess || ms <= 0.f) {
+        snprintf(g_err, sizeof(g_err), "mfma_f64_peak: %s", hipGetErrorString(e));
+        return -1;
+    }
+    const double flop = (double)blocks * (kBlock / 64) * iters * 8 * 2048.0;
+    *tflops = flop / (ms * 1e-3) / 1e12;
+    return 0;
+}
+
+// register blocking of the Gram: NB x NB tiles per wave (16 NB columns a side)
+static int gram_nb(int r) { return r > 16 ? 2 : 1; }
+static long gram_subtiles(int r, int nb) {
+    const long nbc = (r + 16 * nb - 1) / (16 * nb);
+    return nbc * (nbc + 1) / 2 * nb * nb;
+}
 size_t gram_buf_len(int rmax) {
-    const long rt = (rmax + 15) / 16;
-    return (size_t)rmax * rmax + (size_t)kGramMaxChunks * (rt * (rt + 1) / 2) * 256;
+    long sub = 0;
+    for (int nb = 1; nb <= 4; nb *= 2) sub = std::max(sub, gram_subtiles(rmax, nb));
+    return (size_t)rmax * rmax + (size_t)kGramMaxChunks * sub * 256;
 }
 int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y, int avg, double *gram,
-                int *nblk_used, hipStream_t st) {
+                int *nblk_used, hipStream_t st, bool reduce) {
     const DevCone &c = P.cones[cone];
-    const int rt = (c.r + 15) / 16;
-    const int ntiles = rt * (rt + 1) / 2;
-    if (ntiles > kGramMaxTiles) {
+    if (c.r > 512) {
         snprintf(g_err, sizeof(g_err), "gram: rank %d above 512", c.r);
         return -1;
     }
-    // row chunks: a multiple of 8 (chunk x's tiles share an XCD), >= 64 rows each, at most
-    // kGramMaxChunks (the partial buffer)
-    int gx = std::max(1, std::min(kGramMaxChunks, (c.nown + 63) / 64));
+    int nb = gram_nb(c.r);
+#ifdef LRS_GRAM_DIAG
+    if (getenv("LRS_GRAM_NB")) nb = atoi(getenv("LRS_GRAM_NB"));
+#endif
+    const int nbc = (c.r + 16 * nb - 1) / (16 * nb);
+    const int npair = nbc * (nbc + 1) / 2;
+    // row chunks: a multiple of 8 (chunk x's pairs share an XCD), >= 64 rows each, at most
+    // kGramMaxChunks (the partial buffer), about 1024 workgroups in all (the partials' bytes
+    // grow with the chunk count)
+    int gx = std::max(1, std::min({kGramMaxChunks, (c.nown + 63) / 64, std::max(8, 1024 / npair)}));
+#ifdef LRS_GRAM_DIAG
+    if (getenv("LRS_GRAM_C")) gx = std::min(gx, atoi(getenv("LRS_GRAM_C")));
+#endif
     if (gx >= 8) gx &= ~7;
-    hipLaunchKernelGGL(k_gram, dim3(gx, ntiles), dim3(kBlock), 0, st, c.nown, c.r, c.ld,
-                       X + c.foff + (long)c.row0 * c.ld, Y ? Y + c.foff + (long)c.row0 * c.ld : nullptr, avg,
-                       gram + (long)c.r * c.r, gram);
+    const double *Xs = X + c.foff + (long)c.row0 * c.ld;
+    const double *Ys = Y ? Y + c.foff + (long)c.row0 * c.ld : nullptr;
+    double *part = gram + (long)c.r * c.r;
+    const dim3 grid(gx, npair);
+#define LRS_GRAM_GO(NB_, U_)                                                                                      \
+    do {                                                                                                          \
+        if (avg)                                                                                                  \
+            hipLaunchKernelGGL((k_gram<NB_, U_, true>), grid, dim3(kBlock), 0, st, c.nown, c.r, c.ld, nbc, Xs, Ys,  \
+                               part);                                                                             \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_gram<NB_, U_, false>), grid, dim3(kBlock), 0, st, c.nown, c.r, c.ld, nbc, Xs, Ys, \
+                               part);                                                                             \
+    } while (0)
+    if (nb == 4) LRS_GRAM_GO(4, 2);
+    else if (nb == 2 && (c.nown + 16L * gx - 1) / (16L * gx) <= 12) LRS_GRAM_GO(2, 4);   // <= 12 k-steps a wave
+    else if (nb == 2) LRS_GRAM_GO(2, 8);
+    else LRS_GRAM_GO(1, 8);
+#undef LRS_GRAM_GO
     LRS_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_gram_fin, dim3(ntiles), dim3(kBlock), 0, st, c.r, gx, gram + (long)c.r * c.r, gram);
+    if (!reduce) return 0;
+    hipLaunchKernelGGL(k_gram_fin, dim3(npair * nb * nb * 4), dim3(kGramFinThreads), 0, st, c.r, nb, nbc, gx, part,
+                       gram);
     LRS_CHECK_LAUNCH();
     if (nblk_used) *nblk_used = gx;
     return 0;
@@ -3537,6 +3696,11 @@ static int forced_regime() {
     return v;
 }
 // force: the context's kernel path (lrs_set_kernel_path): >= 2 forces the bandwidth regime
+// neighbours in flight per lane group in the bandwidth regime's second halves (MODE 2)
+#ifndef LRS_BW_U
+#define LRS_BW_U 1
+#endif
+constexpr int kBwU = LRS_BW_U;
 static StagePlan plan_stage(long rows_threads, int res_small, int res_large, int K, int T, int force) {
     StagePlan p;
     p.T = T;
@@ -3800,7 +3964,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, c.row0, P.m);
             });
         } else {
-            LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_A(1, 2); });
+            LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_A(kBwU, 2); });
         }
         LRS_CHECK_LAUNCH();
         off += grid;
@@ -3909,7 +4073,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    ctrl_cur, ls_cur, L, W.partC, off, c.row0, P.m);
             });
         } else {
-            LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_B(1, 2); });
+            LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_B(kBwU, 2); });
         }
         LRS_CHECK_LAUNCH();
         off += grid;

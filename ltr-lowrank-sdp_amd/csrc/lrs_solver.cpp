@@ -2691,6 +2691,13 @@ int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {
 // Standalone r x r Gram of cone `cone` on R (one k_gram launch: MFMA tiles + the
 // last-arriving chunk's fixed-order reduction): reps back to back between two HIP events.
 // Both outputs are that launch's average (the reduction is no longer a second kernel).
+int lrs_mfma_f64_peak(lrs_ctx *c, double *tflops) {
+    if (!c || !tflops) { set_err("mfma_f64_peak: null argument"); return -1; }
+    bind(c);
+    OPC(mfma_f64_peak(c->st, tflops));
+    return 0;
+}
+
 int lrs_time_gram(lrs_ctx *c, int cone, int reps, double *avg_ms, double *gram_ms) {
     if (c) bind(c);
     if (cone < 0 || cone >= c->dp.K) {
@@ -2701,15 +2708,20 @@ int lrs_time_gram(lrs_ctx *c, int cone, int reps, double *avg_ms, double *gram_m
     HIPC(hipEventCreate(&e0));
     HIPC(hipEventCreate(&e1));
     int nblk = 0;
-    OPC(launch_gram(c->dp, cone, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st));
-    HIPC(hipEventRecord(e0, c->st));
-    for (int q = 0; q < reps; ++q) OPC(launch_gram(c->dp, cone, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st));
-    HIPC(hipEventRecord(e1, c->st));
-    HIPC(hipEventSynchronize(e1));
     float ms = 0;
-    HIPC(hipEventElapsedTime(&ms, e0, e1));
-    *avg_ms = ms / reps;
-    if (gram_ms) *gram_ms = ms / reps;
+    for (int pass = 0; pass < 2; ++pass) {   // 0: MFMA kernel and reduction, 1: the MFMA kernel alone
+        const bool reduce = pass == 0;
+        OPC(launch_gram(c->dp, cone, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st, reduce));
+        HIPC(hipEventRecord(e0, c->st));
+        for (int q = 0; q < reps; ++q)
+            OPC(launch_gram(c->dp, cone, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st, reduce));
+        HIPC(hipEventRecord(e1, c->st));
+        HIPC(hipEventSynchronize(e1));
+        HIPC(hipEventElapsedTime(&ms, e0, e1));
+        if (pass == 0) *avg_ms = ms / reps;
+        else if (gram_ms) *gram_ms = ms / reps;
+        if (!gram_ms) break;
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return 0;

@@ -202,12 +202,34 @@ def test_bandwidth_regime_matches_latency_regime(tmp_path):
             assert abs(a[2] - b[2]) <= 1e-6 * max(1.0, abs(a[2])), (nm, a, b)
 
 
+# ranks across the register-blocking boundaries (NB = 1 / 2 / 4 tiles a side at r <= 16 /
+# <= 192 / above) and the clamped column path (16 NB blocks wider than the row pitch: r = 17,
+# 33 at ld = 24, 48)
+GRAM_RANKS = [1, 5, 16, 17, 19, 33, 64, 128, 193, 200, 290, 512]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("r", [1, 5, 19, 64, 128, 200, 290])
+@pytest.mark.parametrize("r", GRAM_RANKS)
 def test_gram_mfma_matches_fp64(solver_mod, r):
     """k_gram (v_mfma_f64_16x16x4_f64) == X^T X / ((U+V)/2)^T ((U+V)/2) in FP64
     (build_gram_from_factor / _from_average, lorads_logging.c:216-270)."""
     sv = solver_mod.Solver(instance("mc_rand300w"))
+    _gram_check(solver_mod, sv, r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r", [19, 64, 128, 290])
+def test_gram_mfma_many_chunks(solver_mod, tmp_path, r):
+    """The same at n = 4761 (64 row chunks, ragged last chunk)."""
+    import importlib
+    inst = importlib.import_module("ltr-lowrank-sdp_amd.instances")
+    path = str(tmp_path / "t.dat-s")
+    inst.maxcut_torus(path, 69, 69, seed=3)
+    sv = solver_mod.Solver(path)
+    _gram_check(solver_mod, sv, r)
+
+
+def _gram_check(solver_mod, sv, r):
     n = sv.dims[0]
     sv.set_rank([r])
     rng = np.random.default_rng(r)
