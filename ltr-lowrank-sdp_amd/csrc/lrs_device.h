@@ -101,6 +101,9 @@ struct DevCone {
     std::vector<int> dra_n, drb_n;       // their entry counts (A: lower incl. diagonal, B: all)
     int *dra = nullptr, *drb = nullptr;
     long gl_need = 0;                    // doubles of slice gradients the B slices can need (any layout)
+    // dense objective (lrs_problem.h): C as a full n x n row-major matrix, not in the slots
+    int dense_c = 0;
+    double *Cd = nullptr;
 };
 constexpr int kDenseRow = 64;        // entries of a row past which the latency kernels slice it
 constexpr int kSliceMinB = 28;       // fewest entries of one B slice block (G = 64: 7 groups x 4)
@@ -154,6 +157,8 @@ struct DevProblem {
     double *gpack = nullptr;                                 // [nsh][3] the shared ones, all-reduced
     double *spack = nullptr;                                 // [nsh] one m-vector's shared entries
     std::vector<DevCone> cones;
+    int ndense = 0;                                          // cones with a dense objective (DevCone::Cd)
+    double dense_scale = 1.0;                                // objScale_dualvar's factor on those C
     // K > 1: all cones as one block-diagonal row space (global rows and columns); used by
     // the split iteration when every cone has the same (G, E) row layout
     DevCone merged;
@@ -164,6 +169,9 @@ struct DevProblem {
 struct DevWork {
     double *R = nullptr, *D = nullptr, *G[2] = {nullptr, nullptr};
     double *R2 = nullptr;      // second factor buffer of the split iteration (R double-buffered)
+    // dense-objective cones (DevCone::Cd): C R of the current iterate (carried C R + tau C D
+    // through the inner loop, recomputed by op_grad) and C D of the iteration; zero elsewhere
+    double *CR = nullptr, *CD = nullptr;
     double *ls[2] = {nullptr, nullptr}, *ly[2] = {nullptr, nullptr};
     double *U = nullptr, *V = nullptr, *X = nullptr;         // ADMM / scratch factors
     double *cg_r = nullptr, *cg_p = nullptr, *cg_Q = nullptr, *cg_b = nullptr, *M2 = nullptr;
@@ -227,6 +235,17 @@ int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y,
                 double *gram, int *nblk_used, hipStream_t st, bool reduce = true);
 // sustained v_mfma_f64_16x16x4f64 rate: every CU, 2 waves a SIMD, 8 accumulators a wave
 int mfma_f64_peak(hipStream_t st, double *tflops);
+// dense objective of cone `cone` (DevCone::Cd): Y = scale C X + beta Y on the cone's rows
+// (X, Y full factor buffers; columns r..ld of Y written 0)
+int launch_dense_cx(const DevProblem &P, int cone, const double *X, double *Y, double beta, hipStream_t st);
+// ALM iteration, between stage A and B: CD = scale C D of every dense cone, and the partials
+// <R, CD>, <D, CD> (slots 0, 1 of 8) of stage A's objective terms at partial offset `off`
+// (R: the current iterate by the control block); returns the partial blocks written
+int dense_cd_blocks(const DevProblem &P);
+int launch_dense_cd(const DevProblem &P, const DevWork &W, const double *ctrl, int off, hipStream_t st);
+// Lanczos step add-on: y_j += scale C q_j (dense cone)
+int launch_lanczos_dense(const DevProblem &P, int cone, double *Q, long ldq, double *w0, double *w1, const int *jp,
+                         hipStream_t st);
 
 // ---- fused ALM inner iteration (device-side control; see lrs_kernels.hip) ----
 struct AlmIterArgs {

@@ -1692,7 +1692,7 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_
     const double *__restrict__ b, double *__restrict__ cvs, const double *__restrict__ par,
     const double *__restrict__ ctrl, const double *__restrict__ partA, int nblkA, const double *__restrict__ partB,
     int nblkB, double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int T, int row0,
-    int nall, int pstr, double *hmirror, double seq) {
+    int nall, int pstr, double *hmirror, double seq, double *CRb, const double *__restrict__ CDb) {
     __shared__ double gsh[kRowBlock * E];   // team reduction of the row gradient (T > 1)
     __shared__ double red[12];
     __shared__ double ls[LS_N];
@@ -1885,6 +1885,18 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_
         double sv[E], yv[E], go[E];
         if constexpr (MODE == 2) ld_row<E>(D + oi, di);
         ld_row<E>(Gold + oi, go);
+        if (CRb) {
+            // dense objective: C R_new = C R + tau C D (carried), S R_new += C R_new
+            double cr[E], cd[E];
+            ld_row<E>(CRb + foff + oi, cr);
+            ld_row<E>(CDb + foff + oi, cd);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                cr[e] += tau * cd[e];
+                g[e] += cr[e];
+            }
+            st_row<E>(CRb + foff + oi, cr);
+        }
 #pragma unroll
         for (int e = 0; e < E; ++e) g[e] *= 2.0;
 #pragma unroll
@@ -3081,6 +3093,7 @@ int launch_lanczos_step(const DevProblem &P, int cone, const double *S, int kmax
                            w1, bw2, jp, Q, ldq);
     }
     LRS_CHECK_LAUNCH();
+    if (c.dense_c && launch_lanczos_dense(P, cone, Q, ldq, w0, w1, jp, st)) return -1;
     const int nb = std::max(1, std::min(64, (n + kBlock * 8 - 1) / (kBlock * 8)));
     double *gpart = part + kMaxPartialBlocks;   // past the norm partials
     for (int t = 0; t < 2; ++t) {
@@ -3090,6 +3103,34 @@ int launch_lanczos_step(const DevProblem &P, int cone, const double *S, int kmax
                            Q, ldq, w0, w1, jp, gpart, nb, t, al, part, ticket_ptr(T_DOT), bw2);
         LRS_CHECK_LAUNCH();
     }
+    return 0;
+}
+
+// Lanczos step on a dense-objective cone: y_j += scale C q_j after k_lz_symv (one wave per row)
+__global__ void __launch_bounds__(kBlock) k_lz_dense(int n, double scale, const double *__restrict__ Cd, double *Q,
+                                                     long ldq, double *w0, double *w1, const int *__restrict__ jp) {
+    const int j = *jp;
+    const double *w;
+    double *y;
+    lz_bufs(j, Q, w0, w1, &w, &y);
+    const double *__restrict__ qj = Q + (long)j * ldq;
+    const int lane = threadIdx.x & 63;
+    const int nw = gridDim.x * (kBlock / 64);
+    for (int i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < n; i += nw) {
+        const double *__restrict__ ci = Cd + (long)i * n;
+        double t = 0.0;
+        for (int k = lane; k < n; k += 64) t += ci[k] * qj[k];
+        t = wave_sum(t);
+        if (lane == 0) y[i] += scale * t;
+    }
+}
+int launch_lanczos_dense(const DevProblem &P, int cone, double *Q, long ldq, double *w0, double *w1, const int *jp,
+                         hipStream_t st) {
+    const DevCone &c = P.cones[cone];
+    if (!c.dense_c) return 0;
+    const int grid = std::max(1, std::min(2048, (c.n + kBlock / 64 - 1) / (kBlock / 64)));
+    hipLaunchKernelGGL(k_lz_dense, dim3(grid), dim3(kBlock), 0, st, c.n, P.dense_scale, c.Cd, Q, ldq, w0, w1, jp);
+    LRS_CHECK_LAUNCH();
     return 0;
 }
 
@@ -3567,6 +3608,133 @@ int mfma_f64_peak(hipStream_t st, double *tflops) {
     return 0;
 }
 
+// ---- dense objective on the FP64 matrix cores.  The reference's dense
+// branches form sym(U V^T) in full (fds_syr2k, LORADSUVt lorads_alg_common.c:72-89) and multiply
+// by a packed C (dataMatDenseMultiRkMat lorads_sdp_data.c:948-973); here C stays a full n x n
+// row-major matrix and every C-term is a product with it: <C, sym R D^T> = <R, C D>,
+// <C, D D^T> = <D, C D>, S R = (C + A^*(M1)) R = C R + A^*(M1) R.
+// k_cgemm: Y = scale C X (+ beta Y) on the rows of one cone, X / Y row-major n x ld.  Output
+// tiles of kCgBM rows x kCgBN columns, four waves as 2 x 2, a wave 16 rows x 32 columns (two
+// v_mfma_f64_16x16x4f64 accumulators); C and X staged through double-buffered LDS tiles of
+// kCgBK k-rows, the next tile's global loads issued before the current tile's MFMAs.  With
+// `ctrl` (the ALM iteration): nothing when the iteration is inactive, X = D, and the block's
+// partials <R, Y>, <X, Y> (R the current iterate) in slots 0 and 1 of stage A's 8.
+constexpr int kCgBM = 32, kCgBN = 64, kCgBK = 32, kCgMaxGrid = 1024;
+__global__ void __launch_bounds__(kBlock) k_cgemm(int n, int r, int ld, double scale, const double *__restrict__ Cd,
+                                                  const double *__restrict__ X, double *__restrict__ Y, double beta,
+                                                  const double *__restrict__ ctrl, const double *__restrict__ Rb0,
+                                                  const double *__restrict__ Rb1, double *__restrict__ part, int poff) {
+    __shared__ double Cs[2][kCgBM][kCgBK + 1];
+    __shared__ double Xs[2][kCgBK][kCgBN + 1];
+    const double *__restrict__ R = nullptr;
+    if (ctrl) {
+        if (ctrl[C_ACTIVE] == 0.0) return;   // grid-uniform
+        R = ctrl[C_RCUR] == 0.0 ? Rb0 : Rb1;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+    const int ntm = (n + kCgBM - 1) / kCgBM, ntn = (r + kCgBN - 1) / kCgBN;
+    const int nk = (n + kCgBK - 1) / kCgBK;
+    // staging maps: C tile row t >> 3, k (t & 7) * 4 .. +3; X tile k-row t >> 3, columns (t & 7) * 8 .. +7
+    const int crow = threadIdx.x >> 3, ck = (threadIdx.x & 7) * 4;
+    const int xrow = threadIdx.x >> 3, xc = (threadIdx.x & 7) * 8;
+    double dots[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int tile = blockIdx.x; tile < ntm * ntn; tile += gridDim.x) {
+        const int m0 = (tile / ntn) * kCgBM, n0 = (tile % ntn) * kCgBN;
+        gram_acc_t acc[2] = {gram_acc_t{0.0, 0.0, 0.0, 0.0}, gram_acc_t{0.0, 0.0, 0.0, 0.0}};
+        double cr[4], xr[8];
+        auto gload = [&](int k0) {
+            const int gi = m0 + crow;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int gk = k0 + ck + t;
+                cr[t] = (gi < n && gk < n) ? Cd[(long)gi * n + gk] : 0.0;
+            }
+            const int gk = k0 + xrow;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int col = n0 + xc + t;
+                xr[t] = (gk < n && col < r) ? X[(long)gk * ld + col] : 0.0;
+            }
+        };
+        auto sstore = [&](int buf) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) Cs[buf][crow][ck + t] = cr[t];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) Xs[buf][xrow][xc + t] = xr[t];
+        };
+        gload(0);
+        sstore(0);
+        __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = kt & 1;
+            if (kt + 1 < nk) gload((kt + 1) * kCgBK);
+#pragma unroll
+            for (int ks = 0; ks < kCgBK / 4; ++ks) {
+                const double a = Cs[cur][wm * 16 + (lane & 15)][ks * 4 + (lane >> 4)];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const double b = Xs[cur][ks * 4 + (lane >> 4)][wn * 32 + t * 16 + (lane & 15)];
+                    acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
+                }
+            }
+            if (kt + 1 < nk) sstore(cur ^ 1);
+            __syncthreads();
+        }
+        // D fragment: col = lane & 15, row = (lane >> 4) + 4 q
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = m0 + wm * 16 + (lane >> 4) + 4 * q;
+                const int col = n0 + wn * 32 + t * 16 + (lane & 15);
+                if (row < n && col < r) {
+                    const long o = (long)row * ld + col;
+                    double v = scale * acc[t][q];
+                    if (beta != 0.0) v += beta * Y[o];
+                    Y[o] = v;
+                    if (R) {
+                        dots[0] += R[o] * v;
+                        dots[1] += X[o] * v;
+                    }
+                }
+            }
+    }
+    if (part) write_partials<8, kBlock>(dots, part, poff + blockIdx.x);
+}
+static int cgemm_grid(const DevCone &c) {
+    const long tiles = (long)((c.n + kCgBM - 1) / kCgBM) * ((c.r + kCgBN - 1) / kCgBN);
+    return (int)std::max(1L, std::min((long)kCgMaxGrid, tiles));
+}
+int launch_dense_cx(const DevProblem &P, int cone, const double *X, double *Y, double beta, hipStream_t st) {
+    const DevCone &c = P.cones[cone];
+    if (!c.dense_c) return 0;
+    if (c.nown != c.n) {
+        snprintf(g_err, sizeof(g_err), "dense objective: sharded cones are not supported");
+        return -1;
+    }
+    hipLaunchKernelGGL(k_cgemm, dim3(cgemm_grid(c)), dim3(kBlock), 0, st, c.n, c.r, c.ld, P.dense_scale, c.Cd,
+                       X + c.foff, Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+int dense_cd_blocks(const DevProblem &P) {
+    int nb = 0;
+    for (const DevCone &c : P.cones)
+        if (c.dense_c) nb += cgemm_grid(c);
+    return nb;
+}
+int launch_dense_cd(const DevProblem &P, const DevWork &W, const double *ctrl, int off, hipStream_t st) {
+    for (const DevCone &c : P.cones) {
+        if (!c.dense_c) continue;
+        const int grid = cgemm_grid(c);
+        hipLaunchKernelGGL(k_cgemm, dim3(grid), dim3(kBlock), 0, st, c.n, c.r, c.ld, P.dense_scale, c.Cd, W.D + c.foff,
+                           W.CD + c.foff, 0.0, ctrl, W.R + c.foff, W.R2 + c.foff, W.part, off);
+        LRS_CHECK_LAUNCH();
+        off += grid;
+    }
+    return 0;
+}
+
 // register blocking of the Gram: NB x NB tiles per wave (16 NB columns a side)
 static int gram_nb(int r) { return r > 16 ? 2 : 1; }
 static long gram_subtiles(int r, int nb) {
@@ -3883,7 +4051,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                          : std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
     // latency regime: every launch of both stages on the k_lat kernels, or none
     LatPlan lg[kMaxCones];
-    bool lat = !sh && !split && !P.no_lat;
+    bool lat = !sh && !split && !P.no_lat && !P.ndense;   // the latency kernels carry no dense objective
     int nla = 0, nlb = 0, nlf = 0;
     for (int k = 0; k < KL && lat; ++k) {
         lg[k] = lat_plan(cone_of(k), pa[k], pb[k]);
@@ -3894,6 +4062,19 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     }
     if (lat && (nla > kLatMaxPartials || nlb + nlf > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials)))
         lat = false;
+    // dense-objective cones: C D and its two objective partials after stage A's blocks
+    const int offCD = nblkA, ngd = P.ndense ? dense_cd_blocks(P) : 0;
+    if (ngd) {
+        if (sh) {
+            snprintf(g_err, sizeof(g_err), "dense objective: sharded solves are not supported");
+            return -1;
+        }
+        nblkA += ngd;
+        if (nblkA > kMaxPartialBlocks) {
+            snprintf(g_err, sizeof(g_err), "dense objective: %d partial blocks past %d", nblkA, kMaxPartialBlocks);
+            return -1;
+        }
+    }
     P.last_path = lat ? 0 : 1;
     if (lat) {
         nblkA = nla;
@@ -3970,6 +4151,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         off += grid;
     }
 #undef LRS_LAUNCH_A
+    if (ngd && (mask & 1) && launch_dense_cd(P, W, ctrl_cur, offCD, st)) return -1;
     if (sh && (mask & 1)) {
         hipLaunchKernelGGL(k_fold_partials<8>, dim3(1), dim3(kBlock), 0, st, W.part, nblkA, totA);
         LRS_CHECK_LAUNCH();
@@ -4021,7 +4203,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, inA, nA,            \
                        sh ? totB : W.partB, P.mg > 0 ? (sh ? 1 : gg) : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, \
                        c.n, pstr,                                                                                 \
-                       (MM) != 2 && k == 0 ? a.hmirror : nullptr, a.seq)
+                       (MM) != 2 && k == 0 ? a.hmirror : nullptr, a.seq, P.ndense ? W.CR : nullptr, W.CD)
         const bool small = pb[k].small;
         if (lat) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {

@@ -146,10 +146,22 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
             else
                 me.push_back(raw[e]);
         }
+        // dense objective: C out of the pattern, into a full matrix (lrs_problem.h policy)
+        long ncobj = 0;
+        for (auto &e : me) ncobj += e.con == 0 ? 1 : 0;
+        {
+            const char *ev = getenv("LRS_DENSE_C");
+            const long tri = (long)c.n * (c.n + 1) / 2;
+            if (ev && ev[0] == '0') c.dense_c = false;
+            else if (ev && ev[0] == '1') c.dense_c = ncobj > 0;
+            else c.dense_c = c.n >= kDenseCMinN && 4 * ncobj >= tri;
+        }
+        if (c.dense_c) c.Cfull.assign((size_t)c.n * c.n, 0.0);
         // pattern = unique (row,col), row-major
         std::vector<std::pair<int, int>> pr;
         pr.reserve(me.size());
-        for (auto &e : me) pr.push_back({e.row, e.col});
+        for (auto &e : me)
+            if (!(c.dense_c && e.con == 0)) pr.push_back({e.row, e.col});
         std::sort(pr.begin(), pr.end());
         pr.erase(std::unique(pr.begin(), pr.end()), pr.end());
         const int P = (int)pr.size();
@@ -166,12 +178,24 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
         const double fill = 0.1 * (double)((long)c.n * (c.n + 1) / 2);
         for (size_t e = 0; e < me.size(); ++e) {
             const RawEntry &r = me[e];
-            int sl = slot_of(r.row, r.col);
             if (r.con == 0) {
+                // objective norms (sdpSparseConeObjNrm*, data/lorads_sdp_data.c:217-262)
+                const double a = r.v;
+                const bool dg = r.row == r.col;
+                c.cNrm1 += dg ? std::fabs(a) : 2 * std::fabs(a);
+                c.cNrm2sq += dg ? a * a : 2 * a * a;
+                c.cNrmInf = std::max(c.cNrmInf, std::fabs(a));
+                cn++;
+                if (c.dense_c) {
+                    c.Cfull[(size_t)r.row * c.n + r.col] += r.v;
+                    if (!dg) c.Cfull[(size_t)r.col * c.n + r.row] += r.v;
+                    continue;
+                }
+                const int sl = slot_of(r.row, r.col);
                 c.Craw[sl] += r.v;
                 c.Chas[sl] = 1;
-                cn++;
             } else {
+                const int sl = slot_of(r.row, r.col);
                 c.ent.push_back({r.con - 1, sl, r.v, r.row == r.col});
                 if (r.con != lastCon) {
                     if (lastCon > 0 && cnt > fill) c.denseCoeff = true;
@@ -184,15 +208,6 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
         }
         if (lastCon > 0 && cnt > fill) c.denseCoeff = true;
         if ((double)cn > fill) c.denseCoeff = true;
-        // objective norms (sdpSparseConeObjNrm*, data/lorads_sdp_data.c:217-262)
-        for (int t = 0; t < P; ++t) {
-            if (!c.Chas[t]) continue;
-            double a = c.Craw[t];
-            bool dg = c.prow[t] == c.pcol[t];
-            c.cNrm1 += dg ? std::fabs(a) : 2 * std::fabs(a);
-            c.cNrm2sq += dg ? a * a : 2 * a * a;
-            c.cNrmInf = std::max(c.cNrmInf, std::fabs(a));
-        }
         // symmetric adjacency, columns ascending per row; lower prefix = col <= row
         std::vector<int> deg(c.n, 0);
         for (int t = 0; t < P; ++t) {
@@ -280,6 +295,8 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
     }
     for (int k = 0; k < K; ++k)
         if (g.cones[k].n < world) { err = "sharded solve: a cone has fewer rows than shards"; return false; }
+    for (int k = 0; k < K; ++k)
+        if (g.cones[k].dense_c) { err = "sharded solve: dense-objective cones are not supported"; return false; }
     plan = ShardPlan();
     plan.world = world; plan.rank = rank;
     plan.cones.assign(K, ShardConePlan());
@@ -431,6 +448,8 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
     dp.m = hp.m;
     dp.K = hp.K;
     dp.cones.assign(hp.K, DevCone());
+    dp.ndense = 0;
+    dp.dense_scale = 1.0;
     int Ptot = 0;
     for (int k = 0; k < hp.K; ++k) { dp.cones[k].slot_off = Ptot; dp.cones[k].P = (int)hp.cones[k].prow.size(); Ptot += dp.cones[k].P; }
     dp.Ptot = Ptot;
@@ -643,6 +662,11 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         if (!dput(&d.adj_ptr, c.adj_ptr, err) || !dput(&d.adj_low, c.adj_low, err) ||
             !dput(&d.adj_col, c.adj_col, err) || !dput(&d.adj_slot, adj_slot_g, err))
             return false;
+        if (c.dense_c) {
+            if (!dput(&d.Cd, c.Cfull, err)) return false;
+            d.dense_c = 1;
+            dp.ndense++;
+        }
     }
     return true;
 }
@@ -653,7 +677,7 @@ void free_problem(DevProblem &dp) {
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
-    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); }
+    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);

@@ -26,7 +26,14 @@ struct HostCone {
     std::vector<HostEntry> ent;          // constraint entries sorted by (con, slot)
     std::vector<int> adj_ptr, adj_low, adj_col, adj_slot;   // symmetric adjacency
     double cNrm1 = 0, cNrm2sq = 0, cNrmInf = 0;
+    // dense objective: C kept as a full n x n row-major matrix for the
+    // FP64 matrix cores, out of the slot pattern (which then holds the constraints only)
+    bool dense_c = false;
+    std::vector<double> Cfull;
 };
+// Dense-objective policy: LRS_DENSE_C=0 never, =1 every cone with objective entries, unset:
+// cones with n >= kDenseCMinN whose C fills >= 1/4 of the lower triangle.
+constexpr int kDenseCMinN = 2048;
 
 struct HostProblem {
     int m = 0, K = 0, nLp = 0;

@@ -424,7 +424,7 @@ static void free_work(lrs_ctx *c) {
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
                       W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2,
-                      W.cgc, W.tot, W.gl};
+                      W.cgc, W.tot, W.gl, W.CR, W.CD};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     c->W = DevWork();
@@ -441,8 +441,9 @@ static int zero_work(lrs_ctx *c) {
         {W.U, NR}, {W.V, NR}, {W.X, NR}, {W.cg_r, NR}, {W.cg_p, NR}, {W.cg_Q, NR}, {W.cg_b, NR}, {W.M2, NR},
         {W.R2, NR}, {W.uvt0, Pt}, {W.uvt1, Pt}, {W.uvt2, Pt}, {W.S, Pt}, {W.lam, m}, {W.cvs, m}, {W.q1, m},
         {W.q2, m}, {W.M1, m}, {W.wtmp, m}, {W.cvc, (long)m * std::max(1, P.K)}, {W.ctrl, 2 * C_NCTRL},
-        {W.lsres, 2 * LS_N}, {W.rec, 4L * m}, {W.tot, 32}};
-    for (auto &z : zs) HIPC(hipMemsetAsync(z.p, 0, sizeof(double) * z.n, c->st));
+        {W.lsres, 2 * LS_N}, {W.rec, 4L * m}, {W.tot, 32}, {W.CR, W.CR ? NR : 0}, {W.CD, W.CD ? NR : 0}};
+    for (auto &z : zs)
+        if (z.p) HIPC(hipMemsetAsync(z.p, 0, sizeof(double) * z.n, c->st));
     c->head = 0; c->gcur = 0;
     c->beta[0] = c->beta[1] = c->yy[0] = c->yy[1] = 0;
     return 0;
@@ -494,6 +495,7 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         if (A(&W.gl, gl)) return -1;
         W.gl_len = gl;
     }
+    if (P.ndense && (A(&W.CR, NR) || A(&W.CD, NR))) return -1;
     HIPC(hipStreamSynchronize(c->st));
     c->walloc = true;
     c->head = 0; c->gcur = 0;
@@ -590,6 +592,7 @@ static int read_tmpfin2(lrs_ctx *c, int idx1, int n1, int idx2, int n2, double *
 // ------------------------------------------------------------------------
 // host-driven operators
 // ------------------------------------------------------------------------
+static int op_dot(lrs_ctx *c, long n, const double *x, const double *y, double *out);
 // A(X X^T) for every cone -> cvc[k], cvs = sum_k, returns pinf (primalInfeasibility)
 // and the objective <C, X X^T> (unscaled), with X given per-cone rows in factor buffer.
 // blam != nullptr: also b^T lambda (tmpfin TF_DOT), read behind the same sync
@@ -628,6 +631,15 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
     if (read_tmpfin2(c, TF_SD, 2 * P.K, TF_GATHER, 3, t)) return -1;   // GATHER, RESID, DOT
     double o = 0.0;
     for (int k = 0; k < P.K; ++k) o += t[2 * k];
+    // dense objective: <C, sym X Y^T> = <X, C Y>
+    for (int k = 0; k < P.K && obj; ++k) {
+        const DevCone &dc = P.cones[k];
+        if (!dc.dense_c) continue;
+        OPC(launch_dense_cx(P, k, Y ? Y : X, W.CD, 0.0, c->st));
+        double v;
+        if (op_dot(c, (long)dc.n * dc.ld, X + dc.foff, W.CD + dc.foff, &v)) return -1;
+        o += v;
+    }
     if (pinf) *pinf = std::sqrt(t[2 * P.K + (fin - TF_GATHER)]) / (1 + c->hp.bNrm1);
     if (blam) *blam = t[2 * P.K + (TF_DOT - TF_GATHER)];
     if (obj) *obj = o;
@@ -644,6 +656,15 @@ static int op_grad(lrs_ctx *c, double rho, double *lag) {
         OPC(launch_spmm(P, k, W.S, W.R, 2.0, nullptr, 0.0, W.G[c->gcur], W.part, 0, nullptr, c->st));
     double v[TF_N - TF_SPMM];
     if (read_tmpfin2(c, TF_SPMM, P.K, 0, 0, v)) return -1;
+    // dense objective: C R (the inner loop carries it), G += 2 C R, ||G||^2 anew
+    for (int k = 0; k < P.K; ++k) {
+        const DevCone &dc = P.cones[k];
+        if (!dc.dense_c) continue;
+        double *Gk = W.G[c->gcur] + dc.foff;
+        OPC(launch_dense_cx(P, k, W.R, W.CR, 0.0, c->st));
+        OPC(launch_axpby((long)dc.n * dc.ld, 2.0, W.CR + dc.foff, 1.0, Gk, c->st));
+        if (op_dot(c, (long)dc.n * dc.ld, Gk, Gk, &v[k])) return -1;
+    }
     double tot = 0.0;
     for (int k = 0; k < P.K; ++k) {
         double nrm = std::sqrt(v[k]);
@@ -1637,6 +1658,7 @@ static int update_var_one(lrs_ctx *c, int k, double *X, const double *Y, double 
     OPC(launch_admm_m1(P.m, rho, P.b, W.cvs, W.cvc + (long)k * P.m, W.lam, W.M1, c->st));
     OPC(launch_wsum(P, W.M1, 1, W.S, c->st));
     OPC(launch_spmm(P, k, W.S, Y, 1.0, Y, -rho, W.M2, nullptr, 0, nullptr, c->st));   // M2 = S Y - rho Y
+    OPC(launch_dense_cx(P, k, Y, W.M2, 1.0, c->st));                                     // + C Y (dense objective)
     OPC(launch_axpby((long)d.n * d.ld, -1.0 / rho, W.M2 + d.foff, 0.0, W.cg_b + d.foff, c->st));
     if (cg_solve(c, k, Y, X, W.cg_b, tol, maxit)) return -1;
     c->cgIterTotal += c->cgIterCone[k];
@@ -1916,6 +1938,7 @@ static int obj_scale(lrs_ctx *c, double f) {
         c->c_scaled = true;
     }
     c->scaleObjHis *= f;
+    P.dense_scale *= f;   // dense-objective cones: the factor rides on every product with C
     OPC(launch_axpby(Pt, 0.0, P.Cw, f, P.Cw, c->st));
     OPC(launch_axpby(Pt, 0.0, P.Craw, f, P.Craw, c->st));
     OPC(launch_axpby(P.m, 0.0, c->W.lam, f, c->W.lam, c->st));
@@ -1928,6 +1951,7 @@ static int obj_unscale(lrs_ctx *c) {
     HIPC(hipMemcpyAsync(P.Cw, c->Cw0, sizeof(double) * Pt, hipMemcpyDeviceToDevice, c->st));
     HIPC(hipMemcpyAsync(P.Craw, c->Craw0, sizeof(double) * Pt, hipMemcpyDeviceToDevice, c->st));
     HIPC(hipStreamSynchronize(c->st));
+    P.dense_scale = 1.0;
     c->c_scaled = false;
     return 0;
 }
@@ -2017,6 +2041,7 @@ int lrs_set_kernel_path(lrs_ctx *c, int path) {
         set_err("kernel path %d: expected 0 (auto), 1 (general), 2 (general, bandwidth regime) or 3 (+ long-row kernels)", path);
         return -1;
     }
+    if (c->dp.ndense && path == 3) path = 2;   // the long-row kernels carry no dense objective
     if (c->dp.no_lat != path) {
         drop_graphs(c);   // captured batches hold the previous kernels
         c->dp.no_lat = path;
@@ -2691,6 +2716,29 @@ int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {
 // Standalone r x r Gram of cone `cone` on R (one k_gram launch: MFMA tiles + the
 // last-arriving chunk's fixed-order reduction): reps back to back between two HIP events.
 // Both outputs are that launch's average (the reduction is no longer a second kernel).
+int lrs_time_dense(lrs_ctx *c, int cone, int reps, double *avg_ms) {
+    if (!c || !avg_ms) { set_err("time_dense: null argument"); return -1; }
+    bind(c);
+    if (!c->walloc || cone < 0 || cone >= c->dp.K || !c->dp.cones[cone].dense_c) {
+        set_err("time_dense: cone %d has no dense objective (or no ranks set)", cone);
+        return -1;
+    }
+    hipEvent_t e0, e1;
+    HIPC(hipEventCreate(&e0));
+    HIPC(hipEventCreate(&e1));
+    OPC(launch_dense_cx(c->dp, cone, c->W.R, c->W.CD, 0.0, c->st));
+    HIPC(hipEventRecord(e0, c->st));
+    for (int q = 0; q < reps; ++q) OPC(launch_dense_cx(c->dp, cone, c->W.R, c->W.CD, 0.0, c->st));
+    HIPC(hipEventRecord(e1, c->st));
+    HIPC(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPC(hipEventElapsedTime(&ms, e0, e1));
+    *avg_ms = ms / std::max(1, reps);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 0;
+}
+
 int lrs_mfma_f64_peak(lrs_ctx *c, double *tflops) {
     if (!c || !tflops) { set_err("mfma_f64_peak: null argument"); return -1; }
     bind(c);

@@ -118,6 +118,7 @@ def load_library(path=None):
         "lrs_auut_bytes": (C.c_int, [vp, dp]),
         "lrs_time_gram": (C.c_int, [vp, C.c_int, C.c_int, dp, dp]),
         "lrs_mfma_f64_peak": (C.c_int, [vp, dp]),
+        "lrs_time_dense": (C.c_int, [vp, C.c_int, C.c_int, dp]),
         "lrs_load_coo": (C.c_int, [vp, C.c_int, C.c_int, ip, dp, C.c_long, ip, ip, ip, ip, dp]),
         "lrs_debug_phase_times": (C.c_int, [vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
         "lrs_comm_unique_id": (C.c_int, [C.c_char_p]),
@@ -478,6 +479,12 @@ class Solver:
         ms, kms = C.c_double(), C.c_double()
         self._check(self.lib.lrs_time_gram(self.ctx, cone, reps, C.byref(ms), C.byref(kms)), "time_gram")
         return ms.value, kms.value
+
+    def time_dense(self, cone=0, reps=10):
+        """ms per dense-objective product C R of `cone` on the matrix cores (lrs_time_dense)."""
+        t = C.c_double()
+        self._check(self.lib.lrs_time_dense(self.ctx, cone, reps, C.byref(t)), "time_dense")
+        return t.value
 
     def mfma_f64_peak(self):
         """Measured FP64 matrix-core TFLOP/s of this device (lrs_mfma_f64_peak)."""

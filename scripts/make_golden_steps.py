@@ -40,7 +40,11 @@ CASES = [
     ("checker_1.5", os.path.join(ROOT, "data", "bundled", "checker_1.5.dat-s"), -1, [1, 3, 5]),
     # rank 290 > 256 (the 64 x 8 layout): the n x r arrays stored as n x 4 projections R @ Omega
     ("mc_rand300w_r290", os.path.join(GOLD, "instances", "mc_rand300w.dat-s"), 290, [1, 2, 3, 5, 8]),
+    # dense objective (C5b structure at test size, the reference's dense branches): the instance is
+    # regenerated from ltr-lowrank-sdp_amd/instances.py random_sparse(300, 3000, 6, 7, dense_c=True)
+    ("rdense300", "gen:rdense300", -1, [1, 2, 3, 4, 5]),
 ]
+GEN = {"rdense300": (300, 3000, 6, 7)}
 PROJ = {"mc_rand300w_r290": 4}
 
 
@@ -84,9 +88,17 @@ def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the reference harness first: make -C oracle -f Makefile.ref")
     only = set(sys.argv[1:])
+    gen_dir = tempfile.TemporaryDirectory()
     for name, path, rank, ks in CASES:
         if only and name not in only:
             continue
+        if path.startswith("gen:"):
+            sys.path.insert(0, ROOT)
+            import importlib
+            inst = importlib.import_module("ltr-lowrank-sdp_amd.instances")
+            path = os.path.join(gen_dir.name, f"{name}.dat-s")
+            n_, m_, k_, seed_ = GEN[name]
+            inst.random_sparse(path, n_, m_, k_, seed_, dense_c=True)
         m, dims = dims_of(path)
         # the reference's rank per cone is only known after presolve: read it back from R's size
         probe = None
