@@ -190,6 +190,56 @@ def config_c5(solver, local, iters=20, cpu_seconds=0.0, cache=None):
             "not run (--no-cpu)"}
 
 
+def config_c5b(solver, local, iters=10, ref_densec=None):
+    """BASELINE config C5b in memory: C5 with C a dense random symmetric matrix (N(0, 1/n) + n I),
+    the dense-objective path (C as a full matrix on the FP64 matrix cores):
+    ALM it/s at r = 128, per-stage times, and the C R product against the MFMA roofline
+    (2 n^2 r flop per launch).  The reference's rate on the same structure at test size
+    (tests/golden/solves_densec.json: its own wall clock over its inner iterations) is quoted
+    beside it, labelled as such: a full-size reference run (n = 10^4, 5*10^7 objective entries
+    through its dense syr2k path) is not a bounded sample."""
+    inst = importlib.import_module(PKG + ".instances")
+    t0 = time.perf_counter()
+    sv = solver.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(10000, 1000000, 6, 5, dense_c=True)),
+                       device=local)
+    load_s = time.perf_counter() - t0
+    kw = dict(fixedRank=128, reoptLevel=0)
+    sv.alm_throughput(0, 2, **kw)
+    o = sv.alm_throughput(0, iters, **kw)
+    st = sv.time_stages(3)
+    dm = sv.time_dense(0, 10)
+    ceil_tf = sv.mfma_f64_peak()
+    sv.close()
+    n, r = 10000, 128
+    fl = 2.0 * n * n * r
+    out = {"workload": "random sparse SDP n=1e4, m=1e6, 6 entries/constraint, dense C (N(0,1/n) + n I), "
+                       "--fixedRank 128 (in memory), dense-objective path",
+           "gpu_it_s": o["done"] / o["seconds"], "load_sec": load_s,
+           "stage_us": [round(x * 1e3, 1) for x in st],
+           "dense_cr": {"kernel": "k_cgemm (v_mfma_f64_16x16x4_f64), C R, n=1e4, r=128", "bound": "mfma",
+                        "avg_launch_us": dm * 1e3, "flop_per_launch": fl, "achieved": fl / (dm * 1e-3) / 1e12,
+                        "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": fl / (dm * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS,
+                        "measured_mfma_f64_tflops": ceil_tf, "frac_of_measured": fl / (dm * 1e-3) / 1e12 / ceil_tf}}
+    if ref_densec:
+        out["reference_test_size"] = ref_densec
+    return out
+
+
+def ref_densec_rates():
+    """The reference's inner-iteration rate on the dense-objective fixtures (its own solves,
+    tests/golden/solves_densec.json; wall clock includes presolve and ADMM, so a lower bound)."""
+    path = os.path.join(ROOT, "tests", "golden", "solves_densec.json")
+    if not os.path.exists(path):
+        return None
+    rows = []
+    for g in json.load(open(path)):
+        rows.append({"instance": g["instance"], "n": g["n"], "m": g["m"], "flags": g["flags"],
+                     "alm_inner": g["result"].get("alm_inner"), "wall_sec": g["wall_sec"],
+                     "it_s_lower_bound": g["result"].get("alm_inner", 0) / g["wall_sec"], "cores": 1})
+    return rows
+
+
 def c5_cpu_sample(solver, local, seconds, cache):
     """The reference's rate on the C5 structure with m = 1e5 (a bounded sample: at m = 1e6 its
     hash-chain presolve alone takes ~1600 s; its iteration cost is the dense
@@ -256,6 +306,7 @@ def main():
     ap.add_argument("--no-north-star", action="store_true")
     ap.add_argument("--no-configs", action="store_true")
     ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--no-c5b", action="store_true")
     ap.add_argument("--no-sharded", action="store_true")
     ap.add_argument("--sharded-timeout", type=float, default=300.0)
     args = ap.parse_args()
@@ -406,6 +457,8 @@ def main():
         line["roofline_at_scale"] = rl
     if rank_id == 0 and world == 1 and not args.no_c5:
         line["config_c5"] = config_c5(solver, local, cpu_seconds=0.0 if args.no_cpu else 20.0, cache=cache)
+    if rank_id == 0 and world == 1 and not args.no_c5b:
+        line["config_c5b"] = config_c5b(solver, local, ref_densec=ref_densec_rates())
     if not args.no_sharded:
         # a watchdog keeps a stuck collective from swallowing the result line
         import threading

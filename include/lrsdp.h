@@ -180,7 +180,7 @@ int lrs_time_gram(lrs_ctx *ctx, int cone, int reps, double *avg_ms, double *gram
  * Diagnostics for the Gram's roofline; no reference counterpart. */
 int lrs_mfma_f64_peak(lrs_ctx *ctx, double *tflops);
 
-/* Dense objective (a cone whose C is kept as a full n x n matrix: LRS_DENSE_C=1, or n >= 2048
+/* Dense objective (a cone whose C is kept as a full n x n matrix: LRS_DENSE_C=1, or n >= 1024
  * with C filling >= 1/4 of the lower triangle): ms per C R product on the FP64 matrix cores
  * (k_cgemm, 2 n^2 r flop), averaged over `reps`.  Fails when the cone has no dense objective. */
 int lrs_time_dense(lrs_ctx *ctx, int cone, int reps, double *avg_ms);

@@ -73,8 +73,8 @@ enum ParIdx {
 // ---- line-search result, double-buffered by parity: tau, rootNum, flag
 enum LsIdx { LS_TAU = 0, LS_ROOTNUM, LS_FLAG, LS_N = 4 };
 // ---- finals of the standalone launchers (g_tmpfin offsets)
-enum TmpFinIdx { TF_SD = 0, TF_GATHER = 128, TF_RESID = 129, TF_DOT = 130, TF_SPMM = 131, TF_N = 256 };
-constexpr int kMaxCones = 64;
+constexpr int kMaxCones = 256;
+enum TmpFinIdx { TF_SD = 0, TF_GATHER = 2 * kMaxCones, TF_RESID, TF_DOT, TF_SPMM, TF_N = TF_SPMM + kMaxCones };
 constexpr int kMaxShards = 64;       // processes of one sharded solve
 constexpr int kLongRow = 32;         // constraint rows longer than this get a wave each
 

@@ -444,7 +444,7 @@ static bool dput(T **dst, const std::vector<T> &v, std::string &err) {
 
 bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
     // per-cone scalars live in the fixed tmpfin slots (TF_SD + 2k < TF_GATHER)
-    if (hp.K > TF_GATHER / 2) { err = "at most 64 SDP cones are supported"; return false; }
+    if (hp.K > kMaxCones) { err = "at most " + std::to_string(kMaxCones) + " SDP cones are supported"; return false; }
     dp.m = hp.m;
     dp.K = hp.K;
     dp.cones.assign(hp.K, DevCone());

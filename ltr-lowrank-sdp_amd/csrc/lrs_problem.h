@@ -32,8 +32,9 @@ struct HostCone {
     std::vector<double> Cfull;
 };
 // Dense-objective policy: LRS_DENSE_C=0 never, =1 every cone with objective entries, unset:
-// cones with n >= kDenseCMinN whose C fills >= 1/4 of the lower triangle.
-constexpr int kDenseCMinN = 2048;
+// cones with n >= kDenseCMinN whose C fills >= 1/4 of the lower triangle (measured: the dense
+// path is 0.86x the slot path at n = 500, 2.2x at n = 2000, scripts/c5b_probe.py).
+constexpr int kDenseCMinN = 1024;
 
 struct HostProblem {
     int m = 0, K = 0, nLp = 0;

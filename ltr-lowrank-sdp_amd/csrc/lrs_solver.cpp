@@ -627,7 +627,7 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
         fin = TF_RESID;
     }
     if (blam) OPC(launch_dot(P.m, P.bprim ? P.bprim : P.b, W.lam, W.part, c->st, nullptr));
-    double t[2 * 64 + 3];
+    double t[2 * kMaxCones + 3];
     if (read_tmpfin2(c, TF_SD, 2 * P.K, TF_GATHER, 3, t)) return -1;   // GATHER, RESID, DOT
     double o = 0.0;
     for (int k = 0; k < P.K; ++k) o += t[2 * k];

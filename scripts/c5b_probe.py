@@ -26,6 +26,8 @@ out = sv.alm_throughput(2, iters, fixedRank=rank, reoptLevel=0)
 print(f"alm {out['done']} it in {out['seconds']:.3f}s = {out['done'] / out['seconds']:.1f} it/s", flush=True)
 ms = sv.time_stages(3)
 print(f"stages us {[round(x * 1e3, 1) for x in ms]}", flush=True)
+if os.environ.get("LRS_DENSE_C") == "0":
+    sys.exit(0)
 dm = sv.time_dense(0, 10)
 fl = 2.0 * n * n * rank
 peak = sv.mfma_f64_peak()

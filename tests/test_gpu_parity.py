@@ -363,9 +363,9 @@ def test_dual_infeasibility_matches_dense_eig(solver_mod, name):
     assert abs(res["dinf"] - l1) <= 1e-8 * max(1.0, l1) + 1e-12
 
 
-def test_more_than_64_cones_rejected(solver_mod, tmp_path):
-    """The per-cone scalars live in fixed device slots (lrs_device.h TmpFinIdx): at most 64
-    SDP cones, refused at load with a message instead of overrunning those slots."""
+def test_more_than_256_cones_rejected(solver_mod, tmp_path):
+    """The per-cone scalars live in fixed device slots (lrs_device.h TmpFinIdx, kMaxCones): at
+    most 256 SDP cones, refused at load with a message instead of overrunning those slots."""
     def write(nb):
         lines = ["1", str(nb), " ".join(["2"] * nb), "1.0"]
         for k in range(1, nb + 1):
@@ -373,11 +373,40 @@ def test_more_than_64_cones_rejected(solver_mod, tmp_path):
         p = tmp_path / f"blocks{nb}.dat-s"
         p.write_text("\n".join(lines) + "\n")
         return str(p)
-    sv = solver_mod.Solver(write(64))
-    assert len(sv.dims) == 64
+    sv = solver_mod.Solver(write(256))
+    assert len(sv.dims) == 256
     sv.close()
-    with pytest.raises(RuntimeError, match="64 SDP cones"):
-        solver_mod.Solver(write(65))
+    with pytest.raises(RuntimeError, match="256 SDP cones"):
+        solver_mod.Solver(write(257))
+
+
+def test_many_cones_stack_is_linear(solver_mod, tmp_path):
+    """K = 100 independent copies of one small Lovasz-theta block (above the old 64-cone cap):
+    the stacked SDP separates, so its optimum is K times the single block's (a size-independent
+    property; both solved to the default tolerances)."""
+    import importlib
+    inst = importlib.import_module("ltr-lowrank-sdp_amd.instances")
+    rng = np.random.default_rng(5)
+    n, ne, K = 10, 15, 100
+    ei, ej = inst._random_edges(rng, n, ne)
+
+    def write(nb):
+        entries, b, con0 = [], [], 1
+        for blk in range(1, nb + 1):
+            entries += inst._theta_entries(n, ei, ej, blk, con0)
+            b += [1.0] + [0.0] * ne
+            con0 += 1 + ne
+        p = str(tmp_path / f"theta_stack{nb}.dat-s")
+        inst.write_sdpa(p, len(b), [n] * nb, np.array(b), entries)
+        return p
+    res = {}
+    for nb in (1, K):
+        sv = solver_mod.Solver(write(nb))
+        res[nb] = sv.solve(reoptLevel=0)
+        sv.close()
+    one, many = res[1], res[K]
+    assert abs(many["pobj"] - K * one["pobj"]) <= 1e-4 * abs(K * one["pobj"]), (many["pobj"], K * one["pobj"])
+    assert abs(many["dobj"] - K * one["dobj"]) <= 1e-4 * abs(K * one["dobj"]), (many["dobj"], K * one["dobj"])
 
 
 def test_dinf_step_cap_flagged(solver_mod, monkeypatch):
