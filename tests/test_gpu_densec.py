@@ -150,3 +150,21 @@ def test_dense_and_slot_paths_agree_on_theta(solver_mod):
     for key in ("pobj", "dobj"):
         assert abs(a[key] - b[key]) <= 2 * width, (key, a[key], b[key], width)
     assert abs(a["dinf"] - b["dinf"]) <= 0.05 * abs(a["dinf"]), (a["dinf"], b["dinf"])
+
+
+def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir):
+    """Past the fixtures' size (n = 2000, m = 100 000, r = 64; the reference's dense branches
+    take minutes per trip here): the dense path and the slot path -- two independent
+    evaluations of the same iteration -- give the same K = 1..3 trips (tau to 1e-9, R_K, G_K
+    to 1e-9)."""
+    path = _rdense(gen_dir, 2000, 100000, 6, 5)
+    out = {}
+    for mode in ("0", "1"):
+        with dense_mode(mode):
+            sv = solver_mod.Solver(path)
+        out[mode] = [sv.alm_steps(K, reoptLevel=0, fixedRank=64) for K in (1, 2, 3)]
+        sv.close()
+    for a, b in zip(out["0"], out["1"]):
+        assert abs(a["tau"] - b["tau"]) <= TOL * abs(a["tau"]), (a["tau"], b["tau"])
+        for key in ("R", "G", "cvs"):
+            assert rel_err(a[key], b[key]) < TOL, (key, rel_err(a[key], b[key]))
