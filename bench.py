@@ -169,8 +169,8 @@ def config_c5(solver, local, iters=20, cpu_seconds=0.0, cache=None):
     sv = solver.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(10000, 1000000, 6, 5)), device=local)
     load_s = time.perf_counter() - t0
     kw = dict(fixedRank=128, reoptLevel=0)
-    sv.alm_throughput(0, 4, **kw)
-    o = sv.alm_throughput(0, iters, **kw)
+    # one solve: warmup trips, then `iters` timed trips of the same solve (no setup inside)
+    o = sv.alm_timed(3, iters, **kw)
     rl = stage_roofline(sv, 3)
     ms, kms = sv.time_gram(0, 20)
     ceil_tf = sv.mfma_f64_peak()
@@ -190,7 +190,7 @@ def config_c5(solver, local, iters=20, cpu_seconds=0.0, cache=None):
             "not run (--no-cpu)"}
 
 
-def config_c5b(solver, local, iters=10, ref_densec=None):
+def config_c5b(solver, local, iters=30, ref_densec=None):
     """BASELINE config C5b in memory: C5 with C a dense random symmetric matrix (N(0, 1/n) + n I),
     the dense-objective path (C as a full matrix on the FP64 matrix cores):
     ALM it/s at r = 128, per-stage times, and the C R product against the MFMA roofline
@@ -204,8 +204,7 @@ def config_c5b(solver, local, iters=10, ref_densec=None):
                        device=local)
     load_s = time.perf_counter() - t0
     kw = dict(fixedRank=128, reoptLevel=0)
-    sv.alm_throughput(0, 2, **kw)
-    o = sv.alm_throughput(0, iters, **kw)
+    o = sv.alm_timed(3, iters, **kw)
     st = sv.time_stages(3)
     dm = sv.time_dense(0, 10)
     ceil_tf = sv.mfma_f64_peak()
@@ -254,8 +253,7 @@ def c5_cpu_sample(solver, local, seconds, cache):
     it, sec, kind = cpu_reference_rate(path, 128, seconds)
     sv = solver.Solver(path, device=local)
     kw = dict(fixedRank=128, reoptLevel=0)
-    sv.alm_throughput(0, 4, **kw)
-    o = sv.alm_throughput(0, 20, **kw)
+    o = sv.alm_timed(3, 20, **kw)
     sv.close()
     gpu = o["done"] / o["seconds"]
     return {"value": it / sec, "unit": "ALM inner iterations/s", "cores": 1, "kind": kind,
@@ -448,7 +446,7 @@ def main():
         big = solver.Solver(coo=inst.coo_arrays(inst.maxcut_torus_problem(2000, 2000, 2000)), device=local)
         load_s = time.perf_counter() - t1
         kwb = dict(fixedRank=16, reoptLevel=0)
-        ob = big.alm_throughput(0, 60, **kwb)
+        ob = big.alm_timed(5, 60, **kwb)
         rl = stage_roofline(big, 20)
         rl["workload"] = "MaxCut torus 2000x2000 (n=m=4e6), --fixedRank 16, in-memory load"
         rl["it_s"] = ob["done"] / ob["seconds"]
