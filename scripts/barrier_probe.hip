@@ -65,6 +65,76 @@ __device__ __forceinline__ bool grid_barrier(unsigned *count, unsigned *gen, uns
     return bad == 0;
 }
 
+// Hierarchical variant ("re-measure a hierarchical, XCD-local grid barrier"): the
+// blocks of group x = blockIdx % 8 (one XCD under the round-robin dispatch; speed only, the
+// protocol does not rely on it) count on their own counter (its own 256-byte line); the last
+// arriver of a group counts on the top counter; the last of those bumps the top generation,
+// which the group leaders wait for and pass on through a per-group generation the group's
+// blocks wait on.  Every spin bounded (err word, early exit).
+template <bool FENCE>
+__device__ __forceinline__ bool wait_gen(unsigned *gen, unsigned g, unsigned *err) {
+    long spins = 0;
+    while (__hip_atomic_load(gen, FENCE ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1L << 24)) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+    return true;
+}
+// FENCE = false: relaxed counters and spins, no release / acquire fences -- the cost of the
+// synchronisation alone (data handed off through it would need sc1 stores and loads instead,
+// cdna_hip_programming G16's valid forms)
+template <bool FENCE>
+__device__ __forceinline__ bool grid_barrier_h(unsigned *bar, unsigned nblk, unsigned *err) {
+    // layout (unsigned words, 64 apart = 256 bytes): [0] top count, [64] top gen,
+    // [128 + 128 x] group count, [192 + 128 x] group gen
+    __syncthreads();
+    __shared__ int bad;
+    if (threadIdx.x == 0) {
+        bad = 0;
+        const unsigned x = blockIdx.x & 7;
+        const unsigned gsz = (nblk - x + 7) / 8;
+        unsigned *gc = bar + 128 + 128 * x, *gg = bar + 192 + 128 * x;
+        unsigned *tc = bar, *tg = bar + 64;
+        const unsigned g0 = __hip_atomic_load(gg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned prev = __hip_atomic_fetch_add(gc, 1u, FENCE ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gsz - 1) {   // group leader: the top level
+            __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned t0 = __hip_atomic_load(tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned ngroups = nblk < 8 ? nblk : 8;
+            const unsigned tp = __hip_atomic_fetch_add(tc, 1u, FENCE ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (tp == ngroups - 1) {
+                __hip_atomic_store(tc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(tg, t0 + 1, FENCE ? __ATOMIC_RELEASE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (!wait_gen<FENCE>(tg, t0, err)) {
+                bad = 1;
+            }
+            __hip_atomic_store(gg, g0 + 1, FENCE ? __ATOMIC_RELEASE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (!wait_gen<FENCE>(gg, g0, err)) {
+            bad = 1;
+        }
+        if (FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    return bad == 0;
+}
+template <bool FENCE>
+__global__ void __launch_bounds__(kThreads) k_persist_h(double *b0, double *b1, int S, int work, unsigned *bar,
+                                                        unsigned *err) {
+    for (int s = 0; s < S; ++s) {
+        const double *in = (s & 1) ? b1 : b0;
+        double *out = (s & 1) ? b0 : b1;
+        stage_body(in, out, blockIdx.x, gridDim.x, s, work);
+        if (!grid_barrier_h<FENCE>(bar, gridDim.x, err)) return;
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    }
+}
+
 __global__ void __launch_bounds__(kThreads) k_persist(double *b0, double *b1, int S, int work, unsigned *bar,
                                                       unsigned *err) {
     for (int s = 0; s < S; ++s) {
@@ -83,11 +153,11 @@ int main(int argc, char **argv) {
     unsigned *bar, *err;
     CK(hipMalloc(&b0, sizeof(double) * kChunk * nblk));
     CK(hipMalloc(&b1, sizeof(double) * kChunk * nblk));
-    CK(hipMalloc(&bar, 64));
+    CK(hipMalloc(&bar, 8192));
     CK(hipMalloc(&err, 64));
     CK(hipMemset(b0, 0, sizeof(double) * kChunk * nblk));
     CK(hipMemset(b1, 0, sizeof(double) * kChunk * nblk));
-    CK(hipMemset(bar, 0, 64));
+    CK(hipMemset(bar, 0, 8192));
     CK(hipMemset(err, 0, 64));
     int dev = 0, coop = 0, per_cu = 0, ncu = 0;
     CK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
@@ -130,7 +200,29 @@ int main(int argc, char **argv) {
         CK(hipGraphExecDestroy(ge));
         CK(hipGraphDestroy(g));
     }
-    // correctness of the barrier: after S stages both paths leave the same data
+    // the persistent forms: S stages in one cooperative launch, flat and hierarchical barriers
+    for (int h = 0; h < 3; ++h)
+        for (int work = 0; work < 2; ++work) {
+            unsigned herr = 0;
+            CK(hipMemset(bar, 0, 8192));
+            CK(hipMemset(err, 0, 64));
+            void *args[] = {&b0, &b1, (void *)&S, &work, &bar, &err};
+            const void *fn = h == 0 ? (const void *)k_persist
+                             : h == 1 ? (const void *)k_persist_h<true> : (const void *)k_persist_h<false>;
+            CK(hipLaunchCooperativeKernel(fn, dim3(nblk), dim3(kThreads), args, 0, st));   // warm
+            CK(hipStreamSynchronize(st));
+            CK(hipEventRecord(e0, st));
+            for (int r = 0; r < reps; ++r) CK(hipLaunchCooperativeKernel(fn, dim3(nblk), dim3(kThreads), args, 0, st));
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            CK(hipMemcpy(&herr, err, sizeof(unsigned), hipMemcpyDeviceToHost));
+            printf("persistent, %s barrier, %s: %.3f us per stage%s\n",
+                   h == 0 ? "flat" : h == 1 ? "hierarchical (8 groups)" : "hierarchical, no fences",
+                   work ? "copy" : "empty", ms * 1e3 / (reps * S), herr ? " (SPIN LIMIT HIT)" : "");
+            if (herr) return 1;
+        }
     printf("done\n");
     return 0;
 }
