@@ -1964,6 +1964,23 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_
 // block barrier, so its latency runs beside the reduction and the serial control instead
 // of after them.  Only the neighbours' factor rows (U at a time) are loaded afterwards.
 // ------------------------------------------------------------------------
+// Row block of latency-kernel block b: the row blocks of group x = b % 8 (one XCD under the
+// round-robin dispatch; speed only, any placement is correct) are the contiguous range
+// [start(x), start(x) + count(x)), so a row's w-apart grid neighbours are read through the same
+// L2 instead of being fetched again by another XCD (a bijection on [0, nrb); slice blocks
+// b >= nrb unchanged).  G67: FETCH_SIZE per dispatch 12.6 -> 7.0 MB (k_lat_a), 7.7 -> 4.6 MB
+// (k_lat_b), 42.4K -> 45.5K it/s (scripts/latxcd_check.sh).  LRS_NO_LAT_XCD: identity map.
+__device__ __forceinline__ int lat_row_block(int b, int nrb) {
+#ifndef LRS_NO_LAT_XCD
+    if (b >= nrb || nrb < 16) return b;
+    const int x = b & 7, q8 = nrb >> 3, rem = nrb & 7;
+    const int start = x * q8 + min(x, rem);
+    return start + (b >> 3);
+#else
+    (void)nrb;
+    return b;
+#endif
+}
 constexpr int kLatRowWaves = kRowBlock / 64 - 1;
 constexpr int kLatRows = kLatRowWaves * 64;      // row-wave threads per block
 constexpr int kLatMaxPartials = 256;             // producer blocks one control wave reduces
@@ -2032,7 +2049,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     // every lane group of the block takes kSliceA consecutive lower entries of one dense row
     // (the rows' own groups skip those entries; A's results are per slot, nothing to combine)
     const bool slice = (int)blockIdx.x >= nrb;
-    int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G, sq = 0;
+    int i = lat_row_block((int)blockIdx.x, nrb) * (kLatRows / G) + (int)threadIdx.x / G, sq = 0;
     if (slice) {
         constexpr int per = (kLatRows / G) * kSliceA;
         int q = (int)blockIdx.x - nrb, L = 0;
@@ -2320,7 +2337,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     // every lane group takes kSliceB consecutive entries of one dense row, the block's partial
     // gradient goes to gl[slice] and k_lat_f finishes the row (its own group skips the entries)
     const bool slice = (int)blockIdx.x >= nrb;
-    int i = blockIdx.x * (kLatRows / G) + (int)threadIdx.x / G, sq = 0;
+    int i = lat_row_block((int)blockIdx.x, nrb) * (kLatRows / G) + (int)threadIdx.x / G, sq = 0;
     if (slice) {
         constexpr int per = (kLatRows / G) * kSliceB;
         int q = (int)blockIdx.x - nrb, Ld = 0;
