@@ -2800,7 +2800,8 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
     const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
-    const double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int row0, int m) {
+    const double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int row0, int m, double *CRb,
+    const double *__restrict__ CDb) {
     if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
     const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
     const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
@@ -2894,6 +2895,18 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
         double di[E], go[E], sv2[E], yv[E];
         ld_row<E>(D + oi, di);
         ld_row<E>(Gold + oi, go);
+        if (CRb) {
+            // dense objective: C R_new = C R + tau C D (carried), S R_new += C R_new (as k_it_b)
+            double cr[E], cd[E];
+            ld_row<E>(CRb + foff + oi, cr);
+            ld_row<E>(CDb + foff + oi, cd);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                cr[e] += tau * cd[e];
+                g[e] += cr[e];
+            }
+            st_row<E>(CRb + foff + oi, cr);
+        }
 #pragma unroll
         for (int e = 0; e < E; ++e) g[e] *= 2.0;
 #pragma unroll
@@ -4269,7 +4282,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
                                    P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr,
                                    P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par,
-                                   ctrl_cur, ls_cur, L, W.partC, off, c.row0, P.m);
+                                   ctrl_cur, ls_cur, L, W.partC, off, c.row0, P.m, P.ndense ? W.CR : nullptr, W.CD);
             });
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_B(kBwU, 2); });

@@ -2041,7 +2041,6 @@ int lrs_set_kernel_path(lrs_ctx *c, int path) {
         set_err("kernel path %d: expected 0 (auto), 1 (general), 2 (general, bandwidth regime) or 3 (+ long-row kernels)", path);
         return -1;
     }
-    if (c->dp.ndense && path == 3) path = 2;   // the long-row kernels carry no dense objective
     if (c->dp.no_lat != path) {
         drop_graphs(c);   // captured batches hold the previous kernels
         c->dp.no_lat = path;

@@ -8,7 +8,8 @@ dataMatDenseMultiRkMat lorads_sdp_data.c:948-973) are the oracle:
 * steps_rdense300.npz (scripts/make_golden_steps.py): K = 1..5 trips of the reference's inner
   loop on a C5b-structured instance (n = 300, m = 3000, dense random C) -- tau, R_K, G_K,
   A(R_K R_K^T), the L-BFGS pair to 1e-9 (the bar of test_gpu_steps), through the dense path
-  (LRS_DENSE_C=1) on kernel paths 1 and 2 and through the slot path (LRS_DENSE_C=0);
+  (LRS_DENSE_C=1) on kernel paths 1, 2 and 3 (the long-row kernels k_wide_a / k_wide_b, which
+  C5b's ~1 200-entry rows take) and through the slot path (LRS_DENSE_C=0);
 * the theta fixtures (C = -J, dense) through the dense path, same bar;
 * solves_densec.json (scripts/make_golden_densec.py): whole reference solves; the ALM objectives
   within 1e-4 relative (the reference's own ALM primal-dual gap on them is 1.4e-5 / 2.3e-5 and the
@@ -92,7 +93,7 @@ def _steps_check(solver_mod, path, z, mode, kpath):
     sv.close()
 
 
-@pytest.mark.parametrize("mode,kpath", [("1", 0), ("1", 1), ("1", 2), ("0", 1)])
+@pytest.mark.parametrize("mode,kpath", [("1", 0), ("1", 1), ("1", 2), ("1", 3), ("0", 1)])
 def test_dense_objective_steps_match_reference(solver_mod, gen_dir, mode, kpath):
     z = np.load(os.path.join(GOLDEN, "steps_rdense300.npz"))
     _steps_check(solver_mod, _rdense(gen_dir, 300, 3000, 6, 7), z, mode, kpath)
@@ -152,7 +153,8 @@ def test_dense_and_slot_paths_agree_on_theta(solver_mod):
     assert abs(a["dinf"] - b["dinf"]) <= 0.05 * abs(a["dinf"]), (a["dinf"], b["dinf"])
 
 
-def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir):
+@pytest.mark.parametrize("kpath", [0, 3])
+def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir, kpath):
     """Past the fixtures' size (n = 2000, m = 100 000, r = 64; the reference's dense branches
     take minutes per trip here): the dense path and the slot path -- two independent
     evaluations of the same iteration -- give the same K = 1..3 trips (tau to 1e-9, R_K, G_K
@@ -162,6 +164,7 @@ def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir):
     for mode in ("0", "1"):
         with dense_mode(mode):
             sv = solver_mod.Solver(path)
+        sv.set_kernel_path(kpath)   # 3: the long-row kernels, C5b's path at full size
         out[mode] = [sv.alm_steps(K, reoptLevel=0, fixedRank=64) for K in (1, 2, 3)]
         sv.close()
     for a, b in zip(out["0"], out["1"]):
