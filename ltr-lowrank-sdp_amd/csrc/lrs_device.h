@@ -104,7 +104,12 @@ struct DevCone {
     // dense objective (lrs_problem.h): C as a full n x n row-major matrix, not in the slots
     int dense_c = 0;
     double *Cd = nullptr;
+    // long rows (>= kTileMinDeg adjacency entries per row on average): per row, the first entry
+    // at or past column x n / kNX, x = 0..kNX ([n][kNX + 1]); the column-tiled k_wide_* kernels
+    int *colseg = nullptr;
 };
+constexpr int kNX = 8;              // column blocks of the tiled long-row kernels (one per XCD)
+constexpr int kTileMinDeg = 32;
 constexpr int kDenseRow = 64;        // entries of a row past which the latency kernels slice it
 constexpr int kSliceMinB = 28;       // fewest entries of one B slice block (G = 64: 7 groups x 4)
 constexpr int kMaxDenseRows = 32;    // more dense rows than this: the general row kernels
@@ -158,6 +163,7 @@ struct DevProblem {
     double *spack = nullptr;                                 // [nsh] one m-vector's shared entries
     std::vector<DevCone> cones;
     int ndense = 0;                                          // cones with a dense objective (DevCone::Cd)
+    bool tiles = false;                                      // column-tiled long-row kernels (LRS_TILES=1 at alloc)
     double dense_scale = 1.0;                                // objScale_dualvar's factor on those C
     // K > 1: all cones as one block-diagonal row space (global rows and columns); used by
     // the split iteration when every cone has the same (G, E) row layout
@@ -172,6 +178,9 @@ struct DevWork {
     // dense-objective cones (DevCone::Cd): C R of the current iterate (carried C R + tau C D
     // through the inner loop, recomputed by op_grad) and C D of the iteration; zero elsewhere
     double *CR = nullptr, *CD = nullptr;
+    // column-tiled long-row kernels: kNX partial S R_new factors (kNX * NRpad), null when no cone
+    // has long rows
+    double *GP = nullptr;
     double *ls[2] = {nullptr, nullptr}, *ly[2] = {nullptr, nullptr};
     double *U = nullptr, *V = nullptr, *X = nullptr;         // ADMM / scratch factors
     double *cg_r = nullptr, *cg_p = nullptr, *cg_Q = nullptr, *cg_b = nullptr, *M2 = nullptr;

@@ -2696,9 +2696,31 @@ __device__ __forceinline__ double bcast_d(double v, int u) {
     else return __shfl(v, (int)(threadIdx.x & 63 & ~(G - 1)) + u, 64);
 }
 
+// Column tiles (TL): the random long-row pattern (C5) reads ~10^3 neighbour rows per row from
+// anywhere in the factor, and a 10 MB factor does not fit one XCD's 4 MB L2, so nearly every
+// gather missed to the Infinity Cache (~12 GB per launch).  TL splits every row's entries by
+// column block x = 0..7 (colseg: the row's first entry at or past column x n / 8) and gives
+// column block x to the blocks of group b % 8 (one XCD under the round-robin dispatch; speed
+// only): an XCD then reads neighbour rows from one n / 8 range of the factor -- 1.25 MB per
+// operand at C5 -- through its own L2, and each row's own operands once per group.  Every
+// entry is still visited once; B's per-row gradient becomes eight column-block partials
+// (GP), summed in block order by k_wide_bf with the row epilogue.
+__device__ __forceinline__ void tile_rows(bool tl, int &grp, int &ngrp, int &xg, int G) {
+    if (tl) {
+        xg = blockIdx.x & (kNX - 1);
+        const int bq = blockIdx.x / kNX, nbq = ((int)gridDim.x - xg + kNX - 1) / kNX;
+        grp = (bq * kRowBlock + (int)threadIdx.x) / G;
+        ngrp = nbq * kRowBlock / G;
+    } else {
+        xg = 0;
+        grp = (blockIdx.x * kRowBlock + (int)threadIdx.x) / G;
+        ngrp = gridDim.x * kRowBlock / G;
+    }
+}
+
 // A, second half (SDDMM sym(RD^T), DD^T on the lower slots, local constraints' q1/q2 and
 // dots), D read back; partials 0..6 as k_it_a MODE 2
-template <int G, int E, int U>
+template <int G, int E, int U, bool TL>
 __global__ void __launch_bounds__(kRowBlock) k_wide_a(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
@@ -2707,21 +2729,26 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_a(
     const int *__restrict__ loc_con, const double *__restrict__ loc_w, const double2 *__restrict__ loc1,
     const double *__restrict__ b, const double *__restrict__ cvs, const double *__restrict__ lam,
     double *__restrict__ rec, const double *__restrict__ par, const double *__restrict__ ctrl_cur,
-    double *__restrict__ partA, int pblk_off, int row0, int m) {
+    double *__restrict__ partA, int pblk_off, int row0, int m, const int *__restrict__ colseg) {
     if (ctrl_cur[C_ACTIVE] == 0.0) return;
     const double *__restrict__ R = (ctrl_cur[C_RCUR] == 0.0 ? Rb0 : Rb1) + foff;
     const double *__restrict__ D = Dall + foff;
     const double rho = par[P_RHO], rhoInv = 1.0 / rho;
     const int lane = threadIdx.x & (G - 1);
-    const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
-    const int ngrp = gridDim.x * kRowBlock / G;
+    int grp, ngrp, xg;
+    tile_rows(TL, grp, ngrp, xg, G);
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = row0 + grp; i < row0 + n; i += ngrp) {
+        int kb = adj_ptr[i], ke = adj_low[i];
+        if constexpr (TL) {
+            kb = max(kb, colseg[(long)i * (kNX + 1) + xg]);
+            ke = min(ke, colseg[(long)i * (kNX + 1) + xg + 1]);
+            if (kb >= ke) continue;   // lane-group uniform
+        }
         const long oi = (long)i * ld + lane * E;
         double xi[E], yi[E];
         ld_row<E>(R + oi, xi);
         ld_row<E>(D + oi, yi);
-        const int kb = adj_ptr[i], ke = adj_low[i];
         const int ispare = min(i, m - 1);
         for (int c0 = kb; c0 < ke; c0 += G) {
             // this lane's entry of the chunk: column, slot, records
@@ -2788,9 +2815,62 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_a(
     write_partials_range<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x, 0, 7);
 }
 
+// row epilogue of stage B: G_new = 2 (S R_new [+ C R_new]), s = tau D, y = G_new - G_old
+// (setlbfgsHisTwo lorads_alm.c:842-863) and the nine L-BFGS dots
+template <int E>
+__device__ __forceinline__ void wide_b_epilogue(double (&g)[E], long oi, long foff, double tau, const double *D,
+                                                const double *Gold, double *Gnew, double *sh, double *yh,
+                                                const double *so, const double *yo, bool two, double *CRb,
+                                                const double *CDb, double (&acc)[10]) {
+    double di[E], go[E], sv2[E], yv[E];
+    ld_row<E>(D + oi, di);
+    ld_row<E>(Gold + oi, go);
+    if (CRb) {
+        // dense objective: C R_new = C R + tau C D (carried), S R_new += C R_new (as k_it_b)
+        double cr[E], cd[E];
+        ld_row<E>(CRb + foff + oi, cr);
+        ld_row<E>(CDb + foff + oi, cd);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            cr[e] += tau * cd[e];
+            g[e] += cr[e];
+        }
+        st_row<E>(CRb + foff + oi, cr);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) g[e] *= 2.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) { sv2[e] = tau * di[e]; yv[e] = g[e] - go[e]; }
+    st_row<E>(Gnew + oi, g);
+    st_row<E>(sh + oi, sv2);
+    st_row<E>(yh + oi, yv);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        acc[0] += g[e] * g[e];
+        acc[1] += yv[e] * sv2[e];
+        acc[2] += yv[e] * yv[e];
+        acc[3] += sv2[e] * g[e];
+        acc[4] += yv[e] * g[e];
+    }
+    if (two) {
+        double sov[E], yov[E];
+        ld_row<E>(so + oi, sov);
+        ld_row<E>(yo + oi, yov);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            acc[5] += sov[e] * g[e];
+            acc[6] += yov[e] * g[e];
+            acc[7] += sov[e] * yv[e];
+            acc[8] += yov[e] * yv[e];
+        }
+    }
+}
+
 // B, second half (adjoint S = C + A^*(M1), G = 2 S R_new, A(R_new R_new^T) on the lower
-// slots, L-BFGS pair, nine dots + residual) over the updated factor; as k_it_b MODE 2
-template <int G, int E, int U>
+// slots, L-BFGS pair, nine dots + residual) over the updated factor; as k_it_b MODE 2.
+// TL: the row's entries of column block b % 8 only; the partial S R_new row goes to
+// GP[x] and k_wide_bf runs the epilogue (partials: the residual only here).
+template <int G, int E, int U, bool TL>
 __global__ void __launch_bounds__(kRowBlock) k_wide_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *Rb0, const double *Rb1,
@@ -2801,7 +2881,7 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
     const double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int row0, int m, double *CRb,
-    const double *__restrict__ CDb) {
+    const double *__restrict__ CDb, const int *__restrict__ colseg, double *__restrict__ GP, long gstride) {
     if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
     const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
     const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
@@ -2815,8 +2895,8 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
     const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
     const bool two = (L == 2);
     const int lane = threadIdx.x & (G - 1);
-    const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
-    const int ngrp = gridDim.x * kRowBlock / G;
+    int grp, ngrp, xg;
+    tile_rows(TL, grp, ngrp, xg, G);
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = row0 + grp; i < row0 + n; i += ngrp) {
         const long oi = (long)i * ld + lane * E;
@@ -2824,7 +2904,12 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
         ld_row<E>(Rn + oi, ri);
 #pragma unroll
         for (int e = 0; e < E; ++e) g[e] = 0.0;
-        const int kb = adj_ptr[i], kl = adj_low[i], ke = adj_ptr[i + 1];
+        int kb = adj_ptr[i], ke = adj_ptr[i + 1];
+        const int kl = adj_low[i];
+        if constexpr (TL) {
+            kb = colseg[(long)i * (kNX + 1) + xg];
+            ke = colseg[(long)i * (kNX + 1) + xg + 1];
+        }
         const int ispare = min(i, m - 1);
         for (int c0 = kb; c0 < ke; c0 += G) {
             // this lane's entry: column, slot, S = C + A^*(M1) on the slot (ALMSetGrad
@@ -2891,49 +2976,46 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
                 }
             }
         }
-        // G_new = 2 S R_new, s = tau D, y = G_new - G_old (setlbfgsHisTwo lorads_alm.c:842-863)
-        double di[E], go[E], sv2[E], yv[E];
-        ld_row<E>(D + oi, di);
-        ld_row<E>(Gold + oi, go);
-        if (CRb) {
-            // dense objective: C R_new = C R + tau C D (carried), S R_new += C R_new (as k_it_b)
-            double cr[E], cd[E];
-            ld_row<E>(CRb + foff + oi, cr);
-            ld_row<E>(CDb + foff + oi, cd);
+        if constexpr (TL) st_row<E>(GP + xg * gstride + foff + oi, g);
+        else wide_b_epilogue<E>(g, oi, foff, tau, D, Gold, Gnew, sh, yh, so, yo, two, CRb, CDb, acc);
+    }
+    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+}
+
+// B, column-tiled: the eight partial S R_new rows summed in block order, then the row epilogue
+template <int G, int E>
+__global__ void __launch_bounds__(kRowBlock) k_wide_bf(int n, int ld, long foff, const double *__restrict__ Dall,
+                                                       double *G0, double *G1, double *s0, double *y0, double *s1,
+                                                       double *y1, const double *__restrict__ ctrl,
+                                                       const double *__restrict__ ls_cur, int L,
+                                                       double *__restrict__ partC, int pblk_off, int row0, double *CRb,
+                                                       const double *__restrict__ CDb, const double *__restrict__ GP,
+                                                       long gstride) {
+    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
+    const double tau = ls_cur[LS_TAU];
+    const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
+    const double *__restrict__ D = Dall + foff;
+    const double *__restrict__ Gold = (gcur == 0 ? G0 : G1) + foff;
+    double *__restrict__ Gnew = (gcur == 0 ? G1 : G0) + foff;
+    double *__restrict__ sh = (h == 0 ? s0 : s1) + foff;
+    double *__restrict__ yh = (h == 0 ? y0 : y1) + foff;
+    const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
+    const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kRowBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kRowBlock / G;
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = row0 + grp; i < row0 + n; i += ngrp) {
+        const long oi = (long)i * ld + lane * E;
+        double g[E], t[E];
+        ld_row<E>(GP + foff + oi, g);
 #pragma unroll
-            for (int e = 0; e < E; ++e) {
-                cr[e] += tau * cd[e];
-                g[e] += cr[e];
-            }
-            st_row<E>(CRb + foff + oi, cr);
+        for (int x = 1; x < kNX; ++x) {
+            ld_row<E>(GP + x * gstride + foff + oi, t);
+#pragma unroll
+            for (int e = 0; e < E; ++e) g[e] += t[e];
         }
-#pragma unroll
-        for (int e = 0; e < E; ++e) g[e] *= 2.0;
-#pragma unroll
-        for (int e = 0; e < E; ++e) { sv2[e] = tau * di[e]; yv[e] = g[e] - go[e]; }
-        st_row<E>(Gnew + oi, g);
-        st_row<E>(sh + oi, sv2);
-        st_row<E>(yh + oi, yv);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            acc[0] += g[e] * g[e];
-            acc[1] += yv[e] * sv2[e];
-            acc[2] += yv[e] * yv[e];
-            acc[3] += sv2[e] * g[e];
-            acc[4] += yv[e] * g[e];
-        }
-        if (two) {
-            double sov[E], yov[E];
-            ld_row<E>(so + oi, sov);
-            ld_row<E>(yo + oi, yov);
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                acc[5] += sov[e] * g[e];
-                acc[6] += yov[e] * g[e];
-                acc[7] += sov[e] * yv[e];
-                acc[8] += yov[e] * yv[e];
-            }
-        }
+        wide_b_epilogue<E>(g, oi, foff, tau, D, Gold, Gnew, sh, yh, so, yo, L == 2, CRb, CDb, acc);
     }
     write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
 }
@@ -4076,6 +4158,22 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         nblkB += pb[k].grid;
         if (!pa[k].small) split = true;
     }
+    // long-row kernels in column tiles (k_wide_a / k_wide_b TL): the cone's column segments and
+    // the partial-gradient buffer exist, one cone per launch, not sharded; B adds k_wide_bf's blocks
+    bool tla[kMaxCones], tlb[kMaxCones];
+    int offBF = nblkB;
+    for (int k = 0; k < KL; ++k) {
+        // measured slower (C5: A 2.05 -> 2.95 ms, B 1.68 -> 2.08 ms) although the Infinity-Cache fetch
+        // drops 16x (A) / 3x (B): off unless LRS_TILES=1
+        const bool can = P.tiles && !merge && !sh && W.GP && cone_of(k).colseg && cone_of(k).nown >= kNX;
+        tla[k] = can && pa[k].wide && pa[k].grid >= kNX;
+        tlb[k] = can && pb[k].wide && pb[k].grid >= kNX;
+        if (tlb[k]) nblkB += pb[k].grid;
+    }
+    if (nblkB > kMaxPartialBlocks) {
+        snprintf(g_err, sizeof(g_err), "stage B: %d partial blocks past %d", nblkB, kMaxPartialBlocks);
+        return -1;
+    }
     const int gwide = P.glob_maxlen >= 32 ? 1 : 0;   // long global constraints: a wave each
     const int gg = gwide ? std::min((std::max(1, P.mg) + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks)
                          : std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
@@ -4127,6 +4225,18 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         }
         return 0;
     };
+#define LRS_WIDE_A(TL_)                                                                                        \
+    hipLaunchKernelGGL((k_wide_a<GG, EE, kWideU, TL_>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,   \
+                       c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.uvt0, W.uvt1, P.loc_ptr,  \
+                       P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam, W.rec,      \
+                       W.par, ctrl_cur, W.part, off, c.row0, P.m, c.colseg)
+#define LRS_WIDE_B(TL_)                                                                                        \
+    hipLaunchKernelGGL((k_wide_b<GG, EE, kWideU, TL_>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,   \
+                       c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], \
+                       W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,                          \
+                       reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,             \
+                       reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur, L, W.partC,   \
+                       off, c.row0, P.m, P.ndense ? W.CR : nullptr, W.CD, c.colseg, W.GP, P.NRpad)
     if (mark(0)) return -1;
     // A: control, direction, sym(RD^T) / DD^T, local constraints' q and dots
     int off = 0;
@@ -4169,10 +4279,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const int grid = pa[k].grid;
         if (pa[k].wide) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                hipLaunchKernelGGL((k_wide_a<GG, EE, kWideU>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,
-                                   c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.uvt0,
-                                   W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1),
-                                   P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, c.row0, P.m);
+
+                if (tla[k]) LRS_WIDE_A(true);
+                else LRS_WIDE_A(false);
             });
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_A(kBwU, 2); });
@@ -4277,12 +4386,17 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         if (pb[k].small) { off += grid; continue; }
         if (pb[k].wide) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                hipLaunchKernelGGL((k_wide_b<GG, EE, kWideU>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,
-                                   c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1],
-                                   W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
-                                   P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr,
-                                   P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par,
-                                   ctrl_cur, ls_cur, L, W.partC, off, c.row0, P.m, P.ndense ? W.CR : nullptr, W.CD);
+
+                if (tlb[k]) {
+                    LRS_WIDE_B(true);
+                    LRS_CHECK_LAUNCH();
+                    hipLaunchKernelGGL((k_wide_bf<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,
+                                       W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], ctrl_cur, ls_cur, L,
+                                       W.partC, offBF, c.row0, P.ndense ? W.CR : nullptr, W.CD, W.GP, P.NRpad);
+                    offBF += grid;
+                } else {
+                    LRS_WIDE_B(false);
+                }
             });
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, { LRS_LAUNCH_B(kBwU, 2); });
@@ -4291,6 +4405,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         off += grid;
     }
 #undef LRS_LAUNCH_B
+#undef LRS_WIDE_A
+#undef LRS_WIDE_B
     if (sh && (mask & 4)) {
         hipLaunchKernelGGL(k_fold_partials<10>, dim3(1), dim3(kBlock), 0, st, W.partC, nblkB, totC);
         LRS_CHECK_LAUNCH();

@@ -662,6 +662,18 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         if (!dput(&d.adj_ptr, c.adj_ptr, err) || !dput(&d.adj_low, c.adj_low, err) ||
             !dput(&d.adj_col, c.adj_col, err) || !dput(&d.adj_slot, adj_slot_g, err))
             return false;
+        if (c.n >= kNX && (long)c.adj_col.size() >= (long)kTileMinDeg * c.n) {
+            std::vector<int> cs((size_t)c.n * (kNX + 1));
+            for (int i = 0; i < c.n; ++i) {
+                int e = c.adj_ptr[i];
+                for (int x = 0; x <= kNX; ++x) {
+                    const int cb = (int)((long)x * c.n / kNX);
+                    while (e < c.adj_ptr[i + 1] && c.adj_col[e] < cb) ++e;
+                    cs[(size_t)i * (kNX + 1) + x] = x == kNX ? c.adj_ptr[i + 1] : e;
+                }
+            }
+            if (!dput(&d.colseg, cs, err)) return false;
+        }
         if (c.dense_c) {
             if (!dput(&d.Cd, c.Cfull, err)) return false;
             d.dense_c = 1;
@@ -677,7 +689,7 @@ void free_problem(DevProblem &dp) {
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
-    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); }
+    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);

@@ -424,7 +424,7 @@ static void free_work(lrs_ctx *c) {
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
                       W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2,
-                      W.cgc, W.tot, W.gl, W.CR, W.CD};
+                      W.cgc, W.tot, W.gl, W.CR, W.CD, W.GP};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     c->W = DevWork();
@@ -496,6 +496,13 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         W.gl_len = gl;
     }
     if (P.ndense && (A(&W.CR, NR) || A(&W.CD, NR))) return -1;
+    {   // column-tiled long-row kernels: the partial S R_new factors
+        bool tiles = false;
+        const char *ev = getenv("LRS_TILES");
+        for (const auto &dc : P.cones) tiles = tiles || (dc.colseg != nullptr && ev && ev[0] == '1');
+        if (tiles && A(&W.GP, (long)kNX * NR)) return -1;
+        P.tiles = tiles;
+    }
     HIPC(hipStreamSynchronize(c->st));
     c->walloc = true;
     c->head = 0; c->gcur = 0;

@@ -153,13 +153,16 @@ def test_dense_and_slot_paths_agree_on_theta(solver_mod):
     assert abs(a["dinf"] - b["dinf"]) <= 0.05 * abs(a["dinf"]), (a["dinf"], b["dinf"])
 
 
-@pytest.mark.parametrize("kpath", [0, 3])
-def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir, kpath):
+@pytest.mark.parametrize("kpath,tiles", [(0, "0"), (3, "0"), (3, "1")])
+def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir, kpath, tiles, monkeypatch):
     """Past the fixtures' size (n = 2000, m = 100 000, r = 64; the reference's dense branches
     take minutes per trip here): the dense path and the slot path -- two independent
     evaluations of the same iteration -- give the same K = 1..3 trips (tau to 1e-9, R_K, G_K
     to 1e-9)."""
     path = _rdense(gen_dir, 2000, 100000, 6, 5)
+    # tiles "1": the column-tiled long-row kernels (LRS_TILES, experimental, read at the
+    # workspace allocation and the first enqueue of the process)
+    monkeypatch.setenv("LRS_TILES", tiles)
     out = {}
     for mode in ("0", "1"):
         with dense_mode(mode):
