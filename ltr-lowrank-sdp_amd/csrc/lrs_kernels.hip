@@ -2323,7 +2323,8 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
     const double *__restrict__ partA, int nblkA, const double *__restrict__ partB, int nblkB,
     double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m, double *hmirror,
-    double seq, int nrb, int ndb, const int *__restrict__ drb, double *__restrict__ gl) {
+    double seq, int nrb, int ndb, const int *__restrict__ drb, double *__restrict__ gl, double *CRb,
+    const double *__restrict__ CDb) {
     __shared__ double red[12];
     __shared__ double ls[LS_N];
     __shared__ double pl[P_NPAR];
@@ -2576,6 +2577,18 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
         if (!slice && !dense) {
             // gradient G_new = 2 S R_new, L-BFGS pair s = tau D, y = G_new - G_old, dots
             double sv2[E], yv[E];
+            if (CRb) {
+                // dense objective: C R_new = C R + tau C D (carried), S R_new += C R_new (as k_it_b)
+                double cr[E], cd[E];
+                ld_row<E>(CRb + foff + oi, cr);
+                ld_row<E>(CDb + foff + oi, cd);
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    cr[e] += tau * cd[e];
+                    g[e] += cr[e];
+                }
+                st_row<E>(CRb + foff + oi, cr);
+            }
 #pragma unroll
             for (int e = 0; e < E; ++e) g[e] *= 2.0;
 #pragma unroll
@@ -2633,7 +2646,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_f(
     int ld, int w, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ drb, int per,
     const double *__restrict__ gl, const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0,
     double *s1, double *y1, const double *__restrict__ ctrl, const double *__restrict__ ls_cur, int L,
-    double *__restrict__ partC, int pblk_off) {
+    double *__restrict__ partC, int pblk_off, double *CRb, const double *__restrict__ CDb) {
     if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
     const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
     const double *__restrict__ D = Dall + foff;
@@ -2656,6 +2669,11 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_f(
         const long oi = (long)i * ld + t;
         double g = 0.0;
         for (int q = 0; q < ns; ++q) g += gl[(long)(sl0 + q) * ld + t];
+        if (CRb) {   // dense objective (as k_lat_b)
+            const double cr = CRb[foff + oi] + tau * CDb[foff + oi];
+            CRb[foff + oi] = cr;
+            g += cr;
+        }
         g *= 2.0;
         const double sv2 = tau * D[oi], yv = g - Gold[oi];
         Gnew[oi] = g;
@@ -4179,7 +4197,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                          : std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
     // latency regime: every launch of both stages on the k_lat kernels, or none
     LatPlan lg[kMaxCones];
-    bool lat = !sh && !split && !P.no_lat && !P.ndense;   // the latency kernels carry no dense objective
+    const int ngd = P.ndense ? dense_cd_blocks(P) : 0;   // dense objective: C D's partial blocks
+    bool lat = !sh && !split && !P.no_lat;
     int nla = 0, nlb = 0, nlf = 0;
     for (int k = 0; k < KL && lat; ++k) {
         lg[k] = lat_plan(cone_of(k), pa[k], pb[k]);
@@ -4188,10 +4207,19 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         nlb += lg[k].nrb + lg[k].sb;
         nlf += lg[k].nf;
     }
-    if (lat && (nla > kLatMaxPartials || nlb + nlf > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials)))
+    if (lat && (nla + ngd > kLatMaxPartials || nlb + nlf > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials)))
         lat = false;
+    P.last_path = lat ? 0 : 1;
+    if (lat) {
+        nblkA = nla;
+        nblkB = nlb + nlf;   // the C partials: B's blocks, then k_lat_f's
+        for (int k = 0; k < KL; ++k) {
+            pa[k].grid = lg[k].nrb + lg[k].sa;
+            pb[k].grid = lg[k].nrb + lg[k].sb;
+        }
+    }
     // dense-objective cones: C D and its two objective partials after stage A's blocks
-    const int offCD = nblkA, ngd = P.ndense ? dense_cd_blocks(P) : 0;
+    const int offCD = nblkA;
     if (ngd) {
         if (sh) {
             snprintf(g_err, sizeof(g_err), "dense objective: sharded solves are not supported");
@@ -4201,15 +4229,6 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         if (nblkA > kMaxPartialBlocks) {
             snprintf(g_err, sizeof(g_err), "dense objective: %d partial blocks past %d", nblkA, kMaxPartialBlocks);
             return -1;
-        }
-    }
-    P.last_path = lat ? 0 : 1;
-    if (lat) {
-        nblkA = nla;
-        nblkB = nlb + nlf;   // the C partials: B's blocks, then k_lat_f's
-        for (int k = 0; k < KL; ++k) {
-            pa[k].grid = lg[k].nrb + lg[k].sa;
-            pb[k].grid = lg[k].nrb + lg[k].sb;
         }
     }
     // what the consumers read: every producer block's partials, or (sharded) the summed totals
@@ -4353,7 +4372,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur,
                                    inA, nA, W.partB, P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, P.m,
                                    k == 0 ? a.hmirror : nullptr, a.seq, lg[k].nrb, (int)c.drb_h.size(), c.drb,
-                                   W.gl + glo);
+                                   W.gl + glo, P.ndense ? W.CR : nullptr, W.CD);
             });
             glo += (long)lg[k].sb * c.ld;
         } else {
@@ -4372,7 +4391,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         if (lg[k].nf > 0) {
             hipLaunchKernelGGL(k_lat_f, dim3(lg[k].nf), dim3(kRowBlock), 0, st, c.ld, c.G * c.E, c.foff, c.adj_ptr,
                                c.drb, (kLatRows / c.G) * kSliceB, W.gl + glo, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
-                               W.ls[1], W.ly[1], ctrl_cur, ls_cur, L, W.partC, off);
+                               W.ls[1], W.ly[1], ctrl_cur, ls_cur, L, W.partC, off, P.ndense ? W.CR : nullptr, W.CD);
             LRS_CHECK_LAUNCH();
         }
         glo += (long)lg[k].sb * c.ld;
