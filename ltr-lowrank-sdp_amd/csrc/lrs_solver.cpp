@@ -1033,6 +1033,19 @@ static void record_state(lrs_ctx *c, const lrs_params *p, int phase) {
 }
 
 // ---- rank determination (data/lorads_solver.c:406-459) + schedule hook
+// Ranks past the widest factor layout (choose_layout: 512 columns) are clamped there, with one
+// stderr line per solve: --fixedRank, rank-schedule entries and AUG_RANK's rank_max =
+// sqrt(2 nnzRows) + 1 (C5's m = 10^6 gives 1 415) would otherwise end the solve.
+constexpr int kMaxRank = 512;
+static int clamp_rank(int r, bool *warned) {
+    if (r <= kMaxRank) return r;
+    if (warned && !*warned) {
+        fprintf(stderr, "[lrsdp] rank %d above the device maximum %d: clamped to %d\n", r, kMaxRank, kMaxRank);
+        *warned = true;
+    }
+    return kMaxRank;
+}
+
 static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &rank, std::vector<int> &rmax) {
     const int K = c->hp.K;
     rank.assign(K, 1);
@@ -1069,6 +1082,11 @@ static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &ra
             rank[k] = std::max(1, std::min(rk, cone_n_global(c, k)));
             rmax[k] = std::max(rmax[k], rank[k]);
         }
+    }
+    bool warned = false;
+    for (int k = 0; k < K; ++k) {
+        rank[k] = clamp_rank(rank[k], &warned);
+        rmax[k] = std::min(rmax[k], kMaxRank);   // growth stops at the cap silently (AUG_RANK's max)
     }
 }
 
@@ -1177,7 +1195,8 @@ static int aug_rank(lrs_ctx *c, double f, const lrs_params *p, int *sched_pos, i
         int tot = std::max(1, p->rankSchedule[pos]), cur = sum_rank(c);
         for (int k = 0; k < c->dp.K; ++k) {
             int rk = (int)std::lround((double)tot * c->rank[k] / std::max(1, cur));
-            nr[k] = std::max(c->rank[k], std::min(rk, cone_n_global(c, k)));
+            static bool warned = false;
+            nr[k] = clamp_rank(std::max(c->rank[k], std::min(rk, cone_n_global(c, k))), &warned);
             c->rank_max[k] = std::max(c->rank_max[k], nr[k]);
         }
     } else {

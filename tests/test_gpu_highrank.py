@@ -53,3 +53,15 @@ def test_rank_above_256_cli_trajectory(tmp_path):
     assert out["trajectory"]["phase_1"]["curr_rank"] == ref["trajectory"]["phase_1"]["curr_rank"]
     assert out["trajectory"]["phase_1"]["oracle_rank"] == ref["trajectory"]["phase_1"]["oracle_rank"]
     assert abs(out["metrics"]["primal_obj"] - ref["metrics"]["primal_obj"]) <= 1e-6 * abs(ref["metrics"]["primal_obj"])
+
+
+def test_rank_above_512_clamped(capfd):
+    """A rank past the widest layout (512) is clamped with one stderr line instead of ending the
+    solve: --fixedRank 600 on G11 (n = 800) solves at rank 512."""
+    solver = importlib.import_module("ltr-lowrank-sdp_amd.solver")
+    sv = solver.Solver(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "bundled",
+                                    "G11.dat-s"))
+    res = sv.solve(fixedRank=600, reoptLevel=0, maxALMIter=3, skipADMM=1)
+    sv.close()
+    assert res["final_rank"] == 512
+    assert "clamped to 512" in capfd.readouterr().err
