@@ -107,7 +107,24 @@ struct DevCone {
     // long rows (>= kTileMinDeg adjacency entries per row on average): per row, the first entry
     // at or past column x n / kNX, x = 0..kNX ([n][kNX + 1]); the column-tiled k_wide_* kernels
     int *colseg = nullptr;
+    // A(X Y^T) over 2-D tiles (many constraint entries per row, e.g. C5): the cone's constraint
+    // entries bucketed by (row tile, column tile) of kAuvT rows each, items of at most kAuvItem
+    // entries {row0, col0, begin, end}, per tiled entry its local (row, col) packed 16:16, per
+    // constraint entry (cone order) its tiled position, and the per-entry values (scratch)
+    int auv_items = 0;
+    long auv_ebase = 0;                  // first constraint entry of this cone (con_ptr[k m])
+    int *auv_item = nullptr;             // [items][4]
+    unsigned *auv_pq = nullptr;          // [Zk]
+    int *auv_pos = nullptr;              // [Zk]
+    double *auv_val = nullptr;           // [Zk]
 };
+constexpr int kAuvT = 128;           // rows of one side of an A(X Y^T) tile
+constexpr int kAuvC = 32;            // factor columns staged in LDS at a time
+constexpr int kAuvThreads = 512;
+constexpr int kAuvNpt = 8;           // entries per thread of one item
+constexpr int kAuvItem = kAuvThreads * kAuvNpt;
+constexpr int kAuvMinN = 2048;       // tiled when n >= this and the cone has >= kAuvMinDeg
+constexpr int kAuvMinDeg = 64;       //   constraint entries per row (LRS_AUV_TILES=0/1 overrides)
 constexpr int kNX = 8;              // column blocks of the tiled long-row kernels (one per XCD)
 constexpr int kTileMinDeg = 32;
 constexpr int kDenseRow = 64;        // entries of a row past which the latency kernels slice it

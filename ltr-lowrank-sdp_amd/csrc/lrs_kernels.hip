@@ -481,6 +481,108 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
     if (part) partials_finalize<1>(acc, part, ticket, fin);
 }
 
+// A(X Y^T) over 2-D tiles (cones with many constraint entries per row, e.g. C5's 600):
+// the per-entry gather above reads two (MODE 1) or four (MODE 0) 8r-byte factor rows per
+// entry from L2 / Infinity Cache, ~12 GB per C5 launch for 118 MB of operands.  Here a
+// work item is one (row tile I, column tile J) of kAuvT rows each and up to kAuvItem of the
+// entries that fall in it; the block stages the tiles' factor rows kAuvC columns at a time in
+// LDS (rows padded to kAuvC + 1 doubles against bank conflicts) and every thread accumulates
+// its entries' dot products from there, so each factor row crosses L2 once per tile instead
+// of once per entry.  The entry value d(p, q) is what auv_entry computes (MODE 1 X_p.X_q,
+// MODE 0 (X_p.Y_q + X_q.Y_p) / 2), written per tiled entry; k_auv_tsum then sums each
+// constraint's entries in entry order like k_auv_con.
+template <int MODE>
+__global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, const int4 *__restrict__ items,
+                                                          const unsigned *__restrict__ pq,
+                                                          const double *__restrict__ X,
+                                                          const double *__restrict__ Y, double *__restrict__ val,
+                                                          const double *__restrict__ guard) {
+    if (guard && guard[0] == 0.0) return;
+    constexpr int S = kAuvC + 1;                    // LDS row stride (doubles)
+    constexpr int NA = MODE == 0 ? 4 : 2;           // staged operands: Xa, Xb (+ Ya, Yb)
+    __shared__ double tl[NA][kAuvT * S];
+    const int4 it = items[blockIdx.x];
+    const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
+    int pl[kAuvNpt], ql[kAuvNpt];
+    double acc[kAuvNpt];
+#pragma unroll
+    for (int j = 0; j < kAuvNpt; ++j) {
+        const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+        const unsigned w = t < ee ? pq[t] : 0u;
+        pl[j] = (int)(w >> 16) * S;
+        ql[j] = (int)(w & 0xffffu) * S;
+        acc[j] = 0.0;
+    }
+    for (int c0 = 0; c0 < r; c0 += kAuvC) {
+        __syncthreads();
+        // stage rows I0.., J0.. columns [c0, c0 + kAuvC): two doubles a thread-step, zero past
+        // n rows and r columns
+        for (int x = threadIdx.x; x < kAuvT * kAuvC / 2; x += kAuvThreads) {
+            const int row = x / (kAuvC / 2), col = c0 + 2 * (x % (kAuvC / 2));
+            const int o = row * S + col - c0;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                const int grow = ((a & 1) ? J0 : I0) + row;
+                const double *src = (a < 2) ? X : Y;
+                double2 v = make_double2(0.0, 0.0);
+                if (grow < n && col < r) {
+                    v = *reinterpret_cast<const double2 *>(src + (long)grow * ld + col);
+                    if (col + 1 >= r) v.y = 0.0;
+                }
+                tl[a][o] = v.x;
+                tl[a][o + 1] = v.y;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kAuvNpt; ++j) {
+            if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
+            const double *xa = &tl[0][pl[j]], *xb = &tl[1][ql[j]];
+            double s = acc[j];
+            if constexpr (MODE == 1) {
+#pragma unroll 8
+                for (int c = 0; c < kAuvC; ++c) s += xa[c] * xb[c];
+            } else {
+                const double *ya = &tl[2][pl[j]], *yb = &tl[3][ql[j]];
+#pragma unroll 8
+                for (int c = 0; c < kAuvC; ++c) s += xa[c] * yb[c] + xb[c] * ya[c];
+            }
+            acc[j] = s;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kAuvNpt; ++j) {
+        const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+        if (t < ee) val[t] = MODE == 0 ? 0.5 * acc[j] : acc[j];
+    }
+}
+
+// Per constraint of the cone: sum of w_e d_e over its entries in entry order (the tiled
+// values through auv_pos), then k_auv_con's row epilogue (scale, accumulate, sum_upd, the
+// residual partial against b).
+__global__ void __launch_bounds__(kBlock) k_auv_tsum(int m, int cone, const int *__restrict__ con_ptr,
+                                                     const double *__restrict__ con_w, long ebase,
+                                                     const int *__restrict__ pos, const double *__restrict__ val,
+                                                     double scale, int accumulate, double *__restrict__ out,
+                                                     const double *__restrict__ b, double *part, unsigned *ticket,
+                                                     double *fin, const double *__restrict__ guard,
+                                                     double *__restrict__ sum_upd) {
+    if (guard && guard[0] == 0.0) return;
+    double acc[1] = {0.0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        const long row = (long)cone * m + i;
+        const int e0 = con_ptr[row], e1 = con_ptr[row + 1];
+        double v = 0.0;
+        for (int e = e0; e < e1; ++e) v += con_w[e] * val[pos[e - ebase]];
+        double tot = v * scale;
+        if (accumulate) tot = out[i] + tot;
+        if (sum_upd) sum_upd[i] = (sum_upd[i] - out[i]) + tot;
+        out[i] = tot;
+        if (b) { const double dd = b[i] - tot; acc[0] += dd * dd; }
+    }
+    if (part) partials_finalize<1>(acc, part, ticket, fin);
+}
+
 // S[slot] = (withC ? Craw : 0) + sum w[con] a
 __global__ void __launch_bounds__(kBlock) k_wsum(int Ptot, const int *__restrict__ slot_ptr,
                                                  const int *__restrict__ slot_con, const double *__restrict__ slot_a,
@@ -3615,6 +3717,21 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
     const double *Yc = Y ? Y + c.foff : nullptr;
     unsigned *tk = ticket_ptr(T_GATHER);
     double *fin = tmpfin_ptr() + TF_GATHER;
+    if (c.auv_items > 0 && !P.shard) {
+        // 2-D tiles through LDS, then the per-constraint sums
+        if (mode == 1)
+            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
+                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, Xc, Xc, c.auv_val, guard);
+        else
+            hipLaunchKernelGGL((k_auv_tile<0>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
+                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, Xc, Yc, c.auv_val, guard);
+        LRS_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_auv_tsum, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, cone, P.con_ptr,
+                           P.con_w, c.auv_ebase, c.auv_pos, c.auv_val, scale, accumulate, out, b_for_vio, vio_part,
+                           tk, fin, guard, sum_upd);
+        LRS_CHECK_LAUNCH();
+        return 0;
+    }
     const int l0 = P.long_ptr_h.empty() ? 0 : P.long_ptr_h[cone];
     const int nlong = P.long_ptr_h.empty() ? 0 : P.long_ptr_h[cone + 1] - l0;
     if (nlong > 0 && b_for_vio) {

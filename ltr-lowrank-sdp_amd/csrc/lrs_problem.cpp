@@ -536,6 +536,54 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             c1w[r] = con_w[e];
         }
         if (!dput(&dp.con1_pq, c1pq, err) || !dput(&dp.con1_w, c1w, err)) return false;
+        // 2-D tiles for the constraint-entry A(X Y^T) (lrs_device.h kAuvT): cones with many
+        // entries per row and no long constraint rows
+        const char *ev = getenv("LRS_AUV_TILES");
+        for (int k = 0; k < hp.K; ++k) {
+            const int n = hp.cones[k].n;
+            const long eb = con_ptr[(long)k * m], ee = con_ptr[(long)k * m + m];
+            const long Zk = ee - eb;
+            bool on = n >= kAuvMinN && Zk >= (long)kAuvMinDeg * n;
+            if (ev && ev[0] == '0') on = false;
+            if (ev && ev[0] == '1') on = Zk > 0;
+            if (long_ptr[k + 1] > long_ptr[k]) on = false;
+            if (!on) continue;
+            const long nt = (n + kAuvT - 1) / kAuvT;
+            std::vector<std::pair<unsigned long long, int>> key(Zk);
+            for (long e = eb; e < ee; ++e) {
+                const int s = con_slot[e];
+                int p = slot_rc[2L * s], q = slot_rc[2L * s + 1];
+                if (p < q) std::swap(p, q);
+                const unsigned long long tile = (unsigned long long)(p / kAuvT) * nt + (q / kAuvT);
+                key[e - eb] = {(tile << 32) | ((unsigned)(p % kAuvT) << 16) | (unsigned)(q % kAuvT), (int)(e - eb)};
+            }
+            std::sort(key.begin(), key.end());
+            std::vector<int> item, pos(Zk);
+            std::vector<unsigned> pq(Zk);
+            long t0 = 0;
+            for (long t = 0; t < Zk; ++t) {
+                pq[t] = (unsigned)(key[t].first & 0xffffffffu);
+                pos[key[t].second] = (int)t;
+                const bool last = t + 1 == Zk || (key[t + 1].first >> 32) != (key[t].first >> 32) ||
+                                  t + 1 - t0 == kAuvItem;
+                if (!last) continue;
+                const unsigned long long tile = key[t].first >> 32;
+                item.push_back((int)(tile / nt) * kAuvT);
+                item.push_back((int)(tile % nt) * kAuvT);
+                item.push_back((int)t0);
+                item.push_back((int)(t + 1));
+                t0 = t + 1;
+            }
+            DevCone &d = dp.cones[k];
+            d.auv_items = (int)(item.size() / 4);
+            d.auv_ebase = eb;
+            if (!dput(&d.auv_item, item, err) || !dput(&d.auv_pq, pq, err) || !dput(&d.auv_pos, pos, err))
+                return false;
+            if (hipMalloc((void **)&d.auv_val, (size_t)Zk * sizeof(double)) != hipSuccess) {
+                err = "hipMalloc failed";
+                return false;
+            }
+        }
     }
     // Single-slot ("local") constraints: exactly one merged entry over all cones.  Their
     // A(.) value is one pattern slot, so the row that owns the slot evaluates them inside
@@ -689,7 +737,7 @@ void free_problem(DevProblem &dp) {
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
-    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); }
+    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);
