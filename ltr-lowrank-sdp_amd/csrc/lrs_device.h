@@ -109,14 +109,20 @@ struct DevCone {
     int *colseg = nullptr;
     // A(X Y^T) over 2-D tiles (many constraint entries per row, e.g. C5): the cone's constraint
     // entries bucketed by (row tile, column tile) of kAuvT rows each, items of at most kAuvItem
-    // entries {row0, col0, begin, end}, per tiled entry its local (row, col) packed 16:16, per
-    // constraint entry (cone order) its tiled position, and the per-entry values (scratch)
+    // entries {row0, col0, begin, end}, per tiled entry its local (row, col) packed 16:16 and its
+    // constraint entry (cone order), and the per-entry values in cone entry order (scratch)
     int auv_items = 0;
     long auv_ebase = 0;                  // first constraint entry of this cone (con_ptr[k m])
     int *auv_item = nullptr;             // [items][4]
     unsigned *auv_pq = nullptr;          // [Zk]
     int *auv_pos = nullptr;              // [Zk]
     double *auv_val = nullptr;           // [Zk]
+    // the lower pattern in the same 2-D tiles (k_tile_a, stage A of the long-row path): items
+    // {row0, col0, begin, end}, per tiled slot its local (row, col) 16:16 and its global slot
+    int sa_items = 0;
+    int *sa_item = nullptr;
+    unsigned *sa_pq = nullptr;
+    int *sa_slot = nullptr;
 };
 constexpr int kAuvT = 128;           // rows of one side of an A(X Y^T) tile
 constexpr int kAuvC = 32;            // factor columns staged in LDS at a time
@@ -125,6 +131,7 @@ constexpr int kAuvNpt = 8;           // entries per thread of one item
 constexpr int kAuvItem = kAuvThreads * kAuvNpt;
 constexpr int kAuvMinN = 2048;       // tiled when n >= this and the cone has >= kAuvMinDeg
 constexpr int kAuvMinDeg = 64;       //   constraint entries per row (LRS_AUV_TILES=0/1 overrides)
+constexpr int kSlotTileMinDeg = 32;  // lower pattern slots per row for k_tile_a (LRS_SLOT_TILES=0/1 overrides)
 constexpr int kNX = 8;              // column blocks of the tiled long-row kernels (one per XCD)
 constexpr int kTileMinDeg = 32;
 constexpr int kDenseRow = 64;        // entries of a row past which the latency kernels slice it

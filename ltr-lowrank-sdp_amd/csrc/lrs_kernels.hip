@@ -486,21 +486,74 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
 // entry from L2 / Infinity Cache, ~12 GB per C5 launch for 118 MB of operands.  Here a
 // work item is one (row tile I, column tile J) of kAuvT rows each and up to kAuvItem of the
 // entries that fall in it; the block stages the tiles' factor rows kAuvC columns at a time in
-// LDS (rows padded to kAuvC + 1 doubles against bank conflicts) and every thread accumulates
-// its entries' dot products from there, so each factor row crosses L2 once per tile instead
-// of once per entry.  The entry value d(p, q) is what auv_entry computes (MODE 1 X_p.X_q,
-// MODE 0 (X_p.Y_q + X_q.Y_p) / 2), written per tiled entry; k_auv_tsum then sums each
-// constraint's entries in entry order like k_auv_con.
+// LDS (rows padded to kAuvC + 2 doubles against bank conflicts, read 16 B at a time) and
+// every thread accumulates its entries' dot products from there, so each factor row crosses
+// L2 once per tile instead of once per entry.  The entry value d(p, q) is what auv_entry computes (MODE 1 X_p.X_q,
+// MODE 0 (X_p.Y_q + X_q.Y_p) / 2), stored at the entry's place in the cone's constraint entry
+// order; k_auv_tsum then sums each constraint's entries in entry order like k_auv_con.
+// Stage rows I0.., J0.. (kAuvT each) of X (and Y), columns [c0, c0 + kAuvC), into LDS:
+// tl[0] = X_I, tl[1] = X_J, tl[2] = Y_I, tl[3] = Y_J; two doubles a thread-step, zero past
+// n rows and r columns.
+constexpr int kAuvS = kAuvC + 2;   // LDS row stride (doubles; 16-B aligned rows, 4 banks apart)
+template <int NA>
+__device__ __forceinline__ void auv_stage(double (*tl)[kAuvT * kAuvS], int I0, int J0, int c0, int n, int r,
+                                          int ld, const double *__restrict__ X, const double *__restrict__ Y) {
+    for (int x = threadIdx.x; x < kAuvT * kAuvC / 2; x += kAuvThreads) {
+        const int row = x / (kAuvC / 2), col = c0 + 2 * (x % (kAuvC / 2));
+        const int o = row * kAuvS + col - c0;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            const int grow = ((a & 1) ? J0 : I0) + row;
+            const double *src = (a < 2) ? X : Y;
+            double2 v = make_double2(0.0, 0.0);
+            if (grow < n && col < r) {
+                v = *reinterpret_cast<const double2 *>(src + (long)grow * ld + col);
+                if (col + 1 >= r) v.y = 0.0;
+            }
+            *reinterpret_cast<double2 *>(&tl[a][o]) = v;
+        }
+    }
+}
+
+// One staged column chunk of an entry (p, q): MODE 1 X_p.X_q, MODE 0 X_p.Y_q + X_q.Y_p,
+// MODE 2 both of MODE 0 (into s) and Y_p.Y_q (into s2).
+template <int MODE>
+__device__ __forceinline__ void auv_chunk(const double (*tl)[kAuvT * kAuvS], int pl, int ql, double &s, double &s2) {
+    const double2 *xa = reinterpret_cast<const double2 *>(&tl[0][pl]);
+    const double2 *xb = reinterpret_cast<const double2 *>(&tl[1][ql]);
+    if constexpr (MODE == 1) {
+#pragma unroll 8
+        for (int c = 0; c < kAuvC / 2; ++c) {
+            const double2 a = xa[c], b = xb[c];
+            s += a.x * b.x;
+            s += a.y * b.y;
+        }
+    } else {
+        const double2 *ya = reinterpret_cast<const double2 *>(&tl[2][pl]);
+        const double2 *yb = reinterpret_cast<const double2 *>(&tl[3][ql]);
+#pragma unroll 8
+        for (int c = 0; c < kAuvC / 2; ++c) {
+            const double2 a = xa[c], b = xb[c], ay = ya[c], by = yb[c];
+            s += a.x * by.x + b.x * ay.x;
+            s += a.y * by.y + b.y * ay.y;
+            if constexpr (MODE == 2) {
+                s2 += ay.x * by.x;
+                s2 += ay.y * by.y;
+            }
+        }
+    }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, const int4 *__restrict__ items,
                                                           const unsigned *__restrict__ pq,
+                                                          const int *__restrict__ ent,
                                                           const double *__restrict__ X,
                                                           const double *__restrict__ Y, double *__restrict__ val,
                                                           const double *__restrict__ guard) {
     if (guard && guard[0] == 0.0) return;
-    constexpr int S = kAuvC + 1;                    // LDS row stride (doubles)
     constexpr int NA = MODE == 0 ? 4 : 2;           // staged operands: Xa, Xb (+ Ya, Yb)
-    __shared__ double tl[NA][kAuvT * S];
+    __shared__ double tl[NA][kAuvT * kAuvS];
     const int4 it = items[blockIdx.x];
     const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
     int pl[kAuvNpt], ql[kAuvNpt];
@@ -509,60 +562,33 @@ __global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, 
     for (int j = 0; j < kAuvNpt; ++j) {
         const int t = eb + (int)threadIdx.x + j * kAuvThreads;
         const unsigned w = t < ee ? pq[t] : 0u;
-        pl[j] = (int)(w >> 16) * S;
-        ql[j] = (int)(w & 0xffffu) * S;
+        pl[j] = (int)(w >> 16) * kAuvS;
+        ql[j] = (int)(w & 0xffffu) * kAuvS;
         acc[j] = 0.0;
     }
     for (int c0 = 0; c0 < r; c0 += kAuvC) {
         __syncthreads();
-        // stage rows I0.., J0.. columns [c0, c0 + kAuvC): two doubles a thread-step, zero past
-        // n rows and r columns
-        for (int x = threadIdx.x; x < kAuvT * kAuvC / 2; x += kAuvThreads) {
-            const int row = x / (kAuvC / 2), col = c0 + 2 * (x % (kAuvC / 2));
-            const int o = row * S + col - c0;
-#pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                const int grow = ((a & 1) ? J0 : I0) + row;
-                const double *src = (a < 2) ? X : Y;
-                double2 v = make_double2(0.0, 0.0);
-                if (grow < n && col < r) {
-                    v = *reinterpret_cast<const double2 *>(src + (long)grow * ld + col);
-                    if (col + 1 >= r) v.y = 0.0;
-                }
-                tl[a][o] = v.x;
-                tl[a][o + 1] = v.y;
-            }
-        }
+        auv_stage<NA>(tl, I0, J0, c0, n, r, ld, X, Y);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < kAuvNpt; ++j) {
             if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
-            const double *xa = &tl[0][pl[j]], *xb = &tl[1][ql[j]];
-            double s = acc[j];
-            if constexpr (MODE == 1) {
-#pragma unroll 8
-                for (int c = 0; c < kAuvC; ++c) s += xa[c] * xb[c];
-            } else {
-                const double *ya = &tl[2][pl[j]], *yb = &tl[3][ql[j]];
-#pragma unroll 8
-                for (int c = 0; c < kAuvC; ++c) s += xa[c] * yb[c] + xb[c] * ya[c];
-            }
-            acc[j] = s;
+            double unused = 0.0;
+            auv_chunk<MODE>(tl, pl[j], ql[j], acc[j], unused);
         }
     }
 #pragma unroll
     for (int j = 0; j < kAuvNpt; ++j) {
         const int t = eb + (int)threadIdx.x + j * kAuvThreads;
-        if (t < ee) val[t] = MODE == 0 ? 0.5 * acc[j] : acc[j];
+        if (t < ee) val[ent[t]] = MODE == 0 ? 0.5 * acc[j] : acc[j];
     }
 }
 
-// Per constraint of the cone: sum of w_e d_e over its entries in entry order (the tiled
-// values through auv_pos), then k_auv_con's row epilogue (scale, accumulate, sum_upd, the
+// Per constraint of the cone: sum of w_e d_e over its entries in entry order, then k_auv_con's row epilogue (scale, accumulate, sum_upd, the
 // residual partial against b).
 __global__ void __launch_bounds__(kBlock) k_auv_tsum(int m, int cone, const int *__restrict__ con_ptr,
                                                      const double *__restrict__ con_w, long ebase,
-                                                     const int *__restrict__ pos, const double *__restrict__ val,
+                                                     const double *__restrict__ val,
                                                      double scale, int accumulate, double *__restrict__ out,
                                                      const double *__restrict__ b, double *part, unsigned *ticket,
                                                      double *fin, const double *__restrict__ guard,
@@ -573,7 +599,8 @@ __global__ void __launch_bounds__(kBlock) k_auv_tsum(int m, int cone, const int 
         const long row = (long)cone * m + i;
         const int e0 = con_ptr[row], e1 = con_ptr[row + 1];
         double v = 0.0;
-        for (int e = e0; e < e1; ++e) v += con_w[e] * val[pos[e - ebase]];
+        const double *vr = val - ebase;
+        for (int e = e0; e < e1; ++e) v += con_w[e] * vr[e];
         double tot = v * scale;
         if (accumulate) tot = out[i] + tot;
         if (sum_upd) sum_upd[i] = (sum_upd[i] - out[i]) + tot;
@@ -2935,6 +2962,84 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_a(
     write_partials_range<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x, 0, 7);
 }
 
+// k_wide_a's work over 2-D tiles of the lower pattern (cones with DevCone::sa_items, e.g. C5's
+// ~570 lower slots per row): a work item is one (row tile, column tile) of kAuvT rows each and
+// up to kAuvItem of its slots; R and D of both tiles are staged in LDS kAuvC columns at a time
+// (auv_stage) and each thread evaluates its slots' sym(R D^T) and D D^T from there, instead of
+// every lane group gathering ~570 neighbour rows of R and D per row.  The per-slot epilogue
+// (slot values, C and local-constraint terms, rec) is k_wide_a's.  Same grid and partial
+// slots as k_wide_a (blocks stride over the items), so the consumers are unchanged.
+__global__ void __launch_bounds__(kRowBlock) k_tile_a(
+    int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
+    const int *__restrict__ tslot, const double *__restrict__ Cw, const double *__restrict__ Rb0,
+    const double *__restrict__ Rb1, const double *__restrict__ Dall, double *__restrict__ uRD,
+    double *__restrict__ uDD, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
+    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
+    const double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec,
+    const double *__restrict__ par, const double *__restrict__ ctrl_cur, double *__restrict__ partA, int pblk_off) {
+    static_assert(kRowBlock == kAuvThreads, "k_tile_a runs the A(X Y^T) tile layout");
+    if (ctrl_cur[C_ACTIVE] == 0.0) return;
+    const double *__restrict__ R = (ctrl_cur[C_RCUR] == 0.0 ? Rb0 : Rb1) + foff;
+    const double *__restrict__ D = Dall + foff;
+    const double rho = par[P_RHO], rhoInv = 1.0 / rho;
+    __shared__ double tl[4][kAuvT * kAuvS];
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
+        const int4 it = items[itx];
+        const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
+        int pl[kAuvNpt], ql[kAuvNpt];
+        double s0[kAuvNpt], s1[kAuvNpt];
+#pragma unroll
+        for (int j = 0; j < kAuvNpt; ++j) {
+            const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+            const unsigned w = t < ee ? pq[t] : 0u;
+            pl[j] = (int)(w >> 16) * kAuvS;
+            ql[j] = (int)(w & 0xffffu) * kAuvS;
+            s0[j] = 0.0;
+            s1[j] = 0.0;
+        }
+        for (int c0 = 0; c0 < r; c0 += kAuvC) {
+            __syncthreads();
+            auv_stage<4>(tl, I0, J0, c0, n, r, ld, R, D);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kAuvNpt; ++j) {
+                if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
+                auv_chunk<2>(tl, pl[j], ql[j], s0[j], s1[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kAuvNpt; ++j) {
+            const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+            if (t >= ee) break;
+            const int sl = tslot[t];
+            const double d0 = 0.5 * s0[j], d1 = s1[j];
+            uRD[sl] = d0;
+            uDD[sl] = d1;
+            const double cwl = Cw[sl];
+            acc[0] += cwl * d0;
+            acc[1] += cwl * d1;
+            // local constraints on this slot (ALMCalq12p12 lorads_alm.c:714-734), as k_wide_a
+            const double2 l1l = loc1[sl];
+            const int c1 = (int)l1l.y;
+            const int e0 = c1 == -2 ? loc_ptr[sl] : 0, e1 = c1 == -2 ? loc_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
+            for (int e = e0; e < e1; ++e) {
+                const int ci = c1 >= 0 ? c1 : loc_con[e];
+                const double w = c1 >= 0 ? l1l.x : loc_w[e];
+                const double bi = b[ci], cvi = cvs[ci], li = lam[ci];
+                const double q1 = 2.0 * (w * d0), q2 = w * d1;
+                const double q0 = (bi - cvi) + rhoInv * li;
+                acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1;
+                acc[6] += q0 * q1;
+                double2 *rr = reinterpret_cast<double2 *>(rec + 4L * ci);
+                rr[0] = make_double2(cvi, q1);
+                rr[1] = make_double2(q2, (-li) + (-rho) * bi);
+            }
+        }
+    }
+    write_partials_range<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x, 0, 7);
+}
+
 // row epilogue of stage B: G_new = 2 (S R_new [+ C R_new]), s = tau D, y = G_new - G_old
 // (setlbfgsHisTwo lorads_alm.c:842-863) and the nine L-BFGS dots
 template <int E>
@@ -3721,13 +3826,13 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
         // 2-D tiles through LDS, then the per-constraint sums
         if (mode == 1)
             hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
-                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, Xc, Xc, c.auv_val, guard);
+                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Xc, c.auv_val, guard);
         else
             hipLaunchKernelGGL((k_auv_tile<0>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
-                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, Xc, Yc, c.auv_val, guard);
+                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Yc, c.auv_val, guard);
         LRS_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_auv_tsum, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, cone, P.con_ptr,
-                           P.con_w, c.auv_ebase, c.auv_pos, c.auv_val, scale, accumulate, out, b_for_vio, vio_part,
+                           P.con_w, c.auv_ebase, c.auv_val, scale, accumulate, out, b_for_vio, vio_part,
                            tk, fin, guard, sum_upd);
         LRS_CHECK_LAUNCH();
         return 0;
@@ -4413,9 +4518,15 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     for (int k = 0; k < KL && (mask & 1) && split; ++k) {
         const DevCone &c = cone_of(k);
         const int grid = pa[k].grid;
-        if (pa[k].wide) {
+        if (pa[k].wide && !merge && !sh && !tla[k] && c.sa_items > 0) {
+            // lower pattern in 2-D LDS tiles (k_tile_a), same grid and partial slots
+            hipLaunchKernelGGL(k_tile_a, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
+                               reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2, W.D,
+                               W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,
+                               reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur,
+                               W.part, off);
+        } else if (pa[k].wide) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-
                 if (tla[k]) LRS_WIDE_A(true);
                 else LRS_WIDE_A(false);
             });

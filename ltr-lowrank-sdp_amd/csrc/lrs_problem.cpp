@@ -563,7 +563,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             long t0 = 0;
             for (long t = 0; t < Zk; ++t) {
                 pq[t] = (unsigned)(key[t].first & 0xffffffffu);
-                pos[key[t].second] = (int)t;
+                pos[t] = key[t].second;
                 const bool last = t + 1 == Zk || (key[t + 1].first >> 32) != (key[t].first >> 32) ||
                                   t + 1 - t0 == kAuvItem;
                 if (!last) continue;
@@ -722,6 +722,44 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             }
             if (!dput(&d.colseg, cs, err)) return false;
         }
+        {
+            // the lower pattern in 2-D tiles for k_tile_a (lrs_device.h kAuvT), slots sorted by
+            // (row tile, column tile, row, column), items of at most kAuvItem slots
+            const long P = (long)c.prow.size();
+            const char *ev = getenv("LRS_SLOT_TILES");
+            bool on = c.n >= kAuvMinN && P >= (long)kSlotTileMinDeg * c.n;
+            if (ev && ev[0] == '0') on = false;
+            if (ev && ev[0] == '1') on = P > 0;
+            if (on) {
+                const long nt = (c.n + kAuvT - 1) / kAuvT;
+                std::vector<std::pair<unsigned long long, int>> key(P);
+                for (long t = 0; t < P; ++t) {
+                    const int p = c.prow[t], q = c.pcol[t];   // lower: p >= q
+                    const unsigned long long tile = (unsigned long long)(p / kAuvT) * nt + (q / kAuvT);
+                    key[t] = {(tile << 32) | ((unsigned)(p % kAuvT) << 16) | (unsigned)(q % kAuvT), (int)t};
+                }
+                std::sort(key.begin(), key.end());
+                std::vector<int> item, sl(P);
+                std::vector<unsigned> pq(P);
+                long t0 = 0;
+                for (long t = 0; t < P; ++t) {
+                    pq[t] = (unsigned)(key[t].first & 0xffffffffu);
+                    sl[t] = d.slot_off + key[t].second;
+                    const bool last = t + 1 == P || (key[t + 1].first >> 32) != (key[t].first >> 32) ||
+                                      t + 1 - t0 == kAuvItem;
+                    if (!last) continue;
+                    const unsigned long long tile = key[t].first >> 32;
+                    item.push_back((int)(tile / nt) * kAuvT);
+                    item.push_back((int)(tile % nt) * kAuvT);
+                    item.push_back((int)t0);
+                    item.push_back((int)(t + 1));
+                    t0 = t + 1;
+                }
+                d.sa_items = (int)(item.size() / 4);
+                if (!dput(&d.sa_item, item, err) || !dput(&d.sa_pq, pq, err) || !dput(&d.sa_slot, sl, err))
+                    return false;
+            }
+        }
         if (c.dense_c) {
             if (!dput(&d.Cd, c.Cfull, err)) return false;
             d.dense_c = 1;
@@ -737,7 +775,7 @@ void free_problem(DevProblem &dp) {
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
-    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); }
+    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);

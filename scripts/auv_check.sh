@@ -10,5 +10,5 @@ cat gpurun_out/auv/c5_gather.log
 timeout -k 10 600 python3 -u scripts/c5_probe.py 10000 1000000 128 10 > gpurun_out/auv/c5_tiles.log 2>&1
 cat gpurun_out/auv/c5_tiles.log
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/auv/prof -o c5 -- python3 -u scripts/c5_probe.py 10000 1000000 128 10 > gpurun_out/auv/prof.log 2>&1
-find gpurun_out/auv/prof -name "*stats*" | head
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/auv/prof -o c5 -- python3 -u scripts/c5_probe.py 10000 1000000 128 10 > gpurun_out/auv/prof.log 2>&1
+f=$(find gpurun_out/auv/prof -name "*kernel_stats.csv" | head -1); cut -d, -f1-5 "$f" | head -14

@@ -110,3 +110,31 @@ def test_budget_hook_resumes_same_solve(solver_mod):
     d = sv.alm_steps(30, reoptLevel=0, phase1Tol=1e-300)
     assert np.array_equal(R1, d["R"])
     sv.close()
+
+@pytest.mark.parametrize("name", STEP_CASES)
+def test_fused_iterations_slot_tiles_match_reference(solver_mod, name, monkeypatch):
+    """Path 3 with stage A's lower pattern in 2-D LDS tiles (k_tile_a, forced by
+    LRS_SLOT_TILES=1 at load; C5-like cones take it by default): the same trips to 1e-9."""
+    monkeypatch.setenv("LRS_SLOT_TILES", "1")
+    z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
+    rank = int(z["rank_flag"])
+    kw = {"reoptLevel": 0}
+    if rank > 0:
+        kw["fixedRank"] = rank
+    sv = solver_mod.Solver(_path(name))
+    sv.set_kernel_path(3)
+    for K in [int(k) for k in z["ks"]]:
+        trips = z[f"K{K}_trips"]
+        if trips.shape[0] < K:
+            continue
+        d = sv.alm_steps(K, **kw)
+        assert d["inner"] == K, (K, d["inner"])
+        tau, rn, lag, pinf = trips[K - 1]
+        assert abs(d["tau"] - tau) <= TOL * abs(tau), (K, d["tau"], tau)
+        assert abs(d["lag"] - lag) <= TOL * abs(lag), (K, d["lag"], lag)
+        for key in ("R", "G", "cvs", "s", "y"):
+            ours = d[key]
+            if name in PROJ and key != "cvs":
+                ours = project(ours, int(z["dims"][0]), PROJ[name])
+            assert rel_err(ours, z[f"K{K}_{key}"]) < TOL, (K, key)
+    sv.close()
