@@ -123,6 +123,13 @@ struct DevCone {
     int *sa_item = nullptr;
     unsigned *sa_pq = nullptr;
     int *sa_slot = nullptr;
+    // stage B's gradient S R_new over the symmetric pattern in the same tiles (k_tile_b2): one
+    // block per (row tile I, column group x of kNX), its tile pairs {col0, row-pointer offset}
+    // ([nt * kNX][2] ranges into sb_tp), per tile pair kAuvT + 1 row pointers into the entries
+    // {local column, slot}; sa_S holds the slot values of S = C + A^*(M1) between the two kernels
+    int sb_blocks = 0;
+    int *sb_blk = nullptr, *sb_tp = nullptr, *sb_rp = nullptr, *sb_ent = nullptr;
+    double *sa_S = nullptr;
 };
 constexpr int kAuvT = 128;           // rows of one side of an A(X Y^T) tile
 constexpr int kAuvC = 32;            // factor columns staged in LDS at a time

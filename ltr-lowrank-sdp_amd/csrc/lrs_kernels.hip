@@ -3207,6 +3207,149 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
     write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
 }
 
+// k_wide_b over 2-D tiles (cones with DevCone::sb_blocks), in two kernels and k_wide_bf:
+// k_tile_b1 -- per lower slot of the A-tiles, S = C + A^*(M1) from rec (ALMSetGrad
+//   lorads_alm.c:38-57 as k_wide_b) into sa_S, and A(R_new R_new^T) from R_new staged in LDS
+//   (uRR, local constraints' new A(.) and residual partial);
+// k_tile_b2 -- G partials: block (row tile I, column group x) stages R_new of each column tile
+//   J of its group in LDS, 64 columns at a time, and thread (row, quarter) sums S_ij R_new,j
+//   over its row's entries of the tile pair in column order, 16 columns at a time, into GP[x];
+// k_wide_bf sums the kNX partial rows in group order and runs the row epilogue.
+__global__ void __launch_bounds__(kRowBlock) k_tile_b1(
+    int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
+    const int *__restrict__ tslot, const double *Rb0, const double *Rb1, double *__restrict__ uRR,
+    double *__restrict__ Sv, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
+    const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double2 *__restrict__ slot1,
+    const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
+    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
+    double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
+    const double *__restrict__ ls_cur, double *__restrict__ partC, int pblk_off) {
+    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
+    const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
+    const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
+    __shared__ double tl[2][kAuvT * kAuvS];
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
+        const int4 it = items[itx];
+        const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
+        int pl[kAuvNpt], ql[kAuvNpt];
+        double dv[kAuvNpt];
+#pragma unroll
+        for (int j = 0; j < kAuvNpt; ++j) {
+            const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+            const unsigned w = t < ee ? pq[t] : 0u;
+            pl[j] = (int)(w >> 16) * kAuvS;
+            ql[j] = (int)(w & 0xffffu) * kAuvS;
+            dv[j] = 0.0;
+        }
+        for (int c0 = 0; c0 < r; c0 += kAuvC) {
+            __syncthreads();
+            auv_stage<2>(tl, I0, J0, c0, n, r, ld, Rn, Rn);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kAuvNpt; ++j) {
+                if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
+                double unused = 0.0;
+                auv_chunk<1>(tl, pl[j], ql[j], dv[j], unused);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kAuvNpt; ++j) {
+            const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+            if (t >= ee) break;
+            const int sl = tslot[t];
+            double svl = Craw[sl];
+            const double2 s1l = slot1[sl];
+            const int c1 = (int)s1l.y;
+            if (c1 >= 0) {
+                const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * c1);
+                const double2 ra = q[0], rb = q[1];
+                double cv = ra.x + tau * ra.y;
+                cv = cv + tau2 * rb.x;
+                svl += (rb.y + rho * cv) * s1l.x;
+            } else if (c1 == -2) {
+                for (int e = slot_ptr[sl]; e < slot_ptr[sl + 1]; ++e) {
+                    const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
+                    const double2 x = q[0], y = q[1];
+                    double cv = x.x + tau * x.y;
+                    cv = cv + tau2 * y.x;
+                    svl += (y.y + rho * cv) * slot_a[e];
+                }
+            }
+            Sv[sl] = svl;
+            const double d = dv[j];
+            uRR[sl] = d;
+            const double2 l1l = loc1[sl];
+            const int cl = (int)l1l.y;
+            const int f0 = cl == -2 ? loc_ptr[sl] : 0, f1 = cl == -2 ? loc_ptr[sl + 1] : (cl >= 0 ? 1 : 0);
+            for (int e = f0; e < f1; ++e) {
+                const int ci = cl >= 0 ? cl : loc_con[e];
+                const double tot = (cl >= 0 ? l1l.x : loc_w[e]) * d;
+                cvs[ci] = tot;
+                const double dd = b[ci] - tot;
+                acc[9] += dd * dd;
+            }
+        }
+    }
+    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+}
+
+constexpr int kTbC = 64;            // R_new columns staged per pass in k_tile_b2
+constexpr int kTbS = kTbC + 2;      // LDS row stride (16-B aligned rows)
+__global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff, const int2 *__restrict__ blk,
+                                                       const int2 *__restrict__ tp, const int *__restrict__ rp,
+                                                       const int2 *__restrict__ ent, const double *__restrict__ Sv,
+                                                       const double *Rb0, const double *Rb1, double *__restrict__ GP,
+                                                       long gstride, int r, const double *__restrict__ ctrl,
+                                                       const double *__restrict__ ls_cur) {
+    static_assert(kRowBlock == 4 * kAuvT, "k_tile_b2: four threads per tile row");
+    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
+    const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
+    __shared__ double rj[kAuvT * kTbS];
+    const int I = blockIdx.x / kNX, x = blockIdx.x % kNX;
+    const int pl = threadIdx.x >> 2, cq = threadIdx.x & 3;
+    const int i = I * kAuvT + pl;
+    const int2 br = blk[blockIdx.x];
+    for (int c0 = 0; c0 < ld; c0 += kTbC) {
+        double g[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) g[c] = 0.0;
+        for (int q = br.x; q < br.y; ++q) {   // block-uniform
+            const int2 t = tp[q];
+            __syncthreads();
+            for (int y = threadIdx.x; y < kAuvT * kTbC / 2; y += kRowBlock) {
+                const int row = y / (kTbC / 2), col = c0 + 2 * (y % (kTbC / 2));
+                const int grow = t.x + row;
+                double2 v = make_double2(0.0, 0.0);
+                if (grow < n && col < r) {
+                    v = *reinterpret_cast<const double2 *>(Rn + (long)grow * ld + col);
+                    if (col + 1 >= r) v.y = 0.0;
+                }
+                *reinterpret_cast<double2 *>(&rj[row * kTbS + col - c0]) = v;
+            }
+            __syncthreads();
+            const int e1 = rp[t.y + pl + 1];
+            for (int e = rp[t.y + pl]; e < e1; ++e) {
+                const int2 en = ent[e];
+                const double s = Sv[en.y];
+                const double2 *src = reinterpret_cast<const double2 *>(&rj[en.x * kTbS + cq * 16]);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const double2 v = src[c];
+                    g[2 * c] += s * v.x;
+                    g[2 * c + 1] += s * v.y;
+                }
+            }
+        }
+        if (i < n) {
+            double *dst = GP + x * gstride + foff + (long)i * ld + c0 + cq * 16;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if (c0 + cq * 16 + 2 * c < ld) reinterpret_cast<double2 *>(dst)[c] = make_double2(g[2 * c], g[2 * c + 1]);
+        }
+    }
+}
+
 // B, column-tiled: the eight partial S R_new rows summed in block order, then the row epilogue
 template <int G, int E>
 __global__ void __launch_bounds__(kRowBlock) k_wide_bf(int n, int ld, long foff, const double *__restrict__ Dall,
@@ -4410,6 +4553,12 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         tlb[k] = can && pb[k].wide && pb[k].grid >= kNX;
         if (tlb[k]) nblkB += pb[k].grid;
     }
+    // long-row B over 2-D LDS tiles (k_tile_b1 / k_tile_b2, then k_wide_bf's epilogue blocks)
+    bool tbt[kMaxCones];
+    for (int k = 0; k < KL; ++k) {
+        tbt[k] = !merge && !sh && !tlb[k] && pb[k].wide && W.GP && cone_of(k).sb_blocks > 0 && cone_of(k).sa_items > 0;
+        if (tbt[k]) nblkB += pb[k].grid;
+    }
     if (nblkB > kMaxPartialBlocks) {
         snprintf(g_err, sizeof(g_err), "stage B: %d partial blocks past %d", nblkB, kMaxPartialBlocks);
         return -1;
@@ -4631,9 +4780,27 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const DevCone &c = cone_of(k);
         const int grid = pb[k].grid;
         if (pb[k].small) { off += grid; continue; }
-        if (pb[k].wide) {
+        if (tbt[k]) {
+            hipLaunchKernelGGL(k_tile_b1, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
+                               reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, W.R, W.R2, W.uvt2,
+                               c.sa_S - c.slot_off, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,
+                               reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,
+                               reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur,
+                               W.partC, off);
+            LRS_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_tile_b2, dim3(c.sb_blocks), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
+                               reinterpret_cast<const int2 *>(c.sb_blk), reinterpret_cast<const int2 *>(c.sb_tp),
+                               c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent), c.sa_S - c.slot_off, W.R, W.R2,
+                               W.GP, P.NRpad, c.r, ctrl_cur, ls_cur);
+            LRS_CHECK_LAUNCH();
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-
+                hipLaunchKernelGGL((k_wide_bf<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff, W.D,
+                                   W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], ctrl_cur, ls_cur, L, W.partC,
+                                   offBF, c.row0, P.ndense ? W.CR : nullptr, W.CD, W.GP, P.NRpad);
+            });
+            offBF += grid;
+        } else if (pb[k].wide) {
+            LRS_LAYOUT_SWITCH(c.G, c.E, {
                 if (tlb[k]) {
                     LRS_WIDE_B(true);
                     LRS_CHECK_LAUNCH();

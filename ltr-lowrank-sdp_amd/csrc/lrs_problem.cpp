@@ -758,6 +758,48 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 d.sa_items = (int)(item.size() / 4);
                 if (!dput(&d.sa_item, item, err) || !dput(&d.sa_pq, pq, err) || !dput(&d.sa_slot, sl, err))
                     return false;
+                // symmetric adjacency by (row tile I, column tile J): counting sort over the
+                // row-ordered, column-sorted adjacency keeps (row, column) order inside a tile pair
+                const long nnz = (long)c.adj_col.size();
+                std::vector<long> cnt((size_t)nt * nt + 1, 0);
+                for (int i = 0; i < c.n; ++i)
+                    for (int e = c.adj_ptr[i]; e < c.adj_ptr[i + 1]; ++e)
+                        cnt[(size_t)(i / kAuvT) * nt + c.adj_col[e] / kAuvT + 1]++;
+                for (size_t q = 0; q + 1 < cnt.size(); ++q) cnt[q + 1] += cnt[q];
+                std::vector<int> ent(2 * std::max(1L, nnz)), epl(std::max(1L, nnz));
+                std::vector<long> fill(cnt.begin(), cnt.end() - 1);
+                for (int i = 0; i < c.n; ++i)
+                    for (int e = c.adj_ptr[i]; e < c.adj_ptr[i + 1]; ++e) {
+                        const long at = fill[(size_t)(i / kAuvT) * nt + c.adj_col[e] / kAuvT]++;
+                        ent[2 * at] = c.adj_col[e] % kAuvT;
+                        ent[2 * at + 1] = d.slot_off + c.adj_slot[e];
+                        epl[at] = i % kAuvT;
+                    }
+                std::vector<int> blk(2L * nt * kNX), tp, rp;
+                for (long I = 0; I < nt; ++I)
+                    for (int x = 0; x < kNX; ++x) {
+                        blk[2 * (I * kNX + x)] = (int)(tp.size() / 2);
+                        for (long J = x * nt / kNX; J < (x + 1) * nt / kNX; ++J) {
+                            const long e0 = cnt[I * nt + J], e1 = cnt[I * nt + J + 1];
+                            if (e0 == e1) continue;
+                            tp.push_back((int)(J * kAuvT));
+                            tp.push_back((int)rp.size());
+                            long e = e0;
+                            for (int r0 = 0; r0 <= kAuvT; ++r0) {
+                                while (e < e1 && epl[e] < r0) ++e;
+                                rp.push_back((int)e);
+                            }
+                        }
+                        blk[2 * (I * kNX + x) + 1] = (int)(tp.size() / 2);
+                    }
+                d.sb_blocks = (int)(nt * kNX);
+                if (!dput(&d.sb_blk, blk, err) || !dput(&d.sb_tp, tp, err) || !dput(&d.sb_rp, rp, err) ||
+                    !dput(&d.sb_ent, ent, err))
+                    return false;
+                if (hipMalloc((void **)&d.sa_S, (size_t)P * sizeof(double)) != hipSuccess) {
+                    err = "hipMalloc failed";
+                    return false;
+                }
             }
         }
         if (c.dense_c) {
@@ -775,7 +817,8 @@ void free_problem(DevProblem &dp) {
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
-    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot); }
+    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);
+        f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);

@@ -500,7 +500,9 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         bool tiles = false;
         const char *ev = getenv("LRS_TILES");
         for (const auto &dc : P.cones) tiles = tiles || (dc.colseg != nullptr && ev && ev[0] == '1');
-        if (tiles && A(&W.GP, (long)kNX * NR)) return -1;
+        bool btiles = false;   // long-row B over 2-D tiles (DevCone::sb_blocks): k_wide_bf's partial rows
+        for (const auto &dc : P.cones) btiles = btiles || dc.sb_blocks > 0;
+        if ((tiles || btiles) && A(&W.GP, (long)kNX * NR)) return -1;
         P.tiles = tiles;
     }
     HIPC(hipStreamSynchronize(c->st));
