@@ -491,27 +491,42 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
 // L2 once per tile instead of once per entry.  The entry value d(p, q) is what auv_entry computes (MODE 1 X_p.X_q,
 // MODE 0 (X_p.Y_q + X_q.Y_p) / 2), stored at the entry's place in the cone's constraint entry
 // order; k_auv_tsum then sums each constraint's entries in entry order like k_auv_con.
-// Stage rows I0.., J0.. (kAuvT each) of X (and Y), columns [c0, c0 + kAuvC), into LDS:
-// tl[0] = X_I, tl[1] = X_J, tl[2] = Y_I, tl[3] = Y_J; two doubles a thread-step, zero past
-// n rows and r columns.
+// Staged tiles in LDS: tl[0] = X_I, tl[1] = X_J, tl[2] = Y_I, tl[3] = Y_J, rows I0.., J0..
+// (kAuvT each) of X (and Y), columns [c0, c0 + kAuvC), zero past n rows and r columns.
 constexpr int kAuvS = kAuvC + 2;   // LDS row stride (doubles; 16-B aligned rows, 4 banks apart)
+
+// Staging split in two so that the next chunk's loads are in flight while the current one
+// is computed: auv_fetch into registers, auv_put into LDS (after a barrier).
+constexpr int kAuvPer = kAuvT * kAuvC / 2 / kAuvThreads;   // double2 per thread per operand
+static_assert(kAuvPer * kAuvThreads * 2 == kAuvT * kAuvC, "tile staging divides evenly");
 template <int NA>
-__device__ __forceinline__ void auv_stage(double (*tl)[kAuvT * kAuvS], int I0, int J0, int c0, int n, int r,
-                                          int ld, const double *__restrict__ X, const double *__restrict__ Y) {
-    for (int x = threadIdx.x; x < kAuvT * kAuvC / 2; x += kAuvThreads) {
+__device__ __forceinline__ void auv_fetch(double2 (&v)[NA][kAuvPer], int I0, int J0, int c0, int n, int r, int ld,
+                                          const double *__restrict__ X, const double *__restrict__ Y) {
+#pragma unroll
+    for (int k = 0; k < kAuvPer; ++k) {
+        const int x = threadIdx.x + k * kAuvThreads;
         const int row = x / (kAuvC / 2), col = c0 + 2 * (x % (kAuvC / 2));
-        const int o = row * kAuvS + col - c0;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
             const int grow = ((a & 1) ? J0 : I0) + row;
             const double *src = (a < 2) ? X : Y;
-            double2 v = make_double2(0.0, 0.0);
+            double2 t = make_double2(0.0, 0.0);
             if (grow < n && col < r) {
-                v = *reinterpret_cast<const double2 *>(src + (long)grow * ld + col);
-                if (col + 1 >= r) v.y = 0.0;
+                t = *reinterpret_cast<const double2 *>(src + (long)grow * ld + col);
+                if (col + 1 >= r) t.y = 0.0;
             }
-            *reinterpret_cast<double2 *>(&tl[a][o]) = v;
+            v[a][k] = t;
         }
+    }
+}
+template <int NA>
+__device__ __forceinline__ void auv_put(double (*tl)[kAuvT * kAuvS], const double2 (&v)[NA][kAuvPer]) {
+#pragma unroll
+    for (int k = 0; k < kAuvPer; ++k) {
+        const int x = threadIdx.x + k * kAuvThreads;
+        const int o = (x / (kAuvC / 2)) * kAuvS + 2 * (x % (kAuvC / 2));
+#pragma unroll
+        for (int a = 0; a < NA; ++a) *reinterpret_cast<double2 *>(&tl[a][o]) = v[a][k];
     }
 }
 
@@ -566,10 +581,13 @@ __global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, 
         ql[j] = (int)(w & 0xffffu) * kAuvS;
         acc[j] = 0.0;
     }
+    double2 pre[NA][kAuvPer];
+    auv_fetch<NA>(pre, I0, J0, 0, n, r, ld, X, Y);
     for (int c0 = 0; c0 < r; c0 += kAuvC) {
         __syncthreads();
-        auv_stage<NA>(tl, I0, J0, c0, n, r, ld, X, Y);
+        auv_put<NA>(tl, pre);
         __syncthreads();
+        if (c0 + kAuvC < r) auv_fetch<NA>(pre, I0, J0, c0 + kAuvC, n, r, ld, X, Y);   // in flight meanwhile
 #pragma unroll
         for (int j = 0; j < kAuvNpt; ++j) {
             if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
@@ -2965,7 +2983,7 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_a(
 // k_wide_a's work over 2-D tiles of the lower pattern (cones with DevCone::sa_items, e.g. C5's
 // ~570 lower slots per row): a work item is one (row tile, column tile) of kAuvT rows each and
 // up to kAuvItem of its slots; R and D of both tiles are staged in LDS kAuvC columns at a time
-// (auv_stage) and each thread evaluates its slots' sym(R D^T) and D D^T from there, instead of
+// (auv_fetch / auv_put) and each thread evaluates its slots' sym(R D^T) and D D^T from there, instead of
 // every lane group gathering ~570 neighbour rows of R and D per row.  The per-slot epilogue
 // (slot values, C and local-constraint terms, rec) is k_wide_a's.  Same grid and partial
 // slots as k_wide_a (blocks stride over the items), so the consumers are unchanged.
@@ -2999,8 +3017,10 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_a(
             s1[j] = 0.0;
         }
         for (int c0 = 0; c0 < r; c0 += kAuvC) {
+            double2 v[4][kAuvPer];
+            auv_fetch<4>(v, I0, J0, c0, n, r, ld, R, D);
             __syncthreads();
-            auv_stage<4>(tl, I0, J0, c0, n, r, ld, R, D);
+            auv_put<4>(tl, v);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < kAuvNpt; ++j) {
@@ -3243,8 +3263,10 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b1(
             dv[j] = 0.0;
         }
         for (int c0 = 0; c0 < r; c0 += kAuvC) {
+            double2 v[2][kAuvPer];
+            auv_fetch<2>(v, I0, J0, c0, n, r, ld, Rn, Rn);
             __syncthreads();
-            auv_stage<2>(tl, I0, J0, c0, n, r, ld, Rn, Rn);
+            auv_put<2>(tl, v);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < kAuvNpt; ++j) {
@@ -3296,6 +3318,23 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b1(
 
 constexpr int kTbC = 64;            // R_new columns staged per pass in k_tile_b2
 constexpr int kTbS = kTbC + 2;      // LDS row stride (16-B aligned rows)
+constexpr int kTbPer = kAuvT * kTbC / 2 / kRowBlock;   // double2 per thread per staged tile
+__device__ __forceinline__ void tb_fetch(double2 (&v)[kTbPer], int J0, int c0, int n, int r, int ld,
+                                         const double *__restrict__ Rn) {
+#pragma unroll
+    for (int k = 0; k < kTbPer; ++k) {
+        const int y = threadIdx.x + k * kRowBlock;
+        const int grow = J0 + y / (kTbC / 2), col = c0 + 2 * (y % (kTbC / 2));
+        double2 t = make_double2(0.0, 0.0);
+        if (grow < n && col < r) {
+            t = *reinterpret_cast<const double2 *>(Rn + (long)grow * ld + col);
+            if (col + 1 >= r) t.y = 0.0;
+        }
+        v[k] = t;
+    }
+}
+// grid: (row tile I, column group x) x column chunk; the chunk's kTbC columns of each tile
+// pair's R_new staged in LDS (the next pair's loads in flight during the current one).
 __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff, const int2 *__restrict__ blk,
                                                        const int2 *__restrict__ tp, const int *__restrict__ rp,
                                                        const int2 *__restrict__ ent, const double *__restrict__ Sv,
@@ -3306,47 +3345,47 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
     if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
     const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
     __shared__ double rj[kAuvT * kTbS];
-    const int I = blockIdx.x / kNX, x = blockIdx.x % kNX;
+    const int nch = (ld + kTbC - 1) / kTbC;
+    const int bx = blockIdx.x / nch, c0 = (blockIdx.x % nch) * kTbC;
+    const int I = bx / kNX, x = bx % kNX;
     const int pl = threadIdx.x >> 2, cq = threadIdx.x & 3;
     const int i = I * kAuvT + pl;
-    const int2 br = blk[blockIdx.x];
-    for (int c0 = 0; c0 < ld; c0 += kTbC) {
-        double g[16];
+    const int2 br = blk[bx];
+    double g[16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) g[c] = 0.0;
-        for (int q = br.x; q < br.y; ++q) {   // block-uniform
-            const int2 t = tp[q];
-            __syncthreads();
-            for (int y = threadIdx.x; y < kAuvT * kTbC / 2; y += kRowBlock) {
-                const int row = y / (kTbC / 2), col = c0 + 2 * (y % (kTbC / 2));
-                const int grow = t.x + row;
-                double2 v = make_double2(0.0, 0.0);
-                if (grow < n && col < r) {
-                    v = *reinterpret_cast<const double2 *>(Rn + (long)grow * ld + col);
-                    if (col + 1 >= r) v.y = 0.0;
-                }
-                *reinterpret_cast<double2 *>(&rj[row * kTbS + col - c0]) = v;
-            }
-            __syncthreads();
-            const int e1 = rp[t.y + pl + 1];
-            for (int e = rp[t.y + pl]; e < e1; ++e) {
-                const int2 en = ent[e];
-                const double s = Sv[en.y];
-                const double2 *src = reinterpret_cast<const double2 *>(&rj[en.x * kTbS + cq * 16]);
+    for (int c = 0; c < 16; ++c) g[c] = 0.0;
+    double2 pre[kTbPer];
+    int2 t = br.x < br.y ? tp[br.x] : make_int2(0, 0);
+    if (br.x < br.y) tb_fetch(pre, t.x, c0, n, r, ld, Rn);
+    for (int q = br.x; q < br.y; ++q) {   // block-uniform
+        const int2 cur = t;
+        if (q + 1 < br.y) t = tp[q + 1];
+        __syncthreads();
 #pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    const double2 v = src[c];
-                    g[2 * c] += s * v.x;
-                    g[2 * c + 1] += s * v.y;
-                }
+        for (int k = 0; k < kTbPer; ++k) {
+            const int y = threadIdx.x + k * kRowBlock;
+            *reinterpret_cast<double2 *>(&rj[(y / (kTbC / 2)) * kTbS + 2 * (y % (kTbC / 2))]) = pre[k];
+        }
+        __syncthreads();
+        if (q + 1 < br.y) tb_fetch(pre, t.x, c0, n, r, ld, Rn);
+        const int e1 = rp[cur.y + pl + 1];
+        for (int e = rp[cur.y + pl]; e < e1; ++e) {
+            const int2 en = ent[e];
+            const double s = Sv[en.y];
+            const double2 *src = reinterpret_cast<const double2 *>(&rj[en.x * kTbS + cq * 16]);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const double2 v = src[c];
+                g[2 * c] += s * v.x;
+                g[2 * c + 1] += s * v.y;
             }
         }
-        if (i < n) {
-            double *dst = GP + x * gstride + foff + (long)i * ld + c0 + cq * 16;
+    }
+    if (i < n) {
+        double *dst = GP + x * gstride + foff + (long)i * ld + c0 + cq * 16;
 #pragma unroll
-            for (int c = 0; c < 8; ++c)
-                if (c0 + cq * 16 + 2 * c < ld) reinterpret_cast<double2 *>(dst)[c] = make_double2(g[2 * c], g[2 * c + 1]);
-        }
+        for (int c = 0; c < 8; ++c)
+            if (c0 + cq * 16 + 2 * c < ld) reinterpret_cast<double2 *>(dst)[c] = make_double2(g[2 * c], g[2 * c + 1]);
     }
 }
 
@@ -4788,7 +4827,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur,
                                W.partC, off);
             LRS_CHECK_LAUNCH();
-            hipLaunchKernelGGL(k_tile_b2, dim3(c.sb_blocks), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
+            hipLaunchKernelGGL(k_tile_b2, dim3(c.sb_blocks * ((c.ld + kTbC - 1) / kTbC)), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
                                reinterpret_cast<const int2 *>(c.sb_blk), reinterpret_cast<const int2 *>(c.sb_tp),
                                c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent), c.sa_S - c.slot_off, W.R, W.R2,
                                W.GP, P.NRpad, c.r, ctrl_cur, ls_cur);
