@@ -136,6 +136,12 @@ def stage_roofline(sv, reps, with_traffic=False):
     ms = sv.time_stages(reps)
     by = sv.stage_bytes()
     ka, kb = STAGE_KERNELS.get(sv.kernel_path(), STAGE_KERNELS[1])
+    n0 = sv.dims[0]
+    # long-row cones over 2-D LDS tiles (the upload's rule in lrs_problem.cpp)
+    slot_tiles = len(sv.dims) == 1 and n0 >= 2048 and sv.nslots >= 32 * n0 and sv.kernel_path() == 1
+    auv_tiles = len(sv.dims) == 1 and n0 >= 2048 and sv.nnz >= 64 * n0
+    if slot_tiles:
+        ka, kb = "k_it_a + k_tile_a", "k_it_b + k_tile_b1 + k_tile_b2 + k_wide_bf"
     out = []
     for k in range(3):
         if ms[k] <= 0:
@@ -150,7 +156,9 @@ def stage_roofline(sv, reps, with_traffic=False):
     ams = sv.time_auut(reps)
     aby = sv.auut_bytes()
     agbs = aby / (ams * 1e-3) / 1e9
-    auut = {"kernel": "k_auv_con<XX^T> (A(UU^T) over constraint entries)", "avg_launch_us": ams * 1e3,
+    akern = ("k_auv_tile<1> + k_auv_tsum (A(UU^T) over 2-D LDS tiles of constraint entries)" if auv_tiles
+             else "k_auv_con<XX^T> (A(UU^T) over constraint entries)")
+    auut = {"kernel": akern, "avg_launch_us": ams * 1e3,
             "bytes_per_launch": aby, "achieved_GBs": agbs, "frac": agbs / HBM_PEAK_GBS}
     res = {"bound": "hbm", "kernel": dom["stage"], "achieved": dom["achieved_GBs"], "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": dom["frac"], "traffic": traffic, "bytes_per_launch": dom["bytes_per_launch"],
