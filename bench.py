@@ -138,8 +138,10 @@ def stage_roofline(sv, reps, with_traffic=False):
     ka, kb = STAGE_KERNELS.get(sv.kernel_path(), STAGE_KERNELS[1])
     n0 = sv.dims[0]
     # long-row cones over 2-D LDS tiles (the upload's rule in lrs_problem.cpp)
-    slot_tiles = len(sv.dims) == 1 and n0 >= 2048 and sv.nslots >= 32 * n0 and sv.kernel_path() == 1
-    auv_tiles = len(sv.dims) == 1 and n0 >= 2048 and sv.nnz >= 64 * n0
+    ntl = (n0 + 127) // 128
+    per_tile = 768 * ntl * (ntl + 1) / 2
+    slot_tiles = len(sv.dims) == 1 and n0 >= 2048 and sv.nslots >= per_tile and sv.kernel_path() == 1
+    auv_tiles = len(sv.dims) == 1 and n0 >= 2048 and sv.nnz >= per_tile
     if slot_tiles:
         ka, kb = "k_it_a + k_tile_a", "k_it_b + k_tile_b1 + k_tile_b2 + k_wide_bf"
     out = []

@@ -136,9 +136,11 @@ constexpr int kAuvC = 32;            // factor columns staged in LDS at a time
 constexpr int kAuvThreads = 512;
 constexpr int kAuvNpt = 8;           // entries per thread of one item
 constexpr int kAuvItem = kAuvThreads * kAuvNpt;
-constexpr int kAuvMinN = 2048;       // tiled when n >= this and the cone has >= kAuvMinDeg
-constexpr int kAuvMinDeg = 64;       //   constraint entries per row (LRS_AUV_TILES=0/1 overrides)
-constexpr int kSlotTileMinDeg = 32;  // lower pattern slots per row for k_tile_a (LRS_SLOT_TILES=0/1 overrides)
+constexpr int kAuvMinN = 2048;       // tiled when n >= this and the lower triangle's tiles hold on average
+constexpr int kAuvMinPerTile = 768;  //   >= this many entries (constraint entries for A(X Y^T), pattern slots
+                                     //   for the stage kernels: 3x reuse of each staged row); C5 ~1850, a
+                                     //   C5-structured m = 1e5 ~98 (slower tiled); LRS_AUV_TILES /
+                                     //   LRS_SLOT_TILES = 0/1 override
 constexpr int kNX = 8;              // column blocks of the tiled long-row kernels (one per XCD)
 constexpr int kTileMinDeg = 32;
 constexpr int kDenseRow = 64;        // entries of a row past which the latency kernels slice it

@@ -543,7 +543,8 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             const int n = hp.cones[k].n;
             const long eb = con_ptr[(long)k * m], ee = con_ptr[(long)k * m + m];
             const long Zk = ee - eb;
-            bool on = n >= kAuvMinN && Zk >= (long)kAuvMinDeg * n;
+            const double ntl = (double)((n + kAuvT - 1) / kAuvT);
+            bool on = n >= kAuvMinN && (double)Zk >= kAuvMinPerTile * ntl * (ntl + 1) / 2;
             if (ev && ev[0] == '0') on = false;
             if (ev && ev[0] == '1') on = Zk > 0;
             if (long_ptr[k + 1] > long_ptr[k]) on = false;
@@ -727,7 +728,8 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             // (row tile, column tile, row, column), items of at most kAuvItem slots
             const long P = (long)c.prow.size();
             const char *ev = getenv("LRS_SLOT_TILES");
-            bool on = c.n >= kAuvMinN && P >= (long)kSlotTileMinDeg * c.n;
+            const double ntl = (double)((c.n + kAuvT - 1) / kAuvT);
+            bool on = c.n >= kAuvMinN && (double)P >= kAuvMinPerTile * ntl * (ntl + 1) / 2;
             if (ev && ev[0] == '0') on = false;
             if (ev && ev[0] == '1') on = P > 0;
             if (on) {

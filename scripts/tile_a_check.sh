@@ -9,6 +9,8 @@ LRS_SLOT_TILES=0 timeout -k 10 600 python3 -u scripts/c5_probe.py 10000 1000000 
 cat gpurun_out/ta/c5_off.log
 timeout -k 10 600 python3 -u scripts/c5_probe.py 10000 1000000 128 30 > gpurun_out/ta/c5_on.log 2>&1
 cat gpurun_out/ta/c5_on.log
+timeout -k 10 300 python3 -u scripts/c5_probe.py 10000 100000 128 60 > gpurun_out/ta/c5_m1e5.log 2>&1
+cat gpurun_out/ta/c5_m1e5.log
 O=$GRAFT_REPO_ROOT/gpurun_out/ta; R=$GRAFT_REPO_ROOT
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/scripts/c5_probe.py 10000 1000000 128 30 > $O/trace.log 2>&1) || exit 1
 python3 - "$O/trace/run_kernel_stats.csv" <<'PY'

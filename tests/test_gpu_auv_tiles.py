@@ -1,7 +1,7 @@
 """A(X Y^T) over 2-D LDS tiles (k_auv_tile + k_auv_tsum, lrs_kernels.hip) against the
 per-entry gather k_auv_con and the reference's golden vectors (MI355X).
 
-The tiled path is taken for cones with >= kAuvMinDeg constraint entries per row at
+The tiled path is taken for cones whose lower-triangle tiles hold >= kAuvMinPerTile entries on average at
 n >= kAuvMinN (C5-like), or always with LRS_AUV_TILES=1 (read when the problem is
 uploaded).  Reference semantics: coneAUV data/lorads_sdp_conic.c:378-385 and
 LORADSUpdateConstrValCG lorads_admm.c:442-459.  Tolerances: the entry dot products are
