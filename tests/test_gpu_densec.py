@@ -154,7 +154,7 @@ def test_dense_and_slot_paths_agree_on_theta(solver_mod):
     assert abs(a["dinf"] - b["dinf"]) <= 0.05 * abs(a["dinf"]), (a["dinf"], b["dinf"])
 
 
-@pytest.mark.parametrize("kpath,tiles", [(0, "0"), (3, "0"), (3, "1")])
+@pytest.mark.parametrize("kpath,tiles", [(0, "0"), (3, "0"), (3, "1"), (3, "2d")])
 def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir, kpath, tiles, monkeypatch):
     """Past the fixtures' size (n = 2000, m = 100 000, r = 64; the reference's dense branches
     take minutes per trip here): the dense path and the slot path -- two independent
@@ -163,7 +163,12 @@ def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir, kpath
     path = _rdense(gen_dir, 2000, 100000, 6, 5)
     # tiles "1": the column-tiled long-row kernels (LRS_TILES, experimental, read at the
     # workspace allocation and the first enqueue of the process)
-    monkeypatch.setenv("LRS_TILES", tiles)
+    # tiles "2d": the 2-D LDS tiles of the long-row stages and of A(X Y^T) (DESIGN.md §4.5,
+    # read when the problem is loaded), on both the dense and the slot path
+    monkeypatch.setenv("LRS_TILES", "0" if tiles == "2d" else tiles)
+    if tiles == "2d":
+        monkeypatch.setenv("LRS_SLOT_TILES", "1")
+        monkeypatch.setenv("LRS_AUV_TILES", "1")
     out = {}
     for mode in ("0", "1"):
         with dense_mode(mode):
@@ -174,4 +179,8 @@ def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir, kpath
     for a, b in zip(out["0"], out["1"]):
         assert abs(a["tau"] - b["tau"]) <= TOL * abs(a["tau"]), (a["tau"], b["tau"])
         for key in ("R", "G", "cvs"):
-            assert rel_err(a[key], b[key]) < TOL, (key, rel_err(a[key], b[key]))
+            # with the 2-D tiles both paths' A(R R^T) sums each dot over r in sequence: the
+            # constraint values here are ~1e-11 cancellations of O(1) products, so they carry
+            # the iterate's 1e-16 differences amplified to ~1e-9 (R and G stay at 1e-9)
+            tol = 1e-8 if (tiles == "2d" and key == "cvs") else TOL
+            assert rel_err(a[key], b[key]) < tol, (key, rel_err(a[key], b[key]))
