@@ -3950,10 +3950,47 @@ static int small_team(const DevCone &c, bool lower) {
     return T;
 }
 
+// <C, out0> (and <C, out1>) over one cone's slots after the tiled SDDMM (k_sddmm's fin values)
+__global__ void __launch_bounds__(kBlock) k_slot_cdot(int s0, int P, const double *__restrict__ Cw,
+                                                      const double *__restrict__ out0,
+                                                      const double *__restrict__ out1, double *part,
+                                                      unsigned *ticket, double *fin) {
+    double acc[2] = {0.0, 0.0};
+    for (int s = s0 + blockIdx.x * kBlock + threadIdx.x; s < s0 + P; s += gridDim.x * kBlock) {
+        acc[0] += Cw[s] * out0[s];
+        if (out1) acc[1] += Cw[s] * out1[s];
+    }
+    partials_finalize<2>(acc, part, ticket, fin);
+}
+
 int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double *out0,
                  double *out1, double *part, int pblk_off, int *nblk_used, hipStream_t st) {
     (void)pblk_off;
     const DevCone &c = P.cones[cone];
+    if (c.sa_items > 0 && !P.shard) {
+        // long-row cone: the pattern SDDMM over the 2-D LDS tiles (k_auv_tile on the slot tiles,
+        // values stored per slot), then the objective sums in slot order
+        const double *Xc = X + c.foff, *Yc = Y ? Y + c.foff : nullptr;
+        const int4 *it = reinterpret_cast<const int4 *>(c.sa_item);
+        if (mode == 1)
+            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.sa_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, it,
+                               c.sa_pq, c.sa_slot, Xc, Xc, out0, nullptr);
+        else
+            hipLaunchKernelGGL((k_auv_tile<0>), dim3(c.sa_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, it,
+                               c.sa_pq, c.sa_slot, Xc, Yc, out0, nullptr);
+        LRS_CHECK_LAUNCH();
+        if (mode == 2) {
+            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.sa_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, it,
+                               c.sa_pq, c.sa_slot, Yc, Yc, out1, nullptr);
+            LRS_CHECK_LAUNCH();
+        }
+        const int grid = grid_elems(c.P, 4);
+        hipLaunchKernelGGL(k_slot_cdot, dim3(grid), dim3(kBlock), 0, st, c.slot_off, c.P, P.Cw, out0,
+                           mode == 2 ? out1 : nullptr, part, ticket_ptr(T_SDDMM), tmpfin_ptr() + TF_SD + 2 * cone);
+        LRS_CHECK_LAUNCH();
+        if (nblk_used) *nblk_used = grid;
+        return 0;
+    }
     const int T = small_team(c, true);
     const int grid = grid_rows((long)c.nown * T, c.G);
     double *fin = tmpfin_ptr() + TF_SD + 2 * cone;

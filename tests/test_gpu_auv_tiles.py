@@ -93,3 +93,25 @@ def test_tiled_path_whole_solve(solver_mod, monkeypatch):
     assert abs(a["admm_iter"] - b["admm_iter"]) <= 1
     assert abs(a["alm_pobj"] - b["alm_pobj"]) <= 1e-9 * max(1.0, abs(a["alm_pobj"]))
     assert abs(a["pobj"] - b["pobj"]) <= 1e-6 * max(1.0, abs(a["pobj"]))
+
+
+@pytest.mark.parametrize("name", KERNEL_CASES)
+def test_tiled_pattern_sddmm_matches_reference(solver_mod, name, monkeypatch):
+    """The pattern SDDMM (lrs_op_q12's sym(R D^T) / D D^T, lrs_op_constr_rr's R R^T and their
+    <C, .> sums) over the slot tiles (LRS_SLOT_TILES=1; C5-like cones by default) against the
+    reference's ALMCalq12p12 / primalInfeasibility / CalObjRR vectors at 1e-10."""
+    monkeypatch.setenv("LRS_SLOT_TILES", "1")
+    g = load_kernels(name)
+    s = split_inputs(g)
+    sv = solver_mod.Solver(instance(name))
+    sv.set_rank([s["rank"]] * len(s["dims"]))
+    sv.set_factor(solver_mod.R, s["R"])
+    sv.set_factor(solver_mod.D, s["D"])
+    q1, p1, q2, p2 = sv.q12()
+    assert rel_err(q1, g["q1"]) < TOL and rel_err(q2, g["q2"]) < TOL
+    assert abs(p1 - g["p1"]) <= TOL * max(1, abs(g["p1"])) and abs(p2 - g["p2"]) <= TOL * max(1, abs(g["p2"]))
+    cvs, pinf, pobj = sv.constr_rr()
+    assert rel_err(cvs, g["cvs_rr"]) < TOL
+    assert abs(pinf - g["pinf_rr"]) <= TOL * max(1, abs(g["pinf_rr"]))
+    assert abs(pobj - g["pobj_rr"]) <= TOL * max(1, abs(g["pobj_rr"]))
+    sv.close()
