@@ -197,6 +197,7 @@ struct DevProblem {
     std::vector<DevCone> cones;
     int ndense = 0;                                          // cones with a dense objective (DevCone::Cd)
     bool tiles = false;                                      // column-tiled long-row kernels (LRS_TILES=1 at alloc)
+    double *gp = nullptr;                                    // DevWork::GP (kNX partial factors), the tiled S X's scratch
     double dense_scale = 1.0;                                // objScale_dualvar's factor on those C
     // K > 1: all cones as one block-diagonal row space (global rows and columns); used by
     // the split iteration when every cone has the same (G, E) row layout

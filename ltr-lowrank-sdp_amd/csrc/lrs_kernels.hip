@@ -3342,8 +3342,9 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
                                                        long gstride, int r, const double *__restrict__ ctrl,
                                                        const double *__restrict__ ls_cur) {
     static_assert(kRowBlock == 4 * kAuvT, "k_tile_b2: four threads per tile row");
-    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
-    const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
+    // ctrl == nullptr: the standalone S X of launch_spmm (X in Rb0)
+    if (ctrl && (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0)) return;
+    const double *__restrict__ Rn = ((ctrl && ctrl[C_RCUR] == 0.0) ? Rb1 : Rb0) + foff;
     __shared__ double rj[kAuvT * kTbS];
     const int nch = (ld + kTbC - 1) / kTbC;
     const int bx = blockIdx.x / nch, c0 = (blockIdx.x % nch) * kTbC;
@@ -4088,10 +4089,46 @@ int launch_wsum(const DevProblem &P, const double *w, int withC, double *S, hipS
     return 0;
 }
 
+// launch_spmm over the tiles: out = scale (sum of the kNX partial rows in group order) +
+// addScale addX over the cone's n x ld block, and the partial ||out||^2 (k_spmm's epilogue)
+__global__ void __launch_bounds__(kBlock) k_spmm_fin(long len, const double *__restrict__ GP, long gstride,
+                                                     double scale, const double *__restrict__ addX,
+                                                     double addScale, double *__restrict__ out, double *part,
+                                                     unsigned *ticket, double *fin) {
+    double nrm[1] = {0.0};
+    for (long i = (long)blockIdx.x * kBlock + threadIdx.x; i < len; i += (long)gridDim.x * kBlock) {
+        double g = GP[i];
+#pragma unroll
+        for (int x = 1; x < kNX; ++x) g += GP[x * gstride + i];
+        double v = g * scale;
+        if (addX) v += addScale * addX[i];
+        out[i] = v;
+        nrm[0] += v * v;
+    }
+    if (part) partials_finalize<1>(nrm, part, ticket, fin);
+}
+
 int launch_spmm(const DevProblem &P, int cone, const double *S, const double *X, double scale, const double *addX,
                 double addScale, double *out, double *part, int pblk_off, int *nblk_used, hipStream_t st) {
     (void)pblk_off;
     const DevCone &c = P.cones[cone];
+    if (c.sb_blocks > 0 && P.gp && !P.shard) {
+        // long-row cone: S X per (row tile, column group) from staged X tiles into P.gp's kNX
+        // partial rows (k_tile_b2 without the iteration's control), then the sum and epilogue
+        hipLaunchKernelGGL(k_tile_b2, dim3(c.sb_blocks * ((c.ld + kTbC - 1) / kTbC)), dim3(kRowBlock), 0, st, c.n,
+                           c.ld, c.foff, reinterpret_cast<const int2 *>(c.sb_blk),
+                           reinterpret_cast<const int2 *>(c.sb_tp), c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent),
+                           S, X, X, P.gp, P.NRpad, c.r, nullptr, nullptr);
+        LRS_CHECK_LAUNCH();
+        const long len = (long)c.n * c.ld;
+        const int grid = grid_elems(len, 8);
+        hipLaunchKernelGGL(k_spmm_fin, dim3(grid), dim3(kBlock), 0, st, len, P.gp + c.foff, P.NRpad, scale,
+                           addX ? addX + c.foff : nullptr, addScale, out + c.foff, part, ticket_ptr(T_SPMM),
+                           tmpfin_ptr() + TF_SPMM + cone);
+        LRS_CHECK_LAUNCH();
+        if (nblk_used) *nblk_used = grid;
+        return 0;
+    }
     const int T = small_team(c, false);
     const int grid = grid_rows((long)c.nown * T, c.G);
     double *fin = tmpfin_ptr() + TF_SPMM + cone;

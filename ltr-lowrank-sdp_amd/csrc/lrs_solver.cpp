@@ -428,6 +428,7 @@ static void free_work(lrs_ctx *c) {
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     c->W = DevWork();
+    c->dp.gp = nullptr;
     c->walloc = false;
 }
 
@@ -503,6 +504,7 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         bool btiles = false;   // long-row B over 2-D tiles (DevCone::sb_blocks): k_wide_bf's partial rows
         for (const auto &dc : P.cones) btiles = btiles || dc.sb_blocks > 0;
         if ((tiles || btiles) && A(&W.GP, (long)kNX * NR)) return -1;
+        P.gp = W.GP;
         P.tiles = tiles;
     }
     HIPC(hipStreamSynchronize(c->st));

@@ -98,7 +98,7 @@ def test_tiled_path_whole_solve(solver_mod, monkeypatch):
 @pytest.mark.parametrize("name", KERNEL_CASES)
 def test_tiled_pattern_sddmm_matches_reference(solver_mod, name, monkeypatch):
     """The pattern SDDMM (lrs_op_q12's sym(R D^T) / D D^T, lrs_op_constr_rr's R R^T and their
-    <C, .> sums) over the slot tiles (LRS_SLOT_TILES=1; C5-like cones by default) against the
+    <C, .> sums) and the SpMM (gradient, ADMM half step) over the slot tiles (LRS_SLOT_TILES=1; C5-like cones by default) against the
     reference's ALMCalq12p12 / primalInfeasibility / CalObjRR vectors at 1e-10."""
     monkeypatch.setenv("LRS_SLOT_TILES", "1")
     g = load_kernels(name)
@@ -114,4 +114,18 @@ def test_tiled_pattern_sddmm_matches_reference(solver_mod, name, monkeypatch):
     assert rel_err(cvs, g["cvs_rr"]) < TOL
     assert abs(pinf - g["pinf_rr"]) <= TOL * max(1, abs(g["pinf_rr"]))
     assert abs(pobj - g["pobj_rr"]) <= TOL * max(1, abs(g["pobj_rr"]))
+    # ALMCalGrad and the ADMM half step: S R / S Y over the tiles (launch_spmm -> k_tile_b2 +
+    # k_spmm_fin)
+    sv.set_vec(solver_mod.LAMBDA, s["lam"])
+    sv.set_vec(solver_mod.CVS, s["cvs"])
+    G, lag = sv.grad(s["rho"])
+    assert rel_err(G, g["grad"]) < TOL
+    assert abs(lag - g["lag"]) <= TOL * g["lag"]
+    sv.set_factor(solver_mod.U, s["U"])
+    sv.set_factor(solver_mod.V, s["V"])
+    sv.set_vec(solver_mod.LAMBDA, s["lam"])
+    u, rhs, it = sv.admm_half(s["rho_admm"], s["cg_tol"])
+    assert rel_err(rhs, g["rhs_cg"]) < TOL
+    assert rel_err(u, g["u_cg"]) < 1e-6
+    assert abs(it - g["cg_iters"]) <= max(2, 0.1 * g["cg_iters"])
     sv.close()
