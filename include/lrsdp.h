@@ -60,8 +60,14 @@ typedef struct {
     int traj1_len, traj2_len;
     double rho_max;      /* params.rhoMax after LORADS_ALMtoADMM (written to the JSON) */
     double dinf, dinf_inf, dinf_2;   /* dual infeasibility l_1 / l_inf / l_2 (main.c:515-521); -1 if not evaluated */
-    int dinf_converged;  /* 1: every cone's Lanczos met its residual test; 0: a step cap was hit (dinf is then a
-                            lower bound and status 1 is withheld); -1: not evaluated */
+    int dinf_converged;  /* 1: every cone's eigen-solve met its test (ARPACK's tol 1e-2 relative Ritz estimate,
+                            or an absolute one that pins the l_1 value to 1e-3 phase2Tol); 0: the 600 update
+                            iterations ran out (dinf is then a lower bound and status 1 is withheld); -1: not
+                            evaluated */
+    int dinf_iters;      /* thick-restart update iterations (dsaupd's iparam(3) count) over cones and calls */
+    long dinf_steps;     /* Lanczos steps (matrix-vector products) over cones and calls */
+    double dinf_time;    /* seconds in the dual-infeasibility eigen-solves (inside solve_time, as main.c:515-521) */
+    double obj_scale;    /* scaleObjHis at the end (the reopt rounds' objScale_dualvar factors; 1 without reopt) */
 } lrs_result;
 
 /* factor / vector selectors */
@@ -197,6 +203,13 @@ int lrs_profile_stages(lrs_ctx *ctx, const lrs_params *p, long steps, double *st
  * col, val) with 1-based blk/row/col and con 0 = F0 (C = -F0). */
 int lrs_load_coo(lrs_ctx *ctx, int m, int nblk, const int *dims, const double *b, long nnz, const int *con,
                  const int *blk, const int *row, const int *col, const double *val);
+
+/* Which kernels the upload chose for the long-row cones: *auv = 1 when
+ * some cone's constraint entries are in 2-D LDS tiles (A(XY^T) by k_auv_tile), *slot = 1
+ * when some cone's lower pattern is (stage A / B and S X by k_tile_a / k_tile_b1/b2).  No
+ * reference counterpart (the reference's 10 % dense rule picks a BLAS-3 branch instead,
+ * data/lorads_sdp_data.c:1187-1193). */
+int lrs_tile_info(lrs_ctx *ctx, int *auv, int *slot);
 
 /* Algorithmic HBM bytes per launch of the split-iteration stages A, G, B at the
  * current ranks (the roofline numerators, DESIGN.md "Kernels"). */

@@ -286,9 +286,6 @@ int launch_dense_cx(const DevProblem &P, int cone, const double *X, double *Y, d
 // (R: the current iterate by the control block); returns the partial blocks written
 int dense_cd_blocks(const DevProblem &P);
 int launch_dense_cd(const DevProblem &P, const DevWork &W, const double *ctrl, int off, hipStream_t st);
-// Lanczos step add-on: y_j += scale C q_j (dense cone)
-int launch_lanczos_dense(const DevProblem &P, int cone, double *Q, long ldq, double *w0, double *w1, const int *jp,
-                         hipStream_t st);
 
 // ---- fused ALM inner iteration (device-side control; see lrs_kernels.hip) ----
 struct AlmIterArgs {
@@ -325,9 +322,20 @@ int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, i
 int launch_symv(const DevProblem &P, int cone, const double *S, const double *x, double *y, hipStream_t st);
 // w -= Q (Q^T w): Q column-major n x k (leading dimension ldq); part >= 64 k doubles, h >= k
 int launch_reorth(int n, int k, const double *Q, long ldq, double *w, double *part, double *h, hipStream_t st);
-int launch_lanczos_step(const DevProblem &P, int cone, const double *S, int kmax, double *Q, long ldq, double *w0,
-                        double *w1, int *jp, double *al, double *bw2, double *part, hipStream_t st);
-constexpr int kLzStepCap = 300;   // Lanczos steps at most (the device step kernels take up to 512)
+// thick-restart Lanczos (ARPACK dsaupd semantics, lrs_solver.cpp trl_min): one step's launches.
+// Vectors are cone-local rows; norm / dots / sub / restart take pointers pre-offset to the first
+// owned row and n = owned rows; symv runs the cone's owned rows [row0, row0 + nown) itself.
+constexpr int kTrlMaxV = 64;   // basis vectors at most (ncv = 40 in the reference)
+int trl_nblk(int n);           // partial blocks per column of launch_trl_dots
+int launch_trl_norm(int n, const double *w, const double *b2, double *vj, hipStream_t st);
+// y = S (x / sqrt(*b2)) (+ scale C v on a dense cone); vj (optional) = x / sqrt(*b2); b2 = null: 1
+int launch_trl_symv(const DevProblem &P, int cone, const double *S, const double *x, const double *b2, double *vj,
+                    double *y, hipStream_t st);
+int launch_trl_dots(int n, const double *V, long ldv, int k, const double *y, double *part, hipStream_t st);
+int launch_trl_fold(int k, int nb, const double *part, double *tot, hipStream_t st);
+int launch_trl_sub(int n, const double *V, long ldv, int k, const double *part, int nb, double *y, double *Hc,
+                   int pass, double *npart, double *bw2, hipStream_t st);
+int launch_trl_restart(int n, const double *V, long ldv, int m, const double *Y, int kk, double *Vt, hipStream_t st);
 
 // per-context scratch of the standalone reductions for the calling thread (nullptr: globals)
 void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart);

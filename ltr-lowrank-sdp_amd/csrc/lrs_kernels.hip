@@ -3487,98 +3487,111 @@ __global__ void __launch_bounds__(kBlock) k_gemv_sub(int n, int k, const double 
     }
 }
 
-// ---- Lanczos steps with no host round trip (dual infeasibility).  The step index j lives in
-// device memory (*jp), so one captured step graph is replayed for every step.  Step j: the
-// input residual is Q[0] (j = 0) or the previous step's output (w0 for odd j, w1 for even
-// j > 0), with beta_{j-1}^2 = bw2[j - 1]; the output residual goes to w1 (odd j) or w0.
-__device__ __forceinline__ void lz_bufs(int j, const double *Q, double *w0, double *w1, const double **win,
-                                        double **wout) {
-    *win = j == 0 ? Q : ((j & 1) ? w0 : w1);
-    *wout = (j & 1) ? w1 : w0;
+// ---- Thick-restart Lanczos steps (dual infeasibility, lrs_solver.cpp trl_min).  The host
+// drives step j of a cycle with plain launches (no captured graphs: every argument,
+// dense_scale included, is the current one).  Vectors are the cone's local rows (a sharded
+// solve: owned + halo, the kernels touch the owned rows [r0, r0 + nown) only); the basis
+// V holds ncv + 1 vectors of ldv doubles.  Step j: v_j = w / beta_{j-1} (beta^2 read from
+// device memory; 0 -> v_j = 0, so a breakdown never produces NaN), y = S v_j, two passes of
+// classical Gram-Schmidt against v_0..v_j whose coefficients (the entries of V^T S V) go to
+// column j of H, and ||y||^2 (beta_j^2) to bw2[j].
+__device__ __forceinline__ double trl_inv(const double *b2) {
+    if (!b2) return 1.0;
+    const double v = *b2;
+    return v > 1e-300 ? 1.0 / sqrt(v) : 0.0;
 }
-// q_j = w / beta_{j-1} into Q[j]; y = S q_j - beta_{j-1} q_{j-1}.  alpha_j is not formed here:
-// the reorthogonalisation against Q[0..j] removes the q_j component, and alpha_j is the sum of
-// its two passes' j-th coefficients (the entries of Q^T S Q, as in Arnoldi).
+// vj[i] = w[i] * inv over rows [0, n) (pointers pre-offset to the first owned row)
+__global__ void __launch_bounds__(kBlock) k_trl_norm(int n, const double *__restrict__ w,
+                                                     const double *__restrict__ b2, double *__restrict__ vj) {
+    const double inv = trl_inv(b2);
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) vj[i] = w[i] * inv;
+}
+// y = S (x inv) over rows [r0, r0 + n) (x read at any local row); vj (optional) = x inv on
+// those rows.  A thread per row, or a wave per row (WAVE, long rows).
 template <bool WAVE>
-__global__ void __launch_bounds__(kBlock) k_lz_symv(int n, const int *__restrict__ adj_ptr,
-                                                    const int *__restrict__ adj_col, const int *__restrict__ adj_slot,
-                                                    const double *__restrict__ S, double *w0, double *w1,
-                                                    const double *__restrict__ bw2, const int *__restrict__ jp,
-                                                    double *Q, long ldq) {
-    const int j = *jp;
-    const double *w;
-    double *y;
-    lz_bufs(j, Q, w0, w1, &w, &y);
-    const double beta = j > 0 ? sqrt(fmax(bw2[j - 1], 0.0)) : 1.0;
-    const double inv = 1.0 / beta;
-    double *qj = Q + (long)j * ldq;
-    const double *qp = Q + (long)(j > 0 ? j - 1 : 0) * ldq;
-    const double bp = j > 0 ? beta : 0.0;
+__global__ void __launch_bounds__(kBlock) k_trl_symv(int n, int r0, const int *__restrict__ adj_ptr,
+                                                     const int *__restrict__ adj_col, const int *__restrict__ adj_slot,
+                                                     const double *__restrict__ S, const double *x,
+                                                     const double *__restrict__ b2, double *vj, double *__restrict__ y) {
+    const double inv = trl_inv(b2);
     if constexpr (WAVE) {
         const int lane = threadIdx.x & 63;
         const int nw = gridDim.x * (kBlock / 64);
-        for (int i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < n; i += nw) {
+        for (int i = r0 + blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < r0 + n; i += nw) {
             double t = 0.0;
-            for (int k = adj_ptr[i] + lane; k < adj_ptr[i + 1]; k += 64) t += S[adj_slot[k]] * (w[adj_col[k]] * inv);
+            for (int k = adj_ptr[i] + lane; k < adj_ptr[i + 1]; k += 64) t += S[adj_slot[k]] * x[adj_col[k]];
             t = wave_sum(t);
             if (lane == 0) {
-                if (j > 0) qj[i] = w[i] * inv;
-                y[i] = -bp * qp[i] + t;
+                y[i] = t * inv;
+                if (vj) vj[i] = x[i] * inv;
             }
         }
     } else {
-        for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        for (int i = r0 + blockIdx.x * kBlock + threadIdx.x; i < r0 + n; i += gridDim.x * kBlock) {
             double t = 0.0;
-            for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) t += S[adj_slot[k]] * (w[adj_col[k]] * inv);
-            if (j > 0) qj[i] = w[i] * inv;
-            y[i] = -bp * qp[i] + t;
+            for (int k = adj_ptr[i]; k < adj_ptr[i + 1]; ++k) t += S[adj_slot[k]] * x[adj_col[k]];
+            y[i] = t * inv;
+            if (vj) vj[i] = x[i] * inv;
         }
     }
 }
-// part[c][blockIdx.x] = sum over this block's rows of Q[c][i] y[i], c = blockIdx.y <= j
-__global__ void __launch_bounds__(kBlock) k_lz_gemvt_part(int n, const double *Q, long ldq, double *w0, double *w1,
-                                                          const int *__restrict__ jp, double *__restrict__ part) {
-    const int j = *jp;
+// dense objective: y += scale C v over the cone's rows (one wave per row)
+__global__ void __launch_bounds__(kBlock) k_trl_dense(int n, double scale, const double *__restrict__ Cd,
+                                                      const double *__restrict__ v, double *__restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int nw = gridDim.x * (kBlock / 64);
+    for (int i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < n; i += nw) {
+        const double *__restrict__ ci = Cd + (long)i * n;
+        double t = 0.0;
+        for (int k = lane; k < n; k += 64) t += ci[k] * v[k];
+        t = wave_sum(t);
+        if (lane == 0) y[i] += scale * t;
+    }
+}
+// part[c][blockIdx.x] = sum over this block's rows of V[c][i] y[i], c = blockIdx.y
+__global__ void __launch_bounds__(kBlock) k_trl_dots(int n, const double *__restrict__ V, long ldv,
+                                                     const double *__restrict__ y, double *__restrict__ part) {
     const int c = blockIdx.y;
-    if (c > j) return;
-    const double *w;
-    double *y;
-    lz_bufs(j, Q, w0, w1, &w, &y);
     double a[1] = {0.0};
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) a[0] += Q[c * ldq + i] * y[i];
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) a[0] += V[c * ldv + i] * y[i];
     double s[1];
     block_reduce<1>(a, s);
     if (threadIdx.x == 0) part[(long)c * gridDim.x + blockIdx.x] = s[0];
 }
-// y -= Q h with h[c] = sum of the partials (block order), c <= j < kLzMaxSteps.  A block takes
+// tot[c] = sum of column c's nb partials in block order (sharded: before the all-reduce)
+__global__ void __launch_bounds__(kBlock) k_trl_fold(int k, int nb, const double *__restrict__ part,
+                                                     double *__restrict__ tot) {
+    for (int c = threadIdx.x; c < k; c += kBlock) {
+        double t = 0.0;
+        for (int b = 0; b < nb; ++b) t += part[(long)c * nb + b];
+        tot[c] = t;
+    }
+}
+// y -= V h, h[c] = sum of column c's partials (block order), c < k <= kTrlMaxV.  A block takes
 // 64 rows; its four waves split the columns (wave w: c = w, w + 4, ...), a lane per row, and
-// the waves' sums meet in LDS in wave order.  Pass 0 records alpha_j = h[j], pass 1 adds its
-// h[j], forms ||y||^2 (the last block sums the block partials in order) and advances j.
-constexpr int kLzMaxSteps = 512;
-__global__ void __launch_bounds__(kBlock) k_lz_gemv_sub(int n, const double *Q, long ldq, double *w0, double *w1,
-                                                        int *jp, const double *__restrict__ part, int nb, int pass,
-                                                        double *al, double *npart, unsigned *ticket, double *bw2) {
+// the waves' sums meet in LDS in wave order.  Pass 0 stores h into H's column, pass 1 adds its
+// h and reduces ||y||^2 into *bw2 (the last block sums the block partials in order).
+__global__ void __launch_bounds__(kBlock) k_trl_sub(int n, const double *__restrict__ V, long ldv, int k,
+                                                    const double *__restrict__ part, int nb, double *__restrict__ y,
+                                                    double *__restrict__ Hc, int pass, double *npart, unsigned *ticket,
+                                                    double *bw2) {
     static_assert(kBlock == 256, "four waves per block");
-    __shared__ double h[kLzMaxSteps];
+    __shared__ double h[kTrlMaxV];
     __shared__ double ws[4][64];
-    const int j = *jp, k = j + 1;
-    const double *w;
-    double *y;
-    lz_bufs(j, Q, w0, w1, &w, &y);
     for (int c = threadIdx.x; c < k; c += kBlock) {
         double t = 0.0;
         for (int b = 0; b < nb; ++b) t += part[(long)c * nb + b];
         h[c] = t;
+        if (blockIdx.x == 0) Hc[c] = pass == 0 ? t : Hc[c] + t;
     }
     __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x == 0) al[j] = pass == 0 ? h[j] : al[j] + h[j];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double acc[1] = {0.0};
     for (int i0 = blockIdx.x * 64; i0 < n; i0 += gridDim.x * 64) {   // block-uniform
         const int i = i0 + lane;
         double t = 0.0;
         if (i < n)
-            for (int c = wv; c < k; c += 4) t += Q[c * ldq + i] * h[c];
+            for (int c = wv; c < k; c += 4) t += V[c * ldv + i] * h[c];
         ws[wv][lane] = t;
         __syncthreads();
         if (wv == 0 && i < n) {
@@ -3588,68 +3601,80 @@ __global__ void __launch_bounds__(kBlock) k_lz_gemv_sub(int n, const double *Q, 
         }
         __syncthreads();
     }
-    if (pass == 1) partials_finalize<1>(acc, npart, ticket, bw2 + j, jp);
+    if (pass == 1) partials_finalize<1>(acc, npart, ticket, bw2);
+}
+// thick restart: Vt[c][i] = sum_q V[q][i] Y[q][c] (Y: m x kk row-major), c < kk
+__global__ void __launch_bounds__(kBlock) k_trl_restart(int n, const double *__restrict__ V, long ldv, int m,
+                                                        const double *__restrict__ Y, int kk, double *__restrict__ Vt) {
+    const int c = blockIdx.y;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        double t = 0.0;
+        for (int q = 0; q < m; ++q) t += V[q * ldv + i] * Y[q * kk + c];
+        Vt[c * ldv + i] = t;
+    }
 }
 
 static unsigned *ticket_ptr(int id);
-// One Lanczos step (step index *jp on the device, advanced at the end) on cone `cone`: the
-// launches are step-invariant, so the caller captures them once and replays the graph.
-int launch_lanczos_step(const DevProblem &P, int cone, const double *S, int kmax, double *Q, long ldq, double *w0,
-                        double *w1, int *jp, double *al, double *bw2, double *part, hipStream_t st) {
+int trl_nblk(int n) { return std::max(1, std::min(64, (n + kBlock * 8 - 1) / (kBlock * 8))); }
+
+int launch_trl_norm(int n, const double *w, const double *b2, double *vj, hipStream_t st) {
+    hipLaunchKernelGGL(k_trl_norm, dim3(grid_elems(n, 4)), dim3(kBlock), 0, st, n, w, b2, vj);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+int launch_trl_symv(const DevProblem &P, int cone, const double *S, const double *x, const double *b2, double *vj,
+                    double *y, hipStream_t st) {
     const DevCone &c = P.cones[cone];
-    const int n = c.n;
-    if (kmax > kLzMaxSteps) {
-        snprintf(g_err, sizeof(g_err), "lanczos: %d steps past %d", kmax, kLzMaxSteps);
-        return -1;
-    }
+    const int n = c.nown, r0 = c.row0;
     const double deg = c.n > 0 ? (double)c.adj_nnz / c.n : 0.0;
     if (deg > 32.0) {
-        const int ga = std::max(1, std::min(256, (n + kBlock / 64 - 1) / (kBlock / 64)));
-        hipLaunchKernelGGL(k_lz_symv<true>, dim3(ga), dim3(kBlock), 0, st, n, c.adj_ptr, c.adj_col, c.adj_slot, S, w0,
-                           w1, bw2, jp, Q, ldq);
+        const int ga = std::max(1, std::min(4096, (n + kBlock / 64 - 1) / (kBlock / 64)));
+        hipLaunchKernelGGL(k_trl_symv<true>, dim3(ga), dim3(kBlock), 0, st, n, r0, c.adj_ptr, c.adj_col, c.adj_slot, S,
+                           x, b2, vj, y);
     } else {
-        const int ga = std::max(1, std::min(256, (n + kBlock - 1) / kBlock));
-        hipLaunchKernelGGL(k_lz_symv<false>, dim3(ga), dim3(kBlock), 0, st, n, c.adj_ptr, c.adj_col, c.adj_slot, S, w0,
-                           w1, bw2, jp, Q, ldq);
+        hipLaunchKernelGGL(k_trl_symv<false>, dim3(grid_elems(n, 1)), dim3(kBlock), 0, st, n, r0, c.adj_ptr, c.adj_col,
+                           c.adj_slot, S, x, b2, vj, y);
     }
     LRS_CHECK_LAUNCH();
-    if (c.dense_c && launch_lanczos_dense(P, cone, Q, ldq, w0, w1, jp, st)) return -1;
-    const int nb = std::max(1, std::min(64, (n + kBlock * 8 - 1) / (kBlock * 8)));
-    double *gpart = part + kMaxPartialBlocks;   // past the norm partials
-    for (int t = 0; t < 2; ++t) {
-        hipLaunchKernelGGL(k_lz_gemvt_part, dim3(nb, kmax), dim3(kBlock), 0, st, n, Q, ldq, w0, w1, jp, gpart);
-        LRS_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_lz_gemv_sub, dim3(std::min((n + 63) / 64, kMaxPartialBlocks)), dim3(kBlock), 0, st, n,
-                           Q, ldq, w0, w1, jp, gpart, nb, t, al, part, ticket_ptr(T_DOT), bw2);
+    if (c.dense_c) {   // y += scale C v (v = vj, already normalized by the caller)
+        if (!vj && b2) {
+            snprintf(g_err, sizeof(g_err), "trl: dense cone needs the normalized vector");
+            return -1;
+        }
+        const int grid = std::max(1, std::min(2048, (c.n + kBlock / 64 - 1) / (kBlock / 64)));
+        hipLaunchKernelGGL(k_trl_dense, dim3(grid), dim3(kBlock), 0, st, c.n, P.dense_scale, c.Cd, vj ? vj : x, y);
         LRS_CHECK_LAUNCH();
     }
     return 0;
 }
 
-// Lanczos step on a dense-objective cone: y_j += scale C q_j after k_lz_symv (one wave per row)
-__global__ void __launch_bounds__(kBlock) k_lz_dense(int n, double scale, const double *__restrict__ Cd, double *Q,
-                                                     long ldq, double *w0, double *w1, const int *__restrict__ jp) {
-    const int j = *jp;
-    const double *w;
-    double *y;
-    lz_bufs(j, Q, w0, w1, &w, &y);
-    const double *__restrict__ qj = Q + (long)j * ldq;
-    const int lane = threadIdx.x & 63;
-    const int nw = gridDim.x * (kBlock / 64);
-    for (int i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < n; i += nw) {
-        const double *__restrict__ ci = Cd + (long)i * n;
-        double t = 0.0;
-        for (int k = lane; k < n; k += 64) t += ci[k] * qj[k];
-        t = wave_sum(t);
-        if (lane == 0) y[i] += scale * t;
-    }
+int launch_trl_dots(int n, const double *V, long ldv, int k, const double *y, double *part, hipStream_t st) {
+    hipLaunchKernelGGL(k_trl_dots, dim3(trl_nblk(n), k), dim3(kBlock), 0, st, n, V, ldv, y, part);
+    LRS_CHECK_LAUNCH();
+    return 0;
 }
-int launch_lanczos_dense(const DevProblem &P, int cone, double *Q, long ldq, double *w0, double *w1, const int *jp,
-                         hipStream_t st) {
-    const DevCone &c = P.cones[cone];
-    if (!c.dense_c) return 0;
-    const int grid = std::max(1, std::min(2048, (c.n + kBlock / 64 - 1) / (kBlock / 64)));
-    hipLaunchKernelGGL(k_lz_dense, dim3(grid), dim3(kBlock), 0, st, c.n, P.dense_scale, c.Cd, Q, ldq, w0, w1, jp);
+
+int launch_trl_fold(int k, int nb, const double *part, double *tot, hipStream_t st) {
+    hipLaunchKernelGGL(k_trl_fold, dim3(1), dim3(kBlock), 0, st, k, nb, part, tot);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+int launch_trl_sub(int n, const double *V, long ldv, int k, const double *part, int nb, double *y, double *Hc,
+                   int pass, double *npart, double *bw2, hipStream_t st) {
+    if (k > kTrlMaxV) {
+        snprintf(g_err, sizeof(g_err), "trl: %d basis vectors past %d", k, kTrlMaxV);
+        return -1;
+    }
+    hipLaunchKernelGGL(k_trl_sub, dim3(std::max(1, std::min((n + 63) / 64, kMaxPartialBlocks))), dim3(kBlock), 0, st, n,
+                       V, ldv, k, part, nb, y, Hc, pass, npart, ticket_ptr(T_DOT), bw2);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+int launch_trl_restart(int n, const double *V, long ldv, int m, const double *Y, int kk, double *Vt, hipStream_t st) {
+    hipLaunchKernelGGL(k_trl_restart, dim3(grid_elems(n, 1), kk), dim3(kBlock), 0, st, n, V, ldv, m, Y, kk, Vt);
     LRS_CHECK_LAUNCH();
     return 0;
 }

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <condition_variable>
+#include <limits>
 #include <map>
 #include <mutex>
 #include <string>
@@ -134,17 +135,20 @@ struct lrs_ctx {
     // hipGraph cache of inner-iteration batches (keyed by batch size; the kernels'
     // arguments are the workspace pointers, so a new workspace drops the cache)
     std::map<int, hipGraphExec_t> graphs;
-    // per-cone Lanczos workspace and its two captured graphs (one step, a chunk of steps),
-    // kept across calls: no per-call device allocation around a graph replay
+    // per-cone thick-restart Lanczos workspace (dual infeasibility), kept across calls and
+    // re-allocated only when the cone's local row count changes; no captured graphs
     struct LzWork {
-        int n = 0, kmax = 0;
-        const double *S = nullptr;
-        const int *adj = nullptr;
-        double *Q = nullptr, *w0 = nullptr, *w1 = nullptr, *part = nullptr, *coef = nullptr;
-        int *jp = nullptr;
-        hipGraphExec_t ge[2] = {nullptr, nullptr};
+        int n = 0;                 // local rows the buffers are sized for
+        double *V = nullptr;       // basis: kTrlMaxV + 1 vectors of n doubles
+        double *Vt = nullptr;      // restart product (kTrlMaxV vectors)
+        double *y[2] = {nullptr, nullptr};
+        double *part = nullptr;    // dot partials [kTrlMaxV][64] + norm partials [kMaxPartialBlocks]
+        double *H = nullptr;       // coefficient columns [kTrlMaxV][kTrlMaxV + 1] + bw2 [kTrlMaxV] + tot
+        double *Y = nullptr;       // restart coefficients (ncv x kk)
     };
     std::vector<LzWork> lz;
+    double *d_sendvec = nullptr;   // sharded: packed send rows of one Lanczos vector
+    long sendvec_len = 0;
     // initial point cache (device layout, host copy) for the ranks it was drawn at
     std::vector<int> init_ranks;
     std::vector<double> init_cache;
@@ -187,6 +191,9 @@ struct lrs_ctx {
     double last_ctl[C_NCTRL] = {0};
     double last_trip[3] = {0, 0, 0};   // tau, ||G||^2, pinf of the last completed inner trip
     double dinf_tol = 1e-5;            // phase2Tol of the running solve (dual-infeasibility accuracy)
+    long dinf_steps = 0, dinf_iters = 0;   // eigen-solve work of the running solve
+    bool rank_warned = false;              // the rank clamp's stderr line, once per solve
+    double dinf_time = 0.0;
 };
 
 // ------------------------------------------------------------------------
@@ -201,6 +208,8 @@ struct ShardComm {
     virtual int allreduce_host(lrs_ctx *c, double *v, int n) = 0;
     // direction rows: this shard's send rows to each peer, the halo rows from them
     virtual int halo(lrs_ctx *c, double *D, hipStream_t st) = 0;
+    // the same for one vector x of cone k's local rows (a Lanczos vector)
+    virtual int halo_vec(lrs_ctx *c, int k, double *x, hipStream_t st) = 0;
 };
 static bool sharded(const lrs_ctx *c) { return c->comm != nullptr; }
 static int cone_n_global(const lrs_ctx *c, int k) {
@@ -228,6 +237,18 @@ static int pack_send_rows(lrs_ctx *c, const double *X, hipStream_t st) {
         OPC(launch_pack_rows((int)c->plan.cones[k].send_rows.size(), dc.ld, c->d_send_rows[k], X + dc.foff,
                              c->d_sendbuf + send_base(c->plan, c->dp, k), st));
     }
+    return 0;
+}
+
+// pack cone k's send rows of the vector x (cone-local rows) into c->d_sendvec
+static int pack_send_vec(lrs_ctx *c, int k, const double *x, hipStream_t st) {
+    const long need = std::max<long>(1, (long)c->plan.cones[k].send_rows.size());
+    if (need > c->sendvec_len) {
+        if (c->d_sendvec) HIPC(hipFree(c->d_sendvec));
+        HIPC(hipMalloc((void **)&c->d_sendvec, sizeof(double) * need));
+        c->sendvec_len = need;
+    }
+    OPC(launch_pack_rows((int)c->plan.cones[k].send_rows.size(), 1, c->d_send_rows[k], x, c->d_sendvec, st));
     return 0;
 }
 
@@ -283,6 +304,18 @@ struct RcclComm : ShardComm {
                     NCCLC(ncclRecv(D + dc.foff + (long)cp.recv_start[q] * ld, (size_t)cp.recv_cnt[q] * ld, ncclDouble, q,
                                    comm, st));
             }
+        NCCLC(ncclGroupEnd());
+        return 0;
+    }
+    int halo_vec(lrs_ctx *c, int k, double *x, hipStream_t st) override {
+        const ShardConePlan &cp = c->plan.cones[k];
+        if (pack_send_vec(c, k, x, st)) return -1;
+        NCCLC(ncclGroupStart());
+        for (int q = 0; q < c->plan.world; ++q) {
+            const int ns = cp.send_ptr[q + 1] - cp.send_ptr[q];
+            if (ns > 0) NCCLC(ncclSend(c->d_sendvec + cp.send_ptr[q], (size_t)ns, ncclDouble, q, comm, st));
+            if (cp.recv_cnt[q] > 0) NCCLC(ncclRecv(x + cp.recv_start[q], (size_t)cp.recv_cnt[q], ncclDouble, q, comm, st));
+        }
         NCCLC(ncclGroupEnd());
         return 0;
     }
@@ -371,6 +404,21 @@ struct LoopComm : ShardComm {
             }
         return post(st);
     }
+    int halo_vec(lrs_ctx *c, int k, double *x, hipStream_t st) override {
+        if (pack_send_vec(c, k, x, st)) return -1;
+        g->sendbufs[rank] = c->d_sendvec;
+        if (pre(st)) return -1;
+        const ShardConePlan &cp = c->plan.cones[k];
+        for (int q = 0; q < g->world; ++q) {
+            const int cnt = cp.recv_cnt[q];
+            if (q == rank || cnt == 0) continue;
+            const ShardConePlan &qc = g->plans[q]->cones[k];
+            if (qc.send_ptr[rank + 1] - qc.send_ptr[rank] != cnt) { set_err("loopback halo: plan mismatch"); return -1; }
+            HIPC(hipMemcpyAsync(x + cp.recv_start[q], g->sendbufs[q] + qc.send_ptr[rank], sizeof(double) * cnt,
+                                hipMemcpyDeviceToDevice, st));
+        }
+        return post(st);
+    }
 };
 
 static int hook_halo(void *self, double *D, hipStream_t st) {
@@ -387,15 +435,16 @@ static void bind(lrs_ctx *c) {
     bind_scratch(c->s_tickets, c->s_tmpfin, c->s_rpart);
 }
 
+static void free_lz(lrs_ctx::LzWork &w) {
+    double *ptrs[] = {w.V, w.Vt, w.y[0], w.y[1], w.part, w.H, w.Y};
+    for (double *p : ptrs)
+        if (p) (void)hipFree(p);
+    w = lrs_ctx::LzWork();
+}
 static void drop_lanczos(lrs_ctx *c) {
     if (c->lz.empty()) return;
-    (void)hipStreamSynchronize(c->st);   // nothing captured is still in flight
-    for (auto &w : c->lz) {
-        for (auto &g : w.ge)
-            if (g) (void)hipGraphExecDestroy(g);
-        (void)hipFree(w.Q); (void)hipFree(w.w0); (void)hipFree(w.w1); (void)hipFree(w.part);
-        (void)hipFree(w.coef); (void)hipFree(w.jp);
-    }
+    (void)hipStreamSynchronize(c->st);   // nothing is still in flight on the buffers
+    for (auto &w : c->lz) free_lz(w);
     c->lz.clear();
 }
 static void drop_graphs(lrs_ctx *c) {
@@ -698,196 +747,248 @@ static int op_dot(lrs_ctx *c, long n, const double *x, const double *y, double *
 // here a Lanczos process with full reorthogonalisation (device kernels launch_symv /
 // launch_reorth), run to a 1e-10 relative Ritz residual or its step cap.
 // ------------------------------------------------------------------------
-// smallest eigenvalue of the symmetric tridiagonal T = tridiag(b, a, b) (k x k): bisection
-// on the Sturm count, then the last component of its unit eigenvector by inverse iteration
-static double tridiag_min(const std::vector<double> &a, const std::vector<double> &b, int k, double *last) {
-    double lo = 1e300, hi = -1e300;
-    for (int i = 0; i < k; ++i) {
-        const double r = (i > 0 ? std::fabs(b[i - 1]) : 0.0) + (i < k - 1 ? std::fabs(b[i]) : 0.0);
-        lo = std::min(lo, a[i] - r);
-        hi = std::max(hi, a[i] + r);
+// Symmetric eigen-decomposition of the m x m matrix A (row-major) by cyclic Jacobi rotations:
+// eigenvalues ascending in w, unit eigenvectors in the columns of Z (row-major).  m <= 64.
+static void jacobi_eig(int m, std::vector<double> A, std::vector<double> &w, std::vector<double> &Z) {
+    std::vector<double> V((size_t)m * m, 0.0);
+    for (int i = 0; i < m; ++i) V[(size_t)i * m + i] = 1.0;
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0.0, dia = 0.0;
+        for (int i = 0; i < m; ++i)
+            for (int j = 0; j < m; ++j) (i == j ? dia : off) += A[(size_t)i * m + j] * A[(size_t)i * m + j];
+        if (off <= 1e-32 * (dia + off) || off == 0.0) break;
+        for (int p = 0; p < m; ++p)
+            for (int q = p + 1; q < m; ++q) {
+                const double apq = A[(size_t)p * m + q];
+                if (apq == 0.0) continue;
+                const double th = (A[(size_t)q * m + q] - A[(size_t)p * m + p]) / (2.0 * apq);
+                const double t = std::fabs(th) > 1e150 ? 0.5 / th
+                                                       : (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+                const double cs = 1.0 / std::sqrt(t * t + 1.0), sn = t * cs;
+                for (int r = 0; r < m; ++r) {   // columns p, q
+                    const double ap = A[(size_t)r * m + p], aq = A[(size_t)r * m + q];
+                    A[(size_t)r * m + p] = cs * ap - sn * aq;
+                    A[(size_t)r * m + q] = sn * ap + cs * aq;
+                }
+                for (int r = 0; r < m; ++r) {   // rows p, q
+                    const double ap = A[(size_t)p * m + r], aq = A[(size_t)q * m + r];
+                    A[(size_t)p * m + r] = cs * ap - sn * aq;
+                    A[(size_t)q * m + r] = sn * ap + cs * aq;
+                }
+                A[(size_t)p * m + q] = A[(size_t)q * m + p] = 0.0;
+                for (int r = 0; r < m; ++r) {
+                    const double vp = V[(size_t)r * m + p], vq = V[(size_t)r * m + q];
+                    V[(size_t)r * m + p] = cs * vp - sn * vq;
+                    V[(size_t)r * m + q] = sn * vp + cs * vq;
+                }
+            }
     }
-    auto below = [&](double x) {   // eigenvalues of T smaller than x
-        int cnt = 0;
-        double d = 1.0;
-        for (int i = 0; i < k; ++i) {
-            d = (a[i] - x) - (i > 0 ? b[i - 1] * b[i - 1] / d : 0.0);
-            if (d == 0.0) d = -1e-300;
-            if (d < 0) ++cnt;
-        }
-        return cnt;
-    };
-    for (int it = 0; it < 2000 && hi - lo > 1e-15 * std::max(std::fabs(lo), std::fabs(hi)) + 1e-300; ++it) {
-        const double mid = 0.5 * (lo + hi);
-        if (mid <= lo || mid >= hi) break;
-        if (below(mid) >= 1) hi = mid;
-        else lo = mid;
+    std::vector<int> ord(m);
+    for (int i = 0; i < m; ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&](int a, int b) { return A[(size_t)a * m + a] < A[(size_t)b * m + b]; });
+    w.assign(m, 0.0);
+    Z.assign((size_t)m * m, 0.0);
+    for (int e = 0; e < m; ++e) {
+        w[e] = A[(size_t)ord[e] * m + ord[e]];
+        for (int r = 0; r < m; ++r) Z[(size_t)r * m + e] = V[(size_t)r * m + ord[e]];
     }
-    const double theta = 0.5 * (lo + hi);
-    // inverse iteration on T - theta I (Thomas algorithm; exact singularity nudged)
-    std::vector<double> x(k, 1.0 / std::sqrt((double)k)), cp(k), dp(k);
-    for (int sweep = 0; sweep < 3; ++sweep) {
-        double piv = a[0] - theta;
-        if (piv == 0.0) piv = 1e-300;
-        cp[0] = k > 1 ? b[0] / piv : 0.0;
-        dp[0] = x[0] / piv;
-        for (int i = 1; i < k; ++i) {
-            piv = (a[i] - theta) - b[i - 1] * cp[i - 1];
-            if (piv == 0.0) piv = 1e-300;
-            cp[i] = i < k - 1 ? b[i] / piv : 0.0;
-            dp[i] = (x[i] - b[i - 1] * dp[i - 1]) / piv;
-        }
-        x[k - 1] = dp[k - 1];
-        for (int i = k - 2; i >= 0; --i) x[i] = dp[i] - cp[i] * x[i + 1];
-        double nr = 0.0;
-        for (double v : x) nr += v * v;
-        nr = std::sqrt(nr);
-        if (!(nr > 0.0) || !std::isfinite(nr)) break;
-        for (double &v : x) v /= nr;
-    }
-    *last = std::fabs(x[k - 1]);
-    return theta;
 }
 
 static int op_dot(lrs_ctx *c, long n, const double *x, const double *y, double *out);
-// lambda_min of S on cone k (S: device slot values)
-static int lanczos_min(lrs_ctx *c, int k, const double *S, double *lam_min, int *steps, bool *converged) {
-    const int n = c->dp.cones[k].n;
-    long cap = kLzStepCap;
-    if (const char *e = getenv("LRS_LANCZOS_CAP")) cap = std::max(2L, std::min<long>(kLzStepCap, atol(e)));   // tests
-    const int kmax = (int)std::max(1L, std::min<long>(std::min<long>(n, cap), (long)(2e9 / (8.0 * n))));
-    constexpr int kChunk = 16, kLzTestEvery = 4;
+
+// lambda_min of S on cone k (S: device slot values) with ARPACK dsaupd's semantics, the call
+// of dual_infeasible (data/lorads_sdp_conic.c:1636-1699): which = "SA", nev = 1, ncv = 40
+// (2 when n < 40), exact shifts, tol = 1e-2, at most 600 update iterations.  Restated as a
+// thick-restart Lanczos (Wu & Simon: with exact shifts, implicitly restarted Lanczos keeps the
+// span of the wanted Ritz vectors, which a thick restart keeps explicitly): a cycle extends the
+// basis to ncv vectors (device: S v_j, two Gram-Schmidt passes against the whole basis, the
+// coefficients = the entries of V^T S V), the host takes the Ritz pairs of that ncv x ncv
+// matrix (Jacobi) and the Ritz estimates beta |e_m^T y|, and either stops or restarts from the
+// kk smallest Ritz vectors plus the residual direction.  kk is dsaup2's adjusted nev (nev = 1,
+// no converged value yet: kplusp / 2 = 20, or 2 / 1 for tiny kplusp).  Stop: dsconv's test
+// bound <= tol max(eps^(2/3), |theta|) on the smallest Ritz value, or an absolute bound below
+// 1e-3 of the amount of lambda_min that moves the l_1 dual infeasibility by phase2Tol (the value
+// is then pinned far past every threshold it feeds), or an invariant subspace (breakdown).
+// Sharded: the vectors are the owned rows (the matvec reads the halo rows, exchanged per step),
+// and the coefficient sums and norms are all-reduced in the stream, so every shard sees the
+// same matrix and takes the same decisions.
+static int trl_min(lrs_ctx *c, int k, const double *S, double *lam_min, int *steps_out, int *iters_out,
+                   bool *converged) {
+    const DevCone &dc = c->dp.cones[k];
+    const bool sh = sharded(c);
+    const int nl = dc.n, r0 = dc.row0, nown = dc.nown;
+    const int N = cone_n_global(c, k);
+    int ncv = 40;
+    if (ncv > N) ncv = 2;
+    if (const char *e = getenv("LRS_TRL_NCV")) ncv = std::max(2, std::min(atoi(e), kTrlMaxV));   // tests
+    ncv = std::max(1, std::min(ncv, N));
+    int maxiter = 600;
+    if (const char *e = getenv("LRS_TRL_MAXITER")) maxiter = std::max(0, atoi(e));   // tests
+    const int kk = ncv >= 6 ? ncv / 2 : (ncv > 2 ? 2 : 1);
+    const double tol = 1e-2, eps23 = std::pow(std::numeric_limits<double>::epsilon(), 2.0 / 3.0);
+    const double abs_tol = 1e-3 * c->dinf_tol * (1 + c->hp.cNrm1) * c->scaleObjHis;
+    const long ldv = ((long)nl + 7) & ~7L;
+    constexpr int ldh = kTrlMaxV + 1;
     if ((int)c->lz.size() < c->dp.K) c->lz.resize(c->dp.K);
-    if (c->lz[k].n != n || c->lz[k].kmax != kmax || c->lz[k].S != S || c->lz[k].adj != c->dp.cones[k].adj_ptr) {
-        drop_lanczos(c);
-        c->lz.resize(c->dp.K);
-        lrs_ctx::LzWork &N = c->lz[k];
-        HIPC(hipMalloc((void **)&N.Q, sizeof(double) * (size_t)n * kmax));
-        HIPC(hipMalloc((void **)&N.w0, sizeof(double) * n));
-        HIPC(hipMalloc((void **)&N.w1, sizeof(double) * n));
-        HIPC(hipMalloc((void **)&N.part, sizeof(double) * (kMaxPartialBlocks + 64 * (size_t)kmax)));
-        HIPC(hipMalloc((void **)&N.coef, sizeof(double) * 2 * kmax));
-        HIPC(hipMalloc((void **)&N.jp, sizeof(int)));
-        N.n = n; N.kmax = kmax; N.S = S; N.adj = c->dp.cones[k].adj_ptr;
-        // one step's launches and a chunk of kChunk steps, each captured once and replayed (the
-        // step index lives on the device, so every step's launches are the same)
-        for (int q = 0; q < 2; ++q) {
-            hipGraph_t g = nullptr;
-            HIPC(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
-            int lr = 0;
-            for (int t = 0; t < (q == 0 ? 1 : kChunk) && lr == 0; ++t)
-                lr = launch_lanczos_step(c->dp, k, S, kmax, N.Q, n, N.w0, N.w1, N.jp, N.coef, N.coef + kmax, N.part,
-                                         c->st);
-            const hipError_t e1 = hipStreamEndCapture(c->st, &g);
-            hipError_t e2 = hipErrorUnknown;
-            if (e1 == hipSuccess && lr == 0) e2 = hipGraphInstantiate(&N.ge[q], g, nullptr, nullptr, 0);
-            if (g) (void)hipGraphDestroy(g);
-            if (e2 != hipSuccess) { set_err("lanczos capture: %s", last_device_error()); return -1; }
-        }
+    lrs_ctx::LzWork &Z = c->lz[k];
+    if (Z.n != nl) {   // this cone's buffers only
+        HIPC(hipStreamSynchronize(c->st));
+        free_lz(Z);
+        HIPC(hipMalloc((void **)&Z.V, sizeof(double) * ldv * (kTrlMaxV + 1)));
+        HIPC(hipMalloc((void **)&Z.Vt, sizeof(double) * ldv * kTrlMaxV));
+        HIPC(hipMalloc((void **)&Z.y[0], sizeof(double) * ldv));
+        HIPC(hipMalloc((void **)&Z.y[1], sizeof(double) * ldv));
+        HIPC(hipMalloc((void **)&Z.part, sizeof(double) * (64L * kTrlMaxV + kMaxPartialBlocks)));
+        HIPC(hipMalloc((void **)&Z.H, sizeof(double) * ((long)ldh * kTrlMaxV + 2L * kTrlMaxV + 8)));
+        HIPC(hipMalloc((void **)&Z.Y, sizeof(double) * kTrlMaxV * kTrlMaxV));
+        HIPC(hipMemsetAsync(Z.y[0], 0, sizeof(double) * ldv, c->st));
+        HIPC(hipMemsetAsync(Z.y[1], 0, sizeof(double) * ldv, c->st));
+        Z.n = nl;
     }
-    lrs_ctx::LzWork &Wz = c->lz[k];
-    double *Q = Wz.Q, *al_d = Wz.coef, *bw2_d = Wz.coef + kmax;
-    int *jp = Wz.jp;
-    HIPC(hipMemsetAsync(jp, 0, sizeof(int), c->st));
-    int rc = 0;
-    HIPC(hipMemsetAsync(Q, 0, sizeof(double) * (size_t)n * kmax, c->st));
-    {   // Deterministic start vector (the reference's ARPACK draws its own random residual):
-        // a pseudo-random combination of the factor's columns plus 1 % pseudo-random noise.
-        // Near optimality S R ~ 0 (complementarity), so lambda_min sits in the near-null
-        // cluster spanned by R, and a start there reaches it in far fewer steps than a
-        // plain random vector; the noise keeps every eigendirection in the Krylov space.
-        const DevCone &dc = c->dp.cones[k];
-        std::vector<double> Rh((size_t)n * dc.ld, 0.0), q0(n), g(dc.ld, 0.0);
-        HIPC(hipMemcpyAsync(Rh.data(), c->W.R + dc.foff, sizeof(double) * Rh.size(), hipMemcpyDeviceToHost, c->st));
+    double *V = Z.V, *Hd = Z.H, *bw2 = Z.H + (long)ldh * kTrlMaxV, *tot = bw2 + kTrlMaxV;
+    double *npart = Z.part + 64L * kTrlMaxV;
+    HIPC(hipMemsetAsync(V, 0, sizeof(double) * ldv * (kTrlMaxV + 1), c->st));
+    {   // start vector (the reference's ARPACK draws a random residual): a pseudo-random
+        // combination of the factor's columns plus 1 % pseudo-random noise keyed by the global
+        // row.  Near optimality S R ~ 0 (complementarity), so lambda_min sits in the near-null
+        // cluster spanned by R, which this start reaches in far fewer steps than a plain random
+        // vector; the noise keeps every eigendirection in the Krylov space.  LRS_TRL_START=random:
+        // the noise alone.
+        const bool rnd_only = getenv("LRS_TRL_START") && !strcmp(getenv("LRS_TRL_START"), "random");
+        std::vector<double> Rh((size_t)nown * dc.ld, 0.0), q0(nown), z(nown), g(dc.ld, 0.0);
+        HIPC(hipMemcpyAsync(Rh.data(), c->W.R + dc.foff + (long)r0 * dc.ld, sizeof(double) * Rh.size(),
+                            hipMemcpyDeviceToHost, c->st));
         HIPC(hipStreamSynchronize(c->st));
         unsigned long long st = 0x9E3779B97F4A7C15ULL;
-        auto rnd = [&]() {
+        for (int q = 0; q < dc.r; ++q) {
             st = st * 6364136223846793005ULL + 1442695040888963407ULL;
-            return ((double)(st >> 11) / 9007199254740992.0) - 0.5;
-        };
-        for (int q = 0; q < dc.r; ++q) g[q] = rnd();
-        double nr = 0.0, nn = 0.0;
-        for (int i = 0; i < n; ++i) {
+            g[q] = ((double)(st >> 11) / 9007199254740992.0) - 0.5;
+        }
+        double sums[3] = {0.0, 0.0, 0.0};
+        for (int i = 0; i < nown; ++i) {
             double t = 0.0;
-            for (int q = 0; q < dc.r; ++q) t += Rh[(size_t)i * dc.ld + q] * g[q];
+            if (!rnd_only)
+                for (int q = 0; q < dc.r; ++q) t += Rh[(size_t)i * dc.ld + q] * g[q];
             q0[i] = t;
-            nr += t * t;
+            unsigned long long h = (unsigned long long)(sh ? c->plan.cones[k].gid[r0 + i] : i) + 0x632BE59BD9B4E019ULL;
+            h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ULL;
+            h = (h ^ (h >> 27)) * 0x94D049BB133111EBULL;
+            h ^= h >> 31;
+            z[i] = ((double)(h >> 11) / 9007199254740992.0) - 0.5;
+            sums[0] += t * t;
+            sums[1] += z[i] * z[i];
         }
-        std::vector<double> z(n);
-        for (int i = 0; i < n; ++i) { z[i] = rnd(); nn += z[i] * z[i]; }
-        const double zs = (nr > 0 ? 1e-2 * std::sqrt(nr) : 1.0) / std::sqrt(nn);
-        nr = 0.0;
-        for (int i = 0; i < n; ++i) { q0[i] += zs * z[i]; nr += q0[i] * q0[i]; }
-        nr = std::sqrt(nr);
-        for (double &v : q0) v /= nr;
-        // on the solver stream, after the zero fill above (a null-stream copy can overtake it)
-        HIPC(hipMemcpyAsync(Q, q0.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->st));
-        HIPC(hipStreamSynchronize(c->st));
+        if (sh && c->comm->allreduce_host(c, sums, 2)) return -1;
+        const double zs = (sums[0] > 0 ? 1e-2 * std::sqrt(sums[0]) : 1.0) / std::sqrt(std::max(sums[1], 1e-300));
+        for (int i = 0; i < nown; ++i) {
+            q0[i] += zs * z[i];
+            sums[2] += q0[i] * q0[i];
+        }
+        double nrm2 = sums[2];
+        if (sh && c->comm->allreduce_host(c, &nrm2, 1)) return -1;
+        const double inv = 1.0 / std::sqrt(std::max(nrm2, 1e-300));
+        for (double &v : q0) v *= inv;
+        HIPC(hipMemcpyAsync(V + r0, q0.data(), sizeof(double) * nown, hipMemcpyHostToDevice, c->st));
+        HIPC(hipStreamSynchronize(c->st));   // q0 is a host temporary
     }
-    // Steps run on the device in chunks (alpha_j, ||w_j||^2 stay in device memory); the host
-    // fetches a chunk's coefficients and applies the stopping test step by step (every
-    // kLzTestEvery steps: the Sturm bisection is the host's cost).  Converged: Ritz residual
-    // beta_j |e_j^T y| <= 1e-4 max(|theta|, 1e-10 ||T||) -- the reference's ARPACK test
-    // (|r| <= tol |theta|, dsaupd tol 1e-2, data/lorads_sdp_conic.c:1636-1699) 100x tighter --;
-    // breakdown beta_j <= 1e-14 ||T||; or the step cap.
-    std::vector<double> al, be, alc(kChunk), bwc(kChunk);
-    double theta = 0.0, tnorm = 0.0;   // tnorm: Gershgorin bound of T (~ ||S||)
-    int j = 0;
-    bool done = false, conv = false;
-    while (!done && rc == 0) {
-        const int j0 = j, j1 = std::min(kmax, j0 + kChunk);
-        if (j1 - j0 == kChunk) {
-            if (hipGraphLaunch(Wz.ge[1], c->st) != hipSuccess) rc = -1;
-        } else {
-            for (int t = j0; t < j1 && rc == 0; ++t)
-                if (hipGraphLaunch(Wz.ge[0], c->st) != hipSuccess) rc = -1;
-        }
-        if (rc) break;
-        if (hipMemcpyAsync(alc.data(), al_d + j0, sizeof(double) * (j1 - j0), hipMemcpyDeviceToHost, c->st) !=
-                hipSuccess ||
-            hipMemcpyAsync(bwc.data(), bw2_d + j0, sizeof(double) * (j1 - j0), hipMemcpyDeviceToHost, c->st) !=
-                hipSuccess ||
-            hipStreamSynchronize(c->st) != hipSuccess) {
-            rc = -1;
-            break;
-        }
-        for (int t = j0; t < j1; ++t) {
-            const double alpha = alc[t - j0], bnew = std::sqrt(std::max(bwc[t - j0], 0.0));
-            al.push_back(alpha);
-            const bool cap = t + 1 == kmax;
-            tnorm = std::max(tnorm, std::fabs(alpha) + bnew + (be.empty() ? 0.0 : be.back()));
-            const bool brk = bnew <= 1e-14 * std::max(1.0, tnorm);
-            if (cap || brk || (t + 1) % kLzTestEvery == 0) {
-                double last = 1.0;
-                theta = tridiag_min(al, be, t + 1, &last);
-                const double tol = 1e-4 * std::max(std::fabs(theta), 1e-10 * tnorm);
-                if (getenv("LRS_LANCZOS_TRACE") && (t + 1) % 20 == 0)
-                    fprintf(stderr, "  step %d theta %.12e resid %.3e tnorm %.3e\n", t + 1, theta, bnew * last, tnorm);
-                if (bnew * last <= tol || brk || cap) {
-                    j = t + 1;
-                    done = true;
-                    // converged: the relative Ritz test, a breakdown, or an absolute residual
-                    // (which bounds |theta - lambda|) below 1e-3 of the amount of lambda_min
-                    // that moves the l_1 dual infeasibility by phase2Tol
-                    const double abs_tol = 1e-3 * c->dinf_tol * (1 + c->hp.cNrm1) * c->scaleObjHis;
-                    conv = bnew * last <= tol || brk || bnew * last <= abs_tol;
-                    if (!conv)
-                        fprintf(stderr, "[lrsdp] dual infeasibility: Lanczos on cone %d stopped at its %d-step cap "
-                                "(Ritz value %.6e, residual %.3e): lambda_min may be lower, the l_1 value a lower bound\n",
-                                k, kmax, theta, bnew * last);
-                    break;
-                }
+    std::vector<double> Hh((size_t)ldh * ncv), b2h(ncv), T, w, Zm, Yh, keep;
+    const double *win = V;       // v_j's unnormalized source (the start vector is normalized)
+    const double *b2in = nullptr;
+    int cur = 0, j0 = 0, iter = 0, steps = 0, msz = ncv;
+    double theta = 0.0, bound = 0.0;
+    bool conv = false;
+    int rc = 0;
+    for (;;) {
+        for (int j = j0; j < ncv && rc == 0; ++j) {
+            double *vj = V + (long)j * ldv, *y = Z.y[cur];
+            if (sh) {
+                if (b2in) OPC(launch_trl_norm(nown, win + r0, b2in, vj + r0, c->st));
+                if (c->comm->halo_vec(c, k, vj, c->st)) return -1;
+                OPC(launch_trl_symv(c->dp, k, S, vj, nullptr, nullptr, y, c->st));
+            } else {
+                OPC(launch_trl_symv(c->dp, k, S, win, b2in, b2in ? vj : nullptr, y, c->st));
             }
-            be.push_back(bnew);
+            for (int pass = 0; pass < 2; ++pass) {
+                OPC(launch_trl_dots(nown, V + r0, ldv, j + 1, y + r0, Z.part, c->st));
+                int nb = trl_nblk(nown);
+                const double *pp = Z.part;
+                if (sh) {
+                    OPC(launch_trl_fold(j + 1, nb, Z.part, tot, c->st));
+                    if (c->comm->allreduce_dev(c, tot, j + 1, c->st)) return -1;
+                    pp = tot;
+                    nb = 1;
+                }
+                OPC(launch_trl_sub(nown, V + r0, ldv, j + 1, pp, nb, y + r0, Hd + (long)j * ldh, pass, npart, bw2 + j,
+                                   c->st));
+            }
+            if (sh && c->comm->allreduce_dev(c, bw2 + j, 1, c->st)) return -1;
+            win = y;
+            b2in = bw2 + j;
+            cur ^= 1;
+            steps++;
         }
-        if (!done) j = j1;
+        HIPC(hipMemcpyAsync(Hh.data(), Hd, sizeof(double) * ldh * ncv, hipMemcpyDeviceToHost, c->st));
+        HIPC(hipMemcpyAsync(b2h.data(), bw2, sizeof(double) * ncv, hipMemcpyDeviceToHost, c->st));
+        HIPC(hipStreamSynchronize(c->st));
+        // the Rayleigh matrix V^T S V: kept Ritz values on the diagonal, the new columns from the
+        // coefficients (the coupling to the previous vector averaged with its beta)
+        T.assign((size_t)ncv * ncv, 0.0);
+        for (int q = 0; q < j0; ++q) T[(size_t)q * ncv + q] = keep[q];
+        for (int j = j0; j < ncv; ++j)
+            for (int q = 0; q <= j; ++q) {
+                double v = Hh[(size_t)j * ldh + q];
+                if (q == j - 1 && j > j0) v = 0.5 * (v + std::sqrt(std::max(b2h[j - 1], 0.0)));
+                T[(size_t)q * ncv + j] = T[(size_t)j * ncv + q] = v;
+            }
+        double tnorm = 0.0;
+        for (int q = 0; q < ncv; ++q) {
+            double a = 0.0;
+            for (int j = 0; j < ncv; ++j) a += std::fabs(T[(size_t)q * ncv + j]);
+            tnorm = std::max(tnorm, a);
+        }
+        // an invariant subspace inside this cycle: the leading block is exact
+        msz = ncv;
+        double betam = std::sqrt(std::max(b2h[ncv - 1], 0.0));
+        for (int j = j0; j < ncv - 1; ++j)
+            if (std::sqrt(std::max(b2h[j], 0.0)) <= 1e-14 * std::max(1.0, tnorm)) { msz = j + 1; betam = 0.0; break; }
+        std::vector<double> Tm((size_t)msz * msz);
+        for (int q = 0; q < msz; ++q)
+            for (int j = 0; j < msz; ++j) Tm[(size_t)q * msz + j] = T[(size_t)q * ncv + j];
+        jacobi_eig(msz, Tm, w, Zm);
+        theta = w[0];
+        bound = betam * std::fabs(Zm[(size_t)(msz - 1) * msz + 0]);
+        iter++;
+        const bool brk = betam <= 1e-14 * std::max(1.0, tnorm);
+        conv = brk || bound <= tol * std::max(eps23, std::fabs(theta)) || bound <= abs_tol;
+        if (getenv("LRS_LANCZOS_TRACE") && (iter <= 3 || iter % 20 == 0 || conv))
+            fprintf(stderr, "  trl cone %d iter %d steps %d theta %.12e bound %.3e (tol %.3e abs %.3e)\n", k, iter, steps,
+                    theta, bound, tol * std::max(eps23, std::fabs(theta)), abs_tol);
+        if (conv || iter > maxiter || msz < ncv) break;
+        // restart from the kk smallest Ritz vectors (ascending) and the residual direction
+        Yh.assign((size_t)ncv * kk, 0.0);
+        for (int q = 0; q < ncv; ++q)
+            for (int e = 0; e < kk; ++e) Yh[(size_t)q * kk + e] = Zm[(size_t)q * ncv + e];
+        HIPC(hipMemcpyAsync(Z.Y, Yh.data(), sizeof(double) * Yh.size(), hipMemcpyHostToDevice, c->st));
+        OPC(launch_trl_restart(nown, V + r0, ldv, ncv, Z.Y, kk, Z.Vt + r0, c->st));
+        HIPC(hipMemcpy2DAsync(V + r0, sizeof(double) * ldv, Z.Vt + r0, sizeof(double) * ldv, sizeof(double) * nown, kk,
+                              hipMemcpyDeviceToDevice, c->st));
+        HIPC(hipStreamSynchronize(c->st));   // Yh is a host temporary
+        keep.assign(w.begin(), w.begin() + kk);
+        j0 = kk;
+        b2in = bw2 + (ncv - 1);   // v_kk = residual / beta_m (the residual is `win`)
     }
-    if (rc) set_err("lanczos: %s", last_device_error());
-    (void)hipStreamSynchronize(c->st);
+    if (!conv)
+        fprintf(stderr, "[lrsdp] dual infeasibility: the eigen-solve on cone %d stopped after %d update iterations "
+                "(%d steps; Ritz value %.6e, Ritz estimate %.3e): lambda_min may be lower, the l_1 value a lower bound\n",
+                k, iter, steps, theta, bound);
     *lam_min = theta;
-    if (steps) *steps = j;
+    if (steps_out) *steps_out = steps;
+    if (iters_out) *iters_out = iter;
     if (converged) *converged = conv;
-    if (getenv("LRS_LANCZOS_TRACE")) fprintf(stderr, "lanczos cone %d: n %d, %d steps, lambda_min %.12e\n", k, n, j, theta);
+    if (getenv("LRS_LANCZOS_TRACE"))
+        fprintf(stderr, "trl cone %d: n %d, ncv %d, %d update iterations, %d steps, lambda_min %.12e\n", k, N, ncv, iter,
+                steps, theta);
     return rc;
 }
 
@@ -900,10 +1001,14 @@ static int dual_infeasibility(lrs_ctx *c, double *l1, double *lmin, int *all_con
     OPC(launch_axpby(m, -1.0, W.lam, 1.0, W.wtmp, c->st));          // negLambd = -dualVar
     OPC(launch_wsum(c->dp, W.wtmp, 1, W.S, c->st));                 // S = C + A^*(negLambd)
     double err = 0.0;
+    const double t0 = now_s();
     for (int k = 0; k < c->dp.K; ++k) {
         double lk = 0.0;
         bool conv = true;
-        if (lanczos_min(c, k, W.S, &lk, nullptr, &conv)) return -1;
+        int steps = 0, iters = 0;
+        if (trl_min(c, k, W.S, &lk, &steps, &iters, &conv)) return -1;
+        c->dinf_steps += steps;
+        c->dinf_iters += iters;
         if (lmin) lmin[k] = lk;
         if (all_conv && !conv) *all_conv = 0;
         err += std::fabs(std::min(lk, 0.0));
@@ -911,6 +1016,7 @@ static int dual_infeasibility(lrs_ctx *c, double *l1, double *lmin, int *all_con
     err /= c->scaleObjHis;
     err /= (c->hp.cNrm1 + 1);
     *l1 = err;
+    c->dinf_time += now_s() - t0;
     return 0;
 }
 
@@ -1199,8 +1305,7 @@ static int aug_rank(lrs_ctx *c, double f, const lrs_params *p, int *sched_pos, i
         int tot = std::max(1, p->rankSchedule[pos]), cur = sum_rank(c);
         for (int k = 0; k < c->dp.K; ++k) {
             int rk = (int)std::lround((double)tot * c->rank[k] / std::max(1, cur));
-            static bool warned = false;
-            nr[k] = clamp_rank(std::max(c->rank[k], std::min(rk, cone_n_global(c, k))), &warned);
+            nr[k] = clamp_rank(std::max(c->rank[k], std::min(rk, cone_n_global(c, k))), &c->rank_warned);
             c->rank_max[k] = std::max(c->rank_max[k], nr[k]);
         }
     } else {
@@ -1969,6 +2074,8 @@ static int obj_scale(lrs_ctx *c, double f) {
     }
     c->scaleObjHis *= f;
     P.dense_scale *= f;   // dense-objective cones: the factor rides on every product with C
+    // captured inner-iteration batches (LRS_GRAPHS=1) hold dense_scale as a kernel argument
+    if (P.ndense > 0 && f != 1.0) drop_graphs(c);
     OPC(launch_axpby(Pt, 0.0, P.Cw, f, P.Cw, c->st));
     OPC(launch_axpby(Pt, 0.0, P.Craw, f, P.Craw, c->st));
     OPC(launch_axpby(P.m, 0.0, c->W.lam, f, c->W.lam, c->st));
@@ -1981,6 +2088,7 @@ static int obj_unscale(lrs_ctx *c) {
     HIPC(hipMemcpyAsync(P.Cw, c->Cw0, sizeof(double) * Pt, hipMemcpyDeviceToDevice, c->st));
     HIPC(hipMemcpyAsync(P.Craw, c->Craw0, sizeof(double) * Pt, hipMemcpyDeviceToDevice, c->st));
     HIPC(hipStreamSynchronize(c->st));
+    if (P.ndense > 0 && P.dense_scale != 1.0) drop_graphs(c);
     P.dense_scale = 1.0;
     c->c_scaled = false;
     return 0;
@@ -2113,7 +2221,7 @@ void lrs_ctx_destroy(lrs_ctx *c) {
         if (e) (void)hipEventDestroy(e);
     delete c->comm;
     for (void *q : {(void *)c->s_tickets, (void *)c->s_tmpfin, (void *)c->s_rpart, (void *)c->d_sendbuf,
-                    (void *)c->Cw0, (void *)c->Craw0})
+                    (void *)c->d_sendvec, (void *)c->Cw0, (void *)c->Craw0})
         if (q) (void)hipFree(q);
     for (int *q : c->d_send_rows)
         if (q) (void)hipFree(q);
@@ -2219,6 +2327,19 @@ int lrs_problem_info(lrs_ctx *c, int *m, int *ncones, int *dims, long *nslots, l
     if (dims) for (int k = 0; k < c->hp.K; ++k) dims[k] = c->hp.cones[k].n;
     if (nslots) *nslots = c->dp.Ptot;
     if (nnzc) *nnzc = c->dp.Z;
+    return 0;
+}
+
+int lrs_tile_info(lrs_ctx *c, int *auv, int *slot) {
+    if (c) bind(c);
+    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    int a = 0, sl = 0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        a |= c->dp.cones[k].auv_items > 0;
+        sl |= c->dp.cones[k].sa_items > 0;
+    }
+    if (auv) *auv = a;
+    if (slot) *slot = sl;
     return 0;
 }
 
@@ -2407,6 +2528,9 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     memset(res, 0, sizeof(*res));
     const double tss = now_s();
     c->dinf_tol = p->phase2Tol;
+    c->dinf_steps = c->dinf_iters = 0;
+    c->rank_warned = false;
+    c->dinf_time = 0.0;
     if (obj_unscale(c)) return -1;   // a previous solve's reopt scaled C on the device
     std::vector<int> r, rm;
     determine_rank(c, p, r, rm);
@@ -2460,8 +2584,8 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
         // dual infeasibility of the phase-2 multipliers (main.c:515-527); a time-limit exit of
         // the reopt round jumps past it to END_SOLVING like main.c:505-510
         if (!timeout) {
-            dinf_conv = sharded(c) ? -1 : 1;   // sharded: not evaluated
-            if (!sharded(c) && dual_infeasibility(c, &dinf, nullptr, &dinf_conv)) return -1;
+            dinf_conv = 1;
+            if (dual_infeasibility(c, &dinf, nullptr, &dinf_conv)) return -1;
             admm.gap = c->dimGap;
             admm.pinf1 = c->dimPinf;
             logf_(c, p, "-----------------------------------------------------------------------\n"
@@ -2480,8 +2604,8 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
                     if (reopt(c, p, alm, admm, reopt_param, 3, 50, tss, &bad, 2)) return -1;
                     OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
                     HIPC(hipMemcpyAsync(c->W.V, c->W.R, sizeof(double) * c->dp.NRpad, hipMemcpyDeviceToDevice, c->st));
-                    dinf_conv = sharded(c) ? -1 : 1;   // sharded: not evaluated
-                    if (!sharded(c) && dual_infeasibility(c, &dinf, nullptr, &dinf_conv)) return -1;
+                    dinf_conv = 1;
+                    if (dual_infeasibility(c, &dinf, nullptr, &dinf_conv)) return -1;
                     admm.gap = c->dimGap;
                     admm.pinf1 = c->dimPinf;
                     admm.pinfinf = c->dimPinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
@@ -2516,8 +2640,12 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     res->dinf_inf = dinf < 0 ? dinf : dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrmInf);
     res->dinf_2 = dinf < 0 ? dinf : dinf * (1 + c->hp.cNrm1) / (1 + c->hp.cNrm2);
     res->dinf_converged = dinf_conv;
+    res->dinf_iters = (int)c->dinf_iters;
+    res->dinf_steps = c->dinf_steps;
+    res->dinf_time = c->dinf_time;
+    res->obj_scale = c->scaleObjHis;
     // PRIMAL_DUAL_OPTIMAL only on a dual infeasibility whose eigen-solve converged (a Ritz value
-    // at the step cap only bounds lambda_min from above)
+    // after the last update iteration only bounds lambda_min from above)
     if (timeout) res->status = 4;
     else if (dinf >= 0 && dinf_conv == 1 && dinf <= 5 * p->phase2Tol && admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol)
         res->status = 1;

@@ -53,7 +53,8 @@ class Result(C.Structure):
         ("alm_time", C.c_double), ("admm_time", C.c_double), ("read_time", C.c_double), ("status", C.c_int),
         ("retcode", C.c_int), ("final_rank", C.c_int), ("oracle_rank", C.c_int), ("traj1_len", C.c_int),
         ("traj2_len", C.c_int), ("rho_max", C.c_double), ("dinf", C.c_double), ("dinf_inf", C.c_double),
-        ("dinf_2", C.c_double), ("dinf_converged", C.c_int),
+        ("dinf_2", C.c_double), ("dinf_converged", C.c_int), ("dinf_iters", C.c_int), ("dinf_steps", C.c_long),
+        ("dinf_time", C.c_double), ("obj_scale", C.c_double),
     ]
 
     def as_dict(self):
@@ -115,6 +116,7 @@ def load_library(path=None):
         "lrs_op_dual_infeasibility": (C.c_int, [vp, dp, dp]),
         "lrs_get_kernel_path": (C.c_int, [vp, ip]),
         "lrs_stage_bytes": (C.c_int, [vp, dp]),
+        "lrs_tile_info": (C.c_int, [vp, ip, ip]),
         "lrs_auut_bytes": (C.c_int, [vp, dp]),
         "lrs_time_gram": (C.c_int, [vp, C.c_int, C.c_int, dp, dp]),
         "lrs_mfma_f64_peak": (C.c_int, [vp, dp]),
@@ -430,6 +432,12 @@ class Solver:
         v = C.c_double()
         self._check(self.lib.lrs_auut_bytes(self.ctx, C.byref(v)), "auut_bytes")
         return v.value
+
+    def tile_info(self):
+        """(constraint entries in 2-D tiles, lower pattern in 2-D tiles) for some cone."""
+        a, b = C.c_int(), C.c_int()
+        self._check(self.lib.lrs_tile_info(self.ctx, C.byref(a), C.byref(b)), "tile_info")
+        return a.value, b.value
 
     def stage_bytes(self):
         """Algorithmic bytes per launch of the stages [A, G, B] at the current ranks."""

@@ -19,13 +19,16 @@
  *   kernels <file.dat-s> <rank> <in.bin> <out.bin>
  *       One call of each hot-path operator on caller-provided iterates (see
  *       scripts/make_golden.py for the exact binary layout).
- *   alm_steps <file.dat-s> <rank> <K> <out.bin>
+ *   alm_steps <file.dat-s> <rank> <K[,K2,...]> <out.bin>
  *       From the reference's own initial point (srand(925), data/lorads_solver.c:625)
  *       the preamble of LORADS_ALMOptimize (lorads_alm.c:1233-1243) and exactly K
  *       trips of its inner L-BFGS loop (lorads_alm.c:1302-1379), through the same
  *       lorads_func slots in the same order; dumps per trip (tau, rootNum,
  *       ||G||^2, pinf) and after the last one R, G, A(RR^T), lambda and the newest
  *       L-BFGS pair (s, y, beta).  Layout in scripts/make_golden_steps.py.
+ *       With a comma list of K (ascending) one run dumps the state at each K into
+ *       <out.bin>.K<k>, at the point a stand-alone run with that K stops (so a
+ *       C5-sized presolve is paid once).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -335,12 +338,42 @@ static int mode_kernels(int argc, char **argv) {
 }
 
 /* ---------------- alm_steps mode: K inner iterations, per-iteration dump ---------------- */
+static int steps_dump(lorads_solver *S, const double *trips, long done, const char *out, long K) {
+    char path[4096];
+    if (K >= 0) snprintf(path, sizeof(path), "%s.K%ld", out, K);
+    else snprintf(path, sizeof(path), "%s", out);
+    FILE *fo = fopen(path, "wb");
+    if (!fo) return 1;
+    lorads_int m = S->nRows;
+    double dd = (double)done;
+    fwrite(&dd, 8, 1, fo);
+    fwrite(trips, 8, 4 * done, fo);
+    for (lorads_int k = 0; k < S->nCones; ++k)
+        fwrite(S->var->R[k]->matElem, 8, S->var->R[k]->nRows * S->var->R[k]->rank, fo);
+    for (lorads_int k = 0; k < S->nCones; ++k)
+        fwrite(S->var->Grad[k]->matElem, 8, S->var->Grad[k]->nRows * S->var->Grad[k]->rank, fo);
+    fwrite(S->var->constrValSum, 8, m, fo);
+    fwrite(S->var->dualVar, 8, m, fo);
+    lbfgs_node *newest = S->lbfgsHis->prev;
+    fwrite(newest->s, 8, newest->allElem, fo);
+    fwrite(newest->y, 8, newest->allElem, fo);
+    fwrite(&newest->beta, 8, 1, fo);
+    fclose(fo);
+    printf("REF_STEPS_DUMP K=%ld done=%ld\n", K, done);
+    fflush(stdout);
+    return 0;
+}
+
 static int mode_alm_steps(int argc, char **argv) {
     if (argc < 6) return 2;
     lorads_params p; default_params(&p);
     p.fname = argv[2];
     p.fixedRank = atoi(argv[3]);
-    const long K = atol(argv[4]);
+    long Ks[64]; int nK = 0;
+    for (char *tok = strtok(argv[4], ","); tok && nK < 64; tok = strtok(NULL, ",")) Ks[nK++] = atol(tok);
+    const long K = nK ? Ks[nK - 1] : 0;
+    const int multi = nK > 1;
+    int nextK = 0;
     ref_ctx c; memset(&c, 0, sizeof(c));
     double t_read, tss;
     if (ref_setup(&c, &p, &t_read, &tss)) { fprintf(stderr, "read failed\n"); return 1; }
@@ -378,6 +411,9 @@ static int mode_alm_steps(int argc, char **argv) {
         if (stop) break;
         localIter = 0;
         while (rc_val - rc_tol > p.endALMSubTol) {   /* lorads_alm.c:1302-1379 */
+            while (multi && nextK < nK - 1 && done >= Ks[nextK]) {
+                steps_dump(S, trips, done, argv[5], Ks[nextK]); nextK++;
+            }
             if (done >= K) { stop = 1; break; }
             if (localIter % 300 == 0) clearLBFGS = 0;
             aFunc->LBFGSDirection(&p, S, S->lbfgsHis, S->var->gradLp, S->var->uLp, S->var->Grad, S->var->U, clearLBFGS);
@@ -426,22 +462,9 @@ static int mode_alm_steps(int argc, char **argv) {
             if (st->l_inf_primal_infeasibility <= p.phase1Tol) break;
         }
     }
-    FILE *fo = fopen(argv[5], "wb");
-    if (!fo) return 1;
-    double dd = (double)done;
-    fwrite(&dd, 8, 1, fo);
-    fwrite(trips, 8, 4 * done, fo);
-    for (lorads_int k = 0; k < S->nCones; ++k)
-        fwrite(S->var->R[k]->matElem, 8, S->var->R[k]->nRows * S->var->R[k]->rank, fo);
-    for (lorads_int k = 0; k < S->nCones; ++k)
-        fwrite(S->var->Grad[k]->matElem, 8, S->var->Grad[k]->nRows * S->var->Grad[k]->rank, fo);
-    fwrite(S->var->constrValSum, 8, m, fo);
-    fwrite(S->var->dualVar, 8, m, fo);
-    lbfgs_node *newest = S->lbfgsHis->prev;
-    fwrite(newest->s, 8, newest->allElem, fo);
-    fwrite(newest->y, 8, newest->allElem, fo);
-    fwrite(&newest->beta, 8, 1, fo);
-    fclose(fo);
+    /* Ks not reached (the loop stopped first): the final state, as stand-alone runs would dump */
+    for (; multi && nextK < nK; ++nextK) steps_dump(S, trips, done, argv[5], Ks[nextK]);
+    if (!multi && steps_dump(S, trips, done, argv[5], -1)) return 1;
     free(trips);
     printf("REF_STEPS done=%ld\n", done);
     return 0;

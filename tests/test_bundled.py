@@ -111,3 +111,21 @@ def test_bundled_matches_reference(solver_mod, name):
     assert abs(r["pobj"] - ref["admm_pobj"]) <= tol * max(1.0, abs(ref["admm_pobj"])), (r["pobj"], ref["admm_pobj"])
     assert r["pinf"] <= max(1e-6, 10 * ref["admm_pinf"])
     assert abs(r["gap"]) <= max(1e-5, 2 * abs(ref["admm_gap"]))
+
+
+@pytest.mark.gpu
+def test_bundled_theta102_matches_reference(solver_mod):
+    """theta102 (n = 500, m = 37 467, dense C = -J) with the golden run's flags
+    (--reoptLevel 0): both sides stop unconverged at a gap of ~5e-4 after ~50 000 L-BFGS
+    trips, so the bar is the theta one of test_gpu_parity.py: primal and dual objectives
+    within 10x the two certified gaps, pinf at the reference's level, the same final rank."""
+    g = golden()["theta102"]
+    ref = g["result"]
+    sv = solver_mod.Solver(os.path.join(DATA, "theta102.dat-s"))
+    r = sv.solve(**flags_of(g))
+    sv.close()
+    tol = 10 * (ref["admm_gap"] + r["gap"]) + 1e-6
+    for ours, theirs in (("pobj", "admm_pobj"), ("dobj", "admm_dobj")):
+        assert abs(r[ours] - ref[theirs]) <= tol * (1 + abs(ref[theirs])), (ours, r[ours], ref[theirs], tol)
+    assert r["pinf"] <= max(1e-4, 10 * ref["admm_pinf"])
+    assert r["final_rank"] == g["json"]["trajectory"]["phase_1"]["curr_rank"][-1]

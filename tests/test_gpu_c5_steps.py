@@ -1,0 +1,98 @@
+"""Per-trip parity on BASELINE config C5 (random sparse SDP, n = 10^4, 6 entries per
+constraint, C = I, --fixedRank 128) against the reference LoRADS C code's own trips.
+
+tests/golden/steps_c5_m1e6.npz / steps_c5_m1e5.npz come from scripts/make_golden_c5.py
+(oracle/ref_harness.c `alm_steps` over the reference objects, one run dumping K = 1..3 /
+1..5): per trip tau, rootNum, ||G||^2, pinf, and after trip K the factor, gradient, the
+newest L-BFGS pair (n x 2 projections), A(RR^T) and lambda (every 997th entry + 4 Gaussian
+projections).  At m = 10^6 the reference takes its dense syr2k / symm branches (pattern
+~11.5 % of the lower triangle); the device the 2-D LDS tile kernels, which
+the upload picks for this cone by default.  At m = 10^5 the device's default is the
+per-row gather kernels; the tiles are also forced there (LRS_SLOT_TILES / LRS_AUV_TILES).
+
+The instance is built in memory from the same seeded generator the fixture was made from
+(instances.random_sparse_problem; the file's sha256 is in the fixture, and the in-memory
+load equals the file load: test_gpu_parity.py::test_coo_load_matches_file).
+
+Tolerance: 1e-9 relative, as tests/test_gpu_steps.py.
+"""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN, rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+N = 10000
+
+
+def project_factor(v, n, k=2, seed=7):
+    r = v.size // n
+    om = np.random.default_rng(seed).standard_normal((r, k))
+    return v.reshape(r, n).T @ om
+
+
+def project_mvec(v, k=4, stride=997, seed=11):
+    om = np.random.default_rng(seed).standard_normal((k, v.size))
+    return np.concatenate([v[::stride], om @ v])
+
+
+@pytest.fixture(scope="module")
+def mods():
+    return (importlib.import_module("ltr-lowrank-sdp_amd.solver"),
+            importlib.import_module("ltr-lowrank-sdp_amd.instances"))
+
+
+def _run(mods, name, monkeypatch, tiles):
+    solver, inst = mods
+    fx = os.path.join(GOLDEN, f"steps_{name}.npz")
+    if not os.path.exists(fx):
+        pytest.skip(f"{fx} not generated")
+    z = np.load(fx)
+    m = int(z["m"])
+    if tiles is not None:
+        monkeypatch.setenv("LRS_SLOT_TILES", tiles)
+        monkeypatch.setenv("LRS_AUV_TILES", tiles)
+    sv = solver.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(N, m, 6, 5)))
+    info = sv.tile_info()
+    kw = {"reoptLevel": 0, "fixedRank": int(z["rank_flag"])}
+    worst = {}
+    for K in [int(k) for k in z["ks"]]:
+        trips = z[f"K{K}_trips"]
+        if trips.shape[0] < K:
+            continue
+        d = sv.alm_steps(K, **kw)
+        assert d["inner"] == K, (K, d["inner"])
+        tau, rn, lag, pinf = trips[K - 1]
+        assert abs(d["tau"] - tau) <= TOL * abs(tau), (K, d["tau"], tau)
+        assert abs(d["lag"] - lag) <= TOL * abs(lag), (K, d["lag"], lag)
+        assert abs(d["pinf"] - pinf) <= TOL * max(abs(pinf), 1e-300), (K, d["pinf"], pinf)
+        assert abs(d["beta"] - z[f"K{K}_beta"][0]) <= TOL * abs(z[f"K{K}_beta"][0])
+        for key in ("R", "G", "s", "y", "cvs", "lam"):
+            ref = z[f"K{K}_{key}"]
+            ours = project_mvec(d[key]) if key in ("cvs", "lam") else project_factor(d[key], N)
+            if key == "lam" and np.linalg.norm(ref) == 0:
+                assert np.linalg.norm(ours) == 0
+                continue
+            e = rel_err(ours, ref)
+            worst[key] = max(worst.get(key, 0.0), e)
+            assert e < TOL, (K, key, e)
+    sv.close()
+    print(f"{name} tiles={info}: worst rel errors {worst}")
+    return info
+
+
+def test_c5_full_size_trips_match_reference(mods, monkeypatch):
+    """m = 10^6, the bench's config_c5 workload, on the default (tiled) path."""
+    info = _run(mods, "c5_m1e6", monkeypatch, None)
+    assert info == (1, 1), info   # the 2-D tiles are the path measured by config_c5
+
+
+@pytest.mark.parametrize("tiles", [None, "1"])
+def test_c5_m1e5_trips_match_reference(mods, monkeypatch, tiles):
+    info = _run(mods, "c5_m1e5", monkeypatch, tiles)
+    if tiles == "1":
+        assert info == (1, 1), info

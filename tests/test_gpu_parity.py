@@ -352,12 +352,15 @@ def test_dual_infeasibility_matches_dense_eig(solver_mod, name):
                     S[c, r] -= lam[i] * v
         ev = np.linalg.eigvalsh(S)[0]
         nS = max(1.0, np.abs(S).max() * d)
-        assert abs(lmin[k] - ev) <= 1e-8 * nS, (k, lmin[k], ev)
+        # the reference's ARPACK stopping rule (tol 1e-2 relative Ritz estimate) or the device's
+        # absolute one (1e-3 phase2Tol of the l_1 value): lrs_solver.cpp trl_min
+        bar = 1e-2 * max(abs(ev), 1e-10) + 1e-3 * 1e-5 * (1 + cn1) + 1e-10 * nS
+        assert ev <= lmin[k] + 1e-10 * nS and abs(lmin[k] - ev) <= bar, (k, lmin[k], ev)
         if d >= 40:
             w = sla.eigsh(S, k=1, which="SA", ncv=40, tol=1e-2, maxiter=600, return_eigenvectors=False)[0]
-            assert abs(lmin[k] - w) <= 1e-2 * max(1.0, abs(w)) + 1e-8 * nS, (k, lmin[k], w)
+            assert abs(lmin[k] - w) <= bar + 1e-2 * abs(w), (k, lmin[k], w)
         err += abs(min(ev, 0.0))
-    assert abs(l1 - err / (cn1 + 1)) <= 1e-8 * max(1.0, err / (cn1 + 1)) + 1e-12
+    assert abs(l1 - err / (cn1 + 1)) <= 2e-2 * err / (cn1 + 1) + 1e-3 * 1e-5 * len(dims) + 1e-12
     # the solve evaluated it too (main.c:515) and reports l_inf = l_1 (1 + ||C||_1) / (1 + ||C||_inf)
     assert res["dinf"] >= 0
     assert abs(res["dinf"] - l1) <= 1e-8 * max(1.0, l1) + 1e-12
@@ -410,16 +413,19 @@ def test_many_cones_stack_is_linear(solver_mod, tmp_path):
 
 
 def test_dinf_step_cap_flagged(solver_mod, monkeypatch):
-    """A dual-infeasibility eigen-solve stopped by its step cap reports dinf_converged = 0 and
-    the solve does not claim PRIMAL_DUAL_OPTIMAL on it (the Ritz value only bounds lambda_min
-    from above).  LRS_LANCZOS_CAP forces a 4-step cap."""
-    monkeypatch.setenv("LRS_LANCZOS_CAP", "4")
+    """A dual-infeasibility eigen-solve that runs out of update iterations reports
+    dinf_converged = 0 and the solve does not claim PRIMAL_DUAL_OPTIMAL on it (the Ritz value
+    only bounds lambda_min from above).  LRS_TRL_NCV / LRS_TRL_MAXITER force a
+    4-vector basis and no restart (the reference: ncv 40, 600 update iterations)."""
+    monkeypatch.setenv("LRS_TRL_NCV", "4")
+    monkeypatch.setenv("LRS_TRL_MAXITER", "0")
     sv = solver_mod.Solver(instance("theta40"))
     r = sv.solve(reoptLevel=0)
     sv.close()
     assert r["dinf_converged"] == 0 and r["dinf"] >= 0
     assert r["status"] != 1
-    monkeypatch.delenv("LRS_LANCZOS_CAP")
+    monkeypatch.delenv("LRS_TRL_NCV")
+    monkeypatch.delenv("LRS_TRL_MAXITER")
     sv = solver_mod.Solver(instance("mc_rand200"))
     r = sv.solve(reoptLevel=0)
     sv.close()

@@ -110,7 +110,7 @@ def test_rccl_world1_is_unsharded(solver_mod):
     assert sv.shard_info() == (1, 0, 0, 120, 0)
     r = sv.solve(reoptLevel=0)
     sv.close()
-    assert r["dinf"] >= 0          # the unsharded path (a sharded solve does not evaluate it)
+    assert r["dinf"] >= 0
 
 
 @pytest.mark.parametrize("name,world", [("mc_torus12x10", 2), ("mc_torus12x10", 4), ("mc_rand200", 3),
@@ -135,7 +135,9 @@ def test_sharded_full_solve_matches_single_gpu(solver_mod, name, world):
     for k in ("alm_pobj", "alm_dobj", "pobj", "dobj"):
         assert abs(first[k] - ref[k]) <= 1e-6 * max(1.0, abs(ref[k])), (k, first[k], ref[k])
     assert first["pinf"] <= max(1e-6, 10 * ref["pinf"])
-    assert first["dinf"] == -1.0 and first["dinf_converged"] == -1   # not evaluated when sharded
+    # the dual infeasibility is evaluated sharded too (trl_min over owned rows + halo)
+    assert first["dinf"] >= 0 and first["dinf_converged"] == ref["dinf_converged"]
+    assert first["status"] == ref["status"]
 
 
 @pytest.mark.parametrize("name,world", [("theta40", 2), ("theta40", 3), ("rsparse60", 2), ("rsparse60", 4),
