@@ -193,6 +193,11 @@ struct lrs_ctx {
     double dinf_tol = 1e-5;            // phase2Tol of the running solve (dual-infeasibility accuracy)
     long dinf_steps = 0, dinf_iters = 0;   // eigen-solve work of the running solve
     bool rank_warned = false;              // the rank clamp's stderr line, once per solve
+    int lbfgsL = 2;                        // lbfgsListLength of the running solve
+    // lbfgsListLength >= 3: the ring of L pairs (run_inner_generic)
+    std::vector<double *> ring_s, ring_y;
+    std::vector<double> ring_beta;
+    long ring_len = 0;
     double dinf_time = 0.0;
 };
 
@@ -476,6 +481,9 @@ static void free_work(lrs_ctx *c) {
                       W.cgc, W.tot, W.gl, W.CR, W.CD, W.GP};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
+    for (double *q : c->ring_s) if (q) (void)hipFree(q);
+    for (double *q : c->ring_y) if (q) (void)hipFree(q);
+    c->ring_s.clear(); c->ring_y.clear(); c->ring_beta.clear(); c->ring_len = 0;
     c->W = DevWork();
     c->dp.gp = nullptr;
     c->walloc = false;
@@ -496,6 +504,11 @@ static int zero_work(lrs_ctx *c) {
         if (z.p) HIPC(hipMemsetAsync(z.p, 0, sizeof(double) * z.n, c->st));
     c->head = 0; c->gcur = 0;
     c->beta[0] = c->beta[1] = c->yy[0] = c->yy[1] = 0;
+    for (size_t q = 0; q < c->ring_s.size(); ++q) {   // lbfgsListLength >= 3
+        HIPC(hipMemsetAsync(c->ring_s[q], 0, sizeof(double) * std::max(2L, c->ring_len), c->st));
+        HIPC(hipMemsetAsync(c->ring_y[q], 0, sizeof(double) * std::max(2L, c->ring_len), c->st));
+        c->ring_beta[q] = 0.0;
+    }
     return 0;
 }
 
@@ -1530,6 +1543,159 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     return 0;
 }
 
+// ---- inner loop for lbfgsListLength >= 3 (the fused kernels keep two pairs in coefficient
+// space).  The reference's own step sequence (lorads_alm.c:1302-1379) with the host in control
+// and device operators per step: LBFGSDirection's two-loop over the ring of L pairs
+// (lorads_alm.c:468-505, device dot / axpy), LBFGSDirectionUseGrad (:607-627), ALMCalq12p12
+// (:714-734), ALMLineSearch (:266-333, the device line search), SetyAsNegGrad (:768-783),
+// ALMupdateVar (:826-830), the A(X) update (:1351-1353), ALMCalGrad (:74-87), setlbfgsHisTwo
+// (:842-863), updateDimacsALM (lorads_alg_common.c:424-428) and the exits of :1359-1379.  The
+// ring is L device vectors pairs (lrs_ctx::ring_s / ring_y); about a dozen host reads per trip,
+// so this path is for the option's semantics, not for speed.
+static int ring_alloc(lrs_ctx *c, int L) {
+    if ((int)c->ring_s.size() == L && c->ring_len == c->dp.NRpad) return 0;
+    HIPC(hipStreamSynchronize(c->st));
+    for (double *q : c->ring_s) if (q) (void)hipFree(q);
+    for (double *q : c->ring_y) if (q) (void)hipFree(q);
+    c->ring_s.assign(L, nullptr);
+    c->ring_y.assign(L, nullptr);
+    for (int q = 0; q < L; ++q) {
+        HIPC(hipMalloc((void **)&c->ring_s[q], sizeof(double) * std::max(2L, c->dp.NRpad)));
+        HIPC(hipMalloc((void **)&c->ring_y[q], sizeof(double) * std::max(2L, c->dp.NRpad)));
+        HIPC(hipMemsetAsync(c->ring_s[q], 0, sizeof(double) * std::max(2L, c->dp.NRpad), c->st));
+        HIPC(hipMemsetAsync(c->ring_y[q], 0, sizeof(double) * std::max(2L, c->dp.NRpad), c->st));
+    }
+    c->ring_beta.assign(L, 0.0);
+    c->ring_len = c->dp.NRpad;
+    c->head = 0;
+    return 0;
+}
+
+// q1 = 2 A(sym R D^T), q2 = A(D D^T) into W.q1 / W.q2 and the device line search's finals;
+// p1 (before its factor 2) and p2 returned
+static int op_q12_fin(lrs_ctx *c, double *p1h, double *p2h) {
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    double a = 0, b = 0;
+    for (int k = 0; k < P.K; ++k) {
+        OPC(launch_sddmm(P, k, 2, W.R, W.D, W.uvt0, W.uvt1, W.part, 0, nullptr, c->st));
+        double t[2];
+        if (read_tmpfin(c, TF_SD + 2 * k, 2, t)) return -1;
+        a += t[0]; b += t[1];
+        const DevCone &dc = P.cones[k];
+        if (dc.dense_c) {   // <C, sym R D^T> = <R, C D>, <C, D D^T> = <D, C D>
+            OPC(launch_dense_cx(P, k, W.D, W.CD, 0.0, c->st));
+            double u, v;
+            if (op_dot(c, (long)dc.n * dc.ld, W.R + dc.foff, W.CD + dc.foff, &u)) return -1;
+            if (op_dot(c, (long)dc.n * dc.ld, W.D + dc.foff, W.CD + dc.foff, &v)) return -1;
+            a += u; b += v;
+        }
+    }
+    OPC(launch_gather(P, W.uvt0, 2.0, W.q1, nullptr, nullptr, c->st, nullptr));
+    OPC(launch_gather(P, W.uvt1, 1.0, W.q2, nullptr, nullptr, c->st, nullptr));
+    double *fin = device_fin();
+    double h[64] = {0};
+    h[0] = a; h[1] = b;
+    HIPC(h2d_sync(c, fin, h, sizeof(double) * 2 * std::max(1, std::min(P.K, 32))));
+    *p1h = a; *p2h = b;
+    return 0;
+}
+
+static int run_inner_generic(lrs_ctx *c, const lrs_params *p, double rho, double rctol, double gap, long budget,
+                             InnerIo &io, bool ph1_exit = true) {
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    const int L = p->lbfgsListLength;
+    if (sharded(c)) { set_err("lbfgsListLength %d: not supported in a sharded solve", L); return -1; }
+    if (ring_alloc(c, L)) return -1;
+    const long NR = P.NRpad;
+    double par[P_NPAR] = {0};
+    par[P_RHO] = rho; par[P_ENDTAU] = p->endTauTol;
+    HIPC(h2d_sync(c, W.par, par, sizeof(par)));
+    const double phase1 = ph1_exit ? p->phase1Tol : -1.0;
+    int exitr = EXIT_NONE;
+    for (;;) {
+        // loop head (lorads_alm.c:1302) and the budget (benchmarking)
+        if (!(io.rcval - rctol > p->endALMSubTol)) { exitr = EXIT_CONVERGED; break; }
+        if (budget > 0 && io.inner >= budget) { exitr = EXIT_BUDGET; break; }
+        if (io.local % 300 == 0) io.clear = 0;
+        const int nodeNum = io.clear <= L - 1 ? (int)io.clear : L;
+        double *G = W.G[c->gcur];
+        // LBFGSDirection: Dtemp = G; newest -> oldest alpha_i = beta_i <s_i, Dtemp>, Dtemp -= alpha_i y_i;
+        // oldest -> newest Dtemp += (alpha_i - beta_i <y_i, Dtemp>) s_i; D = -Dtemp
+        HIPC(hipMemcpyAsync(W.D, G, sizeof(double) * NR, hipMemcpyDeviceToDevice, c->st));
+        std::vector<double> alpha(L, 0.0);
+        int node = (c->head - 1 + L) % L;
+        for (int t = 0; t < nodeNum; ++t) {
+            double v;
+            if (op_dot(c, NR, c->ring_s[node], W.D, &v)) return -1;
+            alpha[node] = c->ring_beta[node] * v;
+            OPC(launch_axpby(NR, -alpha[node], c->ring_y[node], 1.0, W.D, c->st));
+            node = (node - 1 + L) % L;
+        }
+        node = (node + 1) % L;
+        for (int t = 0; t < nodeNum; ++t) {
+            double v;
+            if (op_dot(c, NR, c->ring_y[node], W.D, &v)) return -1;
+            OPC(launch_axpby(NR, alpha[node] - c->ring_beta[node] * v, c->ring_s[node], 1.0, W.D, c->st));
+            node = (node + 1) % L;
+        }
+        OPC(launch_axpby(NR, 0.0, W.D, -1.0, W.D, c->st));
+        double dg;
+        if (op_dot(c, NR, W.D, G, &dg)) return -1;
+        if (dg >= 0) OPC(launch_axpby(NR, -1.0, G, 0.0, W.D, c->st));   // LBFGSDirectionUseGrad
+        // q1, q2, p1, p2 and the line search
+        double p1, p2;
+        if (op_q12_fin(c, &p1, &p2)) return -1;
+        OPC(launch_ls_only(P, W, c->st));
+        double ls[LS_N];
+        HIPC(hipMemcpyAsync(c->hpin + 512, W.lsres, sizeof(ls), hipMemcpyDeviceToHost, c->st));
+        HIPC(hipStreamSynchronize(c->st));
+        memcpy(ls, c->hpin + 512, sizeof(ls));
+        const double tau = ls[LS_TAU];
+        if (ls[LS_ROOTNUM] == 0) { exitr = EXIT_NUMERR; break; }
+        if (std::fabs(tau) < p->endTauTol) {
+            io.inner++; io.local++; io.clear++;
+            exitr = EXIT_TINYTAU;
+            break;
+        }
+        // SetyAsNegGrad, ALMupdateVar, A(X) += tau q1 + tau^2 q2
+        double *ys = c->ring_y[c->head], *ss = c->ring_s[c->head];
+        OPC(launch_axpby(NR, -1.0, G, 0.0, ys, c->st));
+        OPC(launch_axpby(NR, tau, W.D, 1.0, W.R, c->st));
+        OPC(launch_axpby(P.m, tau, W.q1, 1.0, W.cvs, c->st));
+        OPC(launch_axpby(P.m, tau * tau, W.q2, 1.0, W.cvs, c->st));
+        // ALMCalGrad into the other gradient buffer
+        c->gcur ^= 1;
+        double lag;
+        if (op_grad(c, rho, &lag)) return -1;
+        // setlbfgsHisTwo: s = tau D, y += G_new, beta = 1 / <y, s>, head advances
+        OPC(launch_axpby(NR, tau, W.D, 0.0, ss, c->st));
+        OPC(launch_axpby(NR, 1.0, W.G[c->gcur], 1.0, ys, c->st));
+        double ysd;
+        if (op_dot(c, NR, ys, ss, &ysd)) return -1;
+        c->ring_beta[c->head] = 1.0 / ysd;
+        c->head = (c->head + 1) % L;
+        // updateDimacsALM (A(RR^T) afresh, the residual) and the exits of lorads_alm.c:1359-1379
+        double pinf;
+        if (op_constr_xx(c, W.R, nullptr, &pinf, nullptr)) return -1;
+        io.inner++; io.local++; io.clear++;
+        io.lag = lag;
+        io.pinf1 = pinf;
+        io.pinfinf = pinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+        c->last_trip[0] = tau; c->last_trip[1] = lag; c->last_trip[2] = pinf;
+        if (io.pinfinf <= phase1 && (gap <= phase1 || !p->highAccMode)) { exitr = EXIT_PHASE1; break; }
+        io.rcval = std::sqrt(lag) / (1 + c->hp.cNrmInf);
+        if (io.local > 800) { exitr = EXIT_LOCAL800; break; }
+    }
+    io.exitReason = exitr;
+    // the newest pair also in (S0, Y0) for the C-ABI readers (lrs_alm_last_step)
+    const int hn = (c->head - 1 + L) % L;
+    HIPC(hipMemcpyAsync(W.ls[0], c->ring_s[hn], sizeof(double) * NR, hipMemcpyDeviceToDevice, c->st));
+    HIPC(hipMemcpyAsync(W.ly[0], c->ring_y[hn], sizeof(double) * NR, hipMemcpyDeviceToDevice, c->st));
+    return 0;
+}
+
 static void alm_log(lrs_ctx *c, const lrs_params *p, const AlmState &st, double t) {
     int cur = c->t1c.empty() ? sum_rank(c) : c->t1c.back();
     int orc = c->t1o.empty() ? cur : c->t1o.back();
@@ -1601,7 +1767,9 @@ ALG_START:
             io.pinf1 = st.pinf1; io.pinfinf = st.pinfinf;
             for (;;) {
                 const long before = st.innerIter;
-                if (run_inner(c, p, st.rho, rc_tol, st.gap, budget, io)) return -1;
+                if (p->lbfgsListLength > 2 ? run_inner_generic(c, p, st.rho, rc_tol, st.gap, budget, io)
+                                           : run_inner(c, p, st.rho, rc_tol, st.gap, budget, io))
+                    return -1;
                 st.innerIter = io.inner; localIter = io.local; clearL = io.clear;
                 cur_iter_counter += io.inner - before;
                 rc_val = io.rcval; lag = io.lag; st.pinf1 = io.pinf1; st.pinfinf = io.pinfinf;
@@ -2530,6 +2698,8 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     c->dinf_tol = p->phase2Tol;
     c->dinf_steps = c->dinf_iters = 0;
     c->rank_warned = false;
+    if (p->lbfgsListLength < 1) { set_err("lbfgsListLength %d < 1", p->lbfgsListLength); return -1; }
+    c->lbfgsL = p->lbfgsListLength;
     c->dinf_time = 0.0;
     if (obj_unscale(c)) return -1;   // a previous solve's reopt scaled C on the device
     std::vector<int> r, rm;
@@ -2760,11 +2930,16 @@ int lrs_set_budget_hook(lrs_ctx *c, lrs_budget_hook hook, void *user) {
 int lrs_alm_last_step(lrs_ctx *c, double *out4, int *newest_pair) {
     if (!c || !out4) { set_err("null argument"); return -1; }
     // the control block the last inner loop stopped on: its fold is the last completed trip
-    const int L = 2;
+    const int L = c->lbfgsL;
     const int hn = c->head == 0 ? L - 1 : c->head - 1;
     out4[0] = c->last_trip[0];
     out4[1] = c->last_trip[1];
     out4[2] = c->last_trip[2];
+    if (L > 2) {   // run_inner_generic: the newest pair was copied to (S0, Y0)
+        out4[3] = c->ring_beta.empty() ? 0.0 : c->ring_beta[hn];
+        if (newest_pair) *newest_pair = 0;
+        return 0;
+    }
     out4[3] = c->beta[hn];
     if (newest_pair) *newest_pair = hn;
     return 0;

@@ -127,8 +127,8 @@ int main(int argc, char **argv) {
             fprintf(stderr, "[lrsdp] could not parse rank schedule %s; ignored\n", schedFile);
         }
     }
-    if (p.lbfgsListLength < 1 || p.lbfgsListLength > 2) {
-        fprintf(stderr, "[lrsdp] lbfgsListLength %d not supported on the device path; using 2\n", p.lbfgsListLength);
+    if (p.lbfgsListLength < 1) {   // the reference's ring needs one node at least (data/lorads_solver.c:686-706)
+        fprintf(stderr, "[lrsdp] lbfgsListLength %d < 1; using 2\n", p.lbfgsListLength);
         p.lbfgsListLength = 2;
     }
     printf("-----------------------------------------------------------\n");

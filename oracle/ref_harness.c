@@ -19,7 +19,7 @@
  *   kernels <file.dat-s> <rank> <in.bin> <out.bin>
  *       One call of each hot-path operator on caller-provided iterates (see
  *       scripts/make_golden.py for the exact binary layout).
- *   alm_steps <file.dat-s> <rank> <K[,K2,...]> <out.bin>
+ *   alm_steps <file.dat-s> <rank> <K[,K2,...]> <out.bin> [--flag value ...]
  *       From the reference's own initial point (srand(925), data/lorads_solver.c:625)
  *       the preamble of LORADS_ALMOptimize (lorads_alm.c:1233-1243) and exactly K
  *       trips of its inner L-BFGS loop (lorads_alm.c:1302-1379), through the same
@@ -368,6 +368,7 @@ static int mode_alm_steps(int argc, char **argv) {
     if (argc < 6) return 2;
     lorads_params p; default_params(&p);
     p.fname = argv[2];
+    if (argc > 6) parse_flags(&p, argc - 5, argv + 5);   /* trailing --flag value pairs */
     p.fixedRank = atoi(argv[3]);
     long Ks[64]; int nK = 0;
     for (char *tok = strtok(argv[4], ","); tok && nK < 64; tok = strtok(NULL, ",")) Ks[nK++] = atol(tok);

@@ -43,7 +43,12 @@ CASES = [
     # dense objective (C5b structure at test size, the reference's dense branches): the instance is
     # regenerated from ltr-lowrank-sdp_amd/instances.py random_sparse(300, 3000, 6, 7, dense_c=True)
     ("rdense300", "gen:rdense300", -1, [1, 2, 3, 4, 5]),
+    # --lbfgsListLength other than 2 (data/lorads_solver.c:686-706, lorads_alm.c:468-505): a ring of 3
+    # (a ring of 1 crashes the reference: its node links are only set in the loop that adds nodes 2..L)
+    ("mc_rand200_l3", os.path.join(GOLD, "instances", "mc_rand200.dat-s"), -1, [1, 2, 3, 4, 5, 8]),
+    ("theta40_l3", os.path.join(GOLD, "instances", "theta40.dat-s"), -1, [1, 2, 3, 4, 5, 8]),
 ]
+FLAGS = {"mc_rand200_l3": ["--lbfgsListLength", "3"], "theta40_l3": ["--lbfgsListLength", "3"]}
 GEN = {"rdense300": (300, 3000, 6, 7)}
 PROJ = {"mc_rand300w_r290": 4}
 
@@ -55,10 +60,10 @@ def project(v, n, k, seed=7):
     return v.reshape(r, n).T @ om
 
 
-def run_steps(path, rank, K, m, nr):
+def run_steps(path, rank, K, m, nr, flags=()):
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "s.bin")
-        r = subprocess.run([HARNESS, "alm_steps", path, str(rank), str(K), out], capture_output=True, text=True,
+        r = subprocess.run([HARNESS, "alm_steps", path, str(rank), str(K), out, *flags], capture_output=True, text=True,
                            env=dict(os.environ, OPENBLAS_NUM_THREADS="1"), timeout=600)
         if r.returncode != 0 or "REF_STEPS" not in r.stdout:
             raise RuntimeError(r.stdout[-2000:] + r.stderr[-2000:])
@@ -108,14 +113,15 @@ def main():
                 # first call with a generous nr guess; the dump's tail fixes the real size
                 with tempfile.TemporaryDirectory() as td:
                     o = os.path.join(td, "s.bin")
-                    subprocess.run([HARNESS, "alm_steps", path, str(rank), "1", o], capture_output=True, check=True,
+                    subprocess.run([HARNESS, "alm_steps", path, str(rank), "1", o, *FLAGS.get(name, [])],
+                                   capture_output=True, check=True,
                                    env=dict(os.environ, OPENBLAS_NUM_THREADS="1"), timeout=600)
                     a = np.fromfile(o)
                 done = int(a[0])
                 rest = a.size - 1 - 4 * done - 2 * m - 1
                 assert rest % 4 == 0
                 probe = rest // 4
-            d = run_steps(path, rank, K, m, probe)
+            d = run_steps(path, rank, K, m, probe, FLAGS.get(name, []))
             for k, v in d.items():
                 if name in PROJ and k in ("R", "G", "s", "y"):
                     v = project(v, dims[0], PROJ[name])
@@ -125,6 +131,7 @@ def main():
         out["dims"] = np.array(dims)
         out["nr"] = np.array(probe)
         out["rank_flag"] = np.array(rank)
+        out["lbfgs_len"] = np.array(int(FLAGS.get(name, ["", "2"])[1]))
         np.savez_compressed(os.path.join(GOLD, f"steps_{name}.npz"), **out)
         t = out[f"K{ks[-1]}_trips"]
         print(f"{name}: m={m} dims={dims} nr={probe} taus={np.round(t[:, 0], 6).tolist()}")

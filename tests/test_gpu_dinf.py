@@ -108,32 +108,43 @@ def run_sharded(mod, path, world, fn):
                                         ("rsparse60", 3), ("theta25x3", 2)])
 def test_sharded_dinf_matches_unsharded(mods, name, world):
     """The sharded eigen-solve (owned-row S v with the halo rows exchanged per step, the
-    Gram-Schmidt coefficients and norms all-reduced) on the same multipliers: every shard
-    reports the same lambda_min, equal to the unsharded one within the ARPACK bar, and a
-    sharded solve reports dinf and the same status as the unsharded solve."""
+    Gram-Schmidt coefficients and norms all-reduced): every shard reports the same lambda_min, and
+    the unsharded eigen-solve on the SAME multipliers (the shards' lambda gathered through the
+    shard plan's constraint ids) agrees within the ARPACK bar.  MaxCut (reproducible trajectory):
+    the sharded solve's dinf and status equal the unsharded solve's; theta / random sparse
+    (thousands of chaotic L-BFGS trips) compare on the shared multipliers only."""
     solver, _ = mods
-    single = solver.Solver(instance(name))
-    ref = single.solve(reoptLevel=0)
-    lam_ref = single.get_vec(solver.LAMBDA)
-    l1_ref, lm_ref = single.dual_infeasibility()
-    single.close()
     m, dims, b, Cb, A = read_sdpa_dense(instance(name))
     cn1 = sum(np.abs(Ck).sum() for Ck in Cb)
+    plans = [solver.shard_plan(instance(name), world, q) for q in range(world)]
 
     def fn(sv):
         r = sv.solve(reoptLevel=0)
-        return r, sv.dual_infeasibility()
+        return r, sv.dual_infeasibility(), sv.get_vec(solver.LAMBDA)
     res = run_sharded(solver, instance(name), world, fn)
     first = res[0]
-    for r, (l1, lm) in res[1:]:
+    for r, (l1, lm), _ in res[1:]:
         assert r["dinf"] == first[0]["dinf"] and np.array_equal(lm, first[1][1])
-    r, (l1, lm) = first
+    r, (l1, lm), _ = first
     assert r["dinf"] >= 0 and r["dinf_converged"] == 1
-    assert r["status"] == ref["status"], (r["status"], ref["status"])
-    # the sharded solve's multipliers differ from the single-GPU ones by summation order only
+    lam = np.full(m, np.nan)
+    for q, (_, _, lq) in enumerate(res):
+        g = plans[q]["con_gid"]
+        prev = lam[g]
+        assert np.all(np.isnan(prev) | (prev == lq)), "holders disagree on a shared multiplier"
+        lam[g] = lq
+    assert not np.isnan(lam).any()
+    single = solver.Solver(instance(name))
+    ref = single.solve(reoptLevel=0)
+    single.set_vec(solver.LAMBDA, lam)
+    l1_s, lm_s = single.dual_infeasibility()
+    single.close()
     for k in range(len(dims)):
-        assert abs(lm[k] - lm_ref[k]) <= 2 * bar(lm_ref[k], cn1) + 1e-6 * max(1.0, abs(lm_ref[k])), (k, lm, lm_ref)
-    assert abs(r["dinf"] - ref["dinf"]) <= 2e-3 * PHASE2 + 2e-2 * max(r["dinf"], ref["dinf"]) + 1e-9
+        assert abs(lm[k] - lm_s[k]) <= bar(lm_s[k], cn1), (k, lm, lm_s)
+    assert abs(l1 - l1_s) <= 2e-2 * max(l1, l1_s) + 1e-3 * PHASE2 * len(dims) + 1e-12
+    if name.startswith("mc_"):
+        assert r["status"] == ref["status"], (r["status"], ref["status"])
+        assert abs(r["dinf"] - ref["dinf"]) <= 2e-3 * PHASE2 + 2e-2 * max(r["dinf"], ref["dinf"]) + 1e-9
 
 
 def test_dense_objective_dinf_after_reopt(mods, monkeypatch, tmp_path):

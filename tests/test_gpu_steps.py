@@ -138,3 +138,43 @@ def test_fused_iterations_slot_tiles_match_reference(solver_mod, name, monkeypat
                 ours = project(ours, int(z["dims"][0]), PROJ[name])
             assert rel_err(ours, z[f"K{K}_{key}"]) < TOL, (K, key)
     sv.close()
+
+
+@pytest.mark.parametrize("name", ["mc_rand200_l3", "theta40_l3"])
+def test_lbfgs_ring_of_three_matches_reference(solver_mod, name):
+    """--lbfgsListLength 3 (data/lorads_solver.c:686-706: a ring of L pairs; LBFGSDirection's
+    two-loop over min(innerIter, L) of them, lorads_alm.c:468-505): the reference's own trips
+    (scripts/make_golden_steps.py with the flag) against run_inner_generic's, 1e-9."""
+    z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
+    assert int(z["lbfgs_len"]) == 3
+    base = name[:name.rindex("_l")]
+    sv = solver_mod.Solver(os.path.join(GOLDEN, "instances", f"{base}.dat-s"))
+    for K in [int(k) for k in z["ks"]]:
+        trips = z[f"K{K}_trips"]
+        if trips.shape[0] < K:
+            continue
+        d = sv.alm_steps(K, reoptLevel=0, lbfgsListLength=3)
+        assert d["inner"] == K, (K, d["inner"])
+        tau, rn, lag, pinf = trips[K - 1]
+        assert abs(d["tau"] - tau) <= TOL * abs(tau), (K, d["tau"], tau)
+        assert abs(d["lag"] - lag) <= TOL * abs(lag), (K, d["lag"], lag)
+        assert abs(d["pinf"] - pinf) <= TOL * max(abs(pinf), 1e-300), (K, d["pinf"], pinf)
+        assert abs(d["beta"] - z[f"K{K}_beta"][0]) <= TOL * abs(z[f"K{K}_beta"][0])
+        for key in ("R", "G", "cvs", "s", "y"):
+            assert rel_err(d[key], z[f"K{K}_{key}"]) < TOL, (K, key)
+    # a whole solve with the ring of 3 converges like the reference's default (objective within
+    # the golden solve's certified gap)
+    r = sv.solve(reoptLevel=0, lbfgsListLength=3)
+    sv.close()
+    assert r["pinf"] <= 1e-4 and r["alm_inner"] > 0
+
+
+def test_lbfgs_ring_of_one(solver_mod):
+    """--lbfgsListLength 1: the fused kernels' one-pair ring (the reference itself crashes on it:
+    its ring links are only set while adding nodes 2..L, data/lorads_solver.c:686-706); the solve
+    converges to the L = 2 objective."""
+    a = solver_mod.Solver(os.path.join(GOLDEN, "instances", "mc_rand200.dat-s"))
+    r1 = a.solve(reoptLevel=0, lbfgsListLength=1)
+    r2 = a.solve(reoptLevel=0)
+    a.close()
+    assert abs(r1["pobj"] - r2["pobj"]) <= 1e-5 * abs(r2["pobj"]), (r1["pobj"], r2["pobj"])
