@@ -3370,23 +3370,26 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
         __syncthreads();
         if (q + 1 < br.y) tb_fetch(pre, t.x, c0, n, r, ld, Rn);
         const int e1 = rp[cur.y + pl + 1];
+        // a thread's columns interleave with its row's three other threads (16-B chunks cq,
+        // cq + 4, ...): the four read 64 contiguous bytes per step, four distinct 16-B LDS slots
+        // (column quarters 256 B apart would put cq and cq + 2 on one bank)
         for (int e = rp[cur.y + pl]; e < e1; ++e) {
             const int2 en = ent[e];
             const double s = Sv[en.y];
-            const double2 *src = reinterpret_cast<const double2 *>(&rj[en.x * kTbS + cq * 16]);
+            const double2 *src = reinterpret_cast<const double2 *>(&rj[en.x * kTbS]) + cq;
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-                const double2 v = src[c];
+                const double2 v = src[4 * c];
                 g[2 * c] += s * v.x;
                 g[2 * c + 1] += s * v.y;
             }
         }
     }
     if (i < n) {
-        double *dst = GP + x * gstride + foff + (long)i * ld + c0 + cq * 16;
+        double2 *dst = reinterpret_cast<double2 *>(GP + x * gstride + foff + (long)i * ld + c0) + cq;
 #pragma unroll
         for (int c = 0; c < 8; ++c)
-            if (c0 + cq * 16 + 2 * c < ld) reinterpret_cast<double2 *>(dst)[c] = make_double2(g[2 * c], g[2 * c + 1]);
+            if (c0 + 2 * (cq + 4 * c) < ld) dst[4 * c] = make_double2(g[2 * c], g[2 * c + 1]);
     }
 }
 

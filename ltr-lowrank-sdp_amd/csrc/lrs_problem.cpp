@@ -431,6 +431,84 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
     return true;
 }
 
+// Entry order inside one 2-D tile item for conflict-free LDS reads (lrs_kernels.hip
+// auv_chunk): position t of an item is lane t % 64 of a wave-round, and a ds_read_b128
+// services a wave in four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32;
+// MI355X_MICROARCH.md §LDS) whose 16-B slots must differ.  A staged row of local index x sits
+// at slot x mod 16 (rows 17 slots apart), so a group reads without conflicts when its 16
+// entries have distinct p mod 16 and distinct q mod 16 (or share p: a broadcast).  The sorted
+// (p, q) order keeps p shared but leaves the 16 random q's colliding (~3-4 way).  Here each
+// group takes one entry from each cell (p mod 16, q mod 16) along a diagonal q = p + s of the
+// 16 x 16 cell grid while one is complete, then greedily distinct q's; only leftovers collide.
+// Results are unchanged: an entry's dot product is the same wherever it runs (k_auv_tsum sums
+// each constraint in entry order through `pos`; the slot epilogue's partial sums change order).
+static int swz_group_of(int lane) {
+    static const signed char g[64] = {0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0,
+                                      0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3,
+                                      2, 2, 2, 2, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2, 3, 3, 3, 3};
+    return g[lane & 63];
+}
+// perm[i] = the sorted-order index of the entry placed at item position i (0 <= i < cnt).
+// Groups of 16 are formed from a window of consecutive rows with distinct p mod 16 (so the
+// p side is conflict-free or a broadcast), taking entries of unused q mod 16 in row order;
+// a group the window cannot complete is filled with the next entries in order.
+static void swizzle_item(const unsigned *pq, long cnt, std::vector<long> &perm) {
+    std::vector<std::vector<long>> rows;   // entries of each row, in (p, q) order
+    for (long t = 0; t < cnt; ++t) {
+        if (t == 0 || (pq[t] >> 16) != (pq[t - 1] >> 16)) rows.emplace_back();
+        rows.back().push_back(t);
+    }
+    std::vector<long> order;
+    order.reserve(cnt);
+    size_t first = 0;
+    long left = cnt;
+    std::vector<long> keep;
+    while (left > 0) {
+        while (first < rows.size() && rows[first].empty()) ++first;
+        long grp[16];
+        int ng = 0;
+        bool pu[16] = {false}, qu[16] = {false};
+        for (size_t r = first; r < rows.size() && ng < 16; ++r) {
+            if (rows[r].empty()) continue;
+            const int pc = (int)((pq[rows[r][0]] >> 16) & 15);
+            if (pu[pc]) break;
+            pu[pc] = true;
+            keep.clear();
+            for (long t : rows[r]) {
+                const int qc = (int)(pq[t] & 15);
+                if (ng < 16 && !qu[qc]) { grp[ng++] = t; qu[qc] = true; }
+                else keep.push_back(t);
+            }
+            rows[r].swap(keep);
+        }
+        for (size_t r = first; r < rows.size() && ng < 16; ++r)
+            while (ng < 16 && !rows[r].empty()) {
+                grp[ng++] = rows[r].front();
+                rows[r].erase(rows[r].begin());
+            }
+        for (int k = 0; k < ng; ++k) order.push_back(grp[k]);
+        left -= ng;
+    }
+    // groups onto lane positions: wave-round w (64 consecutive positions) holds groups
+    // 4w..4w+3, group g's k-th member at the k-th lane of hardware group g; the last partial
+    // round keeps the remaining entries in order
+    perm.assign(cnt, -1);
+    std::vector<int> lanes[4];
+    for (int l = 0; l < 64; ++l) lanes[swz_group_of(l)].push_back(l);
+    const long ngt = (long)order.size() / 16;
+    long gi = 0;
+    for (long base = 0; gi < ngt && base + 64 <= cnt; base += 64)
+        for (int g = 0; g < 4 && gi < ngt; ++g, ++gi)
+            for (int k = 0; k < 16; ++k) perm[base + lanes[g][k]] = order[gi * 16 + k];
+    long o = gi * 16;
+    for (long i = 0; i < cnt; ++i)
+        if (perm[i] < 0) perm[i] = order[o++];
+}
+static bool tile_swizzle_on() {
+    const char *e = getenv("LRS_TILE_SWZ");
+    return !(e && e[0] == '0');
+}
+
 template <typename T>
 static bool dput(T **dst, const std::vector<T> &v, std::string &err) {
     size_t bytes = std::max<size_t>(1, v.size()) * sizeof(T);
@@ -562,6 +640,8 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             std::vector<int> item, pos(Zk);
             std::vector<unsigned> pq(Zk);
             long t0 = 0;
+            const bool swz = tile_swizzle_on();
+            std::vector<long> perm;
             for (long t = 0; t < Zk; ++t) {
                 pq[t] = (unsigned)(key[t].first & 0xffffffffu);
                 pos[t] = key[t].second;
@@ -573,6 +653,14 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 item.push_back((int)(tile % nt) * kAuvT);
                 item.push_back((int)t0);
                 item.push_back((int)(t + 1));
+                if (swz) {   // conflict-free LDS reads (swizzle_item)
+                    swizzle_item(pq.data() + t0, t + 1 - t0, perm);
+                    std::vector<unsigned> pq2(perm.size());
+                    std::vector<int> pos2(perm.size());
+                    for (size_t i = 0; i < perm.size(); ++i) { pq2[i] = pq[t0 + perm[i]]; pos2[i] = pos[t0 + perm[i]]; }
+                    std::copy(pq2.begin(), pq2.end(), pq.begin() + t0);
+                    std::copy(pos2.begin(), pos2.end(), pos.begin() + t0);
+                }
                 t0 = t + 1;
             }
             DevCone &d = dp.cones[k];
@@ -744,6 +832,8 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 std::vector<int> item, sl(P);
                 std::vector<unsigned> pq(P);
                 long t0 = 0;
+                const bool swz = tile_swizzle_on();
+                std::vector<long> perm;
                 for (long t = 0; t < P; ++t) {
                     pq[t] = (unsigned)(key[t].first & 0xffffffffu);
                     sl[t] = d.slot_off + key[t].second;
@@ -755,6 +845,14 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                     item.push_back((int)(tile % nt) * kAuvT);
                     item.push_back((int)t0);
                     item.push_back((int)(t + 1));
+                    if (swz) {   // conflict-free LDS reads (swizzle_item)
+                        swizzle_item(pq.data() + t0, t + 1 - t0, perm);
+                        std::vector<unsigned> pq2(perm.size());
+                        std::vector<int> sl2(perm.size());
+                        for (size_t i = 0; i < perm.size(); ++i) { pq2[i] = pq[t0 + perm[i]]; sl2[i] = sl[t0 + perm[i]]; }
+                        std::copy(pq2.begin(), pq2.end(), pq.begin() + t0);
+                        std::copy(sl2.begin(), sl2.end(), sl.begin() + t0);
+                    }
                     t0 = t + 1;
                 }
                 d.sa_items = (int)(item.size() / 4);

@@ -1543,7 +1543,7 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     return 0;
 }
 
-// ---- inner loop for lbfgsListLength >= 3 (the fused kernels keep two pairs in coefficient
+// ---- inner loop for lbfgsListLength != 2 (the fused kernels keep two pairs in coefficient
 // space).  The reference's own step sequence (lorads_alm.c:1302-1379) with the host in control
 // and device operators per step: LBFGSDirection's two-loop over the ring of L pairs
 // (lorads_alm.c:468-505, device dot / axpy), LBFGSDirectionUseGrad (:607-627), ALMCalq12p12
@@ -1767,7 +1767,7 @@ ALG_START:
             io.pinf1 = st.pinf1; io.pinfinf = st.pinfinf;
             for (;;) {
                 const long before = st.innerIter;
-                if (p->lbfgsListLength > 2 ? run_inner_generic(c, p, st.rho, rc_tol, st.gap, budget, io)
+                if (p->lbfgsListLength != 2 ? run_inner_generic(c, p, st.rho, rc_tol, st.gap, budget, io)
                                            : run_inner(c, p, st.rho, rc_tol, st.gap, budget, io))
                     return -1;
                 st.innerIter = io.inner; localIter = io.local; clearL = io.clear;
@@ -2935,7 +2935,7 @@ int lrs_alm_last_step(lrs_ctx *c, double *out4, int *newest_pair) {
     out4[0] = c->last_trip[0];
     out4[1] = c->last_trip[1];
     out4[2] = c->last_trip[2];
-    if (L > 2) {   // run_inner_generic: the newest pair was copied to (S0, Y0)
+    if (L != 2) {   // run_inner_generic: the newest pair was copied to (S0, Y0)
         out4[3] = c->ring_beta.empty() ? 0.0 : c->ring_beta[hn];
         if (newest_pair) *newest_pair = 0;
         return 0;

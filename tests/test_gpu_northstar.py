@@ -87,3 +87,50 @@ def test_northstar_solve_matches_reference(solver_mod, tmp_path, idx):
     assert abs(j["metrics"]["primal_dual_gap"]) <= max(1e-8, 10 * abs(rj["metrics"]["primal_dual_gap"]))
     for ph in ("phase_1", "phase_2"):
         assert j["trajectory"][ph]["curr_rank"] == rj["trajectory"][ph]["curr_rank"], ph
+
+
+def test_northstar_g81_r64_sharded_world8(solver_mod, tmp_path):
+    """BASELINE config C4 ("G81 rank 64, sharded across 8 MI355X"): the G81-like r = 64 instance
+    row-sharded 8 ways (the loopback transport: eight contexts on this GPU, one host thread each,
+    the same kernels, row partition, halo plan and host control the RCCL transport drives on
+    eight GPUs) against the reference's own solve (solves_northstar.json): ALM primal and dual
+    objectives within 1e-6, inner iterations within 2 %, every shard identical."""
+    import threading
+    g = [c for c in cases() if c["instance"] == "g81_torus100x200_r64"][0]
+    path = regenerate(tmp_path, g)
+    kw = {}
+    for k, v in zip(g["flags"][0::2], g["flags"][1::2]):
+        k = k.lstrip("-")
+        kw[k] = int(v) if k in ("reoptLevel", "fixedRank") else float(v)
+    world = 8
+    grp = solver_mod.LoopbackGroup(world)
+    out, errs = [None] * world, []
+
+    def work(q):
+        try:
+            sv = solver_mod.Solver(path)
+            sv.shard_loopback(grp, q)
+            out[q] = (sv.shard_info(), sv.solve(**kw))
+            sv.close()
+        except Exception as e:   # reported below
+            errs.append(f"rank {q}: {e!r}")
+
+    ts = [threading.Thread(target=work, args=(q,), daemon=True) for q in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(600)
+    assert not any(t.is_alive() for t in ts), "sharded run did not finish"
+    grp.close()
+    assert not errs, errs
+    assert sum(o[0][3] for o in out) == 20000
+    first = out[0][1]
+    for _, r in out[1:]:
+        for k in ("alm_inner", "alm_pobj", "alm_dobj", "pobj", "dinf"):
+            assert r[k] == first[k], (k, r[k], first[k])
+    ref = g["result"]
+    assert abs(first["alm_inner"] - ref["alm_inner"]) <= max(2, 0.02 * ref["alm_inner"]), (first["alm_inner"], ref)
+    assert rclose(first["alm_pobj"], ref["alm_pobj"], 1e-6), (first["alm_pobj"], ref["alm_pobj"])
+    assert rclose(first["alm_dobj"], ref["alm_dobj"], 1e-6), (first["alm_dobj"], ref["alm_dobj"])
+    assert rclose(first["pobj"], g["json"]["metrics"]["primal_obj"], 1e-6)
+    assert first["dinf"] >= 0

@@ -170,11 +170,15 @@ def test_lbfgs_ring_of_three_matches_reference(solver_mod, name):
 
 
 def test_lbfgs_ring_of_one(solver_mod):
-    """--lbfgsListLength 1: the fused kernels' one-pair ring (the reference itself crashes on it:
-    its ring links are only set while adding nodes 2..L, data/lorads_solver.c:686-706); the solve
-    converges to the L = 2 objective."""
+    """--lbfgsListLength 1 (the reference itself crashes on it: its ring links are only set while
+    adding nodes 2..L, data/lorads_solver.c:686-706): the generic ring path with one pair; the ALM
+    phase converges to the L = 2 objective within both phases' certified gaps.  (When the ALM phase
+    already meets phase2Tol the ADMM phase returns at once and reports the initial 1e30
+    objective, as the reference's LORADSADMMOptimize / LORADSInitADMMState do.)"""
     a = solver_mod.Solver(os.path.join(GOLDEN, "instances", "mc_rand200.dat-s"))
     r1 = a.solve(reoptLevel=0, lbfgsListLength=1)
     r2 = a.solve(reoptLevel=0)
     a.close()
-    assert abs(r1["pobj"] - r2["pobj"]) <= 1e-5 * abs(r2["pobj"]), (r1["pobj"], r2["pobj"])
+    tol = 10 * (r1["alm_gap"] + r2["alm_gap"]) + 1e-6
+    assert abs(r1["alm_pobj"] - r2["alm_pobj"]) <= tol * abs(r2["alm_pobj"]), (r1["alm_pobj"], r2["alm_pobj"], tol)
+    assert r1["alm_pinf"] <= 1e-3 and r1["alm_inner"] > 0
