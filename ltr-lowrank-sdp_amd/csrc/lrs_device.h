@@ -101,9 +101,11 @@ struct DevCone {
     std::vector<int> dra_n, drb_n;       // their entry counts (A: lower incl. diagonal, B: all)
     int *dra = nullptr, *drb = nullptr;
     long gl_need = 0;                    // doubles of slice gradients the B slices can need (any layout)
-    // dense objective (lrs_problem.h): C as a full n x n row-major matrix, not in the slots
+    // dense objective (lrs_problem.h), not in the slots: 1 = C as a full n x n row-major
+    // matrix, 2 = the constant C = c_alpha J (rank-one products, no matrix)
     int dense_c = 0;
     double *Cd = nullptr;
+    double c_alpha = 0.0;
     // long rows (>= kTileMinDeg adjacency entries per row on average): per row, the first entry
     // at or past column x n / kNX, x = 0..kNX ([n][kNX + 1]); the column-tiled k_wide_* kernels
     int *colseg = nullptr;
@@ -131,6 +133,7 @@ struct DevCone {
     int *sb_blk = nullptr, *sb_tp = nullptr, *sb_rp = nullptr, *sb_ent = nullptr;
     double *sa_S = nullptr;
 };
+constexpr int kMaxRankLd = 512;      // widest factor row (choose_layout: 64 lanes x 8 doubles)
 constexpr int kAuvT = 128;           // rows of one side of an A(X Y^T) tile
 constexpr int kAuvC = 32;            // factor columns staged in LDS at a time
 constexpr int kAuvThreads = 512;

@@ -3551,6 +3551,18 @@ __global__ void __launch_bounds__(kBlock) k_trl_dense(int n, double scale, const
         if (lane == 0) y[i] += scale * t;
     }
 }
+// constant objective: y += sa sum(v) (one block, fixed order)
+__global__ void __launch_bounds__(kBlock) k_trl_cj(int n, double sa, const double *__restrict__ v,
+                                                   double *__restrict__ y) {
+    double a[1] = {0.0};
+    for (int i = threadIdx.x; i < n; i += kBlock) a[0] += v[i];
+    double s[1];
+    block_reduce<1>(a, s);
+    __shared__ double tot;
+    if (threadIdx.x == 0) tot = sa * s[0];
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += kBlock) y[i] += tot;
+}
 // part[c][blockIdx.x] = sum over this block's rows of V[c][i] y[i], c = blockIdx.y
 __global__ void __launch_bounds__(kBlock) k_trl_dots(int n, const double *__restrict__ V, long ldv,
                                                      const double *__restrict__ y, double *__restrict__ part) {
@@ -3645,8 +3657,12 @@ int launch_trl_symv(const DevProblem &P, int cone, const double *S, const double
             snprintf(g_err, sizeof(g_err), "trl: dense cone needs the normalized vector");
             return -1;
         }
-        const int grid = std::max(1, std::min(2048, (c.n + kBlock / 64 - 1) / (kBlock / 64)));
-        hipLaunchKernelGGL(k_trl_dense, dim3(grid), dim3(kBlock), 0, st, c.n, P.dense_scale, c.Cd, vj ? vj : x, y);
+        if (c.dense_c == 2) {   // y += scale alpha 1 (1^T v)
+            hipLaunchKernelGGL(k_trl_cj, dim3(1), dim3(kBlock), 0, st, c.n, P.dense_scale * c.c_alpha, vj ? vj : x, y);
+        } else {
+            const int grid = std::max(1, std::min(2048, (c.n + kBlock / 64 - 1) / (kBlock / 64)));
+            hipLaunchKernelGGL(k_trl_dense, dim3(grid), dim3(kBlock), 0, st, c.n, P.dense_scale, c.Cd, vj ? vj : x, y);
+        }
         LRS_CHECK_LAUNCH();
     }
     return 0;
@@ -4337,6 +4353,61 @@ __global__ void __launch_bounds__(kBlock) k_cgemm(int n, int r, int ld, double s
     }
     if (part) write_partials<8, kBlock>(dots, part, poff + blockIdx.x);
 }
+// constant objective C = alpha J (DevCone::dense_c == 2, Lovász theta's -J): Y = sa 1 (1^T X)
+// (+ beta Y) with sa = scale alpha; one block of kCjThreads (the theta-class cones are small).
+// Column sums: thread t takes column t % ld over rows t / ld, t / ld + G, ... (G = threads per
+// column, four independent partial sums), then the G partials of a column are added in order:
+// fixed summation order.  With `ctrl` as k_cgemm: X = D and the partials <R, Y>, <X, Y> in
+// slots 0 and 1 of stage A's 8, at partial block `poff`.
+constexpr int kCjThreads = 1024;
+__global__ void __launch_bounds__(kCjThreads) k_cjx(int n, int r, int ld, double sa, const double *__restrict__ X,
+                                                    double *__restrict__ Y, double beta, const double *__restrict__ ctrl,
+                                                    const double *__restrict__ Rb0, const double *__restrict__ Rb1,
+                                                    double *__restrict__ part, int poff) {
+    __shared__ double ps[kCjThreads];
+    __shared__ double cs[kMaxRankLd];
+    const double *__restrict__ R = nullptr;
+    if (ctrl) {
+        if (ctrl[C_ACTIVE] == 0.0) return;
+        R = ctrl[C_RCUR] == 0.0 ? Rb0 : Rb1;
+    }
+    const int G = kCjThreads / ld;   // ld <= kMaxRankLd = kCjThreads / 2
+    const int c = threadIdx.x % ld, g = threadIdx.x / ld;
+    if (g < G) {
+        double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+        int i = g;
+        for (; i + 3 * G < n; i += 4 * G) {
+            t0 += X[(long)i * ld + c];
+            t1 += X[(long)(i + G) * ld + c];
+            t2 += X[(long)(i + 2 * G) * ld + c];
+            t3 += X[(long)(i + 3 * G) * ld + c];
+        }
+        for (; i < n; i += G) t0 += X[(long)i * ld + c];
+        ps[g * ld + c] = (t0 + t1) + (t2 + t3);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < ld; q += kCjThreads) {
+        double t = 0.0;
+        if (q < r)
+            for (int h = 0; h < G; ++h) t += ps[h * ld + q];
+        cs[q] = sa * t;
+    }
+    __syncthreads();
+    double dots[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const long tot = (long)n * ld;
+    for (long t = threadIdx.x; t < tot; t += kCjThreads) {
+        const int cc = (int)(t % ld);
+        if (cc >= r) continue;
+        double v = cs[cc];
+        if (beta != 0.0) v += beta * Y[t];
+        Y[t] = v;
+        if (R) {
+            dots[0] += R[t] * v;
+            dots[1] += X[t] * v;
+        }
+    }
+    if (part) write_partials<8, kCjThreads>(dots, part, poff);
+}
 static int cgemm_grid(const DevCone &c) {
     const long tiles = (long)((c.n + kCgBM - 1) / kCgBM) * ((c.r + kCgBN - 1) / kCgBN);
     return (int)std::max(1L, std::min((long)kCgMaxGrid, tiles));
@@ -4348,6 +4419,12 @@ int launch_dense_cx(const DevProblem &P, int cone, const double *X, double *Y, d
         snprintf(g_err, sizeof(g_err), "dense objective: sharded cones are not supported");
         return -1;
     }
+    if (c.dense_c == 2) {
+        hipLaunchKernelGGL(k_cjx, dim3(1), dim3(kCjThreads), 0, st, c.n, c.r, c.ld, P.dense_scale * c.c_alpha, X + c.foff,
+                           Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0);
+        LRS_CHECK_LAUNCH();
+        return 0;
+    }
     hipLaunchKernelGGL(k_cgemm, dim3(cgemm_grid(c)), dim3(kBlock), 0, st, c.n, c.r, c.ld, P.dense_scale, c.Cd,
                        X + c.foff, Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0);
     LRS_CHECK_LAUNCH();
@@ -4356,12 +4433,19 @@ int launch_dense_cx(const DevProblem &P, int cone, const double *X, double *Y, d
 int dense_cd_blocks(const DevProblem &P) {
     int nb = 0;
     for (const DevCone &c : P.cones)
-        if (c.dense_c) nb += cgemm_grid(c);
+        if (c.dense_c) nb += c.dense_c == 2 ? 1 : cgemm_grid(c);
     return nb;
 }
 int launch_dense_cd(const DevProblem &P, const DevWork &W, const double *ctrl, int off, hipStream_t st) {
     for (const DevCone &c : P.cones) {
         if (!c.dense_c) continue;
+        if (c.dense_c == 2) {
+            hipLaunchKernelGGL(k_cjx, dim3(1), dim3(kCjThreads), 0, st, c.n, c.r, c.ld, P.dense_scale * c.c_alpha,
+                               W.D + c.foff, W.CD + c.foff, 0.0, ctrl, W.R + c.foff, W.R2 + c.foff, W.part, off);
+            LRS_CHECK_LAUNCH();
+            off += 1;
+            continue;
+        }
         const int grid = cgemm_grid(c);
         hipLaunchKernelGGL(k_cgemm, dim3(grid), dim3(kBlock), 0, st, c.n, c.r, c.ld, P.dense_scale, c.Cd, W.D + c.foff,
                            W.CD + c.foff, 0.0, ctrl, W.R + c.foff, W.R2 + c.foff, W.part, off);

@@ -155,8 +155,20 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
             if (ev && ev[0] == '0') c.dense_c = false;
             else if (ev && ev[0] == '1') c.dense_c = ncobj > 0;
             else c.dense_c = c.n >= kDenseCMinN && 4 * ncobj >= tri;
+            // constant C (all entries one value): the rank-one products, no n x n matrix
+            const char *ek = getenv("LRS_CONST_C");
+            if (ek && ek[0] == '1' && !(ev && ev[0] == '0') && c.n >= kConstCMinN && ncobj == tri) {
+                double v0 = 0.0;
+                bool same = true, first = true;
+                for (auto &e : me) {
+                    if (e.con != 0) continue;
+                    if (first) { v0 = e.v; first = false; }
+                    else if (e.v != v0) { same = false; break; }
+                }
+                if (same && v0 != 0.0) { c.const_c = true; c.c_alpha = v0; c.dense_c = true; }
+            }
         }
-        if (c.dense_c) c.Cfull.assign((size_t)c.n * c.n, 0.0);
+        if (c.dense_c && !c.const_c) c.Cfull.assign((size_t)c.n * c.n, 0.0);
         // pattern = unique (row,col), row-major
         std::vector<std::pair<int, int>> pr;
         pr.reserve(me.size());
@@ -187,8 +199,10 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
                 c.cNrmInf = std::max(c.cNrmInf, std::fabs(a));
                 cn++;
                 if (c.dense_c) {
-                    c.Cfull[(size_t)r.row * c.n + r.col] += r.v;
-                    if (!dg) c.Cfull[(size_t)r.col * c.n + r.row] += r.v;
+                    if (!c.const_c) {
+                        c.Cfull[(size_t)r.row * c.n + r.col] += r.v;
+                        if (!dg) c.Cfull[(size_t)r.col * c.n + r.row] += r.v;
+                    }
                     continue;
                 }
                 const int sl = slot_of(r.row, r.col);
@@ -295,8 +309,13 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
     }
     for (int k = 0; k < K; ++k)
         if (g.cones[k].n < world) { err = "sharded solve: a cone has fewer rows than shards"; return false; }
+    // a constant objective (C = c_alpha J) is sharded as the slot path: every pair with an owned
+    // endpoint carries C in the local pattern, every row is in the halo
     for (int k = 0; k < K; ++k)
-        if (g.cones[k].dense_c) { err = "sharded solve: dense-objective cones are not supported"; return false; }
+        if (g.cones[k].dense_c && !g.cones[k].const_c) {
+            err = "sharded solve: dense-objective cones are not supported";
+            return false;
+        }
     plan = ShardPlan();
     plan.world = world; plan.rank = rank;
     plan.cones.assign(K, ShardConePlan());
@@ -342,7 +361,7 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
         const HostCone &gc = g.cones[k];
         ShardConePlan &cp = plan.cones[k];
         const int n = gc.n, r0 = cp.bounds[rank], r1 = cp.bounds[rank + 1];
-        std::vector<char> need(n, 0);
+        std::vector<char> need(n, gc.const_c ? 1 : 0);
         for (int i = r0; i < r1; ++i) {
             need[i] = 1;
             for (int q = gc.adj_ptr[i]; q < gc.adj_ptr[i + 1]; ++q) need[gc.adj_col[q]] = 1;
@@ -374,6 +393,11 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
             if (!gc.Chas[t] || (owner(k, i) != rank && owner(k, j) != rank)) continue;
             raw.push_back({k, 0, lid[k][i], lid[k][j], gc.Craw[t]});
         }
+        if (gc.const_c)   // every lower pair with an owned endpoint (local ids keep the global order)
+            for (int i = 0; i < gc.n; ++i)
+                for (int j = 0; j <= i; ++j)
+                    if (owner(k, i) == rank || owner(k, j) == rank)
+                        raw.push_back({k, 0, lid[k][i], lid[k][j], gc.c_alpha});
         for (const HostEntry &e : gc.ent) {
             const int i = gc.prow[e.slot], j = gc.pcol[e.slot];
             if (owner(k, i) != rank && owner(k, j) != rank) continue;   // slot not present here
@@ -415,7 +439,7 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
             if (q == rank) continue;
             const int q0 = cp.bounds[q], q1 = cp.bounds[q + 1];
             for (int i = r0; i < r1; ++i) {
-                bool adj = false;
+                bool adj = gc.const_c;   // C couples every pair of rows
                 for (int t = gc.adj_ptr[i]; t < gc.adj_ptr[i + 1] && !adj; ++t)
                     adj = gc.adj_col[t] >= q0 && gc.adj_col[t] < q1;
                 if (adj) cp.send_rows.push_back(lid[k][i]);
@@ -903,8 +927,13 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             }
         }
         if (c.dense_c) {
-            if (!dput(&d.Cd, c.Cfull, err)) return false;
-            d.dense_c = 1;
+            if (c.const_c) {
+                d.dense_c = 2;
+                d.c_alpha = c.c_alpha;
+            } else {
+                if (!dput(&d.Cd, c.Cfull, err)) return false;
+                d.dense_c = 1;
+            }
             dp.ndense++;
         }
     }

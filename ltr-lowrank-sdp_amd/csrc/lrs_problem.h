@@ -30,11 +30,20 @@ struct HostCone {
     // FP64 matrix cores, out of the slot pattern (which then holds the constraints only)
     bool dense_c = false;
     std::vector<double> Cfull;
+    // constant objective C = c_alpha J (every entry of the block equal, e.g. Lovász theta's -J):
+    // the dense path's products without the matrix, C X = c_alpha 1 (1^T X)
+    bool const_c = false;
+    double c_alpha = 0.0;
 };
 // Dense-objective policy: LRS_DENSE_C=0 never, =1 every cone with objective entries, unset:
 // cones with n >= kDenseCMinN whose C fills >= 1/4 of the lower triangle (measured: the dense
 // path is 0.86x the slot path at n = 500, 2.2x at n = 2000, scripts/c5b_probe.py).
 constexpr int kDenseCMinN = 1024;
+// Constant-objective policy: with LRS_CONST_C=1 every block whose C has all n (n + 1) / 2
+// entries equal takes the rank-one products (any n >= 2).  Off by default: on the multi-launch
+// iteration theta3 runs 64 us per iteration that way against 44 us on the slot path (its rows
+// lose the ~150 C entries that spread them over lane-group teams; profiles/r03e_theta_const.md).
+constexpr int kConstCMinN = 2;
 
 struct HostProblem {
     int m = 0, K = 0, nLp = 0;

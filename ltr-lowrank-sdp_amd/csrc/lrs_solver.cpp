@@ -2567,22 +2567,12 @@ int lrs_vec_get(lrs_ctx *c, int which, double *v) {
 
 int lrs_op_q12(lrs_ctx *c, double *q1, double *p1, double *q2, double *p2) {
     if (c) bind(c);
-    DevProblem &P = c->dp;
     DevWork &W = c->W;
+    DevProblem &P = c->dp;
+    // q1, q2 and p1, p2 (a dense objective's <R, C D>, <D, C D> included) with the finals the
+    // device line search consumes
     double a = 0, b = 0;
-    for (int k = 0; k < P.K; ++k) {
-        OPC(launch_sddmm(P, k, 2, W.R, W.D, W.uvt0, W.uvt1, W.part, 0, nullptr, c->st));
-        double t[2];
-        if (read_tmpfin(c, TF_SD + 2 * k, 2, t)) return -1;
-        a += t[0]; b += t[1];
-    }
-    OPC(launch_gather(P, W.uvt0, 2.0, W.q1, nullptr, nullptr, c->st, nullptr));
-    OPC(launch_gather(P, W.uvt1, 1.0, W.q2, nullptr, nullptr, c->st, nullptr));
-    // also leave the finals the device line search consumes
-    double *fin = device_fin();
-    double h[128] = {0};
-    for (int k = 0; k < P.K && k < 32; ++k) { h[2 * k] = (k == 0 ? a : 0.0); h[2 * k + 1] = (k == 0 ? b : 0.0); }
-    HIPC(h2d_sync(c, fin, h, sizeof(double) * 2 * std::max(1, std::min(P.K, 32))));
+    if (op_q12_fin(c, &a, &b)) return -1;
     if (p1) *p1 = 2 * a;
     if (p2) *p2 = b;
     HIPC(hipStreamSynchronize(c->st));

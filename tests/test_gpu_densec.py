@@ -99,9 +99,14 @@ def test_dense_objective_steps_match_reference(solver_mod, gen_dir, mode, kpath)
     _steps_check(solver_mod, _rdense(gen_dir, 300, 3000, 6, 7), z, mode, kpath)
 
 
+@pytest.mark.parametrize("const", ["0", "1"])
 @pytest.mark.parametrize("name,kpath", [("theta40", 0), ("theta40", 1), ("theta40", 2), ("theta25x3", 0),
                                         ("theta25x3", 1), ("theta25x3", 2)])
-def test_theta_dense_objective_steps_match_reference(solver_mod, name, kpath):
+def test_theta_dense_objective_steps_match_reference(solver_mod, name, kpath, const, monkeypatch):
+    """theta's C = -J through the dense path: as a full matrix on the matrix cores (k_cgemm,
+    LRS_CONST_C=0) and as the constant objective's rank-one products (k_cjx, the default for a
+    block whose C entries are all equal)."""
+    monkeypatch.setenv("LRS_CONST_C", const)
     z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
     _steps_check(solver_mod, instance(name), z, "1", kpath)
 
@@ -131,7 +136,9 @@ def test_dense_objective_solve_matches_reference(solver_mod, gen_dir, idx):
     assert abs(res["dobj"] - j["dual_obj"]) <= 1e-4 * abs(j["dual_obj"]), (res["dobj"], j["dual_obj"])
 
 
-def test_dense_and_slot_paths_agree_on_theta(solver_mod):
+@pytest.mark.parametrize("const", ["0", "1"])
+def test_dense_and_slot_paths_agree_on_theta(solver_mod, const, monkeypatch):
+    monkeypatch.setenv("LRS_CONST_C", const)
     out = {}
     for mode in ("0", "1"):
         with dense_mode(mode):
