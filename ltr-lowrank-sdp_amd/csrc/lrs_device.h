@@ -163,7 +163,8 @@ struct ShardHooks {
 
 struct DevProblem {
     const ShardHooks *shard = nullptr;   // non-null in a sharded solve
-    int no_lat = 0;                      // kernel path (lrs_set_kernel_path): 1 never the latency kernels, 2 + bandwidth regime, 3 + long-row kernels
+    int no_lat = 0;                      // kernel path (lrs_set_kernel_path): 1 never the latency kernels, 2 + bandwidth regime, 3 + long-row kernels, 4 the single-workgroup inner loop
+    int *slot_g = nullptr;               // [Ptot][2] every slot's (row, col) in the all-cones row space
     mutable int last_path = -1;          // path of the last enqueued iteration (0 lat, 1 general)
     int m = 0, K = 0;
     long NRpad = 0;     // factor buffer length (doubles)
@@ -305,6 +306,12 @@ bool alm_stage_a_split(const DevProblem &P);
 bool alm_stage_b_split(const DevProblem &P);   // stage B likewise (line search + update, gradient)
 // a subset of the stages (mask bit 0 = A, 1 = G, 2 = B), for per-stage timing
 int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t st);
+
+// ---- single-workgroup persistent inner loop (lrs_kernels.hip "Single-workgroup"): small
+// problems (R and D of every cone in one CU's LDS, ld <= 64, no full dense C) ----
+bool small_alm_fits(const DevProblem &P, DevWork &W);
+int launch_small_alm(const DevProblem &P, DevWork &W, const double *ctrl_in, double *ctrl_out, double *ls_out,
+                     hipStream_t st);
 
 // ---- device-resident CG (lrs_kernels.hip "Device-resident CG") ----
 enum CgIdx { CG_ACTIVE = 0, CG_ITERS, CG_BNORM, CG_RR, CG_QTR0, CG_QTR1, CG_N = 8 };

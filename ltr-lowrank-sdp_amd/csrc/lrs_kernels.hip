@@ -4675,11 +4675,15 @@ static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &
     return lp;
 }
 
+// the multi-launch kernel family forced by lrs_set_kernel_path (4, the single-workgroup inner
+// loop, counts as auto here: where that kernel does not fit, the iteration runs as with 0)
+static int multi_path(const DevProblem &P) { return P.no_lat == 4 ? 0 : P.no_lat; }
+
 // Whether stage A runs as two launches (bandwidth regime) for the current layouts.
 bool alm_stage_a_split(const DevProblem &P) {
     for (int k = 0; k < P.K; ++k) {
         StagePlan pa;
-        if (plan_a(P.cones[k], P.K, pa, P.no_lat)) return false;
+        if (plan_a(P.cones[k], P.K, pa, multi_path(P))) return false;
         if (!pa.small) return true;
     }
     return false;
@@ -4689,7 +4693,7 @@ bool alm_stage_a_split(const DevProblem &P) {
 bool alm_stage_b_split(const DevProblem &P) {
     for (int k = 0; k < P.K; ++k) {
         StagePlan pb;
-        if (plan_b(P.cones[k], P.K, pb, P.no_lat)) return false;
+        if (plan_b(P.cones[k], P.K, pb, multi_path(P))) return false;
         if (!pb.small) return true;
     }
     return false;
@@ -4761,7 +4765,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     int nblkA = 0, nblkB = 0;
     bool split = sh != nullptr;   // stage A as two launches (bandwidth regime; always when sharded)
     for (int k = 0; k < KL; ++k) {
-        if (plan_a(cone_of(k), KL, pa[k], P.no_lat) || plan_b(cone_of(k), KL, pb[k], P.no_lat)) return -1;
+        if (plan_a(cone_of(k), KL, pa[k], multi_path(P)) || plan_b(cone_of(k), KL, pb[k], multi_path(P))) return -1;
         nblkA += pa[k].grid;
         nblkB += pb[k].grid;
         if (!pa[k].small) split = true;
@@ -4794,7 +4798,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     // latency regime: every launch of both stages on the k_lat kernels, or none
     LatPlan lg[kMaxCones];
     const int ngd = P.ndense ? dense_cd_blocks(P) : 0;   // dense objective: C D's partial blocks
-    bool lat = !sh && !split && !P.no_lat;
+    bool lat = !sh && !split && !multi_path(P);
     int nla = 0, nlb = 0, nlf = 0;
     for (int k = 0; k < KL && lat; ++k) {
         lg[k] = lat_plan(cone_of(k), pa[k], pb[k]);
@@ -5053,6 +5057,574 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     }
     if (mark(3)) return -1;
     return mark(4);
+}
+
+// ------------------------------------------------------------------------
+// Single-workgroup persistent ALM inner loop (small problems: theta-class cones, tiny MaxCut).
+// The whole inner L-BFGS loop (lorads_alm.c:1302-1379) of one run_inner call runs in ONE
+// launch of one workgroup: the trips are separated by workgroup barriers instead of kernel
+// boundaries (no grid barrier, no inter-workgroup hand-off), the factor R and the direction D
+// stay in LDS, the control block in LDS, the rest (G, the L-BFGS pairs, the per-constraint
+// records) in global memory, which this one CU's L1 / the XCD's L2 serve.  Per trip, the same
+// arithmetic as k_it_a / k_it_g / k_it_b (MODE 0) with the dense objective's carried C R
+// (constant objectives C = alpha J: column sums): ctrl_step (fold of the previous trip's ten
+// dots, L-BFGS coefficients), D, the pattern SDDMM with the local constraints' q1 / q2 and
+// records, the global constraints', the wave-parallel line search, R += tau D, S R_new and
+// A(R_new R_new^T) per row, the new L-BFGS pair and the ten dots.  The loop ends where the
+// multi-launch iteration's control would (ctrl_step's exits), so every run_inner call is one
+// launch and one host synchronisation.
+// ------------------------------------------------------------------------
+constexpr int kSmallThreads = 512;
+constexpr int kSmallMaxConst = 4;     // constant-objective cones the kernel carries
+constexpr int kSmallMaxLd = 64;       // widest factor row (tpr <= 16 threads per row, <= 4 columns each)
+constexpr int kSmallCols = 4;         // factor columns per thread in the row phase
+struct SmallArgs {
+    int N, K, m, Ptot, mg, nadj, al;
+    const int2 *slot_g;                      // [Ptot] merged-space (row, col) of each slot (row >= col)
+    const int *adj_ptr, *adj_low, *adj_col, *adj_slot;   // merged (or the single cone's) adjacency
+    const double *Cw, *Craw;
+    const double2 *loc1, *slot1;
+    const int *loc_ptr, *loc_con, *slot_ptr, *slot_con;
+    const double *loc_w, *slot_a;
+    const int *glob, *con_ptr, *con_slot;
+    const double *con_w;
+    const double *b, *lam;
+    double *cvs, *rec, *uRD, *uDD, *uRR;
+    double *R, *G0, *G1, *s0, *y0, *s1, *y1;
+    const double *par;
+    const double *ctrl_in;
+    double *ctrl_out, *ls_out;
+    int nconst;
+    int cst_row0[kSmallMaxConst], cst_n[kSmallMaxConst];
+    double cst_sa[kSmallMaxConst];
+};
+
+// diagnostics build: thread 0 adds each phase's wall-clock ticks (100 MHz) into g_phase[3][q]
+// (q: 0 control, 1 direction, 2 slots, 3 global + reduction, 4 line search, 5 R / S update,
+// 6 rows, 7 global + reduction; 15 the trips)
+#ifdef LRS_PHASE_TIMING
+#define LRS_SM_T(q) do { if (tid == 0) { const unsigned long long t_ = wall_clock64(); sm_t[q] += t_ - sm_last; sm_last = t_; } } while (0)
+#define LRS_SM_MARK(v) unsigned long long v = tid == 0 ? wall_clock64() : 0
+#define LRS_SM_SUB(q, v) do { if (tid == 0) sm_t[q] += wall_clock64() - v; } while (0)
+#else
+#define LRS_SM_T(q) do { } while (0)
+#define LRS_SM_MARK(v) do { } while (0)
+#define LRS_SM_SUB(q, v) do { } while (0)
+#endif
+template <int LD, bool AL>
+__global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
+    constexpr int LS = LD + 2;          // LDS row stride (doubles): 16-B aligned rows
+    constexpr int H = LD / 2;           // double2 per row
+    constexpr int LS2 = LS / 2;
+    // row phases: TPR threads per row, H2 double2 each (pair p of lane l: columns 2 (l + TPR p), + 1);
+    // few lanes per row: the cross-lane sums of the per-entry dots cost VALU issue per lane
+    // (the loops are VALU-bound, not LDS-bound, at two waves per SIMD)
+    constexpr int TPR = LD <= 32 ? 4 : 8;
+    constexpr int H2 = H / TPR, RPP = kSmallThreads / TPR;
+    static_assert(H2 * TPR == H, "row split");
+    constexpr int T = kSmallThreads;
+    extern __shared__ double dyn[];
+    const int N = A.N, tid = threadIdx.x;
+    // LDS: R, D; per-slot X1 (uDD, then S); with AL a second per-slot array (uRD, then uRR)
+    // and the adjacency ((column, slot) pairs, row pointers, lower-entry ends), without AL
+    // (the lean layout, larger cones) those stay in global memory
+    double *Rs = dyn, *Ds = dyn + (long)N * LS, *X1 = dyn + 2L * N * LS, *X2 = X1 + A.Ptot;
+    int2 *Ladj = reinterpret_cast<int2 *>(X2 + A.Ptot);
+    int *Lptr = reinterpret_cast<int *>(Ladj + A.nadj), *Llow = Lptr + N + 1;
+    double *XA = AL ? X2 : A.uRD, *XB = AL ? X2 : A.uRR;
+    auto adj = [&](int q) -> int2 {
+        if constexpr (AL) return Ladj[q];
+        else return make_int2(A.adj_col[q], A.adj_slot[q]);
+    };
+    auto aptr = [&](int i) -> int {
+        if constexpr (AL) return Lptr[i];
+        else return A.adj_ptr[i];
+    };
+    auto alow = [&](int i) -> int {
+        if constexpr (AL) return Llow[i];
+        else return A.adj_low[i];
+    };
+    const double2 *Rs2 = reinterpret_cast<const double2 *>(Rs), *Ds2 = reinterpret_cast<const double2 *>(Ds);
+    __shared__ double c[C_NCTRL];
+    __shared__ double red[16];
+    __shared__ double ls[LS_N];
+    __shared__ double csR[kSmallMaxConst][kSmallMaxLd], csD[kSmallMaxConst][kSmallMaxLd];
+    __shared__ double cpart[kSmallThreads];
+    const int lane = tid & 63, wv = tid >> 6, sl_lane = tid % TPR;
+    const double rho = A.par[P_RHO], rhoInv = 1.0 / rho;
+    if (tid < LS_N) ls[tid] = 0.0;
+    // R into LDS, the control block, the adjacency
+    for (int e = tid; e < N * H; e += T) {
+        const int i = e / H, q = e - i * H;
+        reinterpret_cast<double2 *>(Rs + (long)i * LS)[q] = reinterpret_cast<const double2 *>(A.R + (long)i * LD)[q];
+    }
+    if (tid < C_NCTRL) c[tid] = A.ctrl_in[tid];
+    if (AL) {
+        for (int e = tid; e < A.nadj; e += T) Ladj[e] = make_int2(A.adj_col[e], A.adj_slot[e]);
+        for (int e = tid; e <= N; e += T) {
+            Lptr[e] = A.adj_ptr[e];
+            if (e < N) Llow[e] = A.adj_low[e];
+        }
+    }
+    __syncthreads();
+    // constant objectives: column sums (C R = sa 1 (1^T R), carried with tau like C R)
+    auto colsums = [&](const double *X, double (*cs)[kSmallMaxLd]) {
+        constexpr int G = kSmallThreads / LD;
+        for (int q = 0; q < A.nconst; ++q) {
+            const int col = tid % LD, g = tid / LD;
+            double t = 0.0;
+            if (g < G)
+                for (int i = g; i < A.cst_n[q]; i += G) t += X[(long)(A.cst_row0[q] + i) * LS + col];
+            __syncthreads();
+            cpart[tid] = t;
+            __syncthreads();
+            if (tid < LD) {
+                double s = 0.0;
+                for (int h = 0; h < G; ++h) s += cpart[h * LD + tid];
+                cs[q][tid] = s;
+            }
+        }
+        __syncthreads();
+    };
+    __syncthreads();
+    if (A.nconst) colsums(Rs, csR);
+    double lsflag = 0.0, lstau = 0.0;
+    int fold = 0;
+#ifdef LRS_PHASE_TIMING
+    unsigned long long sm_t[16] = {0}, sm_last = wall_clock64();
+#endif
+    for (;;) {
+        // ---- control (k_it_a's fold + ctrl_step, the phase-1 test on the whole residual)
+        if (tid == 0) ctrl_step(c, A.par, lsflag, lstau, fold, red, true);
+        __syncthreads();
+        LRS_SM_T(0);
+        if (c[C_ACTIVE] == 0.0) break;
+#ifdef LRS_PHASE_TIMING
+        sm_t[15]++;
+#endif
+        const double cg = c[C_CG], cs0 = c[C_CS0], cy0 = c[C_CY0], cs1 = c[C_CS1], cy1 = c[C_CY1];
+        const bool u0 = (cs0 != 0.0 || cy0 != 0.0), u1 = (cs1 != 0.0 || cy1 != 0.0);
+        const double *__restrict__ Gc = c[C_GCUR] == 0.0 ? A.G0 : A.G1;
+        // ---- D = -(cg G + cs0 s0 + cy0 y0 + cs1 s1 + cy1 y1)  (DirRow's arithmetic), 16-B loads
+        for (int e = tid; e < N * H; e += T) {
+            const int i = e / H, q = e - i * H;
+            const long o = (long)i * LD + 2 * q;
+            const double2 g = *reinterpret_cast<const double2 *>(Gc + o);
+            double dx = cg * g.x, dy = cg * g.y;
+            if (u0) {
+                const double2 a = *reinterpret_cast<const double2 *>(A.s0 + o), bb = *reinterpret_cast<const double2 *>(A.y0 + o);
+                dx += cs0 * a.x + cy0 * bb.x;
+                dy += cs0 * a.y + cy0 * bb.y;
+            }
+            if (u1) {
+                const double2 a = *reinterpret_cast<const double2 *>(A.s1 + o), bb = *reinterpret_cast<const double2 *>(A.y1 + o);
+                dx += cs1 * a.x + cy1 * bb.x;
+                dy += cs1 * a.y + cy1 * bb.y;
+            }
+            reinterpret_cast<double2 *>(Ds + (long)i * LS)[q] = make_double2(-dx, -dy);
+        }
+        __syncthreads();
+        if (A.nconst) colsums(Ds, csD);
+        LRS_SM_T(1);
+        // ---- A: the pattern's lower slots (k_it_a's per-slot arithmetic), a thread per slot
+        // (by rows instead -- a group of lanes per row, each lower entry's R_j / D_j read once --
+        // measured slower: the per-entry cross-lane sums and a second per-slot pass for the
+        // constraints outweigh the halved LDS reads); uRD -> XA, uDD -> X1
+        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int s = tid; s < A.Ptot; s += T) {
+            const int2 ij = A.slot_g[s];
+            const double cw = A.Cw[s];
+            const double2 l1u = A.loc1[s];
+            const double2 *ri = Rs2 + (long)ij.x * LS2, *di = Ds2 + (long)ij.x * LS2;
+            const double2 *rj = Rs2 + (long)ij.y * LS2, *dj = Ds2 + (long)ij.y * LS2;
+            double d0 = 0.0, d1 = 0.0;
+            if (ij.x != ij.y) {
+#pragma unroll 4
+                for (int q = 0; q < H; ++q) {
+                    const double2 a = ri[q], bq = dj[q], cq = rj[q], dq = di[q];
+                    d0 += a.x * bq.x + cq.x * dq.x;
+                    d0 += a.y * bq.y + cq.y * dq.y;
+                    d1 += dq.x * bq.x;
+                    d1 += dq.y * bq.y;
+                }
+                d0 *= 0.5;
+            } else {
+#pragma unroll 4
+                for (int q = 0; q < H; ++q) {
+                    const double2 a = ri[q], dq = di[q];
+                    d0 += a.x * dq.x;
+                    d0 += a.y * dq.y;
+                    d1 += dq.x * dq.x;
+                    d1 += dq.y * dq.y;
+                }
+            }
+            XA[s] = d0;
+            X1[s] = d1;
+            acc[0] += cw * d0;
+            acc[1] += cw * d1;
+            const int c1 = (int)l1u.y;
+            const int e0 = c1 == -2 ? A.loc_ptr[s] : 0, e1 = c1 == -2 ? A.loc_ptr[s + 1] : (c1 >= 0 ? 1 : 0);
+            for (int e = e0; e < e1; ++e) {
+                const int ci = c1 >= 0 ? c1 : A.loc_con[e];
+                const double w = c1 >= 0 ? l1u.x : A.loc_w[e];
+                const double q1 = 2.0 * (w * d0), q2 = w * d1;
+                const double bi = A.b[ci], cv = A.cvs[ci], li = A.lam[ci];
+                const double q0 = (bi - cv) + rhoInv * li;
+                acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1; acc[6] += q0 * q1;
+                double2 *rc = reinterpret_cast<double2 *>(A.rec + 4L * ci);
+                rc[0] = make_double2(cv, q1);
+                rc[1] = make_double2(q2, (-li) + (-rho) * bi);
+            }
+        }
+        __syncthreads();   // uRD / uDD of every slot before the global constraints read them
+        LRS_SM_T(2);
+        // ---- G: the global (multi-slot) constraints, a wave each (k_it_g's arithmetic)
+        for (int g = wv; g < A.mg; g += T / 64) {
+            const int i = A.glob[g];
+            double v1 = 0.0, v2 = 0.0;
+            for (int k = 0; k < A.K; ++k) {
+                const long row = (long)k * A.m + i;
+                double a1 = 0.0, a2 = 0.0;
+                for (int e = A.con_ptr[row] + lane; e < A.con_ptr[row + 1]; e += 64) {
+                    const double w = A.con_w[e];
+                    const int sl = A.con_slot[e];
+                    a1 += w * XA[sl];
+                    a2 += w * X1[sl];
+                }
+                v1 += wave_sum(a1);
+                v2 += wave_sum(a2);
+            }
+            if (lane != 0) continue;
+            v1 *= 2.0;
+            const double bi = A.b[i], ci = A.cvs[i], li = A.lam[i];
+            const double q0 = (bi - ci) + rhoInv * li;
+            acc[2] += v2 * v2; acc[3] += v1 * v2; acc[4] += q0 * v2; acc[5] += v1 * v1; acc[6] += q0 * v1;
+            double2 *rc = reinterpret_cast<double2 *>(A.rec + 4L * i);
+            rc[0] = make_double2(ci, v1);
+            rc[1] = make_double2(v2, (-li) + (-rho) * bi);
+        }
+        {
+            double s7[8];
+            block_reduce<8, kSmallThreads>(acc, s7);
+            if (tid == 0) {
+                // constant objectives: <C, sym R D^T> = sa (1^T R).(1^T D), <C, D D^T> = sa |1^T D|^2
+                for (int q = 0; q < A.nconst; ++q) {
+                    double a = 0.0, bb = 0.0;
+                    for (int e = 0; e < LD; ++e) {
+                        const double y = A.cst_sa[q] * csD[q][e];
+                        a += csR[q][e] * y;
+                        bb += csD[q][e] * y;
+                    }
+                    s7[0] += a;
+                    s7[1] += bb;
+                }
+                for (int q = 0; q < 7; ++q) red[q] = s7[q];
+            }
+        }
+        __syncthreads();   // every rec written, the reduced sums in red
+        LRS_SM_T(3);
+        if (tid < 64) line_search_t<true>(A.par, red[0], red[1], red + 2, ls);   // wave 0
+        __syncthreads();
+        LRS_SM_T(4);
+        lsflag = ls[LS_FLAG];
+        lstau = ls[LS_TAU];
+        fold = 0;
+        if (lsflag != 0.0) continue;   // rootNum 0 / tiny tau: the next ctrl_step exits
+        const double tau = lstau, tau2 = tau * tau;
+        const int gcur = (int)c[C_GCUR], h = (int)c[C_HEAD];
+        // ---- R_new = R + tau D (in place), S = C + A^*(M1) per slot -> X1 (k_it_b's per-entry
+        // arithmetic, once per slot instead of per adjacency entry), the column sums carried
+        for (int e = tid; e < N * H; e += T) {
+            const int i = e / H, q = e - i * H;
+            double2 *rp = reinterpret_cast<double2 *>(Rs + (long)i * LS) + q;
+            const double2 dv = reinterpret_cast<const double2 *>(Ds + (long)i * LS)[q];
+            double2 rv = *rp;
+            rv.x += tau * dv.x;
+            rv.y += tau * dv.y;
+            *rp = rv;
+        }
+        for (int s0 = tid; s0 < A.Ptot; s0 += 2 * T) {
+            double craw[2];
+            double2 s1u[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int s = s0 + u * T < A.Ptot ? s0 + u * T : s0;
+                craw[u] = A.Craw[s];
+                s1u[u] = A.slot1[s];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int s = s0 + u * T;
+                if (s >= A.Ptot) break;
+                double sv = craw[u];
+                const int c1 = (int)s1u[u].y;
+                const int e0 = c1 == -2 ? A.slot_ptr[s] : 0, e1 = c1 == -2 ? A.slot_ptr[s + 1] : (c1 >= 0 ? 1 : 0);
+                for (int e = e0; e < e1; ++e) {
+                    const int con = c1 >= 0 ? c1 : A.slot_con[e];
+                    const double2 *rc = reinterpret_cast<const double2 *>(A.rec + 4L * con);
+                    const double2 ra = rc[0], rb = rc[1];
+                    double cv = ra.x + tau * ra.y;
+                    cv = cv + tau2 * rb.x;
+                    const double M1 = rb.y + rho * cv;
+                    sv += M1 * (c1 >= 0 ? s1u[u].x : A.slot_a[e]);
+                }
+                X1[s] = sv;
+            }
+        }
+        if (tid < LD)
+            for (int q = 0; q < A.nconst; ++q) csR[q][tid] += tau * csD[q][tid];
+        __syncthreads();
+        LRS_SM_T(5);
+        // ---- B: per row, S R_new over the adjacency and A(R_new R_new^T) on the lower slots
+        // (k_it_b's arithmetic); uRR -> XB
+        double *__restrict__ Gold = gcur == 0 ? A.G0 : A.G1, *__restrict__ Gnew = gcur == 0 ? A.G1 : A.G0;
+        double *__restrict__ sh = h == 0 ? A.s0 : A.s1, *__restrict__ yh = h == 0 ? A.y0 : A.y1;
+        const double *__restrict__ so = h == 0 ? A.s1 : A.s0, *__restrict__ yo = h == 0 ? A.y1 : A.y0;
+        double bacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i0 = 0; i0 < N; i0 += RPP) {
+            const int r = i0 + tid / TPR;
+            const bool valid = r < N;
+            const int ii = valid ? r : N - 1;
+            double2 g[H2], rii[H2];
+            const long ob = ((long)ii * LD) / 2 + sl_lane;     // double2 index of this lane's first pair
+#pragma unroll
+            for (int p = 0; p < H2; ++p) {
+                g[p] = make_double2(0.0, 0.0);
+                rii[p] = Rs2[(long)ii * LS2 + sl_lane + TPR * p];
+            }
+            LRS_SM_MARK(t_adj);
+            const int kb = aptr(ii), kl = alow(ii), ke = valid ? aptr(ii + 1) : kb;
+            int2 jn[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) jn[u] = adj(kb + u < ke ? kb + u : kb);
+            for (int k = kb; k < ke; k += 4) {   // four entries per pass, the next four's indices in flight
+                int2 js[4];
+                double sv[4], d[4];
+                double2 x[4][H2];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    js[u] = jn[u];
+                    const int kn = k + 4 + u;
+                    jn[u] = adj(kn < ke ? kn : kb);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double t = X1[js[u].y];
+                    sv[u] = k + u < ke ? t : 0.0;
+#pragma unroll
+                    for (int p = 0; p < H2; ++p) x[u][p] = Rs2[(long)js[u].x * LS2 + sl_lane + TPR * p];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    d[u] = 0.0;
+#pragma unroll
+                    for (int p = 0; p < H2; ++p) {
+                        g[p].x += sv[u] * x[u][p].x;
+                        g[p].y += sv[u] * x[u][p].y;
+                        d[u] += rii[p].x * x[u][p].x;
+                        d[u] += rii[p].y * x[u][p].y;
+                    }
+                    d[u] = group_sum<TPR>(d[u]);
+                }
+                // lower entries: A(R R^T) on this row's slots (their constraints after the barrier)
+                if (sl_lane == 0)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (k + u < kl) XB[js[u].y] = d[u];
+            }
+            LRS_SM_SUB(8, t_adj);
+            if (!valid) continue;
+            LRS_SM_MARK(t_epi);
+            // row epilogue (k_it_b): [C R_new], G_new = 2 (...), s = tau D, y = G_new - G_old
+            int cq = -1;
+            for (int q = 0; q < A.nconst; ++q)
+                if (ii >= A.cst_row0[q] && ii < A.cst_row0[q] + A.cst_n[q]) cq = q;
+            double2 go[H2], sov[H2], yov[H2];
+#pragma unroll
+            for (int p = 0; p < H2; ++p) {
+                go[p] = reinterpret_cast<const double2 *>(Gold)[ob + TPR * p];
+                sov[p] = reinterpret_cast<const double2 *>(so)[ob + TPR * p];
+                yov[p] = reinterpret_cast<const double2 *>(yo)[ob + TPR * p];
+            }
+#pragma unroll
+            for (int p = 0; p < H2; ++p) {
+                const int col = 2 * (sl_lane + TPR * p);
+                double2 gv = g[p];
+                if (cq >= 0) {
+                    gv.x += A.cst_sa[cq] * csR[cq][col];
+                    gv.y += A.cst_sa[cq] * csR[cq][col + 1];
+                }
+                gv.x *= 2.0;
+                gv.y *= 2.0;
+                const double2 dv = Ds2[(long)ii * LS2 + sl_lane + TPR * p];
+                const double2 sv = make_double2(tau * dv.x, tau * dv.y);
+                const double2 yv = make_double2(gv.x - go[p].x, gv.y - go[p].y);
+                const long o = ob + TPR * p;
+                reinterpret_cast<double2 *>(Gnew)[o] = gv;
+                reinterpret_cast<double2 *>(sh)[o] = sv;
+                reinterpret_cast<double2 *>(yh)[o] = yv;
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2) {
+                    const double G_ = h2 ? gv.y : gv.x, S_ = h2 ? sv.y : sv.x, Y_ = h2 ? yv.y : yv.x;
+                    const double SO = h2 ? sov[p].y : sov[p].x, YO = h2 ? yov[p].y : yov[p].x;
+                    bacc[0] += G_ * G_; bacc[1] += Y_ * S_; bacc[2] += Y_ * Y_; bacc[3] += S_ * G_; bacc[4] += Y_ * G_;
+                    bacc[5] += SO * G_; bacc[6] += YO * G_; bacc[7] += SO * Y_; bacc[8] += YO * Y_;
+                }
+            }
+            LRS_SM_SUB(9, t_epi);
+        }
+        __syncthreads();   // uRR of every slot before the constraints read them
+        LRS_SM_T(6);
+        // single-slot constraints: A(R_new R_new^T) and their residual, a thread per slot
+        for (int s = tid; s < A.Ptot; s += T) {
+            const double d = XB[s];
+            const double2 l1u = A.loc1[s];
+            const int c1 = (int)l1u.y;
+            if (AL) A.uRR[s] = d;
+            if (c1 >= 0) {
+                const double tot = l1u.x * d, dd = A.b[c1] - tot;
+                A.cvs[c1] = tot;
+                bacc[9] += dd * dd;
+                continue;
+            }
+            if (c1 == -2)
+                for (int e = A.loc_ptr[s]; e < A.loc_ptr[s + 1]; ++e) {
+                    const int ci = A.loc_con[e];
+                    const double tot = A.loc_w[e] * d, dd = A.b[ci] - tot;
+                    A.cvs[ci] = tot;
+                    bacc[9] += dd * dd;
+                }
+        }
+        // global constraints: A(R_new R_new^T) from the slots and their residual
+        for (int g = wv; g < A.mg; g += T / 64) {
+            const int i = A.glob[g];
+            double tot = 0.0;
+            for (int k = 0; k < A.K; ++k) {
+                const long row = (long)k * A.m + i;
+                double v = 0.0;
+                for (int e = A.con_ptr[row] + lane; e < A.con_ptr[row + 1]; e += 64) v += A.con_w[e] * XB[A.con_slot[e]];
+                tot += wave_sum(v);
+            }
+            if (lane == 0) {
+                A.cvs[i] = tot;
+                const double dd = A.b[i] - tot;
+                bacc[9] += dd * dd;
+            }
+        }
+        {
+            double s10[10];
+            block_reduce<10, kSmallThreads>(bacc, s10);
+            if (tid == 0)
+                for (int q = 0; q < 10; ++q) red[q] = s10[q];
+        }
+        __syncthreads();
+        LRS_SM_T(7);
+        fold = 1;
+    }
+    // R back to global memory (the iterate stays in W.R: RCUR 0), the control block out
+    for (int e = tid; e < N * H; e += T) {
+        const int i = e / H, q = e - i * H;
+        reinterpret_cast<double2 *>(A.R + (long)i * LD)[q] = reinterpret_cast<const double2 *>(Rs + (long)i * LS)[q];
+    }
+    if (tid == 0) c[C_RCUR] = 0.0;
+    __syncthreads();
+    if (tid < C_NCTRL) A.ctrl_out[tid] = c[tid];
+    if (tid < LS_N) A.ls_out[tid] = ls[tid];
+#ifdef LRS_PHASE_TIMING
+    if (tid == 0)
+        for (int q = 0; q < 16; ++q) g_phase[3][q] += sm_t[q];
+#endif
+}
+
+static size_t small_lds_bytes(int N, int ld, int Ptot, long nadj, bool al) {
+    if (!al) return (2UL * N * (ld + 2) + (size_t)Ptot) * sizeof(double);
+    return (2UL * N * (ld + 2) + 2UL * Ptot + (size_t)nadj) * sizeof(double) + (2UL * N + 2) * sizeof(int);
+}
+constexpr size_t kSmallMaxDynLds = 136 * 1024;   // beside ~15 KB of the kernel's static LDS
+static bool small_ld_ok(int ld) { return ld == 8 || ld == 16 || ld == 24 || ld == 32 || ld == 48 || ld == 64; }
+
+// Whether the whole inner loop fits the single-workgroup kernel; fills the launch arguments.
+static bool small_alm_args(const DevProblem &P, DevWork &W, SmallArgs &A, int *ldo) {
+    if (P.shard || !P.slot_g || P.K > kMaxCones) return false;
+    const int ld = P.cones[0].ld;
+    int N = 0, nconst = 0;
+    for (int k = 0; k < P.K; ++k) {
+        const DevCone &c = P.cones[k];
+        if (c.ld != ld || c.dense_c == 1) return false;
+        if (c.dense_c == 2) {
+            if (nconst >= kSmallMaxConst) return false;
+            A.cst_row0[nconst] = N;
+            A.cst_n[nconst] = c.n;
+            A.cst_sa[nconst] = P.dense_scale * c.c_alpha;
+            nconst++;
+        }
+        N += c.n;
+    }
+    if (P.K > 1 && !P.has_merged) return false;
+    const DevCone &a = P.K > 1 ? P.merged : P.cones[0];
+    if (!small_ld_ok(ld) || N <= 0 || small_lds_bytes(N, ld, P.Ptot, a.adj_nnz, false) > kSmallMaxDynLds) return false;
+    A.al = small_lds_bytes(N, ld, P.Ptot, a.adj_nnz, true) <= kSmallMaxDynLds;
+    A.N = N; A.K = P.K; A.m = P.m; A.Ptot = P.Ptot; A.mg = P.mg; A.nadj = (int)a.adj_nnz;
+    A.slot_g = reinterpret_cast<const int2 *>(P.slot_g);
+    A.adj_ptr = a.adj_ptr; A.adj_low = a.adj_low; A.adj_col = a.adj_col; A.adj_slot = a.adj_slot;
+    A.Cw = P.Cw; A.Craw = P.Craw;
+    A.loc1 = reinterpret_cast<const double2 *>(P.loc1); A.slot1 = reinterpret_cast<const double2 *>(P.slot1);
+    A.loc_ptr = P.loc_ptr; A.loc_con = P.loc_con; A.slot_ptr = P.slot_ptr; A.slot_con = P.slot_con;
+    A.loc_w = P.loc_w; A.slot_a = P.slot_a;
+    A.glob = P.glob; A.con_ptr = P.con_ptr; A.con_slot = P.con_slot; A.con_w = P.con_w;
+    A.b = P.b; A.lam = W.lam;
+    A.cvs = W.cvs; A.rec = W.rec; A.uRD = W.uvt0; A.uDD = W.uvt1; A.uRR = W.uvt2;
+    A.R = W.R; A.G0 = W.G[0]; A.G1 = W.G[1]; A.s0 = W.ls[0]; A.y0 = W.ly[0]; A.s1 = W.ls[1]; A.y1 = W.ly[1];
+    A.par = W.par;
+    A.nconst = nconst;
+    if (ldo) *ldo = ld;
+    return true;
+}
+bool small_alm_fits(const DevProblem &P, DevWork &W) {
+    SmallArgs A{};
+    return small_alm_args(P, W, A, nullptr);
+}
+template <int LD, bool AL>
+static int launch_small_ld(const SmallArgs &A, size_t lds, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_small_alm<LD, AL>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmallMaxDynLds) != hipSuccess) {
+            snprintf(g_err, sizeof(g_err), "single-workgroup inner loop: LDS attribute refused");
+            return -1;
+        }
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_small_alm<LD, AL>), dim3(1), dim3(kSmallThreads), lds, st, A);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+// One launch: the inner loop from the control block at ctrl_in to its exit; the final control
+// block to ctrl_out, the last line search to ls_out, the iterate to W.R.
+int launch_small_alm(const DevProblem &P, DevWork &W, const double *ctrl_in, double *ctrl_out, double *ls_out,
+                     hipStream_t st) {
+    SmallArgs A{};
+    int ld = 0;
+    if (!small_alm_args(P, W, A, &ld)) {
+        snprintf(g_err, sizeof(g_err), "single-workgroup inner loop: the problem does not fit");
+        return -1;
+    }
+    A.ctrl_in = ctrl_in;
+    A.ctrl_out = ctrl_out;
+    A.ls_out = ls_out;
+    const size_t lds = small_lds_bytes(A.N, ld, A.Ptot, A.nadj, A.al != 0);
+#define LRS_SMALL_LD(AL)                                      \
+    switch (ld) {                                             \
+    case 8: return launch_small_ld<8, AL>(A, lds, st);        \
+    case 16: return launch_small_ld<16, AL>(A, lds, st);      \
+    case 24: return launch_small_ld<24, AL>(A, lds, st);      \
+    case 32: return launch_small_ld<32, AL>(A, lds, st);      \
+    case 48: return launch_small_ld<48, AL>(A, lds, st);      \
+    default: return launch_small_ld<64, AL>(A, lds, st);      \
+    }
+    if (A.al) { LRS_SMALL_LD(true) }
+    LRS_SMALL_LD(false)
+#undef LRS_SMALL_LD
 }
 
 // Sharded solve: pack the listed rows (ld doubles each) into a contiguous buffer.

@@ -609,6 +609,19 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         }
     }
     if (!dput(&dp.slot_rc, slot_rc, err)) return false;
+    {   // the same in the all-cones row space (the single-workgroup inner loop)
+        std::vector<int> sg(2L * std::max(1, Ptot), 0);
+        long r0 = 0;
+        for (int k = 0; k < hp.K; ++k) {
+            const HostCone &c = hp.cones[k];
+            for (int t = 0; t < (int)c.prow.size(); ++t) {
+                sg[2L * (dp.cones[k].slot_off + t)] = (int)(r0 + c.prow[t]);
+                sg[2L * (dp.cones[k].slot_off + t) + 1] = (int)(r0 + c.pcol[t]);
+            }
+            r0 += c.n;
+        }
+        if (!dput(&dp.slot_g, sg, err)) return false;
+    }
     // per (cone, constraint) row with exactly one entry: its (p, q) and weight, so the
     // constraint-entry kernels read them in one coalesced load; p = -1 otherwise
     {
@@ -943,7 +956,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
 void free_problem(DevProblem &dp) {
     auto f = [](void *p) { if (p) (void)hipFree(p); };
     f(dp.b); f(dp.Cw); f(dp.Craw); f(dp.con_ptr); f(dp.con_slot); f(dp.con_w);
-    f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a);
+    f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a); f(dp.slot_g);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);

@@ -1377,6 +1377,20 @@ struct InnerIo {
     bool resume = false;   // continue from the control block the last call stopped on (budget exit)
 };
 
+// The single-workgroup inner loop (lrs_kernels.hip k_small_alm): kernel path 4 or LRS_SMALL=1,
+// where the problem fits it (not sharded, two L-BFGS pairs, one factor layout, no full dense C,
+// R and D of every cone in one CU's LDS).
+static bool use_small(lrs_ctx *c) {
+    static int env = -1;
+    if (env < 0) {
+        const char *e = getenv("LRS_SMALL");
+        env = e ? atoi(e) : 0;
+    }
+    if (sharded(c) || c->lbfgsL != 2) return false;
+    if (!(c->dp.no_lat == 4 || (env == 1 && c->dp.no_lat == 0))) return false;
+    return small_alm_fits(c->dp, c->W);
+}
+
 static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, double gap, long budget, InnerIo &io,
                      bool ph1_exit = true) {
     double par[P_NPAR] = {0};
@@ -1412,7 +1426,19 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     double *res = c->hpin + 128;
     const double t_in = c->stats ? now_s() : 0.0;
     long enq = 0;
-    if (!c->prof) {
+    // the single-workgroup inner loop (small problems): the whole call is one launch
+    const bool small = !c->prof && use_small(c);
+    if (small) {
+        OPC(launch_small_alm(c->dp, c->W, c->W.ctrl + C_NCTRL, c->W.ctrl + C_NCTRL, c->W.lsres, c->st));
+        HIPC(hipMemcpyAsync(c->hpin + 128, c->W.ctrl + C_NCTRL, sizeof(double) * C_NCTRL, hipMemcpyDeviceToHost,
+                            c->st));
+        HIPC(hipStreamSynchronize(c->st));
+        res = c->hpin + 128;
+        enq = std::max(0L, (long)res[C_INNER] - io.inner);
+        c->dp.last_path = 4;
+        if (c->stats) c->st_batches++;
+    }
+    if (!c->prof && !small) {
         // Two batches in flight: batch k+1 is enqueued before the host waits for batch k, so
         // the GPU never idles on the host's submission or on the wait's wake-up.  Each batch
         // ends with a copy of the control block into its own pinned slot.  At the loop's exit
@@ -2343,8 +2369,9 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
 int lrs_set_kernel_path(lrs_ctx *c, int path) {
     if (c) bind(c);
     if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
-    if (path < 0 || path > 3) {
-        set_err("kernel path %d: expected 0 (auto), 1 (general), 2 (general, bandwidth regime) or 3 (+ long-row kernels)", path);
+    if (path < 0 || path > 4) {
+        set_err("kernel path %d: expected 0 (auto), 1 (general), 2 (general, bandwidth regime), 3 (+ long-row kernels) "
+                "or 4 (the single-workgroup inner loop where it fits)", path);
         return -1;
     }
     if (c->dp.no_lat != path) {

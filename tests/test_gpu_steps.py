@@ -182,3 +182,66 @@ def test_lbfgs_ring_of_one(solver_mod):
     tol = 10 * (r1["alm_gap"] + r2["alm_gap"]) + 1e-6
     assert abs(r1["alm_pobj"] - r2["alm_pobj"]) <= tol * abs(r2["alm_pobj"]), (r1["alm_pobj"], r2["alm_pobj"], tol)
     assert r1["alm_pinf"] <= 1e-3 and r1["alm_inner"] > 0
+
+
+SMALL_CASES = [(n, c) for n in ["mc_rand200", "mc_torus12x10", "mc_rand300w", "theta40", "theta25x3", "rsparse60"]
+               for c in (["0", "1"] if n.startswith("theta") else ["0"])]
+
+
+@pytest.mark.parametrize("name,const", SMALL_CASES)
+def test_single_workgroup_inner_loop_matches_reference(solver_mod, name, const, monkeypatch):
+    """Kernel path 4: the whole inner loop of each run_inner call in one launch of one workgroup
+    (lrs_kernels.hip k_small_alm; R and D in LDS, barriers between the trips' phases), theta's
+    C = -J as a slot pattern (LRS_CONST_C=0) and as the constant objective's column sums (=1):
+    the reference's own trips, 1e-9 as the multi-launch kernels."""
+    monkeypatch.setenv("LRS_CONST_C", const)
+    z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
+    rank = int(z["rank_flag"])
+    kw = {"reoptLevel": 0}
+    if rank > 0:
+        kw["fixedRank"] = rank
+    sv = solver_mod.Solver(_path(name))
+    sv.set_kernel_path(4)
+    worst = {}
+    for K in [int(k) for k in z["ks"]]:
+        trips = z[f"K{K}_trips"]
+        if trips.shape[0] < K:
+            continue
+        d = sv.alm_steps(K, **kw)
+        assert sv.kernel_path() == 4
+        assert d["inner"] == K, (K, d["inner"])
+        tau, rn, lag, pinf = trips[K - 1]
+        assert abs(d["tau"] - tau) <= TOL * abs(tau), (K, d["tau"], tau)
+        assert abs(d["lag"] - lag) <= TOL * abs(lag), (K, d["lag"], lag)
+        assert abs(d["pinf"] - pinf) <= TOL * max(abs(pinf), 1e-300), (K, d["pinf"], pinf)
+        assert abs(d["beta"] - z[f"K{K}_beta"][0]) <= TOL * abs(z[f"K{K}_beta"][0])
+        for key in ("R", "G", "cvs", "s", "y"):
+            e = rel_err(d[key], z[f"K{K}_{key}"])
+            worst[key] = max(worst.get(key, 0.0), e)
+            assert e < TOL, (K, key, e)
+        assert rel_err(d["lam"], z[f"K{K}_lam"]) < TOL or np.linalg.norm(z[f"K{K}_lam"]) == 0
+    print(f"{name} const {const}: worst rel errors {worst}")
+    sv.close()
+
+
+@pytest.mark.parametrize("name", ["theta40", "theta25x3", "mc_torus12x10"])
+def test_single_workgroup_solve_matches_default(solver_mod, name, monkeypatch):
+    """Whole solves on kernel path 4 against the default kernels (same bar as the golden solves:
+    MaxCut objectives 1e-6, theta within the certified gaps)."""
+    out = []
+    for path, const in ((0, "0"), (4, "1")):
+        monkeypatch.setenv("LRS_CONST_C", const)
+        sv = solver_mod.Solver(_path(name))
+        sv.set_kernel_path(path)
+        out.append(sv.solve(reoptLevel=0))
+        sv.close()
+    a, b = out
+    if name.startswith("mc_"):
+        assert abs(a["alm_inner"] - b["alm_inner"]) <= 2
+        for k in ("alm_pobj", "pobj"):
+            assert abs(a[k] - b[k]) <= 1e-6 * abs(a[k]), (k, a[k], b[k])
+    else:
+        tol = 10 * (a["gap"] + b["gap"]) + 1e-6
+        for k in ("pobj", "dobj"):
+            assert abs(a[k] - b[k]) <= tol * (1 + abs(a[k])), (k, a[k], b[k], tol)
+        assert b["pinf"] <= 1e-4
