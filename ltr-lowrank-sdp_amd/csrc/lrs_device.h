@@ -92,6 +92,8 @@ struct DevCone {
     int slot_off = 0, P = 0;
     int *adj_ptr = nullptr, *adj_low = nullptr, *adj_col = nullptr, *adj_slot = nullptr;
     long adj_nnz = 0;
+    // constraint i of this cone is the single entry (i, i), every i (m = n): k_auv_diag
+    bool auv_diag = false;
     // most adjacency entries of one row (all, and lower incl. the diagonal); 0 = unknown
     int maxdeg = 0, maxlow = 0;
     // dense rows (far more entries than the rest, e.g. a hub vertex): the latency kernels

@@ -481,6 +481,53 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
     if (part) partials_finalize<1>(acc, part, ticket, fin);
 }
 
+// A(X Y^T) of a cone whose constraint i is the single entry (i, i) (DevCone::auv_diag,
+// MaxCut's diag(X) = 1): out[i] = w_i d(i, i), the row-wise dot product of X and Y -- no
+// (p, q) index load in front of the factor rows, and kDiagU rows per lane group with their
+// loads issued together, so one memory trip covers them.  Same lane-group layout and
+// group_sum as k_auv_con: bit-identical values.
+constexpr int kDiagU = 4;
+template <int G, int E, int MODE>
+__global__ void __launch_bounds__(kBlock) k_auv_diag(int m, long wbase, int ld, const double *__restrict__ con1_w,
+                                                     const double *__restrict__ X, const double *__restrict__ Y,
+                                                     double scale, int accumulate, double *__restrict__ out,
+                                                     const double *__restrict__ b, double *part, unsigned *ticket,
+                                                     double *fin, const double *__restrict__ guard,
+                                                     double *__restrict__ sum_upd) {
+    if (guard && guard[0] == 0.0) return;
+    double acc[1] = {0.0};
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
+    const int ngrp = gridDim.x * kBlock / G;
+    for (int i0 = grp; i0 < m; i0 += kDiagU * ngrp) {
+        double xv[kDiagU][E], yv[kDiagU][E], w[kDiagU];
+#pragma unroll
+        for (int u = 0; u < kDiagU; ++u) {
+            const int i = min(i0 + u * ngrp, m - 1);
+            const long o = (long)i * ld + lane * E;
+            ld_row<E>(X + o, xv[u]);
+            if (MODE == 0) ld_row<E>(Y + o, yv[u]);
+            w[u] = con1_w[wbase + i];
+        }
+#pragma unroll
+        for (int u = 0; u < kDiagU; ++u) {
+            const int i = i0 + u * ngrp;
+            double d = 0.0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) d += MODE == 1 ? xv[u][e] * xv[u][e] : xv[u][e] * yv[u][e];
+            d = group_sum<G>(d);
+            if (lane == 0 && i < m) {
+                double tot = (w[u] * d) * scale;
+                if (accumulate) tot = out[i] + tot;
+                if (sum_upd) sum_upd[i] = (sum_upd[i] - out[i]) + tot;
+                out[i] = tot;
+                if (b) { const double dd = b[i] - tot; acc[0] += dd * dd; }
+            }
+        }
+    }
+    if (part) partials_finalize<1>(acc, part, ticket, fin);
+}
+
 // A(X Y^T) over 2-D tiles (cones with many constraint entries per row, e.g. C5's 600):
 // the per-entry gather above reads two (MODE 1) or four (MODE 0) 8r-byte factor rows per
 // entry from L2 / Infinity Cache, ~12 GB per C5 launch for 118 MB of operands.  Here a
@@ -4101,6 +4148,21 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
         LRS_CHECK_LAUNCH();
         return 0;
     }
+    if (c.auv_diag && !P.shard && !getenv("LRS_NO_AUV_DIAG")) {
+        const int grid = std::min(grid_rows((P.m + kDiagU - 1) / kDiagU, c.G), kMaxPartialBlocks);
+        LRS_LAYOUT_SWITCH(c.G, c.E, {
+            if (mode == 1)
+                hipLaunchKernelGGL((k_auv_diag<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, P.m, (long)cone * P.m,
+                                   c.ld, P.con1_w, Xc, Xc, scale, accumulate, out, b_for_vio, vio_part, tk, fin, guard,
+                                   sum_upd);
+            else
+                hipLaunchKernelGGL((k_auv_diag<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, P.m, (long)cone * P.m,
+                                   c.ld, P.con1_w, Xc, Yc, scale, accumulate, out, b_for_vio, vio_part, tk, fin, guard,
+                                   sum_upd);
+        });
+        LRS_CHECK_LAUNCH();
+        return 0;
+    }
     const int l0 = P.long_ptr_h.empty() ? 0 : P.long_ptr_h[cone];
     const int nlong = P.long_ptr_h.empty() ? 0 : P.long_ptr_h[cone + 1] - l0;
     if (nlong > 0 && b_for_vio) {
@@ -5076,8 +5138,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
 // ------------------------------------------------------------------------
 constexpr int kSmallThreads = 512;
 constexpr int kSmallMaxConst = 4;     // constant-objective cones the kernel carries
-constexpr int kSmallMaxLd = 64;       // widest factor row (tpr <= 16 threads per row, <= 4 columns each)
-constexpr int kSmallCols = 4;         // factor columns per thread in the row phase
+constexpr int kSmallMaxLd = 64;       // widest factor row
 struct SmallArgs {
     int N, K, m, Ptot, mg, nadj, al;
     const int2 *slot_g;                      // [Ptot] merged-space (row, col) of each slot (row >= col)

@@ -131,6 +131,64 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
         if (a.row != b.row) return a.row < b.row;
         return a.col < b.col;
     });
+    // auto constant objective (lrs_problem.h policy): every cone's C constant or absent, and
+    // the lean single-workgroup layout (R, D at the widest reachable layout + the pattern)
+    // within kSmallLdsBudget
+    bool auto_const = false;
+    {
+        const char *ek = getenv("LRS_CONST_C");
+        const char *ev = getenv("LRS_DENSE_C");
+        if (!ek && !(ev && ev[0] == '0')) {
+            bool ok = true, any = false;
+            long N = 0, Ptot = 0;
+            int ldmax = 0;
+            size_t e0 = 0;
+            for (int k = 0; k < K && ok; ++k) {
+                size_t e1 = e0;
+                while (e1 < raw.size() && raw[e1].cone == k) e1++;
+                const int n = dims[k];
+                N += n;
+                if (N > 4096) { ok = false; break; }
+                std::vector<std::pair<int, int>> pr, cc;
+                std::vector<int> cons;
+                for (size_t e = e0; e < e1; ++e) {
+                    if (raw[e].con == 0) cc.push_back({raw[e].row, raw[e].col});
+                    else { pr.push_back({raw[e].row, raw[e].col}); cons.push_back(raw[e].con); }
+                }
+                std::sort(pr.begin(), pr.end());
+                Ptot += (long)(std::unique(pr.begin(), pr.end()) - pr.begin());
+                std::sort(cons.begin(), cons.end());
+                const long nnzRows = (long)(std::unique(cons.begin(), cons.end()) - cons.begin());
+                std::sort(cc.begin(), cc.end());
+                const long ncobj = (long)(std::unique(cc.begin(), cc.end()) - cc.begin());
+                if (ncobj > 0) {
+                    // every entry of the block equal (duplicates summed like the merge below)
+                    if (ncobj != (long)n * (n + 1) / 2 || n < kConstCMinN) { ok = false; break; }
+                    std::vector<std::pair<std::pair<int, int>, double>> vv;
+                    for (size_t e = e0; e < e1; ++e)
+                        if (raw[e].con == 0) vv.push_back({{raw[e].row, raw[e].col}, raw[e].v});
+                    std::sort(vv.begin(), vv.end());
+                    double v0 = 0.0;
+                    bool first = true;
+                    for (size_t a = 0; a < vv.size() && ok;) {
+                        double s = 0.0;
+                        size_t b2 = a;
+                        while (b2 < vv.size() && vv[b2].first == vv[a].first) s += vv[b2++].second;
+                        if (first) { v0 = s; first = false; }
+                        else if (s != v0) ok = false;
+                        a = b2;
+                    }
+                    if (!ok || v0 == 0.0) { ok = false; break; }
+                    any = true;
+                }
+                const int rmax = std::min((int)std::sqrt(2.0 * nnzRows) + 1, n);
+                ldmax = std::max(ldmax, choose_layout(std::max(1, rmax)).ld);
+                e0 = e1;
+            }
+            auto_const = ok && any && ldmax <= 64 &&
+                         (2L * N * (ldmax + 2) + Ptot) * (long)sizeof(double) <= kSmallLdsBudget;
+        }
+    }
     size_t q = 0;
     for (int k = 0; k < K; ++k) {
         HostCone &c = hp.cones[k];
@@ -157,7 +215,7 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
             else c.dense_c = c.n >= kDenseCMinN && 4 * ncobj >= tri;
             // constant C (all entries one value): the rank-one products, no n x n matrix
             const char *ek = getenv("LRS_CONST_C");
-            if (ek && ek[0] == '1' && !(ev && ev[0] == '0') && c.n >= kConstCMinN && ncobj == tri) {
+            if (((ek && ek[0] == '1') || auto_const) && !(ev && ev[0] == '0') && c.n >= kConstCMinN && ncobj == tri) {
                 double v0 = 0.0;
                 bool same = true, first = true;
                 for (auto &e : me) {
@@ -651,6 +709,16 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             c1w[r] = con_w[e];
         }
         if (!dput(&dp.con1_pq, c1pq, err) || !dput(&dp.con1_w, c1w, err)) return false;
+        // cones whose constraint i is the single entry (i, i) for every i (m = n: MaxCut's
+        // diag(X) = 1): A(X Y^T) is a row-wise dot product (k_auv_diag, no index loads)
+        for (int k = 0; k < hp.K; ++k) {
+            bool id = m == hp.cones[k].n && m > 0;
+            for (int i = 0; id && i < m; ++i) {
+                const long r = (long)k * m + i;
+                id = c1pq[2 * r] == i && c1pq[2 * r + 1] == i;
+            }
+            dp.cones[k].auv_diag = id;
+        }
         // 2-D tiles for the constraint-entry A(X Y^T) (lrs_device.h kAuvT): cones with many
         // entries per row and no long constraint rows
         const char *ev = getenv("LRS_AUV_TILES");

@@ -39,11 +39,16 @@ struct HostCone {
 // cones with n >= kDenseCMinN whose C fills >= 1/4 of the lower triangle (measured: the dense
 // path is 0.86x the slot path at n = 500, 2.2x at n = 2000, scripts/c5b_probe.py).
 constexpr int kDenseCMinN = 1024;
-// Constant-objective policy: with LRS_CONST_C=1 every block whose C has all n (n + 1) / 2
-// entries equal takes the rank-one products (any n >= 2).  Off by default: on the multi-launch
-// iteration theta3 runs 64 us per iteration that way against 44 us on the slot path (its rows
-// lose the ~150 C entries that spread them over lane-group teams; profiles/r03e_theta_const.md).
+// Constant-objective policy: a block whose C has all n (n + 1) / 2 entries equal can take the
+// rank-one products (any n >= 2).  LRS_CONST_C=1 every such block, =0 none; unset: only when
+// the whole problem fits the single-workgroup inner loop at every rank the solve can reach
+// (every cone's C constant or absent; R and D of all cones at the widest layout of
+// sqrt(2 nnzRows) + 1 columns plus the constraint pattern within kSmallLdsBudget of LDS) --
+// that loop needs the constant form (the slot form's n (n + 1) / 2 objective slots do not fit
+// one CU), while the multi-launch iteration runs faster on the slot form (theta3: 44 us vs
+// 64 us per iteration, profiles/r03e_theta_const.md).
 constexpr int kConstCMinN = 2;
+constexpr long kSmallLdsBudget = 136 * 1024;   // = lrs_kernels.hip kSmallMaxDynLds
 
 struct HostProblem {
     int m = 0, K = 0, nLp = 0;

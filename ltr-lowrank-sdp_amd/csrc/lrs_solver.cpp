@@ -1377,17 +1377,21 @@ struct InnerIo {
     bool resume = false;   // continue from the control block the last call stopped on (budget exit)
 };
 
-// The single-workgroup inner loop (lrs_kernels.hip k_small_alm): kernel path 4 or LRS_SMALL=1,
-// where the problem fits it (not sharded, two L-BFGS pairs, one factor layout, no full dense C,
-// R and D of every cone in one CU's LDS).
+// The single-workgroup inner loop (lrs_kernels.hip k_small_alm) where the problem fits it (not
+// sharded, two L-BFGS pairs, one factor layout, no full dense C, R and D of every cone in one
+// CU's LDS): kernel path 4 always; the automatic path 0 unless LRS_SMALL=0, with at most
+// kSmallMaxGlobal multi-slot constraints (LRS_SMALL=1 lifts that bound) -- each takes a wave
+// of the workgroup per phase, and on rsparse60 (every constraint multi-slot) the multi-launch
+// iteration is faster (scripts/small_compare.py).
+constexpr int kSmallMaxGlobal = 16;
 static bool use_small(lrs_ctx *c) {
-    static int env = -1;
-    if (env < 0) {
-        const char *e = getenv("LRS_SMALL");
-        env = e ? atoi(e) : 0;
-    }
+    const char *e = getenv("LRS_SMALL");
+    const int env = e ? atoi(e) : -1;
     if (sharded(c) || c->lbfgsL != 2) return false;
-    if (!(c->dp.no_lat == 4 || (env == 1 && c->dp.no_lat == 0))) return false;
+    if (c->dp.no_lat != 4) {
+        if (c->dp.no_lat != 0 || env == 0) return false;
+        if (env != 1 && c->dp.mg > kSmallMaxGlobal) return false;
+    }
     return small_alm_fits(c->dp, c->W);
 }
 

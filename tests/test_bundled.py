@@ -73,10 +73,11 @@ def solver_mod():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", HUBS)
-def test_dense_row_slices_match_general(solver_mod, name):
+def test_dense_row_slices_match_general(solver_mod, name, monkeypatch):
     """Latency kernels with slice blocks over the dense rows solve like the general row
     kernels (same per-entry arithmetic, other partial-sum partitions, so another trajectory):
     both stop primal-dual optimal (pinf, gap, dual infeasibility), objectives within OBJ_TOL."""
+    monkeypatch.setenv("LRS_SMALL", "0")
     out = []
     for path in (0, 1):
         sv = solver_mod.Solver(os.path.join(DATA, f"{name}.dat-s"))

@@ -287,10 +287,11 @@ def test_device_reopt_level1_matches_reference(solver_mod, case):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["mc_torus12x10", "mc_rand200", "mc_rand300w", "rsparse60", "theta40"])
-def test_latency_kernels_match_general(solver_mod, name):
+def test_latency_kernels_match_general(solver_mod, name, monkeypatch):
     """k_lat_a / k_lat_b (control wave + prefetching row waves) solve like the general row
     kernels k_it_a / k_it_b: same per-entry arithmetic, partial sums over other block
     partitions (MaxCut: inner iterations +-2, ALM objective 1e-8; all: final 1e-6)."""
+    monkeypatch.setenv("LRS_SMALL", "0")   # path 0 = the latency kernels (not the single-workgroup loop)
     out = []
     for path in (0, 1):
         sv = solver_mod.Solver(instance(name))
@@ -310,9 +311,10 @@ def test_latency_kernels_match_general(solver_mod, name):
 
 
 @pytest.mark.gpu
-def test_latency_kernels_throughput_budget(solver_mod):
+def test_latency_kernels_throughput_budget(solver_mod, monkeypatch):
     """The bench's fixed-budget ALM run (phase-1 exit off) does exactly `steps` iterations
     on the latency kernels, deterministically."""
+    monkeypatch.setenv("LRS_SMALL", "0")
     sv = solver_mod.Solver(instance("mc_torus12x10"))
     r = sv.determine_rank()[0]
     outs = []

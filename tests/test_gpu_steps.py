@@ -59,7 +59,8 @@ def _cases():
 
 
 @pytest.mark.parametrize("name,kpath", _cases())
-def test_fused_iterations_match_reference(solver_mod, name, kpath):
+def test_fused_iterations_match_reference(solver_mod, name, kpath, monkeypatch):
+    monkeypatch.setenv("LRS_SMALL", "0")   # path 0 = the latency kernels here (path 4: below)
     z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
     rank = int(z["rank_flag"])
     kw = {"reoptLevel": 0}
