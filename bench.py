@@ -41,6 +41,8 @@ sys.path.insert(0, ROOT)
 PKG = "ltr-lowrank-sdp_amd"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec)
+FP64_VALU_PEAK_TFS = 78.6   # FP64 vector FMA: 256 CUs x 64 FMA/clk x 2 flop x 2.4 GHz
+LDS_PEAK_GBS = 256 * 256 * 2.4   # 256 B/clk/CU for ds_read_b64/b128 (MI355X_MICROARCH.md §LDS), 2.4 GHz
 STAGES = ("A: {a} (control, L-BFGS direction, SDDMM sym(RD^T)/DD^T, local q1/q2)",
           "G: k_it_g (phase-1 test, multi-slot constraints' q1/q2)",
           "B: {b} (line search, R+tau D, adjoint S=C+A*(M1), G=2SR, A(RR^T), L-BFGS pair)")
@@ -130,9 +132,23 @@ def cpu_reference_solve(path, flags, timeout):
     return {"solve_time_sec": float(m.group(1)), "process_wall_sec": wall, "alm_pobj": float(p.group(1))}
 
 
-def stage_roofline(sv, reps, with_traffic=False):
+def tile_bounds(us, lds_bytes, flop):
+    """The LDS-read and FP64-FMA side of a tile kernel whose operands are LDS-resident (the
+    HBM fraction alone does not say how far off its real bound it is): algorithmic LDS bytes
+    and flops per launch against the chip's LDS read rate and FP64 vector peak."""
+    s = us * 1e-6
+    return {"lds_bytes": lds_bytes, "lds_GBs": lds_bytes / s / 1e9, "lds_peak_GBs": LDS_PEAK_GBS,
+            "lds_frac": lds_bytes / s / 1e9 / LDS_PEAK_GBS, "fp64_flop": flop,
+            "fp64_TFs": flop / s / 1e12, "fp64_frac": flop / s / 1e12 / FP64_VALU_PEAK_TFS}
+
+
+def stage_roofline(sv, reps, with_traffic=False, rank=None):
     """Per-launch ms of the split-iteration stages (back-to-back relaunches between two
-    HIP events on the solver stream) and their algorithmic bytes -> GB/s."""
+    HIP events on the solver stream) and their algorithmic bytes -> GB/s.  With `rank` and
+    the 2-D tile kernels active, also each tile stage's LDS-read and FP64 fractions
+    (tile_bounds): per lower slot stage A reads R_i, D_i, R_j, D_j (4 r doubles, 3 r FMA),
+    stage B A(R R^T) on it (2 r doubles, r FMA) and S R over both its adjacency entries
+    (r doubles, r FMA each); A(U U^T) per constraint entry 2 r doubles, r FMA."""
     ms = sv.time_stages(reps)
     by = sv.stage_bytes()
     ka, kb = STAGE_KERNELS.get(sv.kernel_path(), STAGE_KERNELS[1])
@@ -152,6 +168,14 @@ def stage_roofline(sv, reps, with_traffic=False):
         out.append({"stage": STAGES[k].format(a=ka, b=kb), "kernel": (ka, "k_it_g", kb)[k],
                     "avg_launch_us": ms[k] * 1e3, "bytes_per_launch": by[k], "achieved_GBs": gbs,
                     "frac": gbs / HBM_PEAK_GBS})
+    if rank and slot_tiles:
+        P, n = sv.nslots, n0
+        adj = 2 * P - n
+        for o in out:
+            if o["stage"].startswith("A"):
+                o["tile_bounds"] = tile_bounds(o["avg_launch_us"], P * 4 * rank * 8, P * 3 * rank * 2)
+            elif o["stage"].startswith("B"):
+                o["tile_bounds"] = tile_bounds(o["avg_launch_us"], (P * 2 + adj) * rank * 8, (P + adj) * rank * 2)
     dom = max(out, key=lambda s: s["avg_launch_us"])
     traffic, tsrc = pmc_traffic(dom["kernel"]) if with_traffic else (None, None)
     # the north-star's named operator: A(UU^T) straight from the constraint entries
@@ -162,6 +186,8 @@ def stage_roofline(sv, reps, with_traffic=False):
              else "k_auv_con<XX^T> (A(UU^T) over constraint entries)")
     auut = {"kernel": akern, "avg_launch_us": ams * 1e3,
             "bytes_per_launch": aby, "achieved_GBs": agbs, "frac": agbs / HBM_PEAK_GBS}
+    if rank and auv_tiles:
+        auut["tile_bounds"] = tile_bounds(ams * 1e3, sv.nnz * 2 * rank * 8, sv.nnz * rank * 2)
     res = {"bound": "hbm", "kernel": dom["stage"], "achieved": dom["achieved_GBs"], "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": dom["frac"], "traffic": traffic, "bytes_per_launch": dom["bytes_per_launch"],
            "avg_launch_us": dom["avg_launch_us"], "stages": out, "a_uut": auut}
@@ -181,7 +207,7 @@ def config_c5(solver, local, iters=20, cpu_seconds=0.0, cache=None):
     kw = dict(fixedRank=128, reoptLevel=0)
     # one solve: warmup trips, then `iters` timed trips of the same solve (no setup inside)
     o = sv.alm_timed(3, iters, **kw)
-    rl = stage_roofline(sv, 3)
+    rl = stage_roofline(sv, 3, rank=128)
     ms, kms = sv.time_gram(0, 20)
     ceil_tf = sv.mfma_f64_peak()
     n = sv.dims[0]

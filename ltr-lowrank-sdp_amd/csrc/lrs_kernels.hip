@@ -485,10 +485,13 @@ __global__ void __launch_bounds__(kBlock) k_auv_con(int m, int K, int cone, int 
 // MaxCut's diag(X) = 1): out[i] = w_i d(i, i), the row-wise dot product of X and Y -- no
 // (p, q) index load in front of the factor rows, and kDiagU rows per lane group with their
 // loads issued together, so one memory trip covers them.  Same lane-group layout and
-// group_sum as k_auv_con: bit-identical values.
-constexpr int kDiagU = 4;
-template <int G, int E, int MODE>
-__global__ void __launch_bounds__(kBlock) k_auv_diag(int m, long wbase, int ld, const double *__restrict__ con1_w,
+// group_sum as k_auv_con (values equal up to the FMA contraction of the lane sums).  G81-like
+// (n = m = 2e4, r = 64, 10.8 MB), back-to-back launches between HIP events: U = 2 rows per
+// group at 256 threads 2.85-3.04 us, U = 1 3.5-3.8, U = 4 3.3-3.4, U = 8 4.2-4.3; 512 / 1024
+// threads no better (scripts/auut_probe.py; LRS_DIAG_U / LRS_DIAG_BS select them).
+constexpr int kDiagU = 2;
+template <int G, int E, int MODE, int kDiagU, int BS>
+__global__ void __launch_bounds__(BS) k_auv_diag(int m, long wbase, int ld, const double *__restrict__ con1_w,
                                                      const double *__restrict__ X, const double *__restrict__ Y,
                                                      double scale, int accumulate, double *__restrict__ out,
                                                      const double *__restrict__ b, double *part, unsigned *ticket,
@@ -497,8 +500,8 @@ __global__ void __launch_bounds__(kBlock) k_auv_diag(int m, long wbase, int ld, 
     if (guard && guard[0] == 0.0) return;
     double acc[1] = {0.0};
     const int lane = threadIdx.x & (G - 1);
-    const int grp = (blockIdx.x * kBlock + threadIdx.x) / G;
-    const int ngrp = gridDim.x * kBlock / G;
+    const int grp = (blockIdx.x * BS + threadIdx.x) / G;
+    const int ngrp = gridDim.x * BS / G;
     for (int i0 = grp; i0 < m; i0 += kDiagU * ngrp) {
         double xv[kDiagU][E], yv[kDiagU][E], w[kDiagU];
 #pragma unroll
@@ -3585,17 +3588,18 @@ __global__ void __launch_bounds__(kBlock) k_trl_symv(int n, int r0, const int *_
         }
     }
 }
-// dense objective: y += scale C v over the cone's rows (one wave per row)
-__global__ void __launch_bounds__(kBlock) k_trl_dense(int n, double scale, const double *__restrict__ Cd,
+// dense objective: y += scale C v over the cone's row block (rows r0 .. r0 + nr - 1, C row t
+// holding row r0 + t's n columns; one wave per row)
+__global__ void __launch_bounds__(kBlock) k_trl_dense(int n, int nr, int r0, double scale, const double *__restrict__ Cd,
                                                       const double *__restrict__ v, double *__restrict__ y) {
     const int lane = threadIdx.x & 63;
     const int nw = gridDim.x * (kBlock / 64);
-    for (int i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < n; i += nw) {
+    for (int i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); i < nr; i += nw) {
         const double *__restrict__ ci = Cd + (long)i * n;
         double t = 0.0;
         for (int k = lane; k < n; k += 64) t += ci[k] * v[k];
         t = wave_sum(t);
-        if (lane == 0) y[i] += scale * t;
+        if (lane == 0) y[r0 + i] += scale * t;
     }
 }
 // constant objective: y += sa sum(v) (one block, fixed order)
@@ -3707,8 +3711,9 @@ int launch_trl_symv(const DevProblem &P, int cone, const double *S, const double
         if (c.dense_c == 2) {   // y += scale alpha 1 (1^T v)
             hipLaunchKernelGGL(k_trl_cj, dim3(1), dim3(kBlock), 0, st, c.n, P.dense_scale * c.c_alpha, vj ? vj : x, y);
         } else {
-            const int grid = std::max(1, std::min(2048, (c.n + kBlock / 64 - 1) / (kBlock / 64)));
-            hipLaunchKernelGGL(k_trl_dense, dim3(grid), dim3(kBlock), 0, st, c.n, P.dense_scale, c.Cd, vj ? vj : x, y);
+            const int grid = std::max(1, std::min(2048, (c.nown + kBlock / 64 - 1) / (kBlock / 64)));
+            hipLaunchKernelGGL(k_trl_dense, dim3(grid), dim3(kBlock), 0, st, c.n, c.nown, c.row0, P.dense_scale, c.Cd,
+                               vj ? vj : x, y);
         }
         LRS_CHECK_LAUNCH();
     }
@@ -4149,17 +4154,39 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
         return 0;
     }
     if (c.auv_diag && !P.shard && !getenv("LRS_NO_AUV_DIAG")) {
-        const int grid = std::min(grid_rows((P.m + kDiagU - 1) / kDiagU, c.G), kMaxPartialBlocks);
-        LRS_LAYOUT_SWITCH(c.G, c.E, {
-            if (mode == 1)
-                hipLaunchKernelGGL((k_auv_diag<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, P.m, (long)cone * P.m,
-                                   c.ld, P.con1_w, Xc, Xc, scale, accumulate, out, b_for_vio, vio_part, tk, fin, guard,
-                                   sum_upd);
-            else
-                hipLaunchKernelGGL((k_auv_diag<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, P.m, (long)cone * P.m,
-                                   c.ld, P.con1_w, Xc, Yc, scale, accumulate, out, b_for_vio, vio_part, tk, fin, guard,
-                                   sum_upd);
-        });
+        static int U = -1, BSv = 256;
+        if (U < 0) {
+            const char *e = getenv("LRS_DIAG_U"); U = e ? atoi(e) : kDiagU;
+            const char *f = getenv("LRS_DIAG_BS"); BSv = f ? atoi(f) : 256;
+        }
+        const int BSx = vio_part ? 256 : BSv;   // the residual's partials: kBlock-thread blocks
+        const long thr = (long)((P.m + U - 1) / U) * c.G;
+        const int grid = (int)std::max(1L, std::min((long)kMaxPartialBlocks, (thr + BSx - 1) / BSx));
+#define LRS_DIAG(UU, BB)                                                                                          \
+    LRS_LAYOUT_SWITCH(c.G, c.E, {                                                                                 \
+        if (mode == 1)                                                                                            \
+            hipLaunchKernelGGL((k_auv_diag<GG, EE, 1, UU, BB>), dim3(grid), dim3(BB), 0, st, P.m, (long)cone * P.m, \
+                               c.ld, P.con1_w, Xc, Xc, scale, accumulate, out, b_for_vio, vio_part, tk, fin, guard,  \
+                               sum_upd);                                                                          \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_auv_diag<GG, EE, 0, UU, BB>), dim3(grid), dim3(BB), 0, st, P.m, (long)cone * P.m, \
+                               c.ld, P.con1_w, Xc, Yc, scale, accumulate, out, b_for_vio, vio_part, tk, fin, guard,  \
+                               sum_upd);                                                                          \
+    })
+        if (BSx == 1024) {
+            if (U == 1) { LRS_DIAG(1, 1024); }
+            else if (U == 2) { LRS_DIAG(2, 1024); }
+            else { LRS_DIAG(4, 1024); }
+        } else if (BSx == 512) {
+            if (U == 1) { LRS_DIAG(1, 512); }
+            else if (U == 2) { LRS_DIAG(2, 512); }
+            else { LRS_DIAG(4, 512); }
+        } else {
+            if (U == 1) { LRS_DIAG(1, 256); }
+            else if (U == 2) { LRS_DIAG(2, 256); }
+            else { LRS_DIAG(4, 256); }
+        }
+#undef LRS_DIAG
         LRS_CHECK_LAUNCH();
         return 0;
     }
@@ -4327,17 +4354,20 @@ int mfma_f64_peak(hipStream_t st, double *tflops) {
 // by a packed C (dataMatDenseMultiRkMat lorads_sdp_data.c:948-973); here C stays a full n x n
 // row-major matrix and every C-term is a product with it: <C, sym R D^T> = <R, C D>,
 // <C, D D^T> = <D, C D>, S R = (C + A^*(M1)) R = C R + A^*(M1) R.
-// k_cgemm: Y = scale C X (+ beta Y) on the rows of one cone, X / Y row-major n x ld.  Output
+// k_cgemm: Y = scale C X (+ beta Y) on the rows of one cone, X / Y row-major n x ld; C is the
+// cone's row block of nr rows (row r0 + t of the cone: C row t, n columns; unsharded nr = n,
+// r0 = 0; a shard: its owned rows, DevCone row0 / nown).  Output
 // tiles of kCgBM rows x kCgBN columns, four waves as 2 x 2, a wave 16 rows x 32 columns (two
 // v_mfma_f64_16x16x4f64 accumulators); C and X staged through double-buffered LDS tiles of
 // kCgBK k-rows, the next tile's global loads issued before the current tile's MFMAs.  With
 // `ctrl` (the ALM iteration): nothing when the iteration is inactive, X = D, and the block's
 // partials <R, Y>, <X, Y> (R the current iterate) in slots 0 and 1 of stage A's 8.
 constexpr int kCgBM = 32, kCgBN = 64, kCgBK = 32, kCgMaxGrid = 1024;
-__global__ void __launch_bounds__(kBlock) k_cgemm(int n, int r, int ld, double scale, const double *__restrict__ Cd,
-                                                  const double *__restrict__ X, double *__restrict__ Y, double beta,
-                                                  const double *__restrict__ ctrl, const double *__restrict__ Rb0,
-                                                  const double *__restrict__ Rb1, double *__restrict__ part, int poff) {
+__global__ void __launch_bounds__(kBlock) k_cgemm(int n, int nr, int r0, int r, int ld, double scale,
+                                                  const double *__restrict__ Cd, const double *__restrict__ X,
+                                                  double *__restrict__ Y, double beta, const double *__restrict__ ctrl,
+                                                  const double *__restrict__ Rb0, const double *__restrict__ Rb1,
+                                                  double *__restrict__ part, int poff) {
     __shared__ double Cs[2][kCgBM][kCgBK + 1];
     __shared__ double Xs[2][kCgBK][kCgBN + 1];
     const double *__restrict__ R = nullptr;
@@ -4346,7 +4376,7 @@ __global__ void __launch_bounds__(kBlock) k_cgemm(int n, int r, int ld, double s
         R = ctrl[C_RCUR] == 0.0 ? Rb0 : Rb1;
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
-    const int ntm = (n + kCgBM - 1) / kCgBM, ntn = (r + kCgBN - 1) / kCgBN;
+    const int ntm = (nr + kCgBM - 1) / kCgBM, ntn = (r + kCgBN - 1) / kCgBN;
     const int nk = (n + kCgBK - 1) / kCgBK;
     // staging maps: C tile row t >> 3, k (t & 7) * 4 .. +3; X tile k-row t >> 3, columns (t & 7) * 8 .. +7
     const int crow = threadIdx.x >> 3, ck = (threadIdx.x & 7) * 4;
@@ -4361,7 +4391,7 @@ __global__ void __launch_bounds__(kBlock) k_cgemm(int n, int r, int ld, double s
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const int gk = k0 + ck + t;
-                cr[t] = (gi < n && gk < n) ? Cd[(long)gi * n + gk] : 0.0;
+                cr[t] = (gi < nr && gk < n) ? Cd[(long)gi * n + gk] : 0.0;
             }
             const int gk = k0 + xrow;
 #pragma unroll
@@ -4401,8 +4431,8 @@ __global__ void __launch_bounds__(kBlock) k_cgemm(int n, int r, int ld, double s
             for (int q = 0; q < 4; ++q) {
                 const int row = m0 + wm * 16 + (lane >> 4) + 4 * q;
                 const int col = n0 + wn * 32 + t * 16 + (lane & 15);
-                if (row < n && col < r) {
-                    const long o = (long)row * ld + col;
+                if (row < nr && col < r) {
+                    const long o = (long)(r0 + row) * ld + col;
                     double v = scale * acc[t][q];
                     if (beta != 0.0) v += beta * Y[o];
                     Y[o] = v;
@@ -4471,14 +4501,14 @@ __global__ void __launch_bounds__(kCjThreads) k_cjx(int n, int r, int ld, double
     if (part) write_partials<8, kCjThreads>(dots, part, poff);
 }
 static int cgemm_grid(const DevCone &c) {
-    const long tiles = (long)((c.n + kCgBM - 1) / kCgBM) * ((c.r + kCgBN - 1) / kCgBN);
+    const long tiles = (long)((c.nown + kCgBM - 1) / kCgBM) * ((c.r + kCgBN - 1) / kCgBN);
     return (int)std::max(1L, std::min((long)kCgMaxGrid, tiles));
 }
 int launch_dense_cx(const DevProblem &P, int cone, const double *X, double *Y, double beta, hipStream_t st) {
     const DevCone &c = P.cones[cone];
     if (!c.dense_c) return 0;
-    if (c.nown != c.n) {
-        snprintf(g_err, sizeof(g_err), "dense objective: sharded cones are not supported");
+    if (c.dense_c == 2 && c.nown != c.n) {
+        snprintf(g_err, sizeof(g_err), "constant objective: sharded cones take the slot path");
         return -1;
     }
     if (c.dense_c == 2) {
@@ -4487,8 +4517,8 @@ int launch_dense_cx(const DevProblem &P, int cone, const double *X, double *Y, d
         LRS_CHECK_LAUNCH();
         return 0;
     }
-    hipLaunchKernelGGL(k_cgemm, dim3(cgemm_grid(c)), dim3(kBlock), 0, st, c.n, c.r, c.ld, P.dense_scale, c.Cd,
-                       X + c.foff, Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0);
+    hipLaunchKernelGGL(k_cgemm, dim3(cgemm_grid(c)), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld,
+                       P.dense_scale, c.Cd, X + c.foff, Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0);
     LRS_CHECK_LAUNCH();
     return 0;
 }
@@ -4509,8 +4539,8 @@ int launch_dense_cd(const DevProblem &P, const DevWork &W, const double *ctrl, i
             continue;
         }
         const int grid = cgemm_grid(c);
-        hipLaunchKernelGGL(k_cgemm, dim3(grid), dim3(kBlock), 0, st, c.n, c.r, c.ld, P.dense_scale, c.Cd, W.D + c.foff,
-                           W.CD + c.foff, 0.0, ctrl, W.R + c.foff, W.R2 + c.foff, W.part, off);
+        hipLaunchKernelGGL(k_cgemm, dim3(grid), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld, P.dense_scale,
+                           c.Cd, W.D + c.foff, W.CD + c.foff, 0.0, ctrl, W.R + c.foff, W.R2 + c.foff, W.part, off);
         LRS_CHECK_LAUNCH();
         off += grid;
     }
@@ -4883,10 +4913,6 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     // dense-objective cones: C D and its two objective partials after stage A's blocks
     const int offCD = nblkA;
     if (ngd) {
-        if (sh) {
-            snprintf(g_err, sizeof(g_err), "dense objective: sharded solves are not supported");
-            return -1;
-        }
         nblkA += ngd;
         if (nblkA > kMaxPartialBlocks) {
             snprintf(g_err, sizeof(g_err), "dense objective: %d partial blocks past %d", nblkA, kMaxPartialBlocks);

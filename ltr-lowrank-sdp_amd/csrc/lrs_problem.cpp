@@ -34,7 +34,7 @@ bool is_sep(char c) {
 }  // namespace
 
 static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, bool lpEntries,
-                          std::vector<RawEntry> &raw, HostProblem &hp, std::string &err);
+                          std::vector<RawEntry> &raw, HostProblem &hp, std::string &err, bool allow_dense = true);
 
 bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err) {
     FILE *f = fopen(path.c_str(), "rb");
@@ -115,8 +115,10 @@ bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err) {
     return build_problem(m, K, dims, nLp, lpEntries, raw, hp, err);
 }
 
+// allow_dense = false (a shard's local problem): every objective entry stays in the slot
+// pattern; shard_problem installs a dense cone's owned row block itself.
 static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, bool lpEntries,
-                          std::vector<RawEntry> &raw, HostProblem &hp, std::string &err) {
+                          std::vector<RawEntry> &raw, HostProblem &hp, std::string &err, bool allow_dense) {
     if (nLp > 0 || lpEntries) {
         err = "LP blocks are not supported by the device path yet (SURVEY.md §2, out of scope)";
         return false;
@@ -138,7 +140,7 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
     {
         const char *ek = getenv("LRS_CONST_C");
         const char *ev = getenv("LRS_DENSE_C");
-        if (!ek && !(ev && ev[0] == '0')) {
+        if (allow_dense && !ek && !(ev && ev[0] == '0')) {
             bool ok = true, any = false;
             long N = 0, Ptot = 0;
             int ldmax = 0;
@@ -213,9 +215,11 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
             if (ev && ev[0] == '0') c.dense_c = false;
             else if (ev && ev[0] == '1') c.dense_c = ncobj > 0;
             else c.dense_c = c.n >= kDenseCMinN && 4 * ncobj >= tri;
+            if (!allow_dense) c.dense_c = false;
             // constant C (all entries one value): the rank-one products, no n x n matrix
             const char *ek = getenv("LRS_CONST_C");
-            if (((ek && ek[0] == '1') || auto_const) && !(ev && ev[0] == '0') && c.n >= kConstCMinN && ncobj == tri) {
+            if (allow_dense && ((ek && ek[0] == '1') || auto_const) && !(ev && ev[0] == '0') && c.n >= kConstCMinN &&
+                ncobj == tri) {
                 double v0 = 0.0;
                 bool same = true, first = true;
                 for (auto &e : me) {
@@ -368,12 +372,10 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
     for (int k = 0; k < K; ++k)
         if (g.cones[k].n < world) { err = "sharded solve: a cone has fewer rows than shards"; return false; }
     // a constant objective (C = c_alpha J) is sharded as the slot path: every pair with an owned
-    // endpoint carries C in the local pattern, every row is in the halo
-    for (int k = 0; k < K; ++k)
-        if (g.cones[k].dense_c && !g.cones[k].const_c) {
-            err = "sharded solve: dense-objective cones are not supported";
-            return false;
-        }
+    // endpoint carries C in the local pattern, every row is in the halo.  A dense objective
+    // (C a full matrix): each shard holds the row block C_own (owned rows x all n columns) and
+    // every row in its halo, so C_own X reads a complete X after the halo exchange.
+    auto dense_mat = [&](int k) { return g.cones[k].dense_c && !g.cones[k].const_c; };
     plan = ShardPlan();
     plan.world = world; plan.rank = rank;
     plan.cones.assign(K, ShardConePlan());
@@ -419,7 +421,7 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
         const HostCone &gc = g.cones[k];
         ShardConePlan &cp = plan.cones[k];
         const int n = gc.n, r0 = cp.bounds[rank], r1 = cp.bounds[rank + 1];
-        std::vector<char> need(n, gc.const_c ? 1 : 0);
+        std::vector<char> need(n, (gc.const_c || dense_mat(k)) ? 1 : 0);
         for (int i = r0; i < r1; ++i) {
             need[i] = 1;
             for (int q = gc.adj_ptr[i]; q < gc.adj_ptr[i + 1]; ++q) need[gc.adj_col[q]] = 1;
@@ -465,7 +467,7 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
     out = HostProblem();
     out.b.resize(ml);
     for (int q = 0; q < ml; ++q) out.b[q] = g.b[plan.con_gid[q]];
-    if (!build_problem(ml, K, dims, 0, false, raw, out, err)) return false;
+    if (!build_problem(ml, K, dims, 0, false, raw, out, err, false)) return false;
     // the solve's norms and rank statistics are the whole problem's
     out.bNrm1 = g.bNrm1; out.bNrm2 = g.bNrm2; out.bNrmInf = g.bNrmInf;
     out.cNrm1 = g.cNrm1; out.cNrm2 = g.cNrm2; out.cNrmInf = g.cNrmInf;
@@ -478,6 +480,11 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
         // entries count in A(.) on the shard owning their slot's lower row
         const int o0 = cp.row0, o1 = cp.row0 + cp.nown;
         for (HostEntry &e : oc.ent) e.owned = oc.prow[e.slot] >= o0 && oc.prow[e.slot] < o1;
+        if (dense_mat(k)) {   // every row local, local ids = global ids: C's owned row block
+            const int n = gc.n, r0 = cp.bounds[rank];
+            oc.dense_c = true;
+            oc.Cfull.assign(gc.Cfull.begin() + (size_t)r0 * n, gc.Cfull.begin() + (size_t)(r0 + cp.nown) * n);
+        }
     }
     // shared constraints stay on the multi-slot path on every holder
     out.force_glob.assign(ml, 0);
@@ -497,7 +504,7 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
             if (q == rank) continue;
             const int q0 = cp.bounds[q], q1 = cp.bounds[q + 1];
             for (int i = r0; i < r1; ++i) {
-                bool adj = gc.const_c;   // C couples every pair of rows
+                bool adj = gc.const_c || dense_mat(k);   // C couples every pair of rows
                 for (int t = gc.adj_ptr[i]; t < gc.adj_ptr[i + 1] && !adj; ++t)
                     adj = gc.adj_col[t] >= q0 && gc.adj_col[t] < q1;
                 if (adj) cp.send_rows.push_back(lid[k][i]);

@@ -709,8 +709,9 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
         const DevCone &dc = P.cones[k];
         if (!dc.dense_c) continue;
         OPC(launch_dense_cx(P, k, Y ? Y : X, W.CD, 0.0, c->st));
-        double v;
-        if (op_dot(c, (long)dc.n * dc.ld, X + dc.foff, W.CD + dc.foff, &v)) return -1;
+        double v;   // over the rows C X covers (sharded: the owned rows, summed over the shards)
+        const long ro = dc.foff + (long)dc.row0 * dc.ld;
+        if (op_dot(c, (long)dc.nown * dc.ld, X + ro, W.CD + ro, &v)) return -1;
         o += v;
     }
     if (pinf) *pinf = std::sqrt(t[2 * P.K + (fin - TF_GATHER)]) / (1 + c->hp.bNrm1);
@@ -733,10 +734,11 @@ static int op_grad(lrs_ctx *c, double rho, double *lag) {
     for (int k = 0; k < P.K; ++k) {
         const DevCone &dc = P.cones[k];
         if (!dc.dense_c) continue;
-        double *Gk = W.G[c->gcur] + dc.foff;
+        const long ro = dc.foff + (long)dc.row0 * dc.ld;   // the rows C R covers (sharded: owned)
+        double *Gk = W.G[c->gcur] + ro;
         OPC(launch_dense_cx(P, k, W.R, W.CR, 0.0, c->st));
-        OPC(launch_axpby((long)dc.n * dc.ld, 2.0, W.CR + dc.foff, 1.0, Gk, c->st));
-        if (op_dot(c, (long)dc.n * dc.ld, Gk, Gk, &v[k])) return -1;
+        OPC(launch_axpby((long)dc.nown * dc.ld, 2.0, W.CR + ro, 1.0, Gk, c->st));
+        if (op_dot(c, (long)dc.nown * dc.ld, Gk, Gk, &v[k])) return -1;
     }
     double tot = 0.0;
     for (int k = 0; k < P.K; ++k) {
@@ -1616,8 +1618,9 @@ static int op_q12_fin(lrs_ctx *c, double *p1h, double *p2h) {
         if (dc.dense_c) {   // <C, sym R D^T> = <R, C D>, <C, D D^T> = <D, C D>
             OPC(launch_dense_cx(P, k, W.D, W.CD, 0.0, c->st));
             double u, v;
-            if (op_dot(c, (long)dc.n * dc.ld, W.R + dc.foff, W.CD + dc.foff, &u)) return -1;
-            if (op_dot(c, (long)dc.n * dc.ld, W.D + dc.foff, W.CD + dc.foff, &v)) return -1;
+            const long ro = dc.foff + (long)dc.row0 * dc.ld;   // sharded: the owned rows
+            if (op_dot(c, (long)dc.nown * dc.ld, W.R + ro, W.CD + ro, &u)) return -1;
+            if (op_dot(c, (long)dc.nown * dc.ld, W.D + ro, W.CD + ro, &v)) return -1;
             a += u; b += v;
         }
     }

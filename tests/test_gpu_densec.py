@@ -191,3 +191,56 @@ def test_dense_and_slot_paths_agree_per_trip_at_n2000(solver_mod, gen_dir, kpath
             # the iterate's 1e-16 differences amplified to ~1e-9 (R and G stay at 1e-9)
             tol = 1e-8 if (tiles == "2d" and key == "cvs") else TOL
             assert rel_err(a[key], b[key]) < tol, (key, rel_err(a[key], b[key]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_dense_objective_steps_match_reference(solver_mod, gen_dir, world):
+    """A dense objective sharded by rows (lrs_problem.cpp shard_problem): each shard holds C's
+    owned row block (owned rows x all n columns) and every row in its halo, so C_own D / C_own R
+    (k_cgemm over the row block) read a complete factor after the halo exchange, and <R, C D>,
+    <D, C D> are owned-row partials summed with the stage totals.  K trips on every shard
+    against the reference's own (steps_rdense300): tau, ||G||^2 and pinf to 1e-9."""
+    from test_gpu_shard import run_sharded
+    z = np.load(os.path.join(GOLDEN, "steps_rdense300.npz"))
+    path = _rdense(gen_dir, 300, 3000, 6, 7)
+    rank = int(z["rank_flag"])
+    kw = {"reoptLevel": 0}
+    if rank > 0:
+        kw["fixedRank"] = rank
+    with dense_mode("1"):
+        for K in [int(k) for k in z["ks"]]:
+            trips = z[f"K{K}_trips"]
+            if trips.shape[0] < K:
+                continue
+            res = run_sharded(solver_mod, path, world, lambda sv: sv.alm_steps(K, **kw))
+            tau, rn, lag, pinf = trips[K - 1]
+            for info, d in res:
+                assert info[0] == world and info[4] > 0   # sharded, with a halo
+                assert d["inner"] == K
+                assert abs(d["tau"] - tau) <= TOL * abs(tau), (K, d["tau"], tau)
+                assert abs(d["lag"] - lag) <= TOL * abs(lag), (K, d["lag"], lag)
+                assert abs(d["pinf"] - pinf) <= TOL * max(abs(pinf), 1e-300), (K, d["pinf"], pinf)
+
+
+def test_sharded_dense_objective_solve_matches_single_gpu(solver_mod, gen_dir):
+    """Whole sharded ALM + ADMM solve with the dense objective (C_own Y in the ADMM right-hand
+    side, C_own q in the dual-infeasibility Lanczos) against the single-GPU solve: every shard
+    identical; objectives within 10 x the certified gaps, the same final rank and status."""
+    from test_gpu_shard import run_sharded
+    g = _solves()[0]
+    path = _rdense(gen_dir, g["n"], g["m"], g["k"], g["seed"], g["sha256"])
+    kw = dict(reoptLevel=0)
+    with dense_mode("1"):
+        single = solver_mod.Solver(path)
+        ref = single.solve(**kw)
+        single.close()
+        res = run_sharded(solver_mod, path, 2, lambda sv: sv.solve(**kw))
+    first = res[0][1]
+    for _, r in res[1:]:
+        for k in ("alm_inner", "admm_iter", "pobj", "dobj", "pinf", "gap", "final_rank", "status"):
+            assert r[k] == first[k], (k, r[k], first[k])
+    tol = 10 * (ref["gap"] + first["gap"]) + 1e-6
+    for k in ("pobj", "dobj"):
+        assert abs(first[k] - ref[k]) <= tol * (1 + abs(ref[k])), (k, first[k], ref[k], tol)
+    assert first["final_rank"] == ref["final_rank"] and first["status"] == ref["status"]
+    assert first["dinf"] >= 0

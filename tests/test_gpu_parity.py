@@ -138,8 +138,10 @@ def test_stage_timing(solver_mod, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["mc_rand200", "theta25x3", "rsparse60"])
-def test_constraint_entry_auut_matches_pattern_path(solver_mod, name):
-    """k_auv_con (A(RR^T) straight from constraint entries) == SDDMM over the pattern + gather."""
+def test_constraint_entry_auut_matches_pattern_path(solver_mod, name, monkeypatch):
+    """k_auv_con (A(RR^T) straight from constraint entries) == SDDMM over the pattern + gather;
+    k_auv_diag (MaxCut's identity-diagonal constraints: row-wise dot products, no index loads)
+    the same values up to the compiler's FMA contraction of the lane sums (a few ulp)."""
     g = load_kernels(name)
     s = split_inputs(g)
     sv = solver_mod.Solver(instance(name))
@@ -148,8 +150,12 @@ def test_constraint_entry_auut_matches_pattern_path(solver_mod, name):
     cvs, _, _ = sv.constr_rr()
     sv.time_auut(1)
     q = sv.get_vec(solver_mod.Q1)
+    monkeypatch.setenv("LRS_NO_AUV_DIAG", "1")
+    sv.time_auut(1)
+    qc = sv.get_vec(solver_mod.Q1)
     if len(s["dims"]) == 1:
-        assert np.array_equal(q, cvs)          # same arithmetic, same order
+        assert np.array_equal(qc, cvs)          # same arithmetic, same order
+        assert np.max(np.abs(q - cvs) / np.maximum(1.0, np.abs(cvs))) <= 1e-15
     assert rel_err(q, g["cvs_rr"]) < TOL
     assert sv.auut_bytes() > 0
 
