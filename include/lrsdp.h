@@ -185,6 +185,12 @@ int lrs_time_gram(lrs_ctx *ctx, int cone, int reps, double *avg_ms, double *gram
  * v_mfma_f64_16x16x4f64 on every CU (8 independent accumulators a wave, 2 waves a SIMD).
  * Diagnostics for the Gram's roofline; no reference counterpart. */
 int lrs_mfma_f64_peak(lrs_ctx *ctx, double *tflops);
+/* The same probe at `waves_per_simd` (1..8) waves a SIMD with `chains` (4 or 8) independent
+ * accumulators a wave, plus the shader clock under that load (s_memtime against the 100 MHz
+ * wall clock, MHz) and the cycles a SIMD spends per v_mfma_f64_16x16x4f64: the matrix-core
+ * rate separated from the clock (bench.py "mfma_probe").  No reference counterpart. */
+int lrs_mfma_f64_probe(lrs_ctx *ctx, int waves_per_simd, int chains, double *tflops, double *mhz,
+                       double *cycles_per_mfma);
 
 /* Dense objective (a cone whose C is kept as a full n x n matrix: LRS_DENSE_C=1, or n >= 1024
  * with C filling >= 1/4 of the lower triangle): ms per C R product on the FP64 matrix cores

@@ -146,6 +146,7 @@ constexpr int kAuvMinPerTile = 768;  //   >= this many entries (constraint entri
                                      //   for the stage kernels: 3x reuse of each staged row); C5 ~1850, a
                                      //   C5-structured m = 1e5 ~98 (slower tiled); LRS_AUV_TILES /
                                      //   LRS_SLOT_TILES = 0/1 override
+constexpr int kCgSplitSlabs = 8;      // k_cgemm2's most K-slices (DevWork::CGK slabs)
 constexpr int kNX = 8;              // column blocks of the tiled long-row kernels (one per XCD)
 constexpr int kTileMinDeg = 32;
 constexpr int kDenseRow = 64;        // entries of a row past which the latency kernels slice it
@@ -204,6 +205,7 @@ struct DevProblem {
     int ndense = 0;                                          // cones with a dense objective (DevCone::Cd)
     bool tiles = false;                                      // column-tiled long-row kernels (LRS_TILES=1 at alloc)
     double *gp = nullptr;                                    // DevWork::GP (kNX partial factors), the tiled S X's scratch
+    double *cgk = nullptr;                                   // DevWork::CGK: k_cgemm2's split-K slabs (kCgSplitSlabs x NRpad)
     double dense_scale = 1.0;                                // objScale_dualvar's factor on those C
     // K > 1: all cones as one block-diagonal row space (global rows and columns); used by
     // the split iteration when every cone has the same (G, E) row layout
@@ -218,6 +220,7 @@ struct DevWork {
     // dense-objective cones (DevCone::Cd): C R of the current iterate (carried C R + tau C D
     // through the inner loop, recomputed by op_grad) and C D of the iteration; zero elsewhere
     double *CR = nullptr, *CD = nullptr;
+    double *CGK = nullptr;   // k_cgemm2's split-K slabs (dense cones of >= 2048 rows): kCgSplitSlabs x NR
     // column-tiled long-row kernels: kNX partial S R_new factors (kNX * NRpad), null when no cone
     // has long rows
     double *GP = nullptr;
@@ -284,6 +287,7 @@ int launch_gram(const DevProblem &P, int cone, const double *X, const double *Y,
                 double *gram, int *nblk_used, hipStream_t st, bool reduce = true);
 // sustained v_mfma_f64_16x16x4f64 rate: every CU, 2 waves a SIMD, 8 accumulators a wave
 int mfma_f64_peak(hipStream_t st, double *tflops);
+int mfma_f64_probe(hipStream_t st, int wps, int chains, double *tflops, double *mhz, double *cyc_per_mfma);
 // dense objective of cone `cone` (DevCone::Cd): Y = scale C X + beta Y on the cone's rows
 // (X, Y full factor buffers; columns r..ld of Y written 0)
 int launch_dense_cx(const DevProblem &P, int cone, const double *X, double *Y, double beta, hipStream_t st);

@@ -4307,47 +4307,76 @@ int launch_alm_m1(const DevProblem &P, double rho, const double *lam, const doub
 static int num_cus();
 // the FP64 matrix-core ceiling the Gram is measured against (bench.py): back-to-back
 // v_mfma_f64_16x16x4f64 on 8 independent accumulators, 2 waves a SIMD on every CU
-__global__ void __launch_bounds__(kBlock) k_mfma_peak(int iters, double *out) {
-    gram_acc_t acc[8];
+// FP64 matrix-core probe: every wave issues `iters` rounds of CH independent
+// v_mfma_f64_16x16x4f64 (no dependence between consecutive MFMAs of a round), blocks of one
+// wave per SIMD, `wps` blocks per CU.  Block 0's wave 0 stamps the shader clock (s_memtime)
+// and the 100 MHz wall clock at its start and end: the clock under load and, from it, the
+// cycles one SIMD spends per MFMA (an MFMA rate, not a FLOP rate, independent of the clock).
+template <int CH>
+__global__ void __launch_bounds__(kBlock) k_mfma_peak(int iters, double *out, unsigned long long *clk) {
+    gram_acc_t acc[CH];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = gram_acc_t{0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < CH; ++k) acc[k] = gram_acc_t{0.0, 0.0, 0.0, 0.0};
     const double a = 1.0 + 1e-9 * threadIdx.x, b = 1.0 - 1e-9 * threadIdx.x;
+    unsigned long long c0 = 0, w0 = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { c0 = __builtin_amdgcn_s_memtime(); w0 = wall_clock64(); }
     for (int i = 0; i < iters; ++i)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
+        for (int k = 0; k < CH; ++k) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
     double s = 0.0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s += (acc[k][0] + acc[k][1]) + (acc[k][2] + acc[k][3]);
+    for (int k = 0; k < CH; ++k) s += (acc[k][0] + acc[k][1]) + (acc[k][2] + acc[k][3]);
     out[(long)blockIdx.x * kBlock + threadIdx.x] = s;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && s != 12345.678) {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), w1 = wall_clock64();
+        clk[0] = c1 - c0;
+        clk[1] = w1 - w0;
+    }
 }
-int mfma_f64_peak(hipStream_t st, double *tflops) {
-    const int blocks = 2 * num_cus(), iters = 2000;
+// waves per SIMD wps (1..8 blocks of four waves per CU), chains CH in {4, 8}
+int mfma_f64_probe(hipStream_t st, int wps, int chains, double *tflops, double *mhz, double *cyc_per_mfma) {
+    const int blocks = std::max(1, std::min(8, wps)) * num_cus(), iters = 4000;
     double *out = nullptr;
+    unsigned long long *clk = nullptr;
     hipEvent_t e0, e1;
-    if (hipMalloc((void **)&out, sizeof(double) * blocks * kBlock) != hipSuccess) {
-        snprintf(g_err, sizeof(g_err), "mfma_f64_peak: hipMalloc");
+    if (hipMalloc((void **)&out, sizeof(double) * blocks * kBlock) != hipSuccess ||
+        hipMalloc((void **)&clk, 2 * sizeof(unsigned long long)) != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "mfma_f64_probe: hipMalloc");
         return -1;
     }
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kBlock), 0, st, iters, out);   // warm (clocks up)
+    auto go = [&]() {
+        if (chains <= 4) hipLaunchKernelGGL(k_mfma_peak<4>, dim3(blocks), dim3(kBlock), 0, st, iters, out, clk);
+        else hipLaunchKernelGGL(k_mfma_peak<8>, dim3(blocks), dim3(kBlock), 0, st, iters, out, clk);
+    };
+    go();   // warm (clocks up)
     (void)hipEventRecord(e0, st);
-    hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kBlock), 0, st, iters, out);
+    go();
     (void)hipEventRecord(e1, st);
     const hipError_t e = hipEventSynchronize(e1);
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, e0, e1);
+    unsigned long long h[2] = {0, 0};
+    (void)hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipFree(out);
+    (void)hipFree(clk);
     if (e != hipSuccess || ms <= 0.f) {
-        snprintf(g_err, sizeof(g_err), "mfma_f64_peak: %s", hipGetErrorString(e));
+        snprintf(g_err, sizeof(g_err), "mfma_f64_probe: %s", hipGetErrorString(e));
         return -1;
     }
-    const double flop = (double)blocks * (kBlock / 64) * iters * 8 * 2048.0;
+    const int ch = chains <= 4 ? 4 : 8;
+    const double flop = (double)blocks * (kBlock / 64) * iters * ch * 2048.0;
     *tflops = flop / (ms * 1e-3) / 1e12;
+    const double wall_s = h[1] * 1e-8;   // 100 MHz
+    if (mhz) *mhz = wall_s > 0 ? h[0] / wall_s / 1e6 : 0.0;
+    // a SIMD runs wps waves (one per block): its MFMA count over the block-0 wave's span
+    if (cyc_per_mfma) *cyc_per_mfma = (double)h[0] / ((double)std::max(1, std::min(8, wps)) * iters * ch);
     return 0;
 }
+int mfma_f64_peak(hipStream_t st, double *tflops) { return mfma_f64_probe(st, 2, 8, tflops, nullptr, nullptr); }
 
 // ---- dense objective on the FP64 matrix cores.  The reference's dense
 // branches form sym(U V^T) in full (fds_syr2k, LORADSUVt lorads_alg_common.c:72-89) and multiply
@@ -4500,6 +4529,159 @@ __global__ void __launch_bounds__(kCjThreads) k_cjx(int n, int r, int ld, double
     }
     if (part) write_partials<8, kCjThreads>(dots, part, poff);
 }
+// k_cgemm2: the same product as k_cgemm at full column width -- output tiles of kC2BM rows x
+// kC2BN = 128 columns (a wave 16 x 64: four 16 x 16 MFMA accumulators off one A fragment), so
+// C streams from HBM once per 128 factor columns instead of once per 64 -- and split over K:
+// block (tile, s) sums k-tiles [s K / S, (s + 1) K / S) into the scratch slab s (raw sums),
+// k_cgemm2_fin adds the S slabs in slab order (deterministic), scales, applies beta and takes
+// the objective dots.  S = 1: the epilogue is fused (no scratch).  X's LDS rows are padded to
+// 144 doubles so the two k-rows of a ds_read_b64 lane group sit 32 banks apart; C's to 17.
+constexpr int kC2BM = 32, kC2BN = 128, kC2BK = 16, kC2XS = 144, kCgSplitMax = kCgSplitSlabs;
+template <bool SPLIT>
+__global__ void __launch_bounds__(kBlock) k_cgemm2(int n, int nr, int r0, int r, int ld, double scale,
+                                                   const double *__restrict__ Cd, const double *__restrict__ X,
+                                                   double *__restrict__ Y, double beta, const double *__restrict__ ctrl,
+                                                   const double *__restrict__ Rb0, const double *__restrict__ Rb1,
+                                                   double *__restrict__ part, int poff, int S,
+                                                   double *__restrict__ Pk) {
+    __shared__ double Cs[2][kC2BM][kC2BK + 1];
+    __shared__ double Xs[2][kC2BK][kC2XS];
+    const double *__restrict__ R = nullptr;
+    if (ctrl) {
+        if (ctrl[C_ACTIVE] == 0.0) return;   // grid-uniform
+        R = ctrl[C_RCUR] == 0.0 ? Rb0 : Rb1;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+    const int ntm = (nr + kC2BM - 1) / kC2BM, ntn = (r + kC2BN - 1) / kC2BN;
+    const int nk = (n + kC2BK - 1) / kC2BK, kper = (nk + S - 1) / S;
+    // staging maps: C tile row t >> 3, k (t & 7) * 2 .. +1; X tile k-row t >> 4, columns (t & 15) * 8 .. +7
+    const int crow = threadIdx.x >> 3, ck = (threadIdx.x & 7) * 2;
+    const int xrow = threadIdx.x >> 4, xc = (threadIdx.x & 15) * 8;
+    double dots[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int item = blockIdx.x; item < ntm * ntn * S; item += gridDim.x) {
+        const int tile = item / S, sk = item - tile * S;
+        const int m0 = (tile / ntn) * kC2BM, n0 = (tile % ntn) * kC2BN;
+        const int kt0 = sk * kper, kt1 = min(nk, kt0 + kper);
+        gram_acc_t acc[4] = {gram_acc_t{0.0, 0.0, 0.0, 0.0}, gram_acc_t{0.0, 0.0, 0.0, 0.0},
+                             gram_acc_t{0.0, 0.0, 0.0, 0.0}, gram_acc_t{0.0, 0.0, 0.0, 0.0}};
+        double cr[2];
+        double2 xr[4];
+        auto gload = [&](int k0) {
+            const int gi = m0 + crow;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int gk = k0 + ck + t;
+                cr[t] = (gi < nr && gk < n) ? Cd[(long)gi * n + gk] : 0.0;
+            }
+            const int gk = k0 + xrow, col = n0 + xc;
+            const bool ok = gk < n && col < ld;   // padded columns are zero in the factor layout
+            const double2 *xp = reinterpret_cast<const double2 *>(X + (long)(ok ? gk : 0) * ld + (ok ? col : 0));
+#pragma unroll
+            for (int t = 0; t < 4; ++t) xr[t] = ok ? xp[t] : make_double2(0.0, 0.0);
+        };
+        auto sstore = [&](int buf) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) Cs[buf][crow][ck + t] = cr[t];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                Xs[buf][xrow][xc + 2 * t] = xr[t].x;
+                Xs[buf][xrow][xc + 2 * t + 1] = xr[t].y;
+            }
+        };
+        if (kt0 < kt1) {
+            gload(kt0 * kC2BK);
+            sstore(0);
+        }
+        __syncthreads();
+        for (int kt = kt0; kt < kt1; ++kt) {
+            const int cur = (kt - kt0) & 1;
+            if (kt + 1 < kt1) gload((kt + 1) * kC2BK);
+#pragma unroll
+            for (int ks = 0; ks < kC2BK / 4; ++ks) {
+                const double a = Cs[cur][wm * 16 + (lane & 15)][ks * 4 + (lane >> 4)];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const double b = Xs[cur][ks * 4 + (lane >> 4)][wn * 64 + t * 16 + (lane & 15)];
+                    acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
+                }
+            }
+            if (kt + 1 < kt1) sstore(cur ^ 1);
+            __syncthreads();
+        }
+        // D fragment: col = lane & 15, row = (lane >> 4) + 4 q
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = m0 + wm * 16 + (lane >> 4) + 4 * q;
+                const int col = n0 + wn * 64 + t * 16 + (lane & 15);
+                if (row < nr && col < r) {
+                    if (SPLIT) {
+                        Pk[((long)sk * nr + row) * ld + col] = acc[t][q];
+                    } else {
+                        const long o = (long)(r0 + row) * ld + col;
+                        double v = scale * acc[t][q];
+                        if (beta != 0.0) v += beta * Y[o];
+                        Y[o] = v;
+                        if (R) {
+                            dots[0] += R[o] * v;
+                            dots[1] += X[o] * v;
+                        }
+                    }
+                }
+            }
+    }
+    if (!SPLIT && part) write_partials<8, kBlock>(dots, part, poff + blockIdx.x);
+}
+// the S slabs of k_cgemm2<true> in slab order -> Y (scale, beta) and the objective dots
+__global__ void __launch_bounds__(kBlock) k_cgemm2_fin(int nr, int r0, int r, int ld, int S, double scale,
+                                                       const double *__restrict__ Pk, const double *__restrict__ X,
+                                                       double *__restrict__ Y, double beta,
+                                                       const double *__restrict__ ctrl, const double *__restrict__ Rb0,
+                                                       const double *__restrict__ Rb1, double *__restrict__ part,
+                                                       int poff) {
+    const double *__restrict__ R = nullptr;
+    if (ctrl) {
+        if (ctrl[C_ACTIVE] == 0.0) return;
+        R = ctrl[C_RCUR] == 0.0 ? Rb0 : Rb1;
+    }
+    double dots[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const long tot = (long)nr * ld;
+    for (long t = (long)blockIdx.x * kBlock + threadIdx.x; t < tot; t += (long)gridDim.x * kBlock) {
+        const int col = (int)(t % ld);
+        if (col >= r) continue;
+        double a = Pk[t];
+        for (int q = 1; q < S; ++q) a += Pk[(long)q * tot + t];
+        const long o = (long)r0 * ld + t;
+        double v = scale * a;
+        if (beta != 0.0) v += beta * Y[o];
+        Y[o] = v;
+        if (R) {
+            dots[0] += R[o] * v;
+            dots[1] += X[o] * v;
+        }
+    }
+    if (part) write_partials<8, kBlock>(dots, part, poff + blockIdx.x);
+}
+// Which product a dense cone takes: k_cgemm2 for cones of at least kC2MinN rows (C5b-size:
+// C streamed once per 128 columns, split over K to fill the chip), k_cgemm below (theta-size:
+// one launch of small tiles).  S from the tile count (about 3 blocks per CU), LRS_CG_SPLIT.
+constexpr int kC2MinN = 2048, kC2FinGrid = 512;
+struct CgPlan { bool big; int S, grid, fin_grid; };
+static CgPlan cg_plan(const DevCone &c, bool scratch) {
+    CgPlan p{false, 1, 0, 0};
+    if (c.n < kC2MinN || getenv("LRS_CG_OLD")) return p;
+    p.big = true;
+    const long tiles = (long)((c.nown + kC2BM - 1) / kC2BM) * ((c.r + kC2BN - 1) / kC2BN);
+    static int env = -2;
+    if (env == -2) { const char *e = getenv("LRS_CG_SPLIT"); env = e ? atoi(e) : -1; }
+    int S = env > 0 ? env : (int)std::max(1L, std::min((long)kCgSplitMax, (1536 + tiles - 1) / tiles));
+    if (!scratch) S = 1;
+    p.S = std::max(1, std::min(kCgSplitMax, S));
+    p.grid = (int)std::min((long)kMaxPartialBlocks, tiles * p.S);
+    p.fin_grid = p.S > 1 ? kC2FinGrid : 0;
+    return p;
+}
 static int cgemm_grid(const DevCone &c) {
     const long tiles = (long)((c.nown + kCgBM - 1) / kCgBM) * ((c.r + kCgBN - 1) / kCgBN);
     return (int)std::max(1L, std::min((long)kCgMaxGrid, tiles));
@@ -4517,15 +4699,33 @@ int launch_dense_cx(const DevProblem &P, int cone, const double *X, double *Y, d
         LRS_CHECK_LAUNCH();
         return 0;
     }
-    hipLaunchKernelGGL(k_cgemm, dim3(cgemm_grid(c)), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld,
-                       P.dense_scale, c.Cd, X + c.foff, Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0);
+    const CgPlan cp = cg_plan(c, P.cgk != nullptr);
+    if (cp.big && cp.S > 1) {
+        hipLaunchKernelGGL((k_cgemm2<true>), dim3(cp.grid), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld,
+                           P.dense_scale, c.Cd, X + c.foff, Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0,
+                           cp.S, P.cgk);
+        LRS_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_cgemm2_fin, dim3(cp.fin_grid), dim3(kBlock), 0, st, c.nown, c.row0, c.r, c.ld, cp.S,
+                           P.dense_scale, P.cgk, X + c.foff, Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0);
+    } else if (cp.big) {
+        hipLaunchKernelGGL((k_cgemm2<false>), dim3(cp.grid), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld,
+                           P.dense_scale, c.Cd, X + c.foff, Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0, 1,
+                           nullptr);
+    } else {
+        hipLaunchKernelGGL(k_cgemm, dim3(cgemm_grid(c)), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld,
+                           P.dense_scale, c.Cd, X + c.foff, Y + c.foff, beta, nullptr, nullptr, nullptr, nullptr, 0);
+    }
     LRS_CHECK_LAUNCH();
     return 0;
 }
 int dense_cd_blocks(const DevProblem &P) {
     int nb = 0;
-    for (const DevCone &c : P.cones)
-        if (c.dense_c) nb += c.dense_c == 2 ? 1 : cgemm_grid(c);
+    for (const DevCone &c : P.cones) {
+        if (!c.dense_c) continue;
+        if (c.dense_c == 2) { nb += 1; continue; }
+        const CgPlan cp = cg_plan(c, P.cgk != nullptr);
+        nb += !cp.big ? cgemm_grid(c) : (cp.S > 1 ? cp.fin_grid : cp.grid);
+    }
     return nb;
 }
 int launch_dense_cd(const DevProblem &P, const DevWork &W, const double *ctrl, int off, hipStream_t st) {
@@ -4538,11 +4738,28 @@ int launch_dense_cd(const DevProblem &P, const DevWork &W, const double *ctrl, i
             off += 1;
             continue;
         }
-        const int grid = cgemm_grid(c);
-        hipLaunchKernelGGL(k_cgemm, dim3(grid), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld, P.dense_scale,
-                           c.Cd, W.D + c.foff, W.CD + c.foff, 0.0, ctrl, W.R + c.foff, W.R2 + c.foff, W.part, off);
+        const CgPlan cp = cg_plan(c, P.cgk != nullptr);
+        if (cp.big && cp.S > 1) {
+            hipLaunchKernelGGL((k_cgemm2<true>), dim3(cp.grid), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld,
+                               P.dense_scale, c.Cd, W.D + c.foff, W.CD + c.foff, 0.0, ctrl, nullptr, nullptr, nullptr,
+                               0, cp.S, P.cgk);
+            LRS_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_cgemm2_fin, dim3(cp.fin_grid), dim3(kBlock), 0, st, c.nown, c.row0, c.r, c.ld, cp.S,
+                               P.dense_scale, P.cgk, W.D + c.foff, W.CD + c.foff, 0.0, ctrl, W.R + c.foff,
+                               W.R2 + c.foff, W.part, off);
+            off += cp.fin_grid;
+        } else if (cp.big) {
+            hipLaunchKernelGGL((k_cgemm2<false>), dim3(cp.grid), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld,
+                               P.dense_scale, c.Cd, W.D + c.foff, W.CD + c.foff, 0.0, ctrl, W.R + c.foff,
+                               W.R2 + c.foff, W.part, off, 1, nullptr);
+            off += cp.grid;
+        } else {
+            const int grid = cgemm_grid(c);
+            hipLaunchKernelGGL(k_cgemm, dim3(grid), dim3(kBlock), 0, st, c.n, c.nown, c.row0, c.r, c.ld, P.dense_scale,
+                               c.Cd, W.D + c.foff, W.CD + c.foff, 0.0, ctrl, W.R + c.foff, W.R2 + c.foff, W.part, off);
+            off += grid;
+        }
         LRS_CHECK_LAUNCH();
-        off += grid;
     }
     return 0;
 }

@@ -478,7 +478,7 @@ static void free_work(lrs_ctx *c) {
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
                       W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2,
-                      W.cgc, W.tot, W.gl, W.CR, W.CD, W.GP};
+                      W.cgc, W.tot, W.gl, W.CR, W.CD, W.GP, W.CGK};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     for (double *q : c->ring_s) if (q) (void)hipFree(q);
@@ -486,6 +486,7 @@ static void free_work(lrs_ctx *c) {
     c->ring_s.clear(); c->ring_y.clear(); c->ring_beta.clear(); c->ring_len = 0;
     c->W = DevWork();
     c->dp.gp = nullptr;
+    c->dp.cgk = nullptr;
     c->walloc = false;
 }
 
@@ -559,6 +560,12 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         W.gl_len = gl;
     }
     if (P.ndense && (A(&W.CR, NR) || A(&W.CD, NR))) return -1;
+    {   // k_cgemm2's split-K slabs for the large dense cones
+        bool big = false;
+        for (const DevCone &dc : P.cones) big = big || (dc.dense_c == 1 && dc.n >= 2048);
+        if (big && A(&W.CGK, (long)kCgSplitSlabs * NR)) return -1;
+        P.cgk = W.CGK;
+    }
     {   // column-tiled long-row kernels: the partial S R_new factors
         bool tiles = false;
         const char *ev = getenv("LRS_TILES");
@@ -3099,6 +3106,14 @@ int lrs_mfma_f64_peak(lrs_ctx *c, double *tflops) {
     if (!c || !tflops) { set_err("mfma_f64_peak: null argument"); return -1; }
     bind(c);
     OPC(mfma_f64_peak(c->st, tflops));
+    return 0;
+}
+
+int lrs_mfma_f64_probe(lrs_ctx *c, int waves_per_simd, int chains, double *tflops, double *mhz,
+                       double *cycles_per_mfma) {
+    if (!c || !tflops) { set_err("mfma_f64_probe: null argument"); return -1; }
+    bind(c);
+    OPC(mfma_f64_probe(c->st, waves_per_simd, chains, tflops, mhz, cycles_per_mfma));
     return 0;
 }
 

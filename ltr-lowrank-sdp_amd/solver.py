@@ -120,6 +120,7 @@ def load_library(path=None):
         "lrs_auut_bytes": (C.c_int, [vp, dp]),
         "lrs_time_gram": (C.c_int, [vp, C.c_int, C.c_int, dp, dp]),
         "lrs_mfma_f64_peak": (C.c_int, [vp, dp]),
+        "lrs_mfma_f64_probe": (C.c_int, [vp, C.c_int, C.c_int, dp, dp, dp]),
         "lrs_time_dense": (C.c_int, [vp, C.c_int, C.c_int, dp]),
         "lrs_load_coo": (C.c_int, [vp, C.c_int, C.c_int, ip, dp, C.c_long, ip, ip, ip, ip, dp]),
         "lrs_debug_phase_times": (C.c_int, [vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
@@ -499,6 +500,14 @@ class Solver:
         t = C.c_double()
         self._check(self.lib.lrs_mfma_f64_peak(self.ctx, C.byref(t)), "mfma_f64_peak")
         return t.value
+
+    def mfma_f64_probe(self, waves_per_simd=4, chains=8):
+        """(TFLOP/s, shader MHz under the load, cycles per MFMA per SIMD) of the FP64 matrix-core
+        probe at the given occupancy (lrs_mfma_f64_probe)."""
+        t, f, cy = C.c_double(), C.c_double(), C.c_double()
+        self._check(self.lib.lrs_mfma_f64_probe(self.ctx, int(waves_per_simd), int(chains), C.byref(t), C.byref(f),
+                                                C.byref(cy)), "mfma_f64_probe")
+        return t.value, f.value, cy.value
 
     def time_auut(self, reps=100):
         ms = C.c_double()

@@ -244,3 +244,24 @@ def test_sharded_dense_objective_solve_matches_single_gpu(solver_mod, gen_dir):
         assert abs(first[k] - ref[k]) <= tol * (1 + abs(ref[k])), (k, first[k], ref[k], tol)
     assert first["final_rank"] == ref["final_rank"] and first["status"] == ref["status"]
     assert first["dinf"] >= 0
+
+
+@pytest.mark.parametrize("split", ["1", "3", "auto"])
+def test_split_k_cgemm_per_trip_at_n2500(solver_mod, gen_dir, split, monkeypatch):
+    """k_cgemm2 (dense cones of >= 2048 rows: full-width 32 x 128 output tiles, split over K
+    into slabs that k_cgemm2_fin adds in slab order) against the slot path, K = 1..3 trips at
+    n = 2500, r = 96 (tau, R_K, G_K to 1e-9): S = 1 (fused epilogue), S = 3 and the size rule;
+    the ADMM / objective products through the same kernels (final objectives within 1e-6)."""
+    path = _rdense(gen_dir, 2500, 60000, 6, 11)
+    if split != "auto":
+        monkeypatch.setenv("LRS_CG_SPLIT", split)
+    out = {}
+    for mode in ("0", "1"):
+        with dense_mode(mode):
+            sv = solver_mod.Solver(path)
+        out[mode] = [sv.alm_steps(K, reoptLevel=0, fixedRank=96) for K in (1, 2, 3)]
+        sv.close()
+    for a, b in zip(out["0"], out["1"]):
+        assert abs(a["tau"] - b["tau"]) <= TOL * abs(a["tau"]), (a["tau"], b["tau"])
+        for key in ("R", "G"):
+            assert rel_err(a[key], b[key]) < TOL, (key, rel_err(a[key], b[key]))
