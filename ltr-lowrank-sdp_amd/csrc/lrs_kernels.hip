@@ -334,7 +334,20 @@ __global__ void __launch_bounds__(kBlock) k_gather(int m, int K, int cone, const
         for (int k = k0; k < k1; ++k) {
             const long row = (long)k * m + i;
             double v = 0.0;
-            for (int e = con_ptr[row]; e < con_ptr[row + 1]; ++e) v += con_w[e] * uvt[con_slot[e]];
+            int e = con_ptr[row];
+            const int e1 = con_ptr[row + 1];
+            // long rows (a trace constraint): eight entries' loads in flight, the sum in entry order
+            for (; e + 8 <= e1; e += 8) {
+                int sl[8];
+                double w[8], u[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) { sl[t] = con_slot[e + t]; w[t] = con_w[e + t]; }
+#pragma unroll
+                for (int t = 0; t < 8; ++t) u[t] = uvt[sl[t]];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v += w[t] * u[t];
+            }
+            for (; e < e1; ++e) v += con_w[e] * uvt[con_slot[e]];
             tot += v;
         }
         tot *= scale;
@@ -4372,8 +4385,10 @@ int mfma_f64_probe(hipStream_t st, int wps, int chains, double *tflops, double *
     *tflops = flop / (ms * 1e-3) / 1e12;
     const double wall_s = h[1] * 1e-8;   // 100 MHz
     if (mhz) *mhz = wall_s > 0 ? h[0] / wall_s / 1e6 : 0.0;
-    // a SIMD runs wps waves (one per block): its MFMA count over the block-0 wave's span
-    if (cyc_per_mfma) *cyc_per_mfma = (double)h[0] / ((double)std::max(1, std::min(8, wps)) * iters * ch);
+    // a SIMD runs one wave of each of its CU's blocks: its MFMA count over the launch, in
+    // cycles of the measured clock
+    const double per_simd = (double)blocks / num_cus() * iters * ch;
+    if (cyc_per_mfma) *cyc_per_mfma = (mhz && *mhz > 0) ? ms * 1e-3 * (*mhz * 1e6) / per_simd : 0.0;
     return 0;
 }
 int mfma_f64_peak(hipStream_t st, double *tflops) { return mfma_f64_probe(st, 2, 8, tflops, nullptr, nullptr); }
