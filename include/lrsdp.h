@@ -238,12 +238,15 @@ int lrs_debug_phase_times(lrs_ctx *ctx, unsigned long long *out, unsigned long l
  * every process loads the whole problem (lrs_load_sdpa / lrs_load_coo), then calls one
  * lrs_shard_* with its rank; the context then owns a contiguous block of rows (+ the
  * halo of neighbour rows) and the constraints inside it, and lrs_solve /
- * lrs_alm_throughput run the ALM phase (the unit of the metric) with, per inner
- * iteration, one halo exchange of direction rows and two all-reduces of the stage
- * totals (line search; L-BFGS dots + residual).  One SDP cone; every constraint's
- * entries inside one row block (MaxCut's e_i e_i^T).  The ADMM phase is not sharded
- * (lrs_solve stops after the ALM phase).  Every shard must make the same calls in the
- * same order (the collectives are matched by order). */
+ * lrs_alm_throughput run whole solves (ALM + ADMM + reopt rounds + the dual
+ * infeasibility) with, per inner iteration, one halo exchange of direction rows and
+ * all-reduces of the stage totals (line search; L-BFGS dots + residual; shared
+ * constraints' sums).  Any number of SDP cones, each split alike; constraints may span row
+ * blocks (shared: every holder sums its owned entries, the sums meet in an all-reduce);
+ * a dense objective is held as each shard's owned row block of C with every row in the
+ * halo.  The ADMM CG runs on owned rows with its dot products all-reduced; the Lanczos
+ * of the dual infeasibility on owned rows with a vector halo.  DESIGN.md §6.  Every shard
+ * must make the same calls in the same order (the collectives are matched by order). */
 /* RCCL: rank 0 creates the id (128 bytes) and broadcasts it; every rank then calls
  * lrs_shard_rccl on its own GPU (ncclCommInitRank is collective). */
 int lrs_comm_unique_id(char *id_out);
