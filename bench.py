@@ -23,7 +23,8 @@ Prints one JSON line (rank 0).  Besides the contract keys:
                     timed on this host, 1 core, on a bounded sample of the workload
   config_c5         BASELINE config C5 (random sparse SDP n = 1e4, m = 1e6, r = 128): ALM it/s
                     and the r x r Gram on the FP64 matrix cores (TFLOP/s vs the MFMA peak)
-  sharded           ONE G81-like instance (n = 20 000, r = 64) row-sharded over all N ranks
+  sharded           ONE G81-like instance (n = 20 000, r = 64) row-sharded over all N ranks;
+                    at N > 1 also C5 (n = 1e4, m = 1e6, r = 128) and the 2000^2 torus
                     (RCCL: halo exchange of direction rows + all-reduced stage totals per
                     inner iteration): strong-scaling it/s of the single instance
 """
@@ -312,30 +313,65 @@ def c5_cpu_sample(solver, local, seconds, cache):
 
 
 def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=500):
-    """ONE G81-like instance (torus 100 x 200, n = 20 000, r = 64) row-sharded over the
-    `world` ranks through RCCL (lrs_shard_rccl): whole-instance ALM it/s, strong scaling."""
-    p81 = instance_for(0, 100, 200, cache, seed0=81)
-    sv = solver.Solver(p81, device=local)
+    """ONE instance row-sharded over the `world` ranks through RCCL (lrs_shard_rccl): whole-
+    instance ALM it/s, strong scaling.  The G81-like torus (n = 20 000, r = 64) always; at
+    world > 1 also BASELINE config C5 (n = 10^4, m = 10^6, r = 128, the 2-D tile kernels on each
+    shard's owned rows, every row in every halo) and the 2000 x 2000 torus (n = 4*10^6, r = 16),
+    whose one-GPU rates are config_c5.gpu_it_s and roofline_at_scale.it_s of the N = 1 line."""
+    inst = importlib.import_module(PKG + ".instances")
     uid = solver.comm_unique_id() if rank_id == 0 else None
     if dist is not None:
         box = [uid]
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
-    sv.shard_rccl(world, rank_id, uid)
-    info = sv.shard_info()
-    kw = dict(fixedRank=64, reoptLevel=0)
-    sv.alm_throughput(0, 50, **kw)
-    replicas.barrier_sync(dist)
-    t0 = time.perf_counter()
-    out = sv.alm_throughput(0, steps, **kw)
-    replicas.barrier_sync(dist)
-    dt = time.perf_counter() - t0
-    sv.close()
-    _, t_max = replicas.aggregate(dist, out["done"], dt)
-    return {"workload": "MaxCut torus 100x200 (G81 structure), n=m=20000, --fixedRank 64, ONE instance "
-                        f"row-sharded over {world} GPU(s)", "it_s": out["done"] / t_max, "steps": out["done"],
-            "n_gpus": world, "scaling": "strong", "transport": "RCCL (ncclSend/Recv halo, ncclAllReduce totals)",
-            "rank0_rows": info[3], "rank0_halo_rows": info[4]}
+    legs = [("g81", 50, steps)]
+    if world > 1:
+        legs += [("c5", 3, 20), ("torus2000", 5, 40)]
+    out = {}
+    for name, warm, k in legs:
+        t0 = time.perf_counter()
+        if name == "g81":
+            sv = solver.Solver(instance_for(0, 100, 200, cache, seed0=81), device=local)
+            kw = dict(fixedRank=64, reoptLevel=0)
+            wl = "MaxCut torus 100x200 (G81 structure), n=m=20000, --fixedRank 64"
+        elif name == "c5":
+            sv = solver.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(10000, 1000000, 6, 5)), device=local)
+            kw = dict(fixedRank=128, reoptLevel=0)
+            wl = "random sparse SDP n=1e4, m=1e6, 6 entries/constraint, C=I, --fixedRank 128 (BASELINE C5)"
+        else:
+            sv = solver.Solver(coo=inst.coo_arrays(inst.maxcut_torus_problem(2000, 2000, 2000)), device=local)
+            kw = dict(fixedRank=16, reoptLevel=0)
+            wl = "MaxCut torus 2000x2000, n=m=4e6, --fixedRank 16"
+        sv.shard_rccl(world, rank_id, uid)
+        info = sv.shard_info()
+        tiles = sv.tile_info()
+        load_s = time.perf_counter() - t0
+        clock = {}
+
+        def on_start():
+            sv.sync()
+            replicas.barrier_sync(dist)
+            clock["t0"] = time.perf_counter()
+
+        def on_stop():
+            sv.sync()
+            replicas.barrier_sync(dist)
+            clock["t1"] = time.perf_counter()
+
+        o = sv.alm_timed(warm, k, on_start, on_stop, **kw)
+        used = sv.tile_used()
+        sv.close()
+        _, t_max = replicas.aggregate(dist, o["done"], clock["t1"] - clock["t0"])
+        out[name] = {"workload": f"{wl}, ONE instance row-sharded over {world} GPU(s)", "it_s": o["done"] / t_max,
+                     "steps": o["done"], "n_gpus": world, "scaling": "strong", "load_sec": load_s,
+                     "rank0_rows": info[3], "rank0_halo_rows": info[4], "slot_tiles_built": bool(tiles[1]),
+                     "tile_kernels_ran": used}
+    res = dict(out["g81"])
+    res["transport"] = "RCCL (ncclSend/Recv halo, ncclAllReduce totals)"
+    for name in ("c5", "torus2000"):
+        if name in out:
+            res[name] = out[name]
+    return res
 
 
 def main():
@@ -355,7 +391,7 @@ def main():
     ap.add_argument("--no-c5", action="store_true")
     ap.add_argument("--no-c5b", action="store_true")
     ap.add_argument("--no-sharded", action="store_true")
-    ap.add_argument("--sharded-timeout", type=float, default=300.0)
+    ap.add_argument("--sharded-timeout", type=float, default=600.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

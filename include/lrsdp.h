@@ -216,6 +216,9 @@ int lrs_load_coo(lrs_ctx *ctx, int m, int nblk, const int *dims, const double *b
  * reference counterpart (the reference's 10 % dense rule picks a BLAS-3 branch instead,
  * data/lorads_sdp_data.c:1187-1193). */
 int lrs_tile_info(lrs_ctx *ctx, int *auv, int *slot);
+/* *used = 1 when the last enqueued ALM iteration ran its stages over those tiles (k_tile_a,
+ * k_tile_b1/b2: the stage plan picked the long-row kernels for a tiled cone), else 0. */
+int lrs_tile_used(lrs_ctx *ctx, int *used);
 
 /* Algorithmic HBM bytes per launch of the split-iteration stages A, G, B at the
  * current ranks (the roofline numerators, DESIGN.md "Kernels"). */

@@ -130,10 +130,19 @@ struct DevCone {
     // stage B's gradient S R_new over the symmetric pattern in the same tiles (k_tile_b2): one
     // block per (row tile I, column group x of kNX), its tile pairs {col0, row-pointer offset}
     // ([nt * kNX][2] ranges into sb_tp), per tile pair kAuvT + 1 row pointers into the entries
-    // {local column, slot}; sa_S holds the slot values of S = C + A^*(M1) between the two kernels
+    // {local column, slot}; sb_S holds S = C + A^*(M1) in that entry order between the two
+    // kernels (stage B writes each slot's value at its entries' places sb_pos[slot] = {lower
+    // row's, upper row's}, -1 where the row is not tiled here)
     int sb_blocks = 0;
-    int *sb_blk = nullptr, *sb_tp = nullptr, *sb_rp = nullptr, *sb_ent = nullptr;
-    double *sa_S = nullptr;
+    int *sb_blk = nullptr, *sb_tp = nullptr, *sb_rp = nullptr, *sb_ent = nullptr, *sb_pos = nullptr;
+    long sb_nnz = 0;
+    double *sb_S = nullptr;
+    // sharded solve: the tiles cover the owned rows only -- sa_* the owned rows' lower slots,
+    // sb_* the row tiles from sb_I0 on; sx_slot the slots whose lower row is a halo row (the
+    // upper entries of owned rows), whose S k_slot_sv forms for k_tile_b2
+    int sb_I0 = 0;
+    int sx_n = 0;
+    int *sx_slot = nullptr;
 };
 constexpr int kMaxRankLd = 512;      // widest factor row (choose_layout: 64 lanes x 8 doubles)
 constexpr int kAuvT = 128;           // rows of one side of an A(X Y^T) tile
@@ -169,6 +178,7 @@ struct DevProblem {
     int no_lat = 0;                      // kernel path (lrs_set_kernel_path): 1 never the latency kernels, 2 + bandwidth regime, 3 + long-row kernels, 4 the single-workgroup inner loop
     int *slot_g = nullptr;               // [Ptot][2] every slot's (row, col) in the all-cones row space
     mutable int last_path = -1;          // path of the last enqueued iteration (0 lat, 1 general)
+    mutable int last_tiles = 0;          // the last enqueued iteration ran stage A / B over the 2-D tiles
     int m = 0, K = 0;
     long NRpad = 0;     // factor buffer length (doubles)
     int Ptot = 0;
@@ -361,6 +371,8 @@ int launch_pack_rows(int nrows, int ld, const int *rows, const double *src, doub
 int sync_shared(const DevProblem &P, double *v, hipStream_t st);
 // fold one scalar's per-block partials into out[0] (sharded CG, before its all-reduce)
 int launch_fold1(const double *part, int nblk, double *out, hipStream_t st);
+// par[P_NPAR] and ctl[C_NCTRL] (host arrays) into dpar / dctl, stream-ordered, as one launch
+int launch_put_ctrl(const double *par, const double *ctl, double *dpar, double *dctl, hipStream_t st);
 int launch_sum_shards(int n, int world, const double *const *src, double *out, hipStream_t st);
 
 const char *last_device_error();

@@ -16,6 +16,7 @@
 //   k_spmm       mul_rk                        data/lorads_sdp_data.c:750-763
 //   ALM fused iteration (device control)     lorads_alg/lorads_alm.c:1302-1379
 #include <hip/hip_runtime.h>
+#include <utility>
 
 #include <cmath>
 #include <cstdio>
@@ -562,12 +563,14 @@ constexpr int kAuvS = kAuvC + 2;   // LDS row stride (doubles; 16-B aligned rows
 // is computed: auv_fetch into registers, auv_put into LDS (after a barrier).
 constexpr int kAuvPer = kAuvT * kAuvC / 2 / kAuvThreads;   // double2 per thread per operand
 static_assert(kAuvPer * kAuvThreads * 2 == kAuvT * kAuvC, "tile staging divides evenly");
-template <int NA>
-__device__ __forceinline__ void auv_fetch(double2 (&v)[NA][kAuvPer], int I0, int J0, int c0, int n, int r, int ld,
-                                          const double *__restrict__ X, const double *__restrict__ Y) {
+template <int NT>
+constexpr int auv_per() { return kAuvT * kAuvC / 2 / NT; }   // double2 per thread per operand, NT threads
+template <int NA, int NT = kAuvThreads>
+__device__ __forceinline__ void auv_fetch(double2 (&v)[NA][auv_per<NT>()], int I0, int J0, int c0, int n, int r,
+                                          int ld, const double *__restrict__ X, const double *__restrict__ Y) {
 #pragma unroll
-    for (int k = 0; k < kAuvPer; ++k) {
-        const int x = threadIdx.x + k * kAuvThreads;
+    for (int k = 0; k < auv_per<NT>(); ++k) {
+        const int x = threadIdx.x + k * NT;
         const int row = x / (kAuvC / 2), col = c0 + 2 * (x % (kAuvC / 2));
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
@@ -582,11 +585,11 @@ __device__ __forceinline__ void auv_fetch(double2 (&v)[NA][kAuvPer], int I0, int
         }
     }
 }
-template <int NA>
-__device__ __forceinline__ void auv_put(double (*tl)[kAuvT * kAuvS], const double2 (&v)[NA][kAuvPer]) {
+template <int NA, int NT = kAuvThreads>
+__device__ __forceinline__ void auv_put(double (*tl)[kAuvT * kAuvS], const double2 (&v)[NA][auv_per<NT>()]) {
 #pragma unroll
-    for (int k = 0; k < kAuvPer; ++k) {
-        const int x = threadIdx.x + k * kAuvThreads;
+    for (int k = 0; k < auv_per<NT>(); ++k) {
+        const int x = threadIdx.x + k * NT;
         const int o = (x / (kAuvC / 2)) * kAuvS + 2 * (x % (kAuvC / 2));
 #pragma unroll
         for (int a = 0; a < NA; ++a) *reinterpret_cast<double2 *>(&tl[a][o]) = v[a][k];
@@ -3050,7 +3053,8 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_a(
 // every lane group gathering ~570 neighbour rows of R and D per row.  The per-slot epilogue
 // (slot values, C and local-constraint terms, rec) is k_wide_a's.  Same grid and partial
 // slots as k_wide_a (blocks stride over the items), so the consumers are unchanged.
-__global__ void __launch_bounds__(kRowBlock) k_tile_a(
+template <int NT>
+__global__ void __launch_bounds__(NT) k_tile_a(
     int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
     const int *__restrict__ tslot, const double *__restrict__ Cw, const double *__restrict__ Rb0,
     const double *__restrict__ Rb1, const double *__restrict__ Dall, double *__restrict__ uRD,
@@ -3058,7 +3062,8 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_a(
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     const double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec,
     const double *__restrict__ par, const double *__restrict__ ctrl_cur, double *__restrict__ partA, int pblk_off) {
-    static_assert(kRowBlock == kAuvThreads, "k_tile_a runs the A(X Y^T) tile layout");
+    constexpr int NPT = kAuvItem / NT;   // slots per thread of one item
+    static_assert(NPT * NT == kAuvItem, "k_tile_a: items divide over the block");
     if (ctrl_cur[C_ACTIVE] == 0.0) return;
     const double *__restrict__ R = (ctrl_cur[C_RCUR] == 0.0 ? Rb0 : Rb1) + foff;
     const double *__restrict__ D = Dall + foff;
@@ -3068,11 +3073,11 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_a(
     for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
         const int4 it = items[itx];
         const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
-        int pl[kAuvNpt], ql[kAuvNpt];
-        double s0[kAuvNpt], s1[kAuvNpt];
+        int pl[NPT], ql[NPT];
+        double s0[NPT], s1[NPT];
 #pragma unroll
-        for (int j = 0; j < kAuvNpt; ++j) {
-            const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+        for (int j = 0; j < NPT; ++j) {
+            const int t = eb + (int)threadIdx.x + j * NT;
             const unsigned w = t < ee ? pq[t] : 0u;
             pl[j] = (int)(w >> 16) * kAuvS;
             ql[j] = (int)(w & 0xffffu) * kAuvS;
@@ -3080,20 +3085,20 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_a(
             s1[j] = 0.0;
         }
         for (int c0 = 0; c0 < r; c0 += kAuvC) {
-            double2 v[4][kAuvPer];
-            auv_fetch<4>(v, I0, J0, c0, n, r, ld, R, D);
+            double2 v[4][auv_per<NT>()];
+            auv_fetch<4, NT>(v, I0, J0, c0, n, r, ld, R, D);
             __syncthreads();
-            auv_put<4>(tl, v);
+            auv_put<4, NT>(tl, v);
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < kAuvNpt; ++j) {
-                if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
+            for (int j = 0; j < NPT; ++j) {
+                if (eb + (int)threadIdx.x + j * NT >= ee) break;
                 auv_chunk<2>(tl, pl[j], ql[j], s0[j], s1[j]);
             }
         }
 #pragma unroll
-        for (int j = 0; j < kAuvNpt; ++j) {
-            const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+        for (int j = 0; j < NPT; ++j) {
+            const int t = eb + (int)threadIdx.x + j * NT;
             if (t >= ee) break;
             const int sl = tslot[t];
             const double d0 = 0.5 * s0[j], d1 = s1[j];
@@ -3120,7 +3125,7 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_a(
             }
         }
     }
-    write_partials_range<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x, 0, 7);
+    write_partials_range<8, NT>(acc, partA, pblk_off + blockIdx.x, 0, 7);
 }
 
 // row epilogue of stage B: G_new = 2 (S R_new [+ C R_new]), s = tau D, y = G_new - G_old
@@ -3298,10 +3303,10 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
 //   J of its group in LDS, 64 columns at a time, and thread (row, quarter) sums S_ij R_new,j
 //   over its row's entries of the tile pair in column order, 16 columns at a time, into GP[x];
 // k_wide_bf sums the kNX partial rows in group order and runs the row epilogue.
-__global__ void __launch_bounds__(kRowBlock) k_tile_b1(
+__global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: two blocks a CU (68 KB LDS each)
     int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
     const int *__restrict__ tslot, const double *Rb0, const double *Rb1, double *__restrict__ uRR,
-    double *__restrict__ Sv, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
+    double *__restrict__ SE, const int2 *__restrict__ spos, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
     const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double2 *__restrict__ slot1,
     const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
@@ -3338,20 +3343,47 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b1(
                 auv_chunk<1>(tl, pl[j], ql[j], dv[j], unused);
             }
         }
+        // the slot epilogue, kB1H slots at a time with their loads issued before the arithmetic
+        // (branch-free indices: entries past the item read the item's first slot, store nothing)
+        constexpr int kB1H = 4;
 #pragma unroll
-        for (int j = 0; j < kAuvNpt; ++j) {
-            const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+        for (int h = 0; h < kAuvNpt; h += kB1H) {
+        int slv[kB1H];
+        double2 s1v[kB1H], l1v[kB1H];
+        double crv[kB1H];
+        int2 psv[kB1H];
+#pragma unroll
+        for (int j = 0; j < kB1H; ++j) {
+            const int t = eb + (int)threadIdx.x + (h + j) * kAuvThreads;
+            slv[j] = tslot[t < ee ? t : eb];
+        }
+#pragma unroll
+        for (int j = 0; j < kB1H; ++j) {
+            s1v[j] = slot1[slv[j]];
+            l1v[j] = loc1[slv[j]];
+            crv[j] = Craw[slv[j]];
+            psv[j] = spos[slv[j]];
+        }
+        double2 rav[kB1H], rbv[kB1H];
+#pragma unroll
+        for (int j = 0; j < kB1H; ++j) {
+            const int c1 = (int)s1v[j].y;
+            const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * (c1 >= 0 ? c1 : 0));
+            rav[j] = q[0];
+            rbv[j] = q[1];
+        }
+#pragma unroll
+        for (int j = 0; j < kB1H; ++j) {
+            const int t = eb + (int)threadIdx.x + (h + j) * kAuvThreads;
             if (t >= ee) break;
-            const int sl = tslot[t];
-            double svl = Craw[sl];
-            const double2 s1l = slot1[sl];
+            const int sl = slv[j];
+            double svl = crv[j];
+            const double2 s1l = s1v[j];
             const int c1 = (int)s1l.y;
             if (c1 >= 0) {
-                const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * c1);
-                const double2 ra = q[0], rb = q[1];
-                double cv = ra.x + tau * ra.y;
-                cv = cv + tau2 * rb.x;
-                svl += (rb.y + rho * cv) * s1l.x;
+                double cv = rav[j].x + tau * rav[j].y;
+                cv = cv + tau2 * rbv[j].x;
+                svl += (rbv[j].y + rho * cv) * s1l.x;
             } else if (c1 == -2) {
                 for (int e = slot_ptr[sl]; e < slot_ptr[sl + 1]; ++e) {
                     const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
@@ -3361,10 +3393,11 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b1(
                     svl += (y.y + rho * cv) * slot_a[e];
                 }
             }
-            Sv[sl] = svl;
-            const double d = dv[j];
+            if (psv[j].x >= 0) SE[psv[j].x] = svl;
+            if (psv[j].y >= 0) SE[psv[j].y] = svl;
+            const double d = dv[h + j];
             uRR[sl] = d;
-            const double2 l1l = loc1[sl];
+            const double2 l1l = l1v[j];
             const int cl = (int)l1l.y;
             const int f0 = cl == -2 ? loc_ptr[sl] : 0, f1 = cl == -2 ? loc_ptr[sl + 1] : (cl >= 0 ? 1 : 0);
             for (int e = f0; e < f1; ++e) {
@@ -3375,6 +3408,7 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b1(
                 acc[9] += dd * dd;
             }
         }
+        }
     }
     write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
 }
@@ -3382,6 +3416,8 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b1(
 constexpr int kTbC = 64;            // R_new columns staged per pass in k_tile_b2
 constexpr int kTbS = kTbC + 2;      // LDS row stride (16-B aligned rows)
 constexpr int kTbPer = kAuvT * kTbC / 2 / kRowBlock;   // double2 per thread per staged tile
+constexpr int kTbL = 16;            // lanes per tile row in k_tile_b2 (one 256-B LDS row read per 16 lanes)
+constexpr int kTbRows = kAuvT / (kRowBlock / kTbL);     // tile rows per lane group
 __device__ __forceinline__ void tb_fetch(double2 (&v)[kTbPer], int J0, int c0, int n, int r, int ld,
                                          const double *__restrict__ Rn) {
 #pragma unroll
@@ -3396,34 +3432,77 @@ __device__ __forceinline__ void tb_fetch(double2 (&v)[kTbPer], int J0, int c0, i
         v[k] = t;
     }
 }
+// Row broadcast (DPP row_newbcast, gfx90a+): every lane of each 16-lane row gets lane K's value.
+template <int K>
+__device__ __forceinline__ int nbc_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0x150 + K, 0xF, 0xF, false); }
+// one entry of a k_tile_b2 row batch: column and S from lane K of the lane group, the staged
+// neighbour row's two 16-B pieces of this lane, four FMAs
+template <int K>
+__device__ __forceinline__ void b2_entry(const double *rj, int l, int colv, double sv, double (&g)[4]) {
+    const int j = nbc_i<K>(colv);
+    const double s = dpp_mov<0x150 + K>(sv);
+    const double2 *p = reinterpret_cast<const double2 *>(&rj[j * kTbS]) + l;
+    const double2 a0 = p[0], a1 = p[kTbL];
+    g[0] += s * a0.x; g[1] += s * a0.y; g[2] += s * a1.x; g[3] += s * a1.y;
+}
+template <int... K>
+__device__ __forceinline__ void b2_batch(std::integer_sequence<int, K...>, int kmax, const double *rj, int l, int colv,
+                                         double sv, double (&g)[4]) {
+    ((K < kmax ? b2_entry<K>(rj, l, colv, sv, g) : void()), ...);
+}
 // grid: (row tile I, column group x) x column chunk; the chunk's kTbC columns of each tile
-// pair's R_new staged in LDS (the next pair's loads in flight during the current one).
+// pair's R_new staged in LDS (the next pair's loads in flight during the current one).  A lane
+// group of kTbL lanes takes kTbRows rows of the tile; lane l holds the chunk's columns 2l, 2l+1,
+// 32+2l, 33+2l, so the group's two ds_read_b128 of a neighbour row read it whole, 256 B each
+// (no bank conflicts, whatever the row).  A row's entries come 16 at a time, lane k loading
+// entry k's column and S (SE: S in the tile-pair entry order, written by stage B's slot
+// kernels; coalesced, no dependent loads), and the group walks them with a DPP row broadcast
+// of lane k.  Each column's sum runs over the row's entries in column order, tile pair by tile
+// pair.
 __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff, const int2 *__restrict__ blk,
                                                        const int2 *__restrict__ tp, const int *__restrict__ rp,
-                                                       const int2 *__restrict__ ent, const double *__restrict__ Sv,
+                                                       const int2 *__restrict__ ent, const double *__restrict__ SE,
                                                        const double *Rb0, const double *Rb1, double *__restrict__ GP,
                                                        long gstride, int r, const double *__restrict__ ctrl,
-                                                       const double *__restrict__ ls_cur) {
-    static_assert(kRowBlock == 4 * kAuvT, "k_tile_b2: four threads per tile row");
+                                                       const double *__restrict__ ls_cur, int tI0) {
+    static_assert(kTbC == 4 * kTbL && kTbL == 16, "k_tile_b2: four columns per lane, 16-lane DPP rows");
     // ctrl == nullptr: the standalone S X of launch_spmm (X in Rb0)
     if (ctrl && (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0)) return;
     const double *__restrict__ Rn = ((ctrl && ctrl[C_RCUR] == 0.0) ? Rb1 : Rb0) + foff;
+    const int *__restrict__ ecol = reinterpret_cast<const int *>(ent);
     __shared__ double rj[kAuvT * kTbS];
     const int nch = (ld + kTbC - 1) / kTbC;
     const int bx = blockIdx.x / nch, c0 = (blockIdx.x % nch) * kTbC;
-    const int I = bx / kNX, x = bx % kNX;
-    const int pl = threadIdx.x >> 2, cq = threadIdx.x & 3;
-    const int i = I * kAuvT + pl;
+    const int I = tI0 + bx / kNX, x = bx % kNX;   // tI0: a shard's first owned row tile
+    const int grp = threadIdx.x / kTbL, l = threadIdx.x % kTbL;
     const int2 br = blk[bx];
-    double g[16];
+    double g[kTbRows][4];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) g[c] = 0.0;
+    for (int w = 0; w < kTbRows; ++w)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) g[w][c] = 0.0;
     double2 pre[kTbPer];
     int2 t = br.x < br.y ? tp[br.x] : make_int2(0, 0);
     if (br.x < br.y) tb_fetch(pre, t.x, c0, n, r, ld, Rn);
     for (int q = br.x; q < br.y; ++q) {   // block-uniform
         const int2 cur = t;
         if (q + 1 < br.y) t = tp[q + 1];
+        // this tile pair's row ranges and first 16 entries of each row, in flight over the staging
+        int e0[kTbRows], e1[kTbRows], cv[kTbRows];
+        double sv[kTbRows];
+#pragma unroll
+        for (int w = 0; w < kTbRows; ++w) {
+            const int pl = grp + w * (kRowBlock / kTbL);
+            e0[w] = rp[cur.y + pl];
+            e1[w] = rp[cur.y + pl + 1];
+        }
+#pragma unroll
+        for (int w = 0; w < kTbRows; ++w) {
+            const int e = e0[w] + l;
+            const bool ok = e < e1[w];
+            cv[w] = ecol[2L * (ok ? e : e0[w] < e1[w] ? e0[w] : 0)];
+            sv[w] = ok ? SE[e] : 0.0;
+        }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < kTbPer; ++k) {
@@ -3432,27 +3511,77 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
         }
         __syncthreads();
         if (q + 1 < br.y) tb_fetch(pre, t.x, c0, n, r, ld, Rn);
-        const int e1 = rp[cur.y + pl + 1];
-        // a thread's columns interleave with its row's three other threads (16-B chunks cq,
-        // cq + 4, ...): the four read 64 contiguous bytes per step, four distinct 16-B LDS slots
-        // (column quarters 256 B apart would put cq and cq + 2 on one bank)
-        for (int e = rp[cur.y + pl]; e < e1; ++e) {
-            const int2 en = ent[e];
-            const double s = Sv[en.y];
-            const double2 *src = reinterpret_cast<const double2 *>(&rj[en.x * kTbS]) + cq;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const double2 v = src[4 * c];
-                g[2 * c] += s * v.x;
-                g[2 * c + 1] += s * v.y;
+        for (int w = 0; w < kTbRows; ++w) {
+            int base = e0[w], colv = cv[w];
+            double s = sv[w];
+            for (;;) {   // wave-uniform: batches of 16 until the wave's longest row is done
+                int rem = e1[w] - base;
+                rem = rem < 0 ? 0 : (rem > kTbL ? kTbL : rem);
+                const int kmax = max(max(__builtin_amdgcn_readlane(rem, 0), __builtin_amdgcn_readlane(rem, 16)),
+                                     max(__builtin_amdgcn_readlane(rem, 32), __builtin_amdgcn_readlane(rem, 48)));
+                b2_batch(std::make_integer_sequence<int, kTbL>{}, kmax, rj, l, colv, s, g[w]);
+                if (kmax < kTbL) break;
+                base += kTbL;
+                const int e = base + l;
+                const bool ok = e < e1[w];
+                colv = ok ? ecol[2L * e] : 0;
+                s = ok ? SE[e] : 0.0;
             }
         }
     }
-    if (i < n) {
-        double2 *dst = reinterpret_cast<double2 *>(GP + x * gstride + foff + (long)i * ld + c0) + cq;
 #pragma unroll
-        for (int c = 0; c < 8; ++c)
-            if (c0 + 2 * (cq + 4 * c) < ld) dst[4 * c] = make_double2(g[2 * c], g[2 * c + 1]);
+    for (int w = 0; w < kTbRows; ++w) {
+        const int i = I * kAuvT + grp + w * (kRowBlock / kTbL);
+        if (i < n) {
+            double2 *dst = reinterpret_cast<double2 *>(GP + x * gstride + foff + (long)i * ld + c0) + l;
+            if (c0 + 2 * l < ld) dst[0] = make_double2(g[w][0], g[w][1]);
+            if (c0 + 2 * (l + kTbL) < ld) dst[kTbL] = make_double2(g[w][2], g[w][3]);
+        }
+    }
+}
+// launch_spmm: a slot-ordered S into the tile-pair entry order
+__global__ void __launch_bounds__(kBlock) k_gather_se(long nnz, const int2 *__restrict__ ent,
+                                                      const double *__restrict__ S, double *__restrict__ SE) {
+    for (long e = blockIdx.x * (long)kBlock + threadIdx.x; e < nnz; e += (long)gridDim.x * kBlock)
+        SE[e] = S[ent[e].y];
+}
+
+// Sharded long-row B over the tiles: S = C + A^*(M1) (k_tile_b1's slot epilogue, lorads_alm.c:38-57)
+// on the slots whose lower row is a halo row -- k_tile_b2 reads them as owned rows' upper entries;
+// their A(R_new R_new^T) belongs to the shard owning the lower row.
+__global__ void __launch_bounds__(kBlock) k_slot_sv(int nx, const int *__restrict__ sx, double *__restrict__ SE,
+                                                    const int2 *__restrict__ spos,
+                                                    const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
+                                                    const int *__restrict__ slot_con, const double *__restrict__ slot_a,
+                                                    const double2 *__restrict__ slot1, const double *__restrict__ rec,
+                                                    const double *__restrict__ par, const double *__restrict__ ctrl,
+                                                    const double *__restrict__ ls_cur) {
+    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
+    const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
+    for (int t = blockIdx.x * kBlock + threadIdx.x; t < nx; t += gridDim.x * kBlock) {
+        const int sl = sx[t];
+        double svl = Craw[sl];
+        const double2 s1l = slot1[sl];
+        const int c1 = (int)s1l.y;
+        if (c1 >= 0) {
+            const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * c1);
+            const double2 ra = q[0], rb = q[1];
+            double cv = ra.x + tau * ra.y;
+            cv = cv + tau2 * rb.x;
+            svl += (rb.y + rho * cv) * s1l.x;
+        } else if (c1 == -2) {
+            for (int e = slot_ptr[sl]; e < slot_ptr[sl + 1]; ++e) {
+                const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
+                const double2 x = q[0], y = q[1];
+                double cv = x.x + tau * x.y;
+                cv = cv + tau2 * y.x;
+                svl += (y.y + rho * cv) * slot_a[e];
+            }
+        }
+        const int2 ps = spos[sl];
+        if (ps.x >= 0) SE[ps.x] = svl;
+        if (ps.y >= 0) SE[ps.y] = svl;
     }
 }
 
@@ -4261,10 +4390,13 @@ int launch_spmm(const DevProblem &P, int cone, const double *S, const double *X,
     if (c.sb_blocks > 0 && P.gp && !P.shard) {
         // long-row cone: S X per (row tile, column group) from staged X tiles into P.gp's kNX
         // partial rows (k_tile_b2 without the iteration's control), then the sum and epilogue
+        hipLaunchKernelGGL(k_gather_se, dim3(std::min(grid_elems(c.sb_nnz, 4), 4096)), dim3(kBlock), 0, st, c.sb_nnz,
+                           reinterpret_cast<const int2 *>(c.sb_ent), S, c.sb_S);
+        LRS_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_tile_b2, dim3(c.sb_blocks * ((c.ld + kTbC - 1) / kTbC)), dim3(kRowBlock), 0, st, c.n,
                            c.ld, c.foff, reinterpret_cast<const int2 *>(c.sb_blk),
                            reinterpret_cast<const int2 *>(c.sb_tp), c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent),
-                           S, X, X, P.gp, P.NRpad, c.r, nullptr, nullptr);
+                           c.sb_S, X, X, P.gp, P.NRpad, c.r, nullptr, nullptr, c.sb_I0);
         LRS_CHECK_LAUNCH();
         const long len = (long)c.n * c.ld;
         const int grid = grid_elems(len, 8);
@@ -5052,6 +5184,24 @@ int sync_shared(const DevProblem &P, double *v, hipStream_t st) {
     LRS_CHECK_LAUNCH();
     return 0;
 }
+// the inner loop's parameters and control block into device memory as kernel arguments: one
+// queued launch instead of two host-to-device copies (each a DMA / blit round trip the host
+// waits on before the first iteration of a run_inner call can start)
+struct CtrlPut { double v[P_NPAR + C_NCTRL]; };
+__global__ void k_put_ctrl(CtrlPut c, double *__restrict__ par, double *__restrict__ ctl) {
+    const int t = threadIdx.x;
+    if (t < P_NPAR) par[t] = c.v[t];
+    if (t < C_NCTRL) ctl[t] = c.v[P_NPAR + t];
+}
+int launch_put_ctrl(const double *par, const double *ctl, double *dpar, double *dctl, hipStream_t st) {
+    CtrlPut c;
+    for (int q = 0; q < P_NPAR; ++q) c.v[q] = par[q];
+    for (int q = 0; q < C_NCTRL; ++q) c.v[P_NPAR + q] = ctl[q];
+    hipLaunchKernelGGL(k_put_ctrl, dim3(1), dim3(64), 0, st, c, dpar, dctl);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
 // one scalar's partials (the sharded CG's <p, Q>, <r, r>, ||b||_1) -> out[0]
 int launch_fold1(const double *part, int nblk, double *out, hipStream_t st) {
     hipLaunchKernelGGL(k_fold_partials<1>, dim3(1), dim3(kBlock), 0, st, part, nblk, out);
@@ -5109,7 +5259,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     // long-row B over 2-D LDS tiles (k_tile_b1 / k_tile_b2, then k_wide_bf's epilogue blocks)
     bool tbt[kMaxCones];
     for (int k = 0; k < KL; ++k) {
-        tbt[k] = !merge && !sh && !tlb[k] && pb[k].wide && W.GP && cone_of(k).sb_blocks > 0 && cone_of(k).sa_items > 0;
+        tbt[k] = !merge && !tlb[k] && pb[k].wide && W.GP && cone_of(k).sb_blocks > 0 && cone_of(k).sa_items > 0;
         if (tbt[k]) nblkB += pb[k].grid;
     }
     if (nblkB > kMaxPartialBlocks) {
@@ -5134,6 +5284,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     if (lat && (nla + ngd > kLatMaxPartials || nlb + nlf > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials)))
         lat = false;
     P.last_path = lat ? 0 : 1;
+    P.last_tiles = 0;
+    for (int k = 0; k < KL; ++k)
+        if (tbt[k] || (pa[k].wide && !merge && !tla[k] && cone_of(k).sa_items > 0)) P.last_tiles = 1;
     if (lat) {
         nblkA = nla;
         nblkB = nlb + nlf;   // the C partials: B's blocks, then k_lat_f's
@@ -5216,13 +5369,18 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     for (int k = 0; k < KL && (mask & 1) && split; ++k) {
         const DevCone &c = cone_of(k);
         const int grid = pa[k].grid;
-        if (pa[k].wide && !merge && !sh && !tla[k] && c.sa_items > 0) {
+        if (pa[k].wide && !merge && !tla[k] && c.sa_items > 0) {
             // lower pattern in 2-D LDS tiles (k_tile_a), same grid and partial slots
-            hipLaunchKernelGGL(k_tile_a, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
-                               reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2, W.D,
-                               W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,
-                               reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur,
-                               W.part, off);
+            // 1024 threads (16 waves on the CU its 139 KB of LDS allows) unless LRS_TILE_A_NT=512
+            static const int nta = getenv("LRS_TILE_A_NT") ? atoi(getenv("LRS_TILE_A_NT")) : 1024;
+#define LRS_TILE_A(NT_)                                                                                        \
+    hipLaunchKernelGGL(k_tile_a<NT_>, dim3(grid), dim3(NT_), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,         \
+                       reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2, W.D,      \
+                       W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), \
+                       P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off)
+            if (nta == 512) LRS_TILE_A(512);
+            else LRS_TILE_A(1024);
+#undef LRS_TILE_A
         } else if (pa[k].wide) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
                 if (tla[k]) LRS_WIDE_A(true);
@@ -5332,15 +5490,23 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         if (tbt[k]) {
             hipLaunchKernelGGL(k_tile_b1, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
                                reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, W.R, W.R2, W.uvt2,
-                               c.sa_S - c.slot_off, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,
+                               c.sb_S, reinterpret_cast<const int2 *>(c.sb_pos) - c.slot_off, P.Craw, P.slot_ptr,
+                               P.slot_con, P.slot_a,
                                reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,
                                reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur,
                                W.partC, off);
             LRS_CHECK_LAUNCH();
+            if (c.sx_n > 0) {   // sharded: S on the halo rows' lower slots
+                hipLaunchKernelGGL(k_slot_sv, dim3(std::min(grid_elems(c.sx_n, 1), 2048)), dim3(kBlock), 0, st, c.sx_n,
+                                   c.sx_slot, c.sb_S, reinterpret_cast<const int2 *>(c.sb_pos) - c.slot_off, P.Craw,
+                                   P.slot_ptr, P.slot_con, P.slot_a,
+                                   reinterpret_cast<const double2 *>(P.slot1), W.rec, W.par, ctrl_cur, ls_cur);
+                LRS_CHECK_LAUNCH();
+            }
             hipLaunchKernelGGL(k_tile_b2, dim3(c.sb_blocks * ((c.ld + kTbC - 1) / kTbC)), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
                                reinterpret_cast<const int2 *>(c.sb_blk), reinterpret_cast<const int2 *>(c.sb_tp),
-                               c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent), c.sa_S - c.slot_off, W.R, W.R2,
-                               W.GP, P.NRpad, c.r, ctrl_cur, ls_cur);
+                               c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent), c.sb_S, W.R, W.R2,
+                               W.GP, P.NRpad, c.r, ctrl_cur, ls_cur, c.sb_I0);
             LRS_CHECK_LAUNCH();
             LRS_LAYOUT_SWITCH(c.G, c.E, {
                 hipLaunchKernelGGL((k_wide_bf<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff, W.D,

@@ -480,6 +480,8 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
         // entries count in A(.) on the shard owning their slot's lower row
         const int o0 = cp.row0, o1 = cp.row0 + cp.nown;
         for (HostEntry &e : oc.ent) e.owned = oc.prow[e.slot] >= o0 && oc.prow[e.slot] < o1;
+        oc.own0 = o0;
+        oc.own1 = o1;
         if (dense_mat(k)) {   // every row local, local ids = global ids: C's owned row block
             const int n = gc.n, r0 = cp.bounds[rank];
             oc.dense_c = true;
@@ -738,6 +740,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             if (ev && ev[0] == '0') on = false;
             if (ev && ev[0] == '1') on = Zk > 0;
             if (long_ptr[k + 1] > long_ptr[k]) on = false;
+            if (hp.cones[k].own1 >= 0) on = false;   // sharded: the A(.) operators keep the gather path
             if (!on) continue;
             const long nt = (n + kAuvT - 1) / kAuvT;
             std::vector<std::pair<unsigned long long, int>> key(Zk);
@@ -925,31 +928,42 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         }
         {
             // the lower pattern in 2-D tiles for k_tile_a (lrs_device.h kAuvT), slots sorted by
-            // (row tile, column tile, row, column), items of at most kAuvItem slots
+            // (row tile, column tile, row, column), items of at most kAuvItem slots.  A shard
+            // (own1 >= 0) tiles its owned rows only: the lower slots of owned rows, the row tiles
+            // holding them, and lists the slots of halo lower rows (S only, k_slot_sv).
             const long P = (long)c.prow.size();
+            const int o0 = c.own1 >= 0 ? c.own0 : 0, o1 = c.own1 >= 0 ? c.own1 : c.n;
+            const long nt = (c.n + kAuvT - 1) / kAuvT;
+            const long tI0 = o0 / kAuvT, tI1 = o1 > o0 ? (o1 - 1) / kAuvT + 1 : tI0;
+            std::vector<long> own_t;
+            own_t.reserve(P);
+            for (long t = 0; t < P; ++t)
+                if (c.prow[t] >= o0 && c.prow[t] < o1) own_t.push_back(t);
+            const long Po = (long)own_t.size();
+            double pairs = 0;   // lower tile pairs of the owned row tiles: nt (nt + 1) / 2 unsharded
+            for (long I = tI0; I < tI1; ++I) pairs += (double)(I + 1);
             const char *ev = getenv("LRS_SLOT_TILES");
-            const double ntl = (double)((c.n + kAuvT - 1) / kAuvT);
-            bool on = c.n >= kAuvMinN && (double)P >= kAuvMinPerTile * ntl * (ntl + 1) / 2;
+            bool on = c.n >= kAuvMinN && (double)Po >= kAuvMinPerTile * pairs;
             if (ev && ev[0] == '0') on = false;
-            if (ev && ev[0] == '1') on = P > 0;
+            if (ev && ev[0] == '1') on = Po > 0;
             if (on) {
-                const long nt = (c.n + kAuvT - 1) / kAuvT;
-                std::vector<std::pair<unsigned long long, int>> key(P);
-                for (long t = 0; t < P; ++t) {
+                std::vector<std::pair<unsigned long long, int>> key(Po);
+                for (long u = 0; u < Po; ++u) {
+                    const long t = own_t[u];
                     const int p = c.prow[t], q = c.pcol[t];   // lower: p >= q
                     const unsigned long long tile = (unsigned long long)(p / kAuvT) * nt + (q / kAuvT);
-                    key[t] = {(tile << 32) | ((unsigned)(p % kAuvT) << 16) | (unsigned)(q % kAuvT), (int)t};
+                    key[u] = {(tile << 32) | ((unsigned)(p % kAuvT) << 16) | (unsigned)(q % kAuvT), (int)t};
                 }
                 std::sort(key.begin(), key.end());
-                std::vector<int> item, sl(P);
-                std::vector<unsigned> pq(P);
+                std::vector<int> item, sl(Po);
+                std::vector<unsigned> pq(Po);
                 long t0 = 0;
                 const bool swz = tile_swizzle_on();
                 std::vector<long> perm;
-                for (long t = 0; t < P; ++t) {
+                for (long t = 0; t < Po; ++t) {
                     pq[t] = (unsigned)(key[t].first & 0xffffffffu);
                     sl[t] = d.slot_off + key[t].second;
-                    const bool last = t + 1 == P || (key[t + 1].first >> 32) != (key[t].first >> 32) ||
+                    const bool last = t + 1 == Po || (key[t + 1].first >> 32) != (key[t].first >> 32) ||
                                       t + 1 - t0 == kAuvItem;
                     if (!last) continue;
                     const unsigned long long tile = key[t].first >> 32;
@@ -970,27 +984,34 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 d.sa_items = (int)(item.size() / 4);
                 if (!dput(&d.sa_item, item, err) || !dput(&d.sa_pq, pq, err) || !dput(&d.sa_slot, sl, err))
                     return false;
-                // symmetric adjacency by (row tile I, column tile J): counting sort over the
-                // row-ordered, column-sorted adjacency keeps (row, column) order inside a tile pair
-                const long nnz = (long)c.adj_col.size();
+                // symmetric adjacency of the owned rows by (row tile I, column tile J): counting
+                // sort over the row-ordered, column-sorted adjacency keeps (row, column) order
+                // inside a tile pair
+                long nnz = 0;
+                for (int i = o0; i < o1; ++i) nnz += c.adj_ptr[i + 1] - c.adj_ptr[i];
                 std::vector<long> cnt((size_t)nt * nt + 1, 0);
-                for (int i = 0; i < c.n; ++i)
+                for (int i = o0; i < o1; ++i)
                     for (int e = c.adj_ptr[i]; e < c.adj_ptr[i + 1]; ++e)
                         cnt[(size_t)(i / kAuvT) * nt + c.adj_col[e] / kAuvT + 1]++;
                 for (size_t q = 0; q + 1 < cnt.size(); ++q) cnt[q + 1] += cnt[q];
                 std::vector<int> ent(2 * std::max(1L, nnz)), epl(std::max(1L, nnz));
+                // per local slot its entries' places {lower row's, upper row's} (-1: not an owned
+                // row's entry): stage B writes S there in entry order for k_tile_b2
+                std::vector<int> spos(2 * std::max(1L, P), -1);
                 std::vector<long> fill(cnt.begin(), cnt.end() - 1);
-                for (int i = 0; i < c.n; ++i)
+                for (int i = o0; i < o1; ++i)
                     for (int e = c.adj_ptr[i]; e < c.adj_ptr[i + 1]; ++e) {
                         const long at = fill[(size_t)(i / kAuvT) * nt + c.adj_col[e] / kAuvT]++;
                         ent[2 * at] = c.adj_col[e] % kAuvT;
                         ent[2 * at + 1] = d.slot_off + c.adj_slot[e];
                         epl[at] = i % kAuvT;
+                        const int sl = c.adj_slot[e];
+                        spos[2L * sl + (c.prow[sl] == i ? 0 : 1)] = (int)at;
                     }
-                std::vector<int> blk(2L * nt * kNX), tp, rp;
-                for (long I = 0; I < nt; ++I)
+                std::vector<int> blk(2L * std::max(1L, tI1 - tI0) * kNX), tp, rp;
+                for (long I = tI0; I < tI1; ++I)
                     for (int x = 0; x < kNX; ++x) {
-                        blk[2 * (I * kNX + x)] = (int)(tp.size() / 2);
+                        blk[2 * ((I - tI0) * kNX + x)] = (int)(tp.size() / 2);
                         for (long J = x * nt / kNX; J < (x + 1) * nt / kNX; ++J) {
                             const long e0 = cnt[I * nt + J], e1 = cnt[I * nt + J + 1];
                             if (e0 == e1) continue;
@@ -1002,13 +1023,25 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                                 rp.push_back((int)e);
                             }
                         }
-                        blk[2 * (I * kNX + x) + 1] = (int)(tp.size() / 2);
+                        blk[2 * ((I - tI0) * kNX + x) + 1] = (int)(tp.size() / 2);
                     }
-                d.sb_blocks = (int)(nt * kNX);
+                if (tp.empty()) { tp.assign(2, 0); rp.assign(kAuvT + 1, 0); }
+                d.sb_blocks = (int)((tI1 - tI0) * kNX);
+                d.sb_I0 = (int)tI0;
                 if (!dput(&d.sb_blk, blk, err) || !dput(&d.sb_tp, tp, err) || !dput(&d.sb_rp, rp, err) ||
-                    !dput(&d.sb_ent, ent, err))
+                    !dput(&d.sb_ent, ent, err) || !dput(&d.sb_pos, spos, err))
                     return false;
-                if (hipMalloc((void **)&d.sa_S, (size_t)P * sizeof(double)) != hipSuccess) {
+                d.sb_nnz = nnz;
+                // a shard: the slots whose lower row is a halo row (S for k_tile_b2's upper entries)
+                if (c.own1 >= 0) {
+                    std::vector<int> sx;
+                    for (long t = 0; t < P; ++t)
+                        if (c.prow[t] < o0 || c.prow[t] >= o1) sx.push_back(d.slot_off + (int)t);
+                    d.sx_n = (int)sx.size();
+                    if (sx.empty()) sx.push_back(0);
+                    if (!dput(&d.sx_slot, sx, err)) return false;
+                }
+                if (hipMalloc((void **)&d.sb_S, (size_t)std::max(1L, nnz) * sizeof(double)) != hipSuccess) {
                     err = "hipMalloc failed";
                     return false;
                 }
@@ -1035,7 +1068,7 @@ void free_problem(DevProblem &dp) {
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);
-        f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); }
+        f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sb_pos); f(c.sb_S); f(c.sx_slot); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);

@@ -34,6 +34,9 @@ struct HostCone {
     // the dense path's products without the matrix, C X = c_alpha 1 (1^T X)
     bool const_c = false;
     double c_alpha = 0.0;
+    // sharded solve: this shard's owned local rows [own0, own1) (own1 < 0: every row, unsharded).
+    // The 2-D tiles of the stage kernels then cover the owned rows only.
+    int own0 = 0, own1 = -1;
 };
 // Dense-objective policy: LRS_DENSE_C=0 never, =1 every cone with objective entries, unset:
 // cones with n >= kDenseCMinN whose C fills >= 1/4 of the lower triangle (measured: the dense

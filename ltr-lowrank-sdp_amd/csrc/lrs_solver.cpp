@@ -1423,10 +1423,7 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
         memcpy(ctl, c->last_ctl, sizeof(ctl));
         ctl[C_ACTIVE] = 1; ctl[C_EXIT] = EXIT_NONE; ctl[C_ACT2] = 1; ctl[C_EXIT2] = EXIT_NONE; ctl[C_RCUR] = 0;
     }
-    memcpy(c->hpin, par, sizeof(par));
-    HIPC(hipMemcpyAsync(c->W.par, c->hpin, sizeof(par), hipMemcpyHostToDevice, c->st));
-    memcpy(c->hpin + 64, ctl, sizeof(ctl));
-    HIPC(hipMemcpyAsync(c->W.ctrl + C_NCTRL, c->hpin + 64, sizeof(ctl), hipMemcpyHostToDevice, c->st));
+    OPC(launch_put_ctrl(par, ctl, c->W.par, c->W.ctrl + C_NCTRL, c->st));
     AlmIterArgs a{&c->dp, &c->W, nullptr};
     // Batch sizes: start near the running estimate of this call's length, double after
     // each batch, never beyond the iterations to a certain exit (budget, localIter 800)
@@ -1483,7 +1480,7 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
                 for (int j = 0; j < Bk; ++j) {
                     a.hmirror = (j == Bk - 1) ? c->dmir + 64 * (k & 1) : nullptr;
                     a.seq = bseq[k & 1];
-                    OPC(enqueue_alm_iteration(a, j & 1, c->st));
+                    OPC(enqueue_alm_iteration(a, (int)((enq + j) & 1), c->st));   // parity runs across batches
                 }
                 a.hmirror = nullptr;
             }
@@ -1493,12 +1490,18 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
             return 0;
         };
         // small fixed batches: the batch in flight at the exit bounds the no-op iterations,
-        // and one batch of GPU work outlasts the host's submission of the next
+        // and one batch of GPU work outlasts the host's submission of the next.  Eager batches
+        // end exactly at the certain exit (the iteration parity runs on across batches);
+        // captured graphs start at parity 0, so their lengths stay even.
         const int Bp = c->pipe_batch;
-        if (enqueue(std::min(Bp, even_clamp(certain - enq)))) return -1;
+        auto next_b = [&]() -> int {
+            const long left = std::max(1L, certain - enq);
+            return c->use_graphs ? std::min(Bp, even_clamp(left)) : (int)std::min<long>(Bp, left);
+        };
+        if (enqueue(next_b())) return -1;
         for (;;) {
             if (enq < certain) {
-                if (enqueue(std::min(Bp, even_clamp(certain - enq)))) return -1;
+                if (enqueue(next_b())) return -1;
             }
             if (mirror) {
                 volatile double *slot = c->hmir + 64 * (kw & 1);
@@ -2549,6 +2552,13 @@ int lrs_tile_info(lrs_ctx *c, int *auv, int *slot) {
     }
     if (auv) *auv = a;
     if (slot) *slot = sl;
+    return 0;
+}
+
+int lrs_tile_used(lrs_ctx *c, int *used) {
+    if (c) bind(c);
+    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    if (used) *used = c->dp.last_tiles;
     return 0;
 }
 

@@ -117,6 +117,7 @@ def load_library(path=None):
         "lrs_get_kernel_path": (C.c_int, [vp, ip]),
         "lrs_stage_bytes": (C.c_int, [vp, dp]),
         "lrs_tile_info": (C.c_int, [vp, ip, ip]),
+        "lrs_tile_used": (C.c_int, [vp, ip]),
         "lrs_auut_bytes": (C.c_int, [vp, dp]),
         "lrs_time_gram": (C.c_int, [vp, C.c_int, C.c_int, dp, dp]),
         "lrs_mfma_f64_peak": (C.c_int, [vp, dp]),
@@ -133,7 +134,12 @@ def load_library(path=None):
         "lrs_shard_plan": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_long), ip, ip, ip, ip, ip, ip, ip]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if os.environ.get("LRS_LIB"):   # an older build compared side by side (scripts/*_probe.py)
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     _lib = lib
@@ -439,6 +445,12 @@ class Solver:
         a, b = C.c_int(), C.c_int()
         self._check(self.lib.lrs_tile_info(self.ctx, C.byref(a), C.byref(b)), "tile_info")
         return a.value, b.value
+
+    def tile_used(self):
+        """True when the last ALM iteration ran its stages over the 2-D tiles."""
+        v = C.c_int()
+        self._check(self.lib.lrs_tile_used(self.ctx, C.byref(v)), "tile_used")
+        return bool(v.value)
 
     def stage_bytes(self):
         """Algorithmic bytes per launch of the stages [A, G, B] at the current ranks."""
