@@ -130,13 +130,10 @@ struct DevCone {
     // stage B's gradient S R_new over the symmetric pattern in the same tiles (k_tile_b2): one
     // block per (row tile I, column group x of kNX), its tile pairs {col0, row-pointer offset}
     // ([nt * kNX][2] ranges into sb_tp), per tile pair kAuvT + 1 row pointers into the entries
-    // {local column, slot}; sb_S holds S = C + A^*(M1) in that entry order between the two
-    // kernels (stage B writes each slot's value at its entries' places sb_pos[slot] = {lower
-    // row's, upper row's}, -1 where the row is not tiled here)
+    // {local column, slot}; sa_S holds the slot values of S = C + A^*(M1) between the two kernels
     int sb_blocks = 0;
-    int *sb_blk = nullptr, *sb_tp = nullptr, *sb_rp = nullptr, *sb_ent = nullptr, *sb_pos = nullptr;
-    long sb_nnz = 0;
-    double *sb_S = nullptr;
+    int *sb_blk = nullptr, *sb_tp = nullptr, *sb_rp = nullptr, *sb_ent = nullptr;
+    double *sa_S = nullptr;
     // sharded solve: the tiles cover the owned rows only -- sa_* the owned rows' lower slots,
     // sb_* the row tiles from sb_I0 on; sx_slot the slots whose lower row is a halo row (the
     // upper entries of owned rows), whose S k_slot_sv forms for k_tile_b2
@@ -238,6 +235,7 @@ struct DevWork {
     double *U = nullptr, *V = nullptr, *X = nullptr;         // ADMM / scratch factors
     double *cg_r = nullptr, *cg_p = nullptr, *cg_Q = nullptr, *cg_b = nullptr, *M2 = nullptr;
     double *uvt0 = nullptr, *uvt1 = nullptr, *uvt2 = nullptr, *S = nullptr;   // [Ptot]
+    double *uvp = nullptr;   // [Ptot][2] the tiled stage A's (sym(RD^T), DD^T) per slot, for k_it_g
     double *lam = nullptr, *cvs = nullptr, *q1 = nullptr, *q2 = nullptr, *M1 = nullptr, *wtmp = nullptr;
     double *cvc = nullptr;                                   // per-cone A(UV^T), K*m
     double *part = nullptr;    // [kMaxPartialVals][kMaxPartialBlocks] partial sums (scratch A)

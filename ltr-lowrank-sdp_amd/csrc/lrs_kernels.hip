@@ -1711,7 +1711,8 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
                                                  const double *__restrict__ par, double *__restrict__ ctrl_cur,
                                                  const double *__restrict__ partC, int nblkC,
                                                  const double *__restrict__ partA, int nblkA,
-                                                 double *__restrict__ rec, double *__restrict__ partB, int gwide) {
+                                                 double *__restrict__ rec, double *__restrict__ partB, int gwide,
+                                                 const double2 *__restrict__ uvp) {
     __shared__ double cs[3];
     __shared__ double red[2];
     LRS_TS(1, 0);
@@ -1749,11 +1750,20 @@ __global__ void __launch_bounds__(kBlock) k_it_g(int mg, const int *__restrict__
         for (int k = 0; k < K; ++k) {
             const long row = (long)k * m + i;
             double a1 = 0.0, a2 = 0.0;
-            for (int e = con_ptr[row] + sub; e < con_ptr[row + 1]; e += lanes) {
-                const double w = con_w[e];
-                const int s = con_slot[e];
-                a1 += w * uRD[s];
-                a2 += w * uDD[s];
+            if (uvp) {   // the tiled stage A's (RD, DD) records: one 16-B read per entry
+                for (int e = con_ptr[row] + sub; e < con_ptr[row + 1]; e += lanes) {
+                    const double w = con_w[e];
+                    const double2 v = uvp[con_slot[e]];
+                    a1 += w * v.x;
+                    a2 += w * v.y;
+                }
+            } else {
+                for (int e = con_ptr[row] + sub; e < con_ptr[row + 1]; e += lanes) {
+                    const double w = con_w[e];
+                    const int s = con_slot[e];
+                    a1 += w * uRD[s];
+                    a2 += w * uDD[s];
+                }
             }
             if (gwide) { a1 = wave_sum(a1); a2 = wave_sum(a2); }
             v1 += a1; v2 += a2;
@@ -3061,7 +3071,8 @@ __global__ void __launch_bounds__(NT) k_tile_a(
     double *__restrict__ uDD, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     const double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec,
-    const double *__restrict__ par, const double *__restrict__ ctrl_cur, double *__restrict__ partA, int pblk_off) {
+    const double *__restrict__ par, const double *__restrict__ ctrl_cur, double *__restrict__ partA, int pblk_off,
+    double2 *__restrict__ uvp) {
     constexpr int NPT = kAuvItem / NT;   // slots per thread of one item
     static_assert(NPT * NT == kAuvItem, "k_tile_a: items divide over the block");
     if (ctrl_cur[C_ACTIVE] == 0.0) return;
@@ -3102,8 +3113,12 @@ __global__ void __launch_bounds__(NT) k_tile_a(
             if (t >= ee) break;
             const int sl = tslot[t];
             const double d0 = 0.5 * s0[j], d1 = s1[j];
-            uRD[sl] = d0;
-            uDD[sl] = d1;
+            if (uvp) {   // both values of the slot in one 16-B record (k_it_g reads them together)
+                uvp[sl] = make_double2(d0, d1);
+            } else {
+                uRD[sl] = d0;
+                uDD[sl] = d1;
+            }
             const double cwl = Cw[sl];
             acc[0] += cwl * d0;
             acc[1] += cwl * d1;
@@ -3306,7 +3321,7 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_b(
 __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: two blocks a CU (68 KB LDS each)
     int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
     const int *__restrict__ tslot, const double *Rb0, const double *Rb1, double *__restrict__ uRR,
-    double *__restrict__ SE, const int2 *__restrict__ spos, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
+    double *__restrict__ Sv, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
     const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double2 *__restrict__ slot1,
     const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
@@ -3351,7 +3366,6 @@ __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: tw
         int slv[kB1H];
         double2 s1v[kB1H], l1v[kB1H];
         double crv[kB1H];
-        int2 psv[kB1H];
 #pragma unroll
         for (int j = 0; j < kB1H; ++j) {
             const int t = eb + (int)threadIdx.x + (h + j) * kAuvThreads;
@@ -3362,7 +3376,6 @@ __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: tw
             s1v[j] = slot1[slv[j]];
             l1v[j] = loc1[slv[j]];
             crv[j] = Craw[slv[j]];
-            psv[j] = spos[slv[j]];
         }
         double2 rav[kB1H], rbv[kB1H];
 #pragma unroll
@@ -3393,8 +3406,7 @@ __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: tw
                     svl += (y.y + rho * cv) * slot_a[e];
                 }
             }
-            if (psv[j].x >= 0) SE[psv[j].x] = svl;
-            if (psv[j].y >= 0) SE[psv[j].y] = svl;
+            Sv[sl] = svl;
             const double d = dv[h + j];
             uRR[sl] = d;
             const double2 l1l = l1v[j];
@@ -3455,13 +3467,12 @@ __device__ __forceinline__ void b2_batch(std::integer_sequence<int, K...>, int k
 // group of kTbL lanes takes kTbRows rows of the tile; lane l holds the chunk's columns 2l, 2l+1,
 // 32+2l, 33+2l, so the group's two ds_read_b128 of a neighbour row read it whole, 256 B each
 // (no bank conflicts, whatever the row).  A row's entries come 16 at a time, lane k loading
-// entry k's column and S (SE: S in the tile-pair entry order, written by stage B's slot
-// kernels; coalesced, no dependent loads), and the group walks them with a DPP row broadcast
-// of lane k.  Each column's sum runs over the row's entries in column order, tile pair by tile
-// pair.
+// entry k's column and slot and the slot's S (the four rows' batches in flight together), and
+// the group walks them with a DPP row broadcast of lane k.  Each column's sum runs over the
+// row's entries in column order, tile pair by tile pair.
 __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff, const int2 *__restrict__ blk,
                                                        const int2 *__restrict__ tp, const int *__restrict__ rp,
-                                                       const int2 *__restrict__ ent, const double *__restrict__ SE,
+                                                       const int2 *__restrict__ ent, const double *__restrict__ Sv,
                                                        const double *Rb0, const double *Rb1, double *__restrict__ GP,
                                                        long gstride, int r, const double *__restrict__ ctrl,
                                                        const double *__restrict__ ls_cur, int tI0) {
@@ -3469,7 +3480,6 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
     // ctrl == nullptr: the standalone S X of launch_spmm (X in Rb0)
     if (ctrl && (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0)) return;
     const double *__restrict__ Rn = ((ctrl && ctrl[C_RCUR] == 0.0) ? Rb1 : Rb0) + foff;
-    const int *__restrict__ ecol = reinterpret_cast<const int *>(ent);
     __shared__ double rj[kAuvT * kTbS];
     const int nch = (ld + kTbC - 1) / kTbC;
     const int bx = blockIdx.x / nch, c0 = (blockIdx.x % nch) * kTbC;
@@ -3500,8 +3510,9 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
         for (int w = 0; w < kTbRows; ++w) {
             const int e = e0[w] + l;
             const bool ok = e < e1[w];
-            cv[w] = ecol[2L * (ok ? e : e0[w] < e1[w] ? e0[w] : 0)];
-            sv[w] = ok ? SE[e] : 0.0;
+            const int2 en = ent[ok ? e : e0[w] < e1[w] ? e0[w] : 0];
+            cv[w] = en.x;
+            sv[w] = ok ? Sv[en.y] : 0.0;
         }
         __syncthreads();
 #pragma unroll
@@ -3525,8 +3536,9 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
                 base += kTbL;
                 const int e = base + l;
                 const bool ok = e < e1[w];
-                colv = ok ? ecol[2L * e] : 0;
-                s = ok ? SE[e] : 0.0;
+                const int2 en = ent[ok ? e : e0[w]];
+                colv = en.x;
+                s = ok ? Sv[en.y] : 0.0;
             }
         }
     }
@@ -3540,18 +3552,11 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
         }
     }
 }
-// launch_spmm: a slot-ordered S into the tile-pair entry order
-__global__ void __launch_bounds__(kBlock) k_gather_se(long nnz, const int2 *__restrict__ ent,
-                                                      const double *__restrict__ S, double *__restrict__ SE) {
-    for (long e = blockIdx.x * (long)kBlock + threadIdx.x; e < nnz; e += (long)gridDim.x * kBlock)
-        SE[e] = S[ent[e].y];
-}
 
 // Sharded long-row B over the tiles: S = C + A^*(M1) (k_tile_b1's slot epilogue, lorads_alm.c:38-57)
 // on the slots whose lower row is a halo row -- k_tile_b2 reads them as owned rows' upper entries;
 // their A(R_new R_new^T) belongs to the shard owning the lower row.
-__global__ void __launch_bounds__(kBlock) k_slot_sv(int nx, const int *__restrict__ sx, double *__restrict__ SE,
-                                                    const int2 *__restrict__ spos,
+__global__ void __launch_bounds__(kBlock) k_slot_sv(int nx, const int *__restrict__ sx, double *__restrict__ Sv,
                                                     const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
                                                     const int *__restrict__ slot_con, const double *__restrict__ slot_a,
                                                     const double2 *__restrict__ slot1, const double *__restrict__ rec,
@@ -3579,9 +3584,7 @@ __global__ void __launch_bounds__(kBlock) k_slot_sv(int nx, const int *__restric
                 svl += (y.y + rho * cv) * slot_a[e];
             }
         }
-        const int2 ps = spos[sl];
-        if (ps.x >= 0) SE[ps.x] = svl;
-        if (ps.y >= 0) SE[ps.y] = svl;
+        Sv[sl] = svl;
     }
 }
 
@@ -4390,13 +4393,10 @@ int launch_spmm(const DevProblem &P, int cone, const double *S, const double *X,
     if (c.sb_blocks > 0 && P.gp && !P.shard) {
         // long-row cone: S X per (row tile, column group) from staged X tiles into P.gp's kNX
         // partial rows (k_tile_b2 without the iteration's control), then the sum and epilogue
-        hipLaunchKernelGGL(k_gather_se, dim3(std::min(grid_elems(c.sb_nnz, 4), 4096)), dim3(kBlock), 0, st, c.sb_nnz,
-                           reinterpret_cast<const int2 *>(c.sb_ent), S, c.sb_S);
-        LRS_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_tile_b2, dim3(c.sb_blocks * ((c.ld + kTbC - 1) / kTbC)), dim3(kRowBlock), 0, st, c.n,
                            c.ld, c.foff, reinterpret_cast<const int2 *>(c.sb_blk),
                            reinterpret_cast<const int2 *>(c.sb_tp), c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent),
-                           c.sb_S, X, X, P.gp, P.NRpad, c.r, nullptr, nullptr, c.sb_I0);
+                           S, X, X, P.gp, P.NRpad, c.r, nullptr, nullptr, c.sb_I0);
         LRS_CHECK_LAUNCH();
         const long len = (long)c.n * c.ld;
         const int grid = grid_elems(len, 8);
@@ -5266,6 +5266,10 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         snprintf(g_err, sizeof(g_err), "stage B: %d partial blocks past %d", nblkB, kMaxPartialBlocks);
         return -1;
     }
+    // one tiled cone, unsharded: stage A's slot values go to k_it_g as (RD, DD) records
+    const bool use_uvp = !sh && !merge && KL == 1 && W.uvp && split && pa[0].wide && !tla[0] &&
+                         cone_of(0).sa_items > 0;
+    double2 *uvp = use_uvp ? reinterpret_cast<double2 *>(W.uvp) : nullptr;
     const int gwide = P.glob_maxlen >= 32 ? 1 : 0;   // long global constraints: a wave each
     const int gg = gwide ? std::min((std::max(1, P.mg) + kBlock / 64 - 1) / (kBlock / 64), kMaxPartialBlocks)
                          : std::min(grid_elems(std::max(1, P.mg), 1), kMaxPartialBlocks);
@@ -5377,7 +5381,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     hipLaunchKernelGGL(k_tile_a<NT_>, dim3(grid), dim3(NT_), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,         \
                        reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2, W.D,      \
                        W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), \
-                       P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off)
+                       P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, uvp)
             if (nta == 512) LRS_TILE_A(512);
             else LRS_TILE_A(1024);
 #undef LRS_TILE_A
@@ -5427,7 +5431,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     } else if (P.mg > 0 && (mask & 2)) {
         hipLaunchKernelGGL(k_it_g, dim3(gg), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot,
                            P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, nblkB, W.part,
-                           nblkA, W.rec, W.partB, gwide);
+                           nblkA, W.rec, W.partB, gwide, uvp);
         LRS_CHECK_LAUNCH();
     }
     if (mark(2)) return -1;
@@ -5490,7 +5494,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         if (tbt[k]) {
             hipLaunchKernelGGL(k_tile_b1, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
                                reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, W.R, W.R2, W.uvt2,
-                               c.sb_S, reinterpret_cast<const int2 *>(c.sb_pos) - c.slot_off, P.Craw, P.slot_ptr,
+                               c.sa_S - c.slot_off, P.Craw, P.slot_ptr,
                                P.slot_con, P.slot_a,
                                reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,
                                reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur,
@@ -5498,14 +5502,14 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
             LRS_CHECK_LAUNCH();
             if (c.sx_n > 0) {   // sharded: S on the halo rows' lower slots
                 hipLaunchKernelGGL(k_slot_sv, dim3(std::min(grid_elems(c.sx_n, 1), 2048)), dim3(kBlock), 0, st, c.sx_n,
-                                   c.sx_slot, c.sb_S, reinterpret_cast<const int2 *>(c.sb_pos) - c.slot_off, P.Craw,
+                                   c.sx_slot, c.sa_S - c.slot_off, P.Craw,
                                    P.slot_ptr, P.slot_con, P.slot_a,
                                    reinterpret_cast<const double2 *>(P.slot1), W.rec, W.par, ctrl_cur, ls_cur);
                 LRS_CHECK_LAUNCH();
             }
             hipLaunchKernelGGL(k_tile_b2, dim3(c.sb_blocks * ((c.ld + kTbC - 1) / kTbC)), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
                                reinterpret_cast<const int2 *>(c.sb_blk), reinterpret_cast<const int2 *>(c.sb_tp),
-                               c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent), c.sb_S, W.R, W.R2,
+                               c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent), c.sa_S - c.slot_off, W.R, W.R2,
                                W.GP, P.NRpad, c.r, ctrl_cur, ls_cur, c.sb_I0);
             LRS_CHECK_LAUNCH();
             LRS_LAYOUT_SWITCH(c.G, c.E, {

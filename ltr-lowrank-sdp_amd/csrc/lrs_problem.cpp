@@ -995,9 +995,6 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                         cnt[(size_t)(i / kAuvT) * nt + c.adj_col[e] / kAuvT + 1]++;
                 for (size_t q = 0; q + 1 < cnt.size(); ++q) cnt[q + 1] += cnt[q];
                 std::vector<int> ent(2 * std::max(1L, nnz)), epl(std::max(1L, nnz));
-                // per local slot its entries' places {lower row's, upper row's} (-1: not an owned
-                // row's entry): stage B writes S there in entry order for k_tile_b2
-                std::vector<int> spos(2 * std::max(1L, P), -1);
                 std::vector<long> fill(cnt.begin(), cnt.end() - 1);
                 for (int i = o0; i < o1; ++i)
                     for (int e = c.adj_ptr[i]; e < c.adj_ptr[i + 1]; ++e) {
@@ -1005,8 +1002,6 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                         ent[2 * at] = c.adj_col[e] % kAuvT;
                         ent[2 * at + 1] = d.slot_off + c.adj_slot[e];
                         epl[at] = i % kAuvT;
-                        const int sl = c.adj_slot[e];
-                        spos[2L * sl + (c.prow[sl] == i ? 0 : 1)] = (int)at;
                     }
                 std::vector<int> blk(2L * std::max(1L, tI1 - tI0) * kNX), tp, rp;
                 for (long I = tI0; I < tI1; ++I)
@@ -1029,9 +1024,8 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 d.sb_blocks = (int)((tI1 - tI0) * kNX);
                 d.sb_I0 = (int)tI0;
                 if (!dput(&d.sb_blk, blk, err) || !dput(&d.sb_tp, tp, err) || !dput(&d.sb_rp, rp, err) ||
-                    !dput(&d.sb_ent, ent, err) || !dput(&d.sb_pos, spos, err))
+                    !dput(&d.sb_ent, ent, err))
                     return false;
-                d.sb_nnz = nnz;
                 // a shard: the slots whose lower row is a halo row (S for k_tile_b2's upper entries)
                 if (c.own1 >= 0) {
                     std::vector<int> sx;
@@ -1041,7 +1035,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                     if (sx.empty()) sx.push_back(0);
                     if (!dput(&d.sx_slot, sx, err)) return false;
                 }
-                if (hipMalloc((void **)&d.sb_S, (size_t)std::max(1L, nnz) * sizeof(double)) != hipSuccess) {
+                if (hipMalloc((void **)&d.sa_S, (size_t)std::max(1L, P) * sizeof(double)) != hipSuccess) {
                     err = "hipMalloc failed";
                     return false;
                 }
@@ -1068,7 +1062,7 @@ void free_problem(DevProblem &dp) {
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);
-        f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sb_pos); f(c.sb_S); f(c.sx_slot); }
+        f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); f(c.sx_slot); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);

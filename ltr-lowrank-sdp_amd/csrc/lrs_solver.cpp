@@ -478,7 +478,7 @@ static void free_work(lrs_ctx *c) {
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
                       W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2,
-                      W.cgc, W.tot, W.gl, W.CR, W.CD, W.GP, W.CGK};
+                      W.cgc, W.tot, W.gl, W.CR, W.CD, W.GP, W.CGK, W.uvp};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     for (double *q : c->ring_s) if (q) (void)hipFree(q);
@@ -573,6 +573,9 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         bool btiles = false;   // long-row B over 2-D tiles (DevCone::sb_blocks): k_wide_bf's partial rows
         for (const auto &dc : P.cones) btiles = btiles || dc.sb_blocks > 0;
         if ((tiles || btiles) && A(&W.GP, (long)kNX * NR)) return -1;
+        bool stiles = false;   // the tiled stage A's slot-value records (DevWork::uvp)
+        for (const auto &dc : P.cones) stiles = stiles || dc.sa_items > 0;
+        if (stiles && A(&W.uvp, 2L * std::max(1, P.Ptot))) return -1;
         P.gp = W.GP;
         P.tiles = tiles;
     }

@@ -3,7 +3,7 @@
 # tile / C5 / steps parity, then C5 kernel traces: this build vs _build/var (k_tile_b1 without
 
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-R=$PWD; O=$R/gpurun_out/r03q; mkdir -p $O
+R=$PWD; O=$R/gpurun_out/r03r; mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -q -rfE --timeout 600 --timeout-method thread tests/test_gpu_shard_tiles.py \
   tests/test_gpu_auv_tiles.py tests/test_gpu_c5_steps.py tests/test_gpu_steps.py tests/test_gpu_densec.py > $O/pytest.log 2>&1
 rc=$?
