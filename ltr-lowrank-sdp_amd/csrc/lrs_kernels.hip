@@ -3553,19 +3553,184 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
     }
 }
 
+// Stage B's long-row half in ONE pass over the tiles (cones with r <= kTxC; replaces k_tile_b1's
+// A(R_new R_new^T) and k_tile_b2's S R_new): block (row tile I, column group x) stages R_new of
+// each column tile J of its group whole (128 columns), and a
+// group of kTxL lanes takes kTxRows rows of the tile; lane l holds columns 2l, 2l+1, 64+2l, 65+2l
+// (two conflict-free 256-B row reads per 16 lanes).  A row's entries come 16 at a time, lane k
+// of each 16-lane half loading entry k's column, slot and S (from k_slot_sv), broadcast by DPP
+// row_newbcast; per entry the lane adds S_ij R_new,j to its four gradient columns and keeps its
+// four-column part of R_new,i . R_new,j, and after the batch a transposed butterfly over the 16
+// lanes (mirror, half-mirror, quad swaps: each step halves the values a lane holds) plus one
+// exchange between the halves leaves entry k's dot product in lane k -- which stores it when the
+// entry is a lower slot of its row (the slot's owner row; each lower slot once) with the local
+// constraints' new A(.) and residual (ALMupdateVar lorads_alm.c:826-830, as k_tile_b1).
+constexpr int kTxC = 128;                        // columns staged: the whole row (r <= 128)
+constexpr int kTxS = kTxC + 2;                   // LDS row stride (16-B aligned rows)
+constexpr int kTxT = 1024;                       // threads
+constexpr int kTxL = 32;                         // lanes per tile row, four columns each
+constexpr int kTxG = kTxT / kTxL;                // row groups
+constexpr int kTxRows = kAuvT / kTxG;            // rows per group
+constexpr int kTxPer = kAuvT * kTxC / 2 / kTxT;  // double2 per thread per staged tile
+static_assert(kTxL == 32 && kTxC == 4 * kTxL, "k_tile_bx: two 16-lane halves, four columns a lane");
+__device__ __forceinline__ void tx_fetch(double2 (&v)[kTxPer], int J0, int n, int r, int ld,
+                                         const double *__restrict__ Rn) {
+#pragma unroll
+    for (int k = 0; k < kTxPer; ++k) {
+        const int y = threadIdx.x + k * kTxT;
+        const int grow = J0 + y / (kTxC / 2), col = 2 * (y % (kTxC / 2));
+        double2 t = make_double2(0.0, 0.0);
+        if (grow < n && col < r) {
+            t = *reinterpret_cast<const double2 *>(Rn + (long)grow * ld + col);
+            if (col + 1 >= r) t.y = 0.0;
+        }
+        v[k] = t;
+    }
+}
+template <bool DOT, int K>
+__device__ __forceinline__ void bx_entry(const double *rj, int l, int colv, double sv, double (&g)[4],
+                                         const double2 &ra, const double2 &rb, double (&pd)[16]) {
+    const int j = nbc_i<K>(colv);
+    const double s = dpp_mov<0x150 + K>(sv);
+    const double2 *p = reinterpret_cast<const double2 *>(&rj[j * kTxS]) + l;
+    const double2 a0 = p[0], a1 = p[kTxL];
+    g[0] += s * a0.x; g[1] += s * a0.y; g[2] += s * a1.x; g[3] += s * a1.y;
+    if constexpr (DOT) pd[K] = ra.x * a0.x + ra.y * a0.y + rb.x * a1.x + rb.y * a1.y;
+}
+template <bool DOT, int... K>
+__device__ __forceinline__ void bx_batch(std::integer_sequence<int, K...>, int kmax, const double *rj, int l,
+                                         int colv, double sv, double (&g)[4], const double2 &ra, const double2 &rb,
+                                         double (&pd)[16]) {
+    ((K < kmax ? bx_entry<DOT, K>(rj, l, colv, sv, g, ra, rb, pd) : void(pd[K] = 0.0)), ...);
+}
+// one butterfly step: pairs differ in lane bit B (CTRL the DPP pairing), a lane keeps the half
+// of its N values its bit selects and adds its partner's copy of them
+template <int N, int CTRL>
+__device__ __forceinline__ void bx_halve(double (&v)[16], bool hi) {
+#pragma unroll
+    for (int m = 0; m < N / 2; ++m) {
+        const double keep = hi ? v[m + N / 2] : v[m], send = hi ? v[m] : v[m + N / 2];
+        v[m] = keep + dpp_mov<CTRL>(send);
+    }
+}
+__global__ void __launch_bounds__(kTxT) k_tile_bx(
+    int n, int r, int ld, long foff, const int2 *__restrict__ blk, const int2 *__restrict__ tp,
+    const int *__restrict__ rp, const int2 *__restrict__ ent, const double *__restrict__ Sv, const double *Rb0,
+    const double *Rb1, double *__restrict__ GP, long gstride, const double *__restrict__ ctrl,
+    const double *__restrict__ ls_cur, int tI0, double *__restrict__ uRR, const int *__restrict__ loc_ptr,
+    const int *__restrict__ loc_con, const double *__restrict__ loc_w, const double2 *__restrict__ loc1,
+    const double *__restrict__ b, double *__restrict__ cvs, double *__restrict__ partC, int pblk_off) {
+    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
+    const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
+    __shared__ double rj[kAuvT * kTxS];
+    const int bx = blockIdx.x;
+    const int I = tI0 + bx / kNX, x = bx % kNX;   // tI0: a shard's first owned row tile
+    const int grp = threadIdx.x / kTxL, l = threadIdx.x % kTxL, k16 = l & 15;
+    const int2 br = blk[bx];
+    double g[kTxRows][4];
+#pragma unroll
+    for (int w = 0; w < kTxRows; ++w)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) g[w][c] = 0.0;
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int q = br.x; q < br.y; ++q) {   // block-uniform
+        // the tile staged after the barrier (no register prefetch: the 16 partial dots of a
+        // batch and four rows' gradient columns take the registers)
+        const int2 cur = tp[q];
+        {
+            double2 pre[kTxPer];
+            tx_fetch(pre, cur.x, n, r, ld, Rn);
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kTxPer; ++k) {
+                const int y = threadIdx.x + k * kTxT;
+                *reinterpret_cast<double2 *>(&rj[(y / (kTxC / 2)) * kTxS + 2 * (y % (kTxC / 2))]) = pre[k];
+            }
+            __syncthreads();
+        }
+        const int J0 = cur.x;
+        const bool lower = J0 <= I * kAuvT;   // the diagonal tile pair and those left of it hold lower slots
+#pragma unroll
+        for (int w = 0; w < kTxRows; ++w) {
+            const int pl = grp + w * kTxG, i = I * kAuvT + pl;
+            const int e0 = rp[cur.y + pl], e1 = rp[cur.y + pl + 1];
+            double2 ra = make_double2(0.0, 0.0), rb = make_double2(0.0, 0.0);   // row i's own R_new
+            if (e0 < e1 && i < n) {
+                const double *ri = Rn + (long)i * ld;
+                if (2 * l < r) { ra = *reinterpret_cast<const double2 *>(ri + 2 * l); if (2 * l + 1 >= r) ra.y = 0.0; }
+                if (2 * (l + kTxL) < r) {
+                    rb = *reinterpret_cast<const double2 *>(ri + 2 * (l + kTxL));
+                    if (2 * (l + kTxL) + 1 >= r) rb.y = 0.0;
+                }
+            }
+            for (int base = e0;; base += 16) {   // wave-uniform: the wave's two rows, 16 entries at a time
+                int rem = e1 - base;
+                rem = rem < 0 ? 0 : (rem > 16 ? 16 : rem);
+                const int kmax = max(__builtin_amdgcn_readlane(rem, 0), __builtin_amdgcn_readlane(rem, 32));
+                if (kmax == 0) break;
+                const int e = base + k16;
+                const bool ok = k16 < rem;
+                const int2 en = ent[ok ? e : (e0 < e1 ? e0 : 0)];
+                const double sv = ok ? Sv[en.y] : 0.0;
+                double pd[16];
+                if (!lower) {   // a tile pair above the diagonal: no lower slot of these rows
+                    bx_batch<false>(std::make_integer_sequence<int, 16>{}, kmax, rj, l, en.x, sv, g[w], ra, rb, pd);
+                    if (kmax < 16) break;
+                    continue;
+                }
+                bx_batch<true>(std::make_integer_sequence<int, 16>{}, kmax, rj, l, en.x, sv, g[w], ra, rb, pd);
+                // entry k16's dot into lane k16 of each half, then the two halves' sum
+                bx_halve<16, 0x140>(pd, (k16 & 8) != 0);   // row_mirror: partner differs in bit 3
+                bx_halve<8, 0x141>(pd, (k16 & 4) != 0);    // row_half_mirror: bit 2
+                bx_halve<4, 0x4E>(pd, (k16 & 2) != 0);     // quad_perm [2,3,0,1]: bit 1
+                bx_halve<2, 0xB1>(pd, (k16 & 1) != 0);     // quad_perm [1,0,3,2]: bit 0
+                const double d = pd[0] + __shfl_xor(pd[0], 16, 64);
+                if (l < 16 && ok && J0 + en.x <= i) {   // a lower slot of row i: its owner
+                    uRR[en.y] = d;
+                    const double2 l1l = loc1[en.y];
+                    const int cl = (int)l1l.y;
+                    const int f0 = cl == -2 ? loc_ptr[en.y] : 0, f1 = cl == -2 ? loc_ptr[en.y + 1] : (cl >= 0 ? 1 : 0);
+                    for (int f = f0; f < f1; ++f) {
+                        const int ci = cl >= 0 ? cl : loc_con[f];
+                        const double tot = (cl >= 0 ? l1l.x : loc_w[f]) * d;
+                        cvs[ci] = tot;
+                        const double dd = b[ci] - tot;
+                        acc[9] += dd * dd;
+                    }
+                }
+                if (kmax < 16) break;
+            }
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < kTxRows; ++w) {
+        const int i = I * kAuvT + grp + w * kTxG;
+        if (i < n) {
+            double2 *dst = reinterpret_cast<double2 *>(GP + x * gstride + foff + (long)i * ld) + l;
+            if (2 * l < ld) dst[0] = make_double2(g[w][0], g[w][1]);
+            if (2 * (l + kTxL) < ld) dst[kTxL] = make_double2(g[w][2], g[w][3]);
+        }
+    }
+    write_partials<10, kTxT>(acc, partC, pblk_off + blockIdx.x);
+}
+
 // Sharded long-row B over the tiles: S = C + A^*(M1) (k_tile_b1's slot epilogue, lorads_alm.c:38-57)
 // on the slots whose lower row is a halo row -- k_tile_b2 reads them as owned rows' upper entries;
 // their A(R_new R_new^T) belongs to the shard owning the lower row.
-__global__ void __launch_bounds__(kBlock) k_slot_sv(int nx, const int *__restrict__ sx, double *__restrict__ Sv,
+// sx == nullptr: the slots [s0, s0 + nx) (every slot of a cone, k_tile_bx's S); partZ: this
+// launch's partial blocks of stage B (pblk_off on) written as zeros, the partial slots it stands in for.
+__global__ void __launch_bounds__(kBlock) k_slot_sv(int nx, const int *__restrict__ sx, int s0, double *__restrict__ Sv,
                                                     const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
                                                     const int *__restrict__ slot_con, const double *__restrict__ slot_a,
                                                     const double2 *__restrict__ slot1, const double *__restrict__ rec,
                                                     const double *__restrict__ par, const double *__restrict__ ctrl,
-                                                    const double *__restrict__ ls_cur) {
+                                                    const double *__restrict__ ls_cur, double *__restrict__ partZ,
+                                                    int pblk_off) {
     if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
     const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
+    if (partZ && threadIdx.x < 10) partZ[threadIdx.x * kMaxPartialBlocks + pblk_off + blockIdx.x] = 0.0;
     for (int t = blockIdx.x * kBlock + threadIdx.x; t < nx; t += gridDim.x * kBlock) {
-        const int sl = sx[t];
+        const int sl = sx ? sx[t] : s0 + t;
         double svl = Craw[sl];
         const double2 s1l = slot1[sl];
         const int c1 = (int)s1l.y;
@@ -5257,10 +5422,19 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         if (tlb[k]) nblkB += pb[k].grid;
     }
     // long-row B over 2-D LDS tiles (k_tile_b1 / k_tile_b2, then k_wide_bf's epilogue blocks)
-    bool tbt[kMaxCones];
+    bool tbt[kMaxCones], tbx[kMaxCones];
     for (int k = 0; k < KL; ++k) {
         tbt[k] = !merge && !tlb[k] && pb[k].wide && W.GP && cone_of(k).sb_blocks > 0 && cone_of(k).sa_items > 0;
         if (tbt[k]) nblkB += pb[k].grid;
+    }
+    // r <= 128, LRS_TILE_BX=1: the single-pass k_tile_bx (S per slot by k_slot_sv first) instead
+    // of b1 + b2, its blocks' partials after k_wide_bf's (C5: 732 + 144 us against 447 + 400 us
+    // for the two-kernel form before the upper tile pairs skipped their dots; opt-in)
+    static const bool bx_off = !(getenv("LRS_TILE_BX") && getenv("LRS_TILE_BX")[0] == '1');
+    int offBX = nblkB;
+    for (int k = 0; k < KL; ++k) {
+        tbx[k] = tbt[k] && !bx_off && cone_of(k).ld <= kTxC;
+        if (tbx[k]) nblkB += cone_of(k).sb_blocks;
     }
     if (nblkB > kMaxPartialBlocks) {
         snprintf(g_err, sizeof(g_err), "stage B: %d partial blocks past %d", nblkB, kMaxPartialBlocks);
@@ -5491,7 +5665,25 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const DevCone &c = cone_of(k);
         const int grid = pb[k].grid;
         if (pb[k].small) { off += grid; continue; }
-        if (tbt[k]) {
+        if (tbx[k]) {
+            hipLaunchKernelGGL(k_slot_sv, dim3(grid), dim3(kBlock), 0, st, c.P, nullptr, c.slot_off,
+                               c.sa_S - c.slot_off, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,
+                               reinterpret_cast<const double2 *>(P.slot1), W.rec, W.par, ctrl_cur, ls_cur, W.partC, off);
+            LRS_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_tile_bx, dim3(c.sb_blocks), dim3(kTxT), 0, st, c.n, c.r, c.ld, c.foff,
+                               reinterpret_cast<const int2 *>(c.sb_blk), reinterpret_cast<const int2 *>(c.sb_tp),
+                               c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent), c.sa_S - c.slot_off, W.R, W.R2,
+                               W.GP, P.NRpad, ctrl_cur, ls_cur, c.sb_I0, W.uvt2, P.loc_ptr, P.loc_con, P.loc_w,
+                               reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.partC, offBX);
+            LRS_CHECK_LAUNCH();
+            offBX += c.sb_blocks;
+            LRS_LAYOUT_SWITCH(c.G, c.E, {
+                hipLaunchKernelGGL((k_wide_bf<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff, W.D,
+                                   W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], ctrl_cur, ls_cur, L, W.partC,
+                                   offBF, c.row0, P.ndense ? W.CR : nullptr, W.CD, W.GP, P.NRpad);
+            });
+            offBF += grid;
+        } else if (tbt[k]) {
             hipLaunchKernelGGL(k_tile_b1, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
                                reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, W.R, W.R2, W.uvt2,
                                c.sa_S - c.slot_off, P.Craw, P.slot_ptr,
@@ -5502,9 +5694,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
             LRS_CHECK_LAUNCH();
             if (c.sx_n > 0) {   // sharded: S on the halo rows' lower slots
                 hipLaunchKernelGGL(k_slot_sv, dim3(std::min(grid_elems(c.sx_n, 1), 2048)), dim3(kBlock), 0, st, c.sx_n,
-                                   c.sx_slot, c.sa_S - c.slot_off, P.Craw,
+                                   c.sx_slot, 0, c.sa_S - c.slot_off, P.Craw,
                                    P.slot_ptr, P.slot_con, P.slot_a,
-                                   reinterpret_cast<const double2 *>(P.slot1), W.rec, W.par, ctrl_cur, ls_cur);
+                                   reinterpret_cast<const double2 *>(P.slot1), W.rec, W.par, ctrl_cur, ls_cur, nullptr, 0);
                 LRS_CHECK_LAUNCH();
             }
             hipLaunchKernelGGL(k_tile_b2, dim3(c.sb_blocks * ((c.ld + kTbC - 1) / kTbC)), dim3(kRowBlock), 0, st, c.n, c.ld, c.foff,
