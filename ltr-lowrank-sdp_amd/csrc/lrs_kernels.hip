@@ -5430,10 +5430,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     // r <= 128, LRS_TILE_BX=1: the single-pass k_tile_bx (S per slot by k_slot_sv first) instead
     // of b1 + b2, its blocks' partials after k_wide_bf's (C5: 732 + 144 us against 447 + 400 us
     // for the two-kernel form before the upper tile pairs skipped their dots; opt-in)
-    static const bool bx_off = !(getenv("LRS_TILE_BX") && getenv("LRS_TILE_BX")[0] == '1');
     int offBX = nblkB;
     for (int k = 0; k < KL; ++k) {
-        tbx[k] = tbt[k] && !bx_off && cone_of(k).ld <= kTxC;
+        tbx[k] = tbt[k] && P.tile_bx && cone_of(k).ld <= kTxC;
         if (tbx[k]) nblkB += cone_of(k).sb_blocks;
     }
     if (nblkB > kMaxPartialBlocks) {
