@@ -473,12 +473,14 @@ def main():
                                           f"in {sec:.1f} s wall (OPENBLAS_NUM_THREADS=1)",
                                 "host": {"cpu_model": model, "threads_available": nthr}}
         # the reference's BLAS on every thread this process may use (its loop is single-threaded C;
-        # only BLAS calls can spread)
+        # only BLAS calls can spread), at most 16: the GPU box's CPU share for one GPU
+        # (OMP_NUM_THREADS / MAX_JOBS are 16 there; nproc shows the whole host)
         ta = min(nthr, 16)
         it2, sec2, _ = cpu_reference_rate(path, r, min(args.cpu_seconds, 10.0), threads=ta)
         line["cpu_baseline"]["all_cores"] = {"value": it2 / sec2, "threads": ta,
                                              "sample": f"{it2} inner iterations in {sec2:.1f} s wall "
-                                                       f"(OPENBLAS_NUM_THREADS={ta})"}
+                                                       f"(OPENBLAS_NUM_THREADS={ta}: the box's CPU share "
+                                                       f"for one GPU is 16 threads)"}
         if not args.no_eps:
             ref = cpu_reference_solve(path, ["--reoptLevel", "0", "--heuristicFactor", "10", "--phase1Tol", "1e-2"],
                                       timeout=600)

@@ -247,8 +247,9 @@ int lrs_debug_phase_times(lrs_ctx *ctx, unsigned long long *out, unsigned long l
  * constraints' sums).  Any number of SDP cones, each split alike; constraints may span row
  * blocks (shared: every holder sums its owned entries, the sums meet in an all-reduce);
  * a dense objective is held as each shard's owned row block of C with every row in the
- * halo.  The ADMM CG runs on owned rows with its dot products all-reduced; the Lanczos
- * of the dual infeasibility on owned rows with a vector halo.  DESIGN.md §6.  Every shard
+ * halo; long-row cones keep their 2-D tile stage kernels over the owned rows.  The ADMM CG
+ * runs on owned rows with its dot products all-reduced; the Lanczos of the dual
+ * infeasibility on owned rows with a vector halo.  DESIGN.md §6.  Every shard
  * must make the same calls in the same order (the collectives are matched by order). */
 /* RCCL: rank 0 creates the id (128 bytes) and broadcasts it; every rank then calls
  * lrs_shard_rccl on its own GPU (ncclCommInitRank is collective). */
