@@ -5427,9 +5427,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         tbt[k] = !merge && !tlb[k] && pb[k].wide && W.GP && cone_of(k).sb_blocks > 0 && cone_of(k).sa_items > 0;
         if (tbt[k]) nblkB += pb[k].grid;
     }
-    // r <= 128, LRS_TILE_BX=1: the single-pass k_tile_bx (S per slot by k_slot_sv first) instead
-    // of b1 + b2, its blocks' partials after k_wide_bf's (C5: 732 + 144 us against 447 + 400 us
-    // for the two-kernel form before the upper tile pairs skipped their dots; opt-in)
+    // r <= 128, LRS_TILE_BX=1 at upload: the single-pass k_tile_bx (S per slot by k_slot_sv
+    // first) instead of b1 + b2, its blocks' partials after k_wide_bf's (C5: 729 + 144 us against
+    // 451 + ~400 us for the two-kernel form; opt-in)
     int offBX = nblkB;
     for (int k = 0; k < KL; ++k) {
         tbx[k] = tbt[k] && P.tile_bx && cone_of(k).ld <= kTxC;

@@ -103,7 +103,7 @@ def test_sharded_c5_tiles_match_reference(mods, world, monkeypatch):
     check_trips(res, z, K)
 
 
-@pytest.mark.parametrize("name", ["mc_rand200", "theta40", "rsparse60", "theta25x3"])
+@pytest.mark.parametrize("name", ["mc_rand200", "theta40", "rsparse60", "mc_rand300w"])
 def test_single_pass_stage_b_matches_reference(mods, name, monkeypatch):
     """Stage B's long-row half in one pass over the tiles (k_tile_bx, LRS_TILE_BX=1: S R_new and
     A(R_new R_new^T) together, the dots through the transposed DPP butterfly), unsharded: the
