@@ -147,3 +147,23 @@ def test_single_pass_stage_b_c5(mods, world, monkeypatch):
     else:
         res = run_sharded(solver, lambda: solver.Solver(coo=coo), world, lambda sv: sv.alm_steps(K, **kw), path=3)
     check_trips(res, z, K)
+
+
+def test_rccl_transport_tiles_world1(mods, monkeypatch):
+    """The RCCL transport (a one-rank communicator; LRS_FORCE_SHARD=1 keeps the sharded
+    iteration with its halo exchange and all-reduces) over the tiled long-row stages on the C5
+    structure (m = 10^5, tiles forced): the reference's trips at 1e-9.  bench.py's `sharded` C5
+    leg drives the same calls on N GPUs."""
+    solver, inst = mods
+    z = np.load(os.path.join(GOLDEN, "steps_c5_m1e5.npz"))
+    monkeypatch.setenv("LRS_SLOT_TILES", "1")
+    monkeypatch.setenv("LRS_FORCE_SHARD", "1")
+    sv = solver.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(10000, int(z["m"]), 6, 5)))
+    sv.shard_rccl(1, 0, solver.comm_unique_id())
+    sv.set_kernel_path(3)
+    kw = {"reoptLevel": 0, "fixedRank": int(z["rank_flag"])}
+    K = min(3, max(int(k) for k in z["ks"] if z[f"K{int(k)}_trips"].shape[0] >= int(k)))
+    d = sv.alm_steps(K, **kw)
+    res = [(sv.shard_info(), (sv.tile_info(), sv.tile_used()), d)]
+    sv.close()
+    check_trips(res, z, K)
