@@ -312,7 +312,7 @@ def c5_cpu_sample(solver, local, seconds, cache):
             "gpu_it_s_same_file": gpu, "speedup_same_file": gpu / (it / sec) if it else None}
 
 
-def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=500):
+def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=500, all_legs=False):
     """ONE instance row-sharded over the `world` ranks through RCCL (lrs_shard_rccl): whole-
     instance ALM it/s, strong scaling.  The G81-like torus (n = 20 000, r = 64) always; at
     world > 1 also BASELINE config C5 (n = 10^4, m = 10^6, r = 128, the 2-D tile kernels on each
@@ -325,7 +325,7 @@ def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=5
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
     legs = [("g81", 50, steps)]
-    if world > 1:
+    if world > 1 or all_legs:
         legs += [("c5", 3, 20), ("torus2000", 5, 40)]
     out = {}
     for name, warm, k in legs:
@@ -392,6 +392,9 @@ def main():
     ap.add_argument("--no-c5b", action="store_true")
     ap.add_argument("--no-sharded", action="store_true")
     ap.add_argument("--sharded-timeout", type=float, default=300.0)
+    ap.add_argument("--sharded-all", action="store_true",
+                    help="the C5 and 2000^2-torus sharded legs at N = 1 too (with LRS_FORCE_SHARD=1: "
+                         "the sharded iteration over a one-rank RCCL communicator)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -562,7 +565,8 @@ def main():
         wd.daemon = True
         wd.start()
         try:
-            line["sharded"] = sharded_strong(solver, dist, world, rank_id, local, cache, replicas)
+            line["sharded"] = sharded_strong(solver, dist, world, rank_id, local, cache, replicas,
+                                             all_legs=args.sharded_all)
         except Exception as e:   # reported in the line, the headline stands
             line["sharded"] = {"error": repr(e)[:300]}
         wd.cancel()
