@@ -319,11 +319,6 @@ def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=5
     shard's owned rows, every row in every halo) and the 2000 x 2000 torus (n = 4*10^6, r = 16),
     whose one-GPU rates are config_c5.gpu_it_s and roofline_at_scale.it_s of the N = 1 line."""
     inst = importlib.import_module(PKG + ".instances")
-    uid = solver.comm_unique_id() if rank_id == 0 else None
-    if dist is not None:
-        box = [uid]
-        dist.broadcast_object_list(box, src=0)
-        uid = box[0]
     legs = [("g81", 50, steps)]
     if world > 1 or all_legs:
         legs += [("c5", 3, 20), ("torus2000", 5, 40)]
@@ -342,6 +337,12 @@ def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=5
             sv = solver.Solver(coo=inst.coo_arrays(inst.maxcut_torus_problem(2000, 2000, 2000)), device=local)
             kw = dict(fixedRank=16, reoptLevel=0)
             wl = "MaxCut torus 2000x2000, n=m=4e6, --fixedRank 16"
+        # a fresh RCCL id per communicator (an id's bootstrap root ends with its communicator)
+        uid = solver.comm_unique_id() if rank_id == 0 else None
+        if dist is not None:
+            box = [uid]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
         sv.shard_rccl(world, rank_id, uid)
         info = sv.shard_info()
         tiles = sv.tile_info()
