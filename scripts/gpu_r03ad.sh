@@ -12,4 +12,7 @@ for v in sharded unsharded; do
   LRS_FORCE_SHARD=1 timeout -k 10 300 python3 $R/scripts/sharded_c5_probe.py $v > $O/$v.log 2>&1 || { tail -5 $O/$v.log; exit 1; }
   grep -E "info" $O/$v.log
 done
+
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/scripts/c5_probe.py 10000 1000000 128 20 > $O/c5.log 2>&1) || { tail -5 $O/c5.log; exit 1; }
+grep -E "alm|stages" $O/c5.log
 echo done
