@@ -345,6 +345,9 @@ def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=5
             uid = box[0]
         sv.shard_rccl(world, rank_id, uid)
         info = sv.shard_info()
+        comm_ranks = sv.comm_ranks()
+        if world > 1 and comm_ranks != world:
+            raise RuntimeError(f"RCCL communicator counts {comm_ranks} ranks, expected {world}")
         tiles = sv.tile_info()
         load_s = time.perf_counter() - t0
         clock = {}
@@ -365,7 +368,7 @@ def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=5
         _, t_max = replicas.aggregate(dist, o["done"], clock["t1"] - clock["t0"])
         out[name] = {"workload": f"{wl}, ONE instance row-sharded over {world} GPU(s)", "it_s": o["done"] / t_max,
                      "steps": o["done"], "n_gpus": world, "scaling": "strong", "load_sec": load_s,
-                     "rank0_rows": info[3], "rank0_halo_rows": info[4], "slot_tiles_built": bool(tiles[1]),
+                     "comm_ranks": comm_ranks, "rank0_rows": info[3], "rank0_halo_rows": info[4], "slot_tiles_built": bool(tiles[1]),
                      "tile_kernels_ran": used}
     res = dict(out["g81"])
     res["transport"] = "RCCL (ncclSend/Recv halo, ncclAllReduce totals)"
@@ -375,9 +378,82 @@ def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=5
     return res
 
 
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` with no external launcher (WORLD_SIZE unset): start N fresh worker
+    processes of this script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in
+    their environment -- the same environment torch.distributed.run gives them -- before this
+    parent touches the GPU (it never does).  Rank 0's stdout is forwarded line by line and its
+    JSON line checked for n_gpus == N; if a rank fails, the others are ended (their PIDs) and
+    the exit status is the first failure's."""
+    import socket
+    import threading
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+    lines = []
+
+    def pump():
+        for ln in procs[0].stdout:
+            lines.append(ln)
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench.py launcher: rank {r} exited with {c}; ending the other ranks", file=sys.stderr)
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    th.join(timeout=10)
+    js = [ln for ln in lines if ln.lstrip().startswith("{")]
+    if rc == 0:
+        if not js:
+            print("bench.py launcher: rank 0 printed no result line", file=sys.stderr)
+            return 5
+        if json.loads(js[-1]).get("n_gpus") != n:
+            print(f"bench.py launcher: result line does not report n_gpus = {n}", file=sys.stderr)
+            return 5
+    return rc
+
+
+def dry_run_line(args, world, rank_id, dist, replicas):
+    """--dry-run: the launch and timing protocol only (no GPU, no solver): every rank joins the
+    process group, meets the barriers around an empty timed region and contributes to the
+    (sum, max) aggregate, so the multi-rank plumbing is testable on a CPU host with gloo."""
+    replicas.barrier_sync(dist)
+    t0 = time.perf_counter()
+    replicas.barrier_sync(dist)
+    dt = time.perf_counter() - t0
+    joined, t_max = replicas.aggregate(dist, 1, dt)   # each rank counts itself once
+    return {"metric": "ALM iters/sec, MaxCut G67 (torus 100x100 +-1, n=m=10000), fixed default rank",
+            "value": 0.0, "unit": "ALM inner iterations/s", "n_gpus": world, "steps": 0, "warmup": 0,
+            "ms_per_step": t_max * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "dry run: launch and timing protocol only, no GPU work",
+            "config": {"workload": "none (dry run)", "parallelism": f"replicas x{world} (instance-level, weak)"},
+            "dry_run": True, "backend": dist.get_backend() if dist is not None else None,
+            "ranks_aggregated": int(joined)}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node, one process each (default: WORLD_SIZE, else 1); without an "
+                         "external launcher the script starts the N rank processes itself")
     ap.add_argument("--steps", type=int, default=3000)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--rows", type=int, default=100)
@@ -396,18 +472,36 @@ def main():
     ap.add_argument("--sharded-all", action="store_true",
                     help="the C5 and 2000^2-torus sharded legs at N = 1 too (with LRS_FORCE_SHARD=1: "
                          "the sharded iteration over a one-rank RCCL communicator)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch + barrier/aggregate protocol only over gloo, no GPU (CPU tests)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world) if env_world is not None else 1
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE = {world}", file=sys.stderr)
+        sys.exit(2)
     rank_id = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if args.dry_run:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl")
     replicas = importlib.import_module(PKG + ".replicas")
+    if args.dry_run:
+        line = dry_run_line(args, world, rank_id, dist, replicas)
+        if rank_id == 0:
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     solver = importlib.import_module(PKG + ".solver")
     cache = os.path.join(ROOT, ".bench_instances")
@@ -548,33 +642,38 @@ def main():
         line["config_c5"] = config_c5(solver, local, cpu_seconds=0.0 if args.no_cpu else 20.0, cache=cache)
     if rank_id == 0 and world == 1 and not args.no_c5b:
         line["config_c5b"] = config_c5b(solver, local, ref_densec=ref_densec_rates())
+    failed = 0
     if not args.no_sharded:
         # a watchdog keeps a stuck collective from swallowing the result line
         import threading
 
         def fire():
-            # a stuck collective: the headline above is measured and stands; the sharded section
+            # a stuck collective: the headline above is measured and printed, the sharded section
             # is reported as failed in the line and on stderr, and every rank leaves without
-            # waiting on the communicator
+            # waiting on the communicator -- with a non-zero status, so the hang reads as a failure
             if rank_id == 0:
                 line["sharded"] = {"error": f"no result within {args.sharded_timeout:.0f} s"}
                 print(json.dumps(line), flush=True)
             print(f"bench.py rank {rank_id}: sharded section hung for {args.sharded_timeout:.0f} s", file=sys.stderr,
                   flush=True)
-            os._exit(0)
+            os._exit(3)
         wd = threading.Timer(args.sharded_timeout, fire)
         wd.daemon = True
         wd.start()
         try:
             line["sharded"] = sharded_strong(solver, dist, world, rank_id, local, cache, replicas,
                                              all_legs=args.sharded_all)
-        except Exception as e:   # reported in the line, the headline stands
+        except Exception as e:   # reported in the line (the headline stands) and in the exit status
             line["sharded"] = {"error": repr(e)[:300]}
+            print(f"bench.py rank {rank_id}: sharded section failed: {e!r}", file=sys.stderr, flush=True)
+            failed = 4
         wd.cancel()
     if rank_id == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if failed:
+        sys.exit(failed)
 
 
 if __name__ == "__main__":

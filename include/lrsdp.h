@@ -14,7 +14,9 @@
  * binary built on top of this library.
  *
  * Conventions: every function returns 0 on success and a negative code on
- * failure (message via lrs_last_error()); no function calls exit().  All
+ * failure (message via lrs_last_error()); no function calls exit().  A NULL
+ * context, a context with no problem loaded (or, for the operators, no ranks
+ * set) and a NULL required pointer are failures of that kind, never a crash.  All
  * arrays crossing the boundary are host memory, column-major n x r per cone
  * (the reference layout, lorads_alg_common.c:62-68), cones concatenated in
  * cone order.  Device memory is owned by the context.
@@ -110,15 +112,30 @@ int lrs_op_line_search(lrs_ctx *ctx, double rho, double *tau, int *root_num);
  * the ring (S0,Y0 = newest pair with beta_new; S1,Y1 = older pair with beta_old),
  * node_num in {0,1,2}; result in D. */
 int lrs_op_lbfgs(lrs_ctx *ctx, int node_num, double beta_new, double beta_old);
-/* LORADSUpdateSDPVarOne (lorads_admm.c:564) for U of cone 0 with V fixed; state:
- * LAMBDA and A(UV^T) from the current U, V.  Returns CG iterations and the RHS. */
-int lrs_op_admm_half(lrs_ctx *ctx, double rho, double cg_tol, int cg_maxit, int *cg_iters, double *rhs);
+/* LORADSInitConstrValAll + LORADSInitConstrValSum (lorads_alg_common.c:104-229) on (U, V):
+ * the per-cone A_k(sym UV^T) and their sum CVS that the ADMM half-steps read and update. */
+int lrs_op_admm_constr(lrs_ctx *ctx);
+/* One ADMM half-step of LORADSUpdateSDPVar (lorads_alg_common.c:298-326) for cone `cone`:
+ * LORADSUpdateSDPVarOne (lorads_admm.c:564-616) solving side 0 = U with V fixed or side 1 =
+ * V with U fixed (RHS -(S Y - rho Y)/rho with S = C + A*(rho (CVS - A_k(UV^T) - b) - LAMBDA),
+ * CG at cg_tol / cg_maxit, warm-started from the current factor), then the cone's
+ * constraint-value refresh (CVS -= A_k, A_k <- A_k(sym UV^T), CVS += A_k).  Calling it for
+ * (0, 0), (0, 1), (1, 0), (1, 1), ... after lrs_op_admm_constr is the reference's sweep.
+ * cg_iters (may be NULL): this solve's CG iterations; rhs (may be NULL): the cone's
+ * right-hand side, column-major n_k x r_k. */
+int lrs_op_admm_half(lrs_ctx *ctx, int cone, int side, double rho, double cg_tol, int cg_maxit, int *cg_iters,
+                     double *rhs);
+/* LORADSUpdateDualVar (lorads_alg_common.c:511-524): LAMBDA += rho (b - CVS). */
+int lrs_op_dual_update(lrs_ctx *ctx, double rho);
 /* Gram R^T R of cone k (r x r, row-major) */
 int lrs_op_gram(lrs_ctx *ctx, int cone, int which, double *gram);
 /* Dual infeasibility of the current multipliers (calculate_dual_infeasibility_solver,
  * data/lorads_solver.c:1396-1426): l1 = sum_k |min(lambda_min(S_k), 0)| / scaleObjHis /
  * (||C||_1 + 1) with S = C - sum_i lambda_i A_i; lam_min[k] per cone (may be NULL).  The
- * reference's ARPACK dsaupd is replaced by a device Lanczos with full reorthogonalisation. */
+ * reference's ARPACK dsaupd "SA" (ncv 40, tol 1e-2, data/lorads_sdp_conic.c:1636-1699) is
+ * replaced by a device thick-restart Lanczos with dsaupd's semantics: a basis of 40 vectors,
+ * 20 Ritz vectors kept per restart, two-pass classical Gram-Schmidt, convergence when the
+ * Ritz residual is <= tol * max(eps^(2/3), |theta|), at most 600 restarts. */
 int lrs_op_dual_infeasibility(lrs_ctx *ctx, double *l1, double *lam_min);
 
 /* ---- whole solves ---- */
@@ -262,6 +279,9 @@ void lrs_loopback_destroy(lrs_loopback *g);
 int lrs_shard_loopback(lrs_ctx *ctx, lrs_loopback *g, int rank);
 /* world, rank, first global row, owned rows, halo rows of this context (1, 0, 0, n, 0 unsharded) */
 int lrs_shard_info(lrs_ctx *ctx, int *world, int *rank, int *row0, int *nown, int *nhalo);
+/* ranks the context's transport counts itself (RCCL: ncclCommCount; loopback: its group's
+ * world; 1 unsharded), so a launcher can check that every GPU joined the communicator */
+int lrs_shard_comm_ranks(lrs_ctx *ctx, int *count);
 /* Host-only (no device, no context) view of the row partition of a sharded solve of the
    instance at `path`: counts[8] = {n_global, first owned global row, owned rows, local rows
    (owned + halo), send rows (all peers), shared constraints, local constraints, world}, then

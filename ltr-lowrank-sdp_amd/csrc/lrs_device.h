@@ -124,6 +124,7 @@ struct DevCone {
     // the lower pattern in the same 2-D tiles (k_tile_a, stage A of the long-row path): items
     // {row0, col0, begin, end}, per tiled slot its local (row, col) 16:16 and its global slot
     int sa_items = 0;
+    int sa_n = 0;                        // tiled slots (sa_slot's length)
     int *sa_item = nullptr;
     unsigned *sa_pq = nullptr;
     int *sa_slot = nullptr;

@@ -140,10 +140,28 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
     {
         const char *ek = getenv("LRS_CONST_C");
         const char *ev = getenv("LRS_DENSE_C");
-        if (allow_dense && !ek && !(ev && ev[0] == '0')) {
+        const char *es = getenv("LRS_SMALL");
+        if (allow_dense && !ek && !(ev && ev[0] == '0') && !(es && atoi(es) == 0)) {
             bool ok = true, any = false;
             long N = 0, Ptot = 0;
-            int ldmax = 0;
+            int ldmax = 0, ldmin = 1 << 30, nconst = 0;
+            // the single-workgroup loop's own gates (lrs_solver.cpp use_small, lrs_kernels.hip
+            // small_alm_args) that the data decides: at most kSmallAutoMaxGlobal multi-slot
+            // constraints (LRS_SMALL=1 lifts it, as there), at most kSmallAutoMaxConst constant
+            // cones, one row layout for every cone at its largest reachable rank
+            if (!(es && atoi(es) == 1)) {
+                std::vector<int> cnt(m + 1, 0);
+                for (size_t e = 0; e < raw.size(); ++e) {
+                    if (raw[e].con == 0) continue;
+                    if (e > 0 && raw[e - 1].cone == raw[e].cone && raw[e - 1].con == raw[e].con &&
+                        raw[e - 1].row == raw[e].row && raw[e - 1].col == raw[e].col)
+                        continue;   // a duplicate of the previous entry (merged below)
+                    cnt[raw[e].con]++;
+                }
+                long mg = 0;
+                for (int i = 1; i <= m; ++i) mg += cnt[i] > 1 ? 1 : 0;
+                if (mg > kSmallAutoMaxGlobal) ok = false;
+            }
             size_t e0 = 0;
             for (int k = 0; k < K && ok; ++k) {
                 size_t e1 = e0;
@@ -182,12 +200,15 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
                     }
                     if (!ok || v0 == 0.0) { ok = false; break; }
                     any = true;
+                    if (++nconst > kSmallAutoMaxConst) { ok = false; break; }
                 }
                 const int rmax = std::min((int)std::sqrt(2.0 * nnzRows) + 1, n);
-                ldmax = std::max(ldmax, choose_layout(std::max(1, rmax)).ld);
+                const int ldk = choose_layout(std::max(1, rmax)).ld;
+                ldmax = std::max(ldmax, ldk);
+                ldmin = std::min(ldmin, ldk);
                 e0 = e1;
             }
-            auto_const = ok && any && ldmax <= 64 &&
+            auto_const = ok && any && ldmax <= 64 && ldmin == ldmax &&
                          (2L * N * (ldmax + 2) + Ptot) * (long)sizeof(double) <= kSmallLdsBudget;
         }
     }
@@ -986,6 +1007,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                     t0 = t + 1;
                 }
                 d.sa_items = (int)(item.size() / 4);
+                d.sa_n = (int)Po;
                 if (!dput(&d.sa_item, item, err) || !dput(&d.sa_pq, pq, err) || !dput(&d.sa_slot, sl, err))
                     return false;
                 // symmetric adjacency of the owned rows by (row tile I, column tile J): counting

@@ -215,6 +215,8 @@ struct ShardComm {
     virtual int halo(lrs_ctx *c, double *D, hipStream_t st) = 0;
     // the same for one vector x of cone k's local rows (a Lanczos vector)
     virtual int halo_vec(lrs_ctx *c, int k, double *x, hipStream_t st) = 0;
+    // ranks the transport itself counts (RCCL: ncclCommCount; loopback: its world)
+    virtual int ranks(int *n) = 0;
 };
 static bool sharded(const lrs_ctx *c) { return c->comm != nullptr; }
 static int cone_n_global(const lrs_ctx *c, int k) {
@@ -324,6 +326,10 @@ struct RcclComm : ShardComm {
         NCCLC(ncclGroupEnd());
         return 0;
     }
+    int ranks(int *n) override {
+        NCCLC(ncclCommCount(comm, n));
+        return 0;
+    }
 };
 
 // One-process loopback transport for tests: the shards are contexts on one GPU driven by
@@ -354,6 +360,7 @@ struct LoopComm : ShardComm {
     double *dsum = nullptr;
     int dsum_len = 0;
     ~LoopComm() override { if (dsum) (void)hipFree(dsum); }
+    int ranks(int *n) override { *n = g->world; return 0; }
     int pre(hipStream_t st) {
         HIPC(hipEventRecord(g->ev_pre[rank], st));
         g->barrier();
@@ -2033,6 +2040,19 @@ static int refresh_cone(lrs_ctx *c, int k) {   // lorads_alg_common.c:310-314
     return 0;
 }
 
+// LORADSInitConstrValAll + LORADSInitConstrValSum (lorads_alg_common.c:104-229) on (U, V):
+// per-cone A_k(sym UV^T) into cvc[k] and their sum into cvs
+static int admm_init_constr(lrs_ctx *c) {
+    DevProblem &P = c->dp;
+    OPC(launch_fill(P.m, 0.0, c->W.cvs, c->st));
+    for (int k = 0; k < P.K; ++k) {
+        OPC(launch_auv_con(P, k, 0, c->W.U, c->W.V, 1.0, 0, c->W.cvc + (long)k * P.m, nullptr, nullptr, c->st));
+        OPC(sync_shared(P, c->W.cvc + (long)k * P.m, c->st));
+        OPC(launch_axpby(P.m, 1.0, c->W.cvc + (long)k * P.m, 1.0, c->W.cvs, c->st));
+    }
+    return 0;
+}
+
 static int admm_update_var(lrs_ctx *c, double rho, double tol, int maxit) {
     for (int k = 0; k < c->dp.K; ++k) {
         if (update_var_one(c, k, c->W.U, c->W.V, rho, tol, maxit)) return -1;
@@ -2079,16 +2099,7 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
     const double orig = now_s();
     st.rho = std::min(st.rho, p->rhoMax);
     c->cgIterTotal = 0;
-    // LORADSInitConstrValAll(U,V) + Sum
-    {
-        DevProblem &P = c->dp;
-        OPC(launch_fill(P.m, 0.0, c->W.cvs, c->st));
-        for (int k = 0; k < P.K; ++k) {
-            OPC(launch_auv_con(P, k, 0, c->W.U, c->W.V, 1.0, 0, c->W.cvc + (long)k * P.m, nullptr, nullptr, c->st));
-            OPC(sync_shared(P, c->W.cvc + (long)k * P.m, c->st));
-            OPC(launch_axpby(P.m, 1.0, c->W.cvc + (long)k * P.m, 1.0, c->W.cvs, c->st));
-        }
-    }
+    if (admm_init_constr(c)) return -1;
     if (admm_eval(c)) return -1;
     st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.gap = c->dimGap; st.pinf1 = c->dimPinf;
     st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
@@ -2349,7 +2360,30 @@ static int reopt(lrs_ctx *c, lrs_params *p, AlmState &alm, AdmmState &admm, doub
 // ------------------------------------------------------------------------
 extern "C" {
 
+// The error contract of include/lrsdp.h: a NULL context, a context without a problem, without
+// solver state (ranks set), or a NULL required pointer returns -1 with lrs_last_error() set
+#define LRS_NEED_CTX(c)                                                   \
+    do {                                                                  \
+        if (!(c)) { set_err("%s: null context", __func__); return -1; }   \
+        bind(c);                                                          \
+    } while (0)
+#define LRS_NEED_LOADED(c)                                                                \
+    do {                                                                                  \
+        LRS_NEED_CTX(c);                                                                  \
+        if (!(c)->loaded) { set_err("%s: no problem loaded", __func__); return -1; }      \
+    } while (0)
+#define LRS_NEED_STATE(c)                                                                         \
+    do {                                                                                          \
+        LRS_NEED_LOADED(c);                                                                       \
+        if (!(c)->walloc) { set_err("%s: no solver state (ranks not set)", __func__); return -1; } \
+    } while (0)
+#define LRS_NEED_ARG(x)                                                          \
+    do {                                                                         \
+        if (!(x)) { set_err("%s: null argument %s", __func__, #x); return -1; }  \
+    } while (0)
+
 void lrs_params_default(lrs_params *p) {   // main.c:56-86
+    if (!p) return;
     memset(p, 0, sizeof(*p));
     p->initRho = 0.0; p->rhoMax = 5000.0; p->rhoCellingALM = 1e8; p->rhoCellingADMM = 5000.0 * 200;
     p->maxALMIter = 200; p->maxADMMIter = 10000; p->timesLogRank = 2.0; p->fixedRank = -1; p->initRank = -1;
@@ -2364,6 +2398,8 @@ const char *lrs_last_error(void) { return g_lrs_err.c_str(); }
 const char *lrs_version(void) { return "lrsdp-mi355x 0.1 (gfx950)"; }
 
 int lrs_ctx_create(int device, lrs_ctx **out) {
+    LRS_NEED_ARG(out);
+    *out = nullptr;
     lrs_ctx *c = new lrs_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess) { set_err("hipSetDevice(%d) failed", device); delete c; return -1; }
@@ -2387,8 +2423,7 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
 }
 
 int lrs_set_kernel_path(lrs_ctx *c, int path) {
-    if (c) bind(c);
-    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    LRS_NEED_LOADED(c);
     if (path < 0 || path > 4) {
         set_err("kernel path %d: expected 0 (auto), 1 (general), 2 (general, bandwidth regime), 3 (+ long-row kernels) "
                 "or 4 (the single-workgroup inner loop where it fits)", path);
@@ -2402,26 +2437,24 @@ int lrs_set_kernel_path(lrs_ctx *c, int path) {
 }
 
 int lrs_op_dual_infeasibility(lrs_ctx *c, double *l1, double *lam_min) {
-    if (c) bind(c);
-    if (!c || !c->loaded || !c->walloc) { set_err("no solver state"); return -1; }
-    if (!l1) { set_err("null argument"); return -1; }
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(l1);
     return dual_infeasibility(c, l1, lam_min);
 }
 
 int lrs_get_kernel_path(lrs_ctx *c, int *used) {
-    if (c) bind(c);
-    if (!c || !used) { set_err("null argument"); return -1; }
+    LRS_NEED_CTX(c);
+    LRS_NEED_ARG(used);
     *used = c->loaded ? c->dp.last_path : -1;
     return 0;
 }
 
 int lrs_set_log_path(lrs_ctx *c, const char *path) {
-    if (c) bind(c);
+    LRS_NEED_CTX(c);
+    LRS_NEED_ARG(path);
     if (c->logfp) fclose(c->logfp);
     c->logfp = fopen(path, "w");
     if (!c->logfp) { set_err("cannot open log %s", path); return -1; }
-    size_t sl = std::string(path).find_last_of('/');
-    (void)sl;
     return 0;
 }
 
@@ -2446,7 +2479,8 @@ void lrs_ctx_destroy(lrs_ctx *c) {
 }
 
 int lrs_load_sdpa(lrs_ctx *c, const char *path, double *read_seconds) {
-    if (c) bind(c);
+    LRS_NEED_CTX(c);
+    LRS_NEED_ARG(path);
     const double t0 = now_s();
     std::string err;
     HostProblem hp;
@@ -2464,8 +2498,10 @@ int lrs_load_sdpa(lrs_ctx *c, const char *path, double *read_seconds) {
 
 int lrs_load_coo(lrs_ctx *c, int m, int nblk, const int *dims, const double *b, long nnz, const int *con,
                  const int *blk, const int *row, const int *col, const double *val) {
-    if (c) bind(c);
-    if (!c) { set_err("null ctx"); return -1; }
+    LRS_NEED_CTX(c);
+    LRS_NEED_ARG(dims);
+    if (m > 0) LRS_NEED_ARG(b);
+    if (nnz > 0 && (!con || !blk || !row || !col || !val)) { set_err("lrs_load_coo: null entry array"); return -1; }
     std::string err;
     HostProblem hp;
     if (!build_problem_coo(m, nblk, dims, b, nnz, con, blk, row, col, val, hp, err)) {
@@ -2483,11 +2519,11 @@ int lrs_load_coo(lrs_ctx *c, int m, int nblk, const int *dims, const double *b, 
 }
 
 int lrs_auut_bytes(lrs_ctx *c, double *bytes) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(bytes);
     // A(U U^T) over constraint entries (SURVEY.md §8(d) B_A with delta = 1): the factor
     // rows touched (each row once when distinct), per entry con_slot + con_w + slot
     // coordinates (16 B), con_ptr, and the m outputs.
-    if (!c || !c->loaded || !c->walloc) { set_err("no solver state"); return -1; }
     double by = 0;
     for (int k = 0; k < c->dp.K; ++k) {
         const HostCone &hc = c->hp.cones[k];
@@ -2506,12 +2542,12 @@ int lrs_auut_bytes(lrs_ctx *c, double *bytes) {
 }
 
 int lrs_stage_bytes(lrs_ctx *c, double *bytes) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(bytes);
     // Algorithmic HBM bytes per launch of the split-iteration stages:
     // every array the stage must touch, once, at its unpadded size; L-BFGS with two
     // pairs; int32 indices, FP64 values.  n, r per cone; P lower slots; adjacency
     // entries A = 2P - n_diag; Z constraint entries; m constraints (m_l local).
-    if (!c || !c->loaded || !c->walloc) { set_err("no solver state"); return -1; }
     double a = 0, g = 0, bb = 0;
     const DevProblem &P = c->dp;
     for (int k = 0; k < P.K; ++k) {
@@ -2535,8 +2571,7 @@ int lrs_stage_bytes(lrs_ctx *c, double *bytes) {
 }
 
 int lrs_problem_info(lrs_ctx *c, int *m, int *ncones, int *dims, long *nslots, long *nnzc) {
-    if (c) bind(c);
-    if (!c->loaded) { set_err("no problem loaded"); return -1; }
+    LRS_NEED_LOADED(c);
     if (m) *m = c->hp.m;
     if (ncones) *ncones = c->hp.K;
     if (dims) for (int k = 0; k < c->hp.K; ++k) dims[k] = c->hp.cones[k].n;
@@ -2546,8 +2581,7 @@ int lrs_problem_info(lrs_ctx *c, int *m, int *ncones, int *dims, long *nslots, l
 }
 
 int lrs_tile_info(lrs_ctx *c, int *auv, int *slot) {
-    if (c) bind(c);
-    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    LRS_NEED_LOADED(c);
     int a = 0, sl = 0;
     for (int k = 0; k < c->dp.K; ++k) {
         a |= c->dp.cones[k].auv_items > 0;
@@ -2559,15 +2593,15 @@ int lrs_tile_info(lrs_ctx *c, int *auv, int *slot) {
 }
 
 int lrs_tile_used(lrs_ctx *c, int *used) {
-    if (c) bind(c);
-    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    LRS_NEED_LOADED(c);
     if (used) *used = c->dp.last_tiles;
     return 0;
 }
 
 int lrs_determine_rank(lrs_ctx *c, const lrs_params *p, int *ranks_out) {
-    if (c) bind(c);
-    if (!c->loaded) { set_err("no problem loaded"); return -1; }
+    LRS_NEED_LOADED(c);
+    LRS_NEED_ARG(p);
+    LRS_NEED_ARG(ranks_out);
     std::vector<int> r, rm;
     determine_rank(c, p, r, rm);
     for (int k = 0; k < c->hp.K; ++k) ranks_out[k] = r[k];
@@ -2575,43 +2609,44 @@ int lrs_determine_rank(lrs_ctx *c, const lrs_params *p, int *ranks_out) {
 }
 
 int lrs_set_rank(lrs_ctx *c, const int *ranks) {
-    if (c) bind(c);
-    if (!c->loaded) { set_err("no problem loaded"); return -1; }
+    LRS_NEED_LOADED(c);
+    LRS_NEED_ARG(ranks);
     std::vector<int> r(ranks, ranks + c->hp.K);
     c->rank_max = r;
     return alloc_work(c, r);
 }
 int lrs_get_rank(lrs_ctx *c, int *ranks) {
-    if (c) bind(c);
+    LRS_NEED_LOADED(c);
+    LRS_NEED_ARG(ranks);
     for (size_t k = 0; k < c->rank.size(); ++k) ranks[k] = c->rank[k];
     return 0;
 }
 
 int lrs_factor_set(lrs_ctx *c, int which, const double *colmajor) {
-    if (c) bind(c);
-    if (!c->walloc) { set_err("ranks not set"); return -1; }
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(colmajor);
     double *d = factor_ptr(c, which);
     if (!d) { set_err("bad factor id"); return -1; }
     return factor_put(c, d, colmajor);
 }
 int lrs_factor_get(lrs_ctx *c, int which, double *colmajor) {
-    if (c) bind(c);
-    if (!c->walloc) { set_err("ranks not set"); return -1; }
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(colmajor);
     double *d = factor_ptr(c, which);
     if (!d) { set_err("bad factor id"); return -1; }
     return factor_fetch(c, d, colmajor);
 }
 int lrs_vec_set(lrs_ctx *c, int which, const double *v) {
-    if (c) bind(c);
-    if (!c->walloc) { set_err("ranks not set"); return -1; }
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(v);
     double *d = vec_ptr(c, which);
     if (!d) { set_err("bad vector id"); return -1; }
     HIPC(h2d_sync(c, d, v, sizeof(double) * c->dp.m));
     return 0;
 }
 int lrs_vec_get(lrs_ctx *c, int which, double *v) {
-    if (c) bind(c);
-    if (!c->walloc) { set_err("ranks not set"); return -1; }
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(v);
     double *d = vec_ptr(c, which);
     if (!d) { set_err("bad vector id"); return -1; }
     HIPC(hipStreamSynchronize(c->st));
@@ -2620,7 +2655,7 @@ int lrs_vec_get(lrs_ctx *c, int which, double *v) {
 }
 
 int lrs_op_q12(lrs_ctx *c, double *q1, double *p1, double *q2, double *p2) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
     DevWork &W = c->W;
     DevProblem &P = c->dp;
     // q1, q2 and p1, p2 (a dense objective's <R, C D>, <D, C D> included) with the finals the
@@ -2636,7 +2671,7 @@ int lrs_op_q12(lrs_ctx *c, double *q1, double *p1, double *q2, double *p2) {
 }
 
 int lrs_op_constr_rr(lrs_ctx *c, double *cvs, double *pinf, double *pobj) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
     double pi, ob;
     if (op_constr_xx(c, c->W.R, nullptr, &pi, &ob)) return -1;
     if (pinf) *pinf = pi;
@@ -2649,7 +2684,7 @@ int lrs_op_constr_rr(lrs_ctx *c, double *cvs, double *pinf, double *pobj) {
 }
 
 int lrs_op_grad(lrs_ctx *c, double rho, double *lag) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
     double l;
     if (op_grad(c, rho, &l)) return -1;
     if (lag) *lag = l;
@@ -2657,7 +2692,7 @@ int lrs_op_grad(lrs_ctx *c, double rho, double *lag) {
 }
 
 int lrs_op_line_search(lrs_ctx *c, double rho, double *tau, int *root_num) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
     double par[P_NPAR] = {0};
     par[P_RHO] = rho;
     par[P_ENDTAU] = 1e-16;
@@ -2672,7 +2707,7 @@ int lrs_op_line_search(lrs_ctx *c, double rho, double *tau, int *root_num) {
 }
 
 int lrs_op_lbfgs(lrs_ctx *c, int node_num, double beta_new, double beta_old) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
     // White-box test of the fused direction kernel: ring slot 0 = newest pair
     // (S0, Y0, beta_new), slot 1 = older pair (S1, Y1, beta_old), gradient G[gcur].
     if (node_num < 0 || node_num > 2) { set_err("node_num must be 0..2"); return -1; }
@@ -2701,31 +2736,51 @@ int lrs_op_lbfgs(lrs_ctx *c, int node_num, double beta_new, double beta_old) {
     return 0;
 }
 
-int lrs_op_admm_half(lrs_ctx *c, double rho, double cg_tol, int cg_maxit, int *cg_iters, double *rhs) {
-    if (c) bind(c);
+int lrs_op_admm_constr(lrs_ctx *c) {
+    LRS_NEED_STATE(c);
+    if (admm_init_constr(c)) return -1;
+    HIPC(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int lrs_op_admm_half(lrs_ctx *c, int cone, int side, double rho, double cg_tol, int cg_maxit, int *cg_iters,
+                     double *rhs) {
+    LRS_NEED_STATE(c);
     DevProblem &P = c->dp;
-    OPC(launch_fill(P.m, 0.0, c->W.cvs, c->st));
-    for (int k = 0; k < P.K; ++k) {
-        OPC(launch_sddmm(P, k, 0, c->W.U, c->W.V, c->W.uvt2, nullptr, c->W.part, 0, nullptr, c->st));
-        OPC(launch_gather_cone(P, k, c->W.uvt2, c->W.cvc + (long)k * P.m, c->st));
-        OPC(launch_axpby(P.m, 1.0, c->W.cvc + (long)k * P.m, 1.0, c->W.cvs, c->st));
-    }
-    c->cgIterCone.assign(P.K, 0);
-    if (update_var_one(c, 0, c->W.U, c->W.V, rho, cg_tol, cg_maxit)) return -1;
-    if (cg_iters) *cg_iters = (int)c->cgIterCone[0];
+    if (cone < 0 || cone >= P.K) { set_err("lrs_op_admm_half: cone %d of %d", cone, P.K); return -1; }
+    if (side != 0 && side != 1) { set_err("lrs_op_admm_half: side %d (0 = U, 1 = V)", side); return -1; }
+    if (!(rho > 0.0) || cg_maxit < 1) { set_err("lrs_op_admm_half: rho %g, cg_maxit %d", rho, cg_maxit); return -1; }
+    // LORADSUpdateSDPVar's half-step for one cone (lorads_alg_common.c:303-314 for U, :316-324
+    // for V): solve the side with the other fixed, then the cone's constraint-value refresh
+    double *X = side ? c->W.V : c->W.U;
+    const double *Y = side ? c->W.U : c->W.V;
+    c->cgIterCone[cone] = 0;
+    if (update_var_one(c, cone, X, Y, rho, cg_tol, cg_maxit)) return -1;
+    if (refresh_cone(c, cone)) return -1;
+    if (cg_iters) *cg_iters = (int)c->cgIterCone[cone];
+    HIPC(hipStreamSynchronize(c->st));
     if (rhs) {
-        std::vector<double> h(c->dp.NRpad);
-        HIPC(hipStreamSynchronize(c->st));
-        HIPC(hipMemcpy(h.data(), c->W.cg_b, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
-        const DevCone &d = P.cones[0];
+        const DevCone &d = P.cones[cone];
+        std::vector<double> h((size_t)d.n * d.ld);
+        HIPC(hipMemcpy(h.data(), c->W.cg_b + d.foff, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
         for (int q = 0; q < d.r; ++q)
-            for (int i = 0; i < d.n; ++i) rhs[i + (long)q * d.n] = h[d.foff + (long)i * d.ld + q];
+            for (int i = 0; i < d.n; ++i) rhs[i + (long)q * d.n] = h[(long)i * d.ld + q];
     }
     return 0;
 }
 
+int lrs_op_dual_update(lrs_ctx *c, double rho) {
+    LRS_NEED_STATE(c);
+    // LORADSUpdateDualVar (lorads_alg_common.c:511-524): lambda += rho (b - CVS)
+    OPC(launch_dual_update(c->dp, rho, c->W.lam, c->W.cvs, c->st));
+    HIPC(hipStreamSynchronize(c->st));
+    return 0;
+}
+
 int lrs_op_gram(lrs_ctx *c, int cone, int which, double *gram) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(gram);
+    if (cone < 0 || cone >= c->dp.K) { set_err("lrs_op_gram: cone %d of %d", cone, c->dp.K); return -1; }
     std::vector<double> g;
     if (which == LRS_R) { if (gram_of(c, cone, c->W.R, nullptr, 0, g)) return -1; }
     else { if (gram_of(c, cone, c->W.U, c->W.V, 1, g)) return -1; }
@@ -2874,13 +2929,15 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
 }
 
 int lrs_solve(lrs_ctx *c, const lrs_params *p, lrs_result *res) {
-    if (c) bind(c);
-    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    LRS_NEED_LOADED(c);
+    LRS_NEED_ARG(p);
+    LRS_NEED_ARG(res);
     return solve_impl(c, p, res);
 }
 
 int lrs_trajectory(lrs_ctx *c, int phase, int *curr, int *orc, int cap) {
-    if (c) bind(c);
+    LRS_NEED_CTX(c);
+    if (phase != 1 && phase != 2) { set_err("lrs_trajectory: phase %d (1 or 2)", phase); return -1; }
     const std::vector<int> &a = phase == 1 ? c->t1c : c->t2c, &b = phase == 1 ? c->t1o : c->t2o;
     int n = std::min(cap, (int)a.size());
     for (int i = 0; i < n; ++i) { if (curr) curr[i] = a[i]; if (orc) orc[i] = b[i]; }
@@ -2889,7 +2946,12 @@ int lrs_trajectory(lrs_ctx *c, int phase, int *curr, int *orc, int cap) {
 
 int lrs_write_json(lrs_ctx *c, const char *path, const char *pid, const char *fpath, const lrs_result *r,
                    const lrs_params *p) {
-    if (c) bind(c);
+    LRS_NEED_LOADED(c);
+    LRS_NEED_ARG(path);
+    LRS_NEED_ARG(r);
+    LRS_NEED_ARG(p);
+    if (!pid) pid = "";
+    if (!fpath) fpath = "";
     FILE *f = fopen(path, "w");
     if (!f) { set_err("cannot open %s", path); return -1; }
     fprintf(f, "{\n");
@@ -2922,12 +2984,12 @@ int lrs_write_json(lrs_ctx *c, const char *path, const char *pid, const char *fp
 
 int lrs_alm_throughput(lrs_ctx *c, const lrs_params *pin, long warmup, long steps, double *seconds, long *done,
                        double *sddmm_avg_ms, double *iter_avg_ms) {
-    if (c) bind(c);
+    LRS_NEED_LOADED(c);
+    LRS_NEED_ARG(pin);
     // ALM iters/s: the real phase-1 control flow (lorads_alm.c:1220)
     // at fixed rank with the phase-1 exit disabled, stopped after a budget of inner
     // iterations.  Warmup = an untimed run of `warmup` iterations from the same start;
     // the timed run does exactly `steps` inner iterations.
-    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
     lrs_params prm = *pin;
     prm.phase1Tol = 1e-300;
     prm.maxALMIter = 1000000000;
@@ -2972,7 +3034,8 @@ int lrs_set_budget_hook(lrs_ctx *c, lrs_budget_hook hook, void *user) {
 }
 
 int lrs_alm_last_step(lrs_ctx *c, double *out4, int *newest_pair) {
-    if (!c || !out4) { set_err("null argument"); return -1; }
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(out4);
     // the control block the last inner loop stopped on: its fold is the last completed trip
     const int L = c->lbfgsL;
     const int hn = c->head == 0 ? L - 1 : c->head - 1;
@@ -2997,8 +3060,9 @@ int lrs_sync(lrs_ctx *c) {
 }
 
 int lrs_profile_stages(lrs_ctx *c, const lrs_params *pin, long steps, double *stage_ms, long *done) {
-    if (c) bind(c);
-    if (!c || !c->loaded) { set_err("no problem loaded"); return -1; }
+    LRS_NEED_LOADED(c);
+    LRS_NEED_ARG(pin);
+    LRS_NEED_ARG(stage_ms);
     lrs_params prm = *pin;
     prm.phase1Tol = 1e-300;
     prm.maxALMIter = 1000000000;
@@ -3022,13 +3086,13 @@ int lrs_profile_stages(lrs_ctx *c, const lrs_params *pin, long steps, double *st
 }
 
 int lrs_time_stages(lrs_ctx *c, int reps, double *stage_ms) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(stage_ms);
     // Per-launch durations of the split-iteration stages on the current state: each
     // stage is launched `reps` times back to back between two HIP events on the solver
     // stream.  The stages are idempotent for a fixed control block (A reads ctrl[1] and
     // writes ctrl[0]; G and B read ctrl[0]), so the repeats redo identical work.  The
     // control is set active with every exit test disabled.
-    if (!c || !c->loaded || !c->walloc) { set_err("no solver state"); return -1; }
     double *h = c->hpin;
     HIPC(hipMemcpyAsync(h, c->W.ctrl, sizeof(double) * 2 * C_NCTRL, hipMemcpyDeviceToHost, c->st));
     HIPC(hipMemcpyAsync(h + 2 * C_NCTRL, c->W.par, sizeof(double) * P_NPAR, hipMemcpyDeviceToHost, c->st));
@@ -3063,14 +3127,14 @@ int lrs_time_stages(lrs_ctx *c, int reps, double *stage_ms) {
 }
 
 int lrs_debug_phase_times(lrs_ctx *c, unsigned long long *out, unsigned long long *blk) {
-    if (c) bind(c);
-    if (!c) { set_err("null ctx"); return -1; }
+    LRS_NEED_CTX(c);
     HIPC(hipStreamSynchronize(c->st));
     return read_phase_times(out, blk);
 }
 
 int lrs_time_auut(lrs_ctx *c, int reps, double *avg_ms) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(avg_ms);
     hipEvent_t e0, e1;
     HIPC(hipEventCreate(&e0));
     HIPC(hipEventCreate(&e1));
@@ -3131,7 +3195,8 @@ int lrs_mfma_f64_probe(lrs_ctx *c, int waves_per_simd, int chains, double *tflop
 }
 
 int lrs_time_gram(lrs_ctx *c, int cone, int reps, double *avg_ms, double *gram_ms) {
-    if (c) bind(c);
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(avg_ms);
     if (cone < 0 || cone >= c->dp.K) {
         set_err("time_gram: bad cone %d", cone);
         return -1;
@@ -3161,6 +3226,7 @@ int lrs_time_gram(lrs_ctx *c, int cone, int reps, double *avg_ms, double *gram_m
 
 // ---- sharded solve
 int lrs_comm_unique_id(char *id_out) {
+    LRS_NEED_ARG(id_out);
     ncclUniqueId id;
     NCCLC(ncclGetUniqueId(&id));
     memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
@@ -3223,8 +3289,9 @@ static int shard_setup(lrs_ctx *c, int world, int rank) {
 }
 
 int lrs_shard_rccl(lrs_ctx *c, int world, int rank, const char *id) {
-    if (!c) { set_err("null ctx"); return -1; }
-    bind(c);
+    LRS_NEED_LOADED(c);
+    LRS_NEED_ARG(id);
+    if (world < 1 || rank < 0 || rank >= world) { set_err("lrs_shard_rccl: rank %d of world %d", rank, world); return -1; }
     // one shard is the unsharded solve: no fold / all-reduce launches per stage (they cost
     // 19 % of the G81 rate at world 1); LRS_FORCE_SHARD=1 keeps the RCCL plumbing (tests)
     const char *force = getenv("LRS_FORCE_SHARD");
@@ -3245,6 +3312,7 @@ int lrs_shard_rccl(lrs_ctx *c, int world, int rank, const char *id) {
 }
 
 int lrs_loopback_create(int world, lrs_loopback **out) {
+    LRS_NEED_ARG(out);
     if (world < 1 || world > kMaxShards) { set_err("loopback: world %d", world); return -1; }
     lrs_loopback *g = new lrs_loopback();
     g->world = world;
@@ -3266,8 +3334,8 @@ void lrs_loopback_destroy(lrs_loopback *g) {
 }
 
 int lrs_shard_loopback(lrs_ctx *c, lrs_loopback *g, int rank) {
-    if (!c || !g || rank < 0 || rank >= g->world) { set_err("loopback: bad arguments"); return -1; }
-    bind(c);
+    LRS_NEED_LOADED(c);
+    if (!g || rank < 0 || rank >= g->world) { set_err("loopback: bad arguments"); return -1; }
     int rc = shard_setup(c, g->world, rank);
     if (rc == 0 && (hipEventCreateWithFlags(&g->ev_pre[rank], hipEventDisableTiming) != hipSuccess ||
                     hipEventCreateWithFlags(&g->ev_post[rank], hipEventDisableTiming) != hipSuccess)) {
@@ -3294,6 +3362,12 @@ int lrs_shard_info(lrs_ctx *c, int *world, int *rank, int *row0, int *nown, int 
     if (nown) *nown = s ? c->plan.cones[0].nown : (c->loaded ? c->hp.cones[0].n : 0);
     if (nhalo) *nhalo = s ? c->dp.cones[0].n - c->plan.cones[0].nown : 0;
     return 0;
+}
+
+int lrs_shard_comm_ranks(lrs_ctx *c, int *count) {
+    if (!c || !count) { set_err("null argument"); return -1; }
+    if (!sharded(c)) { *count = 1; return 0; }
+    return c->comm->ranks(count);
 }
 
 // Host-only view of shard_problem's partition (no device, no context): the row blocks, this

@@ -97,7 +97,9 @@ def load_library(path=None):
         "lrs_op_grad": (C.c_int, [vp, C.c_double, dp]),
         "lrs_op_line_search": (C.c_int, [vp, C.c_double, dp, ip]),
         "lrs_op_lbfgs": (C.c_int, [vp, C.c_int, C.c_double, C.c_double]),
-        "lrs_op_admm_half": (C.c_int, [vp, C.c_double, C.c_double, C.c_int, ip, dp]),
+        "lrs_op_admm_constr": (C.c_int, [vp]),
+        "lrs_op_admm_half": (C.c_int, [vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, ip, dp]),
+        "lrs_op_dual_update": (C.c_int, [vp, C.c_double]),
         "lrs_op_gram": (C.c_int, [vp, C.c_int, C.c_int, dp]),
         "lrs_solve": (C.c_int, [vp, C.POINTER(Params), C.POINTER(Result)]),
         "lrs_trajectory": (C.c_int, [vp, C.c_int, ip, ip, C.c_int]),
@@ -131,6 +133,7 @@ def load_library(path=None):
         "lrs_loopback_destroy": (None, [vp]),
         "lrs_shard_loopback": (C.c_int, [vp, vp, C.c_int]),
         "lrs_shard_info": (C.c_int, [vp, ip, ip, ip, ip, ip]),
+        "lrs_shard_comm_ranks": (C.c_int, [vp, ip]),
         "lrs_shard_plan": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_long), ip, ip, ip, ip, ip, ip, ip]),
     }
     for name, (res, args) in sig.items():
@@ -263,6 +266,12 @@ class Solver:
         self._check(self.lib.lrs_shard_info(self.ctx, *[C.byref(x) for x in v]), "shard_info")
         return tuple(x.value for x in v)
 
+    def comm_ranks(self):
+        """Ranks the shard transport counts itself (RCCL ncclCommCount; 1 unsharded)."""
+        n = C.c_int()
+        self._check(self.lib.lrs_shard_comm_ranks(self.ctx, C.byref(n)), "shard_comm_ranks")
+        return n.value
+
     # ---- ranks / state
     def determine_rank(self, **kw):
         out = (C.c_int * self.K)()
@@ -324,11 +333,25 @@ class Solver:
         self._check(self.lib.lrs_op_lbfgs(self.ctx, node_num, beta_new, beta_old), "lbfgs")
         return self.get_factor(D)
 
-    def admm_half(self, rho, cg_tol, cg_maxit=800):
+    def admm_constr(self):
+        """LORADSInitConstrValAll + Sum on (U, V): the state the ADMM half-steps read."""
+        self._check(self.lib.lrs_op_admm_constr(self.ctx), "admm_constr")
+
+    def admm_half(self, rho, cg_tol, cg_maxit=800, cone=0, side=0, init=True):
+        """One half-step of LORADSUpdateSDPVar for `cone` (side 0: U with V fixed, 1: V with U
+        fixed) and the cone's constraint refresh; init=True first recomputes the constraint
+        values from (U, V).  Returns (the updated factor, all cones; the cone's RHS; CG its)."""
+        if init:
+            self.admm_constr()
         it = C.c_int()
-        rhs = np.empty(self.dims[0] * self.ranks[0])
-        self._check(self.lib.lrs_op_admm_half(self.ctx, rho, cg_tol, cg_maxit, C.byref(it), _dptr(rhs)), "admm_half")
-        return self.get_factor(U), rhs, it.value
+        rhs = np.empty(self.dims[cone] * self.ranks[cone])
+        self._check(self.lib.lrs_op_admm_half(self.ctx, cone, side, rho, cg_tol, cg_maxit, C.byref(it), _dptr(rhs)),
+                    "admm_half")
+        return self.get_factor(V if side else U), rhs, it.value
+
+    def dual_update(self, rho):
+        """LORADSUpdateDualVar: lambda += rho (b - A(X))."""
+        self._check(self.lib.lrs_op_dual_update(self.ctx, rho), "dual_update")
 
     def gram(self, cone=0, which=R):
         r = self.ranks[cone]

@@ -29,6 +29,10 @@
  *       With a comma list of K (ascending) one run dumps the state at each K into
  *       <out.bin>.K<k>, at the point a stand-alone run with that K stops (so a
  *       C5-sized presolve is paid once).
+ *   admm_sweep <file.dat-s> <rank> <in.bin> <out.bin>
+ *       One ADMM variable update over every cone (LORADSUpdateSDPVar) and the dual
+ *       update after it (LORADSUpdateDualVar) on the `kernels` inputs' U, V, lambda
+ *       (scripts/make_golden_admm.py).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -337,6 +341,53 @@ static int mode_kernels(int argc, char **argv) {
     return 0;
 }
 
+/* ---------------- admm_sweep mode: one ADMM variable update over every cone ----------------
+ * Same input file as `kernels`.  State: U, V, lambda; constraint values from (U, V)
+ * (LORADSInitConstrValAll + Sum); then LORADSUpdateSDPVar (lorads_alg_common.c:298-326: per
+ * cone U with V fixed, refresh, V with U fixed, refresh) at rho_admm, cg_tol, 800 iterations,
+ * then LORADSUpdateDualVar (:511-524) at rho_admm.  Dump: U, V (all cones), constrValSum[m],
+ * dualVar[m], total CG iterations, per cone the last (V-side) CG iteration count. */
+static int mode_admm_sweep(int argc, char **argv) {
+    if (argc < 6) return 2;
+    lorads_params p; default_params(&p);
+    p.fname = argv[2];
+    p.fixedRank = atoi(argv[3]);
+    ref_ctx c; memset(&c, 0, sizeof(c));
+    double t_read, tss;
+    if (ref_setup(&c, &p, &t_read, &tss)) { fprintf(stderr, "read failed\n"); return 1; }
+    lorads_solver *S = c.S;
+    lorads_int m = S->nRows, K = S->nCones, NR = 0;
+    for (lorads_int k = 0; k < K; ++k) NR += S->var->R[k]->nRows * S->var->R[k]->rank;
+    FILE *fi = fopen(argv[4], "rb");
+    if (!fi) return 1;
+    fseek(fi, 0, SEEK_END); long sz = ftell(fi); fseek(fi, 0, SEEK_SET);
+    double *in = malloc(sz); if (fread(in, 1, sz, fi) != (size_t)sz) return 1; fclose(fi);
+    const double *U = in + 7 * NR, *V = in + 8 * NR, *lam = in + 9 * NR;
+    const double *tail = in + 9 * NR + 2 * m;
+    const double rho_admm = tail[3], cg_tol = tail[4];
+    lorads_int off;
+    LOAD(S->var->U, U); LOAD(S->var->V, V);
+    memcpy(S->var->dualVar, lam, 8 * m);
+    LORADSInitConstrValAll(S, S->var->uLp, S->var->vLp, S->var->U, S->var->V);
+    LORADSInitConstrValSum(S);
+    S->cgIter = 0;
+    LORADSUpdateSDPVar(S, rho_admm, cg_tol, 800);
+    LORADSUpdateDualVar(S, rho_admm);
+    FILE *fo = fopen(argv[5], "wb");
+    if (!fo) return 1;
+    DUMPF(S->var->U);
+    DUMPF(S->var->V);
+    fwrite(S->var->constrValSum, 8, m, fo);
+    fwrite(S->var->dualVar, 8, m, fo);
+    double it = (double)S->cgIter;
+    fwrite(&it, 8, 1, fo);
+    for (lorads_int k = 0; k < K; ++k) { it = (double)S->CGLinsys[k]->iter; fwrite(&it, 8, 1, fo); }
+    fclose(fo);
+    free(in);
+    printf("REF_ADMM_SWEEP cg=%ld\n", (long)S->cgIter);
+    return 0;
+}
+
 /* ---------------- alm_steps mode: K inner iterations, per-iteration dump ---------------- */
 static int steps_dump(lorads_solver *S, const double *trips, long done, const char *out, long K) {
     char path[4096];
@@ -477,5 +528,6 @@ int main(int argc, char **argv) {
     if (!strcmp(argv[1], "alm_rate")) return mode_alm_rate(argc, argv);
     if (!strcmp(argv[1], "kernels")) return mode_kernels(argc, argv);
     if (!strcmp(argv[1], "alm_steps")) return mode_alm_steps(argc, argv);
+    if (!strcmp(argv[1], "admm_sweep")) return mode_admm_sweep(argc, argv);
     return 2;
 }

@@ -95,3 +95,65 @@ def test_c_caller_solves_like_reference(built, tmp_path):
     assert abs(float(m.group(1)) - ref["result"]["admm_pobj"]) <= 1e-6 * abs(ref["result"]["admm_pobj"])
     out = json.load(open(js))
     assert set(out["metrics"]) == set(ref["json"]["metrics"])
+
+
+def test_c_caller_null_context_contract(built, tmp_path):
+    """include/lrsdp.h's error contract from a plain-C caller: every entry point handed a NULL
+    context (or a NULL required output) returns a negative code with a message, no crash.  No
+    context is created, so this needs no GPU."""
+    exe = build_c_caller(tmp_path)
+    r = subprocess.run([exe, "--null"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "CAPI_NULL failures=0" in r.stdout
+
+
+def test_python_mirror_null_context(built):
+    """The same contract through ctypes (the test mirror's binding)."""
+    lib = C.CDLL(built)
+    lib.lrs_last_error.restype = C.c_char_p
+    for name, args in (("lrs_op_admm_half", (None, 0, 0, C.c_double(1.0), C.c_double(1e-8), 10, None, None)),
+                       ("lrs_op_dual_update", (None, C.c_double(1.0))), ("lrs_op_admm_constr", (None,)),
+                       ("lrs_set_log_path", (None, b"x.log")), ("lrs_load_sdpa", (None, b"x.dat-s", None)),
+                       ("lrs_problem_info", (None, None, None, None, None, None))):
+        assert getattr(lib, name)(*args) < 0, name
+        assert b"null" in lib.lrs_last_error(), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["theta25x3", "mc_rand200", "rsparse60", "theta40"])
+def test_c_caller_admm_sweep_matches_reference(built, tmp_path, name):
+    """The C caller runs the reference's ADMM variable update (LORADSUpdateSDPVar: every cone, U
+    then V, each followed by the cone's constraint refresh) through lrs_op_admm_half(cone, side)
+    -- cones k > 0 included on theta25x3 -- and LORADSUpdateDualVar through lrs_op_dual_update,
+    against the reference's own run on the same inputs (tests/golden/admm_sweep_*.npz,
+    scripts/make_golden_admm.py).  Bars: factors and multipliers within 1e-6 relative (CG
+    solutions at cg_tol 1e-12, the bar of the single half-step test), the CG counts of each
+    cone's V solve within 10 % and the total within 10 %."""
+    import numpy as np
+    exe = build_c_caller(tmp_path)
+    g = np.load(os.path.join(ROOT, "tests", "golden", f"admm_sweep_{name}.npz"))
+    k = np.load(os.path.join(ROOT, "tests", "golden", f"kernels_{name}.npz"))
+    vec, m = k["inputs"], int(k["m"])
+    dims = [int(d) for d in k["dims"]]
+    rank = int(k["rank"])
+    NR = sum(d * rank for d in dims)
+    tail = vec[9 * NR + 2 * m:]
+    inp = np.concatenate([vec[7 * NR:9 * NR], vec[9 * NR:9 * NR + m], [tail[3], tail[4]]])
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    inp.astype(np.float64).tofile(fin)
+    inst = os.path.join(ROOT, "tests", "golden", "instances", f"{name}.dat-s")
+    r = subprocess.run([exe, "--sweep", inst, str(rank), str(fin), str(fout)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = np.fromfile(fout, dtype=np.float64)
+    U, V, lam, its = out[:NR], out[NR:2 * NR], out[2 * NR:2 * NR + m], out[2 * NR + m:]
+
+    def rel(a, b):
+        return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+    assert rel(U, g["U"]) < 1e-6, rel(U, g["U"])
+    assert rel(V, g["V"]) < 1e-6, rel(V, g["V"])
+    assert rel(lam, g["lam"]) < 1e-6, rel(lam, g["lam"])
+    for c in range(len(dims)):
+        ref = float(g["cg_last"][c])
+        assert abs(its[2 * c + 1] - ref) <= max(2, 0.1 * ref), (c, its, g["cg_last"])
+    assert abs(its.sum() - float(g["cg_total"])) <= max(4, 0.1 * float(g["cg_total"])), (its, g["cg_total"])

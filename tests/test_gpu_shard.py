@@ -94,6 +94,7 @@ def test_rccl_transport_world1(solver_mod, monkeypatch):
     sv = solver_mod.Solver(instance("mc_torus12x10"))
     sv.shard_rccl(1, 0, solver_mod.comm_unique_id())
     assert sv.shard_info() == (1, 0, 0, 120, 0)
+    assert sv.comm_ranks() == 1   # ncclCommCount of the communicator
     r = sv.solve(**kw)
     out = sv.alm_throughput(0, 40, fixedRank=6, reoptLevel=0)
     sv.close()
