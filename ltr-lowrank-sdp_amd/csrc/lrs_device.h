@@ -141,7 +141,19 @@ struct DevCone {
     int sb_I0 = 0;
     int sx_n = 0;
     int *sx_slot = nullptr;
+    // single-workgroup ADMM half-step (launch_small_cg; small unsharded cones, lrs_problem.cpp):
+    // the constraint slots (slots with a constraint entry, cg_ncs) and their symmetric adjacency
+    // per row packed (col << 16 | constraint slot); the cone's constraints in compact order (the
+    // cg_ns short ones, then the long ones; cg_cl_con their ids) with their entries packed
+    // (constraint slot << 1 | diagonal) and weights (2 - delta) a; per constraint slot its
+    // (compact constraint, a) pairs; the objective as constant (cg_cconst 1: slot form, alpha =
+    // Craw[cg_cslot]; 2: the rank-one form) or its entries per row (col, global slot)
+    int cg_ok = 0, cg_ncs = 0, cg_ncl = 0, cg_ns = 0, cg_nce = 0, cg_nsc = 0, cg_nadj = 0, cg_cconst = 0, cg_cslot = 0;
+    int *cg_cadj_ptr = nullptr, *cg_cadj = nullptr, *cg_cl_con = nullptr, *cg_cl_ptr = nullptr, *cg_ce = nullptr;
+    int *cg_sp = nullptr, *cg_sj = nullptr, *cg_cc_ptr = nullptr, *cg_cc = nullptr;
+    double *cg_ce_w = nullptr, *cg_sa = nullptr;
 };
+constexpr int kScMaxN = 256;         // rows of a cone the single-workgroup ADMM half-step takes
 constexpr int kMaxRankLd = 512;      // widest factor row (choose_layout: 64 lanes x 8 doubles)
 constexpr int kAuvT = 128;           // rows of one side of an A(X Y^T) tile
 constexpr int kAuvC = 32;            // factor columns staged in LDS at a time
@@ -330,7 +342,7 @@ int launch_small_alm(const DevProblem &P, DevWork &W, const double *ctrl_in, dou
                      hipStream_t st);
 
 // ---- device-resident CG (lrs_kernels.hip "Device-resident CG") ----
-enum CgIdx { CG_ACTIVE = 0, CG_ITERS, CG_BNORM, CG_RR, CG_QTR0, CG_QTR1, CG_N = 8 };
+enum CgIdx { CG_ACTIVE = 0, CG_ITERS, CG_BNORM, CG_RR, CG_QTR0, CG_QTR1, CG_TOTAL, CG_N = 8 };
 int launch_cg_mv(const DevProblem &P, int cone, const double *w, const double *V, const double *Xin, double *Q,
                  double *part, const double *cgc, int guarded, hipStream_t st, int *nblk);
 int launch_cg_nrm1(long nr, const double *b, double *part, hipStream_t st, int *nblk);
@@ -342,6 +354,12 @@ int launch_cg_resid(long nr, const double *b, const double *Q, double *r, double
                     const double *partA, int nblkA, int init, hipStream_t st, int *nblk);
 int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, int nblkC, double *cgc, double tol,
                      int par, int init, hipStream_t st);
+// single-workgroup ADMM half-step of cone `cone` (LORADSUpdateSDPVarOne + CGSolve + the cone's
+// constraint refresh, one launch): side 0 solves U with V fixed, 1 V with U fixed; the RHS into
+// W.cg_b, this solve's CG iterations into W.cgc[CG_ITERS], added to W.cgc[CG_TOTAL]
+bool small_cg_fits(const DevProblem &P, int cone);
+int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double rho, double tol, int maxit,
+                    hipStream_t st);
 
 // ---- dual infeasibility (Lanczos for lambda_min of S per cone) ----
 // y = S x over one cone's adjacency (S on the global slots, x / y cone-local vectors)

@@ -6523,4 +6523,407 @@ int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, i
     return 0;
 }
 
+
+// ------------------------------------------------------------------------
+// Single-workgroup ADMM half-step (small cones: the theta class).  ONE launch of one workgroup
+// runs LORADSUpdateSDPVarOne (lorads_admm.c:564-616) for one cone and side -- the right-hand
+// side, the whole CGSolve (linalg/lorads_cgs.c:128-287, as the device-resident CG above: the
+// same tolerance test, restart every 20 iterations and iteration count) -- and the cone's
+// constraint refresh of LORADSUpdateSDPVar (lorads_alg_common.c:310-314 / :321-323), where the
+// multi-launch path takes four launches per CG iteration and a host poll per batch (theta3x3:
+// ~20 us a CG iteration).  Layout: the fixed factor Y in LDS (rows of r doubles,
+// odd pitch); the operand x (p, or X at a restart and for the refresh), X, r, p, Q and b of a row
+// in the registers of the 16-lane group that owns it (row i: group i % kScG; column c: lane
+// c % 16, element c / 16); the constraint values (compact order), the per-slot products and the
+// lists of DevCone::cg_* in LDS.  The operator x -> x + A*(A(sym(x Y^T))) Y (linSysProduct,
+// lorads_admm.c:471-486) runs in four phases: (A) every row's group forms x_i . Y_j for each
+// constraint slot (i, j) of its row, so a slot's 1/2 (x_p . Y_q + x_q . Y_p) comes from its two
+// rows' halves; (B) the constraint values from the slots (a thread per short constraint, a wave
+// per long one); (C) A*(w) on the constraint slots; (D) Q_i = sum_j S_ij Y_j + x_i in the
+// adjacency's column order (k_cg_mv's order).  Sums over the block: wave sums, then the eight
+// wave values in wave order (deterministic).
+// ------------------------------------------------------------------------
+constexpr int kScT = 512;                // threads
+constexpr int kScL = 16;                 // lanes per factor row
+constexpr int kScG = kScT / kScL;        // row groups
+constexpr int kScW = kScT / 64;          // waves
+constexpr int kScMaxDynLds = 152 * 1024;
+
+struct SmallCgArgs {
+    int n, r, ld, rS, side, maxit, ncs, ncl, ns, nce, nsc, nadj, cconst, cslot;
+    long foff;
+    double rho, tol, calpha;
+    const int *cadj_ptr, *cadj, *cl_con, *cl_ptr, *ce, *sp, *sj, *cc_ptr, *cc;
+    const double *ce_w, *sa, *Craw, *b, *lam;
+    double *cvs, *cvc, *U, *V, *cg_b, *cgc;
+};
+
+static size_t small_cg_lds(int n, int rS, int ncl, int ncs, int nce, int nsc, int nadj) {
+    const size_t dbl = (size_t)n * rS + ncl + 2 * (size_t)ncs + nce + nsc + rS + 2 * kScW;
+    const size_t in = (size_t)(n + 1) + nadj + (ncl + 1) + nce + (ncs + 1) + nsc;
+    return dbl * sizeof(double) + in * sizeof(int);
+}
+
+template <int EL, int RPG>
+__global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
+    extern __shared__ double smem[];
+    const int n = A.n, r = A.r, rS = A.rS;
+    double *Ys = smem;                         // [n][rS] the fixed factor
+    double *wv = Ys + (long)n * rS;            // [ncl] constraint values (or M1), compact order
+    double *T = wv + A.ncl;                    // [ncs][2] half products; then S on [0, ncs)
+    double *cew = T + 2 * A.ncs;               // [nce]
+    double *sav = cew + A.nce;                 // [nsc]
+    double *csum = sav + A.nsc;                // [rS] column sums of Y (constant objective)
+    double *red = csum + rS;                   // [2][kScW]
+    int *cap = reinterpret_cast<int *>(red + 2 * kScW);   // [n + 1]
+    int *cadj = cap + n + 1;                   // [nadj]
+    int *clp = cadj + A.nadj;                  // [ncl + 1]
+    int *ce = clp + A.ncl + 1;                 // [nce]
+    int *sp = ce + A.nce;                      // [ncs + 1]
+    int *sj = sp + A.ncs + 1;                  // [nsc]
+    const int tid = threadIdx.x, g = tid / kScL, l = tid % kScL, wid = tid >> 6, lane = tid & 63;
+    double *X = (A.side ? A.V : A.U) + A.foff;
+    const double *Yg = (A.side ? A.U : A.V) + A.foff;
+    for (int t = tid; t < n * r; t += kScT) {
+        const int i = t / r, c = t - i * r;
+        Ys[i * rS + c] = Yg[(long)i * A.ld + c];
+    }
+    for (int t = tid; t <= n; t += kScT) cap[t] = A.cadj_ptr[t];
+    for (int t = tid; t < A.nadj; t += kScT) cadj[t] = A.cadj[t];
+    for (int t = tid; t <= A.ncl; t += kScT) clp[t] = A.cl_ptr[t];
+    for (int t = tid; t < A.nce; t += kScT) { ce[t] = A.ce[t]; cew[t] = A.ce_w[t]; }
+    for (int t = tid; t <= A.ncs; t += kScT) sp[t] = A.sp[t];
+    for (int t = tid; t < A.nsc; t += kScT) { sj[t] = A.sj[t]; sav[t] = A.sa[t]; }
+    // this group's rows of X (zero past r and n)
+    double x[RPG][EL], rv[RPG][EL], pv[RPG][EL], Q[RPG][EL], bv[RPG][EL];
+#pragma unroll
+    for (int q = 0; q < RPG; ++q)
+#pragma unroll
+        for (int k = 0; k < EL; ++k) {
+            const int i = g + kScG * q, c = l + kScL * k;
+            x[q][k] = (i < n && c < r) ? X[(long)i * A.ld + c] : 0.0;
+            rv[q][k] = pv[q][k] = Q[q][k] = bv[q][k] = 0.0;
+        }
+    int rp = 0;
+    auto block_sum = [&](double v) -> double {
+        v = wave_sum(v);
+        if (lane == 0) red[rp * kScW + wid] = v;
+        __syncthreads();
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kScW; ++w) s += red[rp * kScW + w];
+        rp ^= 1;
+        return s;
+    };
+    // (A) x_i . Y_j per constraint slot (i, j): half 0 from the slot's lower row, 1 from its upper
+    auto prod_pass = [&](const double (&xv)[RPG][EL]) {
+#pragma unroll
+        for (int q = 0; q < RPG; ++q) {
+            const int i = g + kScG * q;
+            if (i >= n) continue;   // group-uniform
+            for (int e = cap[i]; e < cap[i + 1]; ++e) {
+                const int pk = cadj[e], j = pk >> 16, cs = pk & 0xffff;
+                double d = 0.0;
+#pragma unroll
+                for (int k = 0; k < EL; ++k) {
+                    const int c = l + kScL * k;
+                    if (c < r) d += xv[q][k] * Ys[j * rS + c];
+                }
+                d = group_sum<kScL>(d);
+                if (l == 0) T[2 * cs + (j <= i ? 0 : 1)] = d;
+            }
+        }
+    };
+    // (B) constraint values sum_e w_e d_e (k_auv_con's entry order)
+    auto con_pass = [&]() {
+        for (int j = tid; j < A.ns; j += kScT) {
+            double v = 0.0;
+            for (int e = clp[j]; e < clp[j + 1]; ++e) {
+                const int pk = ce[e], cs = pk >> 1;
+                const double d = (pk & 1) ? T[2 * cs] : 0.5 * (T[2 * cs] + T[2 * cs + 1]);
+                v += cew[e] * d;
+            }
+            wv[j] = v;
+        }
+        for (int j = A.ns + wid; j < A.ncl; j += kScW) {   // wave-uniform
+            double v = 0.0;
+            for (int e = clp[j] + lane; e < clp[j + 1]; e += 64) {
+                const int pk = ce[e], cs = pk >> 1;
+                const double d = (pk & 1) ? T[2 * cs] : 0.5 * (T[2 * cs] + T[2 * cs + 1]);
+                v += cew[e] * d;
+            }
+            v = wave_sum(v);
+            if (lane == 0) wv[j] = v;
+        }
+    };
+    // (C) S = A*(w) on the constraint slots (sdpDataWSum without C), into T[0, ncs)
+    auto slot_pass = [&]() {
+        for (int t = tid; t < A.ncs; t += kScT) {
+            double v = 0.0;
+            for (int e = sp[t]; e < sp[t + 1]; ++e) v += wv[sj[e]] * sav[e];
+            T[t] = v;
+        }
+    };
+    // (D) Q = S Y + x on the group's rows; returns this thread's part of <x, Q>
+    auto apply_pass = [&](const double (&xv)[RPG][EL], double (&Qv)[RPG][EL]) -> double {
+        double dot = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPG; ++q) {
+            const int i = g + kScG * q;
+            double acc[EL];
+#pragma unroll
+            for (int k = 0; k < EL; ++k) acc[k] = 0.0;
+            if (i < n)
+                for (int e = cap[i]; e < cap[i + 1]; ++e) {
+                    const int pk = cadj[e], j = pk >> 16;
+                    const double sv = T[pk & 0xffff];
+#pragma unroll
+                    for (int k = 0; k < EL; ++k) {
+                        const int c = l + kScL * k;
+                        if (c < r) acc[k] += sv * Ys[j * rS + c];
+                    }
+                }
+#pragma unroll
+            for (int k = 0; k < EL; ++k) {
+                double v = acc[k] * 1.0;
+                v += 1.0 * xv[q][k];
+                Qv[q][k] = v;
+                dot += xv[q][k] * v;
+            }
+        }
+        return dot;
+    };
+    auto matvec = [&](const double (&xv)[RPG][EL], double (&Qv)[RPG][EL]) -> double {
+        __syncthreads();   // T free (the previous apply pass is done)
+        prod_pass(xv);
+        __syncthreads();
+        con_pass();
+        __syncthreads();
+        slot_pass();
+        __syncthreads();
+        return apply_pass(xv, Qv);
+    };
+
+    // ---- right-hand side (lorads_admm.c:566-598): M1 = rho (cvs - A_k - b) - lam (compact),
+    // S = A*(M1) on the constraint slots, M2 = S Y + C Y - rho Y, b = -M2 / rho
+    const double rho = A.rho;
+    for (int j = tid; j < A.ncl; j += kScT) {
+        const int gi = A.cl_con[j];
+        double v = -A.b[gi];
+        v = v + A.cvs[gi];
+        v = v + (-1.0) * A.cvc[gi];
+        v = v * rho;
+        wv[j] = v + (-1.0) * A.lam[gi];
+    }
+    __syncthreads();   // Ys and the lists staged, M1 formed
+    if (A.cconst)
+        for (int c = tid; c < r; c += kScT) {
+            double s = 0.0;
+            for (int i = 0; i < n; ++i) s += Ys[i * rS + c];
+            csum[c] = s;
+        }
+    slot_pass();
+    __syncthreads();
+    {
+        const double alpha = A.cconst == 1 ? A.Craw[A.cslot] : A.calpha;
+        double bn = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPG; ++q) {
+            const int i = g + kScG * q;
+            double acc[EL];
+#pragma unroll
+            for (int k = 0; k < EL; ++k) acc[k] = 0.0;
+            if (i < n) {
+                for (int e = cap[i]; e < cap[i + 1]; ++e) {
+                    const int pk = cadj[e], j = pk >> 16;
+                    const double sv = T[pk & 0xffff];
+#pragma unroll
+                    for (int k = 0; k < EL; ++k) {
+                        const int c = l + kScL * k;
+                        if (c < r) acc[k] += sv * Ys[j * rS + c];
+                    }
+                }
+                if (!A.cconst)
+                    for (int e = A.cc_ptr[i]; e < A.cc_ptr[i + 1]; ++e) {
+                        const int j = A.cc[2 * e];
+                        const double cv = A.Craw[A.cc[2 * e + 1]];
+#pragma unroll
+                        for (int k = 0; k < EL; ++k) {
+                            const int c = l + kScL * k;
+                            if (c < r) acc[k] += cv * Ys[j * rS + c];
+                        }
+                    }
+            }
+#pragma unroll
+            for (int k = 0; k < EL; ++k) {
+                const int c = l + kScL * k;
+                const bool ok = i < n && c < r;
+                double m2 = acc[k] * 1.0;
+                m2 += (-rho) * (ok ? Ys[i * rS + c] : 0.0);
+                if (A.cconst && ok) m2 = alpha * csum[c] + 1.0 * m2;
+                const double bvk = ok ? (-1.0 / rho) * m2 : 0.0;
+                bv[q][k] = bvk;
+                if (ok) A.cg_b[A.foff + (long)i * A.ld + c] = bvk;
+                bn += fabs(bvk);
+            }
+        }
+        bn = block_sum(bn);
+
+        // ---- CGSolve: r = b - M X, p = r; then the iterations
+        matvec(x, Q);
+        double rr = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPG; ++q)
+#pragma unroll
+            for (int k = 0; k < EL; ++k) {
+                const double ri = 1.0 * bv[q][k] + -1.0 * Q[q][k];
+                rv[q][k] = ri;
+                pv[q][k] = ri;
+                rr += ri * ri;
+            }
+        rr = block_sum(rr);
+        double qtr[2] = {rr, 0.0};
+        bool active = !(sqrt(rr) / bn < A.tol);
+        int iters = 0;
+        for (int it = 0; active && it < A.maxit; ++it) {   // block-uniform
+            const int par = it & 1;
+            const double pq = block_sum(matvec(pv, Q));
+            const double alph = qtr[par] / pq;
+            iters = it + 1;
+            double rr1 = 0.0;
+#pragma unroll
+            for (int q = 0; q < RPG; ++q)
+#pragma unroll
+                for (int k = 0; k < EL; ++k) {
+                    x[q][k] = alph * pv[q][k] + 1.0 * x[q][k];
+                    const double ri = -alph * Q[q][k] + 1.0 * rv[q][k];
+                    rv[q][k] = ri;
+                    rr1 += ri * ri;
+                }
+            rr1 = block_sum(rr1);
+            const double resi = sqrt(rr1);
+            if (resi / bn < A.tol || resi != resi) { active = false; break; }
+            if (it % 20 != 0) {
+                const double beta = rr1 / qtr[par];
+#pragma unroll
+                for (int q = 0; q < RPG; ++q)
+#pragma unroll
+                    for (int k = 0; k < EL; ++k) pv[q][k] = 1.0 * rv[q][k] + beta * pv[q][k];
+                qtr[par ^ 1] = rr1;
+            } else {
+                // restart (lorads_cgs.c: every 20 iterations): r = b - M X, p = r, then the
+                // beta = 1 step of the same iteration (p = r + p)
+                matvec(x, Q);
+                double rr2 = 0.0;
+#pragma unroll
+                for (int q = 0; q < RPG; ++q)
+#pragma unroll
+                    for (int k = 0; k < EL; ++k) {
+                        const double ri = 1.0 * bv[q][k] + -1.0 * Q[q][k];
+                        rv[q][k] = ri;
+                        pv[q][k] = ri;
+                        rr2 += ri * ri;
+                    }
+                rr2 = block_sum(rr2);
+                const double beta = rr2 / rr2;
+#pragma unroll
+                for (int q = 0; q < RPG; ++q)
+#pragma unroll
+                    for (int k = 0; k < EL; ++k) pv[q][k] = 1.0 * rv[q][k] + beta * pv[q][k];
+                qtr[par ^ 1] = rr2;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < RPG; ++q)
+#pragma unroll
+            for (int k = 0; k < EL; ++k) {
+                const int i = g + kScG * q, c = l + kScL * k;
+                if (i < n && c < r) X[(long)i * A.ld + c] = x[q][k];
+            }
+        if (tid == 0) {
+            A.cgc[CG_ITERS] = iters;
+            A.cgc[CG_TOTAL] += iters;
+        }
+    }
+    // ---- the cone's refresh: A_k <- A_k(sym(U V^T)) (x . Y products of the solved side), CVS += new - old
+    __syncthreads();
+    prod_pass(x);
+    __syncthreads();
+    con_pass();
+    __syncthreads();
+    for (int j = tid; j < A.ncl; j += kScT) {
+        const int gi = A.cl_con[j];
+        const double v = wv[j];
+        A.cvs[gi] = (A.cvs[gi] - A.cvc[gi]) + v;
+        A.cvc[gi] = v;
+    }
+}
+
+bool small_cg_fits(const DevProblem &P, int cone) {
+    const DevCone &c = P.cones[cone];
+    if (P.shard || !c.cg_ok || c.dense_c == 1 || c.r < 1) return false;
+    // the instantiated (elements per lane, rows per group): EL 1-2 with up to 8 rows a group,
+    // EL 3-4 with up to 4 (five register arrays of EL x RPG doubles, 2 waves a SIMD)
+    const int EL = (c.r + kScL - 1) / kScL, RPG = (c.n + kScG - 1) / kScG;
+    const int rpg = RPG <= 2 ? 2 : (RPG <= 4 ? 4 : 8);
+    if (EL > 4 || RPG > 8 || (EL > 2 && rpg > 4)) return false;
+    const int rS = c.r | 1;
+    return small_cg_lds(c.n, rS, c.cg_ncl, c.cg_ncs, c.cg_nce, c.cg_nsc, c.cg_nadj) <= (size_t)kScMaxDynLds;
+}
+
+template <int EL, int RPG>
+static int launch_small_cg_t(const SmallCgArgs &A, size_t lds, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_small_cg<EL, RPG>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScMaxDynLds) != hipSuccess) {
+            snprintf(g_err, sizeof(g_err), "single-workgroup ADMM half-step: LDS attribute refused");
+            return -1;
+        }
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_small_cg<EL, RPG>), dim3(1), dim3(kScT), lds, st, A);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double rho, double tol, int maxit,
+                    hipStream_t st) {
+    if (!small_cg_fits(P, cone)) {
+        snprintf(g_err, sizeof(g_err), "single-workgroup ADMM half-step: cone %d does not fit", cone);
+        return -1;
+    }
+    const DevCone &c = P.cones[cone];
+    SmallCgArgs A{};
+    A.n = c.n; A.r = c.r; A.ld = c.ld; A.rS = c.r | 1; A.side = side; A.maxit = maxit;
+    A.ncs = c.cg_ncs; A.ncl = c.cg_ncl; A.ns = c.cg_ns; A.nce = c.cg_nce; A.nsc = c.cg_nsc; A.nadj = c.cg_nadj;
+    A.cconst = c.dense_c == 2 ? 2 : c.cg_cconst;
+    A.cslot = c.cg_cslot;
+    A.foff = c.foff;
+    A.rho = rho; A.tol = tol;
+    A.calpha = P.dense_scale * c.c_alpha;
+    A.cadj_ptr = c.cg_cadj_ptr; A.cadj = c.cg_cadj; A.cl_con = c.cg_cl_con; A.cl_ptr = c.cg_cl_ptr; A.ce = c.cg_ce;
+    A.sp = c.cg_sp; A.sj = c.cg_sj; A.cc_ptr = c.cg_cc_ptr; A.cc = c.cg_cc; A.ce_w = c.cg_ce_w; A.sa = c.cg_sa;
+    A.Craw = P.Craw; A.b = P.b; A.lam = W.lam;
+    A.cvs = W.cvs; A.cvc = W.cvc + (long)cone * P.m; A.U = W.U; A.V = W.V; A.cg_b = W.cg_b; A.cgc = W.cgc;
+    const size_t lds = small_cg_lds(c.n, A.rS, A.ncl, A.ncs, A.nce, A.nsc, A.nadj);
+    const int EL = (c.r + kScL - 1) / kScL, RPG = (c.n + kScG - 1) / kScG;
+    const int rpg = RPG <= 2 ? 2 : (RPG <= 4 ? 4 : 8);
+    switch (EL * 16 + rpg) {
+    case 1 * 16 + 2: return launch_small_cg_t<1, 2>(A, lds, st);
+    case 1 * 16 + 4: return launch_small_cg_t<1, 4>(A, lds, st);
+    case 1 * 16 + 8: return launch_small_cg_t<1, 8>(A, lds, st);
+    case 2 * 16 + 2: return launch_small_cg_t<2, 2>(A, lds, st);
+    case 2 * 16 + 4: return launch_small_cg_t<2, 4>(A, lds, st);
+    case 2 * 16 + 8: return launch_small_cg_t<2, 8>(A, lds, st);
+    case 3 * 16 + 2: return launch_small_cg_t<3, 2>(A, lds, st);
+    case 3 * 16 + 4: return launch_small_cg_t<3, 4>(A, lds, st);
+    case 4 * 16 + 2: return launch_small_cg_t<4, 2>(A, lds, st);
+    case 4 * 16 + 4: return launch_small_cg_t<4, 4>(A, lds, st);
+    default:
+        snprintf(g_err, sizeof(g_err), "single-workgroup ADMM half-step: no variant for r %d, n %d", c.r, c.n);
+        return -1;
+    }
+}
+
 }  // namespace lrs

@@ -632,6 +632,101 @@ static bool dput(T **dst, const std::vector<T> &v, std::string &err) {
     return true;
 }
 
+// The single-workgroup ADMM half-step's lists of one small cone (lrs_device.h DevCone::cg_*,
+// lrs_kernels.hip k_small_cg): built when the objective is constant (rank-one form, or every
+// slot of the block holding one value), absent, or at most 16 entries a row; else cg_ok stays 0
+// and the cone's half-steps take the multi-launch CG.
+constexpr int kScLong = 16;   // constraints with more entries in the cone: a wave each (= lrs_kernels.hip)
+static bool upload_small_cg(const HostCone &c, int m, DevCone &d, std::string &err) {
+    const int P = (int)c.prow.size();
+    std::vector<int> s2cs(P, -1), csl;
+    for (const HostEntry &e : c.ent) s2cs[e.slot] = 0;
+    for (int t = 0; t < P; ++t)
+        if (s2cs[t] == 0) { s2cs[t] = (int)csl.size(); csl.push_back(t); }
+    const int ncs = (int)csl.size();
+    int cconst = 0, cslot = 0;
+    long nC = 0;
+    if (c.const_c) {
+        cconst = 2;
+    } else {
+        bool same = true;
+        for (int t = 0; t < P; ++t) {
+            if (!c.Chas[t]) continue;
+            if (nC == 0) cslot = t;
+            else if (c.Craw[t] != c.Craw[cslot]) same = false;
+            nC++;
+        }
+        if (nC > 0 && nC == (long)c.n * (c.n + 1) / 2 && same) cconst = 1;
+    }
+    if (ncs == 0 || ncs >= 65536 || (cconst == 0 && nC > 16L * c.n)) return true;
+    // constraint-slot adjacency, in the adjacency's (column) order
+    std::vector<int> cap(c.n + 1, 0), cadj;
+    for (int i = 0; i < c.n; ++i) {
+        for (int q = c.adj_ptr[i]; q < c.adj_ptr[i + 1]; ++q)
+            if (s2cs[c.adj_slot[q]] >= 0) cadj.push_back((c.adj_col[q] << 16) | s2cs[c.adj_slot[q]]);
+        cap[i + 1] = (int)cadj.size();
+    }
+    // the cone's constraints (entries sorted by (con, slot)): the short ones, then the long ones
+    std::vector<int> cons, cbeg;
+    for (size_t e = 0; e < c.ent.size();) {
+        size_t f = e;
+        while (f < c.ent.size() && c.ent[f].con == c.ent[e].con) ++f;
+        cons.push_back(c.ent[e].con);
+        cbeg.push_back((int)e);
+        e = f;
+    }
+    cbeg.push_back((int)c.ent.size());
+    const int ncl = (int)cons.size();
+    std::vector<int> order;
+    for (int pass = 0; pass < 2; ++pass)
+        for (int j = 0; j < ncl; ++j)
+            if ((cbeg[j + 1] - cbeg[j] > kScLong) == (pass == 1)) order.push_back(j);
+    int ns = 0;
+    for (int j = 0; j < ncl; ++j) ns += cbeg[j + 1] - cbeg[j] <= kScLong ? 1 : 0;
+    std::vector<int> compact(std::max(1, m), -1), clcon, clp(1, 0), ce;
+    std::vector<double> cew;
+    for (int o = 0; o < ncl; ++o) {
+        const int j = order[o];
+        compact[cons[j]] = o;
+        clcon.push_back(cons[j]);
+        for (int e = cbeg[j]; e < cbeg[j + 1]; ++e) {
+            const HostEntry &he = c.ent[e];
+            ce.push_back((s2cs[he.slot] << 1) | (he.diag ? 1 : 0));
+            cew.push_back((he.diag ? 1.0 : 2.0) * he.a);
+        }
+        clp.push_back((int)ce.size());
+    }
+    // per constraint slot its (compact constraint, a), constraints ascending (as slot_con)
+    std::vector<int> sp(ncs + 1, 0), sj(c.ent.size());
+    std::vector<double> sa(c.ent.size());
+    for (const HostEntry &he : c.ent) sp[s2cs[he.slot] + 1]++;
+    for (int t = 0; t < ncs; ++t) sp[t + 1] += sp[t];
+    std::vector<int> fp(sp.begin(), sp.end() - 1);
+    for (const HostEntry &he : c.ent) {
+        const int t = s2cs[he.slot];
+        sj[fp[t]] = compact[he.con];
+        sa[fp[t]] = he.a;
+        fp[t]++;
+    }
+    // objective entries of each row (column, global slot) when C is neither constant nor absent
+    std::vector<int> ccp(c.n + 1, 0), cc;
+    if (cconst == 0)
+        for (int i = 0; i < c.n; ++i) {
+            for (int q = c.adj_ptr[i]; q < c.adj_ptr[i + 1]; ++q)
+                if (c.Chas[c.adj_slot[q]]) { cc.push_back(c.adj_col[q]); cc.push_back(d.slot_off + c.adj_slot[q]); }
+            ccp[i + 1] = (int)(cc.size() / 2);
+        }
+    if (!dput(&d.cg_cadj_ptr, cap, err) || !dput(&d.cg_cadj, cadj, err) || !dput(&d.cg_cl_con, clcon, err) ||
+        !dput(&d.cg_cl_ptr, clp, err) || !dput(&d.cg_ce, ce, err) || !dput(&d.cg_ce_w, cew, err) ||
+        !dput(&d.cg_sp, sp, err) || !dput(&d.cg_sj, sj, err) || !dput(&d.cg_sa, sa, err) ||
+        !dput(&d.cg_cc_ptr, ccp, err) || !dput(&d.cg_cc, cc, err))
+        return false;
+    d.cg_ncs = ncs; d.cg_ncl = ncl; d.cg_ns = ns; d.cg_nce = (int)ce.size(); d.cg_nsc = (int)sj.size();
+    d.cg_nadj = (int)cadj.size(); d.cg_cconst = cconst; d.cg_cslot = d.slot_off + cslot;
+    d.cg_ok = 1;
+    return true;
+}
+
 bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
     {   // k_tile_bx (lrs_kernels.hip): opt-in, read when a problem is uploaded
         const char *e = getenv("LRS_TILE_BX");
@@ -939,6 +1034,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         if (!dput(&d.adj_ptr, c.adj_ptr, err) || !dput(&d.adj_low, c.adj_low, err) ||
             !dput(&d.adj_col, c.adj_col, err) || !dput(&d.adj_slot, adj_slot_g, err))
             return false;
+        if (c.own1 < 0 && c.n <= kScMaxN && !c.dense_c && !upload_small_cg(c, hp.m, d, err)) return false;
         if (c.n >= kNX && (long)c.adj_col.size() >= (long)kTileMinDeg * c.n) {
             std::vector<int> cs((size_t)c.n * (kNX + 1));
             for (int i = 0; i < c.n; ++i) {
@@ -1088,7 +1184,9 @@ void free_problem(DevProblem &dp) {
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);
-        f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); f(c.sx_slot); }
+        f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); f(c.sx_slot);
+        f(c.cg_cadj_ptr); f(c.cg_cadj); f(c.cg_cl_con); f(c.cg_cl_ptr); f(c.cg_ce); f(c.cg_sp); f(c.cg_sj);
+        f(c.cg_cc_ptr); f(c.cg_cc); f(c.cg_ce_w); f(c.cg_sa); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);

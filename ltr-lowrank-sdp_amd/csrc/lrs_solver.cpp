@@ -130,6 +130,7 @@ struct lrs_ctx {
     std::vector<int> t1c, t1o, t2c, t2o;
     long cgIterTotal = 0;
     std::vector<long> cgIterCone;
+    bool cg_dev_total = false;   // some half-step of this ADMM iteration counted its CG on the device
     std::string path;
     FILE *logfp = nullptr;
     // hipGraph cache of inner-iteration batches (keyed by batch size; the kernels'
@@ -2053,13 +2054,39 @@ static int admm_init_constr(lrs_ctx *c) {
     return 0;
 }
 
-static int admm_update_var(lrs_ctx *c, double rho, double tol, int maxit) {
-    for (int k = 0; k < c->dp.K; ++k) {
-        if (update_var_one(c, k, c->W.U, c->W.V, rho, tol, maxit)) return -1;
-        if (refresh_cone(c, k)) return -1;
-        if (update_var_one(c, k, c->W.V, c->W.U, rho, tol, maxit)) return -1;
-        if (refresh_cone(c, k)) return -1;
+// One half-step of LORADSUpdateSDPVar (lorads_alg_common.c:298-326) for cone k: side 0 solves U
+// with V fixed, 1 V with U fixed, then the cone's constraint refresh.  Small unsharded cones take
+// the single-workgroup kernel (lrs_kernels.hip k_small_cg: RHS, CG and refresh in one launch, its
+// iterations counted on the device in W.cgc[CG_TOTAL]); LRS_SMALL_CG=0 keeps the multi-launch CG.
+constexpr int kHpinCgTotal = 300;   // pinned slot of the device CG count
+static bool use_small_cg(lrs_ctx *c, int k) {
+    const char *e = getenv("LRS_SMALL_CG");
+    const int env = e ? atoi(e) : -1;
+    return env != 0 && small_cg_fits(c->dp, k);
+}
+static int admm_half_step(lrs_ctx *c, int k, int side, double rho, double tol, int maxit, bool *on_device) {
+    if (use_small_cg(c, k)) {
+        OPC(launch_small_cg(c->dp, c->W, k, side, rho, tol, maxit, c->st));
+        *on_device = true;
+        return 0;
     }
+    *on_device = false;
+    if (update_var_one(c, k, side ? c->W.V : c->W.U, side ? c->W.U : c->W.V, rho, tol, maxit)) return -1;
+    return refresh_cone(c, k);
+}
+
+static int admm_update_var(lrs_ctx *c, double rho, double tol, int maxit) {
+    bool dev = false;
+    for (int k = 0; k < c->dp.K; ++k)
+        for (int side = 0; side < 2; ++side) {
+            bool d = false;
+            if (admm_half_step(c, k, side, rho, tol, maxit, &d)) return -1;
+            dev |= d;
+        }
+    // the device-counted CG iterations, read behind the next stream sync (admm_eval's)
+    if (dev)
+        HIPC(hipMemcpyAsync(c->hpin + kHpinCgTotal, c->W.cgc + CG_TOTAL, sizeof(double), hipMemcpyDeviceToHost, c->st));
+    c->cg_dev_total = dev;
     return 0;
 }
 
@@ -2099,6 +2126,7 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
     const double orig = now_s();
     st.rho = std::min(st.rho, p->rhoMax);
     c->cgIterTotal = 0;
+    HIPC(hipMemsetAsync(c->W.cgc + CG_TOTAL, 0, sizeof(double), c->st));
     if (admm_init_constr(c)) return -1;
     if (admm_eval(c)) return -1;
     st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.gap = c->dimGap; st.pinf1 = c->dimPinf;
@@ -2112,8 +2140,8 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
         }
         const double cgtol = std::min(st.pinf1 * (reopt ? 1e-4 : 1e-2), 1e-8);
         if (admm_update_var(c, st.rho, cgtol, maxCG)) return -1;
-        st.cg_iter = c->cgIterTotal;
         if (admm_eval(c)) return -1;
+        st.cg_iter = c->cgIterTotal + (c->cg_dev_total ? (long)c->hpin[kHpinCgTotal] : 0);
         st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.pinf1 = c->dimPinf;
         st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
         st.gap = c->dimGap;
@@ -2752,13 +2780,15 @@ int lrs_op_admm_half(lrs_ctx *c, int cone, int side, double rho, double cg_tol, 
     if (!(rho > 0.0) || cg_maxit < 1) { set_err("lrs_op_admm_half: rho %g, cg_maxit %d", rho, cg_maxit); return -1; }
     // LORADSUpdateSDPVar's half-step for one cone (lorads_alg_common.c:303-314 for U, :316-324
     // for V): solve the side with the other fixed, then the cone's constraint-value refresh
-    double *X = side ? c->W.V : c->W.U;
-    const double *Y = side ? c->W.U : c->W.V;
     c->cgIterCone[cone] = 0;
-    if (update_var_one(c, cone, X, Y, rho, cg_tol, cg_maxit)) return -1;
-    if (refresh_cone(c, cone)) return -1;
-    if (cg_iters) *cg_iters = (int)c->cgIterCone[cone];
+    bool dev = false;
+    if (admm_half_step(c, cone, side, rho, cg_tol, cg_maxit, &dev)) return -1;
     HIPC(hipStreamSynchronize(c->st));
+    if (cg_iters) {
+        double it = (double)c->cgIterCone[cone];
+        if (dev) HIPC(hipMemcpy(&it, c->W.cgc + CG_ITERS, sizeof(double), hipMemcpyDeviceToHost));
+        *cg_iters = (int)it;
+    }
     if (rhs) {
         const DevCone &d = P.cones[cone];
         std::vector<double> h((size_t)d.n * d.ld);

@@ -43,12 +43,12 @@ def write_sdpa(path, m, dims, b, entries):
         for con, blk, ii, jj, vv in entries:
             con = np.asarray(con, dtype=np.int64)
             blk = np.broadcast_to(np.asarray(blk, dtype=np.int64), con.shape)
-            lines = [
-                f"{c} {bk} {i} {j} {v!r}\n"
-                for c, bk, i, j, v in zip(con.tolist(), blk.tolist(), np.asarray(ii).tolist(),
-                                          np.asarray(jj).tolist(), np.asarray(vv, dtype=float).tolist())
-            ]
-            f.writelines(lines)
+            ii, jj, vv = np.asarray(ii), np.asarray(jj), np.asarray(vv, dtype=float)
+            for a in range(0, con.size, 1 << 20):   # chunks: a dense C has 5e7 entries at n = 1e4
+                z = slice(a, a + (1 << 20))
+                f.writelines(f"{c} {bk} {i} {j} {v!r}\n"
+                             for c, bk, i, j, v in zip(con[z].tolist(), blk[z].tolist(), ii[z].tolist(),
+                                                       jj[z].tolist(), vv[z].tolist()))
     return path
 
 

@@ -1,11 +1,18 @@
 #!/bin/bash
-# Round 4, first call: the sharded-outer-tiles patch (k_g_part guard, sharded outer SDDMM / S.X on
-# the tiles, unpadded k_tile_b2 LDS rows) -- parity tests, the forced one-rank sharded bench legs,
-# a kernel trace of sharded C5, and the k_tile_b2 LDS counters.
+# Round 4: the GPU suite (sharded-tiles patch, C-ABI operators, single-workgroup ADMM half-step),
+# theta3 / theta3x3 ADMM with and without the single-workgroup half-step, the forced one-rank
+# sharded bench legs, a kernel trace of sharded C5 and the k_tile_b2 LDS counters.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-R=$PWD; O=$R/gpurun_out/r04a; mkdir -p $O
-timeout -k 10 700 python3 -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
+R=$PWD; O=$R/gpurun_out/r04b; mkdir -p $O
+timeout -k 10 800 python3 -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
 tail -3 $O/pytest.txt
+for v in 1 0; do
+  for t in theta3 theta3x3; do
+    LRS_SMALL_CG=$v timeout -k 10 120 python3 -u scripts/admm_probe.py $t >> $O/theta.txt 2>&1 || { tail -5 $O/theta.txt; exit 1; }
+  done
+  echo "LRS_SMALL_CG=$v done" >> $O/theta.txt
+done
+cat $O/theta.txt
 LRS_FORCE_SHARD=1 timeout -k 10 400 python3 -u bench.py --steps 50 --warmup 5 --no-cpu --no-eps --no-scale \
   --no-north-star --no-configs --no-c5 --no-c5b --sharded-all > $O/bench_sharded.log 2>&1 || { tail -5 $O/bench_sharded.log; exit 1; }
 python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); s=d['sharded']; print(json.dumps({k: s[k] for k in s if k not in ('c5','torus2000')})); print(json.dumps(s.get('c5'))); print(json.dumps(s.get('torus2000')))" $O/bench_sharded.log
@@ -19,5 +26,4 @@ for c in SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS; do
 done
 find $O/p2 -name "*.csv" -delete
 cat $O/sq.txt
-grep -E "c5_probe|stage|it/s" $O/p2.log | tail -5
 echo done

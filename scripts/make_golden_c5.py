@@ -14,6 +14,11 @@ Cases
             reference takes its dense syr2k / symm branches; the device its 2-D LDS tiles)
   c5_m1e5   the same structure with m = 10^5 (reference sparse branches; the device's
             gather kernels by default, the tiles when forced)
+  c5b_m1e6  C5b: the full C5 instance with C a dense random symmetric matrix (N(0, 1/n) + n I,
+            the bench's config_c5b workload): the reference's dense dsyr2k / dsymm branches
+            (lorads_alg_common.c:72-89, data/lorads_sdp_data.c:948-973) against the device's
+            dense objective on the FP64 matrix cores (k_cgemm2) -- run with the reference's
+            BLAS on 8 threads (OPENBLAS_NUM_THREADS, its n^2 r products)
 
 The instance is regenerated from ltr-lowrank-sdp_amd/instances.py
 random_sparse(10000, m, 6, 5) (the bench's config_c5 workload at m = 10^6) and its sha256
@@ -39,7 +44,10 @@ sys.path.insert(0, ROOT)
 GOLD = os.path.join(ROOT, "tests", "golden")
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "lorads_ref_harness")
 N, K_ENT, SEED, RANK = 10000, 6, 5, 128
-CASES = {"c5_m1e6": (1000000, [1, 2, 3]), "c5_m1e5": (100000, [1, 2, 3, 4, 5])}
+CASES = {"c5_m1e6": (1000000, [1, 2, 3]), "c5_m1e5": (100000, [1, 2, 3, 4, 5]),
+         "c5b_m1e6": (1000000, [1, 2, 3])}
+DENSE_C = {"c5b_m1e6"}
+BLAS_THREADS = {"c5b_m1e6": "8"}
 NPROJ_F, NPROJ_M, STRIDE_M = 2, 4, 997
 
 
@@ -59,12 +67,12 @@ def project_mvec(v, k=NPROJ_M, stride=STRIDE_M, seed=11):
 def main():
     names = sys.argv[1:] or list(CASES)
     inst = importlib.import_module("ltr-lowrank-sdp_amd.instances")
-    env = dict(os.environ, OPENBLAS_NUM_THREADS="1")
     for name in names:
         m, ks = CASES[name]
+        env = dict(os.environ, OPENBLAS_NUM_THREADS=BLAS_THREADS.get(name, "1"))
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             path = os.path.join(td, f"{name}.dat-s")
-            inst.random_sparse(path, N, m, K_ENT, SEED)
+            inst.random_sparse(path, N, m, K_ENT, SEED, dense_c=name in DENSE_C)
             sha = hashlib.sha256(open(path, "rb").read()).hexdigest()
             out = os.path.join(td, "s.bin")
             t0 = time.time()
@@ -75,7 +83,8 @@ def main():
                 raise RuntimeError(r.stdout[-2000:] + r.stderr[-2000:])
             nr = N * RANK
             z = {"ks": np.array(ks), "m": np.array(m), "dims": np.array([N]), "rank_flag": np.array(RANK),
-                 "sha256": np.array(sha), "wall_sec": np.array(wall)}
+                 "sha256": np.array(sha), "wall_sec": np.array(wall), "dense_c": np.array(name in DENSE_C),
+                 "blas_threads": np.array(int(env["OPENBLAS_NUM_THREADS"]))}
             for K in ks:
                 a = np.fromfile(f"{out}.K{K}")
                 done = int(a[0])

@@ -1,0 +1,90 @@
+"""The single-workgroup ADMM half-step (lrs_kernels.hip k_small_cg: LORADSUpdateSDPVarOne's
+right-hand side, CGSolve and the cone's constraint refresh in one launch) against the
+multi-launch device CG (LRS_SMALL_CG=0) and the reference's own sweep
+(tests/golden/admm_sweep_*.npz, scripts/make_golden_admm.py), on the instances where it is
+taken (every cone of <= 256 rows; theta with C = -J as slots and in the rank-one form)."""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import instance
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def solver_mod():
+    return importlib.import_module("ltr-lowrank-sdp_amd.solver")
+
+
+def rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+def sweep(solver_mod, name, monkeypatch, small):
+    """LORADSUpdateSDPVar over every cone + LORADSUpdateDualVar through the C-ABI operators."""
+    monkeypatch.setenv("LRS_SMALL_CG", "1" if small else "0")
+    k = np.load(os.path.join(ROOT, "tests", "golden", f"kernels_{name}.npz"))
+    vec, m, rank = k["inputs"], int(k["m"]), int(k["rank"])
+    dims = [int(d) for d in k["dims"]]
+    NR = sum(d * rank for d in dims)
+    tail = vec[9 * NR + 2 * m:]
+    rho, tol = float(tail[3]), float(tail[4])
+    sv = solver_mod.Solver(instance(name))
+    sv.set_rank([rank] * len(dims))
+    sv.set_factor(solver_mod.U, vec[7 * NR:8 * NR])
+    sv.set_factor(solver_mod.V, vec[8 * NR:9 * NR])
+    sv.set_vec(solver_mod.LAMBDA, vec[9 * NR:9 * NR + m])
+    sv.admm_constr()
+    its, rhs = [], []
+    for c in range(len(dims)):
+        for side in (0, 1):
+            _, rh, it = sv.admm_half(rho, tol, cone=c, side=side, init=False)
+            its.append(it)
+            rhs.append(rh)
+    sv.dual_update(rho)
+    out = dict(U=sv.get_factor(solver_mod.U), V=sv.get_factor(solver_mod.V), lam=sv.get_vec(solver_mod.LAMBDA),
+               its=np.array(its), rhs=rhs)
+    sv.close()
+    return out
+
+
+@pytest.mark.parametrize("name", ["theta25x3", "theta40", "mc_rand200", "rsparse60"])
+def test_small_cg_matches_multi_launch_and_reference(solver_mod, monkeypatch, name):
+    a = sweep(solver_mod, name, monkeypatch, small=True)
+    b = sweep(solver_mod, name, monkeypatch, small=False)
+    g = np.load(os.path.join(ROOT, "tests", "golden", f"admm_sweep_{name}.npz"))
+    # the half-steps' right-hand sides: the same arithmetic in another summation order
+    for x, y in zip(a["rhs"], b["rhs"]):
+        assert rel(x, y) < 1e-10
+    # CG solutions at cg_tol 1e-12: both paths and the reference within 1e-6 (the bar of the
+    # single half-step test), the two device paths far closer
+    for key in ("U", "V", "lam"):
+        assert rel(a[key], b[key]) < 1e-8, (key, rel(a[key], b[key]))
+        assert rel(a[key], g[key]) < 1e-6, (key, rel(a[key], g[key]))
+    for x, y in zip(a["its"], b["its"]):
+        assert abs(int(x) - int(y)) <= max(2, 0.1 * y), (a["its"], b["its"])
+    assert abs(a["its"].sum() - float(g["cg_total"])) <= max(4, 0.1 * float(g["cg_total"]))
+
+
+@pytest.mark.parametrize("name,flags", [("theta40", dict(reoptLevel=0)), ("theta25x3", dict(reoptLevel=0))])
+def test_small_cg_whole_solve(solver_mod, monkeypatch, name, flags):
+    """Whole solves with the ADMM phase on the single-workgroup half-step against the multi-launch
+    CG: the ALM phase is identical (the ADMM phase starts from the same point), ADMM iterations
+    within 2 % and the objectives within 10 x the certified gaps, as the reference bars of
+    tests/test_gpu_parity.py."""
+    res = {}
+    for small in (True, False):
+        monkeypatch.setenv("LRS_SMALL_CG", "1" if small else "0")
+        sv = solver_mod.Solver(instance(name))
+        res[small] = sv.solve(**flags)
+        sv.close()
+    a, b = res[True], res[False]
+    assert a["alm_inner"] == b["alm_inner"] and a["alm_pobj"] == b["alm_pobj"]
+    assert abs(a["admm_iter"] - b["admm_iter"]) <= max(2, 0.02 * b["admm_iter"])
+    tol = 10 * (a["gap"] + b["gap"]) + 1e-6
+    assert abs(a["pobj"] - b["pobj"]) <= tol * (1 + abs(b["pobj"]))
+    assert a["pinf"] <= 1e-4 and a["gap"] <= max(1e-4, 10 * b["gap"])
