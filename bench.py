@@ -378,6 +378,26 @@ def sharded_strong(solver, dist, world, rank_id, local, cache, replicas, steps=5
     return res
 
 
+def build_provenance():
+    """sha256 (first 16 hex) of the HIP library this run loads and of the sources it is built
+    from, and the library's mtime: whether the box ran the build of these sources is checkable
+    against the committed tree (`make -C ltr-lowrank-sdp_amd/csrc` rebuilds it)."""
+    import hashlib
+    csrc = os.path.join(ROOT, PKG, "csrc")
+    lib = os.path.join(ROOT, PKG, "_build", "liblrsdp.so")
+    h = hashlib.sha256()
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".cpp", ".h")) or f == "Makefile")
+    for f in names + ["../../include/lrsdp.h"]:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    out = {"sources_sha256_16": h.hexdigest()[:16], "sources": names + ["include/lrsdp.h"]}
+    if os.path.exists(lib):
+        with open(lib, "rb") as fh:
+            out["liblrsdp_sha256_16"] = hashlib.sha256(fh.read()).hexdigest()[:16]
+        out["liblrsdp_mtime"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(os.path.getmtime(lib)))
+    return out
+
+
 def spawn_ranks(n, argv):
     """`bench.py --gpus N` with no external launcher (WORLD_SIZE unset): start N fresh worker
     processes of this script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in
@@ -550,6 +570,7 @@ def main():
                    "flags": "--fixedRank %d --reoptLevel 0, phase-1 exit disabled, budget = steps" % r,
                    "parallelism": f"replicas x{world} (instance-level, weak)"},
         "alm_phase_rate": done / out["seconds"],
+        "build": build_provenance(),
         "roofline": stage_roofline(sv, 300, with_traffic=True),
     }
     if rank_id == 0 and world == 1 and not args.no_eps:

@@ -152,6 +152,10 @@ struct DevCone {
     int *cg_cadj_ptr = nullptr, *cg_cadj = nullptr, *cg_cl_con = nullptr, *cg_cl_ptr = nullptr, *cg_ce = nullptr;
     int *cg_sp = nullptr, *cg_sj = nullptr, *cg_cc_ptr = nullptr, *cg_cc = nullptr;
     double *cg_ce_w = nullptr, *cg_sa = nullptr;
+    // a cone with constraint-entry tiles (auv_items): the global slots holding C entries, for
+    // <C, X Y^T> straight from the factor rows (launch_cobj)
+    int cobj_n = 0;
+    int *cobj_slot = nullptr;
 };
 constexpr int kScMaxN = 256;         // rows of a cone the single-workgroup ADMM half-step takes
 constexpr int kMaxRankLd = 512;      // widest factor row (choose_layout: 64 lanes x 8 doubles)
@@ -286,6 +290,10 @@ int launch_gather(const DevProblem &P, const double *uvt, double scale, double *
 int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double scale,
                    int accumulate, double *out, const double *b_for_vio, double *vio_part, hipStream_t st,
                    const double *guard = nullptr, double *sum_upd = nullptr);   // sum_upd[i] += new - old out[i]
+// <C, sym(X Y^T)> (mode 0) or <C, X X^T> (mode 1) of a cone with constraint-entry tiles over
+// its C entries only (DevCone::cobj_slot), into tmpfin TF_SD + 2 cone (as launch_sddmm's sums)
+int launch_cobj(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double *part,
+                hipStream_t st);
 // S[slot] = (withC ? Craw[slot] : 0) + sum_(con,a) w[con] * a
 int launch_wsum(const DevProblem &P, const double *w, int withC, double *S, hipStream_t st);
 // out = scale * S X (+ addX * X) per cone, partial ||out||^2 -> part[0][pblk_off+b]

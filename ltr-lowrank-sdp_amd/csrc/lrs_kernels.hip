@@ -4452,6 +4452,41 @@ int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const
     return 0;
 }
 
+// <C, X Y^T> over a cone's C entries only (DevCone::cobj_slot): a lane group per entry reads
+// its two factor rows (auv_entry, as k_auv_con), sum of Cw d -> tmpfin TF_SD + 2 cone [0]
+template <int G, int E, int MODE>
+__global__ void __launch_bounds__(kBlock) k_cobj(int nl, const int *__restrict__ sl, const int *__restrict__ slot_rc,
+                                                 const double *__restrict__ Cw, int ld, const double *__restrict__ X,
+                                                 const double *__restrict__ Y, double *part, unsigned *ticket,
+                                                 double *fin) {
+    const int lane = threadIdx.x & (G - 1);
+    const int grp = (blockIdx.x * kBlock + threadIdx.x) / G, ngrp = gridDim.x * kBlock / G;
+    double acc[2] = {0.0, 0.0};
+    for (int t = grp; t < nl; t += ngrp) {
+        const int s = sl[t];
+        double d = auv_entry<E, MODE>(X, Y, ld, lane, slot_rc[2 * s], slot_rc[2 * s + 1]);
+        d = group_sum<G>(d);
+        if (lane == 0) acc[0] += Cw[s] * d;
+    }
+    partials_finalize<2>(acc, part, ticket, fin);
+}
+int launch_cobj(const DevProblem &P, int cone, int mode, const double *X, const double *Y, double *part,
+                hipStream_t st) {
+    const DevCone &c = P.cones[cone];
+    const int grid = std::max(1, std::min(grid_rows(std::max(1, c.cobj_n), c.G), 512));
+    const double *Xc = X + c.foff, *Yc = Y ? Y + c.foff : X + c.foff;
+    LRS_LAYOUT_SWITCH(c.G, c.E, {
+        if (mode == 1)
+            hipLaunchKernelGGL((k_cobj<GG, EE, 1>), dim3(grid), dim3(kBlock), 0, st, c.cobj_n, c.cobj_slot, P.slot_rc,
+                               P.Cw, c.ld, Xc, Xc, part, ticket_ptr(T_SDDMM), tmpfin_ptr() + TF_SD + 2 * cone);
+        else
+            hipLaunchKernelGGL((k_cobj<GG, EE, 0>), dim3(grid), dim3(kBlock), 0, st, c.cobj_n, c.cobj_slot, P.slot_rc,
+                               P.Cw, c.ld, Xc, Yc, part, ticket_ptr(T_SDDMM), tmpfin_ptr() + TF_SD + 2 * cone);
+    });
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
 int launch_gather(const DevProblem &P, const double *uvt, double scale, double *out, const double *b_for_vio,
                   double *vio_part, hipStream_t st, int *nblk_used) {
     const int grid = grid_elems(P.m, 1);

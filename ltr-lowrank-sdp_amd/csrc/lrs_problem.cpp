@@ -907,6 +907,16 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 err = "hipMalloc failed";
                 return false;
             }
+            // the objective's slots (op_constr_xx of a tiled cone: A(.) from the constraint-entry
+            // tiles, <C, X Y^T> from C's own entries instead of a pattern-wide SDDMM + gather)
+            if (hp.cones[k].own1 < 0) {
+                const HostCone &hc = hp.cones[k];
+                std::vector<int> co;
+                for (size_t t = 0; t < hc.prow.size(); ++t)
+                    if (hc.Chas[t]) co.push_back(d.slot_off + (int)t);
+                d.cobj_n = (int)co.size();
+                if (!dput(&d.cobj_slot, co, err)) return false;
+            }
         }
     }
     // Single-slot ("local") constraints: exactly one merged entry over all cones.  Their
@@ -1186,7 +1196,7 @@ void free_problem(DevProblem &dp) {
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);
         f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); f(c.sx_slot);
         f(c.cg_cadj_ptr); f(c.cg_cadj); f(c.cg_cl_con); f(c.cg_cl_ptr); f(c.cg_ce); f(c.cg_sp); f(c.cg_sj);
-        f(c.cg_cc_ptr); f(c.cg_cc); f(c.cg_ce_w); f(c.cg_sa); }
+        f(c.cg_cc_ptr); f(c.cg_cc); f(c.cg_ce_w); f(c.cg_sa); f(c.cobj_slot); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);

@@ -691,10 +691,21 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
                         double *blam = nullptr) {
     DevProblem &P = c->dp;
     DevWork &W = c->W;
+    int fin;
+    const char *ct = getenv("LRS_CONSTR_TILES");
+    if (P.K == 1 && !sharded(c) && P.cones[0].auv_items > 0 && P.cones[0].cobj_slot && !(ct && ct[0] == '0')) {
+        // a cone with constraint-entry tiles (C5): A(.) and the residual straight from the tiles
+        // (k_auv_tile + k_auv_tsum), <C, .> over C's own entries -- not a pattern-wide SDDMM
+        // then a gather of 10^6 constraints' slot values (C5: 203 + 95 + 282 -> ~240 us)
+        OPC(launch_auv_con(P, 0, Y ? 0 : 1, X, Y, 1.0, 0, W.cvs, P.b, W.part, c->st));
+        OPC(launch_cobj(P, 0, Y ? 0 : 1, X, Y, W.partB, c->st));
+        HIPC(hipMemcpyAsync(W.cvc, W.cvs, sizeof(double) * P.m, hipMemcpyDeviceToDevice, c->st));
+        fin = TF_GATHER;
+        goto READ;
+    }
     // every cone's <C, X Y^T> (tmpfin TF_SD + 2k) and the residual norm in one read
     for (int k = 0; k < P.K; ++k)
         OPC(launch_sddmm(P, k, Y ? 0 : 1, X, Y, W.uvt2, nullptr, W.part, 0, nullptr, c->st));
-    int fin;
     if (P.K == 1 && P.nsh > 0) {
         // sharded, shared constraints: the holders' owned-entry sums summed over the shards,
         // then the residual with each constraint counted once (its primary holder)
@@ -717,6 +728,7 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
         OPC(launch_resid(P.m, P.b, W.cvs, c->st, P.cmask));   // sharded: each constraint once
         fin = TF_RESID;
     }
+READ:
     if (blam) OPC(launch_dot(P.m, P.bprim ? P.bprim : P.b, W.lam, W.part, c->st, nullptr));
     double t[2 * kMaxCones + 3];
     if (read_tmpfin2(c, TF_SD, 2 * P.K, TF_GATHER, 3, t)) return -1;   // GATHER, RESID, DOT
