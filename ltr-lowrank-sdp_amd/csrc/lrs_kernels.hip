@@ -3147,6 +3147,134 @@ __global__ void __launch_bounds__(NT) k_tile_a(
     write_partials_range<8, NT>(acc, partA, pblk_off + blockIdx.x, 0, 7);
 }
 
+// k_tile_a with its factor tiles staged by direct global -> LDS loads (global_load_lds_dwordx4,
+// no VGPR destination) into TWO buffers of kGc-column chunks, so that chunk k + 1's loads are in
+// flight while chunk k is computed (k_tile_a stages through registers, one chunk at a time: its
+// register prefetch spills at 1 024 threads, and its waves wait on memory for ~65 % of their
+// cycles, profiles/r03aa_c5_tile_counters.md).  LDS image: per operand kAuvT rows of kGc doubles
+// (128 B), a row's eight 16-B units XOR-swizzled by (row & 7) through the global addresses (the
+// LDS side of global_load_lds is lane-linear), so the 16 lanes of a ds_read_b128 phase reading
+// 16 rows at one logical unit spread over the banks.  Per slot and chunk the arithmetic and its
+// order are k_tile_a's (auv_chunk<2>), so the values are bitwise equal.  Needs ld % kGc == 0 (a
+// chunk never crosses a row; columns in [r, ld) are the factor's zero padding).
+typedef __attribute__((address_space(1))) void lrs_gvoid;
+typedef __attribute__((address_space(3))) void lrs_lvoid;
+constexpr int kGc = 16;               // columns per staged chunk
+constexpr int kGu = kGc / 2;          // 16-B units per staged row
+constexpr int kGop = kAuvT * kGc;     // doubles per staged operand
+template <int NT, int NA>
+__device__ __forceinline__ void tg_stage(double *buf, int I0, int J0, int c0, int n, int ld,
+                                         const double *__restrict__ X, const double *__restrict__ Y) {
+    constexpr int NW = NT / 64, NP = NA * kAuvT / 8;   // 1-KB pieces (8 rows) of the NA operands
+    static_assert(NP % NW == 0, "tg_stage: pieces divide over the waves");
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < NP / NW; ++q) {
+        const int pc = w + q * NW;
+        const int a = pc / (kAuvT / 8), r0 = (pc % (kAuvT / 8)) * 8;
+        const int row = r0 + (lane >> 3), u = (lane & 7) ^ (row & 7);
+        const int grow = min(((a & 1) ? J0 : I0) + row, n - 1);   // rows past n: any valid row (never read)
+        const double *src = ((a < 2) ? X : Y) + (long)grow * ld + c0 + 2 * u;
+        __builtin_amdgcn_global_load_lds((lrs_gvoid *)src, (lrs_lvoid *)(buf + a * kGop + r0 * kGc), 16, 0, 0);
+    }
+}
+// one staged chunk of slot (pl, ql): auv_chunk<2>'s sums over the logical units in order
+__device__ __forceinline__ void tg_chunk2(const double *buf, int pl, int ql, double &s, double &s2) {
+    const double2 *xa = reinterpret_cast<const double2 *>(buf + pl * kGc);
+    const double2 *xb = reinterpret_cast<const double2 *>(buf + kGop + ql * kGc);
+    const double2 *ya = reinterpret_cast<const double2 *>(buf + 2 * kGop + pl * kGc);
+    const double2 *yb = reinterpret_cast<const double2 *>(buf + 3 * kGop + ql * kGc);
+    const int sp = pl & 7, sq = ql & 7;
+#pragma unroll 2
+    for (int u = 0; u < kGu; ++u) {   // not fully unrolled: the swizzled addresses are per unit
+        const double2 a = xa[u ^ sp], b = xb[u ^ sq], ay = ya[u ^ sp], by = yb[u ^ sq];
+        s += a.x * by.x + b.x * ay.x;
+        s += a.y * by.y + b.y * ay.y;
+        s2 += ay.x * by.x;
+        s2 += ay.y * by.y;
+    }
+}
+template <int NT>
+__global__ void __launch_bounds__(NT) k_tile_a_g(
+    int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
+    const int *__restrict__ tslot, const double *__restrict__ Cw, const double *__restrict__ Rb0,
+    const double *__restrict__ Rb1, const double *__restrict__ Dall, double *__restrict__ uRD,
+    double *__restrict__ uDD, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
+    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
+    const double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec,
+    const double *__restrict__ par, const double *__restrict__ ctrl_cur, double *__restrict__ partA, int pblk_off,
+    double2 *__restrict__ uvp) {
+    constexpr int NPT = kAuvItem / NT;
+    static_assert(NPT * NT == kAuvItem, "k_tile_a_g: items divide over the block");
+    if (ctrl_cur[C_ACTIVE] == 0.0) return;
+    const double *__restrict__ R = (ctrl_cur[C_RCUR] == 0.0 ? Rb0 : Rb1) + foff;
+    const double *__restrict__ D = Dall + foff;
+    const double rho = par[P_RHO], rhoInv = 1.0 / rho;
+    __shared__ double tg[2 * 4 * kGop];   // 128 KB: two buffers of R_I, R_J, D_I, D_J chunks
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int nch = (r + kGc - 1) / kGc;
+    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
+        const int4 it = items[itx];
+        const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
+        int pl[NPT], ql[NPT];
+        double s0[NPT], s1[NPT];
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) {
+            const int t = eb + (int)threadIdx.x + j * NT;
+            const unsigned w = t < ee ? pq[t] : 0u;
+            pl[j] = (int)(w >> 16);
+            ql[j] = (int)(w & 0xffffu);
+            s0[j] = 0.0;
+            s1[j] = 0.0;
+        }
+        __syncthreads();   // the previous item's reads of buffer 0 are done
+        tg_stage<NT, 4>(tg, I0, J0, 0, n, ld, R, D);
+        for (int k = 0; k < nch; ++k) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();   // chunk k landed for every wave; buffer (k + 1) & 1 is free
+            if (k + 1 < nch) tg_stage<NT, 4>(tg + ((k + 1) & 1) * 4 * kGop, I0, J0, (k + 1) * kGc, n, ld, R, D);
+            const double *buf = tg + (k & 1) * 4 * kGop;
+#pragma unroll
+            for (int j = 0; j < NPT; ++j) {
+                if (eb + (int)threadIdx.x + j * NT >= ee) break;
+                tg_chunk2(buf, pl[j], ql[j], s0[j], s1[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) {
+            const int t = eb + (int)threadIdx.x + j * NT;
+            if (t >= ee) break;
+            const int sl = tslot[t];
+            const double d0 = 0.5 * s0[j], d1 = s1[j];
+            if (uvp) {
+                uvp[sl] = make_double2(d0, d1);
+            } else {
+                uRD[sl] = d0;
+                uDD[sl] = d1;
+            }
+            const double cwl = Cw[sl];
+            acc[0] += cwl * d0;
+            acc[1] += cwl * d1;
+            const double2 l1l = loc1[sl];
+            const int c1 = (int)l1l.y;
+            const int e0 = c1 == -2 ? loc_ptr[sl] : 0, e1 = c1 == -2 ? loc_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
+            for (int e = e0; e < e1; ++e) {
+                const int ci = c1 >= 0 ? c1 : loc_con[e];
+                const double w = c1 >= 0 ? l1l.x : loc_w[e];
+                const double bi = b[ci], cvi = cvs[ci], li = lam[ci];
+                const double q1 = 2.0 * (w * d0), q2 = w * d1;
+                const double q0 = (bi - cvi) + rhoInv * li;
+                acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1;
+                acc[6] += q0 * q1;
+                double2 *rr = reinterpret_cast<double2 *>(rec + 4L * ci);
+                rr[0] = make_double2(cvi, q1);
+                rr[1] = make_double2(q2, (-li) + (-rho) * bi);
+            }
+        }
+    }
+    write_partials_range<8, NT>(acc, partA, pblk_off + blockIdx.x, 0, 7);
+}
+
 // row epilogue of stage B: G_new = 2 (S R_new [+ C R_new]), s = tau D, y = G_new - G_old
 // (setlbfgsHisTwo lorads_alm.c:842-863) and the nine L-BFGS dots
 template <int E>
@@ -3360,6 +3488,128 @@ __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: tw
                 if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
                 double unused = 0.0;
                 auv_chunk<1>(tl, pl[j], ql[j], dv[j], unused);
+            }
+        }
+        // the slot epilogue, kB1H slots at a time with their loads issued before the arithmetic
+        // (branch-free indices: entries past the item read the item's first slot, store nothing)
+        constexpr int kB1H = 4;
+#pragma unroll
+        for (int h = 0; h < kAuvNpt; h += kB1H) {
+        int slv[kB1H];
+        double2 s1v[kB1H], l1v[kB1H];
+        double crv[kB1H];
+#pragma unroll
+        for (int j = 0; j < kB1H; ++j) {
+            const int t = eb + (int)threadIdx.x + (h + j) * kAuvThreads;
+            slv[j] = tslot[t < ee ? t : eb];
+        }
+#pragma unroll
+        for (int j = 0; j < kB1H; ++j) {
+            s1v[j] = slot1[slv[j]];
+            l1v[j] = loc1[slv[j]];
+            crv[j] = Craw[slv[j]];
+        }
+        double2 rav[kB1H], rbv[kB1H];
+#pragma unroll
+        for (int j = 0; j < kB1H; ++j) {
+            const int c1 = (int)s1v[j].y;
+            const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * (c1 >= 0 ? c1 : 0));
+            rav[j] = q[0];
+            rbv[j] = q[1];
+        }
+#pragma unroll
+        for (int j = 0; j < kB1H; ++j) {
+            const int t = eb + (int)threadIdx.x + (h + j) * kAuvThreads;
+            if (t >= ee) break;
+            const int sl = slv[j];
+            double svl = crv[j];
+            const double2 s1l = s1v[j];
+            const int c1 = (int)s1l.y;
+            if (c1 >= 0) {
+                double cv = rav[j].x + tau * rav[j].y;
+                cv = cv + tau2 * rbv[j].x;
+                svl += (rbv[j].y + rho * cv) * s1l.x;
+            } else if (c1 == -2) {
+                for (int e = slot_ptr[sl]; e < slot_ptr[sl + 1]; ++e) {
+                    const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
+                    const double2 x = q[0], y = q[1];
+                    double cv = x.x + tau * x.y;
+                    cv = cv + tau2 * y.x;
+                    svl += (y.y + rho * cv) * slot_a[e];
+                }
+            }
+            Sv[sl] = svl;
+            const double d = dv[h + j];
+            uRR[sl] = d;
+            const double2 l1l = l1v[j];
+            const int cl = (int)l1l.y;
+            const int f0 = cl == -2 ? loc_ptr[sl] : 0, f1 = cl == -2 ? loc_ptr[sl + 1] : (cl >= 0 ? 1 : 0);
+            for (int e = f0; e < f1; ++e) {
+                const int ci = cl >= 0 ? cl : loc_con[e];
+                const double tot = (cl >= 0 ? l1l.x : loc_w[e]) * d;
+                cvs[ci] = tot;
+                const double dd = b[ci] - tot;
+                acc[9] += dd * dd;
+            }
+        }
+        }
+    }
+    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+}
+
+// one staged chunk of entry (pl, ql) over two staged operands: auv_chunk<1>'s sums in order
+__device__ __forceinline__ void tg_chunk1(const double *buf, int pl, int ql, double &s) {
+    const double2 *xa = reinterpret_cast<const double2 *>(buf + pl * kGc);
+    const double2 *xb = reinterpret_cast<const double2 *>(buf + kGop + ql * kGc);
+    const int sp = pl & 7, sq = ql & 7;
+#pragma unroll 2
+    for (int u = 0; u < kGu; ++u) {
+        const double2 a = xa[u ^ sp], b = xb[u ^ sq];
+        s += a.x * b.x;
+        s += a.y * b.y;
+    }
+}
+// k_tile_b1 with the R_new tiles staged by direct global -> LDS loads into two buffers (as
+// k_tile_a_g; same arithmetic and order as k_tile_b1, bitwise equal)
+__global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1_g(   // <= 128 VGPRs: two blocks a CU (68 KB LDS each)
+    int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
+    const int *__restrict__ tslot, const double *Rb0, const double *Rb1, double *__restrict__ uRR,
+    double *__restrict__ Sv, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
+    const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double2 *__restrict__ slot1,
+    const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
+    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
+    double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
+    const double *__restrict__ ls_cur, double *__restrict__ partC, int pblk_off) {
+    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
+    const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
+    const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
+    __shared__ double tg[2 * 2 * kGop];   // 64 KB: two buffers of R_new,I and R_new,J chunks
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const int nch = (r + kGc - 1) / kGc;
+    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
+        const int4 it = items[itx];
+        const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
+        int pl[kAuvNpt], ql[kAuvNpt];
+        double dv[kAuvNpt];
+#pragma unroll
+        for (int j = 0; j < kAuvNpt; ++j) {
+            const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+            const unsigned w = t < ee ? pq[t] : 0u;
+            pl[j] = (int)(w >> 16);
+            ql[j] = (int)(w & 0xffffu);
+            dv[j] = 0.0;
+        }
+        __syncthreads();   // the previous item's reads of buffer 0 are done
+        tg_stage<kRowBlock, 2>(tg, I0, J0, 0, n, ld, Rn, Rn);
+        for (int k = 0; k < nch; ++k) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();   // chunk k landed for every wave; buffer (k + 1) & 1 is free
+            if (k + 1 < nch) tg_stage<kRowBlock, 2>(tg + ((k + 1) & 1) * 2 * kGop, I0, J0, (k + 1) * kGc, n, ld, Rn, Rn);
+            const double *buf = tg + (k & 1) * 2 * kGop;
+#pragma unroll
+            for (int j = 0; j < kAuvNpt; ++j) {
+                if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
+                tg_chunk1(buf, pl[j], ql[j], dv[j]);
             }
         }
         // the slot epilogue, kB1H slots at a time with their loads issued before the arithmetic
@@ -5621,7 +5871,15 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2, W.D,      \
                        W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), \
                        P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, uvp)
-            if (nta == 512) LRS_TILE_A(512);
+            // LRS_TILE_GLDS=1: the same work staged by direct global -> LDS loads (k_tile_a_g)
+            static const int glds = getenv("LRS_TILE_GLDS") ? atoi(getenv("LRS_TILE_GLDS")) : 0;
+            if (glds && c.ld % kGc == 0) {
+                hipLaunchKernelGGL(k_tile_a_g<1024>, dim3(grid), dim3(1024), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
+                                   reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2,
+                                   W.D, W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,
+                                   reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam, W.rec, W.par,
+                                   ctrl_cur, W.part, off, uvp);
+            } else if (nta == 512) LRS_TILE_A(512);
             else LRS_TILE_A(1024);
 #undef LRS_TILE_A
         } else if (pa[k].wide) {
@@ -5749,6 +6007,15 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
             });
             offBF += grid;
         } else if (tbt[k]) {
+            static const int glds_b = getenv("LRS_TILE_GLDS") ? atoi(getenv("LRS_TILE_GLDS")) : 0;
+            if (glds_b && c.ld % kGc == 0)
+                hipLaunchKernelGGL(k_tile_b1_g, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
+                                   reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, W.R, W.R2, W.uvt2,
+                                   c.sa_S - c.slot_off, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,
+                                   reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,
+                                   reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur,
+                                   W.partC, off);
+            else
             hipLaunchKernelGGL(k_tile_b1, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
                                reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, W.R, W.R2, W.uvt2,
                                c.sa_S - c.slot_off, P.Craw, P.slot_ptr,

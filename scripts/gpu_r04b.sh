@@ -14,7 +14,10 @@ for v in 1 0; do
 done
 cat $O/theta.txt
 timeout -k 10 300 python3 -u scripts/c5_rate.py > $O/c5_rate.txt 2>&1 || { tail -5 $O/c5_rate.txt; exit 1; }
+LRS_TILE_GLDS=1 timeout -k 10 300 python3 -u scripts/c5_rate.py >> $O/c5_rate.txt 2>&1 || { tail -5 $O/c5_rate.txt; exit 1; }
 cat $O/c5_rate.txt
+LRS_TILE_GLDS=1 timeout -k 10 400 python3 -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests/test_gpu_c5_steps.py > $O/pytest_glds.txt 2>&1 || { tail -20 $O/pytest_glds.txt; exit 1; }
+tail -3 $O/pytest_glds.txt
 LRS_FORCE_SHARD=1 timeout -k 10 400 python3 -u bench.py --steps 50 --warmup 5 --no-cpu --no-eps --no-scale \
   --no-north-star --no-configs --no-c5 --no-c5b --sharded-all > $O/bench_sharded.log 2>&1 || { tail -5 $O/bench_sharded.log; exit 1; }
 python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); s=d['sharded']; print(json.dumps({k: s[k] for k in s if k not in ('c5','torus2000')})); print(json.dumps(s.get('c5'))); print(json.dumps(s.get('torus2000')))" $O/bench_sharded.log
