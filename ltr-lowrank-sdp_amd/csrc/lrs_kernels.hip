@@ -3679,6 +3679,64 @@ __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1_g(   // <= 128 VGPRs: 
     write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
 }
 
+// k_auv_tile staged by direct global -> LDS loads into two buffers (as k_tile_a_g): MODE 1
+// X_p . X_q, MODE 0 (X_p . Y_q + X_q . Y_p) / 2, per constraint entry, same order of sums
+__device__ __forceinline__ void tg_chunk0(const double *buf, int pl, int ql, double &s) {
+    const double2 *xa = reinterpret_cast<const double2 *>(buf + pl * kGc);
+    const double2 *xb = reinterpret_cast<const double2 *>(buf + kGop + ql * kGc);
+    const double2 *ya = reinterpret_cast<const double2 *>(buf + 2 * kGop + pl * kGc);
+    const double2 *yb = reinterpret_cast<const double2 *>(buf + 3 * kGop + ql * kGc);
+    const int sp = pl & 7, sq = ql & 7;
+#pragma unroll 2
+    for (int u = 0; u < kGu; ++u) {
+        const double2 a = xa[u ^ sp], b = xb[u ^ sq], ay = ya[u ^ sp], by = yb[u ^ sq];
+        s += a.x * by.x + b.x * ay.x;
+        s += a.y * by.y + b.y * ay.y;
+    }
+}
+template <int MODE>
+__global__ void __launch_bounds__(kAuvThreads) k_auv_tile_g(int n, int r, int ld, const int4 *__restrict__ items,
+                                                            const unsigned *__restrict__ pq,
+                                                            const int *__restrict__ ent, const double *__restrict__ X,
+                                                            const double *__restrict__ Y, double *__restrict__ val,
+                                                            const double *__restrict__ guard) {
+    if (guard && guard[0] == 0.0) return;
+    constexpr int NA = MODE == 0 ? 4 : 2;
+    __shared__ double tg[2 * NA * kGop];
+    const int4 it = items[blockIdx.x];
+    const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
+    int pl[kAuvNpt], ql[kAuvNpt];
+    double acc[kAuvNpt];
+#pragma unroll
+    for (int j = 0; j < kAuvNpt; ++j) {
+        const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+        const unsigned w = t < ee ? pq[t] : 0u;
+        pl[j] = (int)(w >> 16);
+        ql[j] = (int)(w & 0xffffu);
+        acc[j] = 0.0;
+    }
+    const int nch = (r + kGc - 1) / kGc;
+    __syncthreads();
+    tg_stage<kAuvThreads, NA>(tg, I0, J0, 0, n, ld, X, Y);
+    for (int k = 0; k < nch; ++k) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (k + 1 < nch) tg_stage<kAuvThreads, NA>(tg + ((k + 1) & 1) * NA * kGop, I0, J0, (k + 1) * kGc, n, ld, X, Y);
+        const double *buf = tg + (k & 1) * NA * kGop;
+#pragma unroll
+        for (int j = 0; j < kAuvNpt; ++j) {
+            if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
+            if constexpr (MODE == 1) tg_chunk1(buf, pl[j], ql[j], acc[j]);
+            else tg_chunk0(buf, pl[j], ql[j], acc[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kAuvNpt; ++j) {
+        const int t = eb + (int)threadIdx.x + j * kAuvThreads;
+        if (t < ee) val[ent[t]] = MODE == 0 ? 0.5 * acc[j] : acc[j];
+    }
+}
+
 constexpr int kTbC = 64;            // R_new columns staged per pass in k_tile_b2
 // LDS row stride: unpadded, so every staged row starts on bank 0 and the two rows a
 // ds_read_b128 service group mixes ({0-3,12-15} of one 16-lane row, {20-27} of the next,
@@ -4765,7 +4823,17 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
     double *fin = tmpfin_ptr() + TF_GATHER;
     if (c.auv_items > 0 && !P.shard) {
         // 2-D tiles through LDS, then the per-constraint sums
-        if (mode == 1)
+        static const int glds = getenv("LRS_TILE_GLDS") ? atoi(getenv("LRS_TILE_GLDS")) : 0;
+        if (glds && c.ld % kGc == 0) {
+            if (mode == 1)
+                hipLaunchKernelGGL((k_auv_tile_g<1>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
+                                   reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Xc, c.auv_val,
+                                   guard);
+            else
+                hipLaunchKernelGGL((k_auv_tile_g<0>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
+                                   reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Yc, c.auv_val,
+                                   guard);
+        } else if (mode == 1)
             hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
                                reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Xc, c.auv_val, guard);
         else

@@ -15,6 +15,9 @@ done
 cat $O/theta.txt
 timeout -k 10 300 python3 -u scripts/c5_rate.py > $O/c5_rate.txt 2>&1 || { tail -5 $O/c5_rate.txt; exit 1; }
 LRS_TILE_GLDS=1 timeout -k 10 300 python3 -u scripts/c5_rate.py >> $O/c5_rate.txt 2>&1 || { tail -5 $O/c5_rate.txt; exit 1; }
+for v in 0 1; do
+  LRS_TILE_GLDS=$v timeout -k 10 300 python3 -u scripts/c5_probe.py 10000 1000000 128 20 >> $O/c5_rate.txt 2>&1 || { tail -5 $O/c5_rate.txt; exit 1; }
+done
 cat $O/c5_rate.txt
 LRS_TILE_GLDS=1 timeout -k 10 400 python3 -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests/test_gpu_c5_steps.py > $O/pytest_glds.txt 2>&1 || { tail -20 $O/pytest_glds.txt; exit 1; }
 tail -3 $O/pytest_glds.txt
