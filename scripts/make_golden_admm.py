@@ -21,6 +21,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "lorads_ref_harness")
 NAMES = ["theta25x3", "mc_rand200", "rsparse60", "theta40"]
+# the kernels fixtures' cg_tol (1e-12) sits at the rounding floor of ||r||_2 / ||b||_1, where CG
+# iteration counts follow the rounding; the sweep is pinned at a tolerance the ADMM phase itself
+# reaches (its CG tol is min(1e-2 pinf, 1e-8), lorads_admm.c:127)
+CG_TOL = 1e-9
 
 
 def main():
@@ -29,8 +33,9 @@ def main():
     with tempfile.TemporaryDirectory() as td:
         for name in NAMES:
             k = np.load(os.path.join(GOLD, f"kernels_{name}.npz"))
-            vec, rank, m, dims = k["inputs"], int(k["rank"]), int(k["m"]), [int(d) for d in k["dims"]]
+            vec, rank, m, dims = k["inputs"].copy(), int(k["rank"]), int(k["m"]), [int(d) for d in k["dims"]]
             NR = sum(d * rank for d in dims)
+            vec[9 * NR + 2 * m + 4] = CG_TOL
             fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
             vec.astype(np.float64).tofile(fin)
             path = os.path.join(GOLD, "instances", f"{name}.dat-s")
@@ -46,7 +51,8 @@ def main():
             cg_last = out[p:p + len(dims)]; p += len(dims)
             assert p == out.size, (p, out.size)
             np.savez_compressed(os.path.join(GOLD, f"admm_sweep_{name}.npz"), U=U, V=V, cvs=cvs, lam=lam,
-                                cg_total=cg_total, cg_last=cg_last, rank=rank, m=m, dims=np.array(dims))
+                                cg_total=cg_total, cg_last=cg_last, rank=rank, m=m, dims=np.array(dims),
+                                cg_tol=CG_TOL)
             print("admm_sweep", name, "cones", len(dims), "cg", cg_total, cg_last)
 
 

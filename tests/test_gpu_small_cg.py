@@ -32,7 +32,8 @@ def sweep(solver_mod, name, monkeypatch, small):
     dims = [int(d) for d in k["dims"]]
     NR = sum(d * rank for d in dims)
     tail = vec[9 * NR + 2 * m:]
-    rho, tol = float(tail[3]), float(tail[4])
+    rho = float(tail[3])
+    tol = float(np.load(os.path.join(ROOT, "tests", "golden", f"admm_sweep_{name}.npz"))["cg_tol"])
     sv = solver_mod.Solver(instance(name))
     sv.set_rank([rank] * len(dims))
     sv.set_factor(solver_mod.U, vec[7 * NR:8 * NR])
@@ -60,14 +61,15 @@ def test_small_cg_matches_multi_launch_and_reference(solver_mod, monkeypatch, na
     # the half-steps' right-hand sides: the same arithmetic in another summation order
     for x, y in zip(a["rhs"], b["rhs"]):
         assert rel(x, y) < 1e-10
-    # CG solutions at cg_tol 1e-12: both paths and the reference within 1e-6 (the bar of the
-    # single half-step test), the two device paths far closer
+    # CG solutions at cg_tol 1e-9: both paths and the reference within 1e-6 (the bar of the
+    # single half-step test), the two device paths closer
     for key in ("U", "V", "lam"):
-        assert rel(a[key], b[key]) < 1e-8, (key, rel(a[key], b[key]))
+        assert rel(a[key], b[key]) < 1e-7, (key, rel(a[key], b[key]))
         assert rel(a[key], g[key]) < 1e-6, (key, rel(a[key], g[key]))
+    # CG counts (hundreds here, rounding-sensitive near the tolerance): as tests/test_capi.py
     for x, y in zip(a["its"], b["its"]):
-        assert abs(int(x) - int(y)) <= max(2, 0.1 * y), (a["its"], b["its"])
-    assert abs(a["its"].sum() - float(g["cg_total"])) <= max(4, 0.1 * float(g["cg_total"]))
+        assert abs(int(x) - int(y)) <= max(2, 0.25 * y), (a["its"], b["its"])
+    assert abs(a["its"].sum() - float(g["cg_total"])) <= max(4, 0.15 * float(g["cg_total"]))
 
 
 @pytest.mark.parametrize("name,flags", [("theta40", dict(reoptLevel=0)), ("theta25x3", dict(reoptLevel=0))])
