@@ -1,7 +1,8 @@
 """Per-trip parity on BASELINE config C5 (random sparse SDP, n = 10^4, 6 entries per
 constraint, C = I, --fixedRank 128) against the reference LoRADS C code's own trips.
 
-tests/golden/steps_c5_m1e6.npz / steps_c5_m1e5.npz come from scripts/make_golden_c5.py
+tests/golden/steps_c5_m1e6.npz / steps_c5_m1e5.npz / steps_c5b_m1e6.npz (C5b: the dense
+objective) come from scripts/make_golden_c5.py
 (oracle/ref_harness.c `alm_steps` over the reference objects, one run dumping K = 1..3 /
 1..5): per trip tau, rootNum, ||G||^2, pinf, and after trip K the factor, gradient, the
 newest L-BFGS pair (n x 2 projections), A(RR^T) and lambda (every 997th entry + 4 Gaussian
@@ -46,7 +47,7 @@ def mods():
             importlib.import_module("ltr-lowrank-sdp_amd.instances"))
 
 
-def _run(mods, name, monkeypatch, tiles):
+def _run(mods, name, monkeypatch, tiles, dense_c=False):
     solver, inst = mods
     fx = os.path.join(GOLDEN, f"steps_{name}.npz")
     if not os.path.exists(fx):
@@ -56,7 +57,7 @@ def _run(mods, name, monkeypatch, tiles):
     if tiles is not None:
         monkeypatch.setenv("LRS_SLOT_TILES", tiles)
         monkeypatch.setenv("LRS_AUV_TILES", tiles)
-    sv = solver.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(N, m, 6, 5)))
+    sv = solver.Solver(coo=inst.coo_arrays(inst.random_sparse_problem(N, m, 6, 5, dense_c=dense_c)))
     info = sv.tile_info()
     kw = {"reoptLevel": 0, "fixedRank": int(z["rank_flag"])}
     worst = {}
@@ -89,6 +90,16 @@ def test_c5_full_size_trips_match_reference(mods, monkeypatch):
     """m = 10^6, the bench's config_c5 workload, on the default (tiled) path."""
     info = _run(mods, "c5_m1e6", monkeypatch, None)
     assert info == (1, 1), info   # the 2-D tiles are the path measured by config_c5
+
+
+def test_c5b_full_size_trips_match_reference(mods, monkeypatch):
+    """C5b at full size (n = 10^4, m = 10^6, r = 128, C a dense random symmetric matrix N(0, 1/n)
+    + n I: the bench's config_c5b workload) against the reference's dense dsyr2k / dsymm branches
+    (lorads_alg_common.c:72-89, data/lorads_sdp_data.c:948-973; steps_c5b_m1e6.npz, its BLAS on 8
+    threads): the device keeps C as a full matrix on the FP64 matrix cores (k_cgemm2, DESIGN.md
+    §4.4) and the constraints on the 2-D tiles."""
+    info = _run(mods, "c5b_m1e6", monkeypatch, None, dense_c=True)
+    assert info[0] == 1, info
 
 
 @pytest.mark.parametrize("tiles", [None, "1"])
