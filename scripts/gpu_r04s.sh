@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 4 evidence of the final build: the default bench line (what the driver runs), the
+# headline rocprofv3 trace + FETCH/WRITE passes (profile_r01.sh), a C5 kernel trace.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$PWD; O=$R/gpurun_out/r04s; mkdir -p $O
+timeout -k 10 600 python3 -u bench.py --gpus 1 > $O/bench.json.log 2>&1 || { tail -5 $O/bench.json.log; exit 1; }
+python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d.get('config_c5',{}).get('gpu_it_s'), d.get('config_c5b',{}).get('gpu_it_s'), [ (r['config'], r.get('speedup')) for r in d.get('configs_wall_clock_to_eps', [])])" $O/bench.json.log
+timeout -k 10 900 bash scripts/profile_r01.sh r04s > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; }
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/c5 -o run -- python3 $R/scripts/c5_probe.py 10000 1000000 128 20 > $O/c5.log 2>&1) || { tail -5 $O/c5.log; exit 1; }
+grep -E "alm|stages" $O/c5.log
+echo done
