@@ -1440,6 +1440,38 @@ int oracle_kernels(oproblem *p, int rank, const double *in, double *out) {
     return (int)(op - out);
 }
 
+/* One ADMM variable update over every cone (LORADSUpdateSDPVar, lorads_alg_common.c:298-326)
+ * and the dual update after it (LORADSUpdateDualVar, :511-524) on the `kernels` input layout's
+ * U, V, lambda, rho_admm, cg_tol: out = U, V, A(UV^T) summed, lambda, total CG iterations,
+ * per cone its last (V-side) CG count -- what oracle/ref_harness.c `admm_sweep` dumps. */
+int oracle_admm_sweep(oproblem *p, int rank, const double *in, double *out) {
+    oparams prm;
+    default_oparams(&prm);
+    prm.fixedRank = rank;
+    osolver *s = osolver_new(p, &prm);
+    long NR = s->NR;
+    int m = s->m;
+    const double *U = in + 7 * NR, *V = in + 8 * NR, *lam = in + 9 * NR;
+    const double *tail = in + 9 * NR + 2 * m;
+    const double rho = tail[3], cg_tol = tail[4];
+    memcpy(s->U, U, 8 * NR); memcpy(s->V, V, 8 * NR);
+    memcpy(s->lam, lam, 8 * m);
+    constr_val_all(s, s->U, s->V);
+    s->cgIter = 0;
+    admm_update_var(s, rho, cg_tol, 800);
+    for (int i = 0; i < m; ++i) s->lam[i] += rho * s->p->b[i];
+    for (int i = 0; i < m; ++i) s->lam[i] += -rho * s->cvs[i];
+    double *op = out;
+    memcpy(op, s->U, 8 * NR); op += NR;
+    memcpy(op, s->V, 8 * NR); op += NR;
+    memcpy(op, s->cvs, 8 * m); op += m;
+    memcpy(op, s->lam, 8 * m); op += m;
+    *op++ = (double)s->cgIter;
+    for (int k = 0; k < s->K; ++k) *op++ = (double)s->cgIterCone[k];
+    osolver_free(s);
+    return (int)(op - out);
+}
+
 /* Test hook: first n outputs of the restated glibc generator. */
 int oracle_rand_seq(unsigned seed, int n, int *out) {
     grand_t g;

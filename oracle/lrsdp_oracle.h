@@ -26,6 +26,9 @@ int oracle_dims(const oproblem *p, int *m, int *ncones, int *dims);
 /* One call of each hot-path operator on caller-provided iterates.
  * `in`/`out` use exactly the binary layout of oracle/ref_harness.c mode_kernels. */
 int oracle_kernels(oproblem *p, int rank, const double *in, double *out);
+/* LORADSUpdateSDPVar over every cone + LORADSUpdateDualVar on the same input layout; out = U,
+ * V, A(UV^T), lambda, total CG iterations, per cone its last CG count (returns the length) */
+int oracle_admm_sweep(oproblem *p, int rank, const double *in, double *out);
 
 /* Full solve with LoRADS flags (argv-style, e.g. {"--reoptLevel","0"}).
  * res[0..15] = alm_inner, alm_outer, alm_pobj, alm_dobj, alm_pinf, alm_gap, alm_rho,

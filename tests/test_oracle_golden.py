@@ -92,3 +92,35 @@ def test_oracle_alm_steps_match_reference(oracle_lib, name):
         lam = z[f"K{K}_lam"]
         if np.linalg.norm(lam) > 0:
             assert rel_err(out[2 * nr + m:], lam) < 1e-9, K
+
+
+@pytest.mark.parametrize("name", ["theta25x3", "mc_rand200", "rsparse60", "theta40"])
+def test_oracle_admm_sweep_matches_reference(oracle_lib, name):
+    """The restatement's LORADSUpdateSDPVar over every cone + LORADSUpdateDualVar against the
+    reference's own run on the same inputs (tests/golden/admm_sweep_*.npz, cg_tol 1e-9): the
+    bars of tests/test_capi.py's device sweep."""
+    import ctypes as C
+    import os
+    import numpy as np
+    from golden_util import GOLDEN, instance
+    g = np.load(os.path.join(GOLDEN, f"admm_sweep_{name}.npz"))
+    k = np.load(os.path.join(GOLDEN, f"kernels_{name}.npz"))
+    vec, m, rank = k["inputs"].copy(), int(k["m"]), int(k["rank"])
+    dims = [int(d) for d in k["dims"]]
+    NR = sum(d * rank for d in dims)
+    vec[9 * NR + 2 * m + 4] = float(g["cg_tol"])
+    oracle_lib.oracle_admm_sweep.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    p = oracle_lib.oracle_read(instance(name).encode())
+    out = np.zeros(2 * NR + 2 * m + 1 + len(dims))
+    n = oracle_lib.oracle_admm_sweep(p, rank, vec.ctypes.data_as(C.POINTER(C.c_double)),
+                                     out.ctypes.data_as(C.POINTER(C.c_double)))
+    oracle_lib.oracle_free(p)
+    assert n == out.size
+    U, V, lam = out[:NR], out[NR:2 * NR], out[2 * NR + m:2 * NR + 2 * m]
+    for key, ours in (("U", U), ("V", V), ("lam", lam)):
+        assert rel_err(ours, g[key]) < 1e-6, (key, rel_err(ours, g[key]))
+    cg_last = out[2 * NR + 2 * m + 1:]
+    for c in range(len(dims)):
+        ref = float(g["cg_last"][c])
+        assert abs(cg_last[c] - ref) <= max(2, 0.25 * ref), (cg_last, g["cg_last"])
+    assert abs(out[2 * NR + 2 * m] - float(g["cg_total"])) <= max(4, 0.15 * float(g["cg_total"]))
