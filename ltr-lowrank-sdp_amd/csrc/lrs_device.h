@@ -156,15 +156,7 @@ struct DevCone {
     // <C, X Y^T> straight from the factor rows (launch_cobj)
     int cobj_n = 0;
     int *cobj_slot = nullptr;
-    // latency-regime kernels (k_lat_a / k_lat_b): a fixed-size record per row (kLatRecW int4) with
-    // {kb, kl, ke, 0}, the first kLatRecE adjacency entries {col, slot, the slot's single
-    // constraint (slot1.y), its single local constraint (loc1.y)} and the diagonal entry -- every
-    // index the row's loads need, one dependent load deep (null: the adjacency path)
-    int4 *lat_rec = nullptr;
 };
-constexpr int kLatRecE = 5;                  // entries a record holds (k_lat_b prefetches NO + 1 = 5)
-constexpr int kLatRecW = kLatRecE + 2;       // int4 per row: header, entries, diagonal
-constexpr int kLatRecMaxN = 131072;          // rows past which no record is built (the latency regime ends far earlier)
 constexpr int kScMaxN = 256;         // rows of a cone the single-workgroup ADMM half-step takes
 constexpr int kMaxRankLd = 512;      // widest factor row (choose_layout: 64 lanes x 8 doubles)
 constexpr int kAuvT = 128;           // rows of one side of an A(X Y^T) tile

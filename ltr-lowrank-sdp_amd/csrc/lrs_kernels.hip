@@ -2251,7 +2251,7 @@ __device__ __forceinline__ void wave_reduce_partials(const double *__restrict__ 
 // A in the latency regime (k_it_a MODE 0).  NO: off-diagonal lower entries whose operand
 // rows are prefetched before the barrier (the diagonal entry, the last lower one in the
 // column-sorted adjacency, uses the row's own operands); further ones are loaded after it.
-template <int G, int E, int NO, bool REC>
+template <int G, int E, int NO>
 __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
@@ -2265,8 +2265,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     const int *__restrict__ con_ptr, const int *__restrict__ con_slot, const double *__restrict__ con_w,
     const double *__restrict__ uRR, const double *__restrict__ par, const double *__restrict__ ctrl_prev,
     double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev, const double *__restrict__ partC, int nblkC,
-    double *__restrict__ partA, int pblk_off, int gwide, int nrb, int nda, const int *__restrict__ dra,
-    const int4 *__restrict__ lrec) {
+    double *__restrict__ partA, int pblk_off, int gwide, int nrb, int nda, const int *__restrict__ dra) {
     __shared__ double c[C_NCTRL];
     __shared__ double pl[P_NPAR];
     LRS_TS(0, 0);
@@ -2297,25 +2296,11 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     // (control block and parameters one word per lane: two vector loads, broadcast later)
     double px[kLatQ][10], ccv = 0.0, pvv = 0.0;
     int kb = 0, ke = 0;
-    // REC (row blocks): the row's prefetch record (DevCone::lat_rec) instead of the adjacency
-    // header -- its entries' columns, slots and single local constraints come with it
-    const bool urec = REC && !slice;
-    int4 rq[NO], rdq = make_int4(0, 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < NO; ++u) rq[u] = rdq;
     if (ctrl_wave) {
         load_partials<10>(partC, nblkC, px);
         const int l64 = threadIdx.x & 63;
         ccv = ctrl_prev[min(l64, C_NCTRL - 1)];
         pvv = par[min(l64, P_NPAR - 1)];
-    } else if (urec) {
-        const int4 *q = lrec + (long)ic * kLatRecW;
-        const int4 hd = q[0];
-        kb = hd.x;
-        ke = hd.y;
-#pragma unroll
-        for (int u = 0; u < NO; ++u) rq[u] = q[1 + u];
-        rdq = q[1 + kLatRecE];
     } else {
         kb = adj_ptr[ic];
         ke = adj_low[ic];
@@ -2379,27 +2364,14 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         int eb = kb, nl = valid ? ke - kb : 0;
         if (slice) { eb = kb + sq; nl = valid ? max(0, min(kSliceA, ke - eb)) : 0; }
         else if (nl > kDenseRow) nl = 0;
-        int jd, lcq[NO], lcd = 0;   // lcq / lcd: the entries' single local constraints (REC)
-        if (urec) {
-            jd = rdq.x;
-            sd = rdq.y;
-            lcd = rdq.w;
+        const int kd = nl > 0 ? eb + nl - 1 : 0;
+        const int jd = adj_col[kd];
+        sd = adj_slot[kd];
 #pragma unroll
-            for (int u = 0; u < NO; ++u) {
-                jj[u] = rq[u].x;
-                ss[u] = rq[u].y;
-                lcq[u] = rq[u].w;
-            }
-        } else {
-            const int kd = nl > 0 ? eb + nl - 1 : 0;
-            jd = adj_col[kd];
-            sd = adj_slot[kd];
-#pragma unroll
-            for (int u = 0; u < NO; ++u) {
-                const int k = nl > 0 ? eb + min(u, nl - 1) : 0;
-                jj[u] = adj_col[k];
-                ss[u] = adj_slot[k];
-            }
+        for (int u = 0; u < NO; ++u) {
+            const int k = nl > 0 ? eb + min(u, nl - 1) : 0;
+            jj[u] = adj_col[k];
+            ss[u] = adj_slot[k];
         }
         kb = eb;
         dg = !slice && nl > 0 && jd == i;
@@ -2420,20 +2392,15 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         // slots without a single local constraint read the row's own (spread, cached) index
         // instead of a common one: no hot line shared by every lane
         const int ispare = min(ic, m - 1);
-        if (!urec) {
-#pragma unroll
-            for (int u = 0; u < NO; ++u) lcq[u] = (int)l1[u].y;
-            lcd = (int)l1d.y;
-        }
 #pragma unroll
         for (int u = 0; u < NO; ++u) {
-            const int ci = lcq[u] >= 0 ? lcq[u] : ispare;
+            const int ci = (int)l1[u].y >= 0 ? (int)l1[u].y : ispare;
             bq[u] = b[ci];
             cq[u] = cvs[ci];
             lq[u] = lam[ci];
         }
         {
-            const int ci = lcd >= 0 ? lcd : ispare;
+            const int ci = (int)l1d.y >= 0 ? (int)l1d.y : ispare;
             bd = b[ci];
             cd = cvs[ci];
             lmd = lam[ci];
@@ -2571,7 +2538,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
 // partials and solves the line search while the row waves prefetch the row header, the
 // first NO off-diagonal entries (records and neighbour rows R_j, D_j) and the diagonal
 // entry's records; after the barrier only the tau-dependent arithmetic and the stores run.
-template <int G, int E, int NO, bool REC>
+template <int G, int E, int NO>
 __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
@@ -2584,7 +2551,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     const double *__restrict__ partA, int nblkA, const double *__restrict__ partB, int nblkB,
     double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m, double *hmirror,
     double seq, int nrb, int ndb, const int *__restrict__ drb, double *__restrict__ gl, double *CRb,
-    const double *__restrict__ CDb, const int4 *__restrict__ lrec) {
+    const double *__restrict__ CDb) {
     __shared__ double red[12];
     __shared__ double ls[LS_N];
     __shared__ double pl[P_NPAR];
@@ -2616,24 +2583,10 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     // parameters, the row waves' row header
     double pa[kLatQ][7], pb[kLatQ][5], pvv = 0.0;
     int kb = 0, kl = 0, ke = 0;
-    // REC (row blocks): the row's prefetch record (DevCone::lat_rec), as k_lat_a
-    const bool urec = REC && !slice;
-    int4 rq[NO + 1], rdq = make_int4(0, 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u <= NO; ++u) rq[u] = rdq;
     if (ctrl_wave) {
         load_partials<7>(partA, nblkA, pa);
         if (nblkB > 0) load_partials<5>(partB, nblkB, pb);
         pvv = par[min((int)(threadIdx.x & 63), P_NPAR - 1)];
-    } else if (urec) {
-        const int4 *q = lrec + (long)ic * kLatRecW;
-        const int4 hd = q[0];
-        kb = hd.x;
-        kl = hd.y;
-        ke = hd.z;
-#pragma unroll
-        for (int u = 0; u <= NO; ++u) rq[u] = q[1 + u];
-        rdq = q[1 + kLatRecE];
     } else {
         kb = adj_ptr[ic];
         kl = adj_low[ic];
@@ -2703,43 +2656,24 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
         else if (nt > kDenseRow) { nt = 0; dense = true; }
         // the diagonal is the last lower entry (columns ascending); positions of the first
         // NO + 1 entries, the off-diagonal ones picked after the diagonal test
-        int jd, ja[NO + 1], sa[NO + 1];
-        int ca[NO + 1], la[NO + 1], c1d = 0, cld = 0;   // the entries' single constraints (REC)
-        if (urec) {
-            jd = rdq.x;
-            sd = rdq.y;
-            c1d = rdq.z;
-            cld = rdq.w;
+        const int kd = (!slice && nt > 0 && kl > kb) ? kl - 1 : 0;
+        const int jd = adj_col[kd];
+        sd = adj_slot[kd];
+        int ja[NO + 1], sa[NO + 1];
 #pragma unroll
-            for (int u = 0; u <= NO; ++u) {
-                ja[u] = rq[u].x;
-                sa[u] = rq[u].y;
-                ca[u] = rq[u].z;
-                la[u] = rq[u].w;
-            }
-        } else {
-            const int kd = (!slice && nt > 0 && kl > kb) ? kl - 1 : 0;
-            jd = adj_col[kd];
-            sd = adj_slot[kd];
-#pragma unroll
-            for (int u = 0; u <= NO; ++u) {
-                const int k = nt > 0 ? eb + min(u, nt - 1) : 0;
-                ja[u] = adj_col[k];
-                sa[u] = adj_slot[k];
-                ca[u] = la[u] = 0;
-            }
+        for (int u = 0; u <= NO; ++u) {
+            const int k = nt > 0 ? eb + min(u, nt - 1) : 0;
+            ja[u] = adj_col[k];
+            sa[u] = adj_slot[k];
         }
         dg = !slice && nt > 0 && kl > kb && jd == i;
         no = nt - (dg ? 1 : 0);
         const int pd = dg ? kl - 1 - kb : NO + 1;    // the diagonal's position among the first
-        int c1q[NO], clq[NO];
 #pragma unroll
         for (int u = 0; u < NO; ++u) {
             const bool past = u >= pd;
             const int j = past ? ja[u + 1] : ja[u];
             ss[u] = past ? sa[u + 1] : sa[u];
-            c1q[u] = past ? ca[u + 1] : ca[u];
-            clq[u] = past ? la[u + 1] : la[u];
             lw[u] = eb + u + (past ? 1 : 0) < kl;
             const long oj = (long)(u < no ? j : ic) * ld + lane * E;
             ld_row<E>(R + oj, rjp[u]);
@@ -2754,27 +2688,18 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
         // slots without a single constraint read the row's own (spread, cached) index instead
         // of a common one: no hot line shared by every lane
         const int ispare = min(ic, m - 1);
-        if (!urec) {
-#pragma unroll
-            for (int u = 0; u < NO; ++u) {
-                c1q[u] = (int)s1v[u].y;
-                clq[u] = (int)l1v[u].y;
-            }
-            c1d = (int)s1d.y;
-            cld = (int)l1d.y;
-        }
 #pragma unroll
         for (int u = 0; u < NO; ++u) {
-            const int c1 = c1q[u] >= 0 ? c1q[u] : ispare;
-            const int cl = clq[u] >= 0 ? clq[u] : ispare;
+            const int c1 = (int)s1v[u].y >= 0 ? (int)s1v[u].y : ispare;
+            const int cl = (int)l1v[u].y >= 0 ? (int)l1v[u].y : ispare;
             const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
             ra[u] = r[0];
             rb[u] = r[1];
             bq[u] = b[cl];
         }
         {
-            const int c1 = c1d >= 0 ? c1d : ispare;
-            const int cl = cld >= 0 ? cld : ispare;
+            const int c1 = (int)s1d.y >= 0 ? (int)s1d.y : ispare;
+            const int cl = (int)l1d.y >= 0 ? (int)l1d.y : ispare;
             const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
             rad = r[0];
             rbd = r[1];
@@ -5703,25 +5628,15 @@ static int plan_b(const DevCone &c, int K, StagePlan &p, int force) {
 // resident, no teams (T == 1), and each stage's producer partials within one control
 // wave's reach.  NB (prefetched entries) from the most entries of one row.
 constexpr int kLatNoA = 2, kLatNoB = 4;   // off-diagonal entries prefetched (A: lower, B: all)
-static_assert(kLatNoA <= kLatRecE && kLatNoB + 1 <= kLatRecE, "prefetch records hold the entries the kernels read");
-// resident blocks: the smaller of the two forms (adjacency / prefetch records)
 template <int GG, int EE>
 static int res_la() {
-    static int c = 0, d = 0;
-    return std::min(resident_blocks(k_lat_a<GG, EE, kLatNoA, false>, &c),
-                    resident_blocks(k_lat_a<GG, EE, kLatNoA, true>, &d));
+    static int c = 0;
+    return resident_blocks(k_lat_a<GG, EE, kLatNoA>, &c);
 }
 template <int GG, int EE>
 static int res_lb() {
-    static int c = 0, d = 0;
-    return std::min(resident_blocks(k_lat_b<GG, EE, kLatNoB, false>, &c),
-                    resident_blocks(k_lat_b<GG, EE, kLatNoB, true>, &d));
-}
-// the latency kernels read the prefetch records where the cone has them (LRS_LAT_REC=0: the
-// adjacency path everywhere)
-static const int4 *lat_rec_of(const DevCone &c) {
-    const char *e = getenv("LRS_LAT_REC");   // read per launch (captured once in the ALM graph)
-    return (e && atoi(e) == 0) ? nullptr : c.lat_rec;
+    static int c = 0;
+    return resident_blocks(k_lat_b<GG, EE, kLatNoB>, &c);
 }
 static bool lat_disabled() {
     static int v = -1;
@@ -5991,19 +5906,15 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, pa[k].T, gwide, c.row0, \
                        pstr)
         if (lat) {
-            const int4 *lrec = lat_rec_of(c);
-#define LRS_LAT_A(REC_)                                                                                        \
-    hipLaunchKernelGGL((k_lat_a<GG, EE, kLatNoA, REC_>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,  \
-                       c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0],  \
-                       W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,                 \
-                       reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam, W.rec, k == 0 ? 1 : 0, P.mg,  \
-                       P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w, W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, \
-                       inC, nC, W.part, off, gwide, lg[k].nrb, (int)c.dra_h.size(), c.dra, lrec)
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                if (lrec) LRS_LAT_A(true);
-                else LRS_LAT_A(false);
+                hipLaunchKernelGGL((k_lat_a<GG, EE, kLatNoA>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
+                                   c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D,
+                                   W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr,
+                                   P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam,
+                                   W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,
+                                   W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, gwide,
+                                   lg[k].nrb, (int)c.dra_h.size(), c.dra);
             });
-#undef LRS_LAT_A
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
                 if (!split) LRS_LAUNCH_A(2, 0);
@@ -6106,20 +6017,16 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        (MM) != 2 && k == 0 ? a.hmirror : nullptr, a.seq, P.ndense ? W.CR : nullptr, W.CD)
         const bool small = pb[k].small;
         if (lat) {
-            const int4 *lrec = lat_rec_of(c);
-#define LRS_LAT_B(REC_)                                                                                        \
-    hipLaunchKernelGGL((k_lat_b<GG, EE, kLatNoB, REC_>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,  \
-                       c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], \
-                       W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,                          \
-                       reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,             \
-                       reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, inA, nA, W.partB,     \
-                       P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, P.m, k == 0 ? a.hmirror : nullptr, a.seq,        \
-                       lg[k].nrb, (int)c.drb_h.size(), c.drb, W.gl + glo, P.ndense ? W.CR : nullptr, W.CD, lrec)
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                if (lrec) LRS_LAT_B(true);
-                else LRS_LAT_B(false);
+                hipLaunchKernelGGL((k_lat_b<GG, EE, kLatNoB>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
+                                   c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0],
+                                   W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
+                                   P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con,
+                                   P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur,
+                                   inA, nA, W.partB, P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, P.m,
+                                   k == 0 ? a.hmirror : nullptr, a.seq, lg[k].nrb, (int)c.drb_h.size(), c.drb,
+                                   W.gl + glo, P.ndense ? W.CR : nullptr, W.CD);
             });
-#undef LRS_LAT_B
             glo += (long)lg[k].sb * c.ld;
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {

@@ -632,32 +632,6 @@ static bool dput(T **dst, const std::vector<T> &v, std::string &err) {
     return true;
 }
 
-// The latency kernels' per-row prefetch records (lrs_device.h DevCone::lat_rec): for row i,
-// {kb, kl, ke, 0} (adjacency start, end of the lower part, end), the entries kb, kb + 1, ...
-// (clamped to the row's last, or global entry 0 for an empty row, as the kernels' own clamped
-// loads are) and the diagonal entry (the last lower one, kl - 1, or entry 0) as {col, global
-// slot, slot1's single constraint, loc1's single local constraint}: the row waves of k_lat_a /
-// k_lat_b then have every index one load deep, instead of adj_ptr -> adj_col / adj_slot ->
-// slot1 / loc1 -> the constraint's records.
-static bool build_lat_rec(int n, const int *ap, const int *al, const int *ac, const int *asg,
-                          const std::vector<double> &s1, const std::vector<double> &l1, int4 **dst,
-                          std::string &err) {
-    if (n <= 0 || n > kLatRecMaxN) return true;
-    std::vector<int4> rec((size_t)n * kLatRecW);
-    auto ent = [&](long k) {
-        const int s = asg[k];
-        return make_int4(ac[k], s, (int)s1[2L * s + 1], (int)l1[2L * s + 1]);
-    };
-    for (int i = 0; i < n; ++i) {
-        int4 *r = &rec[(size_t)i * kLatRecW];
-        const int kb = ap[i], kl = al[i], ke = ap[i + 1], nt = ke - kb;
-        r[0] = make_int4(kb, kl, ke, 0);
-        for (int u = 0; u < kLatRecE; ++u) r[1 + u] = ent(nt > 0 ? kb + std::min(u, nt - 1) : 0);
-        r[1 + kLatRecE] = ent(kl > kb ? kl - 1 : 0);
-    }
-    return dput(dst, rec, err);
-}
-
 // The single-workgroup ADMM half-step's lists of one small cone (lrs_device.h DevCone::cg_*,
 // lrs_kernels.hip k_small_cg): built when the objective is constant (rank-one form, or every
 // slot of the block holding one value), absent, or at most 16 entries a row; else cg_ok stays 0
@@ -979,8 +953,8 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
     // per slot, its single constraint entry / single local constraint as one 16-byte record
     // {a or w, con} (con = -1: none, -2: several -> the lists): one dependent load less per
     // neighbour in the row kernels (slot -> record -> rec[con] instead of slot -> ptr -> con -> rec)
-    std::vector<double> s1(2L * std::max(1, Ptot), 0.0), l1(2L * std::max(1, Ptot), 0.0);
     {
+        std::vector<double> s1(2L * std::max(1, Ptot), 0.0), l1(2L * std::max(1, Ptot), 0.0);
         for (int t = 0; t < Ptot; ++t) {
             const int ns = slot_ptr[t + 1] - slot_ptr[t];
             s1[2L * t] = ns == 1 ? slot_a[slot_ptr[t]] : 0.0;
@@ -1043,9 +1017,6 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         if (!dput(&mc.adj_ptr, ap, err) || !dput(&mc.adj_low, al, err) || !dput(&mc.adj_col, ac, err) ||
             !dput(&mc.adj_slot, as, err))
             return false;
-        if (hp.cones[0].own1 < 0 && !build_lat_rec((int)ntot, ap.data(), al.data(), ac.data(), as.data(), s1, l1,
-                                                   &mc.lat_rec, err))
-            return false;
         dp.has_merged = true;
     }
     for (int k = 0; k < hp.K; ++k) {
@@ -1074,9 +1045,6 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             !dput(&d.adj_col, c.adj_col, err) || !dput(&d.adj_slot, adj_slot_g, err))
             return false;
         if (c.own1 < 0 && c.n <= kScMaxN && !c.dense_c && !upload_small_cg(c, hp.m, d, err)) return false;
-        if (c.own1 < 0 && !build_lat_rec(c.n, c.adj_ptr.data(), c.adj_low.data(), c.adj_col.data(), adj_slot_g.data(),
-                                         s1, l1, &d.lat_rec, err))
-            return false;
         if (c.n >= kNX && (long)c.adj_col.size() >= (long)kTileMinDeg * c.n) {
             std::vector<int> cs((size_t)c.n * (kNX + 1));
             for (int i = 0; i < c.n; ++i) {
@@ -1228,10 +1196,10 @@ void free_problem(DevProblem &dp) {
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);
         f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); f(c.sx_slot);
         f(c.cg_cadj_ptr); f(c.cg_cadj); f(c.cg_cl_con); f(c.cg_cl_ptr); f(c.cg_ce); f(c.cg_sp); f(c.cg_sj);
-        f(c.cg_cc_ptr); f(c.cg_cc); f(c.cg_ce_w); f(c.cg_sa); f(c.cobj_slot); f(c.lat_rec); }
+        f(c.cg_cc_ptr); f(c.cg_cc); f(c.cg_ce_w); f(c.cg_sa); f(c.cobj_slot); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
-        f(dp.merged.dra); f(dp.merged.drb); f(dp.merged.lat_rec);
+        f(dp.merged.dra); f(dp.merged.drb);
     }
     dp = DevProblem();
 }

@@ -1,16 +1,8 @@
 #!/bin/bash
-# Round 4: the GPU suite (sharded-tiles patch, C-ABI operators, single-workgroup ADMM half-step),
-# theta3 / theta3x3 ADMM with and without the single-workgroup half-step, the forced one-rank
+# Round 4: theta3 / theta3x3 ADMM with and without the single-workgroup half-step, the forced one-rank
 # sharded bench legs, a kernel trace of sharded C5 and the k_tile_b2 LDS counters.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD; O=$R/gpurun_out/r04b; mkdir -p $O
-# test failures (rc 1) do not stop the probes below; a timeout, abort or crash does
-timeout -k 10 800 python3 -u -m pytest -v -m gpu --timeout 300 --timeout-method thread tests > $O/pytest.txt 2>&1
-rc=$?
-grep -E "FAILED|ERROR" $O/pytest.txt | head -20
-tail -3 $O/pytest.txt
-[ $rc -le 1 ] || exit $rc
-! grep -q -E "^\+* *Timeout|Timeout \(>" $O/pytest.txt || { echo "a test timed out: stopping"; exit 3; }
 for v in 1 0; do
   for t in theta3 theta3x3; do
     LRS_SMALL_CG=$v timeout -k 10 120 python3 -u scripts/admm_probe.py $t >> $O/theta.txt 2>&1 || { tail -5 $O/theta.txt; exit 1; }
@@ -39,7 +31,6 @@ for c in SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS; do
 done
 find $O/p2 -name "*.csv" -delete
 cat $O/sq.txt
-cd $R && timeout -k 10 200 python3 -u scripts/stage_timing.py > $O/stage_timing.txt 2>&1 || { tail -5 $O/stage_timing.txt; exit 1; }
-cat $O/stage_timing.txt
+cd $R
 timeout -k 10 300 bash scripts/gpu_r04c.sh
 echo done

@@ -7,7 +7,6 @@ import importlib
 import json
 import os
 
-import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -131,27 +130,3 @@ def test_bundled_theta102_matches_reference(solver_mod):
         assert abs(r[ours] - ref[theirs]) <= tol * (1 + abs(ref[theirs])), (ours, r[ours], ref[theirs], tol)
     assert r["pinf"] <= max(1e-4, 10 * ref["admm_pinf"])
     assert r["final_rank"] == g["json"]["trajectory"]["phase_1"]["curr_rank"][-1]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("name", ["G11", "cphil12", *HUBS])
-def test_lat_prefetch_records_bit_identical(solver_mod, name, monkeypatch):
-    """The latency kernels' per-row prefetch records (DevCone::lat_rec, lrs_problem.cpp
-    build_lat_rec) only change where the row waves read their indices from: trips, factor,
-    gradient and multipliers bit-identical to the adjacency path (LRS_LAT_REC=0), the hubs'
-    slice blocks included (they keep the adjacency path)."""
-    monkeypatch.setenv("LRS_SMALL", "0")
-    out = []
-    for rec in ("1", "0"):
-        monkeypatch.setenv("LRS_LAT_REC", rec)
-        sv = solver_mod.Solver(os.path.join(DATA, f"{name}.dat-s"))
-        sv.set_kernel_path(0)
-        d = sv.alm_steps(6, reoptLevel=0)
-        assert sv.kernel_path() == 0, "latency kernels not taken"
-        out.append(d)
-        sv.close()
-    a, b = out
-    for key in ("tau", "lag", "pinf"):
-        assert a[key] == b[key], (key, a[key], b[key])
-    for key in ("R", "G", "lam", "cvs"):
-        assert np.array_equal(a[key], b[key]), key
