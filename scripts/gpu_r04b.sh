@@ -10,6 +10,11 @@ for v in 1 0; do
   echo "LRS_SMALL_CG=$v done" >> $O/theta.txt
 done
 cat $O/theta.txt
+LRS_CG_SPLIT=1 timeout -k 10 200 python3 -u scripts/c5b_sens.py $O/c5b_s1.npz > $O/c5b_sens.txt 2>&1 || { tail -5 $O/c5b_sens.txt; exit 1; }
+timeout -k 10 200 python3 -u scripts/c5b_sens.py $O/c5b_sa.npz $O/c5b_s1.npz >> $O/c5b_sens.txt 2>&1 || { tail -5 $O/c5b_sens.txt; exit 1; }
+LRS_CG_SPLIT=3 timeout -k 10 200 python3 -u scripts/c5b_sens.py $O/c5b_s3.npz $O/c5b_sa.npz >> $O/c5b_sens.txt 2>&1 || { tail -5 $O/c5b_sens.txt; exit 1; }
+rm -f $O/*.npz
+cat $O/c5b_sens.txt
 timeout -k 10 300 python3 -u scripts/c5_rate.py > $O/c5_rate.txt 2>&1 || { tail -5 $O/c5_rate.txt; exit 1; }
 LRS_TILE_GLDS=1 timeout -k 10 300 python3 -u scripts/c5_rate.py >> $O/c5_rate.txt 2>&1 || { tail -5 $O/c5_rate.txt; exit 1; }
 for v in 0 1; do
@@ -18,19 +23,4 @@ done
 cat $O/c5_rate.txt
 LRS_TILE_GLDS=1 timeout -k 10 400 python3 -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests/test_gpu_c5_steps.py > $O/pytest_glds.txt 2>&1 || { tail -20 $O/pytest_glds.txt; exit 1; }
 tail -3 $O/pytest_glds.txt
-LRS_FORCE_SHARD=1 timeout -k 10 400 python3 -u bench.py --steps 50 --warmup 5 --no-cpu --no-eps --no-scale \
-  --no-north-star --no-configs --no-c5 --no-c5b --sharded-all > $O/bench_sharded.log 2>&1 || { tail -5 $O/bench_sharded.log; exit 1; }
-python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); s=d['sharded']; print(json.dumps({k: s[k] for k in s if k not in ('c5','torus2000')})); print(json.dumps(s.get('c5'))); print(json.dumps(s.get('torus2000')))" $O/bench_sharded.log
-cd /tmp && export TMPDIR=/tmp
-LRS_FORCE_SHARD=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_sharded -o run -- python3 $R/scripts/sharded_c5_probe.py sharded > $O/sharded.log 2>&1 || { tail -5 $O/sharded.log; exit 1; }
-grep -E "info" $O/sharded.log
-timeout -s KILL 200 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv -d $O/p2 -o run -- python3 -u $R/scripts/c5_probe.py 10000 1000000 128 4 > $O/p2.log 2>&1 || { tail -5 $O/p2.log; exit 1; }
-f=$(ls $O/p2/*counter_collection.csv | head -1)
-for c in SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS; do
-  for k in k_tile_a k_tile_b1 k_tile_b2 k_auv_tile; do python3 $R/scripts/pmc_sum.py $f $c $k >> $O/sq.txt; done
-done
-find $O/p2 -name "*.csv" -delete
-cat $O/sq.txt
-cd $R
-timeout -k 10 300 bash scripts/gpu_r04c.sh
 echo done
