@@ -45,6 +45,19 @@ for ng in ("1", "0"):
                 t = ph[k]
                 seq = [f"{names[k][p]}:{(t[p] - t[p - 1]) * 0.01:.2f}" for p in range(1, len(names[k]))]
                 print(f"K{'AGB'[k]} phases (us):", " ".join(seq))
+            # latency kernels (k_lat_a / k_lat_b, block 0): row waves' own operands / neighbours
+            # loaded, the control wave's partial sums and control step, from the block's entry
+            a0, b0 = ph[0], ph[2]
+            if a0[0] and a0[7] and a0[8]:
+                print("k_lat_a block 0 (us from entry): own rows", round((a0[1] - a0[0]) * 0.01, 2), "neighbours",
+                      round((a0[2] - a0[0]) * 0.01, 2), "| ctrl partials summed", round((a0[8] - a0[0]) * 0.01, 2),
+                      "ctrl_step done", round((a0[7] - a0[0]) * 0.01, 2), "| barrier", round((a0[3] - a0[0]) * 0.01, 2),
+                      "rows done", round((a0[5] - a0[0]) * 0.01, 2), "partials stored", round((a0[6] - a0[0]) * 0.01, 2))
+            if b0[0] and b0[7] and b0[8]:
+                print("k_lat_b block 0 (us from entry): own rows", round((b0[5] - b0[0]) * 0.01, 2), "neighbours",
+                      round((b0[6] - b0[0]) * 0.01, 2), "| ctrl partials summed", round((b0[8] - b0[0]) * 0.01, 2),
+                      "line search done", round((b0[7] - b0[0]) * 0.01, 2), "| barrier", round((b0[2] - b0[0]) * 0.01, 2),
+                      "rows done", round((b0[3] - b0[0]) * 0.01, 2), "partials stored", round((b0[4] - b0[0]) * 0.01, 2))
             t = ph[2]
             if t[6] and t[11]:
                 print("KB rows detail (us from LS end): header", round((t[6] - t[2]) * 0.01, 2), "chunk1 data",

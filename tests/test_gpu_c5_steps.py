@@ -15,7 +15,11 @@ The instance is built in memory from the same seeded generator the fixture was m
 (instances.random_sparse_problem; the file's sha256 is in the fixture, and the in-memory
 load equals the file load: test_gpu_parity.py::test_coo_load_matches_file).
 
-Tolerance: 1e-9 relative, as tests/test_gpu_steps.py.
+Tolerance: 1e-9 relative, as tests/test_gpu_steps.py; C5b 5e-8: its second trip amplifies the
+rounding of the dense C R (n = 10^4 terms a row) ~500x (trip 1: R 1.7e-11 against the reference,
+trip 2: 7e-9), and the device's own summation orders differ from each other by as much -- k_cgemm2
+with one split-K slab against the default split: R 1.1e-8, tau 1.1e-9 at trip 3, and 1.9e-8 against
+the reference (scripts/c5b_sens.py, profiles/r04b_c5b_sens.txt).
 """
 import importlib
 import os
@@ -27,6 +31,7 @@ from golden_util import GOLDEN, rel_err
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-9
+TOL_C5B = 5e-8   # the dense objective's rounding sensitivity (docstring)
 N = 10000
 
 
@@ -47,7 +52,7 @@ def mods():
             importlib.import_module("ltr-lowrank-sdp_amd.instances"))
 
 
-def _run(mods, name, monkeypatch, tiles, dense_c=False):
+def _run(mods, name, monkeypatch, tiles, dense_c=False, tol=TOL):
     solver, inst = mods
     fx = os.path.join(GOLDEN, f"steps_{name}.npz")
     if not os.path.exists(fx):
@@ -68,10 +73,10 @@ def _run(mods, name, monkeypatch, tiles, dense_c=False):
         d = sv.alm_steps(K, **kw)
         assert d["inner"] == K, (K, d["inner"])
         tau, rn, lag, pinf = trips[K - 1]
-        assert abs(d["tau"] - tau) <= TOL * abs(tau), (K, d["tau"], tau)
-        assert abs(d["lag"] - lag) <= TOL * abs(lag), (K, d["lag"], lag)
-        assert abs(d["pinf"] - pinf) <= TOL * max(abs(pinf), 1e-300), (K, d["pinf"], pinf)
-        assert abs(d["beta"] - z[f"K{K}_beta"][0]) <= TOL * abs(z[f"K{K}_beta"][0])
+        assert abs(d["tau"] - tau) <= tol * abs(tau), (K, d["tau"], tau)
+        assert abs(d["lag"] - lag) <= tol * abs(lag), (K, d["lag"], lag)
+        assert abs(d["pinf"] - pinf) <= tol * max(abs(pinf), 1e-300), (K, d["pinf"], pinf)
+        assert abs(d["beta"] - z[f"K{K}_beta"][0]) <= tol * abs(z[f"K{K}_beta"][0])
         for key in ("R", "G", "s", "y", "cvs", "lam"):
             ref = z[f"K{K}_{key}"]
             ours = project_mvec(d[key]) if key in ("cvs", "lam") else project_factor(d[key], N)
@@ -80,7 +85,7 @@ def _run(mods, name, monkeypatch, tiles, dense_c=False):
                 continue
             e = rel_err(ours, ref)
             worst[key] = max(worst.get(key, 0.0), e)
-            assert e < TOL, (K, key, e)
+            assert e < tol, (K, key, e)
     sv.close()
     print(f"{name} tiles={info}: worst rel errors {worst}")
     return info
@@ -98,7 +103,7 @@ def test_c5b_full_size_trips_match_reference(mods, monkeypatch):
     (lorads_alg_common.c:72-89, data/lorads_sdp_data.c:948-973; steps_c5b_m1e6.npz, its BLAS on 8
     threads): the device keeps C as a full matrix on the FP64 matrix cores (k_cgemm2, DESIGN.md
     §4.4) and the constraints on the 2-D tiles."""
-    info = _run(mods, "c5b_m1e6", monkeypatch, None, dense_c=True)
+    info = _run(mods, "c5b_m1e6", monkeypatch, None, dense_c=True, tol=TOL_C5B)
     assert info[0] == 1, info
 
 
