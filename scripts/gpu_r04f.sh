@@ -7,10 +7,10 @@ timeout -k 10 200 python3 -u scripts/stage_timing.py > $O/stage_timing.txt 2>&1 
 cat $O/stage_timing.txt
 timeout -k 10 400 python3 -u -m pytest -x -v -m gpu --timeout 300 --timeout-method thread tests/test_gpu_c5_steps.py > $O/pytest_c5.txt 2>&1 || { tail -20 $O/pytest_c5.txt; exit 1; }
 tail -3 $O/pytest_c5.txt
-(cd /tmp && export TMPDIR=/tmp && LRS_SMALL_CG=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/t3 -o run -- python3 $R/scripts/admm_probe.py theta3 > $O/t3.log 2>&1) || { tail -5 $O/t3.log; exit 1; }
+(cd /tmp && export TMPDIR=/tmp && LRS_SMALL_CG=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t3 -o run -- python3 $R/scripts/admm_probe.py theta3 > $O/t3.log 2>&1) || { tail -5 $O/t3.log; exit 1; }
 grep theta3 $O/t3.log
 f=$(find $O/t3 -name "*kernel_stats.csv" | head -1); head -25 "$f" | cut -d, -f1-8 > $O/t3_stats.txt; cat $O/t3_stats.txt
-find $O/t3 -name "*.db" -delete
+find $O/t3 -name "*.csv" ! -name "*_kernel_stats.csv" -delete
 LRS_FORCE_SHARD=1 timeout -k 10 400 python3 -u bench.py --steps 50 --warmup 5 --no-cpu --no-eps --no-scale \
   --no-north-star --no-configs --no-c5 --no-c5b --sharded-all > $O/bench_sharded.log 2>&1 || { tail -5 $O/bench_sharded.log; exit 1; }
 python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); s=d['sharded']; print(json.dumps({k: s[k] for k in s if k not in ('c5','torus2000')})); print(json.dumps(s.get('c5'))); print(json.dumps(s.get('torus2000')))" $O/bench_sharded.log
