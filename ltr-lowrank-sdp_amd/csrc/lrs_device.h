@@ -74,7 +74,11 @@ enum ParIdx {
 enum LsIdx { LS_TAU = 0, LS_ROOTNUM, LS_FLAG, LS_N = 4 };
 // ---- finals of the standalone launchers (g_tmpfin offsets)
 constexpr int kMaxCones = 256;
-enum TmpFinIdx { TF_SD = 0, TF_GATHER = 2 * kMaxCones, TF_RESID, TF_DOT, TF_SPMM, TF_N = TF_SPMM + kMaxCones };
+// TF_DOTC + k: cone k's <X, C Y> of a dense objective (op_constr_xx), read with the gather's sums
+enum TmpFinIdx {
+    TF_SD = 0, TF_GATHER = 2 * kMaxCones, TF_RESID, TF_DOT, TF_DOTC, TF_SPMM = TF_DOTC + kMaxCones,
+    TF_N = TF_SPMM + kMaxCones
+};
 constexpr int kMaxShards = 64;       // processes of one sharded solve
 constexpr int kLongRow = 32;         // constraint rows longer than this get a wave each
 
@@ -302,7 +306,8 @@ int launch_spmm(const DevProblem &P, int cone, const double *S, const double *X,
                 int *nblk_used, hipStream_t st);
 // generic BLAS-1 over the factor buffer / m-vectors with partial dots
 int launch_axpby(long n, double a, const double *x, double b, double *y, hipStream_t st);
-int launch_dot(long n, const double *x, const double *y, double *part, hipStream_t st, int *nblk_used);
+int launch_dot(long n, const double *x, const double *y, double *part, hipStream_t st, int *nblk_used,
+               int fin = TF_DOT);
 int launch_fill(long n, double v, double *x, hipStream_t st);
 // lam += rho (b - cvs)
 int launch_dual_update(const DevProblem &P, double rho, double *lam, const double *cvs, hipStream_t st);

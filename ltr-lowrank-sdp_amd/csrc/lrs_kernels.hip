@@ -4979,10 +4979,10 @@ int launch_fill(long n, double v, double *x, hipStream_t st) {
     LRS_CHECK_LAUNCH();
     return 0;
 }
-int launch_dot(long n, const double *x, const double *y, double *part, hipStream_t st, int *nblk_used) {
+int launch_dot(long n, const double *x, const double *y, double *part, hipStream_t st, int *nblk_used, int fin) {
     const int grid = grid_elems(n, 8);
     hipLaunchKernelGGL(k_dot, dim3(grid), dim3(kBlock), 0, st, n, x, y, part, ticket_ptr(T_DOT),
-                       tmpfin_ptr() + TF_DOT);
+                       tmpfin_ptr() + fin);
     LRS_CHECK_LAUNCH();
     if (nblk_used) *nblk_used = grid;
     return 0;

@@ -1044,7 +1044,9 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
         if (!dput(&d.adj_ptr, c.adj_ptr, err) || !dput(&d.adj_low, c.adj_low, err) ||
             !dput(&d.adj_col, c.adj_col, err) || !dput(&d.adj_slot, adj_slot_g, err))
             return false;
-        if (c.own1 < 0 && c.n <= kScMaxN && !c.dense_c && !upload_small_cg(c, hp.m, d, err)) return false;
+        // (a constant objective, const_c, is dense_c too: its rank-one form is the kernel's cconst 2)
+        if (c.own1 < 0 && c.n <= kScMaxN && (!c.dense_c || c.const_c) && !upload_small_cg(c, hp.m, d, err))
+            return false;
         if (c.n >= kNX && (long)c.adj_col.size() >= (long)kTileMinDeg * c.n) {
             std::vector<int> cs((size_t)c.n * (kNX + 1));
             for (int i = 0; i < c.n; ++i) {

@@ -730,20 +730,21 @@ static int op_constr_xx(lrs_ctx *c, const double *X, const double *Y, double *pi
     }
 READ:
     if (blam) OPC(launch_dot(P.m, P.bprim ? P.bprim : P.b, W.lam, W.part, c->st, nullptr));
-    double t[2 * kMaxCones + 3];
-    if (read_tmpfin2(c, TF_SD, 2 * P.K, TF_GATHER, 3, t)) return -1;   // GATHER, RESID, DOT
-    double o = 0.0;
-    for (int k = 0; k < P.K; ++k) o += t[2 * k];
-    // dense objective: <C, sym X Y^T> = <X, C Y>
+    // dense objective: <C, sym X Y^T> = <X, C Y> over the rows C X covers (sharded: the owned
+    // rows, summed over the shards), into TF_DOTC + k, read behind the same sync
     for (int k = 0; k < P.K && obj; ++k) {
         const DevCone &dc = P.cones[k];
         if (!dc.dense_c) continue;
         OPC(launch_dense_cx(P, k, Y ? Y : X, W.CD, 0.0, c->st));
-        double v;   // over the rows C X covers (sharded: the owned rows, summed over the shards)
         const long ro = dc.foff + (long)dc.row0 * dc.ld;
-        if (op_dot(c, (long)dc.nown * dc.ld, X + ro, W.CD + ro, &v)) return -1;
-        o += v;
+        OPC(launch_dot((long)dc.nown * dc.ld, X + ro, W.CD + ro, W.part, c->st, nullptr, TF_DOTC + k));
     }
+    double t[3 * kMaxCones + 3];
+    if (read_tmpfin2(c, TF_SD, 2 * P.K, TF_GATHER, 3 + P.K, t)) return -1;   // GATHER, RESID, DOT, DOTC
+    double o = 0.0;
+    for (int k = 0; k < P.K; ++k) o += t[2 * k];
+    for (int k = 0; k < P.K && obj; ++k)
+        if (P.cones[k].dense_c) o += t[2 * P.K + (TF_DOTC - TF_GATHER) + k];
     if (pinf) *pinf = std::sqrt(t[2 * P.K + (fin - TF_GATHER)]) / (1 + c->hp.bNrm1);
     if (blam) *blam = t[2 * P.K + (TF_DOT - TF_GATHER)];
     if (obj) *obj = o;
