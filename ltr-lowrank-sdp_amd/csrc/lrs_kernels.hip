@@ -2310,6 +2310,12 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     // buffers) exactly when `fold` holds
     const double lsflag = ls_prev[LS_FLAG];
     const int fold = (ctrl_prev[C_ACT2] != 0.0 && ctrl_prev[C_PENDING] == 1.0 && lsflag == 0.0) ? 1 : 0;
+#ifdef LRS_PHASE_TIMING
+    // diagnostics: the row header (a vector load) and the control words (scalar loads) arrived
+    if (blockIdx.x == 0 && threadIdx.x == 0 && kb != -12345) g_phase_tmp[0][10] = wall_clock64();
+    if (blockIdx.x == 0 && threadIdx.x == 0 && fold != 12345) g_phase_tmp[0][9] = wall_clock64();
+    if (blockIdx.x == 0 && ctrl_wave && (threadIdx.x & 63) == 0 && ccv != 12345.678) g_phase_tmp[0][11] = wall_clock64();
+#endif
     const bool r1 = (ctrl_prev[C_RCUR] != 0.0) != (fold != 0);
     const bool g1 = (ctrl_prev[C_GCUR] != 0.0) != (fold != 0);
     const double *__restrict__ R = (r1 ? Rb1 : Rb0) + foff;
@@ -6934,6 +6940,53 @@ static size_t small_cg_lds(int n, int rS, int ncl, int ncs, int nce, int nsc, in
     return dbl * sizeof(double) + in * sizeof(int);
 }
 
+// block-wide global -> LDS copy with KB loads in flight per thread: a loop of one load per
+// iteration (trip count unknown to the compiler) waits one memory trip per element it copies
+template <int KB, typename T>
+__device__ __forceinline__ void sc_stage(T *dst, const T *__restrict__ src, int n) {
+    for (int t0 = (int)threadIdx.x; t0 < n; t0 += KB * kScT) {
+        T v[KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const int t = t0 + u * kScT;
+            v[u] = src[t < n ? t : t0];
+        }
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const int t = t0 + u * kScT;
+            if (t < n) dst[t] = v[u];
+        }
+    }
+}
+
+// acc += sum_e S_e Y_j over one row's constraint slots e in [e0, e1) in entry order, four
+// entries a pass (their indices, S values and operand rows loaded together)
+template <int EL>
+__device__ __forceinline__ void sc_row_apply(int e0, int e1, const int *cadj, const double *T, const double *Ys,
+                                             int rS, int r, int l, double (&acc)[EL]) {
+    for (int e = e0; e < e1; e += 4) {
+        int pk[4];
+        double sv[4], y[4][EL];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pk[u] = cadj[min(e + u, e1 - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            sv[u] = T[pk[u] & 0xffff];
+#pragma unroll
+            for (int k = 0; k < EL; ++k) {
+                const int c = l + kScL * k;
+                y[u][k] = c < r ? Ys[(pk[u] >> 16) * rS + c] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (e + u < e1)
+#pragma unroll
+                for (int k = 0; k < EL; ++k)
+                    if (l + kScL * k < r) acc[k] += sv[u] * y[u][k];
+    }
+}
+
 template <int EL, int RPG>
 __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
     extern __shared__ double smem[];
@@ -6954,16 +7007,28 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
     const int tid = threadIdx.x, g = tid / kScL, l = tid % kScL, wid = tid >> 6, lane = tid & 63;
     double *X = (A.side ? A.V : A.U) + A.foff;
     const double *Yg = (A.side ? A.U : A.V) + A.foff;
-    for (int t = tid; t < n * r; t += kScT) {
-        const int i = t / r, c = t - i * r;
-        Ys[i * rS + c] = Yg[(long)i * A.ld + c];
+    // stage the fixed factor and the lists (batched loads: one memory trip per ~4K elements)
+    for (int t0 = tid; t0 < n * r; t0 += 8 * kScT) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = min(t0 + u * kScT, n * r - 1), i = t / r, c = t - i * r;
+            v[u] = Yg[(long)i * A.ld + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int t = t0 + u * kScT, i = t / r, c = t - i * r;
+            if (t < n * r) Ys[i * rS + c] = v[u];
+        }
     }
-    for (int t = tid; t <= n; t += kScT) cap[t] = A.cadj_ptr[t];
-    for (int t = tid; t < A.nadj; t += kScT) cadj[t] = A.cadj[t];
-    for (int t = tid; t <= A.ncl; t += kScT) clp[t] = A.cl_ptr[t];
-    for (int t = tid; t < A.nce; t += kScT) { ce[t] = A.ce[t]; cew[t] = A.ce_w[t]; }
-    for (int t = tid; t <= A.ncs; t += kScT) sp[t] = A.sp[t];
-    for (int t = tid; t < A.nsc; t += kScT) { sj[t] = A.sj[t]; sav[t] = A.sa[t]; }
+    sc_stage<8>(cap, A.cadj_ptr, n + 1);
+    sc_stage<8>(cadj, A.cadj, A.nadj);
+    sc_stage<8>(clp, A.cl_ptr, A.ncl + 1);
+    sc_stage<8>(ce, A.ce, A.nce);
+    sc_stage<8>(cew, A.ce_w, A.nce);
+    sc_stage<8>(sp, A.sp, A.ncs + 1);
+    sc_stage<8>(sj, A.sj, A.nsc);
+    sc_stage<8>(sav, A.sa, A.nsc);
     // this group's rows of X (zero past r and n)
     double x[RPG][EL], rv[RPG][EL], pv[RPG][EL], Q[RPG][EL], bv[RPG][EL];
 #pragma unroll
@@ -6991,16 +7056,29 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
         for (int q = 0; q < RPG; ++q) {
             const int i = g + kScG * q;
             if (i >= n) continue;   // group-uniform
-            for (int e = cap[i]; e < cap[i + 1]; ++e) {
-                const int pk = cadj[e], j = pk >> 16, cs = pk & 0xffff;
-                double d = 0.0;
+            // four entries a pass: their index, operand loads and cross-lane sums overlap
+            const int e1 = cap[i + 1];
+            for (int e = cap[i]; e < e1; e += 4) {
+                int pk[4];
+                double d[4];
 #pragma unroll
-                for (int k = 0; k < EL; ++k) {
-                    const int c = l + kScL * k;
-                    if (c < r) d += xv[q][k] * Ys[j * rS + c];
+                for (int u = 0; u < 4; ++u) pk[u] = cadj[min(e + u, e1 - 1)];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int j = pk[u] >> 16;
+                    d[u] = 0.0;
+#pragma unroll
+                    for (int k = 0; k < EL; ++k) {
+                        const int c = l + kScL * k;
+                        if (c < r) d[u] += xv[q][k] * Ys[j * rS + c];
+                    }
                 }
-                d = group_sum<kScL>(d);
-                if (l == 0) T[2 * cs + (j <= i ? 0 : 1)] = d;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) d[u] = group_sum<kScL>(d[u]);
+                if (l == 0)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (e + u < e1) T[2 * (pk[u] & 0xffff) + ((pk[u] >> 16) <= i ? 0 : 1)] = d[u];
             }
         }
     };
@@ -7043,16 +7121,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
             double acc[EL];
 #pragma unroll
             for (int k = 0; k < EL; ++k) acc[k] = 0.0;
-            if (i < n)
-                for (int e = cap[i]; e < cap[i + 1]; ++e) {
-                    const int pk = cadj[e], j = pk >> 16;
-                    const double sv = T[pk & 0xffff];
-#pragma unroll
-                    for (int k = 0; k < EL; ++k) {
-                        const int c = l + kScL * k;
-                        if (c < r) acc[k] += sv * Ys[j * rS + c];
-                    }
-                }
+            if (i < n) sc_row_apply<EL>(cap[i], cap[i + 1], cadj, T, Ys, rS, r, l, acc);
 #pragma unroll
             for (int k = 0; k < EL; ++k) {
                 double v = acc[k] * 1.0;
@@ -7077,13 +7146,28 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
     // ---- right-hand side (lorads_admm.c:566-598): M1 = rho (cvs - A_k - b) - lam (compact),
     // S = A*(M1) on the constraint slots, M2 = S Y + C Y - rho Y, b = -M2 / rho
     const double rho = A.rho;
-    for (int j = tid; j < A.ncl; j += kScT) {
-        const int gi = A.cl_con[j];
-        double v = -A.b[gi];
-        v = v + A.cvs[gi];
-        v = v + (-1.0) * A.cvc[gi];
-        v = v * rho;
-        wv[j] = v + (-1.0) * A.lam[gi];
+    for (int j0 = tid; j0 < A.ncl; j0 += 4 * kScT) {   // four constraints a thread in flight
+        int gi[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gi[u] = A.cl_con[min(j0 + u * kScT, A.ncl - 1)];
+        double bq[4], cq[4], kq[4], lq[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            bq[u] = A.b[gi[u]];
+            cq[u] = A.cvs[gi[u]];
+            kq[u] = A.cvc[gi[u]];
+            lq[u] = A.lam[gi[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * kScT;
+            if (j >= A.ncl) break;
+            double v = -bq[u];
+            v = v + cq[u];
+            v = v + (-1.0) * kq[u];
+            v = v * rho;
+            wv[j] = v + (-1.0) * lq[u];
+        }
     }
     __syncthreads();   // Ys and the lists staged, M1 formed
     if (A.cconst)
@@ -7104,15 +7188,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
 #pragma unroll
             for (int k = 0; k < EL; ++k) acc[k] = 0.0;
             if (i < n) {
-                for (int e = cap[i]; e < cap[i + 1]; ++e) {
-                    const int pk = cadj[e], j = pk >> 16;
-                    const double sv = T[pk & 0xffff];
-#pragma unroll
-                    for (int k = 0; k < EL; ++k) {
-                        const int c = l + kScL * k;
-                        if (c < r) acc[k] += sv * Ys[j * rS + c];
-                    }
-                }
+                sc_row_apply<EL>(cap[i], cap[i + 1], cadj, T, Ys, rS, r, l, acc);
                 if (!A.cconst)
                     for (int e = A.cc_ptr[i]; e < A.cc_ptr[i + 1]; ++e) {
                         const int j = A.cc[2 * e];
@@ -7221,11 +7297,24 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
     __syncthreads();
     con_pass();
     __syncthreads();
-    for (int j = tid; j < A.ncl; j += kScT) {
-        const int gi = A.cl_con[j];
-        const double v = wv[j];
-        A.cvs[gi] = (A.cvs[gi] - A.cvc[gi]) + v;
-        A.cvc[gi] = v;
+    for (int j0 = tid; j0 < A.ncl; j0 += 4 * kScT) {
+        int gi[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gi[u] = A.cl_con[min(j0 + u * kScT, A.ncl - 1)];
+        double cq[4], kq[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            cq[u] = A.cvs[gi[u]];
+            kq[u] = A.cvc[gi[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * kScT;
+            if (j >= A.ncl) break;
+            const double v = wv[j];
+            A.cvs[gi[u]] = (cq[u] - kq[u]) + v;
+            A.cvc[gi[u]] = v;
+        }
     }
 }
 

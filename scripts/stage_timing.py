@@ -52,7 +52,9 @@ for ng in ("1", "0"):
                 print("k_lat_a block 0 (us from entry): own rows", round((a0[1] - a0[0]) * 0.01, 2), "neighbours",
                       round((a0[2] - a0[0]) * 0.01, 2), "| ctrl partials summed", round((a0[8] - a0[0]) * 0.01, 2),
                       "ctrl_step done", round((a0[7] - a0[0]) * 0.01, 2), "| barrier", round((a0[3] - a0[0]) * 0.01, 2),
-                      "rows done", round((a0[5] - a0[0]) * 0.01, 2), "partials stored", round((a0[6] - a0[0]) * 0.01, 2))
+                      "rows done", round((a0[5] - a0[0]) * 0.01, 2), "partials stored", round((a0[6] - a0[0]) * 0.01, 2),
+                      "| row header", round((a0[10] - a0[0]) * 0.01, 2), "control words", round((a0[9] - a0[0]) * 0.01, 2),
+                      "ctrl wave's control block", round((a0[11] - a0[0]) * 0.01, 2))
             if b0[0] and b0[7] and b0[8]:
                 print("k_lat_b block 0 (us from entry): own rows", round((b0[5] - b0[0]) * 0.01, 2), "neighbours",
                       round((b0[6] - b0[0]) * 0.01, 2), "| ctrl partials summed", round((b0[8] - b0[0]) * 0.01, 2),
