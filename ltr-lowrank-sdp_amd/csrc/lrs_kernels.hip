@@ -1294,8 +1294,8 @@ __device__ __forceinline__ void reduce_partials(const double *__restrict__ part,
 
 // ALMLineSearch (lorads_alm.c:266-333) from reduced values: p1, p2 objective parts
 // (p1 before its factor 2), dots = {q2q2, q1q2, q0q2, q1q1, q0q1}.
-template <bool WAVE>
-__device__ __forceinline__ void line_search_t(const double *__restrict__ par, double p1, double p2, const double *dots, double *ls) {
+template <bool WAVE, typename PB>
+__device__ __forceinline__ void line_search_t(const PB &par, double p1, double p2, const double *dots, double *ls) {
     p1 *= 2.0;
     const double rho = par[P_RHO];
     const double a = rho * dots[0] / 2;
@@ -1329,10 +1329,13 @@ __device__ void line_search_v(const double *__restrict__ par, double p1, double 
 // Control of one split iteration (thread 0).  c: shared copy of the previous control,
 // updated in place.
 // d = the nine dots of the previous gradient stage when `fold`.
-__device__ __forceinline__ void ctrl_step(double *c, const double *__restrict__ par, double lsflag, double lstau,
-                                          int fold, const double *d, bool ph1) {
-    // in place on the shared copy: a register copy of the block would set the VGPR
-    // peak (and so the occupancy) of the whole row kernel
+// CB / PB: the control block and parameters as LDS / global pointers (in place on the shared
+// copy: in k_it_a a register copy of the block would set the VGPR peak, and so the occupancy,
+// of the whole row kernel), or as register arrays (k_lat_a's control wave: every word a
+// register, no LDS round trip per access on the launch's critical path).
+template <typename CB, typename PB>
+__device__ __forceinline__ void ctrl_step(CB &&c, const PB &par, double lsflag, double lstau, int fold,
+                                          const double *d, bool ph1) {
     const int L = (int)par[P_L];
     const double cninf = par[P_CNINF], rctol = par[P_RCTOL], endsub = par[P_ENDSUB], budget = par[P_BUDGET];
     c[C_ACTIVE] = c[C_ACT2];
@@ -2354,6 +2357,8 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && l64 == 0 && s[9] != 12345.678 && ccv != 12345.678) g_phase_tmp[0][8] = wall_clock64();
 #endif
+        // (lane 0 on the LDS copy: a register copy of the block, every word read back from
+        // its lane, measured 0.5 us slower on G67, scripts/gpu_r04h.sh)
         if (l64 == 0) ctrl_step(c, pl, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && l64 == 0) g_phase_tmp[0][7] = wall_clock64();
@@ -2558,9 +2563,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m, double *hmirror,
     double seq, int nrb, int ndb, const int *__restrict__ drb, double *__restrict__ gl, double *CRb,
     const double *__restrict__ CDb) {
-    __shared__ double red[12];
     __shared__ double ls[LS_N];
-    __shared__ double pl[P_NPAR];
     __shared__ double gsh[kLatRows * E];   // slice blocks: the lane groups' partial gradients
     LRS_TS(2, 0);
     LRS_BLK_BEGIN();
@@ -2635,17 +2638,15 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
 #pragma unroll
             for (int q = 0; q < 5; ++q) sA[2 + q] += sB[q];
         }
-        if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-            for (int v = 0; v < 7; ++v) red[v] = sA[v];
-        }
-        __builtin_amdgcn_wave_barrier();
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && sA[6] != 12345.678) g_phase_tmp[2][8] = wall_clock64();
 #endif
-        if ((threadIdx.x & 63) < P_NPAR) pl[threadIdx.x & 63] = pvv;
-        __builtin_amdgcn_wave_barrier();
-        line_search_t<true>(pl, red[0], red[1], red + 2, ls);
+        // the sums (wave-uniform) and the parameters (one per lane, read back as uniform
+        // values) in registers: no LDS round trip on the launch's critical path
+        double pr[P_NPAR];
+#pragma unroll
+        for (int q = 0; q < P_NPAR; ++q) pr[q] = read_lane(pvv, q);
+        line_search_t<true>(pr, sA[0], sA[1], sA + 2, ls);
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_phase_tmp[2][7] = wall_clock64();
 #endif
@@ -7005,6 +7006,15 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
     int *sp = ce + A.nce;                      // [ncs + 1]
     int *sj = sp + A.ncs + 1;                  // [nsc]
     const int tid = threadIdx.x, g = tid / kScL, l = tid % kScL, wid = tid >> 6, lane = tid & 63;
+    // diagnostics build: thread 0 adds its phases' wall-clock ticks into g_phase[1][8..13]
+    // (staging, right-hand side, first residual, CG iterations, refresh), iterations into
+    // [1][14], launches into [1][15]
+#ifdef LRS_PHASE_TIMING
+    unsigned long long sc_t = wall_clock64();
+#define LRS_SC_T(q) do { if (tid == 0) { const unsigned long long t_ = wall_clock64(); g_phase[1][q] += t_ - sc_t; sc_t = t_; } } while (0)
+#else
+#define LRS_SC_T(q) do { } while (0)
+#endif
     double *X = (A.side ? A.V : A.U) + A.foff;
     const double *Yg = (A.side ? A.U : A.V) + A.foff;
     // stage the fixed factor and the lists (batched loads: one memory trip per ~4K elements)
@@ -7170,6 +7180,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
         }
     }
     __syncthreads();   // Ys and the lists staged, M1 formed
+    LRS_SC_T(8);
     if (A.cconst)
         for (int c = tid; c < r; c += kScT) {
             double s = 0.0;
@@ -7214,6 +7225,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
             }
         }
         bn = block_sum(bn);
+        LRS_SC_T(9);
 
         // ---- CGSolve: r = b - M X, p = r; then the iterations
         matvec(x, Q);
@@ -7231,6 +7243,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
         double qtr[2] = {rr, 0.0};
         bool active = !(sqrt(rr) / bn < A.tol);
         int iters = 0;
+        LRS_SC_T(10);
         for (int it = 0; active && it < A.maxit; ++it) {   // block-uniform
             const int par = it & 1;
             const double pq = block_sum(matvec(pv, Q));
@@ -7286,9 +7299,14 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
                 const int i = g + kScG * q, c = l + kScL * k;
                 if (i < n && c < r) X[(long)i * A.ld + c] = x[q][k];
             }
+        LRS_SC_T(11);
         if (tid == 0) {
             A.cgc[CG_ITERS] = iters;
             A.cgc[CG_TOTAL] += iters;
+#ifdef LRS_PHASE_TIMING
+            g_phase[1][14] += iters;
+            g_phase[1][15] += 1;
+#endif
         }
     }
     // ---- the cone's refresh: A_k <- A_k(sym(U V^T)) (x . Y products of the solved side), CVS += new - old
@@ -7316,6 +7334,8 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
             A.cvc[gi[u]] = v;
         }
     }
+    LRS_SC_T(12);
+#undef LRS_SC_T
 }
 
 bool small_cg_fits(const DevProblem &P, int cone) {

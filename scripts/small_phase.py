@@ -21,15 +21,23 @@ NAMES = ["control", "direction", "slots", "global+reduce", "linesearch", "R/S up
 for name in sys.argv[1:] or ["theta3"]:
     os.environ["LRS_SMALL"] = "1"
     sv = solver.Solver(inst.config_instance(name, cache))
-    before = sv.debug_phase_times()[0][3]
+    before = sv.debug_phase_times()[0]
     t0 = time.perf_counter()
     r = sv.solve(**sdplib)
     wall = time.perf_counter() - t0
-    ph = [a - b for a, b in zip(sv.debug_phase_times()[0][3], before)]
+    after = sv.debug_phase_times()[0]
+    ph = [a - b for a, b in zip(after[3], before[3])]
+    cg = [a - b for a, b in zip(after[1], before[1])]
     trips = max(1, ph[15])
     print(f"{name}: solve {wall:.3f} s alm {r['alm_time']:.3f} s ({r['alm_inner']} inner) admm {r['admm_time']:.3f} s "
           f"({r['admm_iter']} it, cg {r['cg_iter']}); k_small_alm trips {ph[15]}")
     tot = sum(ph[q] for q in range(8))
     print("  us/trip:", " ".join(f"{NAMES[q]} {ph[q] * 0.01 / trips:.2f}" for q in range(10)),
           f"| sum {tot * 0.01 / trips:.2f}")
+    if cg[15]:
+        nl = cg[15]
+        print(f"  k_small_cg launches {nl}, CG iterations {cg[14]} ({cg[14] / nl:.2f} a launch); us/launch:",
+              " ".join(f"{k} {cg[q] * 0.01 / nl:.2f}" for q, k in zip(range(8, 13), ["staging", "rhs", "first-residual",
+                                                                               "cg-iterations", "refresh"])),
+              f"| per CG iteration {cg[11] * 0.01 / max(1, cg[14]):.2f}")
     sv.close()

@@ -129,8 +129,10 @@ def test_c_caller_admm_sweep_matches_reference(built, tmp_path, name):
     scripts/make_golden_admm.py, CG at cg_tol 1e-9).  Bars: factors and multipliers within 1e-6
     relative (the bar of the single half-step test); the CG counts -- hundreds of iterations on
     these random starting factors, where the residual curve is flat near the tolerance and the
-    count follows the summation order -- of each cone's V solve within 25 % and the total within
-    15 %."""
+    count follows the summation order -- of each cone's V solve within 25 % (50 % where the
+    reference's count exceeds the n r unknowns of the solve: past CG's exact-arithmetic
+    termination the count is set by rounding alone, e.g. theta25x3's 289 iterations for 125
+    unknowns) and the total within 15 %."""
     import numpy as np
     exe = build_c_caller(tmp_path)
     g = np.load(os.path.join(ROOT, "tests", "golden", f"admm_sweep_{name}.npz"))
@@ -157,5 +159,6 @@ def test_c_caller_admm_sweep_matches_reference(built, tmp_path, name):
     assert rel(lam, g["lam"]) < 1e-6, rel(lam, g["lam"])
     for c in range(len(dims)):
         ref = float(g["cg_last"][c])
-        assert abs(its[2 * c + 1] - ref) <= max(2, 0.25 * ref), (c, its, g["cg_last"])
+        bar = 0.5 if ref > dims[c] * rank else 0.25
+        assert abs(its[2 * c + 1] - ref) <= max(2, bar * ref), (c, its, g["cg_last"])
     assert abs(its.sum() - float(g["cg_total"])) <= max(4, 0.15 * float(g["cg_total"])), (its, g["cg_total"])

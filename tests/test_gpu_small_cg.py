@@ -66,9 +66,13 @@ def test_small_cg_matches_multi_launch_and_reference(solver_mod, monkeypatch, na
     for key in ("U", "V", "lam"):
         assert rel(a[key], b[key]) < 1e-7, (key, rel(a[key], b[key]))
         assert rel(a[key], g[key]) < 1e-6, (key, rel(a[key], g[key]))
-    # CG counts (hundreds here, rounding-sensitive near the tolerance): as tests/test_capi.py
-    for x, y in zip(a["its"], b["its"]):
-        assert abs(int(x) - int(y)) <= max(2, 0.25 * y), (a["its"], b["its"])
+    # CG counts (hundreds here, rounding-sensitive near the tolerance): as tests/test_capi.py,
+    # 50 % past the n r unknowns of a solve (there the count is set by rounding alone)
+    k = np.load(os.path.join(ROOT, "tests", "golden", f"kernels_{name}.npz"))
+    dims, rank = [int(d) for d in k["dims"]], int(k["rank"])
+    for q, (x, y) in enumerate(zip(a["its"], b["its"])):
+        bar = 0.5 if max(x, y) > dims[q // 2] * rank else 0.25
+        assert abs(int(x) - int(y)) <= max(2, bar * y), (a["its"], b["its"])
     assert abs(a["its"].sum() - float(g["cg_total"])) <= max(4, 0.15 * float(g["cg_total"]))
 
 
