@@ -7061,11 +7061,16 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
         return s;
     };
     // (A) x_i . Y_j per constraint slot (i, j): half 0 from the slot's lower row, 1 from its upper
-    auto prod_pass = [&](const double (&xv)[RPG][EL]) {
+    // the operand is p (usep) or x: selected per row, not copied (a copy of the block's rows
+    // spills at EL 2 / RPG 8)
+    auto prod_pass = [&](bool usep) {
 #pragma unroll
         for (int q = 0; q < RPG; ++q) {
             const int i = g + kScG * q;
             if (i >= n) continue;   // group-uniform
+            double xq[EL];
+#pragma unroll
+            for (int k = 0; k < EL; ++k) xq[k] = usep ? pv[q][k] : x[q][k];
             // four entries a pass: their index, operand loads and cross-lane sums overlap
             const int e1 = cap[i + 1];
             for (int e = cap[i]; e < e1; e += 4) {
@@ -7080,7 +7085,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
 #pragma unroll
                     for (int k = 0; k < EL; ++k) {
                         const int c = l + kScL * k;
-                        if (c < r) d[u] += xv[q][k] * Ys[j * rS + c];
+                        if (c < r) d[u] += xq[k] * Ys[j * rS + c];
                     }
                 }
 #pragma unroll
@@ -7123,7 +7128,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
         }
     };
     // (D) Q = S Y + x on the group's rows; returns this thread's part of <x, Q>
-    auto apply_pass = [&](const double (&xv)[RPG][EL], double (&Qv)[RPG][EL]) -> double {
+    auto apply_pass = [&](bool usep, double (&Qv)[RPG][EL]) -> double {
         double dot = 0.0;
 #pragma unroll
         for (int q = 0; q < RPG; ++q) {
@@ -7134,23 +7139,14 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
             if (i < n) sc_row_apply<EL>(cap[i], cap[i + 1], cadj, T, Ys, rS, r, l, acc);
 #pragma unroll
             for (int k = 0; k < EL; ++k) {
+                const double xk = usep ? pv[q][k] : x[q][k];
                 double v = acc[k] * 1.0;
-                v += 1.0 * xv[q][k];
+                v += 1.0 * xk;
                 Qv[q][k] = v;
-                dot += xv[q][k] * v;
+                dot += xk * v;
             }
         }
         return dot;
-    };
-    auto matvec = [&](const double (&xv)[RPG][EL], double (&Qv)[RPG][EL]) -> double {
-        __syncthreads();   // T free (the previous apply pass is done)
-        prod_pass(xv);
-        __syncthreads();
-        con_pass();
-        __syncthreads();
-        slot_pass();
-        __syncthreads();
-        return apply_pass(xv, Qv);
     };
 
     // ---- right-hand side (lorads_admm.c:566-598): M1 = rho (cvs - A_k - b) - lam (compact),
@@ -7227,77 +7223,91 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
         bn = block_sum(bn);
         LRS_SC_T(9);
 
-        // ---- CGSolve: r = b - M X, p = r; then the iterations
-        matvec(x, Q);
-        double rr = 0.0;
-#pragma unroll
-        for (int q = 0; q < RPG; ++q)
-#pragma unroll
-            for (int k = 0; k < EL; ++k) {
-                const double ri = 1.0 * bv[q][k] + -1.0 * Q[q][k];
-                rv[q][k] = ri;
-                pv[q][k] = ri;
-                rr += ri * ri;
-            }
-        rr = block_sum(rr);
-        double qtr[2] = {rr, 0.0};
-        bool active = !(sqrt(rr) / bn < A.tol);
-        int iters = 0;
-        LRS_SC_T(10);
-        for (int it = 0; active && it < A.maxit; ++it) {   // block-uniform
-            const int par = it & 1;
-            const double pq = block_sum(matvec(pv, Q));
-            const double alph = qtr[par] / pq;
-            iters = it + 1;
-            double rr1 = 0.0;
-#pragma unroll
-            for (int q = 0; q < RPG; ++q)
-#pragma unroll
-                for (int k = 0; k < EL; ++k) {
-                    x[q][k] = alph * pv[q][k] + 1.0 * x[q][k];
-                    const double ri = -alph * Q[q][k] + 1.0 * rv[q][k];
-                    rv[q][k] = ri;
-                    rr1 += ri * ri;
-                }
-            rr1 = block_sum(rr1);
-            const double resi = sqrt(rr1);
-            if (resi / bn < A.tol || resi != resi) { active = false; break; }
-            if (it % 20 != 0) {
-                const double beta = rr1 / qtr[par];
+        // ---- CGSolve with ONE operator site (the whole operator inlined once keeps the kernel
+        // inside the instruction cache; three inlined copies made it 96 KB and every CG iteration
+        // missed): mode 0 the first residual r = b - M X, 1 an iteration's M p, 2 the restart's
+        // r = b - M X (lorads_cgs.c: every 20 iterations, then its beta = 1 step p = r + p),
+        // 3 the cone's refresh A_k <- A_k(sym(U V^T)) from the solved side (the operator's
+        // first two passes).  The arithmetic and the block sums' order are CGSolve's.
+        int mode = 0, it = 0, iters = 0;   // block-uniform
+        double qtr[2] = {0.0, 0.0};
+        for (;;) {
+            const bool usep = mode == 1;
+            __syncthreads();   // T free (the previous apply pass is done)
+            prod_pass(usep);
+            __syncthreads();
+            con_pass();
+            if (mode == 3) break;
+            __syncthreads();
+            slot_pass();
+            __syncthreads();
+            const double dot = apply_pass(usep, Q);
+            if (mode == 1) {
+                const int par = it & 1;
+                const double pq = block_sum(dot);
+                const double alph = qtr[par] / pq;
+                iters = it + 1;
+                double rr1 = 0.0;
 #pragma unroll
                 for (int q = 0; q < RPG; ++q)
 #pragma unroll
-                    for (int k = 0; k < EL; ++k) pv[q][k] = 1.0 * rv[q][k] + beta * pv[q][k];
-                qtr[par ^ 1] = rr1;
-            } else {
-                // restart (lorads_cgs.c: every 20 iterations): r = b - M X, p = r, then the
-                // beta = 1 step of the same iteration (p = r + p)
-                matvec(x, Q);
-                double rr2 = 0.0;
-#pragma unroll
-                for (int q = 0; q < RPG; ++q)
-#pragma unroll
-                    for (int k = 0; k < EL; ++k) {
-                        const double ri = 1.0 * bv[q][k] + -1.0 * Q[q][k];
-                        rv[q][k] = ri;
-                        pv[q][k] = ri;
-                        rr2 += ri * ri;
+                    for (int kk = 0; kk < EL; ++kk) {
+                        x[q][kk] = alph * pv[q][kk] + 1.0 * x[q][kk];
+                        const double ri = -alph * Q[q][kk] + 1.0 * rv[q][kk];
+                        rv[q][kk] = ri;
+                        rr1 += ri * ri;
                     }
-                rr2 = block_sum(rr2);
-                const double beta = rr2 / rr2;
+                rr1 = block_sum(rr1);
+                const double resi = sqrt(rr1);
+                if (resi / bn < A.tol || resi != resi) {
+                    mode = 3;
+                } else if (it % 20 != 0) {
+                    const double beta = rr1 / qtr[par];
+#pragma unroll
+                    for (int q = 0; q < RPG; ++q)
+#pragma unroll
+                        for (int kk = 0; kk < EL; ++kk) pv[q][kk] = 1.0 * rv[q][kk] + beta * pv[q][kk];
+                    qtr[par ^ 1] = rr1;
+                    ++it;
+                    mode = it < A.maxit ? 1 : 3;
+                } else {
+                    mode = 2;
+                }
+            } else {   // r = b - M X, p = r
+                double rr = 0.0;
 #pragma unroll
                 for (int q = 0; q < RPG; ++q)
 #pragma unroll
-                    for (int k = 0; k < EL; ++k) pv[q][k] = 1.0 * rv[q][k] + beta * pv[q][k];
-                qtr[par ^ 1] = rr2;
+                    for (int kk = 0; kk < EL; ++kk) {
+                        const double ri = 1.0 * bv[q][kk] + -1.0 * Q[q][kk];
+                        rv[q][kk] = ri;
+                        pv[q][kk] = ri;
+                        rr += ri * ri;
+                    }
+                rr = block_sum(rr);
+                if (mode == 0) {
+                    qtr[0] = rr;
+                    mode = (!(sqrt(rr) / bn < A.tol) && A.maxit > 0) ? 1 : 3;
+                    LRS_SC_T(10);
+                } else {
+                    const int par = it & 1;
+                    const double beta = rr / rr;
+#pragma unroll
+                    for (int q = 0; q < RPG; ++q)
+#pragma unroll
+                        for (int kk = 0; kk < EL; ++kk) pv[q][kk] = 1.0 * rv[q][kk] + beta * pv[q][kk];
+                    qtr[par ^ 1] = rr;
+                    ++it;
+                    mode = it < A.maxit ? 1 : 3;
+                }
             }
         }
 #pragma unroll
         for (int q = 0; q < RPG; ++q)
 #pragma unroll
-            for (int k = 0; k < EL; ++k) {
-                const int i = g + kScG * q, c = l + kScL * k;
-                if (i < n && c < r) X[(long)i * A.ld + c] = x[q][k];
+            for (int kk = 0; kk < EL; ++kk) {
+                const int i = g + kScG * q, c = l + kScL * kk;
+                if (i < n && c < r) X[(long)i * A.ld + c] = x[q][kk];
             }
         LRS_SC_T(11);
         if (tid == 0) {
@@ -7309,11 +7319,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
 #endif
         }
     }
-    // ---- the cone's refresh: A_k <- A_k(sym(U V^T)) (x . Y products of the solved side), CVS += new - old
-    __syncthreads();
-    prod_pass(x);
-    __syncthreads();
-    con_pass();
+    // ---- the refresh's writes: CVS += new - old per constraint of the cone (values from mode 3)
     __syncthreads();
     for (int j0 = tid; j0 < A.ncl; j0 += 4 * kScT) {
         int gi[4];
@@ -7338,14 +7344,19 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
 #undef LRS_SC_T
 }
 
+// The instantiated (elements per lane, rows per group) for a cone, 0 if none: EL 1 with up to
+// 8 rows a group, EL 2 up to 6, EL 3 up to 4, EL 4 up to 2 (five register arrays of EL x RPG
+// doubles at two waves a SIMD; the larger products spill)
+static int small_cg_rpg(int EL, int RPG) {
+    const int lim = EL == 1 ? 8 : (EL == 2 ? 6 : (EL == 3 ? 4 : (EL == 4 ? 2 : 0)));
+    const int rpg = RPG <= 2 ? 2 : (RPG <= 4 ? 4 : (RPG <= 6 ? 6 : 8));
+    return (RPG >= 1 && rpg <= lim) ? rpg : 0;
+}
 bool small_cg_fits(const DevProblem &P, int cone) {
     const DevCone &c = P.cones[cone];
     if (P.shard || !c.cg_ok || c.dense_c == 1 || c.r < 1) return false;
-    // the instantiated (elements per lane, rows per group): EL 1-2 with up to 8 rows a group,
-    // EL 3-4 with up to 4 (five register arrays of EL x RPG doubles, 2 waves a SIMD)
     const int EL = (c.r + kScL - 1) / kScL, RPG = (c.n + kScG - 1) / kScG;
-    const int rpg = RPG <= 2 ? 2 : (RPG <= 4 ? 4 : 8);
-    if (EL > 4 || RPG > 8 || (EL > 2 && rpg > 4)) return false;
+    if (!small_cg_rpg(EL, RPG)) return false;
     const int rS = c.r | 1;
     return small_cg_lds(c.n, rS, c.cg_ncl, c.cg_ncs, c.cg_nce, c.cg_nsc, c.cg_nadj) <= (size_t)kScMaxDynLds;
 }
@@ -7387,18 +7398,18 @@ int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double 
     A.cvs = W.cvs; A.cvc = W.cvc + (long)cone * P.m; A.U = W.U; A.V = W.V; A.cg_b = W.cg_b; A.cgc = W.cgc;
     const size_t lds = small_cg_lds(c.n, A.rS, A.ncl, A.ncs, A.nce, A.nsc, A.nadj);
     const int EL = (c.r + kScL - 1) / kScL, RPG = (c.n + kScG - 1) / kScG;
-    const int rpg = RPG <= 2 ? 2 : (RPG <= 4 ? 4 : 8);
+    const int rpg = small_cg_rpg(EL, RPG);
     switch (EL * 16 + rpg) {
     case 1 * 16 + 2: return launch_small_cg_t<1, 2>(A, lds, st);
     case 1 * 16 + 4: return launch_small_cg_t<1, 4>(A, lds, st);
+    case 1 * 16 + 6: return launch_small_cg_t<1, 6>(A, lds, st);
     case 1 * 16 + 8: return launch_small_cg_t<1, 8>(A, lds, st);
     case 2 * 16 + 2: return launch_small_cg_t<2, 2>(A, lds, st);
     case 2 * 16 + 4: return launch_small_cg_t<2, 4>(A, lds, st);
-    case 2 * 16 + 8: return launch_small_cg_t<2, 8>(A, lds, st);
+    case 2 * 16 + 6: return launch_small_cg_t<2, 6>(A, lds, st);
     case 3 * 16 + 2: return launch_small_cg_t<3, 2>(A, lds, st);
     case 3 * 16 + 4: return launch_small_cg_t<3, 4>(A, lds, st);
     case 4 * 16 + 2: return launch_small_cg_t<4, 2>(A, lds, st);
-    case 4 * 16 + 4: return launch_small_cg_t<4, 4>(A, lds, st);
     default:
         snprintf(g_err, sizeof(g_err), "single-workgroup ADMM half-step: no variant for r %d, n %d", c.r, c.n);
         return -1;

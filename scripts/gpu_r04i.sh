@@ -7,7 +7,7 @@ LRS_SMALL_CG=1 timeout -k 10 200 python3 -u scripts/small_phase.py theta3 theta3
 cat $O/small_phase.txt
 timeout -k 10 200 python3 -u scripts/stage_timing.py > $O/stage_timing.txt 2>&1 || { tail -5 $O/stage_timing.txt; exit 1; }
 grep -E "block 0|it/s" $O/stage_timing.txt
-timeout -k 10 400 python3 -u -m pytest -v -m gpu --timeout 300 --timeout-method thread tests/test_gpu_small_cg.py tests/test_capi.py > $O/pytest.txt 2>&1
+timeout -k 10 400 python3 -u -m pytest -v -m gpu --timeout 300 --timeout-method thread tests/test_gpu_small_cg.py tests/test_capi.py tests/test_gpu_configs.py > $O/pytest.txt 2>&1
 rc=$?
 grep -E "FAILED|ERROR|passed|failed" $O/pytest.txt | tail -8
 exit $rc
