@@ -7234,14 +7234,30 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
         for (;;) {
             const bool usep = mode == 1;
             __syncthreads();   // T free (the previous apply pass is done)
+#ifdef LRS_PHASE_TIMING
+            // diagnostics: the operator's four passes of the first residual into g_phase[1][4..7]
+            const bool pt = mode == 0 && tid == 0;
+            unsigned long long p_t = pt ? wall_clock64() : 0;
+#define LRS_SC_P(q) do { if (pt) { const unsigned long long t_ = wall_clock64(); g_phase[1][q] += t_ - p_t; p_t = t_; } } while (0)
+#else
+#define LRS_SC_P(q) do { } while (0)
+#endif
             prod_pass(usep);
             __syncthreads();
+            LRS_SC_P(4);
             con_pass();
             if (mode == 3) break;
             __syncthreads();
+            LRS_SC_P(5);
             slot_pass();
             __syncthreads();
+            LRS_SC_P(6);
             const double dot = apply_pass(usep, Q);
+#ifdef LRS_PHASE_TIMING
+            __syncthreads();
+#endif
+            LRS_SC_P(7);
+#undef LRS_SC_P
             if (mode == 1) {
                 const int par = it & 1;
                 const double pq = block_sum(dot);

@@ -40,4 +40,6 @@ for name in sys.argv[1:] or ["theta3"]:
               " ".join(f"{k} {cg[q] * 0.01 / nl:.2f}" for q, k in zip(range(8, 13), ["staging", "rhs", "first-residual",
                                                                                "cg-iterations", "refresh"])),
               f"| per CG iteration {cg[11] * 0.01 / max(1, cg[14]):.2f}")
+        print("  first residual's operator passes (us/launch):",
+              " ".join(f"{k} {cg[q] * 0.01 / nl:.2f}" for q, k in zip(range(4, 8), ["prod", "constraints", "slots", "apply"])))
     sv.close()
