@@ -6974,17 +6974,15 @@ __device__ __forceinline__ void sc_row_apply(int e0, int e1, const int *cadj, co
         for (int u = 0; u < 4; ++u) {
             sv[u] = T[pk[u] & 0xffff];
 #pragma unroll
-            for (int k = 0; k < EL; ++k) {
-                const int c = l + kScL * k;
-                y[u][k] = c < r ? Ys[(pk[u] >> 16) * rS + c] : 0.0;
-            }
+            for (int k = 0; k < EL; ++k) y[u][k] = Ys[(pk[u] >> 16) * rS + l + kScL * k];   // unconditional (selects below)
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (e + u < e1)
 #pragma unroll
-                for (int k = 0; k < EL; ++k)
-                    if (l + kScL * k < r) acc[k] += sv[u] * y[u][k];
+            for (int k = 0; k < EL; ++k) {
+                const bool ok = e + u < e1 && l + kScL * k < r;
+                acc[k] = ok ? fma(sv[u], y[u][k], acc[k]) : acc[k];
+            }
     }
 }
 
@@ -7078,6 +7076,9 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
                 double d[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) pk[u] = cadj[min(e + u, e1 - 1)];
+                // loads unconditional, the column test a select (a load under a branch is
+                // waited for before the next one issues: eight serial LDS round trips a pass);
+                // columns past r read the next row's words, a select drops them
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int j = pk[u] >> 16;
@@ -7085,7 +7086,8 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
 #pragma unroll
                     for (int k = 0; k < EL; ++k) {
                         const int c = l + kScL * k;
-                        if (c < r) d[u] += xq[k] * Ys[j * rS + c];
+                        const double y = Ys[j * rS + c];
+                        d[u] = c < r ? fma(xq[k], y, d[u]) : d[u];
                     }
                 }
 #pragma unroll

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4: k_small_cg with branch-free row loops -- phases, tests, theta timings.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$PWD; O=$R/gpurun_out/r04k; mkdir -p $O
+LRS_SMALL_CG=1 timeout -k 10 200 python3 -u scripts/small_phase.py theta3 > $O/small_phase.txt 2>&1 || { tail -5 $O/small_phase.txt; exit 1; }
+cat $O/small_phase.txt
+timeout -k 10 400 python3 -u -m pytest -v -m gpu --timeout 300 --timeout-method thread tests/test_gpu_small_cg.py tests/test_capi.py tests/test_gpu_configs.py > $O/pytest.txt 2>&1
+rc=$?
+grep -E "FAILED|ERROR|passed|failed" $O/pytest.txt | tail -8
+[ $rc -le 1 ] || exit $rc
+for v in 1 0; do
+  for t in theta3 theta3x3; do
+    LRS_SMALL_CG=$v timeout -k 10 120 python3 -u scripts/admm_probe.py $t >> $O/theta.txt 2>&1 || { tail -5 $O/theta.txt; exit 1; }
+  done
+  echo "LRS_SMALL_CG=$v done" >> $O/theta.txt
+done
+cat $O/theta.txt
+exit $rc
