@@ -6294,22 +6294,36 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         const bool u0 = (cs0 != 0.0 || cy0 != 0.0), u1 = (cs1 != 0.0 || cy1 != 0.0);
         const double *__restrict__ Gc = c[C_GCUR] == 0.0 ? A.G0 : A.G1;
         // ---- D = -(cg G + cs0 s0 + cy0 y0 + cs1 s1 + cy1 y1)  (DirRow's arithmetic), 16-B loads
-        for (int e = tid; e < N * H; e += T) {
-            const int i = e / H, q = e - i * H;
-            const long o = (long)i * LD + 2 * q;
-            const double2 g = *reinterpret_cast<const double2 *>(Gc + o);
-            double dx = cg * g.x, dy = cg * g.y;
-            if (u0) {
-                const double2 a = *reinterpret_cast<const double2 *>(A.s0 + o), bb = *reinterpret_cast<const double2 *>(A.y0 + o);
-                dx += cs0 * a.x + cy0 * bb.x;
-                dy += cs0 * a.y + cy0 * bb.y;
+        // two elements a thread at a time, every operand load issued before the arithmetic
+        // (one memory trip per pair instead of one per element and operand)
+        for (int e0 = tid; e0 < N * H; e0 += 2 * T) {
+            double2 gv[2], a0[2], b0[2], a1[2], b1[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = min(e0 + u * T, N * H - 1), i = e / H, q = e - i * H;
+                const long o = (long)i * LD + 2 * q;
+                gv[u] = *reinterpret_cast<const double2 *>(Gc + o);
+                a0[u] = *reinterpret_cast<const double2 *>(A.s0 + o);
+                b0[u] = *reinterpret_cast<const double2 *>(A.y0 + o);
+                a1[u] = *reinterpret_cast<const double2 *>(A.s1 + o);
+                b1[u] = *reinterpret_cast<const double2 *>(A.y1 + o);
             }
-            if (u1) {
-                const double2 a = *reinterpret_cast<const double2 *>(A.s1 + o), bb = *reinterpret_cast<const double2 *>(A.y1 + o);
-                dx += cs1 * a.x + cy1 * bb.x;
-                dy += cs1 * a.y + cy1 * bb.y;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = e0 + u * T;
+                if (e >= N * H) break;
+                const int i = e / H, q = e - i * H;
+                double dx = cg * gv[u].x, dy = cg * gv[u].y;
+                if (u0) {
+                    dx += cs0 * a0[u].x + cy0 * b0[u].x;
+                    dy += cs0 * a0[u].y + cy0 * b0[u].y;
+                }
+                if (u1) {
+                    dx += cs1 * a1[u].x + cy1 * b1[u].x;
+                    dy += cs1 * a1[u].y + cy1 * b1[u].y;
+                }
+                reinterpret_cast<double2 *>(Ds + (long)i * LS)[q] = make_double2(-dx, -dy);
             }
-            reinterpret_cast<double2 *>(Ds + (long)i * LS)[q] = make_double2(-dx, -dy);
         }
         __syncthreads();
         if (A.nconst) colsums(Ds, csD);
@@ -6319,10 +6333,24 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         // measured slower: the per-entry cross-lane sums and a second per-slot pass for the
         // constraints outweigh the halved LDS reads); uRD -> XA, uDD -> X1
         double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        // software-pipelined: the next slot's records and this slot's single constraint's
+        // values are in flight while this slot's dots run on LDS (one memory trip a slot, not
+        // two); loads clamped, not branched
+        int2 ijn = A.slot_g[min(tid, A.Ptot - 1)];
+        double cwn = A.Cw[min(tid, A.Ptot - 1)];
+        double2 l1n = A.loc1[min(tid, A.Ptot - 1)];
         for (int s = tid; s < A.Ptot; s += T) {
-            const int2 ij = A.slot_g[s];
-            const double cw = A.Cw[s];
-            const double2 l1u = A.loc1[s];
+            const int2 ij = ijn;
+            const double cw = cwn;
+            const double2 l1u = l1n;
+            {
+                const int sn = min(s + T, A.Ptot - 1);
+                ijn = A.slot_g[sn];
+                cwn = A.Cw[sn];
+                l1n = A.loc1[sn];
+            }
+            const int c1p = (int)l1u.y >= 0 ? (int)l1u.y : 0;
+            const double bp = A.b[c1p], cvp = A.cvs[c1p], lp = A.lam[c1p];
             const double2 *ri = Rs2 + (long)ij.x * LS2, *di = Ds2 + (long)ij.x * LS2;
             const double2 *rj = Rs2 + (long)ij.y * LS2, *dj = Ds2 + (long)ij.y * LS2;
             double d0 = 0.0, d1 = 0.0;
@@ -6356,7 +6384,8 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                 const int ci = c1 >= 0 ? c1 : A.loc_con[e];
                 const double w = c1 >= 0 ? l1u.x : A.loc_w[e];
                 const double q1 = 2.0 * (w * d0), q2 = w * d1;
-                const double bi = A.b[ci], cv = A.cvs[ci], li = A.lam[ci];
+                double bi = bp, cv = cvp, li = lp;
+                if (c1 < 0) { bi = A.b[ci]; cv = A.cvs[ci]; li = A.lam[ci]; }
                 const double q0 = (bi - cv) + rhoInv * li;
                 acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1; acc[6] += q0 * q1;
                 double2 *rc = reinterpret_cast<double2 *>(A.rec + 4L * ci);
@@ -6373,11 +6402,28 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
             for (int k = 0; k < A.K; ++k) {
                 const long row = (long)k * A.m + i;
                 double a1 = 0.0, a2 = 0.0;
-                for (int e = A.con_ptr[row] + lane; e < A.con_ptr[row + 1]; e += 64) {
-                    const double w = A.con_w[e];
-                    const int sl = A.con_slot[e];
-                    a1 += w * XA[sl];
-                    a2 += w * X1[sl];
+                // four entries a lane in flight, summed in entry order
+                const int eb = A.con_ptr[row], ee = A.con_ptr[row + 1];
+                for (int e0 = eb + lane; e0 < ee; e0 += 256) {
+                    double w[4], xa[4], x1[4];
+                    int sl[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int e = min(e0 + 64 * u, ee - 1);
+                        w[u] = A.con_w[e];
+                        sl[u] = A.con_slot[e];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        xa[u] = XA[sl[u]];
+                        x1[u] = X1[sl[u]];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool ok = e0 + 64 * u < ee;
+                        a1 = ok ? a1 + w[u] * xa[u] : a1;
+                        a2 = ok ? a2 + w[u] * x1[u] : a2;
+                    }
                 }
                 v1 += wave_sum(a1);
                 v2 += wave_sum(a2);
@@ -6564,13 +6610,17 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         __syncthreads();   // uRR of every slot before the constraints read them
         LRS_SM_T(6);
         // single-slot constraints: A(R_new R_new^T) and their residual, a thread per slot
+        // software-pipelined as the slot phase: the next slot's record and this slot's b in flight
+        double2 l1nx = A.loc1[min(tid, A.Ptot - 1)];
         for (int s = tid; s < A.Ptot; s += T) {
             const double d = XB[s];
-            const double2 l1u = A.loc1[s];
+            const double2 l1u = l1nx;
+            l1nx = A.loc1[min(s + T, A.Ptot - 1)];
             const int c1 = (int)l1u.y;
+            const double bc = A.b[c1 >= 0 ? c1 : 0];
             if (AL) A.uRR[s] = d;
             if (c1 >= 0) {
-                const double tot = l1u.x * d, dd = A.b[c1] - tot;
+                const double tot = l1u.x * d, dd = bc - tot;
                 A.cvs[c1] = tot;
                 bacc[9] += dd * dd;
                 continue;
@@ -6590,7 +6640,22 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
             for (int k = 0; k < A.K; ++k) {
                 const long row = (long)k * A.m + i;
                 double v = 0.0;
-                for (int e = A.con_ptr[row] + lane; e < A.con_ptr[row + 1]; e += 64) v += A.con_w[e] * XB[A.con_slot[e]];
+                // four entries a lane in flight, summed in entry order
+                const int eb = A.con_ptr[row], ee = A.con_ptr[row + 1];
+                for (int e0 = eb + lane; e0 < ee; e0 += 256) {
+                    double w[4], xv[4];
+                    int sl[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int e = min(e0 + 64 * u, ee - 1);
+                        w[u] = A.con_w[e];
+                        sl[u] = A.con_slot[e];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) xv[u] = XB[sl[u]];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v = e0 + 64 * u < ee ? v + w[u] * xv[u] : v;
+                }
                 tot += wave_sum(v);
             }
             if (lane == 0) {
