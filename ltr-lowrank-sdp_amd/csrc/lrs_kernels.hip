@@ -86,6 +86,16 @@ const char *last_device_error() { return g_err; }
     } while (0)
 
 Layout choose_layout(int r) {
+    // LRS_LAYOUT=GxE (diagnostics): that layout wherever it holds r columns
+    if (const char *e = getenv("LRS_LAYOUT")) {
+        int g = 0, el = 0;
+        if (sscanf(e, "%dx%d", &g, &el) == 2 && (g == 8 || g == 16 || g == 32 || g == 64) && el >= 1 && el <= 4 &&
+            g * el >= r) {
+            Layout f;
+            f.G = g; f.E = el; f.ld = g * el;
+            return f;
+        }
+    }
     static const int Gs[4] = {8, 16, 32, 64};
     static const int Es[4] = {2, 1, 4, 3};   // preference order at equal ld
     Layout best;

@@ -15,4 +15,12 @@ for v in 1 0; do
   echo "LRS_SMALL_CG=$v done" >> $O/theta.txt
 done
 cat $O/theta.txt
+# headline factor layout A/B (G67, r = 19: default 8 lanes x 3 doubles, ld 24)
+H="--no-cpu --no-eps --no-scale --no-north-star --no-configs --no-c5 --no-c5b --no-sharded"
+for v in default 8x4 16x2 default 8x4; do
+  if [ $v = default ]; then unset LRS_LAYOUT; else export LRS_LAYOUT=$v; fi
+  timeout -k 10 200 python3 -u bench.py --steps 3000 --warmup 300 $H > $O/head_$v.log 2>&1 || { tail -5 $O/head_$v.log; exit 1; }
+  python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print('LRS_LAYOUT=$v', round(d['value']), [round(s['avg_launch_us'], 2) for s in d['roofline']['stages']])" $O/head_$v.log | tee -a $O/head.txt
+done
+unset LRS_LAYOUT
 exit $rc
