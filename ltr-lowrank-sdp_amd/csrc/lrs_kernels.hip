@@ -2573,7 +2573,9 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m, double *hmirror,
     double seq, int nrb, int ndb, const int *__restrict__ drb, double *__restrict__ gl, double *CRb,
     const double *__restrict__ CDb) {
+    __shared__ double red[12];
     __shared__ double ls[LS_N];
+    __shared__ double pl[P_NPAR];
     __shared__ double gsh[kLatRows * E];   // slice blocks: the lane groups' partial gradients
     LRS_TS(2, 0);
     LRS_BLK_BEGIN();
@@ -2648,15 +2650,19 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
 #pragma unroll
             for (int q = 0; q < 5; ++q) sA[2 + q] += sB[q];
         }
+        if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+            for (int v = 0; v < 7; ++v) red[v] = sA[v];
+        }
+        __builtin_amdgcn_wave_barrier();
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && sA[6] != 12345.678) g_phase_tmp[2][8] = wall_clock64();
 #endif
-        // the sums (wave-uniform) and the parameters (one per lane, read back as uniform
-        // values) in registers: no LDS round trip on the launch's critical path
-        double pr[P_NPAR];
-#pragma unroll
-        for (int q = 0; q < P_NPAR; ++q) pr[q] = read_lane(pvv, q);
-        line_search_t<true>(pr, sA[0], sA[1], sA + 2, ls);
+        // (sums and parameters through LDS: on register operands, every parameter read back
+        // from its lane, the launch measured 0.4 us slower on G67, scripts/gpu_r04k.sh)
+        if ((threadIdx.x & 63) < P_NPAR) pl[threadIdx.x & 63] = pvv;
+        __builtin_amdgcn_wave_barrier();
+        line_search_t<true>(pl, red[0], red[1], red + 2, ls);
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_phase_tmp[2][7] = wall_clock64();
 #endif
@@ -7055,8 +7061,10 @@ __device__ __forceinline__ void sc_row_apply(int e0, int e1, const int *cadj, co
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int k = 0; k < EL; ++k) {
-                const bool ok = e + u < e1 && l + kScL * k < r;
-                acc[k] = ok ? fma(sv[u], y[u][k], acc[k]) : acc[k];
+                // the test selects the coefficient, not the load (see prod_pass): a masked
+                // entry or column adds +-0
+                const double sc = (e + u < e1 && l + kScL * k < r) ? sv[u] : 0.0;
+                acc[k] += sc * y[u][k];
             }
     }
 }
@@ -7104,6 +7112,8 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
             if (t < n * r) Ys[i * rS + c] = v[u];
         }
     }
+    if (rS > r)   // the pad columns [r, rS): zero (the row loops read them unmasked)
+        for (int t = tid; t < n * (rS - r); t += kScT) Ys[(t / (rS - r)) * rS + r + t % (rS - r)] = 0.0;
     sc_stage<8>(cap, A.cadj_ptr, n + 1);
     sc_stage<8>(cadj, A.cadj, A.nadj);
     sc_stage<8>(clp, A.cl_ptr, A.ncl + 1);
@@ -7151,19 +7161,16 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
                 double d[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) pk[u] = cadj[min(e + u, e1 - 1)];
-                // loads unconditional, the column test a select (a load under a branch is
-                // waited for before the next one issues: eight serial LDS round trips a pass);
-                // columns past r read the next row's words, a select drops them
+                // no branch around a load (the compiler sinks a load into its branch and then
+                // waits for it before the next one issues: eight serial LDS round trips a pass):
+                // columns past r hold x = 0 exactly and read the zeroed pad or the next row's
+                // finite words, so their products are +-0
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int j = pk[u] >> 16;
                     d[u] = 0.0;
 #pragma unroll
-                    for (int k = 0; k < EL; ++k) {
-                        const int c = l + kScL * k;
-                        const double y = Ys[j * rS + c];
-                        d[u] = c < r ? fma(xq[k], y, d[u]) : d[u];
-                    }
+                    for (int k = 0; k < EL; ++k) d[u] += xq[k] * Ys[j * rS + l + kScL * k];
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) d[u] = group_sum<kScL>(d[u]);
