@@ -138,6 +138,16 @@ __device__ __forceinline__ double group_sum(double v) {
     return v;
 }
 
+// Kernel arguments (and uniform words) in SGPRs at this point: the compiler otherwise sinks
+// each argument load to the basic block that first uses it, and every branch level of a
+// kernel's prologue then waits for its own argument trip (three dependent trips in k_lat_a /
+// k_lat_b before the first vector load was issued).  Pinned at the top, the argument loads
+// are one batch, one trip.
+template <typename T>
+__device__ __forceinline__ void karg_pin1(const T &x) { asm volatile("" ::"s"(x)); }
+template <typename... T>
+__device__ __forceinline__ void karg_pin(const T &...x) { (karg_pin1(x), ...); }
+
 __device__ __forceinline__ double read_lane(double v, int l) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readlane((int)b, l);
@@ -2282,6 +2292,17 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     __shared__ double c[C_NCTRL];
     __shared__ double pl[P_NPAR];
     LRS_TS(0, 0);
+#ifdef LRS_KARG_PIN
+    karg_pin(n, ld, foff, adj_ptr, adj_low, adj_col, adj_slot, Cw, Rb0, Rb1, Dall, G0, G1, s0a, y0a, s1a, y1a, uRD,
+             uDD, loc_ptr, loc_con, loc_w, loc1, b, cvs, lam, rec, do_glob, mg, glob, m, K);
+    karg_pin(con_ptr, con_slot, con_w, uRR, par, ctrl_prev, ctrl_cur, ls_prev, partC, nblkC, partA, pblk_off, gwide,
+             nrb, nda, dra);
+#elif defined(LRS_KARG_PIN2)
+    // the arguments of the prologue (the first loads of both wave kinds, the operand bases):
+    // one batch; the rest below, beside the first vector loads' trip
+    karg_pin(n, ld, foff, adj_ptr, adj_low, adj_col, adj_slot, Cw, Rb0, Rb1, G0, G1, s0a, y0a, s1a, y1a, loc1, b,
+             cvs, lam, m, par, ctrl_prev, ls_prev, partC, nblkC, nrb, nda, dra);
+#endif
     LRS_BLK_BEGIN();
     const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == kLatRowWaves;   // wave-uniform
     const int lane = threadIdx.x & (G - 1);
@@ -2321,8 +2342,21 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     __builtin_amdgcn_sched_barrier(0);
     // this iteration's operands: ctrl_step folds the previous stage (and flips the G and R
     // buffers) exactly when `fold` holds
+#if defined(LRS_KARG_PIN) || defined(LRS_KARG_PIN2)
+    // the control words every wave needs as one batch (no short-circuit chain of loads)
+    const double cw_act2 = ctrl_prev[C_ACT2], cw_pend = ctrl_prev[C_PENDING], cw_rcur = ctrl_prev[C_RCUR],
+                 cw_gcur = ctrl_prev[C_GCUR], lsflag = ls_prev[LS_FLAG];
+#ifdef LRS_KARG_PIN2
+    karg_pin(cw_act2, cw_pend, cw_rcur, cw_gcur, lsflag, Dall, uRD, uDD, loc_ptr, loc_con, loc_w, rec, do_glob, mg,
+             glob, K, con_ptr, con_slot, con_w, uRR, ctrl_cur, partA, pblk_off, gwide);
+#else
+    karg_pin(cw_act2, cw_pend, cw_rcur, cw_gcur, lsflag);
+#endif
+    const int fold = ((cw_act2 != 0.0) & (cw_pend == 1.0) & (lsflag == 0.0)) ? 1 : 0;
+#else
     const double lsflag = ls_prev[LS_FLAG];
     const int fold = (ctrl_prev[C_ACT2] != 0.0 && ctrl_prev[C_PENDING] == 1.0 && lsflag == 0.0) ? 1 : 0;
+#endif
 #ifdef LRS_PHASE_TIMING
     // diagnostics: the row header (a vector load) and the control words (scalar loads) arrived
     if (blockIdx.x == 0 && threadIdx.x == 0 && kb != -12345) g_phase_tmp[0][10] = wall_clock64();
@@ -2369,7 +2403,24 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
 #endif
         // (lane 0 on the LDS copy: a register copy of the block, every word read back from
         // its lane, measured 0.5 us slower on G67, scripts/gpu_r04h.sh)
+#ifdef LRS_CTRL_SREG
+        // every lane on a private copy loaded through the scalar cache (constant indices
+        // only: the copy lives in registers), lane 0 publishes the result to LDS
+        {
+            double cr[C_NCTRL], pr[P_NPAR];
+#pragma unroll
+            for (int q = 0; q < C_NCTRL; ++q) cr[q] = ctrl_prev[q];
+#pragma unroll
+            for (int q = 0; q < P_NPAR; ++q) pr[q] = par[q];
+            ctrl_step(cr, pr, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
+            if (l64 == 0) {
+#pragma unroll
+                for (int q = 0; q < C_NCTRL; ++q) c[q] = cr[q];
+            }
+        }
+#else
         if (l64 == 0) ctrl_step(c, pl, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
+#endif
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && l64 == 0) g_phase_tmp[0][7] = wall_clock64();
 #endif
@@ -2578,6 +2629,17 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     __shared__ double pl[P_NPAR];
     __shared__ double gsh[kLatRows * E];   // slice blocks: the lane groups' partial gradients
     LRS_TS(2, 0);
+#ifdef LRS_KARG_PIN
+    karg_pin(n, ld, foff, adj_ptr, adj_low, adj_col, adj_slot, Rb0, Rb1, Dall, G0, G1, s0, y0, s1, y1, uRR, Craw,
+             slot_ptr, slot_con, slot_a, slot1, rec, loc_ptr, loc_con, loc_w, loc1, b, cvs, par, ctrl);
+    karg_pin(partA, nblkA, partB, nblkB, ls_cur, L, partC, pblk_off, m, hmirror, seq, nrb, ndb, drb, gl, CRb, CDb);
+#elif defined(LRS_KARG_PIN2)
+    // the prologue's arguments as one batch; the rest with the control words below
+    karg_pin(n, ld, foff, adj_ptr, adj_low, adj_col, adj_slot, Rb0, Rb1, Dall, G0, G1, s0, y0, s1, y1, Craw, slot1,
+             rec, loc1, b, par, ctrl, partA, nblkA, partB, nblkB, L, m, nrb, ndb, drb, hmirror, seq);
+#define LRS_B_PIN2() karg_pin(cw_act2, cw_gcur, cw_head, cw_rcur, uRR, slot_ptr, slot_con, slot_a, loc_ptr, loc_con, \
+                              loc_w, cvs, ls_cur, partC, pblk_off, gl, CRb, CDb)
+#endif
     LRS_BLK_BEGIN();
     mirror_ctrl(ctrl, hmirror, seq);
     const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == kLatRowWaves;   // wave-uniform
@@ -2614,9 +2676,26 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
         ke = adj_ptr[ic + 1];
     }
     __builtin_amdgcn_sched_barrier(0);
+#if defined(LRS_KARG_PIN) || defined(LRS_KARG_PIN2)
+    // the control words as one batch before the first test on them
+    const double cw_act2 = ctrl[C_ACT2], cw_gcur = ctrl[C_GCUR], cw_head = ctrl[C_HEAD], cw_rcur = ctrl[C_RCUR];
+#ifndef LRS_LAT_SPEC
+#ifdef LRS_KARG_PIN2
+    LRS_B_PIN2();
+#else
+    karg_pin(cw_act2, cw_gcur, cw_head, cw_rcur);
+#endif
+    if (cw_act2 == 0.0) return;
+#endif
+    const int gcur = (int)cw_gcur, h = (int)cw_head;
+    const bool r1 = cw_rcur != 0.0;
+#else
+#ifndef LRS_LAT_SPEC
     if (ctrl[C_ACT2] == 0.0) return;
+#endif
     const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
     const bool r1 = ctrl[C_RCUR] != 0.0;
+#endif
     const double *__restrict__ R = (r1 ? Rb1 : Rb0) + foff;
     double *__restrict__ Rn = (r1 ? Rb0 : Rb1) + foff;
     const double *__restrict__ D = Dall + foff;
@@ -2640,8 +2719,19 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     int sd = 0;
     double svd = 0.0, bqd = 0.0;
     double2 s1d = make_double2(0.0, -1.0), l1d = s1d, rad = make_double2(0.0, 0.0), rbd = rad;
+#ifdef LRS_LAT_SPEC
+    // the row waves' operand rows from BOTH buffers of every double-buffered array, issued
+    // before the control words arrive (the buffer choice is control state); picked after
+    double riB[E], goB[E], sovB[E], yovB[E], rjpB[NO][E];
+    const double *__restrict__ RA = Rb0 + foff, *__restrict__ RB = Rb1 + foff;
+#else
+    const double *__restrict__ RA = R;
+#endif
     if (ctrl_wave) {
         // ---- control wave: line search (ALMLineSearch lorads_alm.c:266-333)
+#if defined(LRS_KARG_PIN2) && defined(LRS_LAT_SPEC)
+        LRS_B_PIN2();
+#endif
         double sA[7];
         sum_partials<7>(pa, nblkA, sA);
         if (nblkB > 0) {
@@ -2668,10 +2758,22 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
 #endif
     } else {
         // ---- row waves: prefetch, one memory trip per dependency level, clamped loads
+#ifdef LRS_LAT_SPEC
+        ld_row<E>(RA + oi, ri);
+        ld_row<E>(RB + oi, riB);
+        ld_row<E>(D + oi, di);
+        ld_row<E>(G0 + foff + oi, go);
+        ld_row<E>(G1 + foff + oi, goB);
+        if (two) {
+            ld_row<E>(s0 + foff + oi, sov); ld_row<E>(s1 + foff + oi, sovB);
+            ld_row<E>(y0 + foff + oi, yov); ld_row<E>(y1 + foff + oi, yovB);
+        }
+#else
         ld_row<E>(R + oi, ri);
         ld_row<E>(D + oi, di);
         ld_row<E>(Gold + oi, go);
         if (two) { ld_row<E>(so + oi, sov); ld_row<E>(yo + oi, yov); }
+#endif
         // entries of this group: the row's adjacency (a dense row's own group: none, it only
         // updates R), or its slice of a dense row (no diagonal special case there)
         int eb = kb, nt = valid ? ke - kb : 0;
@@ -2699,7 +2801,10 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
             ss[u] = past ? sa[u + 1] : sa[u];
             lw[u] = eb + u + (past ? 1 : 0) < kl;
             const long oj = (long)(u < no ? j : ic) * ld + lane * E;
-            ld_row<E>(R + oj, rjp[u]);
+            ld_row<E>(RA + oj, rjp[u]);
+#ifdef LRS_LAT_SPEC
+            ld_row<E>(RB + oj, rjpB[u]);
+#endif
             ld_row<E>(D + oj, djp[u]);
             sv[u] = Craw[ss[u]];
             s1v[u] = slot1[ss[u]];
@@ -2734,7 +2839,26 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
         if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && ra[0].x != 12345.678 && rjp[0][0] != 12345.678)
             g_phase_tmp[2][6] = wall_clock64();
 #endif
+#if defined(LRS_KARG_PIN2) && defined(LRS_LAT_SPEC)
+        LRS_B_PIN2();
+#endif
     }
+#ifdef LRS_LAT_SPEC
+    if (ctrl[C_ACT2] == 0.0) return;   // block-uniform
+    if (!ctrl_wave) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            ri[e] = r1 ? riB[e] : ri[e];
+            go[e] = gcur != 0 ? goB[e] : go[e];
+            sov[e] = h == 0 ? sovB[e] : sov[e];   // so = s_{1-h}
+            yov[e] = h == 0 ? yovB[e] : yov[e];
+        }
+#pragma unroll
+        for (int u = 0; u < NO; ++u)
+#pragma unroll
+            for (int e = 0; e < E; ++e) rjp[u][e] = r1 ? rjpB[u][e] : rjp[u][e];
+    }
+#endif
     __syncthreads();
     LRS_TS(2, 2);
     if (pblk_off == 0 && blockIdx.x == 0 && threadIdx.x < LS_N) ls_cur[threadIdx.x] = ls[threadIdx.x];

@@ -15,7 +15,7 @@ cols = int(sys.argv[3]) if len(sys.argv) > 3 else 100
 cache = os.path.join(ROOT, ".bench_instances")
 os.makedirs(cache, exist_ok=True)
 path = bench.instance_for(0, rows, cols, cache)
-for kp in (0, 1):
+for kp in [int(x) for x in os.environ.get("LRS_VAR_PATHS", "0,1").split(",")]:
     sv = solver.Solver(path)
     sv.set_kernel_path(kp)
     r = sv.determine_rank()[0]
