@@ -1261,7 +1261,10 @@ __device__ void line_search(const double *__restrict__ par, int K, double *ls) {
 // Block sums of NV accumulators into part[v][slot]: wave sums meet in LDS, then thread v
 // adds value v over the waves in wave order (the order of block_reduce) and stores it --
 // one barrier, the NV sums in parallel.
-template <int NV, int NT = kBlock>
+// LAST: the block's last wave adds and stores (the latency kernels' control wave, which has no
+// stores of its own in flight: a row wave's first vector wait after the barrier would also wait
+// for every row store it issued, one more memory trip before the partials leave).
+template <int NV, int NT = kBlock, bool LAST = false>
 __device__ __forceinline__ void write_partials(double (&acc)[NV], double *__restrict__ part, int slot) {
     __shared__ double sh[NV][NT / 64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1271,8 +1274,9 @@ __device__ __forceinline__ void write_partials(double (&acc)[NV], double *__rest
         if (lane == 0) sh[v][wid] = t;
     }
     __syncthreads();
-    if (threadIdx.x < NV) {
-        const int v = threadIdx.x;
+    const int t0 = LAST ? NT - 64 : 0;
+    if ((int)threadIdx.x >= t0 && (int)threadIdx.x < t0 + NV) {
+        const int v = threadIdx.x - t0;
         double t = 0.0;
 #pragma unroll
         for (int w = 0; w < NT / 64; ++w) t += sh[v][w];
@@ -2418,6 +2422,21 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
                 for (int q = 0; q < C_NCTRL; ++q) c[q] = cr[q];
             }
         }
+#elif defined(LRS_CTRL_LREG)
+        // the block and the parameters read back from LDS as one batch of loads (constant
+        // indices: registers), the step on registers, lane 0 writes the block back
+        {
+            double cr[C_NCTRL], pr[P_NPAR];
+#pragma unroll
+            for (int q = 0; q < C_NCTRL; ++q) cr[q] = c[q];
+#pragma unroll
+            for (int q = 0; q < P_NPAR; ++q) pr[q] = pl[q];
+            ctrl_step(cr, pr, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
+            if (l64 == 0) {
+#pragma unroll
+                for (int q = 0; q < C_NCTRL; ++q) c[q] = cr[q];
+            }
+        }
 #else
         if (l64 == 0) ctrl_step(c, pl, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
 #endif
@@ -2597,7 +2616,11 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         if (dg) entry(i, sd, xi, yi, cwd, l1d, bd, cd, lmd);
     }
     LRS_TS(0, 5);
+#ifdef LRS_PART_LAST
+    write_partials<8, kRowBlock, true>(acc, partA, pblk_off + blockIdx.x);
+#else
     write_partials<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x);
+#endif
     LRS_TS_END(0, 6);
 #ifdef LRS_PHASE_TIMING
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -3004,7 +3027,11 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
         }
     }
     LRS_TS(2, 3);
+#ifdef LRS_PART_LAST
+    write_partials<10, kRowBlock, true>(acc, partC, pblk_off + blockIdx.x);
+#else
     write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+#endif
     LRS_TS_END(2, 4);
 #ifdef LRS_PHASE_TIMING
     if (blockIdx.x == 0 && threadIdx.x == 0)
