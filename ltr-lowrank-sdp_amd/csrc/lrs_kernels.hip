@@ -2235,7 +2235,12 @@ __device__ __forceinline__ int lat_row_block(int b, int nrb) {
     return b;
 #endif
 }
-constexpr int kLatRowWaves = kRowBlock / 64 - 1;
+// threads per latency-kernel block (one control wave, the rest row waves); LRS_LAT_NT overrides
+#ifndef LRS_LAT_NT
+#define LRS_LAT_NT 512
+#endif
+constexpr int kLatNT = LRS_LAT_NT;
+constexpr int kLatRowWaves = kLatNT / 64 - 1;
 constexpr int kLatRows = kLatRowWaves * 64;      // row-wave threads per block
 constexpr int kLatMaxPartials = 256;             // producer blocks one control wave reduces
 constexpr int kSliceA = 2;                       // lower entries per lane group in a dense-row slice of A
@@ -2279,7 +2284,7 @@ __device__ __forceinline__ void wave_reduce_partials(const double *__restrict__ 
 // rows are prefetched before the barrier (the diagonal entry, the last lower one in the
 // column-sorted adjacency, uses the row's own operands); further ones are loaded after it.
 template <int G, int E, int NO>
-__global__ void __launch_bounds__(kRowBlock) k_lat_a(
+__global__ void __launch_bounds__(kLatNT) k_lat_a(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, const double *__restrict__ Cw,
     const double *__restrict__ Rb0, const double *__restrict__ Rb1, double *__restrict__ Dall,
@@ -2512,8 +2517,8 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
         // global constraints: A(RR^T) from the slots and their residual (as k_it_a)
         if (gwide) {
             const int lane64 = threadIdx.x & 63;
-            const int nw = gridDim.x * (kRowBlock / 64);
-            for (int g = blockIdx.x * (kRowBlock / 64) + (threadIdx.x >> 6); g < mg; g += nw) {
+            const int nw = gridDim.x * (kLatNT / 64);
+            for (int g = blockIdx.x * (kLatNT / 64) + (threadIdx.x >> 6); g < mg; g += nw) {
                 const int ig = glob[g];
                 double tot = 0.0;
                 for (int k = 0; k < K; ++k) {
@@ -2529,7 +2534,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
                 }
             }
         } else {
-            for (int g = blockIdx.x * kRowBlock + threadIdx.x; g < mg; g += gridDim.x * kRowBlock) {
+            for (int g = blockIdx.x * kLatNT + threadIdx.x; g < mg; g += gridDim.x * kLatNT) {
                 const int ig = glob[g];
                 double tot = 0.0;
                 for (int k = 0; k < K; ++k) {
@@ -2617,9 +2622,9 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
     }
     LRS_TS(0, 5);
 #ifdef LRS_PART_LAST
-    write_partials<8, kRowBlock, true>(acc, partA, pblk_off + blockIdx.x);
+    write_partials<8, kLatNT, true>(acc, partA, pblk_off + blockIdx.x);
 #else
-    write_partials<8, kRowBlock>(acc, partA, pblk_off + blockIdx.x);
+    write_partials<8, kLatNT>(acc, partA, pblk_off + blockIdx.x);
 #endif
     LRS_TS_END(0, 6);
 #ifdef LRS_PHASE_TIMING
@@ -2634,7 +2639,7 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_a(
 // first NO off-diagonal entries (records and neighbour rows R_j, D_j) and the diagonal
 // entry's records; after the barrier only the tau-dependent arithmetic and the stores run.
 template <int G, int E, int NO>
-__global__ void __launch_bounds__(kRowBlock) k_lat_b(
+__global__ void __launch_bounds__(kLatNT) k_lat_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
     const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0, double *s1, double *y1,
@@ -3028,9 +3033,9 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_b(
     }
     LRS_TS(2, 3);
 #ifdef LRS_PART_LAST
-    write_partials<10, kRowBlock, true>(acc, partC, pblk_off + blockIdx.x);
+    write_partials<10, kLatNT, true>(acc, partC, pblk_off + blockIdx.x);
 #else
-    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+    write_partials<10, kLatNT>(acc, partC, pblk_off + blockIdx.x);
 #endif
     LRS_TS_END(2, 4);
 #ifdef LRS_PHASE_TIMING
@@ -5711,10 +5716,10 @@ static int num_cus() {
     return cus[dev];
 }
 template <typename KernelT>
-static int resident_blocks(KernelT kern, int *cache) {
+static int resident_blocks(KernelT kern, int *cache, int nt = kRowBlock) {
     if (*cache <= 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), kRowBlock, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), nt, 0) !=
                 hipSuccess || nb < 1)
             nb = 1;
         *cache = nb * num_cus();
@@ -5805,12 +5810,12 @@ constexpr int kLatNoA = 2, kLatNoB = 4;   // off-diagonal entries prefetched (A:
 template <int GG, int EE>
 static int res_la() {
     static int c = 0;
-    return resident_blocks(k_lat_a<GG, EE, kLatNoA>, &c);
+    return resident_blocks(k_lat_a<GG, EE, kLatNoA>, &c, kLatNT);
 }
 template <int GG, int EE>
 static int res_lb() {
     static int c = 0;
-    return resident_blocks(k_lat_b<GG, EE, kLatNoB>, &c);
+    return resident_blocks(k_lat_b<GG, EE, kLatNoB>, &c, kLatNT);
 }
 static bool lat_disabled() {
     static int v = -1;
@@ -6081,7 +6086,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        pstr)
         if (lat) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                hipLaunchKernelGGL((k_lat_a<GG, EE, kLatNoA>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
+                hipLaunchKernelGGL((k_lat_a<GG, EE, kLatNoA>), dim3(grid), dim3(kLatNT), 0, st, c.nown,
                                    c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D,
                                    W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr,
                                    P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam,
@@ -6192,7 +6197,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const bool small = pb[k].small;
         if (lat) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                hipLaunchKernelGGL((k_lat_b<GG, EE, kLatNoB>), dim3(grid), dim3(kRowBlock), 0, st, c.nown,
+                hipLaunchKernelGGL((k_lat_b<GG, EE, kLatNoB>), dim3(grid), dim3(kLatNT), 0, st, c.nown,
                                    c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0],
                                    W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
                                    P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con,
