@@ -162,8 +162,17 @@ __device__ __forceinline__ double wave_sum(double v) {
     return (read_lane(v, 0) + read_lane(v, 16)) + (read_lane(v, 32) + read_lane(v, 48));
 }
 
+// two doubles at 8-byte alignment (gfx950 global loads/stores take unaligned 16-byte accesses)
+typedef double d2u8 __attribute__((ext_vector_type(2), aligned(8)));
 template <int E>
 __device__ __forceinline__ void ld_row(const double *__restrict__ p, double (&v)[E]) {
+#ifdef LRS_ROW_X4
+    if constexpr (E == 3) {   // 16 + 8 bytes (8-byte aligned 16-byte load: two instructions, not three)
+        const d2u8 t = *reinterpret_cast<const d2u8 *>(p);
+        v[0] = t.x; v[1] = t.y; v[2] = p[2];
+        return;
+    }
+#endif
     if constexpr (E == 2) {
         double2 t = *reinterpret_cast<const double2 *>(p);
         v[0] = t.x; v[1] = t.y;
@@ -179,6 +188,15 @@ __device__ __forceinline__ void ld_row(const double *__restrict__ p, double (&v)
 
 template <int E>
 __device__ __forceinline__ void st_row(double *__restrict__ p, const double (&v)[E]) {
+#ifdef LRS_ROW_X4
+    if constexpr (E == 3) {
+        d2u8 t;
+        t.x = v[0]; t.y = v[1];
+        *reinterpret_cast<d2u8 *>(p) = t;
+        p[2] = v[2];
+        return;
+    }
+#endif
     if constexpr (E == 2) {
         *reinterpret_cast<double2 *>(p) = make_double2(v[0], v[1]);
     } else if constexpr (E == 4) {
@@ -1261,10 +1279,7 @@ __device__ void line_search(const double *__restrict__ par, int K, double *ls) {
 // Block sums of NV accumulators into part[v][slot]: wave sums meet in LDS, then thread v
 // adds value v over the waves in wave order (the order of block_reduce) and stores it --
 // one barrier, the NV sums in parallel.
-// LAST: the block's last wave adds and stores (the latency kernels' control wave, which has no
-// stores of its own in flight: a row wave's first vector wait after the barrier would also wait
-// for every row store it issued, one more memory trip before the partials leave).
-template <int NV, int NT = kBlock, bool LAST = false>
+template <int NV, int NT = kBlock>
 __device__ __forceinline__ void write_partials(double (&acc)[NV], double *__restrict__ part, int slot) {
     __shared__ double sh[NV][NT / 64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1274,12 +1289,33 @@ __device__ __forceinline__ void write_partials(double (&acc)[NV], double *__rest
         if (lane == 0) sh[v][wid] = t;
     }
     __syncthreads();
-    const int t0 = LAST ? NT - 64 : 0;
-    if ((int)threadIdx.x >= t0 && (int)threadIdx.x < t0 + NV) {
-        const int v = threadIdx.x - t0;
+    if (threadIdx.x < NV) {
+        const int v = threadIdx.x;
         double t = 0.0;
 #pragma unroll
         for (int w = 0; w < NT / 64; ++w) t += sh[v][w];
+        part[v * kMaxPartialBlocks + slot] = t;
+    }
+}
+
+// write_partials for a block of nw <= 8 waves (the latency kernels' run-time block size): the
+// same wave-order sums
+template <int NV>
+__device__ __forceinline__ void write_partials_nw(double (&acc)[NV], double *__restrict__ part, int slot, int nw) {
+    __shared__ double sh[NV][8];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const double t = wave_sum(acc[v]);
+        if (lane == 0) sh[v][wid] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        const int v = threadIdx.x;
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+            if (w < nw) t += sh[v][w];
         part[v * kMaxPartialBlocks + slot] = t;
     }
 }
@@ -2235,13 +2271,14 @@ __device__ __forceinline__ int lat_row_block(int b, int nrb) {
     return b;
 #endif
 }
-// threads per latency-kernel block (one control wave, the rest row waves); LRS_LAT_NT overrides
-#ifndef LRS_LAT_NT
-#define LRS_LAT_NT 512
-#endif
-constexpr int kLatNT = LRS_LAT_NT;
+// Latency-kernel blocks: w row waves (1 <= w <= 7) and one control wave, w chosen per launch at
+// run time (blockDim.x = 64 (w + 1)) so that the grid spreads the row waves over as many CUs as
+// it can (<= 256 blocks): the row waves' vector memory instructions per CU bound the launch
+// (G67: 7 row waves a block, 179 blocks -> 5, 250 blocks: k_lat_a 9.1 -> 8.7, k_lat_b 10.1 ->
+// 9.55 us, scripts/gpu_r04v.sh).
+constexpr int kLatNT = 512;                      // the largest block (launch bounds)
 constexpr int kLatRowWaves = kLatNT / 64 - 1;
-constexpr int kLatRows = kLatRowWaves * 64;      // row-wave threads per block
+constexpr int kLatRows = kLatRowWaves * 64;      // row-wave threads of the largest block
 constexpr int kLatMaxPartials = 256;             // producer blocks one control wave reduces
 constexpr int kSliceA = 2;                       // lower entries per lane group in a dense-row slice of A
 constexpr int kSliceB = 4;                       // entries per lane group in a dense-row slice of B
@@ -2313,15 +2350,16 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
              cvs, lam, m, par, ctrl_prev, ls_prev, partC, nblkC, nrb, nda, dra);
 #endif
     LRS_BLK_BEGIN();
-    const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == kLatRowWaves;   // wave-uniform
+    const int nwv = (int)(blockDim.x >> 6), rpb = (nwv - 1) * 64 / G;   // waves, rows of this block
+    const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == nwv - 1;   // wave-uniform
     const int lane = threadIdx.x & (G - 1);
     // blocks [0, nrb): one row per lane group.  Blocks past nrb: slices of the dense rows --
     // every lane group of the block takes kSliceA consecutive lower entries of one dense row
     // (the rows' own groups skip those entries; A's results are per slot, nothing to combine)
     const bool slice = (int)blockIdx.x >= nrb;
-    int i = lat_row_block((int)blockIdx.x, nrb) * (kLatRows / G) + (int)threadIdx.x / G, sq = 0;
+    int i = lat_row_block((int)blockIdx.x, nrb) * rpb + (int)threadIdx.x / G, sq = 0;
     if (slice) {
-        constexpr int per = (kLatRows / G) * kSliceA;
+        const int per = rpb * kSliceA;
         int q = (int)blockIdx.x - nrb, L = 0;
         for (; L < nda - 1; ++L) {
             const int r = dra[L], ns = (adj_low[r] - adj_ptr[r] + per - 1) / per;
@@ -2517,8 +2555,8 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
         // global constraints: A(RR^T) from the slots and their residual (as k_it_a)
         if (gwide) {
             const int lane64 = threadIdx.x & 63;
-            const int nw = gridDim.x * (kLatNT / 64);
-            for (int g = blockIdx.x * (kLatNT / 64) + (threadIdx.x >> 6); g < mg; g += nw) {
+            const int nw = gridDim.x * nwv;
+            for (int g = blockIdx.x * nwv + (threadIdx.x >> 6); g < mg; g += nw) {
                 const int ig = glob[g];
                 double tot = 0.0;
                 for (int k = 0; k < K; ++k) {
@@ -2534,7 +2572,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
                 }
             }
         } else {
-            for (int g = blockIdx.x * kLatNT + threadIdx.x; g < mg; g += gridDim.x * kLatNT) {
+            for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < mg; g += gridDim.x * blockDim.x) {
                 const int ig = glob[g];
                 double tot = 0.0;
                 for (int k = 0; k < K; ++k) {
@@ -2621,11 +2659,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
         if (dg) entry(i, sd, xi, yi, cwd, l1d, bd, cd, lmd);
     }
     LRS_TS(0, 5);
-#ifdef LRS_PART_LAST
-    write_partials<8, kLatNT, true>(acc, partA, pblk_off + blockIdx.x);
-#else
-    write_partials<8, kLatNT>(acc, partA, pblk_off + blockIdx.x);
-#endif
+    write_partials_nw<8>(acc, partA, pblk_off + blockIdx.x, nwv);
     LRS_TS_END(0, 6);
 #ifdef LRS_PHASE_TIMING
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -2670,15 +2704,16 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
 #endif
     LRS_BLK_BEGIN();
     mirror_ctrl(ctrl, hmirror, seq);
-    const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == kLatRowWaves;   // wave-uniform
+    const int nwv = (int)(blockDim.x >> 6), rpb = (nwv - 1) * 64 / G;   // waves, rows of this block
+    const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == nwv - 1;   // wave-uniform
     const int lane = threadIdx.x & (G - 1);
     // blocks [0, nrb): one row per lane group.  Blocks past nrb: slices of the dense rows --
     // every lane group takes kSliceB consecutive entries of one dense row, the block's partial
     // gradient goes to gl[slice] and k_lat_f finishes the row (its own group skips the entries)
     const bool slice = (int)blockIdx.x >= nrb;
-    int i = lat_row_block((int)blockIdx.x, nrb) * (kLatRows / G) + (int)threadIdx.x / G, sq = 0;
+    int i = lat_row_block((int)blockIdx.x, nrb) * rpb + (int)threadIdx.x / G, sq = 0;
     if (slice) {
-        constexpr int per = (kLatRows / G) * kSliceB;
+        const int per = rpb * kSliceB;
         int q = (int)blockIdx.x - nrb, Ld = 0;
         for (; Ld < ndb - 1; ++Ld) {
             const int r = drb[Ld], ns = (adj_ptr[r + 1] - adj_ptr[r] + per - 1) / per;
@@ -3027,16 +3062,12 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
         if ((int)threadIdx.x < G * E) {
             const int ln = threadIdx.x / E, e = threadIdx.x % E;
             double t = 0.0;
-            for (int q = 0; q < kLatRows / G; ++q) t += gsh[(q * G + ln) * E + e];
+            for (int q = 0; q < rpb; ++q) t += gsh[(q * G + ln) * E + e];
             gl[(long)((int)blockIdx.x - nrb) * ld + threadIdx.x] = t;
         }
     }
     LRS_TS(2, 3);
-#ifdef LRS_PART_LAST
-    write_partials<10, kLatNT, true>(acc, partC, pblk_off + blockIdx.x);
-#else
-    write_partials<10, kLatNT>(acc, partC, pblk_off + blockIdx.x);
-#endif
+    write_partials_nw<10>(acc, partC, pblk_off + blockIdx.x, nwv);
     LRS_TS_END(2, 4);
 #ifdef LRS_PHASE_TIMING
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -5829,7 +5860,7 @@ static bool lat_disabled() {
 // then sa / sb slice blocks over the dense rows' entries (A: lower, B: all) and nf k_lat_f
 // blocks.  nrb == 0: they do not apply.
 struct LatPlan {
-    int nrb = 0, sa = 0, sb = 0, nf = 0;
+    int nrb = 0, sa = 0, sb = 0, nf = 0, nt = kLatNT;   // nt: threads a block (w row waves + 1)
 };
 static int lat_slices(const std::vector<int> &cnt, int per) {
     int s = 0;
@@ -5840,14 +5871,15 @@ static int lat_resident(const DevCone &c, int &ra, int &rb) {
     LRS_LAYOUT_SWITCH(c.G, c.E, { ra = (res_la<GG, EE>)(); rb = (res_lb<GG, EE>)(); });
     return 0;
 }
-static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &pb) {
+static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &pb, int w = kLatRowWaves) {
     LatPlan lp;
     if (lat_disabled() || forced_regime() == 2 || c.maxdeg <= 0 || !pa.small || !pb.small || pa.T != 1 || pb.T != 1)
         return lp;
     if ((int)c.dra_h.size() > kMaxDenseRows || (int)c.drb_h.size() > kMaxDenseRows) return lp;
-    const long need = std::max(1L, ((long)c.nown * c.G + kLatRows - 1) / kLatRows);
-    const int sa = lat_slices(c.dra_n, (kLatRows / c.G) * kSliceA);
-    const int sb = lat_slices(c.drb_n, (kLatRows / c.G) * kSliceB);
+    const int rows = 64 * w;   // row-wave threads a block
+    const long need = std::max(1L, ((long)c.nown * c.G + rows - 1) / rows);
+    const int sa = lat_slices(c.dra_n, (rows / c.G) * kSliceA);
+    const int sb = lat_slices(c.drb_n, (rows / c.G) * kSliceB);
     int ra = 0, rb = 0;
     if (lat_resident(c, ra, rb)) return lp;
     if (need + sa > ra || need + sb > rb || need + sa > kLatMaxPartials) return lp;
@@ -5856,7 +5888,17 @@ static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &
     lp.sa = sa;
     lp.sb = sb;
     lp.nf = (int)c.drb_h.size();
+    lp.nt = 64 * (w + 1);
     return lp;
+}
+// LRS_LAT_ROWWAVES = 1..7 forces the row waves per latency block (0: chosen per launch)
+static int lat_forced_waves() {
+    static int forced = -1;
+    if (forced < 0) {
+        const char *e = getenv("LRS_LAT_ROWWAVES");
+        forced = e ? std::max(0, std::min(kLatRowWaves, atoi(e))) : 0;
+    }
+    return forced;
 }
 
 // the multi-launch kernel family forced by lrs_set_kernel_path (4, the single-workgroup inner
@@ -6017,9 +6059,25 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     for (int k = 0; k < KL && lat; ++k) {
         lg[k] = lat_plan(cone_of(k), pa[k], pb[k]);
         if (lg[k].nrb <= 0) lat = false;
-        nla += lg[k].nrb + lg[k].sa;
-        nlb += lg[k].nrb + lg[k].sb;
-        nlf += lg[k].nf;
+    }
+    if (lat) {
+        // row waves per block: the fewest whose grids (every cone's row and slice blocks, the
+        // dense objective's and k_lat_f's partial blocks) stay within min(kLatMaxPartials, CUs)
+        // blocks a stage -- one block a CU with as few row waves as the grid allows; else 7
+        const int cap = std::min(kLatMaxPartials, num_cus());
+        const int wf = lat_forced_waves();
+        for (int w = wf > 0 ? wf : 1; w <= kLatRowWaves; ++w) {
+            nla = nlb = nlf = 0;
+            for (int k = 0; k < KL; ++k) {
+                lg[k] = lat_plan(cone_of(k), pa[k], pb[k], w);
+                if (lg[k].nrb <= 0) lat = false;
+                nla += lg[k].nrb + lg[k].sa;
+                nlb += lg[k].nrb + lg[k].sb;
+                nlf += lg[k].nf;
+            }
+            if (!lat || wf > 0 || w == kLatRowWaves) break;
+            if (nla + ngd <= cap && nlb + nlf <= cap && (P.mg == 0 || gg <= cap)) break;
+        }
     }
     if (lat && (nla + ngd > kLatMaxPartials || nlb + nlf > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials)))
         lat = false;
@@ -6086,7 +6144,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        pstr)
         if (lat) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                hipLaunchKernelGGL((k_lat_a<GG, EE, kLatNoA>), dim3(grid), dim3(kLatNT), 0, st, c.nown,
+                hipLaunchKernelGGL((k_lat_a<GG, EE, kLatNoA>), dim3(grid), dim3(lg[k].nt), 0, st, c.nown,
                                    c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, P.Cw, W.R, W.R2, W.D,
                                    W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt0, W.uvt1, P.loc_ptr,
                                    P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam,
@@ -6197,7 +6255,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const bool small = pb[k].small;
         if (lat) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                hipLaunchKernelGGL((k_lat_b<GG, EE, kLatNoB>), dim3(grid), dim3(kLatNT), 0, st, c.nown,
+                hipLaunchKernelGGL((k_lat_b<GG, EE, kLatNoB>), dim3(grid), dim3(lg[k].nt), 0, st, c.nown,
                                    c.ld, c.foff, c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0],
                                    W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
                                    P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con,
@@ -6222,7 +6280,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const DevCone &c = cone_of(k);
         if (lg[k].nf > 0) {
             hipLaunchKernelGGL(k_lat_f, dim3(lg[k].nf), dim3(kRowBlock), 0, st, c.ld, c.G * c.E, c.foff, c.adj_ptr,
-                               c.drb, (kLatRows / c.G) * kSliceB, W.gl + glo, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
+                               c.drb, ((lg[k].nt - 64) / c.G) * kSliceB, W.gl + glo, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
                                W.ls[1], W.ly[1], ctrl_cur, ls_cur, L, W.partC, off, P.ndense ? W.CR : nullptr, W.CD);
             LRS_CHECK_LAUNCH();
         }
