@@ -2334,7 +2334,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
     const int *__restrict__ con_ptr, const int *__restrict__ con_slot, const double *__restrict__ con_w,
     const double *__restrict__ uRR, const double *__restrict__ par, const double *__restrict__ ctrl_prev,
     double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev, const double *__restrict__ partC, int nblkC,
-    double *__restrict__ partA, int pblk_off, int gwide, int nrb, int nda, const int *__restrict__ dra) {
+    double *__restrict__ partA, int pblk_off, int gwide, int nrb, int lrw, int nda, const int *__restrict__ dra) {
     __shared__ double c[C_NCTRL];
     __shared__ double pl[P_NPAR];
     LRS_TS(0, 0);
@@ -2350,7 +2350,9 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
              cvs, lam, m, par, ctrl_prev, ls_prev, partC, nblkC, nrb, nda, dra);
 #endif
     LRS_BLK_BEGIN();
-    const int nwv = (int)(blockDim.x >> 6), rpb = (nwv - 1) * 64 / G;   // waves, rows of this block
+    // lrw row waves + the control wave (an argument beside nrb, loaded in the first argument batch:
+    // blockDim.x would be one more load before the first branch)
+    const int nwv = lrw + 1, rpb = lrw * 64 / G;   // waves, rows of this block
     const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == nwv - 1;   // wave-uniform
     const int lane = threadIdx.x & (G - 1);
     // blocks [0, nrb): one row per lane group.  Blocks past nrb: slices of the dense rows --
@@ -2572,7 +2574,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
                 }
             }
         } else {
-            for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < mg; g += gridDim.x * blockDim.x) {
+            for (int g = blockIdx.x * nwv * 64 + threadIdx.x; g < mg; g += gridDim.x * nwv * 64) {
                 const int ig = glob[g];
                 double tot = 0.0;
                 for (int k = 0; k < K; ++k) {
@@ -2684,7 +2686,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
     double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
     const double *__restrict__ partA, int nblkA, const double *__restrict__ partB, int nblkB,
     double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m, double *hmirror,
-    double seq, int nrb, int ndb, const int *__restrict__ drb, double *__restrict__ gl, double *CRb,
+    double seq, int nrb, int lrw, int ndb, const int *__restrict__ drb, double *__restrict__ gl, double *CRb,
     const double *__restrict__ CDb) {
     __shared__ double red[12];
     __shared__ double ls[LS_N];
@@ -2704,7 +2706,9 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
 #endif
     LRS_BLK_BEGIN();
     mirror_ctrl(ctrl, hmirror, seq);
-    const int nwv = (int)(blockDim.x >> 6), rpb = (nwv - 1) * 64 / G;   // waves, rows of this block
+    // lrw row waves + the control wave (an argument beside nrb, loaded in the first argument batch:
+    // blockDim.x would be one more load before the first branch)
+    const int nwv = lrw + 1, rpb = lrw * 64 / G;   // waves, rows of this block
     const bool ctrl_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == nwv - 1;   // wave-uniform
     const int lane = threadIdx.x & (G - 1);
     // blocks [0, nrb): one row per lane group.  Blocks past nrb: slices of the dense rows --
@@ -6068,15 +6072,19 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const int wf = lat_forced_waves();
         for (int w = wf > 0 ? wf : 1; w <= kLatRowWaves; ++w) {
             nla = nlb = nlf = 0;
+            bool fits = true;
             for (int k = 0; k < KL; ++k) {
                 lg[k] = lat_plan(cone_of(k), pa[k], pb[k], w);
-                if (lg[k].nrb <= 0) lat = false;
+                if (lg[k].nrb <= 0) fits = false;
                 nla += lg[k].nrb + lg[k].sa;
                 nlb += lg[k].nrb + lg[k].sb;
                 nlf += lg[k].nf;
             }
-            if (!lat || wf > 0 || w == kLatRowWaves) break;
-            if (nla + ngd <= cap && nlb + nlf <= cap && (P.mg == 0 || gg <= cap)) break;
+            if (wf > 0 || w == kLatRowWaves) {
+                lat = fits;
+                break;
+            }
+            if (fits && nla + ngd <= cap && nlb + nlf <= cap && (P.mg == 0 || gg <= cap)) break;
         }
     }
     if (lat && (nla + ngd > kLatMaxPartials || nlb + nlf > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials)))
@@ -6150,7 +6158,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam,
                                    W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,
                                    W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, gwide,
-                                   lg[k].nrb, (int)c.dra_h.size(), c.dra);
+                                   lg[k].nrb, lg[k].nt / 64 - 1, (int)c.dra_h.size(), c.dra);
             });
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
@@ -6261,7 +6269,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con,
                                    P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur,
                                    inA, nA, W.partB, P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, P.m,
-                                   k == 0 ? a.hmirror : nullptr, a.seq, lg[k].nrb, (int)c.drb_h.size(), c.drb,
+                                   k == 0 ? a.hmirror : nullptr, a.seq, lg[k].nrb, lg[k].nt / 64 - 1, (int)c.drb_h.size(), c.drb,
                                    W.gl + glo, P.ndense ? W.CR : nullptr, W.CD);
             });
             glo += (long)lg[k].sb * c.ld;

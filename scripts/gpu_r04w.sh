@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD; O=$R/gpurun_out/r04w; mkdir -p $O
 B=$R/ltr-lowrank-sdp_amd/_build
 for rep in 1 2 3; do
-  for v in auto w7 w5 x4 lat6x4; do
+  for v in auto w7 w5 x4; do
     case $v in
       auto) LIB=liblrsdp; W= ;; w7) LIB=liblrsdp; W=7 ;; w5) LIB=liblrsdp; W=5 ;; *) LIB=liblrsdp_$v; W= ;;
     esac
