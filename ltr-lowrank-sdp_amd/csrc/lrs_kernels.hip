@@ -2528,6 +2528,21 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
         // slots without a single local constraint read the row's own (spread, cached) index
         // instead of a common one: no hot line shared by every lane
         const int ispare = min(ic, m - 1);
+#ifdef LRS_LAT_SKIPREC
+        // entries without a single local constraint (MaxCut's off-diagonal ones) load nothing:
+        // a wave whose entries u have none skips the loads (exec-masked branch)
+#pragma unroll
+        for (int u = 0; u < NO; ++u) {
+            const int ci = (int)l1[u].y;
+            bq[u] = cq[u] = lq[u] = 0.0;
+            if (ci >= 0) { bq[u] = b[ci]; cq[u] = cvs[ci]; lq[u] = lam[ci]; }
+        }
+        {
+            const int ci = (int)l1d.y;
+            if (ci >= 0) { bd = b[ci]; cd = cvs[ci]; lmd = lam[ci]; }
+        }
+        (void)ispare;
+#else
 #pragma unroll
         for (int u = 0; u < NO; ++u) {
             const int ci = (int)l1[u].y >= 0 ? (int)l1[u].y : ispare;
@@ -2541,6 +2556,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
             cd = cvs[ci];
             lmd = lam[ci];
         }
+#endif
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && threadIdx.x == 0 && xi[0] != 12345.678) g_phase_tmp[0][1] = wall_clock64();
         if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && xj[0][0] != 12345.678 && bd != 12345.678)
@@ -2883,6 +2899,29 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
         // slots without a single constraint read the row's own (spread, cached) index instead
         // of a common one: no hot line shared by every lane
         const int ispare = min(ic, m - 1);
+#ifdef LRS_LAT_SKIPREC
+#pragma unroll
+        for (int u = 0; u < NO; ++u) {
+            const int c1 = (int)s1v[u].y, cl = (int)l1v[u].y;
+            ra[u] = rb[u] = make_double2(0.0, 0.0);
+            bq[u] = 0.0;
+            if (c1 >= 0) {
+                const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
+                ra[u] = r[0];
+                rb[u] = r[1];
+            }
+            if (cl >= 0) bq[u] = b[cl];
+        }
+        {
+            const int c1 = (int)s1d.y, cl = (int)l1d.y;
+            if (c1 >= 0) {
+                const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
+                rad = r[0];
+                rbd = r[1];
+            }
+            if (cl >= 0) bqd = b[cl];
+            (void)ispare;
+#else
 #pragma unroll
         for (int u = 0; u < NO; ++u) {
             const int c1 = (int)s1v[u].y >= 0 ? (int)s1v[u].y : ispare;
@@ -2899,6 +2938,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
             rad = r[0];
             rbd = r[1];
             bqd = b[cl];
+#endif
         }
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && threadIdx.x == 0 && ri[0] != 12345.678 && sv[0] != 12345.678)
