@@ -6441,7 +6441,10 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
 // multi-launch iteration's control would (ctrl_step's exits), so every run_inner call is one
 // launch and one host synchronisation.
 // ------------------------------------------------------------------------
-constexpr int kSmallThreads = 512;
+#ifndef LRS_SMALL_NT
+#define LRS_SMALL_NT 512
+#endif
+constexpr int kSmallThreads = LRS_SMALL_NT;   // the single workgroup's threads
 constexpr int kSmallMaxConst = 4;     // constant-objective cones the kernel carries
 constexpr int kSmallMaxLd = 64;       // widest factor row
 struct SmallArgs {
@@ -7263,7 +7266,10 @@ int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, i
 // adjacency's column order (k_cg_mv's order).  Sums over the block: wave sums, then the eight
 // wave values in wave order (deterministic).
 // ------------------------------------------------------------------------
-constexpr int kScT = 512;                // threads
+#ifndef LRS_SC_NT
+#define LRS_SC_NT 512
+#endif
+constexpr int kScT = LRS_SC_NT;          // threads
 constexpr int kScL = 16;                 // lanes per factor row
 constexpr int kScG = kScT / kScL;        // row groups
 constexpr int kScW = kScT / 64;          // waves
@@ -7710,6 +7716,12 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
 // 8 rows a group, EL 2 up to 6, EL 3 up to 4, EL 4 up to 2 (five register arrays of EL x RPG
 // doubles at two waves a SIMD; the larger products spill)
 static int small_cg_rpg(int EL, int RPG) {
+    if constexpr (kScT == 1024) {
+        // 128 VGPRs a lane at 1024 threads: the variants that do not spill
+        const int lim = EL == 1 ? 6 : (EL == 2 ? 3 : (EL == 3 ? 2 : 0));
+        const int rpg = RPG <= 2 ? 2 : (RPG <= 3 ? 3 : (RPG <= 4 ? 4 : (RPG <= 6 ? 6 : 8)));
+        return (RPG >= 1 && rpg <= lim) ? rpg : 0;
+    }
     const int lim = EL == 1 ? 8 : (EL == 2 ? 6 : (EL == 3 ? 4 : (EL == 4 ? 2 : 0)));
     const int rpg = RPG <= 2 ? 2 : (RPG <= 4 ? 4 : (RPG <= 6 ? 6 : 8));
     return (RPG >= 1 && rpg <= lim) ? rpg : 0;
@@ -7767,6 +7779,10 @@ int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double 
     case 1 * 16 + 6: return launch_small_cg_t<1, 6>(A, lds, st);
     case 1 * 16 + 8: return launch_small_cg_t<1, 8>(A, lds, st);
     case 2 * 16 + 2: return launch_small_cg_t<2, 2>(A, lds, st);
+#if LRS_SC_NT == 1024
+    case 1 * 16 + 3: return launch_small_cg_t<1, 3>(A, lds, st);
+    case 2 * 16 + 3: return launch_small_cg_t<2, 3>(A, lds, st);
+#endif
     case 2 * 16 + 4: return launch_small_cg_t<2, 4>(A, lds, st);
     case 2 * 16 + 6: return launch_small_cg_t<2, 6>(A, lds, st);
     case 3 * 16 + 2: return launch_small_cg_t<3, 2>(A, lds, st);

@@ -9,6 +9,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 solver = importlib.import_module("ltr-lowrank-sdp_amd.solver")
 inst = importlib.import_module("ltr-lowrank-sdp_amd.instances")
+if os.environ.get("LRS_PROBE_LIB"):   # a variant build (ltr-lowrank-sdp_amd/_build/liblrsdp_<v>.so)
+    solver.load_library(os.environ["LRS_PROBE_LIB"])
 cache = os.path.join(ROOT, ".bench_instances")
 os.makedirs(cache, exist_ok=True)
 sdplib = {"reoptLevel": 0, "heuristicFactor": 1.0, "phase1Tol": 1e-3, "rhoMax": 5000.0}
