@@ -7267,7 +7267,7 @@ int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, i
 // wave values in wave order (deterministic).
 // ------------------------------------------------------------------------
 #ifndef LRS_SC_NT
-#define LRS_SC_NT 512
+#define LRS_SC_NT 1024
 #endif
 constexpr int kScT = LRS_SC_NT;          // threads
 constexpr int kScL = 16;                 // lanes per factor row
