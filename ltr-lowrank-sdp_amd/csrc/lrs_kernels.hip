@@ -138,6 +138,32 @@ __device__ __forceinline__ double group_sum(double v) {
     return v;
 }
 
+// Four dot products reduced over an aligned group of G = 4 or 16 lanes by a transposed
+// butterfly: each exchange step halves the values a lane holds (G = 4: xor 2, xor 1; G = 16:
+// row_mirror, row_half_mirror, then the quad sums), so four sums cost 3 (G = 4) or 5 (G = 16)
+// double moves instead of 8 / 16.  Returns entry q's total in the lanes whose group offset
+// o satisfies q = o / (G / 4) (G = 4: lane o holds entry o).
+template <int G>
+__device__ __forceinline__ double group_sum4(const double (&d)[4], int o) {
+    static_assert(G == 4 || G == 16, "group of 4 or 16 lanes");
+    if constexpr (G == 4) {
+        const bool h1 = (o & 2) != 0, h0 = (o & 1) != 0;
+        double a0 = h1 ? d[2] : d[0], a1 = h1 ? d[3] : d[1];
+        a0 += dpp_mov<0x4E>(h1 ? d[0] : d[2]);
+        a1 += dpp_mov<0x4E>(h1 ? d[1] : d[3]);
+        return (h0 ? a1 : a0) + dpp_mov<0xB1>(h0 ? a0 : a1);
+    } else {
+        const bool h3 = (o & 8) != 0, h2 = (o & 4) != 0;
+        double a0 = h3 ? d[2] : d[0], a1 = h3 ? d[3] : d[1];
+        a0 += dpp_mov<0x140>(h3 ? d[0] : d[2]);
+        a1 += dpp_mov<0x140>(h3 ? d[1] : d[3]);
+        double v = (h2 ? a1 : a0) + dpp_mov<0x141>(h2 ? a0 : a1);
+        v += dpp_mov<0x4E>(v);
+        v += dpp_mov<0xB1>(v);
+        return v;
+    }
+}
+
 // Kernel arguments (and uniform words) in SGPRs at this point: the compiler otherwise sinks
 // each argument load to the basic block that first uses it, and every branch level of a
 // kernel's prologue then waits for its own argument trip (three dependent trips in k_lat_a /
@@ -1302,6 +1328,56 @@ __device__ __forceinline__ void write_partials(double (&acc)[NV], double *__rest
 // same wave-order sums
 template <int NV>
 __device__ __forceinline__ void write_partials_nw(double (&acc)[NV], double *__restrict__ part, int slot, int nw) {
+#ifdef LRS_BFLY
+    // transposed butterfly in each 16-lane row (row_mirror, row_half_mirror, xor 2, xor 1: each
+    // step halves the values a lane holds; 15 double moves for up to 16 values instead of four a
+    // value plus the readlanes): value v's row sum ends in lane v of every row; the four rows of
+    // every wave meet in LDS and thread v adds them in (wave, row) order
+    static_assert(NV <= 16, "one value a lane of a 16-lane row");
+    __shared__ double sh[NV][32];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, o = lane & 15;
+    double x[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) x[v] = v < NV ? acc[v] : 0.0;
+    {
+        const bool h = (o & 8) != 0;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const double keep = h ? x[m + 8] : x[m], send = h ? x[m] : x[m + 8];
+            x[m] = keep + dpp_mov<0x140>(send);
+        }
+    }
+    {
+        const bool h = (o & 4) != 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const double keep = h ? x[m + 4] : x[m], send = h ? x[m] : x[m + 4];
+            x[m] = keep + dpp_mov<0x141>(send);
+        }
+    }
+    {
+        const bool h = (o & 2) != 0;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const double keep = h ? x[m + 2] : x[m], send = h ? x[m] : x[m + 2];
+            x[m] = keep + dpp_mov<0x4E>(send);
+        }
+    }
+    {
+        const bool h = (o & 1) != 0;
+        x[0] = (h ? x[1] : x[0]) + dpp_mov<0xB1>(h ? x[0] : x[1]);
+    }
+    if (o < NV) sh[o][wid * 4 + (lane >> 4)] = x[0];
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        const int v = threadIdx.x;
+        double t = 0.0;
+#pragma unroll
+        for (int q = 0; q < 32; ++q)
+            if (q < 4 * nw) t += sh[v][q];
+        part[v * kMaxPartialBlocks + slot] = t;
+    }
+#else
     __shared__ double sh[NV][8];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -1318,6 +1394,7 @@ __device__ __forceinline__ void write_partials_nw(double (&acc)[NV], double *__r
             if (w < nw) t += sh[v][w];
         part[v * kMaxPartialBlocks + slot] = t;
     }
+#endif
 }
 
 template <int NV, int NT = kBlock>
@@ -6839,13 +6916,31 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                         d[u] += rii[p].x * x[u][p].x;
                         d[u] += rii[p].y * x[u][p].y;
                     }
+#if !defined(LRS_BFLY)
                     d[u] = group_sum<TPR>(d[u]);
+#endif
                 }
                 // lower entries: A(R R^T) on this row's slots (their constraints after the barrier)
+#ifdef LRS_BFLY
+                if constexpr (TPR == 4) {
+                    const double v = group_sum4<4>(d, sl_lane);   // lane u: entry u
+                    const int u = sl_lane;
+                    const int su = u == 0 ? js[0].y : (u == 1 ? js[1].y : (u == 2 ? js[2].y : js[3].y));
+                    if (k + u < kl) XB[su] = v;
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) d[u] = group_sum<TPR>(d[u]);
+                    if (sl_lane == 0)
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (k + u < kl) XB[js[u].y] = d[u];
+                }
+#else
                 if (sl_lane == 0)
 #pragma unroll
                     for (int u = 0; u < 4; ++u)
                         if (k + u < kl) XB[js[u].y] = d[u];
+#endif
             }
             LRS_SM_SUB(8, t_adj);
             if (!valid) continue;
@@ -7440,12 +7535,22 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
 #pragma unroll
                     for (int k = 0; k < EL; ++k) d[u] += xq[k] * Ys[j * rS + l + kScL * k];
                 }
+#ifdef LRS_BFLY
+                {
+                    // entry u's total in lanes 4u..4u+3; lane 4u stores it
+                    const double v = group_sum4<kScL>(d, l);
+                    const int u = l >> 2;
+                    const int pku = u == 0 ? pk[0] : (u == 1 ? pk[1] : (u == 2 ? pk[2] : pk[3]));
+                    if ((l & 3) == 0 && e + u < e1) T[2 * (pku & 0xffff) + ((pku >> 16) <= i ? 0 : 1)] = v;
+                }
+#else
 #pragma unroll
                 for (int u = 0; u < 4; ++u) d[u] = group_sum<kScL>(d[u]);
                 if (l == 0)
 #pragma unroll
                     for (int u = 0; u < 4; ++u)
                         if (e + u < e1) T[2 * (pk[u] & 0xffff) + ((pk[u] >> 16) <= i ? 0 : 1)] = d[u];
+#endif
             }
         }
     };
