@@ -1328,56 +1328,6 @@ __device__ __forceinline__ void write_partials(double (&acc)[NV], double *__rest
 // same wave-order sums
 template <int NV>
 __device__ __forceinline__ void write_partials_nw(double (&acc)[NV], double *__restrict__ part, int slot, int nw) {
-#ifdef LRS_BFLY
-    // transposed butterfly in each 16-lane row (row_mirror, row_half_mirror, xor 2, xor 1: each
-    // step halves the values a lane holds; 15 double moves for up to 16 values instead of four a
-    // value plus the readlanes): value v's row sum ends in lane v of every row; the four rows of
-    // every wave meet in LDS and thread v adds them in (wave, row) order
-    static_assert(NV <= 16, "one value a lane of a 16-lane row");
-    __shared__ double sh[NV][32];
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, o = lane & 15;
-    double x[16];
-#pragma unroll
-    for (int v = 0; v < 16; ++v) x[v] = v < NV ? acc[v] : 0.0;
-    {
-        const bool h = (o & 8) != 0;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const double keep = h ? x[m + 8] : x[m], send = h ? x[m] : x[m + 8];
-            x[m] = keep + dpp_mov<0x140>(send);
-        }
-    }
-    {
-        const bool h = (o & 4) != 0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const double keep = h ? x[m + 4] : x[m], send = h ? x[m] : x[m + 4];
-            x[m] = keep + dpp_mov<0x141>(send);
-        }
-    }
-    {
-        const bool h = (o & 2) != 0;
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            const double keep = h ? x[m + 2] : x[m], send = h ? x[m] : x[m + 2];
-            x[m] = keep + dpp_mov<0x4E>(send);
-        }
-    }
-    {
-        const bool h = (o & 1) != 0;
-        x[0] = (h ? x[1] : x[0]) + dpp_mov<0xB1>(h ? x[0] : x[1]);
-    }
-    if (o < NV) sh[o][wid * 4 + (lane >> 4)] = x[0];
-    __syncthreads();
-    if (threadIdx.x < NV) {
-        const int v = threadIdx.x;
-        double t = 0.0;
-#pragma unroll
-        for (int q = 0; q < 32; ++q)
-            if (q < 4 * nw) t += sh[v][q];
-        part[v * kMaxPartialBlocks + slot] = t;
-    }
-#else
     __shared__ double sh[NV][8];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -1394,7 +1344,6 @@ __device__ __forceinline__ void write_partials_nw(double (&acc)[NV], double *__r
             if (w < nw) t += sh[v][w];
         part[v * kMaxPartialBlocks + slot] = t;
     }
-#endif
 }
 
 template <int NV, int NT = kBlock>
@@ -6916,12 +6865,12 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                         d[u] += rii[p].x * x[u][p].x;
                         d[u] += rii[p].y * x[u][p].y;
                     }
-#if !defined(LRS_BFLY)
+#if defined(LRS_NO_BFLY)
                     d[u] = group_sum<TPR>(d[u]);
 #endif
                 }
                 // lower entries: A(R R^T) on this row's slots (their constraints after the barrier)
-#ifdef LRS_BFLY
+#ifndef LRS_NO_BFLY
                 if constexpr (TPR == 4) {
                     const double v = group_sum4<4>(d, sl_lane);   // lane u: entry u
                     const int u = sl_lane;
@@ -7535,7 +7484,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
 #pragma unroll
                     for (int k = 0; k < EL; ++k) d[u] += xq[k] * Ys[j * rS + l + kScL * k];
                 }
-#ifdef LRS_BFLY
+#ifndef LRS_NO_BFLY
                 {
                     // entry u's total in lanes 4u..4u+3; lane 4u stores it
                     const double v = group_sum4<kScL>(d, l);
