@@ -2493,9 +2493,10 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
                 for (int q = 0; q < C_NCTRL; ++q) c[q] = cr[q];
             }
         }
-#elif defined(LRS_CTRL_LREG)
+#elif !defined(LRS_NO_CTRL_LREG)
         // the block and the parameters read back from LDS as one batch of loads (constant
-        // indices: registers), the step on registers, lane 0 writes the block back
+        // indices: registers), the step on registers, lane 0 writes the block back (k_lat_a
+        // 9.1 -> 8.95 us on G67, profiles/r04u_lat_ab.txt; LRS_NO_CTRL_LREG: on the LDS copy)
         {
             double cr[C_NCTRL], pr[P_NPAR];
 #pragma unroll
