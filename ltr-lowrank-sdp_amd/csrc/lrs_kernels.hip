@@ -6935,41 +6935,29 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         }
         __syncthreads();   // uRR of every slot before the constraints read them
         LRS_SM_T(6);
-        // single-slot constraints: A(R_new R_new^T) and their residual, a thread per slot,
-        // four of a thread's slots a batch: their records, then their b, each one memory trip
-        // for the batch (the slots in the same order as one at a time: bitwise the same sums)
-        for (int s0 = tid; s0 < A.Ptot; s0 += 4 * T) {
-            double2 l1b[4];
-            double bcb[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) l1b[u] = A.loc1[min(s0 + u * T, A.Ptot - 1)];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int c1 = (int)l1b[u].y;
-                bcb[u] = A.b[c1 >= 0 ? c1 : 0];
+        // single-slot constraints: A(R_new R_new^T) and their residual, a thread per slot
+        // software-pipelined as the slot phase: the next slot's record and this slot's b in flight
+        double2 l1nx = A.loc1[min(tid, A.Ptot - 1)];
+        for (int s = tid; s < A.Ptot; s += T) {
+            const double d = XB[s];
+            const double2 l1u = l1nx;
+            l1nx = A.loc1[min(s + T, A.Ptot - 1)];
+            const int c1 = (int)l1u.y;
+            const double bc = A.b[c1 >= 0 ? c1 : 0];
+            if (AL) A.uRR[s] = d;
+            if (c1 >= 0) {
+                const double tot = l1u.x * d, dd = bc - tot;
+                A.cvs[c1] = tot;
+                bacc[9] += dd * dd;
+                continue;
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int s = s0 + u * T;
-                if (s >= A.Ptot) break;
-                const double d = XB[s];
-                const double2 l1u = l1b[u];
-                const int c1 = (int)l1u.y;
-                if (AL) A.uRR[s] = d;
-                if (c1 >= 0) {
-                    const double tot = l1u.x * d, dd = bcb[u] - tot;
-                    A.cvs[c1] = tot;
+            if (c1 == -2)
+                for (int e = A.loc_ptr[s]; e < A.loc_ptr[s + 1]; ++e) {
+                    const int ci = A.loc_con[e];
+                    const double tot = A.loc_w[e] * d, dd = A.b[ci] - tot;
+                    A.cvs[ci] = tot;
                     bacc[9] += dd * dd;
-                    continue;
                 }
-                if (c1 == -2)
-                    for (int e = A.loc_ptr[s]; e < A.loc_ptr[s + 1]; ++e) {
-                        const int ci = A.loc_con[e];
-                        const double tot = A.loc_w[e] * d, dd = A.b[ci] - tot;
-                        A.cvs[ci] = tot;
-                        bacc[9] += dd * dd;
-                    }
-            }
         }
         // global constraints: A(R_new R_new^T) from the slots and their residual
         for (int g = wv; g < A.mg; g += T / 64) {
