@@ -1209,13 +1209,8 @@ __device__ int dev_cubic(double a, double b, double c, double d, double *res) {
     if (delta > 0) {
         const double Y1 = A * b + 1.5 * a * (-B + sqrt(delta));
         const double Y2 = A * b + 1.5 * a * (-B - sqrt(delta));
-#ifdef LRS_POW_CBRT
         const double Y13 = Y1 > 0 ? pow(Y1, 1.0 / 3) : -pow(-Y1, 1.0 / 3);
         const double Y23 = Y2 > 0 ? pow(Y2, 1.0 / 3) : -pow(-Y2, 1.0 / 3);
-#else
-        const double Y13 = Y1 > 0 ? cbrt(Y1) : -cbrt(-Y1);   // as dev_cubic_wave
-        const double Y23 = Y2 > 0 ? cbrt(Y2) : -cbrt(-Y2);
-#endif
         res[0] = fmax(res[0], (-b - Y13 - Y23) / 3 / a);
         return 1;
     }
@@ -1250,14 +1245,7 @@ __device__ __forceinline__ int dev_cubic_wave(double a, double b, double c, doub
         const double Y2 = A * b + 1.5 * a * (-B - sq);
         const double y = (threadIdx.x & 1) ? Y2 : Y1;
         const double ay = y > 0 ? y : -y;
-        // the cube root by cbrt, not the reference's pow(., 1.0 / 3) (1/3 rounded: the two differ
-        // by an ulp or two; k_lat_b 9.65 -> 9.50 us on G67, profiles/r04cbrt_ab.txt; per-trip
-        // parity against the reference's trips stays at 1e-9).  LRS_POW_CBRT: pow as the reference
-#ifdef LRS_POW_CBRT
         double r = pow(ay, 1.0 / 3);
-#else
-        double r = cbrt(ay);
-#endif
         r = y > 0 ? r : -r;
         const double Y13 = read_lane(r, 0), Y23 = read_lane(r, 1);
         res[0] = fmax(res[0], (-b - Y13 - Y23) / 3 / a);
