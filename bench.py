@@ -427,7 +427,22 @@ def spawn_ranks(n, argv):
     th.start()
     rc = 0
     live = set(range(n))
+    # an overall deadline: ranks stalled before the sharded leg's own watchdog starts (e.g. in
+    # init_process_group) end the launcher with a non-zero status instead of hanging it
+    deadline = time.time() + float(os.environ.get("LRS_BENCH_DEADLINE_S", "1500"))
     while live:
+        if time.time() > deadline:
+            print(f"bench.py launcher: ranks {sorted(live)} still running past the deadline; ending them",
+                  file=sys.stderr)
+            for q in live:
+                procs[q].terminate()
+            for q in live:
+                try:
+                    procs[q].wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    procs[q].kill()
+            rc = rc or 124
+            break
         for r in sorted(live):
             c = procs[r].poll()
             if c is None:

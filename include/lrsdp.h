@@ -23,6 +23,10 @@
  */
 #ifndef LRSDP_H
 #define LRSDP_H
+/* ABI revision, also in lrs_version()'s string.  2: lrs_op_admm_half takes (cone, side) and
+ * refreshes the cone's constraint values itself (was: the whole sweep's first half-step);
+ * lrs_op_alm_update, lrs_op_adjoint, lrs_op_auv and lrs_op_dimacs added. */
+#define LRSDP_ABI_VERSION 2
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -79,6 +83,7 @@ enum { LRS_LAMBDA = 0, LRS_CVS = 1, LRS_Q1 = 2, LRS_Q2 = 3, LRS_B = 4 };
 void lrs_params_default(lrs_params *p);
 const char *lrs_last_error(void);
 const char *lrs_version(void);
+int lrs_abi_version(void);   /* LRSDP_ABI_VERSION of the library */
 
 int lrs_ctx_create(int device, lrs_ctx **out);
 void lrs_ctx_destroy(lrs_ctx *ctx);
@@ -127,6 +132,30 @@ int lrs_op_admm_half(lrs_ctx *ctx, int cone, int side, double rho, double cg_tol
                      double *rhs);
 /* LORADSUpdateDualVar (lorads_alg_common.c:511-524): LAMBDA += rho (b - CVS). */
 int lrs_op_dual_update(lrs_ctx *ctx, double rho);
+/* The second half of one ALM inner trip after the line search (lorads_alm.c:1340-1355):
+ * setAsNegGrad (:780-801), ALMupdateVar R += tau D (:804-833), CVS += tau q1 + tau^2 q2 with the
+ * q1, q2 of the last lrs_op_q12 (:1349-1352), ALMCalGrad at rho (:74-87: G <- 2(C + A^*(M1))R,
+ * lag_norm_sq = ||G||^2) and setlbfgsHisTwo (:842-863: s = tau D, y = G_new - G_old, beta =
+ * 1/<y,s>).  The new pair lands in (LRS_S0, LRS_Y0) and the previous newest moves to (LRS_S1,
+ * LRS_Y1), the roles lrs_op_lbfgs reads, so a caller steps the reference's loop with
+ * lrs_op_lbfgs -> lrs_op_q12 -> lrs_op_line_search -> lrs_op_alm_update -> lrs_op_dimacs
+ * (updateDimacsALM).  lag_norm_sq, beta may be NULL.  Unsharded contexts. */
+int lrs_op_alm_update(lrs_ctx *ctx, double rho, double tau, double *lag_norm_sq, double *beta);
+/* sdpDataWSum + mul_rk (data/def_lorads_sdp_data.h:66-85) over every cone: out = scale (with_C C +
+ * sum_i y[i] A_i) X, X the factor `which` (LRS_R, LRS_U, ...), y[m] host, out column-major like
+ * lrs_factor_get.  Unsharded contexts. */
+int lrs_op_adjoint(lrs_ctx *ctx, const double *y, int which, double *out, double scale, int with_C);
+/* coneAUV + objAUV (data/def_lorads_sdp_conic.h:106-111) summed over the cones: out_m[i] =
+ * <A_i, sym(X_u X_v^T)> (u == v: X_u X_u^T), cobj = <C, sym(X_u X_v^T)> before the division by
+ * the reopt objective scale.  Leaves the solver state (CVS) unchanged.  out_m, cobj may be NULL.
+ * Unsharded contexts. */
+int lrs_op_auv(lrs_ctx *ctx, int u, int v, double *out_m, double *cobj);
+/* LORADSUpdateDimacsErrorALM (admm = 0, on R) / LORADSUpdateDimacsErrorADMM (admm = 1: R = (U +
+ * V)/2 first) (lorads_alg/lorads_alg_common.c:424-428, :454-462) with the objectives they read
+ * (LORADSCalObjRR_ALM lorads_alm.c:1488, LORADSCalObjUV_ADMM, LORADSCalDualObj
+ * lorads_alg_common.c:531): CVS <- A(R R^T); out5 = {pObj, dObj, l_1 primal infeasibility, l_inf
+ * primal infeasibility, |pObj - dObj| / (1 + |pObj| + |dObj|)}. */
+int lrs_op_dimacs(lrs_ctx *ctx, int admm, double *out5);
 /* Gram R^T R of cone k (r x r, row-major) */
 int lrs_op_gram(lrs_ctx *ctx, int cone, int which, double *gram);
 /* Dual infeasibility of the current multipliers (calculate_dual_infeasibility_solver,

@@ -72,8 +72,9 @@ enum ParIdx {
 };
 // ---- line-search result, double-buffered by parity: tau, rootNum, flag
 enum LsIdx { LS_TAU = 0, LS_ROOTNUM, LS_FLAG, LS_N = 4 };
-// ---- finals of the standalone launchers (g_tmpfin offsets)
+// ---- finals of the standalone launchers (offsets into the per-context tmpfin scratch)
 constexpr int kMaxCones = 256;
+constexpr int kFinN = 416;           // per-context finals of the line search / direction kernels (FinIdx)
 // TF_DOTC + k: cone k's <X, C Y> of a dense objective (op_constr_xx), read with the gather's sums
 enum TmpFinIdx {
     TF_SD = 0, TF_GATHER = 2 * kMaxCones, TF_RESID, TF_DOT, TF_DOTC, TF_SPMM = TF_DOTC + kMaxCones,
@@ -394,8 +395,8 @@ int launch_trl_sub(int n, const double *V, long ldv, int k, const double *part, 
                    int pass, double *npart, double *bw2, hipStream_t st);
 int launch_trl_restart(int n, const double *V, long ldv, int m, const double *Y, int kk, double *Vt, hipStream_t st);
 
-// per-context scratch of the standalone reductions for the calling thread (nullptr: globals)
-void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart);
+// per-context scratch of the standalone reductions for the calling thread (no module-level fallback)
+void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart, double *fin);
 // sharded solve helpers
 int launch_pack_rows(int nrows, int ld, const int *rows, const double *src, double *dst, hipStream_t st);
 // sharded: sum an m-vector's shared-constraint entries over the shards (no-op otherwise)

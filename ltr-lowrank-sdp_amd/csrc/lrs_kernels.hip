@@ -32,9 +32,9 @@ static thread_local char g_err[512] = "";
 
 // Optional in-kernel phase timestamps (block 0, thread 0; s_memrealtime, 100 MHz):
 // built only into the diagnostics library (make timing -> liblrsdp_timing.so).
+#ifdef LRS_PHASE_TIMING
 __device__ unsigned long long g_phase[4][16];
 __device__ unsigned long long g_phase_tmp[4][16];
-#ifdef LRS_PHASE_TIMING
 #define LRS_TS(k, p)                                                                  \
     do {                                                                              \
         if (blockIdx.x == 0 && threadIdx.x == 0) g_phase_tmp[k][p] = wall_clock64();  \
@@ -313,10 +313,11 @@ static inline int grid_elems(long n, int per_thread) {
 }
 
 // ------------------------------------------------------------------------
-// Scratch for tickets / finals (module-level device memory)
+// Tickets / finals of the standalone reductions: per-context device scratch (lrs_ctx
+// s_tickets / s_tmpfin / s_fin / s_rpart), bound to the calling thread by bind_scratch --
+// no module-level device state, so contexts on several host threads never share it
 // ------------------------------------------------------------------------
 enum TicketId { T_SDDMM = 0, T_GATHER, T_SPMM, T_DOT, T_GRAD, T_RR, T_Q, T_NT = 16 };
-__device__ unsigned g_tickets[64];
 
 // ------------------------------------------------------------------------
 // SDDMM over the lower pattern (row-owned).  MODE 0: sym(X Y^T); MODE 1: X X^T;
@@ -1041,12 +1042,12 @@ struct AlmFinal {            // finals produced inside one iteration (device mem
 //   FIN_Q   .. +5 : gather_q dots
 //   FIN_GR  + 9*k : grad dots of cone k
 //   FIN_RR        : residual
+// (FIN_N: lrs_device.h kFinN, the per-context buffer's size)
 enum FinIdx { FIN_SD = 0, FIN_Q = 64, FIN_GR = 80, FIN_RR = 400, FIN_N = 416 };
-__device__ double g_fin[FIN_N];
-__device__ double g_tmpfin[TF_N];
+static_assert(FIN_N == kFinN, "finals layout");
 
 __device__ int ctrl_compute(double *c, const double *__restrict__ prev, const double *__restrict__ par,
-                            const double *__restrict__ lsprev, int K) {
+                            const double *__restrict__ lsprev, int K, const double *__restrict__ fin) {
     // executed by thread 0 only; c is shared memory.
     // PENDING: 0 = nothing to fold (host start: clear == 0), 1 = fold the previous
     // iteration's finals, 2 = dots already stashed in C_DSG..C_DYOY.
@@ -1064,7 +1065,7 @@ __device__ int ctrl_compute(double *c, const double *__restrict__ prev, const do
         } else {
             double d[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             for (int k = 0; k < K; ++k)
-                for (int q = 0; q < 9; ++q) d[q] += g_fin[FIN_GR + 9 * k + q];
+                for (int q = 0; q < 9; ++q) d[q] += fin[FIN_GR + 9 * k + q];
             const int h = (int)c[C_HEAD];
             // setlbfgsHisTwo (lorads_alm.c:861): beta = 1/<y,s>; ring head advances (:862)
             c[C_BETA0 + h] = 1.0 / d[1];
@@ -1074,7 +1075,7 @@ __device__ int ctrl_compute(double *c, const double *__restrict__ prev, const do
             c[C_LAG] = d[0];
             c[C_LASTTAU] = lsprev[LS_TAU];
             // primalInfeasibility (lorads_alg_common.c:393) and l_inf (lorads_alm.c:1359)
-            const double pinf1 = sqrt(g_fin[FIN_RR]) / (1.0 + par[P_BN1]);
+            const double pinf1 = sqrt(fin[FIN_RR]) / (1.0 + par[P_BN1]);
             c[C_PINF1] = pinf1;
             c[C_PINFINF] = pinf1 * (1.0 + par[P_BN1]) / (1.0 + par[P_BNINF]);
             c[C_DSG] = d[3]; c[C_DYG] = d[4]; c[C_DSOG] = d[5]; c[C_DYOG] = d[6];
@@ -1141,9 +1142,9 @@ __global__ void __launch_bounds__(kBlock) k_alm_dir(long NR, const double *__res
                                                     double *__restrict__ D, const double *__restrict__ G0,
                                                     const double *__restrict__ G1, const double *__restrict__ s0,
                                                     const double *__restrict__ y0, const double *__restrict__ s1,
-                                                    const double *__restrict__ y1) {
+                                                    const double *__restrict__ y1, const double *__restrict__ fin) {
     __shared__ double c[C_NCTRL];
-    if (threadIdx.x == 0) ctrl_compute(c, ctrl_prev, par, lsprev, K);
+    if (threadIdx.x == 0) ctrl_compute(c, ctrl_prev, par, lsprev, K, fin);
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x < C_NCTRL) ctrl_cur[threadIdx.x] = c[threadIdx.x];
     if (c[C_ACTIVE] == 0.0) return;
@@ -1278,11 +1279,11 @@ __device__ __forceinline__ double quartic(double a, double b, double c, double d
 
 // ALMLineSearch (lorads_alm.c:266-333) from the finals; writes ls[0..2]
 __device__ void line_search_v(const double *__restrict__ par, double p1, double p2, const double *dots, double *ls);
-__device__ void line_search(const double *__restrict__ par, int K, double *ls) {
+__device__ void line_search(const double *__restrict__ par, int K, const double *__restrict__ fin, double *ls) {
     double p1 = 0.0, p2 = 0.0;
-    for (int k = 0; k < K; ++k) { p1 += g_fin[FIN_SD + 2 * k]; p2 += g_fin[FIN_SD + 2 * k + 1]; }
+    for (int k = 0; k < K; ++k) { p1 += fin[FIN_SD + 2 * k]; p2 += fin[FIN_SD + 2 * k + 1]; }
     double dots[5];
-    for (int q = 0; q < 5; ++q) dots[q] = g_fin[FIN_Q + q];
+    for (int q = 0; q < 5; ++q) dots[q] = fin[FIN_Q + q];
     line_search_v(par, p1, p2, dots, ls);
 }
 // ------------------------------------------------------------------------
@@ -4888,33 +4889,22 @@ __global__ void __launch_bounds__(kBlock) k_cg_resid2(long nr, const double *__r
 // ------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------
-// Per-context scratch of the standalone reductions (tickets, finals, residual partials),
-// bound to the calling thread by the context (several contexts may run concurrently in
-// one process, e.g. the shards of the loopback transport); unbound: the module globals.
+// Per-context scratch of the standalone reductions (tickets, finals, the line search's and
+// the fused direction kernel's finals, residual partials), bound to the calling thread by
+// the context's every C-ABI entry (several contexts may run concurrently in one process,
+// e.g. the shards of the loopback transport, or two solves on two host threads).  There is
+// no module-level fallback: the launchers only run inside a bound entry point.
 static thread_local unsigned *t_tickets = nullptr;
-static thread_local double *t_tmpfin = nullptr, *t_rpart = nullptr;
-void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart) {
+static thread_local double *t_tmpfin = nullptr, *t_rpart = nullptr, *t_fin = nullptr;
+void bind_scratch(unsigned *tickets, double *tmpfin, double *rpart, double *fin) {
     t_tickets = tickets;
     t_tmpfin = tmpfin;
     t_rpart = rpart;
+    t_fin = fin;
 }
-static unsigned *ticket_ptr(int id) {
-    if (t_tickets) return t_tickets + id;
-    unsigned *p = nullptr;
-    (void)hipGetSymbolAddress((void **)&p, HIP_SYMBOL(g_tickets));
-    return p + id;
-}
-static double *fin_ptr() {
-    double *p = nullptr;
-    (void)hipGetSymbolAddress((void **)&p, HIP_SYMBOL(g_fin));
-    return p;
-}
-static double *tmpfin_ptr() {
-    if (t_tmpfin) return t_tmpfin;
-    double *p = nullptr;
-    (void)hipGetSymbolAddress((void **)&p, HIP_SYMBOL(g_tmpfin));
-    return p;
-}
+static unsigned *ticket_ptr(int id) { return t_tickets + id; }
+static double *fin_ptr() { return t_fin; }
+static double *tmpfin_ptr() { return t_tmpfin; }
 double *device_tmpfin() { return tmpfin_ptr(); }
 double *device_fin() { return fin_ptr(); }
 
@@ -6644,9 +6634,11 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         // software-pipelined: the next slot's records and this slot's single constraint's
         // values are in flight while this slot's dots run on LDS (one memory trip a slot, not
         // two); loads clamped, not branched
-        int2 ijn = A.slot_g[min(tid, A.Ptot - 1)];
-        double cwn = A.Cw[min(tid, A.Ptot - 1)];
-        double2 l1n = A.loc1[min(tid, A.Ptot - 1)];
+        // (Ptot == 0: index 0 of the >= 1-element arrays, never used -- the loop does not run)
+        const int s0c = max(0, min(tid, A.Ptot - 1));
+        int2 ijn = A.slot_g[s0c];
+        double cwn = A.Cw[s0c];
+        double2 l1n = A.loc1[s0c];
         for (int s = tid; s < A.Ptot; s += T) {
             const int2 ij = ijn;
             const double cw = cwn;
@@ -6937,7 +6929,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         LRS_SM_T(6);
         // single-slot constraints: A(R_new R_new^T) and their residual, a thread per slot
         // software-pipelined as the slot phase: the next slot's record and this slot's b in flight
-        double2 l1nx = A.loc1[min(tid, A.Ptot - 1)];
+        double2 l1nx = A.loc1[max(0, min(tid, A.Ptot - 1))];
         for (int s = tid; s < A.Ptot; s += T) {
             const double d = XB[s];
             const double2 l1u = l1nx;
@@ -7172,19 +7164,19 @@ __global__ void __launch_bounds__(kBlock) k_admm_m1(int m, double rho, const dou
         M1[i] = v + (-1.0) * lam[i];
     }
 }
-__global__ void k_ls_only(const double *__restrict__ par, int K, double *__restrict__ lsout) {
+__global__ void k_ls_only(const double *__restrict__ par, int K, const double *__restrict__ fin,
+                          double *__restrict__ lsout) {
     __shared__ double ls[LS_N];
-    if (threadIdx.x == 0) line_search(par, K, ls);
+    if (threadIdx.x == 0) line_search(par, K, fin, ls);
     __syncthreads();
     if (threadIdx.x < LS_N) lsout[threadIdx.x] = ls[threadIdx.x];
 }
 
 int launch_resid(int m, const double *b, const double *x, hipStream_t st, const double *mask) {
-    static double *gpart = nullptr;
     double *part = t_rpart;
     if (!part) {
-        if (!gpart && hipMalloc((void **)&gpart, sizeof(double) * kMaxPartialBlocks) != hipSuccess) return -1;
-        part = gpart;
+        snprintf(g_err, sizeof(g_err), "launch_resid: no context scratch bound");
+        return -1;
     }
     hipLaunchKernelGGL(k_resid, dim3(grid_elems(m, 1)), dim3(kBlock), 0, st, m, b, x, mask, part, ticket_ptr(T_RR + 40),
                        tmpfin_ptr() + TF_RESID);
@@ -7212,7 +7204,7 @@ int launch_ls_only(const DevProblem &P, DevWork &W, hipStream_t st) {
                        P.con_slot, P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, W.q1, W.q2, W.partB,
                        ticket_ptr(T_Q), fin + FIN_Q, W.ctrl);
     LRS_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_ls_only, dim3(1), dim3(64), 0, st, W.par, P.K, W.lsres);
+    hipLaunchKernelGGL(k_ls_only, dim3(1), dim3(64), 0, st, W.par, P.K, fin, W.lsres);
     LRS_CHECK_LAUNCH();
     return 0;
 }
@@ -7220,7 +7212,7 @@ int launch_ls_only(const DevProblem &P, DevWork &W, hipStream_t st) {
 int launch_alm_dir_only(const DevProblem &P, DevWork &W, hipStream_t st) {
     hipLaunchKernelGGL(k_alm_dir, dim3(grid_elems(P.NRpad, 2)), dim3(kBlock), 0, st, P.NRpad, W.par,
                        W.ctrl + C_NCTRL, W.ctrl, W.lsres + LS_N, P.K, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0],
-                       W.ls[1], W.ly[1]);
+                       W.ls[1], W.ly[1], fin_ptr());
     LRS_CHECK_LAUNCH();
     return 0;
 }
@@ -7368,7 +7360,9 @@ __device__ __forceinline__ void sc_row_apply(int e0, int e1, const int *cadj, co
         for (int u = 0; u < 4; ++u) {
             sv[u] = T[pk[u] & 0xffff];
 #pragma unroll
-            for (int k = 0; k < EL; ++k) y[u][k] = Ys[(pk[u] >> 16) * rS + l + kScL * k];   // unconditional (selects below)
+            // unconditional (selects below); columns past the row pitch clamped into the row, whose
+            // words are finite (Y or the zeroed pad), so a masked column adds 0 * finite = +-0
+            for (int k = 0; k < EL; ++k) y[u][k] = Ys[(pk[u] >> 16) * rS + min(l + kScL * k, rS - 1)];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -7476,14 +7470,15 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
                 for (int u = 0; u < 4; ++u) pk[u] = cadj[min(e + u, e1 - 1)];
                 // no branch around a load (the compiler sinks a load into its branch and then
                 // waits for it before the next one issues: eight serial LDS round trips a pass):
-                // columns past r hold x = 0 exactly and read the zeroed pad or the next row's
-                // finite words, so their products are +-0
+                // columns past r hold x = 0 exactly and read the zeroed pad, or (past the row
+                // pitch) are clamped into the row: finite words, so their products are +-0 (an
+                // unclamped read past the last row would reach wv / T, not yet written)
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int j = pk[u] >> 16;
                     d[u] = 0.0;
 #pragma unroll
-                    for (int k = 0; k < EL; ++k) d[u] += xq[k] * Ys[j * rS + l + kScL * k];
+                    for (int k = 0; k < EL; ++k) d[u] += xq[k] * Ys[j * rS + min(l + kScL * k, rS - 1)];
                 }
 #ifndef LRS_NO_BFLY
                 {

@@ -31,7 +31,6 @@
 #include "lrs_problem.h"
 
 namespace lrs {
-double *device_fin();
 double *device_tmpfin();
 int launch_gather_cone(const DevProblem &P, int cone, const double *uvt, double *out, hipStream_t st);
 int launch_resid(int m, const double *b, const double *x, hipStream_t st, const double *mask = nullptr);
@@ -111,6 +110,21 @@ struct AdmmState {
     double rho = 0, pobj = 1e30, dobj = 1e30, pinf1 = 1e30, pinfinf = 1e30, gap = 1e30;
 };
 
+// Pinned host scratch (lrs_ctx::hpin), one region per user, so that reads staged behind one
+// sync never overlap: standalone reads (read_tmpfin, lrs_time_stages), the two ALM control
+// mirrors, the device CG's control-block poll, the CG total read behind admm_eval's sync, the
+// line search of the generic L-BFGS loop, and read_tmpfin2's several ranges.
+enum HpinSlot {
+    kHpRead = 0, kHpReadN = 128,
+    kHpCtrl = 128,          // 2 x 64: [128, 256)
+    kHpCg = 256,            // CG_N (8)
+    kHpCgTotal = 300,       // 1
+    kHpLs = 512,            // LS_N (4)
+    kHpRead2 = 1024, kHpRead2N = 1024,
+    kHpinN = 4096
+};
+static_assert(CG_N <= kHpCgTotal - kHpCg && 2 * 64 <= kHpCg - kHpCtrl && LS_N <= kHpRead2 - kHpLs, "pinned layout");
+
 struct lrs_ctx {
     int device = 0;
     hipStream_t st = nullptr;
@@ -121,7 +135,7 @@ struct lrs_ctx {
     std::vector<Layout> lay;
     DevWork W;
     bool walloc = false;
-    double *hpin = nullptr;     // pinned scalars
+    double *hpin = nullptr;     // pinned scalars (layout: HpinSlot)
     // L-BFGS mirror
     int head = 0, gcur = 0;
     double beta[2] = {0, 0}, yy[2] = {0, 0};
@@ -177,7 +191,7 @@ struct lrs_ctx {
     bool c_scaled = false;
     // per-context scratch of the standalone reductions (bound to the calling thread)
     unsigned *s_tickets = nullptr;
-    double *s_tmpfin = nullptr, *s_rpart = nullptr;
+    double *s_tmpfin = nullptr, *s_rpart = nullptr, *s_fin = nullptr;
     // sharded solve (lrs_shard_*): this process's rows, the transport, the stage hooks
     struct ShardComm *comm = nullptr;
     ShardPlan plan;
@@ -260,11 +274,25 @@ static int pack_send_vec(lrs_ctx *c, int k, const double *x, hipStream_t st) {
     return 0;
 }
 
+#define LRS_STR_(x) #x
+#define LRS_STR(x) LRS_STR_(x)
 #define NCCLC(x)                                                                            \
     do {                                                                                    \
         ncclResult_t r_ = (x);                                                              \
         if (r_ != ncclSuccess) {                                                            \
             set_err("%s:%d %s: %s", __FILE__, __LINE__, #x, ncclGetErrorString(r_));        \
+            return -1;                                                                      \
+        }                                                                                   \
+    } while (0)
+
+// inside ncclGroupStart / ncclGroupEnd: an error closes the group before returning, so the
+// communicator is left usable (no dangling group on this thread)
+#define NCCLG(x)                                                                            \
+    do {                                                                                    \
+        ncclResult_t r_ = (x);                                                              \
+        if (r_ != ncclSuccess) {                                                            \
+            set_err("%s:%d %s: %s", __FILE__, __LINE__, #x, ncclGetErrorString(r_));        \
+            (void)ncclGroupEnd();                                                           \
             return -1;                                                                      \
         }                                                                                   \
     } while (0)
@@ -306,10 +334,10 @@ struct RcclComm : ShardComm {
                 const int ld = dc.ld;
                 const int ns = cp.send_ptr[q + 1] - cp.send_ptr[q];
                 if (ns > 0)
-                    NCCLC(ncclSend(c->d_sendbuf + send_base(pl, c->dp, k) + (long)cp.send_ptr[q] * ld, (size_t)ns * ld,
+                    NCCLG(ncclSend(c->d_sendbuf + send_base(pl, c->dp, k) + (long)cp.send_ptr[q] * ld, (size_t)ns * ld,
                                    ncclDouble, q, comm, st));
                 if (cp.recv_cnt[q] > 0)
-                    NCCLC(ncclRecv(D + dc.foff + (long)cp.recv_start[q] * ld, (size_t)cp.recv_cnt[q] * ld, ncclDouble, q,
+                    NCCLG(ncclRecv(D + dc.foff + (long)cp.recv_start[q] * ld, (size_t)cp.recv_cnt[q] * ld, ncclDouble, q,
                                    comm, st));
             }
         NCCLC(ncclGroupEnd());
@@ -321,8 +349,8 @@ struct RcclComm : ShardComm {
         NCCLC(ncclGroupStart());
         for (int q = 0; q < c->plan.world; ++q) {
             const int ns = cp.send_ptr[q + 1] - cp.send_ptr[q];
-            if (ns > 0) NCCLC(ncclSend(c->d_sendvec + cp.send_ptr[q], (size_t)ns, ncclDouble, q, comm, st));
-            if (cp.recv_cnt[q] > 0) NCCLC(ncclRecv(x + cp.recv_start[q], (size_t)cp.recv_cnt[q], ncclDouble, q, comm, st));
+            if (ns > 0) NCCLG(ncclSend(c->d_sendvec + cp.send_ptr[q], (size_t)ns, ncclDouble, q, comm, st));
+            if (cp.recv_cnt[q] > 0) NCCLG(ncclRecv(x + cp.recv_start[q], (size_t)cp.recv_cnt[q], ncclDouble, q, comm, st));
         }
         NCCLC(ncclGroupEnd());
         return 0;
@@ -445,7 +473,7 @@ static int hook_allreduce(void *self, double *buf, int n, hipStream_t st) {
 // this context's device, stream-free scratch bound to the calling thread
 static void bind(lrs_ctx *c) {
     (void)hipSetDevice(c->device);
-    bind_scratch(c->s_tickets, c->s_tmpfin, c->s_rpart);
+    bind_scratch(c->s_tickets, c->s_tmpfin, c->s_rpart, c->s_fin);
 }
 
 static void free_lz(lrs_ctx::LzWork &w) {
@@ -658,19 +686,23 @@ static double *vec_ptr(lrs_ctx *c, int which) {
     return nullptr;
 }
 
+static int read_tmpfin2(lrs_ctx *c, int idx1, int n1, int idx2, int n2, double *out);
 static int read_tmpfin(lrs_ctx *c, int idx, int n, double *out) {
-    HIPC(hipMemcpyAsync(c->hpin, device_tmpfin() + idx, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
+    if (n > kHpReadN) return read_tmpfin2(c, idx, n, 0, 0, out);
+    double *h = c->hpin + kHpRead;
+    HIPC(hipMemcpyAsync(h, device_tmpfin() + idx, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
     HIPC(hipStreamSynchronize(c->st));
-    for (int i = 0; i < n; ++i) out[i] = c->hpin[i];
+    for (int i = 0; i < n; ++i) out[i] = h[i];
     // sharded: every standalone reduction is a sum over the shard's rows / constraints
     if (sharded(c)) return c->comm->allreduce_host(c, out, n);
     return 0;
 }
 
-// several tmpfin ranges behind one stream sync (staged at hpin + 1024, clear of the
+// several tmpfin ranges behind one stream sync (staged at hpin + kHpRead2, clear of the
 // ALM mirror slots and the CG poll): out = [idx1, idx1 + n1) ++ [idx2, idx2 + n2)
 static int read_tmpfin2(lrs_ctx *c, int idx1, int n1, int idx2, int n2, double *out) {
-    double *h = c->hpin + 1024;
+    if (n1 + n2 > kHpRead2N) { set_err("read_tmpfin2: %d values past the %d staged", n1 + n2, kHpRead2N); return -1; }
+    double *h = c->hpin + kHpRead2;
     HIPC(hipMemcpyAsync(h, device_tmpfin() + idx1, sizeof(double) * n1, hipMemcpyDeviceToHost, c->st));
     if (n2 > 0)
         HIPC(hipMemcpyAsync(h + n1, device_tmpfin() + idx2, sizeof(double) * n2, hipMemcpyDeviceToHost, c->st));
@@ -1457,17 +1489,17 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     certain = std::max(0L, certain) + 1;
     auto even_clamp = [](long v) { v = std::max(4L, std::min(64L, v)); return (int)(v + (v & 1)); };
     int B = even_clamp((long)(c->inner_est * 0.5));
-    double *res = c->hpin + 128;
+    double *res = c->hpin + kHpCtrl;
     const double t_in = c->stats ? now_s() : 0.0;
     long enq = 0;
     // the single-workgroup inner loop (small problems): the whole call is one launch
     const bool small = !c->prof && use_small(c);
     if (small) {
         OPC(launch_small_alm(c->dp, c->W, c->W.ctrl + C_NCTRL, c->W.ctrl + C_NCTRL, c->W.lsres, c->st));
-        HIPC(hipMemcpyAsync(c->hpin + 128, c->W.ctrl + C_NCTRL, sizeof(double) * C_NCTRL, hipMemcpyDeviceToHost,
+        HIPC(hipMemcpyAsync(c->hpin + kHpCtrl, c->W.ctrl + C_NCTRL, sizeof(double) * C_NCTRL, hipMemcpyDeviceToHost,
                             c->st));
         HIPC(hipStreamSynchronize(c->st));
-        res = c->hpin + 128;
+        res = c->hpin + kHpCtrl;
         enq = std::max(0L, (long)res[C_INNER] - io.inner);
         c->dp.last_path = 4;
         if (c->stats) c->st_batches++;
@@ -1496,7 +1528,7 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
                 hipGraphExec_t ge;
                 if (get_batch_graph(c, Bk, &ge)) return -1;
                 HIPC(hipGraphLaunch(ge, c->st));
-                HIPC(hipMemcpyAsync(c->hpin + 128 + 64 * (k & 1), c->W.ctrl + C_NCTRL, sizeof(double) * C_NCTRL,
+                HIPC(hipMemcpyAsync(c->hpin + kHpCtrl + 64 * (k & 1), c->W.ctrl + C_NCTRL, sizeof(double) * C_NCTRL,
                                     hipMemcpyDeviceToHost, c->st));
                 HIPC(hipEventRecord(c->bev[k & 1], c->st));
             } else {
@@ -1541,11 +1573,11 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
                     }
                 }
                 std::atomic_thread_fence(std::memory_order_acquire);
-                for (int q = 0; q < C_NCTRL; ++q) c->hpin[128 + 64 * (kw & 1) + q] = slot[q];
+                for (int q = 0; q < C_NCTRL; ++q) c->hpin[kHpCtrl + 64 * (kw & 1) + q] = slot[q];
             } else {
                 HIPC(hipEventSynchronize(c->bev[kw & 1]));
             }
-            res = c->hpin + 128 + 64 * (kw & 1);
+            res = c->hpin + kHpCtrl + 64 * (kw & 1);
             ++kw;
             if (res[C_ACT2] == 0.0) break;
             if (kw == k) {   // still active past the certain exits (cannot happen): keep going
@@ -1660,7 +1692,7 @@ static int op_q12_fin(lrs_ctx *c, double *p1h, double *p2h) {
     }
     OPC(launch_gather(P, W.uvt0, 2.0, W.q1, nullptr, nullptr, c->st, nullptr));
     OPC(launch_gather(P, W.uvt1, 1.0, W.q2, nullptr, nullptr, c->st, nullptr));
-    double *fin = device_fin();
+    double *fin = c->s_fin;   // this context's finals (the line search reads them)
     double h[64] = {0};
     h[0] = a; h[1] = b;
     HIPC(h2d_sync(c, fin, h, sizeof(double) * 2 * std::max(1, std::min(P.K, 32))));
@@ -1673,7 +1705,7 @@ static int run_inner_generic(lrs_ctx *c, const lrs_params *p, double rho, double
     DevProblem &P = c->dp;
     DevWork &W = c->W;
     const int L = p->lbfgsListLength;
-    if (sharded(c)) { set_err("lbfgsListLength %d: not supported in a sharded solve", L); return -1; }
+    if (sharded(c)) { set_err("lbfgsListLength %d: not supported in a sharded solve", L); return -1; }   // (solve_impl refuses first)
     if (ring_alloc(c, L)) return -1;
     const long NR = P.NRpad;
     double par[P_NPAR] = {0};
@@ -1716,9 +1748,9 @@ static int run_inner_generic(lrs_ctx *c, const lrs_params *p, double rho, double
         if (op_q12_fin(c, &p1, &p2)) return -1;
         OPC(launch_ls_only(P, W, c->st));
         double ls[LS_N];
-        HIPC(hipMemcpyAsync(c->hpin + 512, W.lsres, sizeof(ls), hipMemcpyDeviceToHost, c->st));
+        HIPC(hipMemcpyAsync(c->hpin + kHpLs, W.lsres, sizeof(ls), hipMemcpyDeviceToHost, c->st));
         HIPC(hipStreamSynchronize(c->st));
-        memcpy(ls, c->hpin + 512, sizeof(ls));
+        memcpy(ls, c->hpin + kHpLs, sizeof(ls));
         const double tau = ls[LS_TAU];
         if (ls[LS_ROOTNUM] == 0) { exitr = EXIT_NUMERR; break; }
         if (std::fabs(tau) < p->endTauTol) {
@@ -1985,7 +2017,7 @@ static int cg_solve(lrs_ctx *c, int k, const double *Y, double *X, const double 
     OPC(launch_cg_resid(nr, bk, Q, r, p, W.partC, cgc, pA, nA, 1, c->st, &nC));
     if (sum(W.partC, nC)) return -1;
     OPC(launch_cg_resid2(nr, r, p, pC, nC, cgc, tol, 0, 1, c->st));
-    double *h = c->hpin + 256;
+    double *h = c->hpin + kHpCg;
     // first batch sized from this cone's previous solve (ADMM's CG solves take a handful of
     // iterations each; the batch past convergence runs guarded no-op launches), then doubling
     const long prev = c->cgIterCone[k];
@@ -2071,7 +2103,6 @@ static int admm_init_constr(lrs_ctx *c) {
 // with V fixed, 1 V with U fixed, then the cone's constraint refresh.  Small unsharded cones take
 // the single-workgroup kernel (lrs_kernels.hip k_small_cg: RHS, CG and refresh in one launch, its
 // iterations counted on the device in W.cgc[CG_TOTAL]); LRS_SMALL_CG=0 keeps the multi-launch CG.
-constexpr int kHpinCgTotal = 300;   // pinned slot of the device CG count
 static bool use_small_cg(lrs_ctx *c, int k) {
     const char *e = getenv("LRS_SMALL_CG");
     const int env = e ? atoi(e) : -1;
@@ -2098,7 +2129,7 @@ static int admm_update_var(lrs_ctx *c, double rho, double tol, int maxit) {
         }
     // the device-counted CG iterations, read behind the next stream sync (admm_eval's)
     if (dev)
-        HIPC(hipMemcpyAsync(c->hpin + kHpinCgTotal, c->W.cgc + CG_TOTAL, sizeof(double), hipMemcpyDeviceToHost, c->st));
+        HIPC(hipMemcpyAsync(c->hpin + kHpCgTotal, c->W.cgc + CG_TOTAL, sizeof(double), hipMemcpyDeviceToHost, c->st));
     c->cg_dev_total = dev;
     return 0;
 }
@@ -2154,7 +2185,7 @@ static int admm_optimize(lrs_ctx *c, lrs_params *p, AdmmState &st, long ceiling,
         const double cgtol = std::min(st.pinf1 * (reopt ? 1e-4 : 1e-2), 1e-8);
         if (admm_update_var(c, st.rho, cgtol, maxCG)) return -1;
         if (admm_eval(c)) return -1;
-        st.cg_iter = c->cgIterTotal + (c->cg_dev_total ? (long)c->hpin[kHpinCgTotal] : 0);
+        st.cg_iter = c->cgIterTotal + (c->cg_dev_total ? (long)c->hpin[kHpCgTotal] : 0);
         st.pobj = c->pObjVal; st.dobj = c->dObjVal; st.pinf1 = c->dimPinf;
         st.pinfinf = st.pinf1 * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
         st.gap = c->dimGap;
@@ -2436,7 +2467,8 @@ void lrs_params_default(lrs_params *p) {   // main.c:56-86
 }
 
 const char *lrs_last_error(void) { return g_lrs_err.c_str(); }
-const char *lrs_version(void) { return "lrsdp-mi355x 0.1 (gfx950)"; }
+const char *lrs_version(void) { return "lrsdp-mi355x 0.5 (abi " LRS_STR(LRSDP_ABI_VERSION) ", gfx950)"; }
+int lrs_abi_version(void) { return LRSDP_ABI_VERSION; }
 
 int lrs_ctx_create(int device, lrs_ctx **out) {
     LRS_NEED_ARG(out);
@@ -2449,11 +2481,13 @@ int lrs_ctx_create(int device, lrs_ctx **out) {
     if (const char *sv = getenv("LRS_STATS")) c->stats = (atoi(sv) != 0);
     if (const char *cs = getenv("LRS_CG_SLACK")) c->cg_slack = std::max(0, std::min(8, atoi(cs)));
     if (const char *pb = getenv("LRS_PIPE_BATCH")) c->pipe_batch = std::max(2, std::min(64, (atoi(pb) + 1) & ~1));
-    if (hipHostMalloc((void **)&c->hpin, 4096 * sizeof(double), 0) != hipSuccess) { set_err("pinned alloc failed"); delete c; return -1; }
+    if (hipHostMalloc((void **)&c->hpin, kHpinN * sizeof(double), 0) != hipSuccess) { set_err("pinned alloc failed"); delete c; return -1; }
     if (hipMalloc((void **)&c->s_tickets, 64 * sizeof(unsigned)) != hipSuccess ||
         hipMemset(c->s_tickets, 0, 64 * sizeof(unsigned)) != hipSuccess ||
         hipMalloc((void **)&c->s_tmpfin, TF_N * sizeof(double)) != hipSuccess ||
-        hipMalloc((void **)&c->s_rpart, kMaxPartialBlocks * sizeof(double)) != hipSuccess) {
+        hipMalloc((void **)&c->s_rpart, kMaxPartialBlocks * sizeof(double)) != hipSuccess ||
+        hipMalloc((void **)&c->s_fin, kFinN * sizeof(double)) != hipSuccess ||
+        hipMemset(c->s_fin, 0, kFinN * sizeof(double)) != hipSuccess) {
         set_err("scratch alloc failed");
         lrs_ctx_destroy(c);
         return -1;
@@ -2509,12 +2543,12 @@ void lrs_ctx_destroy(lrs_ctx *c) {
     for (auto &e : c->bev)
         if (e) (void)hipEventDestroy(e);
     delete c->comm;
-    for (void *q : {(void *)c->s_tickets, (void *)c->s_tmpfin, (void *)c->s_rpart, (void *)c->d_sendbuf,
+    for (void *q : {(void *)c->s_tickets, (void *)c->s_tmpfin, (void *)c->s_rpart, (void *)c->s_fin, (void *)c->d_sendbuf,
                     (void *)c->d_sendvec, (void *)c->Cw0, (void *)c->Craw0})
         if (q) (void)hipFree(q);
     for (int *q : c->d_send_rows)
         if (q) (void)hipFree(q);
-    bind_scratch(nullptr, nullptr, nullptr);
+    bind_scratch(nullptr, nullptr, nullptr, nullptr);
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
 }
@@ -2820,6 +2854,119 @@ int lrs_op_dual_update(lrs_ctx *c, double rho) {
     return 0;
 }
 
+// The host-stepped ALM trip's second half (lorads_alm.c:1340-1355): setAsNegGrad (:780-801),
+// ALMupdateVar (:804-833), constrValSum += tau ARDSum + tau^2 ADDSum (:1349-1352), ALMCalGrad
+// (:74-87) into the other gradient buffer and setlbfgsHisTwo (:842-863).  The ring keeps
+// lrs_op_lbfgs's convention: the new pair goes to (S0, Y0), the previous newest to (S1, Y1).
+int lrs_op_alm_update(lrs_ctx *c, double rho, double tau, double *lag_norm_sq, double *beta) {
+    LRS_NEED_STATE(c);
+    if (sharded(c)) { set_err("lrs_op_alm_update: unsharded contexts only (the ring's dots span whole buffers)"); return -1; }
+    if (!(rho > 0.0)) { set_err("lrs_op_alm_update: rho %g", rho); return -1; }
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    const long NR = P.NRpad;
+    HIPC(hipMemcpyAsync(W.ls[1], W.ls[0], sizeof(double) * NR, hipMemcpyDeviceToDevice, c->st));
+    HIPC(hipMemcpyAsync(W.ly[1], W.ly[0], sizeof(double) * NR, hipMemcpyDeviceToDevice, c->st));
+    OPC(launch_axpby(NR, -1.0, W.G[c->gcur], 0.0, W.ly[0], c->st));   // y = -G
+    OPC(launch_axpby(NR, tau, W.D, 1.0, W.R, c->st));                 // R += tau D
+    OPC(launch_axpby(P.m, tau, W.q1, 1.0, W.cvs, c->st));
+    OPC(launch_axpby(P.m, tau * tau, W.q2, 1.0, W.cvs, c->st));
+    c->gcur ^= 1;
+    double lag;
+    if (op_grad(c, rho, &lag)) return -1;
+    OPC(launch_axpby(NR, tau, W.D, 0.0, W.ls[0], c->st));             // s = tau D
+    OPC(launch_axpby(NR, 1.0, W.G[c->gcur], 1.0, W.ly[0], c->st));    // y += G_new
+    double ys;
+    if (op_dot(c, NR, W.ly[0], W.ls[0], &ys)) return -1;
+    if (lag_norm_sq) *lag_norm_sq = lag;
+    if (beta) *beta = 1.0 / ys;
+    return 0;
+}
+
+// sdpDataWSum + mul_rk (data/def_lorads_sdp_data.h:66-85) over every cone: out = scale (with_C C
+// + sum_i y_i A_i) X with X the factor `which` (the ADMM right-hand side's S Y, ALMCalGrad's S R)
+int lrs_op_adjoint(lrs_ctx *c, const double *y, int which, double *out, double scale, int with_C) {
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(y);
+    LRS_NEED_ARG(out);
+    if (sharded(c)) { set_err("lrs_op_adjoint: unsharded contexts only"); return -1; }
+    const double *X = factor_ptr(c, which);
+    if (!X) { set_err("lrs_op_adjoint: bad factor id %d", which); return -1; }
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    HIPC(h2d_sync(c, W.M1, y, sizeof(double) * P.m));
+    OPC(launch_wsum(P, W.M1, with_C ? 1 : 0, W.S, c->st));
+    for (int k = 0; k < P.K; ++k)
+        OPC(launch_spmm(P, k, W.S, X, scale, nullptr, 0.0, W.X, W.part, 0, nullptr, c->st));
+    for (int k = 0; k < P.K && with_C; ++k) {
+        const DevCone &dc = P.cones[k];
+        if (!dc.dense_c) continue;   // a dense objective is not on the slots: + scale C X
+        OPC(launch_dense_cx(P, k, X, W.cg_Q, 0.0, c->st));
+        OPC(launch_axpby((long)dc.n * dc.ld, scale, W.cg_Q + dc.foff, 1.0, W.X + dc.foff, c->st));
+    }
+    return factor_fetch(c, W.X, out);
+}
+
+// coneAUV + objAUV (data/def_lorads_sdp_conic.h:106-111): out_m[i] = A_i(sym(X_u X_v^T)) summed
+// over the cones, cobj = <C, sym(X_u X_v^T)> (before the division by scaleObjHis); u == v: X X^T.
+// The solver state (CVS and the per-cone values) is left as it was.
+int lrs_op_auv(lrs_ctx *c, int u, int v, double *out_m, double *cobj) {
+    LRS_NEED_STATE(c);
+    if (sharded(c)) { set_err("lrs_op_auv: unsharded contexts only"); return -1; }
+    const double *X = factor_ptr(c, u), *Y = factor_ptr(c, v);
+    if (!X || !Y) { set_err("lrs_op_auv: bad factor ids %d, %d", u, v); return -1; }
+    DevProblem &P = c->dp;
+    DevWork &W = c->W;
+    const long nsave = (long)P.m * (std::max(1, P.K) + 1);
+    double *save = nullptr;
+    HIPC(hipMalloc((void **)&save, sizeof(double) * nsave));
+    int rc = -1;
+    double obj = 0.0;
+    if (hipMemcpyAsync(save, W.cvs, sizeof(double) * P.m, hipMemcpyDeviceToDevice, c->st) != hipSuccess ||
+        hipMemcpyAsync(save + P.m, W.cvc, sizeof(double) * (nsave - P.m), hipMemcpyDeviceToDevice, c->st) != hipSuccess) {
+        set_err("lrs_op_auv: copy failed");
+    } else if (op_constr_xx(c, X, u == v ? nullptr : Y, nullptr, &obj) == 0) {
+        rc = 0;
+        if (out_m && (hipStreamSynchronize(c->st) != hipSuccess ||
+                      hipMemcpy(out_m, W.cvs, sizeof(double) * P.m, hipMemcpyDeviceToHost) != hipSuccess)) {
+            set_err("lrs_op_auv: fetch failed");
+            rc = -1;
+        }
+    }
+    if (hipMemcpyAsync(W.cvs, save, sizeof(double) * P.m, hipMemcpyDeviceToDevice, c->st) != hipSuccess ||
+        hipMemcpyAsync(W.cvc, save + P.m, sizeof(double) * (nsave - P.m), hipMemcpyDeviceToDevice, c->st) != hipSuccess ||
+        hipStreamSynchronize(c->st) != hipSuccess) {
+        set_err("lrs_op_auv: restore failed");
+        rc = -1;
+    }
+    (void)hipFree(save);
+    if (rc == 0 && cobj) *cobj = obj;
+    return rc;
+}
+
+// LORADSUpdateDimacsErrorALM / ADMM (lorads_alg/lorads_alg_common.c:424-428, :454-462) with the
+// objectives they read, LORADSCalObjRR_ALM / LORADSCalObjUV_ADMM (lorads_alm.c:1488-1497,
+// lorads_admm.c:398-410) and LORADSCalDualObj (lorads_alg_common.c:531): admm = 1 first sets
+// R = (U + V) / 2.  CVS <- A(R R^T); out5 = {pObj, dObj, l_1 primal infeasibility, l_inf primal
+// infeasibility, relative gap}.
+int lrs_op_dimacs(lrs_ctx *c, int admm, double *out5) {
+    LRS_NEED_STATE(c);
+    LRS_NEED_ARG(out5);
+    if (admm) OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
+    double pinf, obj, blam;
+    if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj, &blam)) return -1;
+    c->pObjVal = obj / c->scaleObjHis;
+    c->dObjVal = blam / c->scaleObjHis;
+    c->dimPinf = pinf;
+    c->dimGap = std::fabs(c->pObjVal - c->dObjVal) / (1 + std::fabs(c->pObjVal) + std::fabs(c->dObjVal));
+    out5[0] = c->pObjVal;
+    out5[1] = c->dObjVal;
+    out5[2] = pinf;
+    out5[3] = pinf * (1 + c->hp.bNrm1) / (1 + c->hp.bNrmInf);
+    out5[4] = c->dimGap;
+    return 0;
+}
+
 int lrs_op_gram(lrs_ctx *c, int cone, int which, double *gram) {
     LRS_NEED_STATE(c);
     LRS_NEED_ARG(gram);
@@ -2841,6 +2988,14 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     c->dinf_steps = c->dinf_iters = 0;
     c->rank_warned = false;
     if (p->lbfgsListLength < 1) { set_err("lbfgsListLength %d < 1", p->lbfgsListLength); return -1; }
+    // a sharded solve runs the fused two-pair L-BFGS only: the ring of L != 2 pairs
+    // (run_inner_generic) takes its dots over whole local buffers, halo rows included.  Refused
+    // here, before any device work, rather than part-way into the ALM phase.
+    if (sharded(c) && p->lbfgsListLength != 2) {
+        set_err("lbfgsListLength %d: a sharded solve (lrs_shard_rccl / lrs_shard_loopback) supports "
+                "lbfgsListLength 2 only (the reference's default, main.c:80)", p->lbfgsListLength);
+        return -1;
+    }
     c->lbfgsL = p->lbfgsListLength;
     c->dinf_time = 0.0;
     if (obj_unscale(c)) return -1;   // a previous solve's reopt scaled C on the device
@@ -3136,7 +3291,8 @@ int lrs_time_stages(lrs_ctx *c, int reps, double *stage_ms) {
     // stream.  The stages are idempotent for a fixed control block (A reads ctrl[1] and
     // writes ctrl[0]; G and B read ctrl[0]), so the repeats redo identical work.  The
     // control is set active with every exit test disabled.
-    double *h = c->hpin;
+    double *h = c->hpin + kHpRead;
+    static_assert(2 * C_NCTRL + P_NPAR <= kHpReadN, "lrs_time_stages staging");
     HIPC(hipMemcpyAsync(h, c->W.ctrl, sizeof(double) * 2 * C_NCTRL, hipMemcpyDeviceToHost, c->st));
     HIPC(hipMemcpyAsync(h + 2 * C_NCTRL, c->W.par, sizeof(double) * P_NPAR, hipMemcpyDeviceToHost, c->st));
     HIPC(hipStreamSynchronize(c->st));

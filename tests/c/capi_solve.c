@@ -12,7 +12,15 @@
  *          the reference's ADMM variable update over every cone through the per-cone
  *          operators (LORADSUpdateSDPVar, lorads_alg_common.c:298-326) and the dual update
  *          (:511-524): in.bin = U, V (column-major per cone, cones concatenated), lambda[m],
- *          rho, cg_tol; out.bin = U, V, lambda, CG iterations per (cone, side) */
+ *          rho, cg_tol; out.bin = U, V, lambda, CG iterations per (cone, side)
+ *        capi_solve --steps <file.dat-s> <rank> <in.bin> <out.bin> <ntrips>
+ *          the reference's ALM inner loop (lorads_alm.c:1302-1379) stepped from the operators
+ *          alone: per trip lrs_op_lbfgs (LBFGSDirection + UseGrad), lrs_op_q12 (ALMCalq12p12),
+ *          lrs_op_line_search (ALMLineSearch), lrs_op_alm_update (setAsNegGrad, ALMupdateVar,
+ *          the constrValSum update, ALMCalGrad, setlbfgsHisTwo) and lrs_op_dimacs
+ *          (updateDimacsALM).  in.bin = R, G, s, y (the newest pair), lambda[m], CVS[m], beta,
+ *          rho, trips done so far (the clearLBFGS count); out.bin = per trip {tau, rootNum,
+ *          ||G||^2, pinf}, then R, G, CVS, lambda, s, y, beta after the last trip */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -50,6 +58,10 @@ static int null_contract(void) {
     EXPECT_FAIL(lrs_op_admm_constr(NULL));
     EXPECT_FAIL(lrs_op_admm_half(NULL, 0, 0, 1.0, 1e-8, 10, NULL, NULL));
     EXPECT_FAIL(lrs_op_dual_update(NULL, 1.0));
+    EXPECT_FAIL(lrs_op_alm_update(NULL, 1.0, 0.5, &dv, &dv));
+    EXPECT_FAIL(lrs_op_adjoint(NULL, &dv, LRS_R, &dv, 1.0, 1));
+    EXPECT_FAIL(lrs_op_auv(NULL, LRS_R, LRS_R, &dv, &dv));
+    EXPECT_FAIL(lrs_op_dimacs(NULL, 0, &dv));
     EXPECT_FAIL(lrs_op_gram(NULL, 0, LRS_R, &dv));
     EXPECT_FAIL(lrs_op_dual_infeasibility(NULL, &dv, NULL));
     EXPECT_FAIL(lrs_solve(NULL, &p, &r));
@@ -159,9 +171,90 @@ done:
     return rc;
 }
 
+static int steps(const char *path, int rank, const char *in_path, const char *out_path, int ntrips) {
+    lrs_ctx *ctx = NULL;
+    if (lrs_ctx_create(0, &ctx) != 0) { fprintf(stderr, "ctx: %s\n", lrs_last_error()); return 1; }
+    int rc = 1, m = 0, K = 0;
+    int *dims = NULL, *ranks = NULL;
+    double *buf = NULL, *trips = NULL;
+    FILE *f = NULL;
+    if (lrs_load_sdpa(ctx, path, NULL) != 0) { fprintf(stderr, "load: %s\n", lrs_last_error()); goto done; }
+    lrs_problem_info(ctx, &m, &K, NULL, NULL, NULL);
+    dims = malloc(sizeof(int) * K);
+    ranks = malloc(sizeof(int) * K);
+    lrs_problem_info(ctx, &m, &K, dims, NULL, NULL);
+    long NR = 0;
+    for (int k = 0; k < K; ++k) {
+        ranks[k] = rank;
+        NR += (long)dims[k] * rank;
+    }
+    if (lrs_set_rank(ctx, ranks) != 0) { fprintf(stderr, "rank: %s\n", lrs_last_error()); goto done; }
+    const long nin = 4 * NR + 2 * m + 3;
+    buf = malloc(sizeof(double) * (4 * NR + 2 * m + 1));
+    trips = malloc(sizeof(double) * 4 * (ntrips > 0 ? ntrips : 1));
+    double *in = malloc(sizeof(double) * nin);
+    f = fopen(in_path, "rb");
+    if (!in || !f || fread(in, sizeof(double), nin, f) != (size_t)nin) { fprintf(stderr, "read %s\n", in_path); free(in); goto done; }
+    fclose(f);
+    f = NULL;
+    double beta_new = in[4 * NR + 2 * m], beta_old = 0.0;
+    const double rho = in[4 * NR + 2 * m + 1];
+    long clear = (long)in[4 * NR + 2 * m + 2];
+    if (lrs_factor_set(ctx, LRS_R, in) || lrs_factor_set(ctx, LRS_G, in + NR) || lrs_factor_set(ctx, LRS_S0, in + 2 * NR) ||
+        lrs_factor_set(ctx, LRS_Y0, in + 3 * NR) || lrs_vec_set(ctx, LRS_LAMBDA, in + 4 * NR) ||
+        lrs_vec_set(ctx, LRS_CVS, in + 4 * NR + m)) {
+        fprintf(stderr, "state: %s\n", lrs_last_error());
+        free(in);
+        goto done;
+    }
+    free(in);
+    for (int t = 0; t < ntrips; ++t) {
+        /* lorads_alm.c:1304-1309: the ring holds min(clearLBFGS, L = 2) pairs */
+        const int nodes = clear < 2 ? (int)clear : 2;
+        double tau = 0.0, lag = 0.0, beta = 0.0, dm[5];
+        int rn = 0;
+        if (lrs_op_lbfgs(ctx, nodes, beta_new, beta_old) || lrs_op_q12(ctx, NULL, NULL, NULL, NULL) ||
+            lrs_op_line_search(ctx, rho, &tau, &rn)) {
+            fprintf(stderr, "trip %d: %s\n", t, lrs_last_error());
+            goto done;
+        }
+        trips[4 * t] = tau;
+        trips[4 * t + 1] = rn;
+        if (rn == 0) { fprintf(stderr, "trip %d: no root\n", t); goto done; }
+        if (lrs_op_alm_update(ctx, rho, tau, &lag, &beta) || lrs_op_dimacs(ctx, 0, dm)) {
+            fprintf(stderr, "trip %d: %s\n", t, lrs_last_error());
+            goto done;
+        }
+        trips[4 * t + 2] = lag;
+        trips[4 * t + 3] = dm[2];
+        beta_old = beta_new;
+        beta_new = beta;
+        clear++;
+        printf("CAPI_TRIP %d tau=%.17g root=%d lag=%.17g pinf=%.17g pobj=%.17g\n", t, tau, rn, lag, dm[2], dm[0]);
+    }
+    if (lrs_factor_get(ctx, LRS_R, buf) || lrs_factor_get(ctx, LRS_G, buf + NR) ||
+        lrs_vec_get(ctx, LRS_CVS, buf + 2 * NR) || lrs_vec_get(ctx, LRS_LAMBDA, buf + 2 * NR + m) ||
+        lrs_factor_get(ctx, LRS_S0, buf + 2 * NR + 2 * m) || lrs_factor_get(ctx, LRS_Y0, buf + 3 * NR + 2 * m)) {
+        fprintf(stderr, "fetch: %s\n", lrs_last_error());
+        goto done;
+    }
+    buf[4 * NR + 2 * m] = beta_new;
+    f = fopen(out_path, "wb");
+    if (!f) goto done;
+    fwrite(trips, sizeof(double), 4 * ntrips, f);
+    fwrite(buf, sizeof(double), 4 * NR + 2 * m + 1, f);
+    rc = 0;
+done:
+    if (f) fclose(f);
+    free(dims); free(ranks); free(buf); free(trips);
+    lrs_ctx_destroy(ctx);
+    return rc;
+}
+
 int main(int argc, char **argv) {
     if (argc >= 2 && !strcmp(argv[1], "--null")) return null_contract();
     if (argc >= 6 && !strcmp(argv[1], "--sweep")) return sweep(argv[2], atoi(argv[3]), argv[4], argv[5]);
+    if (argc >= 7 && !strcmp(argv[1], "--steps")) return steps(argv[2], atoi(argv[3]), argv[4], argv[5], atoi(argv[6]));
     if (argc < 3) {
         fprintf(stderr, "usage: %s <file.dat-s> <out.json> [reoptLevel] | --null | --sweep ...\n", argv[0]);
         return 2;

@@ -162,3 +162,58 @@ def test_c_caller_admm_sweep_matches_reference(built, tmp_path, name):
         bar = 0.5 if ref > dims[c] * rank else 0.25
         assert abs(its[2 * c + 1] - ref) <= max(2, bar * ref), (c, its, g["cg_last"])
     assert abs(its.sum() - float(g["cg_total"])) <= max(4, 0.15 * float(g["cg_total"])), (its, g["cg_total"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mc_rand200", "theta40"])
+def test_c_caller_steps_alm_from_operators(built, tmp_path, name):
+    """The reference's ALM inner loop (lorads_alm.c:1302-1379) stepped by a plain-C caller from
+    the C-ABI operators alone -- lrs_op_lbfgs, lrs_op_q12, lrs_op_line_search,
+    lrs_op_alm_update (setAsNegGrad + ALMupdateVar + the constrValSum update + ALMCalGrad +
+    setlbfgsHisTwo) and lrs_op_dimacs (updateDimacsALM) -- from the reference's own state
+    after its first trip (tests/golden/steps_<name>.npz K1: R, G, the newest L-BFGS pair and
+    its beta, lambda, constrValSum; rho = 1/sqrt(sum of block sizes), the reference's initial
+    penalty with initRho 0, data/lorads_solver.c:1598-1607), four more trips, against the
+    reference's trips 2..5 and its state after trip 5 (the K5 dump).  Bars as the fused
+    kernels' per-trip test: tau, ||G||^2 and pinf to 1e-9 relative with the same root count;
+    R, G, A(RR^T), the newest pair and its beta to 1e-9 (norm-wise)."""
+    import numpy as np
+    exe = build_c_caller(tmp_path)
+    z = np.load(os.path.join(ROOT, "tests", "golden", f"steps_{name}.npz"))
+    dims = [int(d) for d in z["dims"]]
+    m, nr = int(z["m"]), int(z["nr"])
+    rank = nr // sum(dims)
+    assert rank * sum(dims) == nr
+    rho = 1.0 / np.sqrt(float(sum(dims)))
+    assert int(z["K5_trips"].shape[0]) == 5
+    inp = np.concatenate([z["K1_R"], z["K1_G"], z["K1_s"], z["K1_y"], z["K1_lam"], z["K1_cvs"],
+                          [float(z["K1_beta"][0]), rho, 1.0]])
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    inp.astype(np.float64).tofile(fin)
+    inst = os.path.join(ROOT, "tests", "golden", "instances", f"{name}.dat-s")
+    nt = 4
+    r = subprocess.run([exe, "--steps", inst, str(rank), str(fin), str(fout), str(nt)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = np.fromfile(fout, dtype=np.float64)
+    trips = out[:4 * nt].reshape(nt, 4)
+    o = 4 * nt
+    R, G = out[o:o + nr], out[o + nr:o + 2 * nr]
+    cvs, lam = out[o + 2 * nr:o + 2 * nr + m], out[o + 2 * nr + m:o + 2 * nr + 2 * m]
+    s, y = out[o + 2 * nr + 2 * m:o + 3 * nr + 2 * m], out[o + 3 * nr + 2 * m:o + 4 * nr + 2 * m]
+    beta = out[o + 4 * nr + 2 * m]
+    ref = z["K5_trips"]
+    tol = 1e-9
+    for t in range(nt):
+        tau, rn, lag, pinf = ref[t + 1]
+        assert int(trips[t, 1]) == int(rn), (t, trips[t], ref[t + 1])
+        for q, v in ((0, tau), (2, lag), (3, pinf)):
+            assert abs(trips[t, q] - v) <= tol * abs(v), (t, q, trips[t, q], v)
+
+    def rel(a, b):
+        return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+    for nm, got, want in (("R", R, z["K5_R"]), ("G", G, z["K5_G"]), ("cvs", cvs, z["K5_cvs"]), ("s", s, z["K5_s"]),
+                          ("y", y, z["K5_y"])):
+        assert rel(got, want) <= tol, (nm, rel(got, want))
+    assert np.array_equal(lam, z["K5_lam"])
+    assert abs(beta - float(z["K5_beta"][0])) <= tol * abs(float(z["K5_beta"][0])), (beta, z["K5_beta"])
