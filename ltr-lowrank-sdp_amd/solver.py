@@ -101,6 +101,11 @@ def load_library(path=None):
         "lrs_op_admm_half": (C.c_int, [vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, ip, dp]),
         "lrs_op_dual_update": (C.c_int, [vp, C.c_double]),
         "lrs_op_gram": (C.c_int, [vp, C.c_int, C.c_int, dp]),
+        "lrs_op_alm_update": (C.c_int, [vp, C.c_double, C.c_double, dp, dp]),
+        "lrs_op_adjoint": (C.c_int, [vp, dp, C.c_int, dp, C.c_double, C.c_int]),
+        "lrs_op_auv": (C.c_int, [vp, C.c_int, C.c_int, dp, dp]),
+        "lrs_op_dimacs": (C.c_int, [vp, C.c_int, dp]),
+        "lrs_abi_version": (C.c_int, []),
         "lrs_solve": (C.c_int, [vp, C.POINTER(Params), C.POINTER(Result)]),
         "lrs_trajectory": (C.c_int, [vp, C.c_int, ip, ip, C.c_int]),
         "lrs_write_json": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(Result),
@@ -284,6 +289,9 @@ class Solver:
         self.ranks = ranks
 
     def nr(self):
+        # the context's current ranks (a solve may have grown them since set_rank): every host
+        # buffer handed to the library is sized from them
+        self.ranks = self.get_rank()
         return sum(n * r for n, r in zip(self.dims, self.ranks))
 
     def set_factor(self, which, x):
@@ -344,7 +352,7 @@ class Solver:
         if init:
             self.admm_constr()
         it = C.c_int()
-        rhs = np.empty(self.dims[cone] * self.ranks[cone])
+        rhs = np.empty(self.dims[cone] * self.get_rank()[cone])
         self._check(self.lib.lrs_op_admm_half(self.ctx, cone, side, rho, cg_tol, cg_maxit, C.byref(it), _dptr(rhs)),
                     "admm_half")
         return self.get_factor(V if side else U), rhs, it.value
@@ -353,8 +361,36 @@ class Solver:
         """LORADSUpdateDualVar: lambda += rho (b - A(X))."""
         self._check(self.lib.lrs_op_dual_update(self.ctx, rho), "dual_update")
 
+    def alm_update(self, rho, tau):
+        """setAsNegGrad + ALMupdateVar + constrValSum update + ALMCalGrad + setlbfgsHisTwo
+        (lorads_alm.c:1340-1355): returns (||G||^2, beta of the new pair)."""
+        lag, beta = C.c_double(), C.c_double()
+        self._check(self.lib.lrs_op_alm_update(self.ctx, rho, tau, C.byref(lag), C.byref(beta)), "alm_update")
+        return lag.value, beta.value
+
+    def adjoint(self, y, which=R, scale=1.0, with_c=True):
+        """scale (with_c C + sum_i y_i A_i) X_which (sdpDataWSum + mul_rk)."""
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        assert y.size == self.m
+        out = np.empty(self.nr())
+        self._check(self.lib.lrs_op_adjoint(self.ctx, _dptr(y), which, _dptr(out), scale, 1 if with_c else 0),
+                    "adjoint")
+        return out
+
+    def auv(self, u=R, v=R):
+        """(A(sym(X_u X_v^T)), <C, sym(X_u X_v^T)>) -- coneAUV + objAUV; the state is unchanged."""
+        out, cobj = np.empty(self.m), C.c_double()
+        self._check(self.lib.lrs_op_auv(self.ctx, u, v, _dptr(out), C.byref(cobj)), "auv")
+        return out, cobj.value
+
+    def dimacs(self, admm=False):
+        """updateDimacsALM / ADMM with the objectives: {pobj, dobj, pinf, pinf_inf, gap}."""
+        o = np.empty(5)
+        self._check(self.lib.lrs_op_dimacs(self.ctx, 1 if admm else 0, _dptr(o)), "dimacs")
+        return dict(zip(("pobj", "dobj", "pinf", "pinf_inf", "gap"), o.tolist()))
+
     def gram(self, cone=0, which=R):
-        r = self.ranks[cone]
+        r = self.get_rank()[cone]
         g = np.empty(r * r)
         self._check(self.lib.lrs_op_gram(self.ctx, cone, which, _dptr(g)), "gram")
         return g.reshape(r, r)

@@ -198,6 +198,23 @@ END:;
                              c.admm.l_1_primal_infeasibility, c.admm.l_inf_primal_infeasibility,
                              c.admm.primal_dual_gap, all_time, p.rhoMax, p.heuristicFactor);
     lorads_logging_close(S);
+    /* REF_DUMP=<file>: the final iterate for a device-side check (tests/test_tight_objectives.py):
+       doubles {K, rank_0..rank_{K-1}, R_0..R_{K-1} (column-major n_k x rank_k), m, lambda[m]} */
+    const char *dump = getenv("REF_DUMP");
+    if (dump) {
+        FILE *fd = fopen(dump, "wb");
+        if (fd) {
+            double v = (double)S->nCones;
+            fwrite(&v, 8, 1, fd);
+            for (lorads_int k = 0; k < S->nCones; ++k) { v = (double)S->var->R[k]->rank; fwrite(&v, 8, 1, fd); }
+            for (lorads_int k = 0; k < S->nCones; ++k)
+                fwrite(S->var->R[k]->matElem, 8, (size_t)S->var->R[k]->nRows * S->var->R[k]->rank, fd);
+            v = (double)S->nRows;
+            fwrite(&v, 8, 1, fd);
+            fwrite(S->var->dualVar, 8, (size_t)S->nRows, fd);
+            fclose(fd);
+        }
+    }
     printf("REF_RESULT alm_inner=%ld alm_outer=%ld alm_time=%.9e alm_pobj=%.17e alm_dobj=%.17e "
            "alm_pinf=%.17e alm_gap=%.17e alm_rho=%.17e\n",
            alm_inner, (long)c.alm.outerIter, t_alm, c.alm.primal_objective_value,

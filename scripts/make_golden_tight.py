@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Reference solves of the general SDPs and theta3 at tighter tolerances than the
 reference's default phase2Tol 1e-5 (main.c:75), so that the device's objectives can be
-pinned beyond what the default stopping rule fixes (checker_1.5 /
+pinned beyond what the default stopping rule fixes; the tightest run's final iterate (R per cone,
+lambda) goes to tests/golden/tight_final_<name>.npz (REF_DUMP, oracle/ref_harness.c) (checker_1.5 /
 ice_2.0 / p_auss2_3.0 agree only to ~1e-4 at 1e-5).
 
 The reference LoRADS C code built by oracle/Makefile.ref (oracle/_ref/lorads_ref_harness)
@@ -18,6 +19,8 @@ import subprocess
 import sys
 import tempfile
 import time
+
+import numpy as np
 from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -46,6 +49,9 @@ def run_one(name, kind, flags, tol, td):
     js = os.path.join(td, f"{name}_{tol}.json")
     fl = [*flags, "--phase2Tol", tol]
     env = dict(os.environ, OPENBLAS_NUM_THREADS="1")
+    dump = os.path.join(td, f"{name}_{tol}.final")
+    if tol == TOLS[-1]:   # the tightest run's final iterate (R per cone, lambda) for the device check
+        env["REF_DUMP"] = dump
     t0 = time.time()
     r = subprocess.run([HARNESS, "solve", path, *fl, "--timeSecLimit", "3000", "--jsonfile", js],
                        capture_output=True, text=True, cwd=td, env=env)
@@ -57,6 +63,16 @@ def run_one(name, kind, flags, tol, td):
                 k, v = kv.split("=")
                 res[k] = float(v)
     log = [[int(a), int(b), float(c), float(d), float(e)] for a, b, c, d, e in LINE.findall(r.stdout)]
+    if os.path.exists(dump):
+        # {K, ranks[K], R (cones concatenated), m, lambda[m]}: m is the count of the trailing block
+        v = np.fromfile(dump, dtype=np.float64)
+        K = int(v[0])
+        ranks = v[1:1 + K].astype(np.int64)
+        rest = v.size - 1 - K
+        mm = next(c for c in range(1, rest) if v[1 + K + rest - 1 - c] == c)
+        NR = rest - 1 - mm
+        np.savez_compressed(os.path.join(ROOT, "tests", "golden", f"tight_final_{name}.npz"), ranks=ranks,
+                            R=v[1 + K:1 + K + NR], lam=v[2 + K + NR:], m=mm, tol=float(tol))
     out = {"instance": name, "kind": kind, "sha256": sha, "flags": fl, "result": res, "alm_log": log,
            "wall_sec": wall, "json": json.load(open(js)) if os.path.exists(js) else None}
     print(name, tol, {k: res.get(k) for k in ("alm_inner", "admm_iter", "admm_pobj", "admm_dobj", "admm_gap",

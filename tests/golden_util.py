@@ -123,3 +123,35 @@ def read_sdpa_dense(path):
         else:
             A.setdefault((i - 1, blk), []).append((r, c, v))
     return m, dims, b, C, A
+
+
+def fixed_trace(path):
+    """tr(X) when the constraints fix it for every feasible X of the SDPA file at `path`, else
+    None: either every diagonal entry of every block is its own single-entry constraint
+    v X_kk = b (MaxCut-type diag(X) = b / v), or one constraint is v I over all blocks (theta-type
+    tr(X) = b / v).  Used for the weak-duality bound <C, X> >= b^T lambda + lambda_min(S) tr(X)."""
+    with open(path) as f:
+        toks = [t for ln in f if not ln.lstrip().startswith(("*", '"')) for t in ln.replace(",", " ").replace("{", " ")
+                .replace("}", " ").replace("(", " ").replace(")", " ").split()]
+    m, nb = int(toks[0]), int(toks[1])
+    dims = [abs(int(float(t))) for t in toks[2:2 + nb]]
+    b = [float(t) for t in toks[2 + nb:2 + nb + m]]
+    ents = {}
+    q = 2 + nb + m
+    while q + 4 < len(toks):
+        c, blk, i, j, v = int(toks[q]), int(toks[q + 1]), int(toks[q + 2]), int(toks[q + 3]), float(toks[q + 4])
+        q += 5
+        if c >= 1 and v != 0.0:
+            ents.setdefault(c, []).append((blk, i, j, v))
+    ndiag = sum(dims)
+    diag = {}
+    for c, e in ents.items():
+        if len(e) == 1 and e[0][1] == e[0][2]:
+            diag[(e[0][0], e[0][1])] = b[c - 1] / e[0][3]
+    if len(diag) == ndiag:
+        return sum(diag.values())
+    for c, e in ents.items():
+        if len(e) == ndiag and all(i == j for _, i, j, _ in e) and len({v for *_, v in e}) == 1 and \
+                len({(blk, i) for blk, i, _, _ in e}) == ndiag:
+            return b[c - 1] / e[0][3]
+    return None
