@@ -123,6 +123,8 @@ struct DevCone {
     int auv_items = 0;
     long auv_ebase = 0;                  // first constraint entry of this cone (con_ptr[k m])
     int *auv_item = nullptr;             // [items][4]
+    int *auv_xo = nullptr;               // [kXcdBands + 1] XCD bands of the items (null: none)
+    int auv_xmax = 0;                    // items of the longest band
     unsigned *auv_pq = nullptr;          // [Zk]
     int *auv_pos = nullptr;              // [Zk]
     double *auv_val = nullptr;           // [Zk]
@@ -131,6 +133,8 @@ struct DevCone {
     int sa_items = 0;
     int sa_n = 0;                        // tiled slots (sa_slot's length)
     int *sa_item = nullptr;
+    int *sa_xo = nullptr;                // [kXcdBands + 1] XCD bands of the items (null: none)
+    int sa_xmax = 0;                     // items of the longest band
     unsigned *sa_pq = nullptr;
     int *sa_slot = nullptr;
     // stage B's gradient S R_new over the symmetric pattern in the same tiles (k_tile_b2): one
@@ -176,6 +180,7 @@ constexpr int kAuvMinPerTile = 768;  //   >= this many entries (constraint entri
                                      //   LRS_SLOT_TILES = 0/1 override
 constexpr int kCgSplitSlabs = 8;      // k_cgemm2's most K-slices (DevWork::CGK slabs)
 constexpr int kNX = 8;              // column blocks of the tiled long-row kernels (one per XCD)
+constexpr int kXcdBands = 8;         // XCDs: bands of the 2-D tile items (lrs_problem.cpp xcd_bands)
 constexpr int kTileMinDeg = 32;
 constexpr int kDenseRow = 64;        // entries of a row past which the latency kernels slice it
 constexpr int kSliceMinB = 28;       // fewest entries of one B slice block (G = 64: 7 groups x 4)

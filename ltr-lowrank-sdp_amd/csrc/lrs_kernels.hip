@@ -690,8 +690,21 @@ __device__ __forceinline__ void auv_chunk(const double (*tl)[kAuvT * kAuvS], int
     }
 }
 
+// The items a block takes (block-uniform): with XCD bands (xo, lrs_problem.cpp xcd_bands) block b
+// walks band b % 8 -- the XCD that round-robin dispatch gives it -- from its index b / 8 among that
+// band's blocks; without, the grid strides over all items.
+struct BandWalk {
+    int q, end, step;
+};
+__device__ __forceinline__ BandWalk band_walk(const int *__restrict__ xo, int nitems) {
+    if (!xo || gridDim.x < kXcdBands) return {(int)blockIdx.x, nitems, (int)gridDim.x};
+    const int x = blockIdx.x % kXcdBands;
+    return {xo[x] + (int)blockIdx.x / kXcdBands, xo[x + 1], ((int)gridDim.x - x + kXcdBands - 1) / kXcdBands};
+}
+
 template <int MODE>
-__global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, const int4 *__restrict__ items,
+__global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, int nitems, const int4 *__restrict__ items,
+                                                          const int *__restrict__ xo,
                                                           const unsigned *__restrict__ pq,
                                                           const int *__restrict__ ent,
                                                           const double *__restrict__ X,
@@ -700,7 +713,8 @@ __global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, 
     if (guard && guard[0] == 0.0) return;
     constexpr int NA = MODE == 0 ? 4 : 2;           // staged operands: Xa, Xb (+ Ya, Yb)
     __shared__ double tl[NA][kAuvT * kAuvS];
-    const int4 it = items[blockIdx.x];
+    for (BandWalk bw = band_walk(xo, nitems); bw.q < bw.end; bw.q += bw.step) {
+    const int4 it = items[bw.q];
     const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
     int pl[kAuvNpt], ql[kAuvNpt];
     double acc[kAuvNpt];
@@ -731,6 +745,7 @@ __global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, 
         const int t = eb + (int)threadIdx.x + j * kAuvThreads;
         if (t < ee) val[ent[t]] = MODE == 0 ? 0.5 * acc[j] : acc[j];
     }
+    }   // items
 }
 
 // Per constraint of the cone: sum of w_e d_e over its entries in entry order, then k_auv_con's row epilogue (scale, accumulate, sum_upd, the
@@ -3358,7 +3373,7 @@ __global__ void __launch_bounds__(NT) k_tile_a(
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     const double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec,
     const double *__restrict__ par, const double *__restrict__ ctrl_cur, double *__restrict__ partA, int pblk_off,
-    double2 *__restrict__ uvp) {
+    double2 *__restrict__ uvp, const int *__restrict__ xo) {
     constexpr int NPT = kAuvItem / NT;   // slots per thread of one item
     static_assert(NPT * NT == kAuvItem, "k_tile_a: items divide over the block");
     if (ctrl_cur[C_ACTIVE] == 0.0) return;
@@ -3367,8 +3382,8 @@ __global__ void __launch_bounds__(NT) k_tile_a(
     const double rho = par[P_RHO], rhoInv = 1.0 / rho;
     __shared__ double tl[4][kAuvT * kAuvS];
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
-        const int4 it = items[itx];
+    for (BandWalk bw = band_walk(xo, nitems); bw.q < bw.end; bw.q += bw.step) {   // block-uniform
+        const int4 it = items[bw.q];
         const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
         int pl[NPT], ql[NPT];
         double s0[NPT], s1[NPT];
@@ -3740,14 +3755,14 @@ __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: tw
     const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
-    const double *__restrict__ ls_cur, double *__restrict__ partC, int pblk_off) {
+    const double *__restrict__ ls_cur, double *__restrict__ partC, int pblk_off, const int *__restrict__ xo) {
     if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
     const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
     const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
     __shared__ double tl[2][kAuvT * kAuvS];
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
-        const int4 it = items[itx];
+    for (BandWalk bw = band_walk(xo, nitems); bw.q < bw.end; bw.q += bw.step) {   // block-uniform
+        const int4 it = items[bw.q];
         const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
         int pl[kAuvNpt], ql[kAuvNpt];
         double dv[kAuvNpt];
@@ -4979,16 +4994,17 @@ int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const
         // values stored per slot), then the objective sums in slot order
         const double *Xc = X + c.foff, *Yc = Y ? Y + c.foff : nullptr;
         const int4 *it = reinterpret_cast<const int4 *>(c.sa_item);
+        const int tg = c.sa_xo ? kXcdBands * c.sa_xmax : c.sa_items;   // one block per item (band_walk)
         if (mode == 1)
-            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.sa_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, it,
-                               c.sa_pq, c.sa_slot, Xc, Xc, out0, nullptr);
+            hipLaunchKernelGGL((k_auv_tile<1>), dim3(tg), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, c.sa_items, it,
+                               c.sa_xo, c.sa_pq, c.sa_slot, Xc, Xc, out0, nullptr);
         else
-            hipLaunchKernelGGL((k_auv_tile<0>), dim3(c.sa_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, it,
-                               c.sa_pq, c.sa_slot, Xc, Yc, out0, nullptr);
+            hipLaunchKernelGGL((k_auv_tile<0>), dim3(tg), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, c.sa_items, it,
+                               c.sa_xo, c.sa_pq, c.sa_slot, Xc, Yc, out0, nullptr);
         LRS_CHECK_LAUNCH();
         if (mode == 2) {
-            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.sa_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, it,
-                               c.sa_pq, c.sa_slot, Yc, Yc, out1, nullptr);
+            hipLaunchKernelGGL((k_auv_tile<1>), dim3(tg), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, c.sa_items, it,
+                               c.sa_xo, c.sa_pq, c.sa_slot, Yc, Yc, out1, nullptr);
             LRS_CHECK_LAUNCH();
         }
         if (P.shard) {   // the owned rows' lower slots only, as k_sddmm over the owned rows
@@ -5105,11 +5121,13 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
                                    reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Yc, c.auv_val,
                                    guard);
         } else if (mode == 1)
-            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
-                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Xc, c.auv_val, guard);
+            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.auv_xo ? kXcdBands * c.auv_xmax : c.auv_items), dim3(kAuvThreads),
+                               0, st, c.n, c.r, c.ld, c.auv_items, reinterpret_cast<const int4 *>(c.auv_item), c.auv_xo,
+                               c.auv_pq, c.auv_pos, Xc, Xc, c.auv_val, guard);
         else
-            hipLaunchKernelGGL((k_auv_tile<0>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
-                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Yc, c.auv_val, guard);
+            hipLaunchKernelGGL((k_auv_tile<0>), dim3(c.auv_xo ? kXcdBands * c.auv_xmax : c.auv_items), dim3(kAuvThreads),
+                               0, st, c.n, c.r, c.ld, c.auv_items, reinterpret_cast<const int4 *>(c.auv_item), c.auv_xo,
+                               c.auv_pq, c.auv_pos, Xc, Yc, c.auv_val, guard);
         LRS_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_auv_tsum, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, cone, P.con_ptr,
                            P.con_w, c.auv_ebase, c.auv_val, scale, accumulate, out, b_for_vio, vio_part,
@@ -6240,7 +6258,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     hipLaunchKernelGGL(k_tile_a<NT_>, dim3(grid), dim3(NT_), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,         \
                        reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2, W.D,      \
                        W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), \
-                       P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, uvp)
+                       P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, uvp, c.sa_xo)
             // LRS_TILE_GLDS=1: the same work staged by direct global -> LDS loads (k_tile_a_g)
             static const int glds = getenv("LRS_TILE_GLDS") ? atoi(getenv("LRS_TILE_GLDS")) : 0;
             if (glds && c.ld % kGc == 0) {
@@ -6392,7 +6410,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                P.slot_con, P.slot_a,
                                reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,
                                reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur,
-                               W.partC, off);
+                               W.partC, off, c.sa_xo);
             LRS_CHECK_LAUNCH();
             if (c.sx_n > 0) {   // sharded: S on the halo rows' lower slots
                 hipLaunchKernelGGL(k_slot_sv, dim3(std::min(grid_elems(c.sx_n, 1), 2048)), dim3(kBlock), 0, st, c.sx_n,
