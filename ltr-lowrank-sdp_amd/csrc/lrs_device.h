@@ -238,7 +238,6 @@ struct DevProblem {
     std::vector<DevCone> cones;
     int ndense = 0;                                          // cones with a dense objective (DevCone::Cd)
     bool tiles = false;                                      // column-tiled long-row kernels (LRS_TILES=1 at alloc)
-    bool tile_bx = false;                                    // stage B over the tiles in one pass (LRS_TILE_BX=1 at upload)
     double *gp = nullptr;                                    // DevWork::GP (kNX partial factors), the tiled S X's scratch
     double *cgk = nullptr;                                   // DevWork::CGK: k_cgemm2's split-K slabs (kCgSplitSlabs x NRpad)
     double dense_scale = 1.0;                                // objScale_dualvar's factor on those C

@@ -164,16 +164,6 @@ __device__ __forceinline__ double group_sum4(const double (&d)[4], int o) {
     }
 }
 
-// Kernel arguments (and uniform words) in SGPRs at this point: the compiler otherwise sinks
-// each argument load to the basic block that first uses it, and every branch level of a
-// kernel's prologue then waits for its own argument trip (three dependent trips in k_lat_a /
-// k_lat_b before the first vector load was issued).  Pinned at the top, the argument loads
-// are one batch, one trip.
-template <typename T>
-__device__ __forceinline__ void karg_pin1(const T &x) { asm volatile("" ::"s"(x)); }
-template <typename... T>
-__device__ __forceinline__ void karg_pin(const T &...x) { (karg_pin1(x), ...); }
-
 __device__ __forceinline__ double read_lane(double v, int l) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readlane((int)b, l);
@@ -188,17 +178,8 @@ __device__ __forceinline__ double wave_sum(double v) {
     return (read_lane(v, 0) + read_lane(v, 16)) + (read_lane(v, 32) + read_lane(v, 48));
 }
 
-// two doubles at 8-byte alignment (gfx950 global loads/stores take unaligned 16-byte accesses)
-typedef double d2u8 __attribute__((ext_vector_type(2), aligned(8)));
 template <int E>
 __device__ __forceinline__ void ld_row(const double *__restrict__ p, double (&v)[E]) {
-#ifdef LRS_ROW_X4
-    if constexpr (E == 3) {   // 16 + 8 bytes (8-byte aligned 16-byte load: two instructions, not three)
-        const d2u8 t = *reinterpret_cast<const d2u8 *>(p);
-        v[0] = t.x; v[1] = t.y; v[2] = p[2];
-        return;
-    }
-#endif
     if constexpr (E == 2) {
         double2 t = *reinterpret_cast<const double2 *>(p);
         v[0] = t.x; v[1] = t.y;
@@ -214,15 +195,6 @@ __device__ __forceinline__ void ld_row(const double *__restrict__ p, double (&v)
 
 template <int E>
 __device__ __forceinline__ void st_row(double *__restrict__ p, const double (&v)[E]) {
-#ifdef LRS_ROW_X4
-    if constexpr (E == 3) {
-        d2u8 t;
-        t.x = v[0]; t.y = v[1];
-        *reinterpret_cast<d2u8 *>(p) = t;
-        p[2] = v[2];
-        return;
-    }
-#endif
     if constexpr (E == 2) {
         *reinterpret_cast<double2 *>(p) = make_double2(v[0], v[1]);
     } else if constexpr (E == 4) {
@@ -2380,17 +2352,6 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
     __shared__ double c[C_NCTRL];
     __shared__ double pl[P_NPAR];
     LRS_TS(0, 0);
-#ifdef LRS_KARG_PIN
-    karg_pin(n, ld, foff, adj_ptr, adj_low, adj_col, adj_slot, Cw, Rb0, Rb1, Dall, G0, G1, s0a, y0a, s1a, y1a, uRD,
-             uDD, loc_ptr, loc_con, loc_w, loc1, b, cvs, lam, rec, do_glob, mg, glob, m, K);
-    karg_pin(con_ptr, con_slot, con_w, uRR, par, ctrl_prev, ctrl_cur, ls_prev, partC, nblkC, partA, pblk_off, gwide,
-             nrb, nda, dra);
-#elif defined(LRS_KARG_PIN2)
-    // the arguments of the prologue (the first loads of both wave kinds, the operand bases):
-    // one batch; the rest below, beside the first vector loads' trip
-    karg_pin(n, ld, foff, adj_ptr, adj_low, adj_col, adj_slot, Cw, Rb0, Rb1, G0, G1, s0a, y0a, s1a, y1a, loc1, b,
-             cvs, lam, m, par, ctrl_prev, ls_prev, partC, nblkC, nrb, nda, dra);
-#endif
     LRS_BLK_BEGIN();
     // lrw row waves + the control wave (an argument beside nrb, loaded in the first argument batch:
     // blockDim.x would be one more load before the first branch)
@@ -2433,21 +2394,8 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
     __builtin_amdgcn_sched_barrier(0);
     // this iteration's operands: ctrl_step folds the previous stage (and flips the G and R
     // buffers) exactly when `fold` holds
-#if defined(LRS_KARG_PIN) || defined(LRS_KARG_PIN2)
-    // the control words every wave needs as one batch (no short-circuit chain of loads)
-    const double cw_act2 = ctrl_prev[C_ACT2], cw_pend = ctrl_prev[C_PENDING], cw_rcur = ctrl_prev[C_RCUR],
-                 cw_gcur = ctrl_prev[C_GCUR], lsflag = ls_prev[LS_FLAG];
-#ifdef LRS_KARG_PIN2
-    karg_pin(cw_act2, cw_pend, cw_rcur, cw_gcur, lsflag, Dall, uRD, uDD, loc_ptr, loc_con, loc_w, rec, do_glob, mg,
-             glob, K, con_ptr, con_slot, con_w, uRR, ctrl_cur, partA, pblk_off, gwide);
-#else
-    karg_pin(cw_act2, cw_pend, cw_rcur, cw_gcur, lsflag);
-#endif
-    const int fold = ((cw_act2 != 0.0) & (cw_pend == 1.0) & (lsflag == 0.0)) ? 1 : 0;
-#else
     const double lsflag = ls_prev[LS_FLAG];
     const int fold = (ctrl_prev[C_ACT2] != 0.0 && ctrl_prev[C_PENDING] == 1.0 && lsflag == 0.0) ? 1 : 0;
-#endif
 #ifdef LRS_PHASE_TIMING
     // diagnostics: the row header (a vector load) and the control words (scalar loads) arrived
     if (blockIdx.x == 0 && threadIdx.x == 0 && kb != -12345) g_phase_tmp[0][10] = wall_clock64();
@@ -2494,22 +2442,6 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
 #endif
         // (lane 0 on the LDS copy: a register copy of the block, every word read back from
         // its lane, measured 0.5 us slower on G67, scripts/gpu_r04h.sh)
-#ifdef LRS_CTRL_SREG
-        // every lane on a private copy loaded through the scalar cache (constant indices
-        // only: the copy lives in registers), lane 0 publishes the result to LDS
-        {
-            double cr[C_NCTRL], pr[P_NPAR];
-#pragma unroll
-            for (int q = 0; q < C_NCTRL; ++q) cr[q] = ctrl_prev[q];
-#pragma unroll
-            for (int q = 0; q < P_NPAR; ++q) pr[q] = par[q];
-            ctrl_step(cr, pr, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
-            if (l64 == 0) {
-#pragma unroll
-                for (int q = 0; q < C_NCTRL; ++q) c[q] = cr[q];
-            }
-        }
-#elif !defined(LRS_NO_CTRL_LREG)
         // the block and the parameters read back from LDS as one batch of loads (constant
         // indices: registers), the step on registers, lane 0 writes the block back (k_lat_a
         // 9.1 -> 8.95 us on G67, profiles/r04u_lat_ab.txt; LRS_NO_CTRL_LREG: on the LDS copy)
@@ -2525,9 +2457,6 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
                 for (int q = 0; q < C_NCTRL; ++q) c[q] = cr[q];
             }
         }
-#else
-        if (l64 == 0) ctrl_step(c, pl, lsflag, ls_prev[LS_TAU], fold, s, mg == 0);
-#endif
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && l64 == 0) g_phase_tmp[0][7] = wall_clock64();
 #endif
@@ -2571,21 +2500,6 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
         // slots without a single local constraint read the row's own (spread, cached) index
         // instead of a common one: no hot line shared by every lane
         const int ispare = min(ic, m - 1);
-#ifdef LRS_LAT_SKIPREC
-        // entries without a single local constraint (MaxCut's off-diagonal ones) load nothing:
-        // a wave whose entries u have none skips the loads (exec-masked branch)
-#pragma unroll
-        for (int u = 0; u < NO; ++u) {
-            const int ci = (int)l1[u].y;
-            bq[u] = cq[u] = lq[u] = 0.0;
-            if (ci >= 0) { bq[u] = b[ci]; cq[u] = cvs[ci]; lq[u] = lam[ci]; }
-        }
-        {
-            const int ci = (int)l1d.y;
-            if (ci >= 0) { bd = b[ci]; cd = cvs[ci]; lmd = lam[ci]; }
-        }
-        (void)ispare;
-#else
 #pragma unroll
         for (int u = 0; u < NO; ++u) {
             const int ci = (int)l1[u].y >= 0 ? (int)l1[u].y : ispare;
@@ -2599,7 +2513,6 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
             cd = cvs[ci];
             lmd = lam[ci];
         }
-#endif
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && threadIdx.x == 0 && xi[0] != 12345.678) g_phase_tmp[0][1] = wall_clock64();
         if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && xj[0][0] != 12345.678 && bd != 12345.678)
@@ -2752,17 +2665,6 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
     __shared__ double pl[P_NPAR];
     __shared__ double gsh[kLatRows * E];   // slice blocks: the lane groups' partial gradients
     LRS_TS(2, 0);
-#ifdef LRS_KARG_PIN
-    karg_pin(n, ld, foff, adj_ptr, adj_low, adj_col, adj_slot, Rb0, Rb1, Dall, G0, G1, s0, y0, s1, y1, uRR, Craw,
-             slot_ptr, slot_con, slot_a, slot1, rec, loc_ptr, loc_con, loc_w, loc1, b, cvs, par, ctrl);
-    karg_pin(partA, nblkA, partB, nblkB, ls_cur, L, partC, pblk_off, m, hmirror, seq, nrb, ndb, drb, gl, CRb, CDb);
-#elif defined(LRS_KARG_PIN2)
-    // the prologue's arguments as one batch; the rest with the control words below
-    karg_pin(n, ld, foff, adj_ptr, adj_low, adj_col, adj_slot, Rb0, Rb1, Dall, G0, G1, s0, y0, s1, y1, Craw, slot1,
-             rec, loc1, b, par, ctrl, partA, nblkA, partB, nblkB, L, m, nrb, ndb, drb, hmirror, seq);
-#define LRS_B_PIN2() karg_pin(cw_act2, cw_gcur, cw_head, cw_rcur, uRR, slot_ptr, slot_con, slot_a, loc_ptr, loc_con, \
-                              loc_w, cvs, ls_cur, partC, pblk_off, gl, CRb, CDb)
-#endif
     LRS_BLK_BEGIN();
     mirror_ctrl(ctrl, hmirror, seq);
     // lrw row waves + the control wave (an argument beside nrb, loaded in the first argument batch:
@@ -2802,26 +2704,9 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
         ke = adj_ptr[ic + 1];
     }
     __builtin_amdgcn_sched_barrier(0);
-#if defined(LRS_KARG_PIN) || defined(LRS_KARG_PIN2)
-    // the control words as one batch before the first test on them
-    const double cw_act2 = ctrl[C_ACT2], cw_gcur = ctrl[C_GCUR], cw_head = ctrl[C_HEAD], cw_rcur = ctrl[C_RCUR];
-#ifndef LRS_LAT_SPEC
-#ifdef LRS_KARG_PIN2
-    LRS_B_PIN2();
-#else
-    karg_pin(cw_act2, cw_gcur, cw_head, cw_rcur);
-#endif
-    if (cw_act2 == 0.0) return;
-#endif
-    const int gcur = (int)cw_gcur, h = (int)cw_head;
-    const bool r1 = cw_rcur != 0.0;
-#else
-#ifndef LRS_LAT_SPEC
     if (ctrl[C_ACT2] == 0.0) return;
-#endif
     const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
     const bool r1 = ctrl[C_RCUR] != 0.0;
-#endif
     const double *__restrict__ R = (r1 ? Rb1 : Rb0) + foff;
     double *__restrict__ Rn = (r1 ? Rb0 : Rb1) + foff;
     const double *__restrict__ D = Dall + foff;
@@ -2845,19 +2730,9 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
     int sd = 0;
     double svd = 0.0, bqd = 0.0;
     double2 s1d = make_double2(0.0, -1.0), l1d = s1d, rad = make_double2(0.0, 0.0), rbd = rad;
-#ifdef LRS_LAT_SPEC
-    // the row waves' operand rows from BOTH buffers of every double-buffered array, issued
-    // before the control words arrive (the buffer choice is control state); picked after
-    double riB[E], goB[E], sovB[E], yovB[E], rjpB[NO][E];
-    const double *__restrict__ RA = Rb0 + foff, *__restrict__ RB = Rb1 + foff;
-#else
     const double *__restrict__ RA = R;
-#endif
     if (ctrl_wave) {
         // ---- control wave: line search (ALMLineSearch lorads_alm.c:266-333)
-#if defined(LRS_KARG_PIN2) && defined(LRS_LAT_SPEC)
-        LRS_B_PIN2();
-#endif
         double sA[7];
         sum_partials<7>(pa, nblkA, sA);
         if (nblkB > 0) {
@@ -2884,22 +2759,10 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
 #endif
     } else {
         // ---- row waves: prefetch, one memory trip per dependency level, clamped loads
-#ifdef LRS_LAT_SPEC
-        ld_row<E>(RA + oi, ri);
-        ld_row<E>(RB + oi, riB);
-        ld_row<E>(D + oi, di);
-        ld_row<E>(G0 + foff + oi, go);
-        ld_row<E>(G1 + foff + oi, goB);
-        if (two) {
-            ld_row<E>(s0 + foff + oi, sov); ld_row<E>(s1 + foff + oi, sovB);
-            ld_row<E>(y0 + foff + oi, yov); ld_row<E>(y1 + foff + oi, yovB);
-        }
-#else
         ld_row<E>(R + oi, ri);
         ld_row<E>(D + oi, di);
         ld_row<E>(Gold + oi, go);
         if (two) { ld_row<E>(so + oi, sov); ld_row<E>(yo + oi, yov); }
-#endif
         // entries of this group: the row's adjacency (a dense row's own group: none, it only
         // updates R), or its slice of a dense row (no diagonal special case there)
         int eb = kb, nt = valid ? ke - kb : 0;
@@ -2928,9 +2791,6 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
             lw[u] = eb + u + (past ? 1 : 0) < kl;
             const long oj = (long)(u < no ? j : ic) * ld + lane * E;
             ld_row<E>(RA + oj, rjp[u]);
-#ifdef LRS_LAT_SPEC
-            ld_row<E>(RB + oj, rjpB[u]);
-#endif
             ld_row<E>(D + oj, djp[u]);
             sv[u] = Craw[ss[u]];
             s1v[u] = slot1[ss[u]];
@@ -2942,29 +2802,6 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
         // slots without a single constraint read the row's own (spread, cached) index instead
         // of a common one: no hot line shared by every lane
         const int ispare = min(ic, m - 1);
-#ifdef LRS_LAT_SKIPREC
-#pragma unroll
-        for (int u = 0; u < NO; ++u) {
-            const int c1 = (int)s1v[u].y, cl = (int)l1v[u].y;
-            ra[u] = rb[u] = make_double2(0.0, 0.0);
-            bq[u] = 0.0;
-            if (c1 >= 0) {
-                const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
-                ra[u] = r[0];
-                rb[u] = r[1];
-            }
-            if (cl >= 0) bq[u] = b[cl];
-        }
-        {
-            const int c1 = (int)s1d.y, cl = (int)l1d.y;
-            if (c1 >= 0) {
-                const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
-                rad = r[0];
-                rbd = r[1];
-            }
-            if (cl >= 0) bqd = b[cl];
-            (void)ispare;
-#else
 #pragma unroll
         for (int u = 0; u < NO; ++u) {
             const int c1 = (int)s1v[u].y >= 0 ? (int)s1v[u].y : ispare;
@@ -2981,7 +2818,6 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
             rad = r[0];
             rbd = r[1];
             bqd = b[cl];
-#endif
         }
 #ifdef LRS_PHASE_TIMING
         if (blockIdx.x == 0 && threadIdx.x == 0 && ri[0] != 12345.678 && sv[0] != 12345.678)
@@ -2989,26 +2825,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
         if (blockIdx.x == 0 && threadIdx.x == 0 && bq[0] != 12345.678 && ra[0].x != 12345.678 && rjp[0][0] != 12345.678)
             g_phase_tmp[2][6] = wall_clock64();
 #endif
-#if defined(LRS_KARG_PIN2) && defined(LRS_LAT_SPEC)
-        LRS_B_PIN2();
-#endif
     }
-#ifdef LRS_LAT_SPEC
-    if (ctrl[C_ACT2] == 0.0) return;   // block-uniform
-    if (!ctrl_wave) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            ri[e] = r1 ? riB[e] : ri[e];
-            go[e] = gcur != 0 ? goB[e] : go[e];
-            sov[e] = h == 0 ? sovB[e] : sov[e];   // so = s_{1-h}
-            yov[e] = h == 0 ? yovB[e] : yov[e];
-        }
-#pragma unroll
-        for (int u = 0; u < NO; ++u)
-#pragma unroll
-            for (int e = 0; e < E; ++e) rjp[u][e] = r1 ? rjpB[u][e] : rjp[u][e];
-    }
-#endif
     __syncthreads();
     LRS_TS(2, 2);
     if (pblk_off == 0 && blockIdx.x == 0 && threadIdx.x < LS_N) ls_cur[threadIdx.x] = ls[threadIdx.x];
@@ -3444,134 +3261,6 @@ __global__ void __launch_bounds__(NT) k_tile_a(
     write_partials_range<8, NT>(acc, partA, pblk_off + blockIdx.x, 0, 7);
 }
 
-// k_tile_a with its factor tiles staged by direct global -> LDS loads (global_load_lds_dwordx4,
-// no VGPR destination) into TWO buffers of kGc-column chunks, so that chunk k + 1's loads are in
-// flight while chunk k is computed (k_tile_a stages through registers, one chunk at a time: its
-// register prefetch spills at 1 024 threads, and its waves wait on memory for ~65 % of their
-// cycles, profiles/r03aa_c5_tile_counters.md).  LDS image: per operand kAuvT rows of kGc doubles
-// (128 B), a row's eight 16-B units XOR-swizzled by (row & 7) through the global addresses (the
-// LDS side of global_load_lds is lane-linear), so the 16 lanes of a ds_read_b128 phase reading
-// 16 rows at one logical unit spread over the banks.  Per slot and chunk the arithmetic and its
-// order are k_tile_a's (auv_chunk<2>), so the values are bitwise equal.  Needs ld % kGc == 0 (a
-// chunk never crosses a row; columns in [r, ld) are the factor's zero padding).
-typedef __attribute__((address_space(1))) void lrs_gvoid;
-typedef __attribute__((address_space(3))) void lrs_lvoid;
-constexpr int kGc = 16;               // columns per staged chunk
-constexpr int kGu = kGc / 2;          // 16-B units per staged row
-constexpr int kGop = kAuvT * kGc;     // doubles per staged operand
-template <int NT, int NA>
-__device__ __forceinline__ void tg_stage(double *buf, int I0, int J0, int c0, int n, int ld,
-                                         const double *__restrict__ X, const double *__restrict__ Y) {
-    constexpr int NW = NT / 64, NP = NA * kAuvT / 8;   // 1-KB pieces (8 rows) of the NA operands
-    static_assert(NP % NW == 0, "tg_stage: pieces divide over the waves");
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int q = 0; q < NP / NW; ++q) {
-        const int pc = w + q * NW;
-        const int a = pc / (kAuvT / 8), r0 = (pc % (kAuvT / 8)) * 8;
-        const int row = r0 + (lane >> 3), u = (lane & 7) ^ (row & 7);
-        const int grow = min(((a & 1) ? J0 : I0) + row, n - 1);   // rows past n: any valid row (never read)
-        const double *src = ((a < 2) ? X : Y) + (long)grow * ld + c0 + 2 * u;
-        __builtin_amdgcn_global_load_lds((lrs_gvoid *)src, (lrs_lvoid *)(buf + a * kGop + r0 * kGc), 16, 0, 0);
-    }
-}
-// one staged chunk of slot (pl, ql): auv_chunk<2>'s sums over the logical units in order
-__device__ __forceinline__ void tg_chunk2(const double *buf, int pl, int ql, double &s, double &s2) {
-    const double2 *xa = reinterpret_cast<const double2 *>(buf + pl * kGc);
-    const double2 *xb = reinterpret_cast<const double2 *>(buf + kGop + ql * kGc);
-    const double2 *ya = reinterpret_cast<const double2 *>(buf + 2 * kGop + pl * kGc);
-    const double2 *yb = reinterpret_cast<const double2 *>(buf + 3 * kGop + ql * kGc);
-    const int sp = pl & 7, sq = ql & 7;
-#pragma unroll 2
-    for (int u = 0; u < kGu; ++u) {   // not fully unrolled: the swizzled addresses are per unit
-        const double2 a = xa[u ^ sp], b = xb[u ^ sq], ay = ya[u ^ sp], by = yb[u ^ sq];
-        s += a.x * by.x + b.x * ay.x;
-        s += a.y * by.y + b.y * ay.y;
-        s2 += ay.x * by.x;
-        s2 += ay.y * by.y;
-    }
-}
-template <int NT>
-__global__ void __launch_bounds__(NT) k_tile_a_g(
-    int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
-    const int *__restrict__ tslot, const double *__restrict__ Cw, const double *__restrict__ Rb0,
-    const double *__restrict__ Rb1, const double *__restrict__ Dall, double *__restrict__ uRD,
-    double *__restrict__ uDD, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
-    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
-    const double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec,
-    const double *__restrict__ par, const double *__restrict__ ctrl_cur, double *__restrict__ partA, int pblk_off,
-    double2 *__restrict__ uvp) {
-    constexpr int NPT = kAuvItem / NT;
-    static_assert(NPT * NT == kAuvItem, "k_tile_a_g: items divide over the block");
-    if (ctrl_cur[C_ACTIVE] == 0.0) return;
-    const double *__restrict__ R = (ctrl_cur[C_RCUR] == 0.0 ? Rb0 : Rb1) + foff;
-    const double *__restrict__ D = Dall + foff;
-    const double rho = par[P_RHO], rhoInv = 1.0 / rho;
-    __shared__ double tg[2 * 4 * kGop];   // 128 KB: two buffers of R_I, R_J, D_I, D_J chunks
-    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int nch = (r + kGc - 1) / kGc;
-    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
-        const int4 it = items[itx];
-        const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
-        int pl[NPT], ql[NPT];
-        double s0[NPT], s1[NPT];
-#pragma unroll
-        for (int j = 0; j < NPT; ++j) {
-            const int t = eb + (int)threadIdx.x + j * NT;
-            const unsigned w = t < ee ? pq[t] : 0u;
-            pl[j] = (int)(w >> 16);
-            ql[j] = (int)(w & 0xffffu);
-            s0[j] = 0.0;
-            s1[j] = 0.0;
-        }
-        __syncthreads();   // the previous item's reads of buffer 0 are done
-        tg_stage<NT, 4>(tg, I0, J0, 0, n, ld, R, D);
-        for (int k = 0; k < nch; ++k) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();   // chunk k landed for every wave; buffer (k + 1) & 1 is free
-            if (k + 1 < nch) tg_stage<NT, 4>(tg + ((k + 1) & 1) * 4 * kGop, I0, J0, (k + 1) * kGc, n, ld, R, D);
-            const double *buf = tg + (k & 1) * 4 * kGop;
-#pragma unroll
-            for (int j = 0; j < NPT; ++j) {
-                if (eb + (int)threadIdx.x + j * NT >= ee) break;
-                tg_chunk2(buf, pl[j], ql[j], s0[j], s1[j]);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < NPT; ++j) {
-            const int t = eb + (int)threadIdx.x + j * NT;
-            if (t >= ee) break;
-            const int sl = tslot[t];
-            const double d0 = 0.5 * s0[j], d1 = s1[j];
-            if (uvp) {
-                uvp[sl] = make_double2(d0, d1);
-            } else {
-                uRD[sl] = d0;
-                uDD[sl] = d1;
-            }
-            const double cwl = Cw[sl];
-            acc[0] += cwl * d0;
-            acc[1] += cwl * d1;
-            const double2 l1l = loc1[sl];
-            const int c1 = (int)l1l.y;
-            const int e0 = c1 == -2 ? loc_ptr[sl] : 0, e1 = c1 == -2 ? loc_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
-            for (int e = e0; e < e1; ++e) {
-                const int ci = c1 >= 0 ? c1 : loc_con[e];
-                const double w = c1 >= 0 ? l1l.x : loc_w[e];
-                const double bi = b[ci], cvi = cvs[ci], li = lam[ci];
-                const double q1 = 2.0 * (w * d0), q2 = w * d1;
-                const double q0 = (bi - cvi) + rhoInv * li;
-                acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1;
-                acc[6] += q0 * q1;
-                double2 *rr = reinterpret_cast<double2 *>(rec + 4L * ci);
-                rr[0] = make_double2(cvi, q1);
-                rr[1] = make_double2(q2, (-li) + (-rho) * bi);
-            }
-        }
-    }
-    write_partials_range<8, NT>(acc, partA, pblk_off + blockIdx.x, 0, 7);
-}
-
 // row epilogue of stage B: G_new = 2 (S R_new [+ C R_new]), s = tau D, y = G_new - G_old
 // (setlbfgsHisTwo lorads_alm.c:842-863) and the nine L-BFGS dots
 template <int E>
@@ -3854,186 +3543,6 @@ __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: tw
     write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
 }
 
-// one staged chunk of entry (pl, ql) over two staged operands: auv_chunk<1>'s sums in order
-__device__ __forceinline__ void tg_chunk1(const double *buf, int pl, int ql, double &s) {
-    const double2 *xa = reinterpret_cast<const double2 *>(buf + pl * kGc);
-    const double2 *xb = reinterpret_cast<const double2 *>(buf + kGop + ql * kGc);
-    const int sp = pl & 7, sq = ql & 7;
-#pragma unroll 2
-    for (int u = 0; u < kGu; ++u) {
-        const double2 a = xa[u ^ sp], b = xb[u ^ sq];
-        s += a.x * b.x;
-        s += a.y * b.y;
-    }
-}
-// k_tile_b1 with the R_new tiles staged by direct global -> LDS loads into two buffers (as
-// k_tile_a_g; same arithmetic and order as k_tile_b1, bitwise equal)
-__global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1_g(   // <= 128 VGPRs: two blocks a CU (68 KB LDS each)
-    int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
-    const int *__restrict__ tslot, const double *Rb0, const double *Rb1, double *__restrict__ uRR,
-    double *__restrict__ Sv, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
-    const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double2 *__restrict__ slot1,
-    const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
-    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
-    double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
-    const double *__restrict__ ls_cur, double *__restrict__ partC, int pblk_off) {
-    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
-    const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
-    const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
-    __shared__ double tg[2 * 2 * kGop];   // 64 KB: two buffers of R_new,I and R_new,J chunks
-    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const int nch = (r + kGc - 1) / kGc;
-    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
-        const int4 it = items[itx];
-        const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
-        int pl[kAuvNpt], ql[kAuvNpt];
-        double dv[kAuvNpt];
-#pragma unroll
-        for (int j = 0; j < kAuvNpt; ++j) {
-            const int t = eb + (int)threadIdx.x + j * kAuvThreads;
-            const unsigned w = t < ee ? pq[t] : 0u;
-            pl[j] = (int)(w >> 16);
-            ql[j] = (int)(w & 0xffffu);
-            dv[j] = 0.0;
-        }
-        __syncthreads();   // the previous item's reads of buffer 0 are done
-        tg_stage<kRowBlock, 2>(tg, I0, J0, 0, n, ld, Rn, Rn);
-        for (int k = 0; k < nch; ++k) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();   // chunk k landed for every wave; buffer (k + 1) & 1 is free
-            if (k + 1 < nch) tg_stage<kRowBlock, 2>(tg + ((k + 1) & 1) * 2 * kGop, I0, J0, (k + 1) * kGc, n, ld, Rn, Rn);
-            const double *buf = tg + (k & 1) * 2 * kGop;
-#pragma unroll
-            for (int j = 0; j < kAuvNpt; ++j) {
-                if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
-                tg_chunk1(buf, pl[j], ql[j], dv[j]);
-            }
-        }
-        // the slot epilogue, kB1H slots at a time with their loads issued before the arithmetic
-        // (branch-free indices: entries past the item read the item's first slot, store nothing)
-        constexpr int kB1H = 4;
-#pragma unroll
-        for (int h = 0; h < kAuvNpt; h += kB1H) {
-        int slv[kB1H];
-        double2 s1v[kB1H], l1v[kB1H];
-        double crv[kB1H];
-#pragma unroll
-        for (int j = 0; j < kB1H; ++j) {
-            const int t = eb + (int)threadIdx.x + (h + j) * kAuvThreads;
-            slv[j] = tslot[t < ee ? t : eb];
-        }
-#pragma unroll
-        for (int j = 0; j < kB1H; ++j) {
-            s1v[j] = slot1[slv[j]];
-            l1v[j] = loc1[slv[j]];
-            crv[j] = Craw[slv[j]];
-        }
-        double2 rav[kB1H], rbv[kB1H];
-#pragma unroll
-        for (int j = 0; j < kB1H; ++j) {
-            const int c1 = (int)s1v[j].y;
-            const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * (c1 >= 0 ? c1 : 0));
-            rav[j] = q[0];
-            rbv[j] = q[1];
-        }
-#pragma unroll
-        for (int j = 0; j < kB1H; ++j) {
-            const int t = eb + (int)threadIdx.x + (h + j) * kAuvThreads;
-            if (t >= ee) break;
-            const int sl = slv[j];
-            double svl = crv[j];
-            const double2 s1l = s1v[j];
-            const int c1 = (int)s1l.y;
-            if (c1 >= 0) {
-                double cv = rav[j].x + tau * rav[j].y;
-                cv = cv + tau2 * rbv[j].x;
-                svl += (rbv[j].y + rho * cv) * s1l.x;
-            } else if (c1 == -2) {
-                for (int e = slot_ptr[sl]; e < slot_ptr[sl + 1]; ++e) {
-                    const double2 *q = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
-                    const double2 x = q[0], y = q[1];
-                    double cv = x.x + tau * x.y;
-                    cv = cv + tau2 * y.x;
-                    svl += (y.y + rho * cv) * slot_a[e];
-                }
-            }
-            Sv[sl] = svl;
-            const double d = dv[h + j];
-            uRR[sl] = d;
-            const double2 l1l = l1v[j];
-            const int cl = (int)l1l.y;
-            const int f0 = cl == -2 ? loc_ptr[sl] : 0, f1 = cl == -2 ? loc_ptr[sl + 1] : (cl >= 0 ? 1 : 0);
-            for (int e = f0; e < f1; ++e) {
-                const int ci = cl >= 0 ? cl : loc_con[e];
-                const double tot = (cl >= 0 ? l1l.x : loc_w[e]) * d;
-                cvs[ci] = tot;
-                const double dd = b[ci] - tot;
-                acc[9] += dd * dd;
-            }
-        }
-        }
-    }
-    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
-}
-
-// k_auv_tile staged by direct global -> LDS loads into two buffers (as k_tile_a_g): MODE 1
-// X_p . X_q, MODE 0 (X_p . Y_q + X_q . Y_p) / 2, per constraint entry, same order of sums
-__device__ __forceinline__ void tg_chunk0(const double *buf, int pl, int ql, double &s) {
-    const double2 *xa = reinterpret_cast<const double2 *>(buf + pl * kGc);
-    const double2 *xb = reinterpret_cast<const double2 *>(buf + kGop + ql * kGc);
-    const double2 *ya = reinterpret_cast<const double2 *>(buf + 2 * kGop + pl * kGc);
-    const double2 *yb = reinterpret_cast<const double2 *>(buf + 3 * kGop + ql * kGc);
-    const int sp = pl & 7, sq = ql & 7;
-#pragma unroll 2
-    for (int u = 0; u < kGu; ++u) {
-        const double2 a = xa[u ^ sp], b = xb[u ^ sq], ay = ya[u ^ sp], by = yb[u ^ sq];
-        s += a.x * by.x + b.x * ay.x;
-        s += a.y * by.y + b.y * ay.y;
-    }
-}
-template <int MODE>
-__global__ void __launch_bounds__(kAuvThreads) k_auv_tile_g(int n, int r, int ld, const int4 *__restrict__ items,
-                                                            const unsigned *__restrict__ pq,
-                                                            const int *__restrict__ ent, const double *__restrict__ X,
-                                                            const double *__restrict__ Y, double *__restrict__ val,
-                                                            const double *__restrict__ guard) {
-    if (guard && guard[0] == 0.0) return;
-    constexpr int NA = MODE == 0 ? 4 : 2;
-    __shared__ double tg[2 * NA * kGop];
-    const int4 it = items[blockIdx.x];
-    const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
-    int pl[kAuvNpt], ql[kAuvNpt];
-    double acc[kAuvNpt];
-#pragma unroll
-    for (int j = 0; j < kAuvNpt; ++j) {
-        const int t = eb + (int)threadIdx.x + j * kAuvThreads;
-        const unsigned w = t < ee ? pq[t] : 0u;
-        pl[j] = (int)(w >> 16);
-        ql[j] = (int)(w & 0xffffu);
-        acc[j] = 0.0;
-    }
-    const int nch = (r + kGc - 1) / kGc;
-    __syncthreads();
-    tg_stage<kAuvThreads, NA>(tg, I0, J0, 0, n, ld, X, Y);
-    for (int k = 0; k < nch; ++k) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (k + 1 < nch) tg_stage<kAuvThreads, NA>(tg + ((k + 1) & 1) * NA * kGop, I0, J0, (k + 1) * kGc, n, ld, X, Y);
-        const double *buf = tg + (k & 1) * NA * kGop;
-#pragma unroll
-        for (int j = 0; j < kAuvNpt; ++j) {
-            if (eb + (int)threadIdx.x + j * kAuvThreads >= ee) break;
-            if constexpr (MODE == 1) tg_chunk1(buf, pl[j], ql[j], acc[j]);
-            else tg_chunk0(buf, pl[j], ql[j], acc[j]);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < kAuvNpt; ++j) {
-        const int t = eb + (int)threadIdx.x + j * kAuvThreads;
-        if (t < ee) val[ent[t]] = MODE == 0 ? 0.5 * acc[j] : acc[j];
-    }
-}
-
 constexpr int kTbC = 64;            // R_new columns staged per pass in k_tile_b2
 // LDS row stride: unpadded, so every staged row starts on bank 0 and the two rows a
 // ds_read_b128 service group mixes ({0-3,12-15} of one 16-lane row, {20-27} of the next,
@@ -4165,171 +3674,10 @@ __global__ void __launch_bounds__(kRowBlock) k_tile_b2(int n, int ld, long foff,
     }
 }
 
-// Stage B's long-row half in ONE pass over the tiles (cones with r <= kTxC; replaces k_tile_b1's
-// A(R_new R_new^T) and k_tile_b2's S R_new): block (row tile I, column group x) stages R_new of
-// each column tile J of its group whole (128 columns), and a
-// group of kTxL lanes takes kTxRows rows of the tile; lane l holds columns 2l, 2l+1, 64+2l, 65+2l
-// (two conflict-free 256-B row reads per 16 lanes).  A row's entries come 16 at a time, lane k
-// of each 16-lane half loading entry k's column, slot and S (from k_slot_sv), broadcast by DPP
-// row_newbcast; per entry the lane adds S_ij R_new,j to its four gradient columns and keeps its
-// four-column part of R_new,i . R_new,j, and after the batch a transposed butterfly over the 16
-// lanes (mirror, half-mirror, quad swaps: each step halves the values a lane holds) plus one
-// exchange between the halves leaves entry k's dot product in lane k -- which stores it when the
-// entry is a lower slot of its row (the slot's owner row; each lower slot once) with the local
-// constraints' new A(.) and residual (ALMupdateVar lorads_alm.c:826-830, as k_tile_b1).
-constexpr int kTxC = 128;                        // columns staged: the whole row (r <= 128)
-constexpr int kTxS = kTxC + 2;                   // LDS row stride (16-B aligned rows)
-constexpr int kTxT = 1024;                       // threads
-constexpr int kTxL = 32;                         // lanes per tile row, four columns each
-constexpr int kTxG = kTxT / kTxL;                // row groups
-constexpr int kTxRows = kAuvT / kTxG;            // rows per group
-constexpr int kTxPer = kAuvT * kTxC / 2 / kTxT;  // double2 per thread per staged tile
-static_assert(kTxL == 32 && kTxC == 4 * kTxL, "k_tile_bx: two 16-lane halves, four columns a lane");
-__device__ __forceinline__ void tx_fetch(double2 (&v)[kTxPer], int J0, int n, int r, int ld,
-                                         const double *__restrict__ Rn) {
-#pragma unroll
-    for (int k = 0; k < kTxPer; ++k) {
-        const int y = threadIdx.x + k * kTxT;
-        const int grow = J0 + y / (kTxC / 2), col = 2 * (y % (kTxC / 2));
-        double2 t = make_double2(0.0, 0.0);
-        if (grow < n && col < r) {
-            t = *reinterpret_cast<const double2 *>(Rn + (long)grow * ld + col);
-            if (col + 1 >= r) t.y = 0.0;
-        }
-        v[k] = t;
-    }
-}
-template <bool DOT, int K>
-__device__ __forceinline__ void bx_entry(const double *rj, int l, int colv, double sv, double (&g)[4],
-                                         const double2 &ra, const double2 &rb, double (&pd)[16]) {
-    const int j = nbc_i<K>(colv);
-    const double s = dpp_mov<0x150 + K>(sv);
-    const double2 *p = reinterpret_cast<const double2 *>(&rj[j * kTxS]) + l;
-    const double2 a0 = p[0], a1 = p[kTxL];
-    g[0] += s * a0.x; g[1] += s * a0.y; g[2] += s * a1.x; g[3] += s * a1.y;
-    if constexpr (DOT) pd[K] = ra.x * a0.x + ra.y * a0.y + rb.x * a1.x + rb.y * a1.y;
-}
-template <bool DOT, int... K>
-__device__ __forceinline__ void bx_batch(std::integer_sequence<int, K...>, int kmax, const double *rj, int l,
-                                         int colv, double sv, double (&g)[4], const double2 &ra, const double2 &rb,
-                                         double (&pd)[16]) {
-    ((K < kmax ? bx_entry<DOT, K>(rj, l, colv, sv, g, ra, rb, pd) : void(pd[K] = 0.0)), ...);
-}
-// one butterfly step: pairs differ in lane bit B (CTRL the DPP pairing), a lane keeps the half
-// of its N values its bit selects and adds its partner's copy of them
-template <int N, int CTRL>
-__device__ __forceinline__ void bx_halve(double (&v)[16], bool hi) {
-#pragma unroll
-    for (int m = 0; m < N / 2; ++m) {
-        const double keep = hi ? v[m + N / 2] : v[m], send = hi ? v[m] : v[m + N / 2];
-        v[m] = keep + dpp_mov<CTRL>(send);
-    }
-}
-__global__ void __launch_bounds__(kTxT) k_tile_bx(
-    int n, int r, int ld, long foff, const int2 *__restrict__ blk, const int2 *__restrict__ tp,
-    const int *__restrict__ rp, const int2 *__restrict__ ent, const double *__restrict__ Sv, const double *Rb0,
-    const double *Rb1, double *__restrict__ GP, long gstride, const double *__restrict__ ctrl,
-    const double *__restrict__ ls_cur, int tI0, double *__restrict__ uRR, const int *__restrict__ loc_ptr,
-    const int *__restrict__ loc_con, const double *__restrict__ loc_w, const double2 *__restrict__ loc1,
-    const double *__restrict__ b, double *__restrict__ cvs, double *__restrict__ partC, int pblk_off) {
-    if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
-    const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
-    __shared__ double rj[kAuvT * kTxS];
-    const int bx = blockIdx.x;
-    const int I = tI0 + bx / kNX, x = bx % kNX;   // tI0: a shard's first owned row tile
-    const int grp = threadIdx.x / kTxL, l = threadIdx.x % kTxL, k16 = l & 15;
-    const int2 br = blk[bx];
-    double g[kTxRows][4];
-#pragma unroll
-    for (int w = 0; w < kTxRows; ++w)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) g[w][c] = 0.0;
-    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int q = br.x; q < br.y; ++q) {   // block-uniform
-        // the tile staged after the barrier (no register prefetch: the 16 partial dots of a
-        // batch and four rows' gradient columns take the registers)
-        const int2 cur = tp[q];
-        {
-            double2 pre[kTxPer];
-            tx_fetch(pre, cur.x, n, r, ld, Rn);
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < kTxPer; ++k) {
-                const int y = threadIdx.x + k * kTxT;
-                *reinterpret_cast<double2 *>(&rj[(y / (kTxC / 2)) * kTxS + 2 * (y % (kTxC / 2))]) = pre[k];
-            }
-            __syncthreads();
-        }
-        const int J0 = cur.x;
-        const bool lower = J0 <= I * kAuvT;   // the diagonal tile pair and those left of it hold lower slots
-#pragma unroll
-        for (int w = 0; w < kTxRows; ++w) {
-            const int pl = grp + w * kTxG, i = I * kAuvT + pl;
-            const int e0 = rp[cur.y + pl], e1 = rp[cur.y + pl + 1];
-            double2 ra = make_double2(0.0, 0.0), rb = make_double2(0.0, 0.0);   // row i's own R_new
-            if (e0 < e1 && i < n) {
-                const double *ri = Rn + (long)i * ld;
-                if (2 * l < r) { ra = *reinterpret_cast<const double2 *>(ri + 2 * l); if (2 * l + 1 >= r) ra.y = 0.0; }
-                if (2 * (l + kTxL) < r) {
-                    rb = *reinterpret_cast<const double2 *>(ri + 2 * (l + kTxL));
-                    if (2 * (l + kTxL) + 1 >= r) rb.y = 0.0;
-                }
-            }
-            for (int base = e0;; base += 16) {   // wave-uniform: the wave's two rows, 16 entries at a time
-                int rem = e1 - base;
-                rem = rem < 0 ? 0 : (rem > 16 ? 16 : rem);
-                const int kmax = max(__builtin_amdgcn_readlane(rem, 0), __builtin_amdgcn_readlane(rem, 32));
-                if (kmax == 0) break;
-                const int e = base + k16;
-                const bool ok = k16 < rem;
-                const int2 en = ent[ok ? e : (e0 < e1 ? e0 : 0)];
-                const double sv = ok ? Sv[en.y] : 0.0;
-                double pd[16];
-                if (!lower) {   // a tile pair above the diagonal: no lower slot of these rows
-                    bx_batch<false>(std::make_integer_sequence<int, 16>{}, kmax, rj, l, en.x, sv, g[w], ra, rb, pd);
-                    if (kmax < 16) break;
-                    continue;
-                }
-                bx_batch<true>(std::make_integer_sequence<int, 16>{}, kmax, rj, l, en.x, sv, g[w], ra, rb, pd);
-                // entry k16's dot into lane k16 of each half, then the two halves' sum
-                bx_halve<16, 0x140>(pd, (k16 & 8) != 0);   // row_mirror: partner differs in bit 3
-                bx_halve<8, 0x141>(pd, (k16 & 4) != 0);    // row_half_mirror: bit 2
-                bx_halve<4, 0x4E>(pd, (k16 & 2) != 0);     // quad_perm [2,3,0,1]: bit 1
-                bx_halve<2, 0xB1>(pd, (k16 & 1) != 0);     // quad_perm [1,0,3,2]: bit 0
-                const double d = pd[0] + __shfl_xor(pd[0], 16, 64);
-                if (l < 16 && ok && J0 + en.x <= i) {   // a lower slot of row i: its owner
-                    uRR[en.y] = d;
-                    const double2 l1l = loc1[en.y];
-                    const int cl = (int)l1l.y;
-                    const int f0 = cl == -2 ? loc_ptr[en.y] : 0, f1 = cl == -2 ? loc_ptr[en.y + 1] : (cl >= 0 ? 1 : 0);
-                    for (int f = f0; f < f1; ++f) {
-                        const int ci = cl >= 0 ? cl : loc_con[f];
-                        const double tot = (cl >= 0 ? l1l.x : loc_w[f]) * d;
-                        cvs[ci] = tot;
-                        const double dd = b[ci] - tot;
-                        acc[9] += dd * dd;
-                    }
-                }
-                if (kmax < 16) break;
-            }
-        }
-    }
-#pragma unroll
-    for (int w = 0; w < kTxRows; ++w) {
-        const int i = I * kAuvT + grp + w * kTxG;
-        if (i < n) {
-            double2 *dst = reinterpret_cast<double2 *>(GP + x * gstride + foff + (long)i * ld) + l;
-            if (2 * l < ld) dst[0] = make_double2(g[w][0], g[w][1]);
-            if (2 * (l + kTxL) < ld) dst[kTxL] = make_double2(g[w][2], g[w][3]);
-        }
-    }
-    write_partials<10, kTxT>(acc, partC, pblk_off + blockIdx.x);
-}
-
 // Sharded long-row B over the tiles: S = C + A^*(M1) (k_tile_b1's slot epilogue, lorads_alm.c:38-57)
 // on the slots whose lower row is a halo row -- k_tile_b2 reads them as owned rows' upper entries;
 // their A(R_new R_new^T) belongs to the shard owning the lower row.
-// sx == nullptr: the slots [s0, s0 + nx) (every slot of a cone, k_tile_bx's S); partZ: this
+// sx == nullptr: the slots [s0, s0 + nx) (every slot of a cone); partZ: this
 // launch's partial blocks of stage B (pblk_off on) written as zeros, the partial slots it stands in for.
 __global__ void __launch_bounds__(kBlock) k_slot_sv(int nx, const int *__restrict__ sx, int s0, double *__restrict__ Sv,
                                                     const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
@@ -5110,17 +4458,7 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
     double *fin = tmpfin_ptr() + TF_GATHER;
     if (c.auv_items > 0 && !P.shard) {
         // 2-D tiles through LDS, then the per-constraint sums
-        static const int glds = getenv("LRS_TILE_GLDS") ? atoi(getenv("LRS_TILE_GLDS")) : 0;
-        if (glds && c.ld % kGc == 0) {
-            if (mode == 1)
-                hipLaunchKernelGGL((k_auv_tile_g<1>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
-                                   reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Xc, c.auv_val,
-                                   guard);
-            else
-                hipLaunchKernelGGL((k_auv_tile_g<0>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
-                                   reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Yc, c.auv_val,
-                                   guard);
-        } else if (mode == 1)
+        if (mode == 1)
             hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.auv_xo ? kXcdBands * c.auv_xmax : c.auv_items), dim3(kAuvThreads),
                                0, st, c.n, c.r, c.ld, c.auv_items, reinterpret_cast<const int4 *>(c.auv_item), c.auv_xo,
                                c.auv_pq, c.auv_pos, Xc, Xc, c.auv_val, guard);
@@ -6106,18 +5444,10 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         if (tlb[k]) nblkB += pb[k].grid;
     }
     // long-row B over 2-D LDS tiles (k_tile_b1 / k_tile_b2, then k_wide_bf's epilogue blocks)
-    bool tbt[kMaxCones], tbx[kMaxCones];
+    bool tbt[kMaxCones];
     for (int k = 0; k < KL; ++k) {
         tbt[k] = !merge && !tlb[k] && pb[k].wide && W.GP && cone_of(k).sb_blocks > 0 && cone_of(k).sa_items > 0;
         if (tbt[k]) nblkB += pb[k].grid;
-    }
-    // r <= 128, LRS_TILE_BX=1 at upload: the single-pass k_tile_bx (S per slot by k_slot_sv
-    // first) instead of b1 + b2, its blocks' partials after k_wide_bf's (C5: 729 + 144 us against
-    // 451 + ~400 us for the two-kernel form; opt-in)
-    int offBX = nblkB;
-    for (int k = 0; k < KL; ++k) {
-        tbx[k] = tbt[k] && P.tile_bx && cone_of(k).ld <= kTxC;
-        if (tbx[k]) nblkB += cone_of(k).sb_blocks;
     }
     if (nblkB > kMaxPartialBlocks) {
         snprintf(g_err, sizeof(g_err), "stage B: %d partial blocks past %d", nblkB, kMaxPartialBlocks);
@@ -6259,15 +5589,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2, W.D,      \
                        W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), \
                        P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, uvp, c.sa_xo)
-            // LRS_TILE_GLDS=1: the same work staged by direct global -> LDS loads (k_tile_a_g)
-            static const int glds = getenv("LRS_TILE_GLDS") ? atoi(getenv("LRS_TILE_GLDS")) : 0;
-            if (glds && c.ld % kGc == 0) {
-                hipLaunchKernelGGL(k_tile_a_g<1024>, dim3(grid), dim3(1024), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
-                                   reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2,
-                                   W.D, W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,
-                                   reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam, W.rec, W.par,
-                                   ctrl_cur, W.part, off, uvp);
-            } else if (nta == 512) LRS_TILE_A(512);
+            if (nta == 512) LRS_TILE_A(512);
             else LRS_TILE_A(1024);
 #undef LRS_TILE_A
         } else if (pa[k].wide) {
@@ -6376,34 +5698,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const DevCone &c = cone_of(k);
         const int grid = pb[k].grid;
         if (pb[k].small) { off += grid; continue; }
-        if (tbx[k]) {
-            hipLaunchKernelGGL(k_slot_sv, dim3(grid), dim3(kBlock), 0, st, c.P, nullptr, c.slot_off,
-                               c.sa_S - c.slot_off, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,
-                               reinterpret_cast<const double2 *>(P.slot1), W.rec, W.par, ctrl_cur, ls_cur, W.partC, off);
-            LRS_CHECK_LAUNCH();
-            hipLaunchKernelGGL(k_tile_bx, dim3(c.sb_blocks), dim3(kTxT), 0, st, c.n, c.r, c.ld, c.foff,
-                               reinterpret_cast<const int2 *>(c.sb_blk), reinterpret_cast<const int2 *>(c.sb_tp),
-                               c.sb_rp, reinterpret_cast<const int2 *>(c.sb_ent), c.sa_S - c.slot_off, W.R, W.R2,
-                               W.GP, P.NRpad, ctrl_cur, ls_cur, c.sb_I0, W.uvt2, P.loc_ptr, P.loc_con, P.loc_w,
-                               reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.partC, offBX);
-            LRS_CHECK_LAUNCH();
-            offBX += c.sb_blocks;
-            LRS_LAYOUT_SWITCH(c.G, c.E, {
-                hipLaunchKernelGGL((k_wide_bf<GG, EE>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff, W.D,
-                                   W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], ctrl_cur, ls_cur, L, W.partC,
-                                   offBF, c.row0, P.ndense ? W.CR : nullptr, W.CD, W.GP, P.NRpad);
-            });
-            offBF += grid;
-        } else if (tbt[k]) {
-            static const int glds_b = getenv("LRS_TILE_GLDS") ? atoi(getenv("LRS_TILE_GLDS")) : 0;
-            if (glds_b && c.ld % kGc == 0)
-                hipLaunchKernelGGL(k_tile_b1_g, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
-                                   reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, W.R, W.R2, W.uvt2,
-                                   c.sa_S - c.slot_off, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,
-                                   reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,
-                                   reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur,
-                                   W.partC, off);
-            else
+        if (tbt[k]) {
             hipLaunchKernelGGL(k_tile_b1, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
                                reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, W.R, W.R2, W.uvt2,
                                c.sa_S - c.slot_off, P.Craw, P.slot_ptr,
@@ -6876,12 +6171,8 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                         d[u] += rii[p].x * x[u][p].x;
                         d[u] += rii[p].y * x[u][p].y;
                     }
-#if defined(LRS_NO_BFLY)
-                    d[u] = group_sum<TPR>(d[u]);
-#endif
                 }
                 // lower entries: A(R R^T) on this row's slots (their constraints after the barrier)
-#ifndef LRS_NO_BFLY
                 if constexpr (TPR == 4) {
                     const double v = group_sum4<4>(d, sl_lane);   // lane u: entry u
                     const int u = sl_lane;
@@ -6895,12 +6186,6 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                         for (int u = 0; u < 4; ++u)
                             if (k + u < kl) XB[js[u].y] = d[u];
                 }
-#else
-                if (sl_lane == 0)
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (k + u < kl) XB[js[u].y] = d[u];
-#endif
             }
             LRS_SM_SUB(8, t_adj);
             if (!valid) continue;
@@ -7498,7 +6783,6 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
 #pragma unroll
                     for (int k = 0; k < EL; ++k) d[u] += xq[k] * Ys[j * rS + min(l + kScL * k, rS - 1)];
                 }
-#ifndef LRS_NO_BFLY
                 {
                     // entry u's total in lanes 4u..4u+3; lane 4u stores it
                     const double v = group_sum4<kScL>(d, l);
@@ -7506,14 +6790,6 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
                     const int pku = u == 0 ? pk[0] : (u == 1 ? pk[1] : (u == 2 ? pk[2] : pk[3]));
                     if ((l & 3) == 0 && e + u < e1) T[2 * (pku & 0xffff) + ((pku >> 16) <= i ? 0 : 1)] = v;
                 }
-#else
-#pragma unroll
-                for (int u = 0; u < 4; ++u) d[u] = group_sum<kScL>(d[u]);
-                if (l == 0)
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (e + u < e1) T[2 * (pk[u] & 0xffff) + ((pk[u] >> 16) <= i ? 0 : 1)] = d[u];
-#endif
             }
         }
     };

@@ -776,10 +776,6 @@ static bool upload_small_cg(const HostCone &c, int m, DevCone &d, std::string &e
 }
 
 bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
-    {   // k_tile_bx (lrs_kernels.hip): opt-in, read when a problem is uploaded
-        const char *e = getenv("LRS_TILE_BX");
-        dp.tile_bx = e && e[0] == '1';
-    }
     // per-cone scalars live in the fixed tmpfin slots (TF_SD + 2k < TF_GATHER)
     if (hp.K > kMaxCones) { err = "at most " + std::to_string(kMaxCones) + " SDP cones are supported"; return false; }
     dp.m = hp.m;

@@ -103,52 +103,6 @@ def test_sharded_c5_tiles_match_reference(mods, world, monkeypatch):
     check_trips(res, z, K)
 
 
-@pytest.mark.parametrize("name", ["mc_rand200", "theta40", "rsparse60", "mc_rand300w"])
-def test_single_pass_stage_b_matches_reference(mods, name, monkeypatch):
-    """Stage B's long-row half in one pass over the tiles (k_tile_bx, LRS_TILE_BX=1: S R_new and
-    A(R_new R_new^T) together, the dots through the transposed DPP butterfly), unsharded: the
-    reference's own K trips at 1e-9."""
-    solver, _ = mods
-    monkeypatch.setenv("LRS_SLOT_TILES", "1")
-    monkeypatch.setenv("LRS_TILE_BX", "1")
-    z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
-    rank = int(z["rank_flag"])
-    kw = {"reoptLevel": 0}
-    if rank > 0:
-        kw["fixedRank"] = rank
-    sv = solver.Solver(instance(name))
-    sv.set_kernel_path(3)
-    for K in [int(k) for k in z["ks"]]:
-        if z[f"K{K}_trips"].shape[0] < K:
-            continue
-        d = sv.alm_steps(K, **kw)
-        assert sv.tile_used()
-        check_trips([(None, ((0, 1), True), d)], z, K)
-    sv.close()
-
-
-@pytest.mark.parametrize("world", [1, 2])
-def test_single_pass_stage_b_c5(mods, world, monkeypatch):
-    """k_tile_b1 + k_tile_b2 replaced by k_tile_bx on the C5 structure (m = 10^5, tiles forced),
-    unsharded and over two shards: the reference's trips at 1e-9."""
-    solver, inst = mods
-    z = np.load(os.path.join(GOLDEN, "steps_c5_m1e5.npz"))
-    monkeypatch.setenv("LRS_SLOT_TILES", "1")
-    monkeypatch.setenv("LRS_TILE_BX", "1")
-    coo = inst.coo_arrays(inst.random_sparse_problem(10000, int(z["m"]), 6, 5))
-    kw = {"reoptLevel": 0, "fixedRank": int(z["rank_flag"])}
-    K = min(3, max(int(k) for k in z["ks"] if z[f"K{int(k)}_trips"].shape[0] >= int(k)))
-    if world == 1:
-        sv = solver.Solver(coo=coo)
-        sv.set_kernel_path(3)
-        d = sv.alm_steps(K, **kw)
-        res = [(None, (sv.tile_info(), sv.tile_used()), d)]
-        sv.close()
-    else:
-        res = run_sharded(solver, lambda: solver.Solver(coo=coo), world, lambda sv: sv.alm_steps(K, **kw), path=3)
-    check_trips(res, z, K)
-
-
 def test_rccl_transport_tiles_world1(mods, monkeypatch):
     """The RCCL transport (a one-rank communicator; LRS_FORCE_SHARD=1 keeps the sharded
     iteration with its halo exchange and all-reduces) over the tiled long-row stages on the C5
