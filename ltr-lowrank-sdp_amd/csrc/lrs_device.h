@@ -25,6 +25,7 @@ namespace lrs {
 
 constexpr int kBlock = 256;          // threads per block (4 waves)
 constexpr int kMaxPartialBlocks = 4096;
+constexpr int kFoldMinBlocks = 1024;   // stages with this many producer blocks fold their partials once (totals)
 constexpr int kMaxPartialVals = 16;
 
 // ---- ALM inner-loop control block (double array, double-buffered by iteration parity)

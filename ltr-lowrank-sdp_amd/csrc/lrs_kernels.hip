@@ -5516,11 +5516,18 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         }
     }
     // what the consumers read: every producer block's partials, or (sharded) the summed totals
-    double *totA = sh ? W.tot : nullptr, *totC = sh ? W.tot + 16 : nullptr;
-    const double *inC = sh ? totC : W.partC;
-    const int nC = sh ? 1 : nblkB, pstr = sh ? 1 : kMaxPartialBlocks;
-    const double *inA = sh ? totA : W.part;
-    const int nA = sh ? 1 : nblkA;
+    // Wide grids (the general kernels at G81 size: 2 500 blocks a stage) fold each stage's
+    // per-block partials once, into the stage totals (k_fold_partials, one workgroup, fixed block
+    // order), and the next stage's blocks read those totals.  Without the fold every consumer block
+    // re-reads every producer block's partials -- 2 500 x 2 500 x 10 doubles = 500 MB of L2 reads a
+    // launch -- before its rows can start.  Sharded solves always fold (the totals then take the
+    // all-reduce).  The latency kernels keep their control-wave reduction (<= 256 producers).
+    const bool totals = sh || (!lat && std::max(nblkA, nblkB) >= kFoldMinBlocks);
+    double *totA = totals ? W.tot : nullptr, *totC = totals ? W.tot + 16 : nullptr;
+    const double *inC = totals ? totC : W.partC;
+    const int nC = totals ? 1 : nblkB, pstr = totals ? 1 : kMaxPartialBlocks;
+    const double *inA = totals ? totA : W.part;
+    const int nA = totals ? 1 : nblkA;
     auto mark = [&](int q) -> int {
         if (a.ev && hipEventRecord(a.ev[q], st) != hipSuccess) {
             snprintf(g_err, sizeof(g_err), "hipEventRecord failed");
@@ -5605,14 +5612,14 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     }
 #undef LRS_LAUNCH_A
     if (ngd && (mask & 1) && launch_dense_cd(P, W, ctrl_cur, offCD, st)) return -1;
-    if (sh && (mask & 1)) {
+    if (totals && (mask & 1)) {
         hipLaunchKernelGGL(k_fold_partials<8>, dim3(1), dim3(kBlock), 0, st, W.part, nblkA, totA);
         LRS_CHECK_LAUNCH();
-        if (sh->allreduce(sh->self, totA, 8, st)) return -1;
+        if (sh && sh->allreduce(sh->self, totA, 8, st)) return -1;
     }
     if (mark(1)) return -1;
     // G: phase-1 test and the global constraints' q and dots
-    double *totB = sh ? W.tot + 8 : nullptr;
+    double *totB = totals ? W.tot + 8 : nullptr;
     if (sh && P.mg > 0 && (mask & 2)) {
         // sharded: each holder's owned-entry sums, the shared constraints' summed over the
         // shards, then q / rec / dots from the totals, the dots and residual summed, the
@@ -5640,6 +5647,10 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                            P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, nblkB, W.part,
                            nblkA, W.rec, W.partB, gwide, uvp);
         LRS_CHECK_LAUNCH();
+        if (totals) {   // its five line-search dots as totals for B (as A's)
+            hipLaunchKernelGGL(k_fold_partials<5>, dim3(1), dim3(kBlock), 0, st, W.partB, gg, totB);
+            LRS_CHECK_LAUNCH();
+        }
     }
     if (mark(2)) return -1;
     // B: line search, R update, adjoint, gradient, A(RR^T), L-BFGS pair, dots
@@ -5654,7 +5665,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,                        \
                        reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,           \
                        reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, inA, nA,            \
-                       sh ? totB : W.partB, P.mg > 0 ? (sh ? 1 : gg) : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, \
+                       totals ? totB : W.partB, P.mg > 0 ? (totals ? 1 : gg) : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, \
                        c.n, pstr,                                                                                 \
                        (MM) != 2 && k == 0 ? a.hmirror : nullptr, a.seq, P.ndense ? W.CR : nullptr, W.CD)
         const bool small = pb[k].small;
@@ -5747,10 +5758,10 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
 #undef LRS_LAUNCH_B
 #undef LRS_WIDE_A
 #undef LRS_WIDE_B
-    if (sh && (mask & 4)) {
+    if (totals && (mask & 4)) {
         hipLaunchKernelGGL(k_fold_partials<10>, dim3(1), dim3(kBlock), 0, st, W.partC, nblkB, totC);
         LRS_CHECK_LAUNCH();
-        if (sh->allreduce(sh->self, totC, 10, st)) return -1;
+        if (sh && sh->allreduce(sh->self, totC, 10, st)) return -1;
     }
     if (mark(3)) return -1;
     return mark(4);
