@@ -94,3 +94,49 @@ def test_small_cg_whole_solve(solver_mod, monkeypatch, name, flags):
     tol = 10 * (a["gap"] + b["gap"]) + 1e-6
     assert abs(a["pobj"] - b["pobj"]) <= tol * (1 + abs(b["pobj"]))
     assert a["pinf"] <= 1e-4 and a["gap"] <= max(1e-4, 10 * b["gap"])
+
+
+def _write_theta_cycle(path, n):
+    """Lovasz theta of the n-cycle in SDPA form: min <-J, X> s.t. tr X = 1, X_ij = 0 on the edges."""
+    edges = [(i, (i + 1) % n) for i in range(n)]
+    m = 1 + len(edges)
+    with open(path, "w") as f:
+        f.write(f"{m}\n1\n{n}\n" + " ".join(["1.0"] + ["0.0"] * len(edges)) + "\n")
+        for i in range(1, n + 1):
+            for j in range(i, n + 1):
+                f.write(f"0 1 {i} {j} 1.0\n")   # F0 = J, C = -F0
+        for i in range(1, n + 1):
+            f.write(f"1 1 {i} {i} 1.0\n")
+        for c, (i, j) in enumerate(edges):
+            a, b = min(i, j) + 1, max(i, j) + 1
+            f.write(f"{c + 2} 1 {a} {b} 1.0\n")
+
+
+def test_small_cg_tiny_cone_rank_below_16(solver_mod, monkeypatch, tmp_path):
+    """A cone with r < 16 and a handful of constraints (theta of the 5-cycle: n = 5, m = 6, r = 3):
+    the single-workgroup CG's 16-lane column groups read Y's row pitch past r (those
+    lanes must read finite words -- Y's zeroed pad or a clamped in-row column -- never the LDS past
+    the last row).  The half-steps match the multi-launch CG and stay finite."""
+    path = str(tmp_path / "theta_c5.dat-s")
+    _write_theta_cycle(path, 5)
+    rng = np.random.default_rng(11)
+    out = []
+    for small in (True, False):
+        monkeypatch.setenv("LRS_SMALL_CG", "1" if small else "0")
+        sv = solver_mod.Solver(path)
+        sv.set_rank([3])
+        n = sv.nr()
+        U0, V0 = rng.standard_normal(n), rng.standard_normal(n)
+        lam = rng.standard_normal(sv.m)
+        rng = np.random.default_rng(11)   # the same inputs for both runs
+        sv.set_factor(solver_mod.U, U0)
+        sv.set_factor(solver_mod.V, V0)
+        sv.set_vec(solver_mod.LAMBDA, lam)
+        sv.admm_constr()
+        for side in (0, 1, 0, 1):
+            sv.admm_half(2.0, 1e-10, cone=0, side=side, init=False)
+        out.append((sv.get_factor(solver_mod.U), sv.get_factor(solver_mod.V)))
+        sv.close()
+    (ua, va), (ub, vb) = out
+    assert np.all(np.isfinite(ua)) and np.all(np.isfinite(va))
+    assert rel(ua, ub) < 1e-8 and rel(va, vb) < 1e-8, (rel(ua, ub), rel(va, vb))
