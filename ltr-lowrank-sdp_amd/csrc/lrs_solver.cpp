@@ -2625,15 +2625,18 @@ int lrs_stage_bytes(lrs_ctx *c, double *bytes) {
     // entries A = 2P - n_diag; Z constraint entries; m constraints (m_l local).
     double a = 0, g = 0, bb = 0;
     const DevProblem &P = c->dp;
+    // the latency kernels (the last enqueued iteration's path 0) run each stage as one launch
+    const bool lat = P.last_path == 0;
+    const bool split_a = !lat && alm_stage_a_split(c->dp), split_b = !lat && alm_stage_b_split(c->dp);
     for (int k = 0; k < P.K; ++k) {
         const HostCone &hc = c->hp.cones[k];
         const double n = hc.n, r = c->rank[k], Pk = (double)hc.prow.size(), A = (double)hc.adj_col.size();
         const double nr8 = 8.0 * n * r;
         // split stage A (bandwidth regime): D is written by the first launch and read back
-        a += (alm_stage_a_split(c->dp) ? 8 : 7) * nr8 + 8 * (n + 1) + 8 * Pk /*lower adj col+slot*/ + 8 * Pk /*Cw*/ +
+        a += (split_a ? 8 : 7) * nr8 + 8 * (n + 1) + 8 * Pk /*lower adj col+slot*/ + 8 * Pk /*Cw*/ +
              16 * Pk /*uRD,uDD*/ + 4 * (Pk + 1);
         // split stage B: R_new is written by the first launch and read back by the second
-        bb += (alm_stage_b_split(c->dp) ? 11 : 9) * nr8 + 8 * (n + 1) + 8 * A /*adj col+slot*/ + 8 * Pk /*Craw*/ + 4 * (Pk + 1) /*slot_ptr*/ +
+        bb += (split_b ? 11 : 9) * nr8 + 8 * (n + 1) + 8 * A /*adj col+slot*/ + 8 * Pk /*Craw*/ + 4 * (Pk + 1) /*slot_ptr*/ +
               8 * Pk /*uRR*/ + 4 * (Pk + 1) /*loc_ptr*/;
     }
     const double m = P.m, ml = P.m - P.mg, Z = (double)P.Z;
