@@ -5563,7 +5563,8 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     // re-reads every producer block's partials -- 2 500 x 2 500 x 10 doubles = 500 MB of L2 reads a
     // launch -- before its rows can start.  Sharded solves always fold (the totals then take the
     // all-reduce).  The latency kernels keep their control-wave reduction (<= 256 producers).
-    static const int fold_min = getenv("LRS_FOLD_MIN") ? atoi(getenv("LRS_FOLD_MIN")) : kFoldMinBlocks;   // A/B
+    const char *fm = getenv("LRS_FOLD_MIN");   // A/B and tests (read per enqueue: tests switch it per case)
+    const int fold_min = fm ? atoi(fm) : kFoldMinBlocks;
     const bool totals = sh || lat_wide || std::max(nblkA, nblkB) >= fold_min;
     double *totA = totals ? W.tot : nullptr, *totC = totals ? W.tot + 16 : nullptr;
     const double *inC = totals ? totC : W.partC;
