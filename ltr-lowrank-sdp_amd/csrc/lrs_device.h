@@ -25,7 +25,9 @@ namespace lrs {
 
 constexpr int kBlock = 256;          // threads per block (4 waves)
 constexpr int kMaxPartialBlocks = 4096;
-constexpr int kFoldMinBlocks = 1024;   // stages with this many producer blocks fold their partials once (totals)
+constexpr int kFoldMinBlocks = 1 << 30;   // unsharded stages fold their partials into totals only on the wide latency
+                                          // plan (or LRS_FOLD_MIN, tests): on the general kernels at G81 / C5 size the
+                                          // fold measured no faster (profiles/r05f_g81_ab.txt)
 constexpr int kMaxPartialVals = 16;
 
 // ---- ALM inner-loop control block (double array, double-buffered by iteration parity)
@@ -124,8 +126,6 @@ struct DevCone {
     int auv_items = 0;
     long auv_ebase = 0;                  // first constraint entry of this cone (con_ptr[k m])
     int *auv_item = nullptr;             // [items][4]
-    int *auv_xo = nullptr;               // [kXcdBands + 1] XCD bands of the items (null: none)
-    int auv_xmax = 0;                    // items of the longest band
     unsigned *auv_pq = nullptr;          // [Zk]
     int *auv_pos = nullptr;              // [Zk]
     double *auv_val = nullptr;           // [Zk]
@@ -134,8 +134,6 @@ struct DevCone {
     int sa_items = 0;
     int sa_n = 0;                        // tiled slots (sa_slot's length)
     int *sa_item = nullptr;
-    int *sa_xo = nullptr;                // [kXcdBands + 1] XCD bands of the items (null: none)
-    int sa_xmax = 0;                     // items of the longest band
     unsigned *sa_pq = nullptr;
     int *sa_slot = nullptr;
     // stage B's gradient S R_new over the symmetric pattern in the same tiles (k_tile_b2): one
@@ -181,7 +179,6 @@ constexpr int kAuvMinPerTile = 768;  //   >= this many entries (constraint entri
                                      //   LRS_SLOT_TILES = 0/1 override
 constexpr int kCgSplitSlabs = 8;      // k_cgemm2's most K-slices (DevWork::CGK slabs)
 constexpr int kNX = 8;              // column blocks of the tiled long-row kernels (one per XCD)
-constexpr int kXcdBands = 8;         // XCDs: bands of the 2-D tile items (lrs_problem.cpp xcd_bands)
 constexpr int kTileMinDeg = 32;
 constexpr int kDenseRow = 64;        // entries of a row past which the latency kernels slice it
 constexpr int kSliceMinB = 28;       // fewest entries of one B slice block (G = 64: 7 groups x 4)

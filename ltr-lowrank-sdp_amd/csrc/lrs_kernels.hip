@@ -662,21 +662,8 @@ __device__ __forceinline__ void auv_chunk(const double (*tl)[kAuvT * kAuvS], int
     }
 }
 
-// The items a block takes (block-uniform): with XCD bands (xo, lrs_problem.cpp xcd_bands) block b
-// walks band b % 8 -- the XCD that round-robin dispatch gives it -- from its index b / 8 among that
-// band's blocks; without, the grid strides over all items.
-struct BandWalk {
-    int q, end, step;
-};
-__device__ __forceinline__ BandWalk band_walk(const int *__restrict__ xo, int nitems) {
-    if (!xo || gridDim.x < kXcdBands) return {(int)blockIdx.x, nitems, (int)gridDim.x};
-    const int x = blockIdx.x % kXcdBands;
-    return {xo[x] + (int)blockIdx.x / kXcdBands, xo[x + 1], ((int)gridDim.x - x + kXcdBands - 1) / kXcdBands};
-}
-
 template <int MODE>
-__global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, int nitems, const int4 *__restrict__ items,
-                                                          const int *__restrict__ xo,
+__global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, const int4 *__restrict__ items,
                                                           const unsigned *__restrict__ pq,
                                                           const int *__restrict__ ent,
                                                           const double *__restrict__ X,
@@ -685,8 +672,7 @@ __global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, 
     if (guard && guard[0] == 0.0) return;
     constexpr int NA = MODE == 0 ? 4 : 2;           // staged operands: Xa, Xb (+ Ya, Yb)
     __shared__ double tl[NA][kAuvT * kAuvS];
-    for (BandWalk bw = band_walk(xo, nitems); bw.q < bw.end; bw.q += bw.step) {
-    const int4 it = items[bw.q];
+    const int4 it = items[blockIdx.x];
     const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
     int pl[kAuvNpt], ql[kAuvNpt];
     double acc[kAuvNpt];
@@ -717,7 +703,6 @@ __global__ void __launch_bounds__(kAuvThreads) k_auv_tile(int n, int r, int ld, 
         const int t = eb + (int)threadIdx.x + j * kAuvThreads;
         if (t < ee) val[ent[t]] = MODE == 0 ? 0.5 * acc[j] : acc[j];
     }
-    }   // items
 }
 
 // Per constraint of the cone: sum of w_e d_e over its entries in entry order, then k_auv_con's row epilogue (scale, accumulate, sum_upd, the
@@ -3194,7 +3179,7 @@ __global__ void __launch_bounds__(NT) k_tile_a(
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     const double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec,
     const double *__restrict__ par, const double *__restrict__ ctrl_cur, double *__restrict__ partA, int pblk_off,
-    double2 *__restrict__ uvp, const int *__restrict__ xo) {
+    double2 *__restrict__ uvp) {
     constexpr int NPT = kAuvItem / NT;   // slots per thread of one item
     static_assert(NPT * NT == kAuvItem, "k_tile_a: items divide over the block");
     if (ctrl_cur[C_ACTIVE] == 0.0) return;
@@ -3203,8 +3188,8 @@ __global__ void __launch_bounds__(NT) k_tile_a(
     const double rho = par[P_RHO], rhoInv = 1.0 / rho;
     __shared__ double tl[4][kAuvT * kAuvS];
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (BandWalk bw = band_walk(xo, nitems); bw.q < bw.end; bw.q += bw.step) {   // block-uniform
-        const int4 it = items[bw.q];
+    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
+        const int4 it = items[itx];
         const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
         int pl[NPT], ql[NPT];
         double s0[NPT], s1[NPT];
@@ -3448,14 +3433,14 @@ __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: tw
     const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
-    const double *__restrict__ ls_cur, double *__restrict__ partC, int pblk_off, const int *__restrict__ xo) {
+    const double *__restrict__ ls_cur, double *__restrict__ partC, int pblk_off) {
     if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
     const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
     const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
     __shared__ double tl[2][kAuvT * kAuvS];
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (BandWalk bw = band_walk(xo, nitems); bw.q < bw.end; bw.q += bw.step) {   // block-uniform
-        const int4 it = items[bw.q];
+    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
+        const int4 it = items[itx];
         const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
         int pl[kAuvNpt], ql[kAuvNpt];
         double dv[kAuvNpt];
@@ -4346,17 +4331,16 @@ int launch_sddmm(const DevProblem &P, int cone, int mode, const double *X, const
         // values stored per slot), then the objective sums in slot order
         const double *Xc = X + c.foff, *Yc = Y ? Y + c.foff : nullptr;
         const int4 *it = reinterpret_cast<const int4 *>(c.sa_item);
-        const int tg = c.sa_xo ? kXcdBands * c.sa_xmax : c.sa_items;   // one block per item (band_walk)
         if (mode == 1)
-            hipLaunchKernelGGL((k_auv_tile<1>), dim3(tg), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, c.sa_items, it,
-                               c.sa_xo, c.sa_pq, c.sa_slot, Xc, Xc, out0, nullptr);
+            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.sa_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, it,
+                               c.sa_pq, c.sa_slot, Xc, Xc, out0, nullptr);
         else
-            hipLaunchKernelGGL((k_auv_tile<0>), dim3(tg), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, c.sa_items, it,
-                               c.sa_xo, c.sa_pq, c.sa_slot, Xc, Yc, out0, nullptr);
+            hipLaunchKernelGGL((k_auv_tile<0>), dim3(c.sa_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, it,
+                               c.sa_pq, c.sa_slot, Xc, Yc, out0, nullptr);
         LRS_CHECK_LAUNCH();
         if (mode == 2) {
-            hipLaunchKernelGGL((k_auv_tile<1>), dim3(tg), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, c.sa_items, it,
-                               c.sa_xo, c.sa_pq, c.sa_slot, Yc, Yc, out1, nullptr);
+            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.sa_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld, it,
+                               c.sa_pq, c.sa_slot, Yc, Yc, out1, nullptr);
             LRS_CHECK_LAUNCH();
         }
         if (P.shard) {   // the owned rows' lower slots only, as k_sddmm over the owned rows
@@ -4463,13 +4447,11 @@ int launch_auv_con(const DevProblem &P, int cone, int mode, const double *X, con
     if (c.auv_items > 0 && !P.shard) {
         // 2-D tiles through LDS, then the per-constraint sums
         if (mode == 1)
-            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.auv_xo ? kXcdBands * c.auv_xmax : c.auv_items), dim3(kAuvThreads),
-                               0, st, c.n, c.r, c.ld, c.auv_items, reinterpret_cast<const int4 *>(c.auv_item), c.auv_xo,
-                               c.auv_pq, c.auv_pos, Xc, Xc, c.auv_val, guard);
+            hipLaunchKernelGGL((k_auv_tile<1>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
+                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Xc, c.auv_val, guard);
         else
-            hipLaunchKernelGGL((k_auv_tile<0>), dim3(c.auv_xo ? kXcdBands * c.auv_xmax : c.auv_items), dim3(kAuvThreads),
-                               0, st, c.n, c.r, c.ld, c.auv_items, reinterpret_cast<const int4 *>(c.auv_item), c.auv_xo,
-                               c.auv_pq, c.auv_pos, Xc, Yc, c.auv_val, guard);
+            hipLaunchKernelGGL((k_auv_tile<0>), dim3(c.auv_items), dim3(kAuvThreads), 0, st, c.n, c.r, c.ld,
+                               reinterpret_cast<const int4 *>(c.auv_item), c.auv_pq, c.auv_pos, Xc, Yc, c.auv_val, guard);
         LRS_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_auv_tsum, dim3(grid_elems(P.m, 1)), dim3(kBlock), 0, st, P.m, cone, P.con_ptr,
                            P.con_w, c.auv_ebase, c.auv_val, scale, accumulate, out, b_for_vio, vio_part,
@@ -5296,7 +5278,7 @@ static int lat_resident(const DevCone &c, int &ra, int &rb) {
 // of seven row waves): the stages' partials are folded into totals between the launches and the
 // control waves read those (enqueue_alm_stages `totals`); up to kLatWideWaves waves of resident
 // blocks, any layout a small-regime plan (or a bandwidth-regime one no larger) would take.
-constexpr int kLatWideWaves = 4;
+constexpr int kLatWideWaves = 8;
 static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &pb, int w = kLatRowWaves,
                         bool wide = false) {
     LatPlan lp;
@@ -5376,11 +5358,14 @@ int enqueue_alm_iteration(const AlmIterArgs &a, int parity, hipStream_t st) {
 // Sharded solve: one block folds a stage's per-block partials (fixed order) into NV
 // contiguous totals, which the shards then sum (ShardHooks::allreduce); the next stage
 // reads the totals as a single "block" with stride 1.
-template <int NV>
-__global__ void __launch_bounds__(kBlock) k_fold_partials(const double *__restrict__ part, int nblk,
-                                                          double *__restrict__ out) {
+template <int NV, int NT = kRowBlock>
+__global__ void __launch_bounds__(NT) k_fold_partials(const double *__restrict__ part, int nblk,
+                                                      double *__restrict__ out) {
+    // the consumers' own reduction tree (reduce_partials<NV, NT>: the row kernels' kRowBlock, the
+    // CG kernels' kBlock): a total read back by a consumer is bitwise the sum that consumer would
+    // have formed from the partials
     __shared__ double red[NV];
-    reduce_partials<NV, kBlock>(part, nblk, red);
+    reduce_partials<NV, NT>(part, nblk, red);
     if (threadIdx.x < NV) out[threadIdx.x] = red[threadIdx.x];
 }
 // sharded: an m-vector's shared entries summed over the shards (the holders' partial sums of
@@ -5416,7 +5401,7 @@ int launch_put_ctrl(const double *par, const double *ctl, double *dpar, double *
 
 // one scalar's partials (the sharded CG's <p, Q>, <r, r>, ||b||_1) -> out[0]
 int launch_fold1(const double *part, int nblk, double *out, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_partials<1>, dim3(1), dim3(kBlock), 0, st, part, nblk, out);
+    hipLaunchKernelGGL((k_fold_partials<1, kBlock>), dim3(1), dim3(kBlock), 0, st, part, nblk, out);
     LRS_CHECK_LAUNCH();
     return 0;
 }
@@ -5638,7 +5623,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     hipLaunchKernelGGL(k_tile_a<NT_>, dim3(grid), dim3(NT_), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,         \
                        reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2, W.D,      \
                        W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), \
-                       P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, uvp, c.sa_xo)
+                       P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, uvp)
             if (nta == 512) LRS_TILE_A(512);
             else LRS_TILE_A(1024);
 #undef LRS_TILE_A
@@ -5656,7 +5641,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
 #undef LRS_LAUNCH_A
     if (ngd && (mask & 1) && launch_dense_cd(P, W, ctrl_cur, offCD, st)) return -1;
     if (totals && (mask & 1)) {
-        hipLaunchKernelGGL(k_fold_partials<8>, dim3(1), dim3(kBlock), 0, st, W.part, nblkA, totA);
+        hipLaunchKernelGGL(k_fold_partials<8>, dim3(1), dim3(kRowBlock), 0, st, W.part, nblkA, totA);
         LRS_CHECK_LAUNCH();
         if (sh && sh->allreduce(sh->self, totA, 8, st)) return -1;
     }
@@ -5680,7 +5665,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         hipLaunchKernelGGL(k_it_g_sh, dim3(g2), dim3(kBlock), 0, st, P.mg, P.glob, P.m, P.sh_idx, P.g3, P.gpack, P.cmask,
                            P.b, W.cvs, W.lam, W.par, ctrl_cur, W.rec, W.partB);
         LRS_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_fold_partials<6>, dim3(1), dim3(kBlock), 0, st, W.partB, g2, totB);
+        hipLaunchKernelGGL(k_fold_partials<6>, dim3(1), dim3(kRowBlock), 0, st, W.partB, g2, totB);
         LRS_CHECK_LAUNCH();
         if (sh->allreduce(sh->self, totB, 6, st)) return -1;
         hipLaunchKernelGGL(k_g_ph1, dim3(1), dim3(64), 0, st, W.par, ctrl_cur, totC, totB);
@@ -5691,7 +5676,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                            nblkA, W.rec, W.partB, gwide, uvp);
         LRS_CHECK_LAUNCH();
         if (totals) {   // its five line-search dots as totals for B (as A's)
-            hipLaunchKernelGGL(k_fold_partials<5>, dim3(1), dim3(kBlock), 0, st, W.partB, gg, totB);
+            hipLaunchKernelGGL(k_fold_partials<5>, dim3(1), dim3(kRowBlock), 0, st, W.partB, gg, totB);
             LRS_CHECK_LAUNCH();
         }
     }
@@ -5760,7 +5745,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                P.slot_con, P.slot_a,
                                reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,
                                reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur,
-                               W.partC, off, c.sa_xo);
+                               W.partC, off);
             LRS_CHECK_LAUNCH();
             if (c.sx_n > 0) {   // sharded: S on the halo rows' lower slots
                 hipLaunchKernelGGL(k_slot_sv, dim3(std::min(grid_elems(c.sx_n, 1), 2048)), dim3(kBlock), 0, st, c.sx_n,
@@ -5803,7 +5788,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
 #undef LRS_WIDE_A
 #undef LRS_WIDE_B
     if (totals && (mask & 4)) {
-        hipLaunchKernelGGL(k_fold_partials<10>, dim3(1), dim3(kBlock), 0, st, W.partC, nblkB, totC);
+        hipLaunchKernelGGL(k_fold_partials<10>, dim3(1), dim3(kRowBlock), 0, st, W.partC, nblkB, totC);
         LRS_CHECK_LAUNCH();
         if (sh && sh->allreduce(sh->self, totC, 10, st)) return -1;
     }

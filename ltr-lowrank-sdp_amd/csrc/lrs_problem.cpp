@@ -621,53 +621,6 @@ static bool tile_swizzle_on() {
     return !(e && e[0] == '0');
 }
 
-// XCD bands of 2-D tile items {row0, col0, begin, end} (DevCone::sa_xo / auv_xo).  A launch's
-// workgroups go to the 8 XCDs round-robin (block b -> XCD b % 8) and block b walks band b % 8's
-// items (lrs_kernels.hip band_walk), so each XCD's 4 MB L2 sees one band: a contiguous range of
-// row tiles I holding ~1/8 of the entries, its items reordered by (J, I).  The band's row tiles
-// (~10 at C5: R_I and D_I, ~2.5 MB) stay resident in that L2 while the column tiles J stream
-// past, each fetched once for all the band's row tiles -- with the (I, J) order over all XCDs
-// every XCD fetched its own copy of every tile.  Items keep their entry ranges, so only the
-// order of the work changes (and with it which block sums which items' partials).
-// xo[x] .. xo[x + 1]: band x's items in the new order; xo empty (no bands) when the items
-// span fewer than 2 kXcdBands row tiles or LRS_TILE_XCD=0.
-static void xcd_bands(std::vector<int> &item, std::vector<int> &xo) {
-    xo.clear();
-    const long ni = (long)item.size() / 4;
-    if (const char *e = getenv("LRS_TILE_XCD"))
-        if (e[0] == '0') return;
-    long tot = 0, nI = 0;
-    for (long q = 0; q < ni; ++q) {
-        tot += item[4 * q + 3] - item[4 * q + 2];
-        if (q == 0 || item[4 * q] != item[4 * (q - 1)]) ++nI;
-    }
-    if (nI < 2 * kXcdBands || tot == 0) return;
-    std::vector<int> band(ni);
-    long cum = 0;
-    int b = 0;
-    for (long q = 0; q < ni; ++q) {   // bands start at row-tile changes (items are in (I, J) order)
-        if (q > 0 && item[4 * q] != item[4 * (q - 1)] && b < kXcdBands - 1 &&
-            (double)cum >= (double)(b + 1) * (double)tot / kXcdBands)
-            ++b;
-        band[q] = b;
-        cum += item[4 * q + 3] - item[4 * q + 2];
-    }
-    std::vector<long> ord(ni);
-    for (long q = 0; q < ni; ++q) ord[q] = q;
-    std::stable_sort(ord.begin(), ord.end(), [&](long a, long c) {
-        if (band[a] != band[c]) return band[a] < band[c];
-        if (item[4 * a + 1] != item[4 * c + 1]) return item[4 * a + 1] < item[4 * c + 1];
-        return item[4 * a] < item[4 * c];
-    });
-    std::vector<int> out(item.size());
-    xo.assign(kXcdBands + 1, 0);
-    for (long q = 0; q < ni; ++q) {
-        for (int t = 0; t < 4; ++t) out[4 * q + t] = item[4 * ord[q] + t];
-        xo[band[ord[q]] + 1]++;
-    }
-    for (int x = 0; x < kXcdBands; ++x) xo[x + 1] += xo[x];
-    item.swap(out);
-}
 
 template <typename T>
 static bool dput(T **dst, const std::vector<T> &v, std::string &err) {
@@ -945,12 +898,6 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             DevCone &d = dp.cones[k];
             d.auv_items = (int)(item.size() / 4);
             d.auv_ebase = eb;
-            {
-                std::vector<int> xo;
-                xcd_bands(item, xo);
-                if (!xo.empty() && !dput(&d.auv_xo, xo, err)) return false;
-                for (size_t x = 0; x + 1 < xo.size(); ++x) d.auv_xmax = std::max(d.auv_xmax, xo[x + 1] - xo[x]);
-            }
             if (!dput(&d.auv_item, item, err) || !dput(&d.auv_pq, pq, err) || !dput(&d.auv_pos, pos, err))
                 return false;
             if (hipMalloc((void **)&d.auv_val, (size_t)Zk * sizeof(double)) != hipSuccess) {
@@ -1166,12 +1113,6 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 }
                 d.sa_items = (int)(item.size() / 4);
                 d.sa_n = (int)Po;
-                {
-                    std::vector<int> xo;
-                    xcd_bands(item, xo);
-                    if (!xo.empty() && !dput(&d.sa_xo, xo, err)) return false;
-                    for (size_t x = 0; x + 1 < xo.size(); ++x) d.sa_xmax = std::max(d.sa_xmax, xo[x + 1] - xo[x]);
-                }
                 if (!dput(&d.sa_item, item, err) || !dput(&d.sa_pq, pq, err) || !dput(&d.sa_slot, sl, err))
                     return false;
                 // symmetric adjacency of the owned rows by (row tile I, column tile J): counting
@@ -1251,7 +1192,7 @@ void free_problem(DevProblem &dp) {
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a); f(dp.slot_g);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
-    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_xo); f(c.sa_xo); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);
+    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);
         f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); f(c.sx_slot);
         f(c.cg_cadj_ptr); f(c.cg_cadj); f(c.cg_cl_con); f(c.cg_cl_ptr); f(c.cg_ce); f(c.cg_sp); f(c.cg_sj);
         f(c.cg_cc_ptr); f(c.cg_cc); f(c.cg_ce_w); f(c.cg_sa); f(c.cobj_slot); }
