@@ -25,9 +25,6 @@ namespace lrs {
 
 constexpr int kBlock = 256;          // threads per block (4 waves)
 constexpr int kMaxPartialBlocks = 4096;
-constexpr int kFoldMinBlocks = 1 << 30;   // unsharded stages fold their partials into totals only on the wide latency
-                                          // plan (or LRS_FOLD_MIN, tests): on the general kernels at G81 / C5 size the
-                                          // fold measured no faster (profiles/r05f_g81_ab.txt)
 constexpr int kMaxPartialVals = 16;
 
 // ---- ALM inner-loop control block (double array, double-buffered by iteration parity)

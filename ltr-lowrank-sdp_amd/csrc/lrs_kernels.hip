@@ -2286,17 +2286,14 @@ constexpr int kSliceB = 4;                       // entries per lane group in a 
 // (lane l takes blocks l, l+64, ...).  Split in two so that the loads can be issued first
 // thing in the kernel (clamped, not branched): the wave then waits for one memory trip.
 constexpr int kLatQ = kLatMaxPartials / 64;
-// pstr: the value stride of `part` (kMaxPartialBlocks for per-block partials; 1 with nblk = 1
-// for the folded stage totals of a wide grid)
 template <int NV>
-__device__ __forceinline__ void load_partials(const double *__restrict__ part, int nblk, double (&x)[kLatQ][NV],
-                                              int pstr = kMaxPartialBlocks) {
+__device__ __forceinline__ void load_partials(const double *__restrict__ part, int nblk, double (&x)[kLatQ][NV]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int q = 0; q < kLatQ; ++q) {
         const int bc = min(lane + 64 * q, nblk - 1);
 #pragma unroll
-        for (int v = 0; v < NV; ++v) x[q][v] = part[v * pstr + bc];
+        for (int v = 0; v < NV; ++v) x[q][v] = part[v * kMaxPartialBlocks + bc];
     }
 }
 // wave-uniform sums of what load_partials fetched
@@ -2336,8 +2333,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
     const int *__restrict__ con_ptr, const int *__restrict__ con_slot, const double *__restrict__ con_w,
     const double *__restrict__ uRR, const double *__restrict__ par, const double *__restrict__ ctrl_prev,
     double *__restrict__ ctrl_cur, const double *__restrict__ ls_prev, const double *__restrict__ partC, int nblkC,
-    double *__restrict__ partA, int pblk_off, int gwide, int nrb, int lrw, int nda, const int *__restrict__ dra,
-    int pstr) {
+    double *__restrict__ partA, int pblk_off, int gwide, int nrb, int lrw, int nda, const int *__restrict__ dra) {
     __shared__ double c[C_NCTRL];
     __shared__ double pl[P_NPAR];
     LRS_TS(0, 0);
@@ -2372,7 +2368,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_a(
     double px[kLatQ][10], ccv = 0.0, pvv = 0.0;
     int kb = 0, ke = 0;
     if (ctrl_wave) {
-        load_partials<10>(partC, nblkC, px, pstr);
+        load_partials<10>(partC, nblkC, px);
         const int l64 = threadIdx.x & 63;
         ccv = ctrl_prev[min(l64, C_NCTRL - 1)];
         pvv = par[min(l64, P_NPAR - 1)];
@@ -2648,7 +2644,7 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
     const double *__restrict__ partA, int nblkA, const double *__restrict__ partB, int nblkB,
     double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int m, double *hmirror,
     double seq, int nrb, int lrw, int ndb, const int *__restrict__ drb, double *__restrict__ gl, double *CRb,
-    const double *__restrict__ CDb, int pstr) {
+    const double *__restrict__ CDb) {
     __shared__ double red[12];
     __shared__ double ls[LS_N];
     __shared__ double pl[P_NPAR];
@@ -2684,8 +2680,8 @@ __global__ void __launch_bounds__(kLatNT) k_lat_b(
     double pa[kLatQ][7], pb[kLatQ][5], pvv = 0.0;
     int kb = 0, kl = 0, ke = 0;
     if (ctrl_wave) {
-        load_partials<7>(partA, nblkA, pa, pstr);
-        if (nblkB > 0) load_partials<5>(partB, nblkB, pb, pstr);
+        load_partials<7>(partA, nblkA, pa);
+        if (nblkB > 0) load_partials<5>(partB, nblkB, pb);
         pvv = par[min((int)(threadIdx.x & 63), P_NPAR - 1)];
     } else {
         kb = adj_ptr[ic];
@@ -5274,17 +5270,10 @@ static int lat_resident(const DevCone &c, int &ra, int &rb) {
     LRS_LAYOUT_SWITCH(c.G, c.E, { ra = (res_la<GG, EE>)(); rb = (res_lb<GG, EE>)(); });
     return 0;
 }
-// wide: a grid past one resident wave and past the control wave's reach (G81 size: 1 429 blocks
-// of seven row waves): the stages' partials are folded into totals between the launches and the
-// control waves read those (enqueue_alm_stages `totals`); up to kLatWideWaves waves of resident
-// blocks, any layout a small-regime plan (or a bandwidth-regime one no larger) would take.
-constexpr int kLatWideWaves = 8;
-static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &pb, int w = kLatRowWaves,
-                        bool wide = false) {
+static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &pb, int w = kLatRowWaves) {
     LatPlan lp;
-    if (lat_disabled() || forced_regime() == 2 || c.maxdeg <= 0 || pa.T != 1 || pb.T != 1) return lp;
-    if (!wide && (!pa.small || !pb.small)) return lp;
-    if (wide && (pa.wide || pb.wide)) return lp;   // long rows: the neighbour kernels
+    if (lat_disabled() || forced_regime() == 2 || c.maxdeg <= 0 || !pa.small || !pb.small || pa.T != 1 || pb.T != 1)
+        return lp;
     if ((int)c.dra_h.size() > kMaxDenseRows || (int)c.drb_h.size() > kMaxDenseRows) return lp;
     const int rows = 64 * w;   // row-wave threads a block
     const long need = std::max(1L, ((long)c.nown * c.G + rows - 1) / rows);
@@ -5292,28 +5281,14 @@ static LatPlan lat_plan(const DevCone &c, const StagePlan &pa, const StagePlan &
     const int sb = lat_slices(c.drb_n, (rows / c.G) * kSliceB);
     int ra = 0, rb = 0;
     if (lat_resident(c, ra, rb)) return lp;
-    if (wide) {
-        if (need + sa > (long)kLatWideWaves * ra || need + sb > (long)kLatWideWaves * rb) return lp;
-        if (need + std::max(sa, sb) + (long)c.drb_h.size() > kMaxPartialBlocks) return lp;
-    } else {
-        if (need + sa > ra || need + sb > rb || need + sa > kLatMaxPartials) return lp;
-        if (need + sb + (long)c.drb_h.size() > kLatMaxPartials) return lp;
-    }
+    if (need + sa > ra || need + sb > rb || need + sa > kLatMaxPartials) return lp;
+    if (need + sb + (long)c.drb_h.size() > kLatMaxPartials) return lp;
     lp.nrb = (int)need;
     lp.sa = sa;
     lp.sb = sb;
     lp.nf = (int)c.drb_h.size();
     lp.nt = 64 * (w + 1);
     return lp;
-}
-// LRS_LAT_WIDE=0: no latency kernels past the control waves' reach (the general kernels, A/B)
-static bool lat_wide_disabled() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("LRS_LAT_WIDE");
-        v = (e && e[0] == '0') ? 1 : 0;
-    }
-    return v != 0;
 }
 // LRS_LAT_ROWWAVES = 1..7 forces the row waves per latency block (0: chosen per launch)
 static int lat_forced_waves() {
@@ -5504,20 +5479,6 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     }
     if (lat && (nla + ngd > kLatMaxPartials || nlb + nlf > kLatMaxPartials || (P.mg > 0 && gg > kLatMaxPartials)))
         lat = false;
-    // a grid past the control waves' reach (G81 size): the latency kernels over folded totals
-    bool lat_wide = false;
-    if (!lat && !sh && !multi_path(P) && !lat_wide_disabled() && !P.shard) {
-        bool ok = true;
-        nla = nlb = nlf = 0;
-        for (int k = 0; k < KL && ok; ++k) {
-            lg[k] = lat_plan(cone_of(k), pa[k], pb[k], kLatRowWaves, true);
-            ok = lg[k].nrb > 0;
-            nla += lg[k].nrb + lg[k].sa;
-            nlb += lg[k].nrb + lg[k].sb;
-            nlf += lg[k].nf;
-        }
-        if (ok && nla + ngd <= kMaxPartialBlocks && nlb + nlf <= kMaxPartialBlocks) lat = lat_wide = true;
-    }
     P.last_path = lat ? 0 : 1;
     P.last_tiles = 0;
     for (int k = 0; k < KL; ++k)
@@ -5528,9 +5489,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         for (int k = 0; k < KL; ++k) {
             pa[k].grid = lg[k].nrb + lg[k].sa;
             pb[k].grid = lg[k].nrb + lg[k].sb;
-            pa[k].small = pb[k].small = true;   // (a wide latency plan replaces a split one: one launch a stage)
         }
-        split = false;
     }
     // dense-objective cones: C D and its two objective partials after stage A's blocks
     const int offCD = nblkA;
@@ -5542,15 +5501,11 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         }
     }
     // what the consumers read: every producer block's partials, or (sharded) the summed totals
-    // Wide grids (the general kernels at G81 size: 2 500 blocks a stage) fold each stage's
-    // per-block partials once, into the stage totals (k_fold_partials, one workgroup, fixed block
-    // order), and the next stage's blocks read those totals.  Without the fold every consumer block
-    // re-reads every producer block's partials -- 2 500 x 2 500 x 10 doubles = 500 MB of L2 reads a
-    // launch -- before its rows can start.  Sharded solves always fold (the totals then take the
-    // all-reduce).  The latency kernels keep their control-wave reduction (<= 256 producers).
-    const char *fm = getenv("LRS_FOLD_MIN");   // A/B and tests (read per enqueue: tests switch it per case)
-    const int fold_min = fm ? atoi(fm) : kFoldMinBlocks;
-    const bool totals = sh || lat_wide || std::max(nblkA, nblkB) >= fold_min;
+    // sharded: each stage's per-block partials folded once into the stage totals (k_fold_partials,
+    // the consumers' reduction tree), which take the all-reduce; the next stage reads the totals
+    // (measured unsharded at G81 / C5 size, where every consumer block re-reads every producer's
+    // partials: no faster, profiles/r05f_g81_ab.txt)
+    const bool totals = sh != nullptr;
     double *totA = totals ? W.tot : nullptr, *totC = totals ? W.tot + 16 : nullptr;
     const double *inC = totals ? totC : W.partC;
     const int nC = totals ? 1 : nblkB, pstr = totals ? 1 : kMaxPartialBlocks;
@@ -5598,7 +5553,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam,
                                    W.rec, k == 0 ? 1 : 0, P.mg, P.glob, P.m, P.K, P.con_ptr, P.con_slot, P.con_w,
                                    W.uvt2, W.par, ctrl_prev, ctrl_cur, ls_prev, inC, nC, W.part, off, gwide,
-                                   lg[k].nrb, lg[k].nt / 64 - 1, (int)c.dra_h.size(), c.dra, pstr);
+                                   lg[k].nrb, lg[k].nt / 64 - 1, (int)c.dra_h.size(), c.dra);
             });
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
@@ -5675,10 +5630,6 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                            P.con_w, W.uvt0, W.uvt1, P.b, W.cvs, W.lam, W.par, ctrl_cur, W.partC, nblkB, W.part,
                            nblkA, W.rec, W.partB, gwide, uvp);
         LRS_CHECK_LAUNCH();
-        if (totals) {   // its five line-search dots as totals for B (as A's)
-            hipLaunchKernelGGL(k_fold_partials<5>, dim3(1), dim3(kRowBlock), 0, st, W.partB, gg, totB);
-            LRS_CHECK_LAUNCH();
-        }
     }
     if (mark(2)) return -1;
     // B: line search, R update, adjoint, gradient, A(RR^T), L-BFGS pair, dots
@@ -5693,7 +5644,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                        W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con, P.slot_a,                        \
                        reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,           \
                        reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, inA, nA,            \
-                       totals ? totB : W.partB, P.mg > 0 ? (totals ? 1 : gg) : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, \
+                       sh ? totB : W.partB, P.mg > 0 ? (sh ? 1 : gg) : 0, ls_cur, L, W.partC, off, pb[k].T, c.row0, \
                        c.n, pstr,                                                                                 \
                        (MM) != 2 && k == 0 ? a.hmirror : nullptr, a.seq, P.ndense ? W.CR : nullptr, W.CD)
         const bool small = pb[k].small;
@@ -5704,10 +5655,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
                                    W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
                                    P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con,
                                    P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur,
-                                   inA, nA, totals ? totB : W.partB, P.mg > 0 ? (totals ? 1 : gg) : 0, ls_cur, L,
-                                   W.partC, off, P.m,
+                                   inA, nA, W.partB, P.mg > 0 ? gg : 0, ls_cur, L, W.partC, off, P.m,
                                    k == 0 ? a.hmirror : nullptr, a.seq, lg[k].nrb, lg[k].nt / 64 - 1, (int)c.drb_h.size(), c.drb,
-                                   W.gl + glo, P.ndense ? W.CR : nullptr, W.CD, pstr);
+                                   W.gl + glo, P.ndense ? W.CR : nullptr, W.CD);
             });
             glo += (long)lg[k].sb * c.ld;
         } else {

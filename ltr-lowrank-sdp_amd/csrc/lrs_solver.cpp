@@ -2626,6 +2626,7 @@ int lrs_stage_bytes(lrs_ctx *c, double *bytes) {
     double a = 0, g = 0, bb = 0;
     const DevProblem &P = c->dp;
     // the latency kernels (the last enqueued iteration's path 0) run each stage as one launch
+    // (alm_stage_*_split describe the general kernels' plan)
     const bool lat = P.last_path == 0;
     const bool split_a = !lat && alm_stage_a_split(c->dp), split_b = !lat && alm_stage_b_split(c->dp);
     for (int k = 0; k < P.K; ++k) {

@@ -141,39 +141,6 @@ def test_fused_iterations_slot_tiles_match_reference(solver_mod, name, monkeypat
     sv.close()
 
 
-@pytest.mark.parametrize("name,kpath", [(n, p) for n in ("mc_rand200", "mc_torus12x10", "theta40", "rsparse60",
-                                                           "checker_1.5") for p in (0, 1)])
-def test_fused_iterations_over_folded_totals_match_reference(solver_mod, name, kpath, monkeypatch):
-    """The consumers of the stage partials reading folded stage totals (k_fold_partials after each
-    stage: what wide grids -- G81 on the latency kernels -- do, LRS_FOLD_MIN=1 forces it here) on
-    the latency kernels (path 0; hub rows' slice blocks on checker_1.5) and the general ones (path
-    1; rsparse60's multi-slot constraints through k_it_g's folded dots): the reference's trips at
-    1e-9, as the per-block partials."""
-    monkeypatch.setenv("LRS_SMALL", "0")
-    monkeypatch.setenv("LRS_FOLD_MIN", "1")
-    z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
-    rank = int(z["rank_flag"])
-    kw = {"reoptLevel": 0}
-    if rank > 0:
-        kw["fixedRank"] = rank
-    sv = solver_mod.Solver(_path(name))
-    sv.set_kernel_path(kpath)
-    for K in [int(k) for k in z["ks"]]:
-        trips = z[f"K{K}_trips"]
-        if trips.shape[0] < K:
-            continue
-        d = sv.alm_steps(K, **kw)
-        assert d["inner"] == K, (K, d["inner"])
-        tau, rn, lag, pinf = trips[K - 1]
-        assert abs(d["tau"] - tau) <= TOL * abs(tau), (K, d["tau"], tau)
-        assert abs(d["lag"] - lag) <= TOL * abs(lag), (K, d["lag"], lag)
-        assert abs(d["pinf"] - pinf) <= TOL * max(abs(pinf), 1e-300), (K, d["pinf"], pinf)
-        for key in ("R", "G", "cvs", "s", "y"):
-            assert rel_err(d[key], z[f"K{K}_{key}"]) < TOL, (K, key)
-    assert sv.kernel_path() == (0 if kpath == 0 else 1)
-    sv.close()
-
-
 @pytest.mark.parametrize("name", ["mc_rand200_l3", "theta40_l3"])
 def test_lbfgs_ring_of_three_matches_reference(solver_mod, name):
     """--lbfgsListLength 3 (data/lorads_solver.c:686-706: a ring of L pairs; LBFGSDirection's
