@@ -7,19 +7,22 @@ import importlib
 import json
 import os
 
+import numpy as np
 import pytest
+
+from golden_util import fixed_trace
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DATA = os.path.join(ROOT, "data", "bundled")
 GOLD = os.path.join(ROOT, "tests", "golden", "solves_bundled.json")
 HUBS = ["checker_1.5", "ice_2.0", "p_auss2_3.0"]
-# Relative spread of the final primal objective between solves that all stop primal-dual
-# optimal at the reference's tolerances (pinf ~1e-9, gap ~1e-7, dual infeasibility ~1e-8,
-# each scaled by the data's norms): measured on checker_1.5 as 3304.56 (reference),
-# 3304.48 / 3304.16 / 3304.12 (device paths) -- the stopping rule pins the objective to
-# about 1e-4 of its size there, not closer.
-OBJ_TOL = 2e-4
-
+# The general SDPs (HUBS) stop "primal-dual optimal" at the reference's default tolerances with
+# objectives ~1e-4 apart: the DIMACS dual-infeasibility measure lets through a lambda_min(S) of
+# ~-3e-4 (test_tight_objectives.py).  Their objectives are compared through weak duality instead
+# of a bar: tr X is fixed by diag(X) = 1, so each primal-feasible iterate certifies
+#   b^T lambda + min(lambda_min(S), 0) tr X  <=  OPT  <=  <C, X>,
+# and two solves agree when their intervals intersect.  The reference's interval comes from its
+# final iterate (tests/golden/bundled_final_<name>.npz, REF_DUMP) evaluated on the device operators.
 
 def golden():
     with open(GOLD) as f:
@@ -40,6 +43,11 @@ def test_bundled_fixtures_complete():
         assert name in g and os.path.exists(os.path.join(DATA, f"{name}.dat-s"))
         r = g[name]["result"]
         assert r["admm_pinf"] < 1e-4 and r["alm_inner"] > 0
+    for name in HUBS:   # the reference's final iterates: one cone, R (n x rank) and lambda (m)
+        z = np.load(os.path.join(ROOT, "tests", "golden", f"bundled_final_{name}.npz"))
+        n = fixed_trace(os.path.join(DATA, f"{name}.dat-s"))
+        assert z["ranks"].shape == (1,) and z["R"].size == int(n) * int(z["ranks"][0])
+        assert z["lam"].size == int(z["m"]) and np.isfinite(z["lam"]).all()
 
 
 def dense_rows(path, thresh=64):
@@ -71,45 +79,82 @@ def solver_mod():
     return importlib.import_module("ltr-lowrank-sdp_amd.solver")
 
 
+def certified(sv, r, trace):
+    """[b^T lambda + min(lambda_min(S), 0) tr X, <C, X>] of the context's current iterate."""
+    _, lmin = sv.dual_infeasibility()
+    return r["dobj"] + min(float(np.min(lmin)), 0.0) * trace, r["pobj"]
+
+
+def intersect(a, b, scale):
+    return max(a[0], b[0]) <= min(a[1], b[1]) + 1e-9 * abs(scale)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", HUBS)
 def test_dense_row_slices_match_general(solver_mod, name, monkeypatch):
     """Latency kernels with slice blocks over the dense rows solve like the general row
     kernels (same per-entry arithmetic, other partial-sum partitions, so another trajectory):
-    both stop primal-dual optimal (pinf, gap, dual infeasibility), objectives within OBJ_TOL."""
+    both stop primal-dual optimal (pinf, gap, dual infeasibility) and their certified
+    intervals intersect."""
     monkeypatch.setenv("LRS_SMALL", "0")
+    path_ = os.path.join(DATA, f"{name}.dat-s")
+    trace = fixed_trace(path_)
     out = []
     for path in (0, 1):
-        sv = solver_mod.Solver(os.path.join(DATA, f"{name}.dat-s"))
+        sv = solver_mod.Solver(path_)
         sv.set_kernel_path(path)
         # the kernels the first trips run on (at the initial rank; a later, larger rank may
         # outgrow the latency kernels' partial-block budget and fall back to the general ones)
         sv.alm_steps(3, reoptLevel=0)
         first = sv.kernel_path()
         r = sv.solve(reoptLevel=0)
-        out.append((r, first))
+        out.append((r, first, certified(sv, r, trace)))
         sv.close()
-    (a, pa), (b, pb) = out
+    (a, pa, ia), (b, pb, ib) = out
+    print(f"{name}: latency [{ia[0]:.9g}, {ia[1]:.9g}], general [{ib[0]:.9g}, {ib[1]:.9g}]")
     assert pa == 0, "latency kernels not taken on a hub instance"
     assert pb == 1
     for r in (a, b):
         assert r["status"] == 1 and r["pinf"] < 1e-6 and r["gap"] < 1e-5 and r["dinf"] < 1e-6, r
-    assert abs(a["pobj"] - b["pobj"]) <= OBJ_TOL * max(1.0, abs(b["pobj"])), (a["pobj"], b["pobj"])
+    assert intersect(ia, ib, b["pobj"]), (ia, ib)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["G11", "G12", "G13", "cphil12", *HUBS, "MC_500"])
 def test_bundled_matches_reference(solver_mod, name):
-    """Device solve with the golden run's flags against the reference's final result: the
-    primal objective within OBJ_TOL (MaxCut, where both stop at a gap of ~1e-7: 1e-6),
-    primal infeasibility and gap at the reference's level."""
+    """Device solve with the golden run's flags against the reference's final result:
+    MaxCut (both stop at a gap of ~1e-7) primal objectives within 1e-6; the general SDPs'
+    certified intervals intersecting the reference's; cphil12 / MC_500 (no fixed trace, so no
+    interval) within 10x the two stopping gaps, the theta102 bar; pinf and gap at the
+    reference's level."""
     g = golden()[name]
     ref = g["result"]
-    sv = solver_mod.Solver(os.path.join(DATA, f"{name}.dat-s"))
+    path = os.path.join(DATA, f"{name}.dat-s")
+    sv = solver_mod.Solver(path)
+    if name in HUBS:
+        trace = fixed_trace(path)
+        z = np.load(os.path.join(ROOT, "tests", "golden", f"bundled_final_{name}.npz"))
+        sv.set_rank([int(q) for q in z["ranks"]])
+        sv.set_factor(solver_mod.R, z["R"])
+        sv.set_vec(solver_mod.LAMBDA, z["lam"])
+        ev = sv.dimacs()
+        assert abs(ev["pobj"] - ref["admm_pobj"]) <= 1e-12 * abs(ref["admm_pobj"]), (ev, ref)
+        iref = certified(sv, ev, trace)
     r = sv.solve(**flags_of(g))
+    if name in HUBS:
+        idev = certified(sv, r, trace)
+        print(f"{name}: reference [{iref[0]:.9g}, {iref[1]:.9g}], device [{idev[0]:.9g}, {idev[1]:.9g}]")
+        assert intersect(iref, idev, ref["admm_pobj"]), (iref, idev)
     sv.close()
-    tol = 1e-6 if name.startswith("G") else OBJ_TOL
-    assert abs(r["pobj"] - ref["admm_pobj"]) <= tol * max(1.0, abs(ref["admm_pobj"])), (r["pobj"], ref["admm_pobj"])
+    if name.startswith("G"):
+        tol = 1e-6
+    elif name not in HUBS:
+        tol = 10 * (abs(ref["admm_gap"]) + abs(r["gap"])) + 1e-6
+    else:
+        tol = None
+    print(f"{name}: pObj {r['pobj']:.12g} vs {ref['admm_pobj']:.12g}, gap {r['gap']:.2e} vs {ref['admm_gap']:.2e}")
+    if tol is not None:
+        assert abs(r["pobj"] - ref["admm_pobj"]) <= tol * max(1.0, abs(ref["admm_pobj"])), (r["pobj"], ref["admm_pobj"], tol)
     assert r["pinf"] <= max(1e-6, 10 * ref["admm_pinf"])
     assert abs(r["gap"]) <= max(1e-5, 2 * abs(ref["admm_gap"]))
 
