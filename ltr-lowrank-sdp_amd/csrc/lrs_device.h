@@ -131,6 +131,10 @@ struct DevCone {
     int sa_items = 0;
     int sa_n = 0;                        // tiled slots (sa_slot's length)
     int *sa_item = nullptr;
+    int sa_nsub = 0;                     // the items cut at kTileSub slots (k_tile_a's sub-items)
+    int *sa_sub = nullptr;
+    int sa_ngrp = 0;                     // runs of <= kTileGrp sub-items of one row tile: [ngrp + 1] starts
+    int *sa_grp = nullptr;
     unsigned *sa_pq = nullptr;
     int *sa_slot = nullptr;
     // stage B's gradient S R_new over the symmetric pattern in the same tiles (k_tile_b2): one
@@ -169,6 +173,8 @@ constexpr int kAuvC = 32;            // factor columns staged in LDS at a time
 constexpr int kAuvThreads = 512;
 constexpr int kAuvNpt = 8;           // entries per thread of one item
 constexpr int kAuvItem = kAuvThreads * kAuvNpt;
+constexpr int kTileSub = 1024;       // slots of one k_tile_a sub-item (one a thread)
+constexpr int kTileGrp = 2;          // most sub-items of one k_tile_a group (one row tile)
 constexpr int kAuvMinN = 2048;       // tiled when n >= this and the lower triangle's tiles hold on average
 constexpr int kAuvMinPerTile = 768;  //   >= this many entries (constraint entries for A(X Y^T), pattern slots
                                      //   for the stage kernels: 3x reuse of each staged row); C5 ~1850, a

@@ -3160,86 +3160,136 @@ __global__ void __launch_bounds__(kRowBlock) k_wide_a(
 }
 
 // k_wide_a's work over 2-D tiles of the lower pattern (cones with DevCone::sa_items, e.g. C5's
-// ~570 lower slots per row): a work item is one (row tile, column tile) of kAuvT rows each and
-// up to kAuvItem of its slots; R and D of both tiles are staged in LDS kAuvC columns at a time
-// (auv_fetch / auv_put) and each thread evaluates its slots' sym(R D^T) and D D^T from there, instead of
-// every lane group gathering ~570 neighbour rows of R and D per row.  The per-slot epilogue
-// (slot values, C and local-constraint terms, rec) is k_wide_a's.  Same grid and partial
-// slots as k_wide_a (blocks stride over the items), so the consumers are unchanged.
-template <int NT>
-__global__ void __launch_bounds__(NT) k_tile_a(
-    int n, int r, int ld, long foff, int nitems, const int4 *__restrict__ items, const unsigned *__restrict__ pq,
-    const int *__restrict__ tslot, const double *__restrict__ Cw, const double *__restrict__ Rb0,
-    const double *__restrict__ Rb1, const double *__restrict__ Dall, double *__restrict__ uRD,
-    double *__restrict__ uDD, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
-    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
-    const double *__restrict__ cvs, const double *__restrict__ lam, double *__restrict__ rec,
-    const double *__restrict__ par, const double *__restrict__ ctrl_cur, double *__restrict__ partA, int pblk_off,
-    double2 *__restrict__ uvp) {
-    constexpr int NPT = kAuvItem / NT;   // slots per thread of one item
-    static_assert(NPT * NT == kAuvItem, "k_tile_a: items divide over the block");
+// ~570 lower slots per row): per (row tile I, column tile J) of kAuvT rows each, R and D of both
+// tiles are staged in LDS kAuvC columns at a time and each thread evaluates its slots'
+// sym(R D^T) and D D^T from there (auv_chunk<2>), instead of every lane group gathering ~570
+// neighbour rows of R and D per row; the per-slot epilogue (slot values, C and local-constraint
+// terms, rec) is k_wide_a's.  Work: the tile pairs' slots cut into sub-items of kTileSub (one
+// slot a thread), in groups of at most kTileGrp sub-items of one row tile (the I side staged once
+// per column chunk for the group, each new J side after it); the resident blocks (nwork) stride
+// over the groups in order, so the groups in flight are neighbours and share their tiles in L2;
+// the blocks past nwork write zero partials (same grid and partial slots as k_wide_a).  Staging,
+// not the LDS reads, bounds it (C5, profiles/r05q_c5_tile_a_ab.txt: 0.27 ms of the 0.47 ms stage
+// the tiles, 0.15 ms sum them), and the staging rounds' latency more than their bytes: groups of
+// 4 / 6 / 8 sub-items (a third to a half fewer staged bytes) measured no faster (616 / 640 / 665
+// against 610 us for stage A), register prefetch of the next round at 512 threads slower (806).
+__device__ __forceinline__ void tile_side_fetch(double2 (&v)[2][auv_per<1024>()], int row0, int c0, int n, int r,
+                                                int ld, const double *__restrict__ X, const double *__restrict__ Y) {
+#pragma unroll
+    for (int k = 0; k < auv_per<1024>(); ++k) {
+        const int x = threadIdx.x + k * 1024;
+        const int row = row0 + x / (kAuvC / 2), col = c0 + 2 * (x % (kAuvC / 2));
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            double2 t = make_double2(0.0, 0.0);
+            if (row < n && col < r) {
+                t = *reinterpret_cast<const double2 *>((a == 0 ? X : Y) + (long)row * ld + col);
+                if (col + 1 >= r) t.y = 0.0;
+            }
+            v[a][k] = t;
+        }
+    }
+}
+__device__ __forceinline__ void tile_side_put(double (*tl)[kAuvT * kAuvS], int side,
+                                              const double2 (&v)[2][auv_per<1024>()]) {
+#pragma unroll
+    for (int k = 0; k < auv_per<1024>(); ++k) {
+        const int x = threadIdx.x + k * 1024;
+        const int o = (x / (kAuvC / 2)) * kAuvS + 2 * (x % (kAuvC / 2));
+        *reinterpret_cast<double2 *>(&tl[side][o]) = v[0][k];       // X side: tl[0] (I) / tl[1] (J)
+        *reinterpret_cast<double2 *>(&tl[side + 2][o]) = v[1][k];   // Y side: tl[2] / tl[3]
+    }
+}
+__global__ void __launch_bounds__(1024) k_tile_a(
+    int n, int r, int ld, long foff, int ngrp, const int *__restrict__ grp, int nwork, const int4 *__restrict__ subs,
+    const unsigned *__restrict__ pq, const int *__restrict__ tslot, const double *__restrict__ Cw,
+    const double *__restrict__ Rb0, const double *__restrict__ Rb1, const double *__restrict__ Dall,
+    double *__restrict__ uRD, double *__restrict__ uDD, const int *__restrict__ loc_ptr,
+    const int *__restrict__ loc_con, const double *__restrict__ loc_w, const double2 *__restrict__ loc1,
+    const double *__restrict__ b, const double *__restrict__ cvs, const double *__restrict__ lam,
+    double *__restrict__ rec, const double *__restrict__ par, const double *__restrict__ ctrl_cur,
+    double *__restrict__ partA, int pblk_off, double2 *__restrict__ uvp) {
+    constexpr int NT = 1024, KM = kTileGrp;
+    static_assert(kTileSub == NT, "k_tile_a: one slot of a sub-item a thread");
     if (ctrl_cur[C_ACTIVE] == 0.0) return;
     const double *__restrict__ R = (ctrl_cur[C_RCUR] == 0.0 ? Rb0 : Rb1) + foff;
     const double *__restrict__ D = Dall + foff;
     const double rho = par[P_RHO], rhoInv = 1.0 / rho;
     __shared__ double tl[4][kAuvT * kAuvS];
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
-        const int4 it = items[itx];
-        const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
-        int pl[NPT], ql[NPT];
-        double s0[NPT], s1[NPT];
+    for (int g = blockIdx.x; g < ngrp && (int)blockIdx.x < nwork; g += nwork) {   // block-uniform
+        {
+            const int g0 = grp[g], g1 = grp[g + 1];
+            const int I0 = subs[g0].x;
+            int pl[KM], ql[KM];
+            double s0[KM], s1[KM];
 #pragma unroll
-        for (int j = 0; j < NPT; ++j) {
-            const int t = eb + (int)threadIdx.x + j * NT;
-            const unsigned w = t < ee ? pq[t] : 0u;
-            pl[j] = (int)(w >> 16) * kAuvS;
-            ql[j] = (int)(w & 0xffffu) * kAuvS;
-            s0[j] = 0.0;
-            s1[j] = 0.0;
-        }
-        for (int c0 = 0; c0 < r; c0 += kAuvC) {
-            double2 v[4][auv_per<NT>()];
-            auv_fetch<4, NT>(v, I0, J0, c0, n, r, ld, R, D);
-            __syncthreads();
-            auv_put<4, NT>(tl, v);
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < NPT; ++j) {
-                if (eb + (int)threadIdx.x + j * NT >= ee) break;
-                auv_chunk<2>(tl, pl[j], ql[j], s0[j], s1[j]);
+            for (int j = 0; j < KM; ++j) {
+                const int4 it = g0 + j < g1 ? subs[g0 + j] : make_int4(0, 0, 0, 0);
+                const int t = it.z + (int)threadIdx.x;
+                const unsigned w = t < it.w ? pq[t] : 0u;
+                pl[j] = (int)(w >> 16) * kAuvS;
+                ql[j] = (int)(w & 0xffffu) * kAuvS;
+                s0[j] = 0.0;
+                s1[j] = 0.0;
             }
-        }
+            for (int c0 = 0; c0 < r; c0 += kAuvC) {
+                int Jprev = -1;
 #pragma unroll
-        for (int j = 0; j < NPT; ++j) {
-            const int t = eb + (int)threadIdx.x + j * NT;
-            if (t >= ee) break;
-            const int sl = tslot[t];
-            const double d0 = 0.5 * s0[j], d1 = s1[j];
-            if (uvp) {   // both values of the slot in one 16-B record (k_it_g reads them together)
-                uvp[sl] = make_double2(d0, d1);
-            } else {
-                uRD[sl] = d0;
-                uDD[sl] = d1;
+                for (int j = 0; j < KM; ++j) {
+                    if (g0 + j >= g1) break;
+                    const int4 it = subs[g0 + j];
+                    if (it.y != Jprev) {   // a new column tile (and, first, the row tile's chunk)
+                        double2 vj[2][auv_per<1024>()];
+                        tile_side_fetch(vj, it.y, c0, n, r, ld, R, D);
+                        if (j == 0) {
+                            double2 vi[2][auv_per<1024>()];
+                            tile_side_fetch(vi, I0, c0, n, r, ld, R, D);
+                            __syncthreads();
+                            tile_side_put(tl, 0, vi);
+                        } else {
+                            __syncthreads();
+                        }
+                        tile_side_put(tl, 1, vj);
+                        __syncthreads();
+                        Jprev = it.y;
+                    }
+                    if (it.z + (int)threadIdx.x < it.w) auv_chunk<2>(tl, pl[j], ql[j], s0[j], s1[j]);
+                }
             }
-            const double cwl = Cw[sl];
-            acc[0] += cwl * d0;
-            acc[1] += cwl * d1;
-            // local constraints on this slot (ALMCalq12p12 lorads_alm.c:714-734), as k_wide_a
-            const double2 l1l = loc1[sl];
-            const int c1 = (int)l1l.y;
-            const int e0 = c1 == -2 ? loc_ptr[sl] : 0, e1 = c1 == -2 ? loc_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
-            for (int e = e0; e < e1; ++e) {
-                const int ci = c1 >= 0 ? c1 : loc_con[e];
-                const double w = c1 >= 0 ? l1l.x : loc_w[e];
-                const double bi = b[ci], cvi = cvs[ci], li = lam[ci];
-                const double q1 = 2.0 * (w * d0), q2 = w * d1;
-                const double q0 = (bi - cvi) + rhoInv * li;
-                acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1;
-                acc[6] += q0 * q1;
-                double2 *rr = reinterpret_cast<double2 *>(rec + 4L * ci);
-                rr[0] = make_double2(cvi, q1);
-                rr[1] = make_double2(q2, (-li) + (-rho) * bi);
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                if (g0 + j >= g1) break;
+                const int4 it = subs[g0 + j];
+                const int t = it.z + (int)threadIdx.x;
+                if (t >= it.w) continue;
+                const int sl = tslot[t];
+                const double d0 = 0.5 * s0[j], d1 = s1[j];
+                if (uvp) {
+                    uvp[sl] = make_double2(d0, d1);
+                } else {
+                    uRD[sl] = d0;
+                    uDD[sl] = d1;
+                }
+                const double cwl = Cw[sl];
+                acc[0] += cwl * d0;
+                acc[1] += cwl * d1;
+                // local constraints on this slot (ALMCalq12p12 lorads_alm.c:714-734), as k_wide_a
+                const double2 l1l = loc1[sl];
+                const int c1 = (int)l1l.y;
+                const int e0 = c1 == -2 ? loc_ptr[sl] : 0, e1 = c1 == -2 ? loc_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
+                for (int e = e0; e < e1; ++e) {
+                    const int ci = c1 >= 0 ? c1 : loc_con[e];
+                    const double w = c1 >= 0 ? l1l.x : loc_w[e];
+                    const double bi = b[ci], cvi = cvs[ci], li = lam[ci];
+                    const double q1 = 2.0 * (w * d0), q2 = w * d1;
+                    const double q0 = (bi - cvi) + rhoInv * li;
+                    acc[2] += q2 * q2; acc[3] += q1 * q2; acc[4] += q0 * q2; acc[5] += q1 * q1;
+                    acc[6] += q0 * q1;
+                    double2 *rr = reinterpret_cast<double2 *>(rec + 4L * ci);
+                    rr[0] = make_double2(cvi, q1);
+                    rr[1] = make_double2(q2, (-li) + (-rho) * bi);
+                }
             }
         }
     }
@@ -3429,13 +3479,13 @@ __global__ void __launch_bounds__(kRowBlock, 4) k_tile_b1(   // <= 128 VGPRs: tw
     const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
     const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
     double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
-    const double *__restrict__ ls_cur, double *__restrict__ partC, int pblk_off) {
+    const double *__restrict__ ls_cur, double *__restrict__ partC, int pblk_off, int nwork) {
     if (ctrl[C_ACT2] == 0.0 || ls_cur[LS_FLAG] != 0.0) return;
     const double tau = ls_cur[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
     const double *__restrict__ Rn = (ctrl[C_RCUR] == 0.0 ? Rb1 : Rb0) + foff;
     __shared__ double tl[2][kAuvT * kAuvS];
     double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int itx = blockIdx.x; itx < nitems; itx += gridDim.x) {   // block-uniform
+    for (int itx = blockIdx.x; itx < nitems && (int)blockIdx.x < nwork; itx += nwork) {   // block-uniform
         const int4 it = items[itx];
         const int I0 = it.x, J0 = it.y, eb = it.z, ee = it.w;
         int pl[kAuvNpt], ql[kAuvNpt];
@@ -5571,17 +5621,14 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const DevCone &c = cone_of(k);
         const int grid = pa[k].grid;
         if (pa[k].wide && !merge && !tla[k] && c.sa_items > 0) {
-            // lower pattern in 2-D LDS tiles (k_tile_a), same grid and partial slots
-            // 1024 threads (16 waves on the CU its 139 KB of LDS allows) unless LRS_TILE_A_NT=512
-            static const int nta = getenv("LRS_TILE_A_NT") ? atoi(getenv("LRS_TILE_A_NT")) : 1024;
-#define LRS_TILE_A(NT_)                                                                                        \
-    hipLaunchKernelGGL(k_tile_a<NT_>, dim3(grid), dim3(NT_), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,         \
-                       reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2, W.D,      \
-                       W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), \
-                       P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur, W.part, off, uvp)
-            if (nta == 512) LRS_TILE_A(512);
-            else LRS_TILE_A(1024);
-#undef LRS_TILE_A
+            // lower pattern in 2-D LDS tiles (k_tile_a): the resident blocks work, the rest write zero partials
+            static int rca = 0;
+            const int nwork = std::min(grid, resident_blocks(k_tile_a, &rca, 1024));
+            hipLaunchKernelGGL(k_tile_a, dim3(grid), dim3(1024), 0, st, c.n, c.r, c.ld, c.foff, c.sa_ngrp, c.sa_grp,
+                               nwork, reinterpret_cast<const int4 *>(c.sa_sub), c.sa_pq, c.sa_slot, P.Cw, W.R, W.R2,
+                               W.D, W.uvt0, W.uvt1, P.loc_ptr, P.loc_con, P.loc_w,
+                               reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.lam, W.rec, W.par, ctrl_cur,
+                               W.part, off, uvp);
         } else if (pa[k].wide) {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
                 if (tla[k]) LRS_WIDE_A(true);
@@ -5689,13 +5736,15 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         const int grid = pb[k].grid;
         if (pb[k].small) { off += grid; continue; }
         if (tbt[k]) {
+            static int rcb = 0;   // the resident blocks stride over the items (stage B 864 -> 803 us on C5)
+            const int nwb = std::min(grid, resident_blocks(k_tile_b1, &rcb, kRowBlock));
             hipLaunchKernelGGL(k_tile_b1, dim3(grid), dim3(kRowBlock), 0, st, c.n, c.r, c.ld, c.foff, c.sa_items,
                                reinterpret_cast<const int4 *>(c.sa_item), c.sa_pq, c.sa_slot, W.R, W.R2, W.uvt2,
                                c.sa_S - c.slot_off, P.Craw, P.slot_ptr,
                                P.slot_con, P.slot_a,
                                reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr, P.loc_con, P.loc_w,
                                reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs, W.par, ctrl_cur, ls_cur,
-                               W.partC, off);
+                               W.partC, off, nwb);
             LRS_CHECK_LAUNCH();
             if (c.sx_n > 0) {   // sharded: S on the halo rows' lower slots
                 hipLaunchKernelGGL(k_slot_sv, dim3(std::min(grid_elems(c.sx_n, 1), 2048)), dim3(kBlock), 0, st, c.sx_n,

@@ -1113,7 +1113,20 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 }
                 d.sa_items = (int)(item.size() / 4);
                 d.sa_n = (int)Po;
-                if (!dput(&d.sa_item, item, err) || !dput(&d.sa_pq, pq, err) || !dput(&d.sa_slot, sl, err))
+                // sub-items of at most kTileSub slots (cut at multiples of 16: the swizzled groups stay whole)
+                std::vector<int> sub;
+                for (size_t q = 0; q < item.size(); q += 4)
+                    for (int e = item[q + 2]; e < item[q + 3]; e += kTileSub)
+                        sub.insert(sub.end(), {item[q], item[q + 1], e, std::min(e + kTileSub, item[q + 3])});
+                d.sa_nsub = (int)(sub.size() / 4);
+                // k_tile_a's groups: runs of at most kTileGrp sub-items of one row tile
+                std::vector<int> grp;
+                for (int q = 0; q < d.sa_nsub; ++q)
+                    if (grp.empty() || q - grp.back() == kTileGrp || sub[4 * q] != sub[4 * grp.back()]) grp.push_back(q);
+                d.sa_ngrp = (int)grp.size();
+                grp.push_back(d.sa_nsub);
+                if (!dput(&d.sa_item, item, err) || !dput(&d.sa_pq, pq, err) || !dput(&d.sa_slot, sl, err) ||
+                    !dput(&d.sa_sub, sub, err) || !dput(&d.sa_grp, grp, err))
                     return false;
                 // symmetric adjacency of the owned rows by (row tile I, column tile J): counting
                 // sort over the row-ordered, column-sorted adjacency keeps (row, column) order
@@ -1192,7 +1205,7 @@ void free_problem(DevProblem &dp) {
     f(dp.slot_ptr); f(dp.slot_con); f(dp.slot_a); f(dp.slot_g);
     f(dp.glob); f(dp.loc_ptr); f(dp.loc_con); f(dp.loc_w); f(dp.slot1); f(dp.loc1); f(dp.slot_rc); f(dp.con1_pq); f(dp.con1_w); f(dp.long_rows);
     f(dp.sh_idx); f(dp.cmask); f(dp.bprim); f(dp.g3); f(dp.gpack); f(dp.spack);
-    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_pq); f(c.sa_slot);
+    for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_sub); f(c.sa_grp); f(c.sa_pq); f(c.sa_slot);
         f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); f(c.sx_slot);
         f(c.cg_cadj_ptr); f(c.cg_cadj); f(c.cg_cl_con); f(c.cg_cl_ptr); f(c.cg_ce); f(c.cg_sp); f(c.cg_sj);
         f(c.cg_cc_ptr); f(c.cg_cc); f(c.cg_ce_w); f(c.cg_sa); f(c.cobj_slot); }
