@@ -63,7 +63,8 @@ enum ExitReason {
     EXIT_LOCAL800 = 3,    // localIter > 800          -> break
     EXIT_TINYTAU = 4,     // |tau| < endTauTol        -> UpdateRho
     EXIT_NUMERR = 5,      // no root                  -> RET_CODE_NUM_ERR
-    EXIT_BUDGET = 6       // bench budget of inner iterations reached
+    EXIT_BUDGET = 6,      // bench budget of inner iterations reached
+    EXIT_XWG = 7          // one-workgroup-per-cone loop: the workgroups' exchange timed out (an error)
 };
 // ---- parameters read by the device loop
 enum ParIdx {
@@ -246,6 +247,7 @@ struct DevProblem {
     // the split iteration when every cone has the same (G, E) row layout
     DevCone merged;
     bool has_merged = false;
+    bool cone_sep = false;                                   // every constraint's entries lie in one cone
 };
 
 // Scratch shared by the kernels of one solve.
@@ -379,6 +381,11 @@ int launch_cg_resid2(long nr, const double *r, double *p, const double *partC, i
 bool small_cg_fits(const DevProblem &P, int cone);
 int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double rho, double tol, int maxit,
                     hipStream_t st);
+// every cone's half-step of one side in one launch (a block a cone; cones whose constraints
+// each lie in one cone, all fitting k_small_cg with the same variant)
+bool small_cg_batch_fits(const DevProblem &P);
+int launch_small_cg_batch(const DevProblem &P, DevWork &W, int side, double rho, double tol, int maxit,
+                          hipStream_t st);
 
 // ---- dual infeasibility (Lanczos for lambda_min of S per cone) ----
 // y = S x over one cone's adjacency (S on the global slots, x / y cone-local vectors)

@@ -5815,11 +5815,16 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
 #endif
 constexpr int kSmallThreads = LRS_SMALL_NT;   // the single workgroup's threads
 constexpr int kSmallMaxConst = 4;     // constant-objective cones the kernel carries
+constexpr int kSmallMaxWg = 8;        // cones of a one-workgroup-per-cone launch
+constexpr int kSmallXcds = 8;         // block stride between those cones' workgroups (MI355X: 8 XCDs)
 constexpr int kSmallMaxLd = 64;       // widest factor row
+struct SmallWg {
+    int n, r0, s0, P, nadj;                      // rows, first (all-cone) row, first slot, slots, adjacency
+    const int *adj_ptr, *adj_low, *adj_col, *adj_slot;
+};
 struct SmallArgs {
     int N, K, m, Ptot, mg, nadj, al;
     const int2 *slot_g;                      // [Ptot] merged-space (row, col) of each slot (row >= col)
-    const int *adj_ptr, *adj_low, *adj_col, *adj_slot;   // merged (or the single cone's) adjacency
     const double *Cw, *Craw;
     const double2 *loc1, *slot1;
     const int *loc_ptr, *loc_con, *slot_ptr, *slot_con;
@@ -5835,7 +5840,44 @@ struct SmallArgs {
     int nconst;
     int cst_row0[kSmallMaxConst], cst_n[kSmallMaxConst];
     double cst_sa[kSmallMaxConst];
+    // one workgroup per cone (nwg > 1; cones whose constraints each lie in one cone): workgroup k
+    // at block k * xs runs cone k's rows [r0, r0 + n) and slots [s0, s0 + P) over the cone's own
+    // adjacency; the per-trip sums are exchanged through xbuf ([2][kSmallMaxWg][16]) and the
+    // arrival counter xcnt
+    int nwg, xs;
+    SmallWg wg[kSmallMaxWg];   // [0]: the single workgroup's (all cones, merged adjacency) when nwg == 1
+    double *xbuf;
+    unsigned *xcnt;
 };
+// The per-trip sums of the workgroups of one multi-cone launch (SmallArgs::nwg > 1): thread 0
+// of each stores its nv partial sums (relaxed device-scope stores, which reach the coherence
+// point), waits for their completion, counts itself in, spins on the counter until every
+// workgroup of this exchange has arrived and sums the nwg partials in workgroup order, so every
+// workgroup holds the same totals.  Two parities of the buffer: a workgroup cannot reach
+// exchange e + 2 before every workgroup has read exchange e.  Returns false when the others do
+// not arrive within the spin limit (the caller ends the loop).
+__device__ __forceinline__ bool xwg_sum(const SmallArgs &A, int wg, unsigned &xe, int nv, const double *v,
+                                        double *out) {
+    double *buf = A.xbuf + (long)(xe & 1u) * kSmallMaxWg * 16;
+    for (int q = 0; q < nv; ++q)
+        __hip_atomic_store(buf + wg * 16 + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);   // the stores acknowledged before the arrival is counted
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_fetch_add(A.xcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (xe + 1u) * (unsigned)A.nwg;
+    xe++;
+    for (long spin = 0; __hip_atomic_load(A.xcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+        if (spin > (1L << 26)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    for (int q = 0; q < nv; ++q) out[q] = 0.0;
+    for (int k = 0; k < A.nwg; ++k)
+        for (int q = 0; q < nv; ++q)
+            out[q] += __hip_atomic_load(buf + k * 16 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
 
 // diagnostics build: thread 0 adds each phase's wall-clock ticks (100 MHz) into g_phase[3][q]
 // (q: 0 control, 1 direction, 2 slots, 3 global + reduction, 4 line search, 5 R / S update,
@@ -5849,7 +5891,7 @@ struct SmallArgs {
 #define LRS_SM_MARK(v) do { } while (0)
 #define LRS_SM_SUB(q, v) do { } while (0)
 #endif
-template <int LD, bool AL>
+template <int LD, bool AL, bool MC>
 __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
     constexpr int LS = LD + 2;          // LDS row stride (doubles): 16-B aligned rows
     constexpr int H = LD / 2;           // double2 per row
@@ -5861,26 +5903,47 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
     constexpr int H2 = H / TPR, RPP = kSmallThreads / TPR;
     static_assert(H2 * TPR == H, "row split");
     constexpr int T = kSmallThreads;
-    extern __shared__ double dyn[];
-    const int N = A.N, tid = threadIdx.x;
+    // dynamic LDS 16-B aligned whatever the static arrays' size: R / D rows are read 16 B at a time
+    extern __shared__ __attribute__((aligned(16))) double dyn[];
+    // one workgroup per cone (A.nwg > 1): this block's cone, its rows, slots and adjacency; the
+    // blocks between the cones' (blockIdx % xs != 0) leave at once
+    // (MC: A.wg[wg] and the kernel arguments are re-read where used: the loop holds no copies)
+    constexpr bool mc = MC;
+    if (MC && blockIdx.x % A.xs != 0) return;
+    const int wg = MC ? (int)blockIdx.x / A.xs : 0;
+    const int N = MC ? A.wg[wg].n : A.N, tid = threadIdx.x;
+    const int rb = MC ? A.wg[wg].r0 : 0, sb = MC ? A.wg[wg].s0 : 0, Pn = MC ? A.wg[wg].P : A.Ptot;
+    const int nadj = MC ? A.wg[wg].nadj : A.nadj;
+    const long rbo = (long)rb * LD;   // this cone's first factor element
+    // this workgroup's slot-indexed arrays and adjacency (MC == false: the arguments themselves)
+    const int2 *__restrict__ slot_g = MC ? A.slot_g + sb : A.slot_g;
+    const double *__restrict__ Cw = MC ? A.Cw + sb : A.Cw;
+    const double *__restrict__ Craw = MC ? A.Craw + sb : A.Craw;
+    const double2 *__restrict__ loc1 = MC ? A.loc1 + sb : A.loc1;
+    const double2 *__restrict__ slot1 = MC ? A.slot1 + sb : A.slot1;
+    const int *__restrict__ loc_ptr = MC ? A.loc_ptr + sb : A.loc_ptr;
+    const int *__restrict__ slot_ptr = MC ? A.slot_ptr + sb : A.slot_ptr;
+    const int *__restrict__ adj_ptr = A.wg[wg].adj_ptr, *__restrict__ adj_low = A.wg[wg].adj_low;
+    const int *__restrict__ adj_col = A.wg[wg].adj_col, *__restrict__ adj_slot = A.wg[wg].adj_slot;
+    auto own_c = [&](int q) { return A.cst_row0[q] >= rb && A.cst_row0[q] < rb + N; };   // this cone's constant C
     // LDS: R, D; per-slot X1 (uDD, then S); with AL a second per-slot array (uRD, then uRR)
     // and the adjacency ((column, slot) pairs, row pointers, lower-entry ends), without AL
     // (the lean layout, larger cones) those stay in global memory
-    double *Rs = dyn, *Ds = dyn + (long)N * LS, *X1 = dyn + 2L * N * LS, *X2 = X1 + A.Ptot;
-    int2 *Ladj = reinterpret_cast<int2 *>(X2 + A.Ptot);
-    int *Lptr = reinterpret_cast<int *>(Ladj + A.nadj), *Llow = Lptr + N + 1;
-    double *XA = AL ? X2 : A.uRD, *XB = AL ? X2 : A.uRR;
+    double *Rs = dyn, *Ds = dyn + (long)N * LS, *X1 = dyn + 2L * N * LS, *X2 = X1 + Pn;
+    int2 *Ladj = reinterpret_cast<int2 *>(X2 + Pn);
+    int *Lptr = reinterpret_cast<int *>(Ladj + nadj), *Llow = Lptr + N + 1;
+    double *XA = AL ? X2 : A.uRD + sb, *XB = AL ? X2 : A.uRR + sb;
     auto adj = [&](int q) -> int2 {
         if constexpr (AL) return Ladj[q];
-        else return make_int2(A.adj_col[q], A.adj_slot[q]);
+        else return make_int2(adj_col[q], adj_slot[q] - sb);
     };
     auto aptr = [&](int i) -> int {
         if constexpr (AL) return Lptr[i];
-        else return A.adj_ptr[i];
+        else return adj_ptr[i];
     };
     auto alow = [&](int i) -> int {
         if constexpr (AL) return Llow[i];
-        else return A.adj_low[i];
+        else return adj_low[i];
     };
     const double2 *Rs2 = reinterpret_cast<const double2 *>(Rs), *Ds2 = reinterpret_cast<const double2 *>(Ds);
     __shared__ double c[C_NCTRL];
@@ -5888,20 +5951,23 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
     __shared__ double ls[LS_N];
     __shared__ double csR[kSmallMaxConst][kSmallMaxLd], csD[kSmallMaxConst][kSmallMaxLd];
     __shared__ double cpart[kSmallThreads];
+    __shared__ int xfail;
+    unsigned xe = 0;   // exchanges so far (thread 0)
     const int lane = tid & 63, wv = tid >> 6, sl_lane = tid % TPR;
     const double rho = A.par[P_RHO], rhoInv = 1.0 / rho;
     if (tid < LS_N) ls[tid] = 0.0;
+    if (tid == 0) xfail = 0;
     // R into LDS, the control block, the adjacency
     for (int e = tid; e < N * H; e += T) {
         const int i = e / H, q = e - i * H;
-        reinterpret_cast<double2 *>(Rs + (long)i * LS)[q] = reinterpret_cast<const double2 *>(A.R + (long)i * LD)[q];
+        reinterpret_cast<double2 *>(Rs + (long)i * LS)[q] = reinterpret_cast<const double2 *>((MC ? A.R + rbo : A.R) + (long)i * LD)[q];
     }
     if (tid < C_NCTRL) c[tid] = A.ctrl_in[tid];
     if (AL) {
-        for (int e = tid; e < A.nadj; e += T) Ladj[e] = make_int2(A.adj_col[e], A.adj_slot[e]);
+        for (int e = tid; e < nadj; e += T) Ladj[e] = make_int2(adj_col[e], adj_slot[e] - sb);
         for (int e = tid; e <= N; e += T) {
-            Lptr[e] = A.adj_ptr[e];
-            if (e < N) Llow[e] = A.adj_low[e];
+            Lptr[e] = adj_ptr[e];
+            if (e < N) Llow[e] = adj_low[e];
         }
     }
     __syncthreads();
@@ -5909,10 +5975,11 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
     auto colsums = [&](const double *X, double (*cs)[kSmallMaxLd]) {
         constexpr int G = kSmallThreads / LD;
         for (int q = 0; q < A.nconst; ++q) {
+            if (!own_c(q)) continue;   // block-uniform
             const int col = tid % LD, g = tid / LD;
             double t = 0.0;
             if (g < G)
-                for (int i = g; i < A.cst_n[q]; i += G) t += X[(long)(A.cst_row0[q] + i) * LS + col];
+                for (int i = g; i < A.cst_n[q]; i += G) t += X[(long)(A.cst_row0[q] - rb + i) * LS + col];
             __syncthreads();
             cpart[tid] = t;
             __syncthreads();
@@ -5942,7 +6009,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
 #endif
         const double cg = c[C_CG], cs0 = c[C_CS0], cy0 = c[C_CY0], cs1 = c[C_CS1], cy1 = c[C_CY1];
         const bool u0 = (cs0 != 0.0 || cy0 != 0.0), u1 = (cs1 != 0.0 || cy1 != 0.0);
-        const double *__restrict__ Gc = c[C_GCUR] == 0.0 ? A.G0 : A.G1;
+        const double *__restrict__ Gc = c[C_GCUR] == 0.0 ? (MC ? A.G0 + rbo : A.G0) : (MC ? A.G1 + rbo : A.G1);
         // ---- D = -(cg G + cs0 s0 + cy0 y0 + cs1 s1 + cy1 y1)  (DirRow's arithmetic), 16-B loads
         // two elements a thread at a time, every operand load issued before the arithmetic
         // (one memory trip per pair instead of one per element and operand)
@@ -5953,10 +6020,10 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                 const int e = min(e0 + u * T, N * H - 1), i = e / H, q = e - i * H;
                 const long o = (long)i * LD + 2 * q;
                 gv[u] = *reinterpret_cast<const double2 *>(Gc + o);
-                a0[u] = *reinterpret_cast<const double2 *>(A.s0 + o);
-                b0[u] = *reinterpret_cast<const double2 *>(A.y0 + o);
-                a1[u] = *reinterpret_cast<const double2 *>(A.s1 + o);
-                b1[u] = *reinterpret_cast<const double2 *>(A.y1 + o);
+                a0[u] = *reinterpret_cast<const double2 *>((MC ? A.s0 + rbo : A.s0) + o);
+                b0[u] = *reinterpret_cast<const double2 *>((MC ? A.y0 + rbo : A.y0) + o);
+                a1[u] = *reinterpret_cast<const double2 *>((MC ? A.s1 + rbo : A.s1) + o);
+                b1[u] = *reinterpret_cast<const double2 *>((MC ? A.y1 + rbo : A.y1) + o);
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -5987,19 +6054,19 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         // values are in flight while this slot's dots run on LDS (one memory trip a slot, not
         // two); loads clamped, not branched
         // (Ptot == 0: index 0 of the >= 1-element arrays, never used -- the loop does not run)
-        const int s0c = max(0, min(tid, A.Ptot - 1));
-        int2 ijn = A.slot_g[s0c];
-        double cwn = A.Cw[s0c];
-        double2 l1n = A.loc1[s0c];
-        for (int s = tid; s < A.Ptot; s += T) {
-            const int2 ij = ijn;
+        const int s0c = max(0, min(tid, Pn - 1));
+        int2 ijn = slot_g[s0c];
+        double cwn = Cw[s0c];
+        double2 l1n = loc1[s0c];
+        for (int s = tid; s < Pn; s += T) {
+            const int2 ij = make_int2(ijn.x - rb, ijn.y - rb);
             const double cw = cwn;
             const double2 l1u = l1n;
             {
-                const int sn = min(s + T, A.Ptot - 1);
-                ijn = A.slot_g[sn];
-                cwn = A.Cw[sn];
-                l1n = A.loc1[sn];
+                const int sn = min(s + T, Pn - 1);
+                ijn = slot_g[sn];
+                cwn = Cw[sn];
+                l1n = loc1[sn];
             }
             const int c1p = (int)l1u.y >= 0 ? (int)l1u.y : 0;
             const double bp = A.b[c1p], cvp = A.cvs[c1p], lp = A.lam[c1p];
@@ -6031,7 +6098,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
             acc[0] += cw * d0;
             acc[1] += cw * d1;
             const int c1 = (int)l1u.y;
-            const int e0 = c1 == -2 ? A.loc_ptr[s] : 0, e1 = c1 == -2 ? A.loc_ptr[s + 1] : (c1 >= 0 ? 1 : 0);
+            const int e0 = c1 == -2 ? loc_ptr[s] : 0, e1 = c1 == -2 ? loc_ptr[s + 1] : (c1 >= 0 ? 1 : 0);
             for (int e = e0; e < e1; ++e) {
                 const int ci = c1 >= 0 ? c1 : A.loc_con[e];
                 const double w = c1 >= 0 ? l1u.x : A.loc_w[e];
@@ -6050,8 +6117,10 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         // ---- G: the global (multi-slot) constraints, a wave each (k_it_g's arithmetic)
         for (int g = wv; g < A.mg; g += T / 64) {
             const int i = A.glob[g];
+            // one workgroup per cone: the constraint is this cone's, or another's (wave-uniform)
+            if (mc && A.con_ptr[(long)wg * A.m + i] == A.con_ptr[(long)wg * A.m + i + 1]) continue;
             double v1 = 0.0, v2 = 0.0;
-            for (int k = 0; k < A.K; ++k) {
+            for (int k = mc ? wg : 0; k < (mc ? wg + 1 : A.K); ++k) {
                 const long row = (long)k * A.m + i;
                 double a1 = 0.0, a2 = 0.0;
                 // four entries a lane in flight, summed in entry order
@@ -6067,8 +6136,8 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                     }
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        xa[u] = XA[sl[u]];
-                        x1[u] = X1[sl[u]];
+                        xa[u] = XA[sl[u] - sb];
+                        x1[u] = X1[sl[u] - sb];
                     }
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
@@ -6095,6 +6164,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
             if (tid == 0) {
                 // constant objectives: <C, sym R D^T> = sa (1^T R).(1^T D), <C, D D^T> = sa |1^T D|^2
                 for (int q = 0; q < A.nconst; ++q) {
+                    if (!own_c(q)) continue;
                     double a = 0.0, bb = 0.0;
                     for (int e = 0; e < LD; ++e) {
                         const double y = A.cst_sa[q] * csD[q][e];
@@ -6104,10 +6174,15 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                     s7[0] += a;
                     s7[1] += bb;
                 }
-                for (int q = 0; q < 7; ++q) red[q] = s7[q];
+                if (!mc) {
+                    for (int q = 0; q < 7; ++q) red[q] = s7[q];
+                } else if (!xwg_sum(A, wg, xe, 7, s7, red)) {
+                    xfail = 1;
+                }
             }
         }
         __syncthreads();   // every rec written, the reduced sums in red
+        if (xfail) break;
         LRS_SM_T(3);
         if (tid < 64) line_search_t<true>(A.par, red[0], red[1], red + 2, ls);   // wave 0
         __syncthreads();
@@ -6129,22 +6204,22 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
             rv.y += tau * dv.y;
             *rp = rv;
         }
-        for (int s0 = tid; s0 < A.Ptot; s0 += 2 * T) {
+        for (int s0 = tid; s0 < Pn; s0 += 2 * T) {
             double craw[2];
             double2 s1u[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                const int s = s0 + u * T < A.Ptot ? s0 + u * T : s0;
-                craw[u] = A.Craw[s];
-                s1u[u] = A.slot1[s];
+                const int s = s0 + u * T < Pn ? s0 + u * T : s0;
+                craw[u] = Craw[s];
+                s1u[u] = slot1[s];
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int s = s0 + u * T;
-                if (s >= A.Ptot) break;
+                if (s >= Pn) break;
                 double sv = craw[u];
                 const int c1 = (int)s1u[u].y;
-                const int e0 = c1 == -2 ? A.slot_ptr[s] : 0, e1 = c1 == -2 ? A.slot_ptr[s + 1] : (c1 >= 0 ? 1 : 0);
+                const int e0 = c1 == -2 ? slot_ptr[s] : 0, e1 = c1 == -2 ? slot_ptr[s + 1] : (c1 >= 0 ? 1 : 0);
                 for (int e = e0; e < e1; ++e) {
                     const int con = c1 >= 0 ? c1 : A.slot_con[e];
                     const double2 *rc = reinterpret_cast<const double2 *>(A.rec + 4L * con);
@@ -6158,14 +6233,15 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
             }
         }
         if (tid < LD)
-            for (int q = 0; q < A.nconst; ++q) csR[q][tid] += tau * csD[q][tid];
+            for (int q = 0; q < A.nconst; ++q)
+                if (own_c(q)) csR[q][tid] += tau * csD[q][tid];
         __syncthreads();
         LRS_SM_T(5);
         // ---- B: per row, S R_new over the adjacency and A(R_new R_new^T) on the lower slots
         // (k_it_b's arithmetic); uRR -> XB
-        double *__restrict__ Gold = gcur == 0 ? A.G0 : A.G1, *__restrict__ Gnew = gcur == 0 ? A.G1 : A.G0;
-        double *__restrict__ sh = h == 0 ? A.s0 : A.s1, *__restrict__ yh = h == 0 ? A.y0 : A.y1;
-        const double *__restrict__ so = h == 0 ? A.s1 : A.s0, *__restrict__ yo = h == 0 ? A.y1 : A.y0;
+        double *__restrict__ Gold = gcur == 0 ? (MC ? A.G0 + rbo : A.G0) : (MC ? A.G1 + rbo : A.G1), *__restrict__ Gnew = gcur == 0 ? (MC ? A.G1 + rbo : A.G1) : (MC ? A.G0 + rbo : A.G0);
+        double *__restrict__ sh = h == 0 ? (MC ? A.s0 + rbo : A.s0) : (MC ? A.s1 + rbo : A.s1), *__restrict__ yh = h == 0 ? (MC ? A.y0 + rbo : A.y0) : (MC ? A.y1 + rbo : A.y1);
+        const double *__restrict__ so = h == 0 ? (MC ? A.s1 + rbo : A.s1) : (MC ? A.s0 + rbo : A.s0), *__restrict__ yo = h == 0 ? (MC ? A.y1 + rbo : A.y1) : (MC ? A.y0 + rbo : A.y0);
         double bacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (int i0 = 0; i0 < N; i0 += RPP) {
             const int r = i0 + tid / TPR;
@@ -6232,7 +6308,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
             // row epilogue (k_it_b): [C R_new], G_new = 2 (...), s = tau D, y = G_new - G_old
             int cq = -1;
             for (int q = 0; q < A.nconst; ++q)
-                if (ii >= A.cst_row0[q] && ii < A.cst_row0[q] + A.cst_n[q]) cq = q;
+                if (ii + rb >= A.cst_row0[q] && ii + rb < A.cst_row0[q] + A.cst_n[q]) cq = q;
             double2 go[H2], sov[H2], yov[H2];
 #pragma unroll
             for (int p = 0; p < H2; ++p) {
@@ -6271,14 +6347,14 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         LRS_SM_T(6);
         // single-slot constraints: A(R_new R_new^T) and their residual, a thread per slot
         // software-pipelined as the slot phase: the next slot's record and this slot's b in flight
-        double2 l1nx = A.loc1[max(0, min(tid, A.Ptot - 1))];
-        for (int s = tid; s < A.Ptot; s += T) {
+        double2 l1nx = loc1[max(0, min(tid, Pn - 1))];
+        for (int s = tid; s < Pn; s += T) {
             const double d = XB[s];
             const double2 l1u = l1nx;
-            l1nx = A.loc1[min(s + T, A.Ptot - 1)];
+            l1nx = loc1[min(s + T, Pn - 1)];
             const int c1 = (int)l1u.y;
             const double bc = A.b[c1 >= 0 ? c1 : 0];
-            if (AL) A.uRR[s] = d;
+            if (AL) A.uRR[sb + s] = d;
             if (c1 >= 0) {
                 const double tot = l1u.x * d, dd = bc - tot;
                 A.cvs[c1] = tot;
@@ -6286,7 +6362,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                 continue;
             }
             if (c1 == -2)
-                for (int e = A.loc_ptr[s]; e < A.loc_ptr[s + 1]; ++e) {
+                for (int e = loc_ptr[s]; e < loc_ptr[s + 1]; ++e) {
                     const int ci = A.loc_con[e];
                     const double tot = A.loc_w[e] * d, dd = A.b[ci] - tot;
                     A.cvs[ci] = tot;
@@ -6296,8 +6372,9 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         // global constraints: A(R_new R_new^T) from the slots and their residual
         for (int g = wv; g < A.mg; g += T / 64) {
             const int i = A.glob[g];
+            if (mc && A.con_ptr[(long)wg * A.m + i] == A.con_ptr[(long)wg * A.m + i + 1]) continue;
             double tot = 0.0;
-            for (int k = 0; k < A.K; ++k) {
+            for (int k = mc ? wg : 0; k < (mc ? wg + 1 : A.K); ++k) {
                 const long row = (long)k * A.m + i;
                 double v = 0.0;
                 // four entries a lane in flight, summed in entry order
@@ -6312,7 +6389,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                         sl[u] = A.con_slot[e];
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) xv[u] = XB[sl[u]];
+                    for (int u = 0; u < 4; ++u) xv[u] = XB[sl[u] - sb];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) v = e0 + 64 * u < ee ? v + w[u] * xv[u] : v;
                 }
@@ -6327,24 +6404,33 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         {
             double s10[10];
             block_reduce<10, kSmallThreads>(bacc, s10);
-            if (tid == 0)
-                for (int q = 0; q < 10; ++q) red[q] = s10[q];
+            if (tid == 0) {
+                if (!mc) {
+                    for (int q = 0; q < 10; ++q) red[q] = s10[q];
+                } else if (!xwg_sum(A, wg, xe, 10, s10, red)) {
+                    xfail = 1;
+                }
+            }
         }
         __syncthreads();
+        if (xfail) break;
         LRS_SM_T(7);
         fold = 1;
     }
     // R back to global memory (the iterate stays in W.R: RCUR 0), the control block out
     for (int e = tid; e < N * H; e += T) {
         const int i = e / H, q = e - i * H;
-        reinterpret_cast<double2 *>(A.R + (long)i * LD)[q] = reinterpret_cast<const double2 *>(Rs + (long)i * LS)[q];
+        reinterpret_cast<double2 *>((MC ? A.R + rbo : A.R) + (long)i * LD)[q] = reinterpret_cast<const double2 *>(Rs + (long)i * LS)[q];
     }
-    if (tid == 0) c[C_RCUR] = 0.0;
+    if (tid == 0) {
+        c[C_RCUR] = 0.0;
+        if (xfail) { c[C_ACTIVE] = 0.0; c[C_EXIT] = (double)EXIT_XWG; }
+    }
     __syncthreads();
-    if (tid < C_NCTRL) A.ctrl_out[tid] = c[tid];
-    if (tid < LS_N) A.ls_out[tid] = ls[tid];
+    if (wg == 0 && tid < C_NCTRL) A.ctrl_out[tid] = c[tid];
+    if (wg == 0 && tid < LS_N) A.ls_out[tid] = ls[tid];
 #ifdef LRS_PHASE_TIMING
-    if (tid == 0)
+    if (tid == 0 && wg == 0)
         for (int q = 0; q < 16; ++q) g_phase[3][q] += sm_t[q];
 #endif
 }
@@ -6373,13 +6459,39 @@ static bool small_alm_args(const DevProblem &P, DevWork &W, SmallArgs &A, int *l
         }
         N += c.n;
     }
-    if (P.K > 1 && !P.has_merged) return false;
-    const DevCone &a = P.K > 1 ? P.merged : P.cones[0];
-    if (!small_ld_ok(ld) || N <= 0 || small_lds_bytes(N, ld, P.Ptot, a.adj_nnz, false) > kSmallMaxDynLds) return false;
-    A.al = small_lds_bytes(N, ld, P.Ptot, a.adj_nnz, true) <= kSmallMaxDynLds;
+    if (!small_ld_ok(ld) || N <= 0) return false;
+    const DevCone &a = P.K > 1 && P.has_merged ? P.merged : P.cones[0];
+    A.nwg = 1;
+    A.xs = 1;
+    // LRS_SMALL_MC=1 (tests): one workgroup per cone wherever that applies, also where all fit one
+    const bool force_mc = getenv("LRS_SMALL_MC") && atoi(getenv("LRS_SMALL_MC")) != 0;
+    if ((P.K == 1 || P.has_merged) && !(force_mc && P.K >= 2 && P.cone_sep) &&
+        small_lds_bytes(N, ld, P.Ptot, a.adj_nnz, false) <= kSmallMaxDynLds) {
+        A.al = small_lds_bytes(N, ld, P.Ptot, a.adj_nnz, true) <= kSmallMaxDynLds;
+    } else {
+        // one workgroup per cone: every constraint within one cone, each cone in one CU's LDS
+        if (P.K < 2 || P.K > kSmallMaxWg || !P.cone_sep) return false;
+        bool al = true;
+        for (int k = 0; k < P.K; ++k) {
+            const DevCone &ck = P.cones[k];
+            if (small_lds_bytes(ck.n, ld, ck.P, ck.adj_nnz, false) > kSmallMaxDynLds) return false;
+            al = al && small_lds_bytes(ck.n, ld, ck.P, ck.adj_nnz, true) <= kSmallMaxDynLds;
+        }
+        A.al = al;
+        A.nwg = P.K;
+        A.xs = kSmallXcds;
+        int r0 = 0;
+        for (int k = 0; k < P.K; ++k) {
+            const DevCone &ck = P.cones[k];
+            A.wg[k] = SmallWg{ck.n, r0, ck.slot_off, ck.P, (int)ck.adj_nnz, ck.adj_ptr, ck.adj_low, ck.adj_col, ck.adj_slot};
+            r0 += ck.n;
+        }
+        A.xbuf = W.partB;
+        A.xcnt = reinterpret_cast<unsigned *>(W.partB + 2 * kSmallMaxWg * 16);
+    }
     A.N = N; A.K = P.K; A.m = P.m; A.Ptot = P.Ptot; A.mg = P.mg; A.nadj = (int)a.adj_nnz;
     A.slot_g = reinterpret_cast<const int2 *>(P.slot_g);
-    A.adj_ptr = a.adj_ptr; A.adj_low = a.adj_low; A.adj_col = a.adj_col; A.adj_slot = a.adj_slot;
+    if (A.nwg == 1) A.wg[0] = SmallWg{N, 0, 0, P.Ptot, (int)a.adj_nnz, a.adj_ptr, a.adj_low, a.adj_col, a.adj_slot};
     A.Cw = P.Cw; A.Craw = P.Craw;
     A.loc1 = reinterpret_cast<const double2 *>(P.loc1); A.slot1 = reinterpret_cast<const double2 *>(P.slot1);
     A.loc_ptr = P.loc_ptr; A.loc_con = P.loc_con; A.slot_ptr = P.slot_ptr; A.slot_con = P.slot_con;
@@ -6397,18 +6509,25 @@ bool small_alm_fits(const DevProblem &P, DevWork &W) {
     SmallArgs A{};
     return small_alm_args(P, W, A, nullptr);
 }
-template <int LD, bool AL>
+template <int LD, bool AL, bool MC>
 static int launch_small_ld(const SmallArgs &A, size_t lds, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_small_alm<LD, AL>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_small_alm<LD, AL, MC>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSmallMaxDynLds) != hipSuccess) {
             snprintf(g_err, sizeof(g_err), "single-workgroup inner loop: LDS attribute refused");
             return -1;
         }
         attr = true;
     }
-    hipLaunchKernelGGL((k_small_alm<LD, AL>), dim3(1), dim3(kSmallThreads), lds, st, A);
+    if (A.nwg > 1 && hipMemsetAsync(A.xcnt, 0, sizeof(unsigned), st) != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "single-workgroup inner loop: exchange counter reset failed");
+        return -1;
+    }
+    // one workgroup per cone at blocks 0, xs, 2 xs, ...: consecutive blocks go to consecutive XCDs,
+    // so the cones' workgroups share one XCD's L2 (the blocks between leave at once)
+    const int grid = A.nwg > 1 ? (A.nwg - 1) * A.xs + 1 : 1;
+    hipLaunchKernelGGL((k_small_alm<LD, AL, MC>), dim3(grid), dim3(kSmallThreads), lds, st, A);
     LRS_CHECK_LAUNCH();
     return 0;
 }
@@ -6425,18 +6544,26 @@ int launch_small_alm(const DevProblem &P, DevWork &W, const double *ctrl_in, dou
     A.ctrl_in = ctrl_in;
     A.ctrl_out = ctrl_out;
     A.ls_out = ls_out;
-    const size_t lds = small_lds_bytes(A.N, ld, A.Ptot, A.nadj, A.al != 0);
-#define LRS_SMALL_LD(AL)                                      \
-    switch (ld) {                                             \
-    case 8: return launch_small_ld<8, AL>(A, lds, st);        \
-    case 16: return launch_small_ld<16, AL>(A, lds, st);      \
-    case 24: return launch_small_ld<24, AL>(A, lds, st);      \
-    case 32: return launch_small_ld<32, AL>(A, lds, st);      \
-    case 48: return launch_small_ld<48, AL>(A, lds, st);      \
-    default: return launch_small_ld<64, AL>(A, lds, st);      \
+    size_t lds = small_lds_bytes(A.N, ld, A.Ptot, A.nadj, A.al != 0);
+    if (A.nwg > 1) {   // the largest cone's
+        lds = 0;
+        for (int k = 0; k < A.nwg; ++k) lds = std::max(lds, small_lds_bytes(A.wg[k].n, ld, A.wg[k].P, A.wg[k].nadj, A.al != 0));
     }
-    if (A.al) { LRS_SMALL_LD(true) }
-    LRS_SMALL_LD(false)
+#define LRS_SMALL_LD(AL, MC)                                      \
+    switch (ld) {                                                 \
+    case 8: return launch_small_ld<8, AL, MC>(A, lds, st);        \
+    case 16: return launch_small_ld<16, AL, MC>(A, lds, st);      \
+    case 24: return launch_small_ld<24, AL, MC>(A, lds, st);      \
+    case 32: return launch_small_ld<32, AL, MC>(A, lds, st);      \
+    case 48: return launch_small_ld<48, AL, MC>(A, lds, st);      \
+    default: return launch_small_ld<64, AL, MC>(A, lds, st);      \
+    }
+    if (A.nwg > 1) {
+        if (A.al) { LRS_SMALL_LD(true, true) }
+        LRS_SMALL_LD(false, true)
+    }
+    if (A.al) { LRS_SMALL_LD(true, false) }
+    LRS_SMALL_LD(false, false)
 #undef LRS_SMALL_LD
 }
 
@@ -6662,6 +6789,12 @@ struct SmallCgArgs {
     const double *ce_w, *sa, *Craw, *b, *lam;
     double *cvs, *cvc, *U, *V, *cg_b, *cgc;
 };
+// One launch of k_small_cg: block k runs the half-step of a[k] (several cones' half-steps side
+// by side where no constraint spans two cones: their solves and refreshes touch disjoint rows
+// and constraints, so the reference's cone-by-cone sweep gives the same values)
+struct SmallCgBatch {
+    SmallCgArgs a[kSmallMaxWg];
+};
 
 static size_t small_cg_lds(int n, int rS, int ncl, int ncs, int nce, int nsc, int nadj) {
     const size_t dbl = (size_t)n * rS + ncl + 2 * (size_t)ncs + nce + nsc + rS + 2 * kScW;
@@ -6719,7 +6852,8 @@ __device__ __forceinline__ void sc_row_apply(int e0, int e1, const int *cadj, co
 }
 
 template <int EL, int RPG>
-__global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
+__global__ void __launch_bounds__(kScT) k_small_cg(SmallCgBatch Bt) {
+    const SmallCgArgs &A = Bt.a[blockIdx.x];
     extern __shared__ double smem[];
     const int n = A.n, r = A.r, rS = A.rS;
     double *Ys = smem;                         // [n][rS] the fixed factor
@@ -7063,7 +7197,7 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgArgs A) {
         LRS_SC_T(11);
         if (tid == 0) {
             A.cgc[CG_ITERS] = iters;
-            A.cgc[CG_TOTAL] += iters;
+            atomicAdd(A.cgc + CG_TOTAL, (double)iters);   // several cones' blocks: integers, exact in any order
 #ifdef LRS_PHASE_TIMING
             g_phase[1][14] += iters;
             g_phase[1][15] += 1;
@@ -7119,7 +7253,7 @@ bool small_cg_fits(const DevProblem &P, int cone) {
 }
 
 template <int EL, int RPG>
-static int launch_small_cg_t(const SmallCgArgs &A, size_t lds, hipStream_t st) {
+static int launch_small_cg_t(const SmallCgBatch &A, int nb, size_t lds, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
         if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_small_cg<EL, RPG>),
@@ -7129,19 +7263,15 @@ static int launch_small_cg_t(const SmallCgArgs &A, size_t lds, hipStream_t st) {
         }
         attr = true;
     }
-    hipLaunchKernelGGL((k_small_cg<EL, RPG>), dim3(1), dim3(kScT), lds, st, A);
+    hipLaunchKernelGGL((k_small_cg<EL, RPG>), dim3(nb), dim3(kScT), lds, st, A);
     LRS_CHECK_LAUNCH();
     return 0;
 }
 
-int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double rho, double tol, int maxit,
-                    hipStream_t st) {
-    if (!small_cg_fits(P, cone)) {
-        snprintf(g_err, sizeof(g_err), "single-workgroup ADMM half-step: cone %d does not fit", cone);
-        return -1;
-    }
+static void small_cg_args(const DevProblem &P, DevWork &W, int cone, int side, double rho, double tol, int maxit,
+                          SmallCgArgs &A) {
     const DevCone &c = P.cones[cone];
-    SmallCgArgs A{};
+    A = SmallCgArgs{};
     A.n = c.n; A.r = c.r; A.ld = c.ld; A.rS = c.r | 1; A.side = side; A.maxit = maxit;
     A.ncs = c.cg_ncs; A.ncl = c.cg_ncl; A.ns = c.cg_ns; A.nce = c.cg_nce; A.nsc = c.cg_nsc; A.nadj = c.cg_nadj;
     A.cconst = c.dense_c == 2 ? 2 : c.cg_cconst;
@@ -7153,28 +7283,72 @@ int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double 
     A.sp = c.cg_sp; A.sj = c.cg_sj; A.cc_ptr = c.cg_cc_ptr; A.cc = c.cg_cc; A.ce_w = c.cg_ce_w; A.sa = c.cg_sa;
     A.Craw = P.Craw; A.b = P.b; A.lam = W.lam;
     A.cvs = W.cvs; A.cvc = W.cvc + (long)cone * P.m; A.U = W.U; A.V = W.V; A.cg_b = W.cg_b; A.cgc = W.cgc;
-    const size_t lds = small_cg_lds(c.n, A.rS, A.ncl, A.ncs, A.nce, A.nsc, A.nadj);
+}
+static int small_cg_variant(const DevCone &c) {   // EL * 16 + rows per group, 0 if none
     const int EL = (c.r + kScL - 1) / kScL, RPG = (c.n + kScG - 1) / kScG;
     const int rpg = small_cg_rpg(EL, RPG);
-    switch (EL * 16 + rpg) {
-    case 1 * 16 + 2: return launch_small_cg_t<1, 2>(A, lds, st);
-    case 1 * 16 + 4: return launch_small_cg_t<1, 4>(A, lds, st);
-    case 1 * 16 + 6: return launch_small_cg_t<1, 6>(A, lds, st);
-    case 1 * 16 + 8: return launch_small_cg_t<1, 8>(A, lds, st);
-    case 2 * 16 + 2: return launch_small_cg_t<2, 2>(A, lds, st);
+    return rpg ? EL * 16 + rpg : 0;
+}
+static int launch_small_cg_v(int v, const SmallCgBatch &B, int nb, size_t lds, hipStream_t st) {
+    switch (v) {
+    case 1 * 16 + 2: return launch_small_cg_t<1, 2>(B, nb, lds, st);
+    case 1 * 16 + 4: return launch_small_cg_t<1, 4>(B, nb, lds, st);
+    case 1 * 16 + 6: return launch_small_cg_t<1, 6>(B, nb, lds, st);
+    case 1 * 16 + 8: return launch_small_cg_t<1, 8>(B, nb, lds, st);
+    case 2 * 16 + 2: return launch_small_cg_t<2, 2>(B, nb, lds, st);
 #if LRS_SC_NT == 1024
-    case 1 * 16 + 3: return launch_small_cg_t<1, 3>(A, lds, st);
-    case 2 * 16 + 3: return launch_small_cg_t<2, 3>(A, lds, st);
+    case 1 * 16 + 3: return launch_small_cg_t<1, 3>(B, nb, lds, st);
+    case 2 * 16 + 3: return launch_small_cg_t<2, 3>(B, nb, lds, st);
 #endif
-    case 2 * 16 + 4: return launch_small_cg_t<2, 4>(A, lds, st);
-    case 2 * 16 + 6: return launch_small_cg_t<2, 6>(A, lds, st);
-    case 3 * 16 + 2: return launch_small_cg_t<3, 2>(A, lds, st);
-    case 3 * 16 + 4: return launch_small_cg_t<3, 4>(A, lds, st);
-    case 4 * 16 + 2: return launch_small_cg_t<4, 2>(A, lds, st);
+    case 2 * 16 + 4: return launch_small_cg_t<2, 4>(B, nb, lds, st);
+    case 2 * 16 + 6: return launch_small_cg_t<2, 6>(B, nb, lds, st);
+    case 3 * 16 + 2: return launch_small_cg_t<3, 2>(B, nb, lds, st);
+    case 3 * 16 + 4: return launch_small_cg_t<3, 4>(B, nb, lds, st);
+    case 4 * 16 + 2: return launch_small_cg_t<4, 2>(B, nb, lds, st);
     default:
-        snprintf(g_err, sizeof(g_err), "single-workgroup ADMM half-step: no variant for r %d, n %d", c.r, c.n);
+        snprintf(g_err, sizeof(g_err), "single-workgroup ADMM half-step: no variant %d", v);
         return -1;
     }
+}
+
+int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double rho, double tol, int maxit,
+                    hipStream_t st) {
+    if (!small_cg_fits(P, cone)) {
+        snprintf(g_err, sizeof(g_err), "single-workgroup ADMM half-step: cone %d does not fit", cone);
+        return -1;
+    }
+    const DevCone &c = P.cones[cone];
+    SmallCgBatch B{};
+    small_cg_args(P, W, cone, side, rho, tol, maxit, B.a[0]);
+    const SmallCgArgs &A = B.a[0];
+    const size_t lds = small_cg_lds(c.n, A.rS, A.ncl, A.ncs, A.nce, A.nsc, A.nadj);
+    return launch_small_cg_v(small_cg_variant(c), B, 1, lds, st);
+}
+
+// Every cone's half-step on one side in one launch (a block a cone): the cones each fit the
+// single-workgroup kernel with the same variant, no constraint spans two cones (DevProblem::cone_sep).
+bool small_cg_batch_fits(const DevProblem &P) {
+    if (P.K < 2 || P.K > kSmallMaxWg || !P.cone_sep) return false;
+    const int v = small_cg_fits(P, 0) ? small_cg_variant(P.cones[0]) : 0;
+    if (!v) return false;
+    for (int k = 1; k < P.K; ++k)
+        if (!small_cg_fits(P, k) || small_cg_variant(P.cones[k]) != v) return false;
+    return true;
+}
+int launch_small_cg_batch(const DevProblem &P, DevWork &W, int side, double rho, double tol, int maxit,
+                          hipStream_t st) {
+    if (!small_cg_batch_fits(P)) {
+        snprintf(g_err, sizeof(g_err), "single-workgroup ADMM half-steps: the cones do not fit one launch");
+        return -1;
+    }
+    SmallCgBatch B{};
+    size_t lds = 0;
+    for (int k = 0; k < P.K; ++k) {
+        small_cg_args(P, W, k, side, rho, tol, maxit, B.a[k]);
+        const SmallCgArgs &A = B.a[k];
+        lds = std::max(lds, small_cg_lds(A.n, A.rS, A.ncl, A.ncs, A.nce, A.nsc, A.nadj));
+    }
+    return launch_small_cg_v(small_cg_variant(P.cones[0]), B, P.K, lds, st);
 }
 
 }  // namespace lrs

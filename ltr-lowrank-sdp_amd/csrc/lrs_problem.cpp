@@ -163,10 +163,13 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
                 if (mg > kSmallAutoMaxGlobal) ok = false;
             }
             size_t e0 = 0;
+            std::vector<long> cone_lds(K, 0);   // per cone: 2 n + (slots) ... in doubles, ld added below
+            std::vector<int> cone_n(K, 0);
             for (int k = 0; k < K && ok; ++k) {
                 size_t e1 = e0;
                 while (e1 < raw.size() && raw[e1].cone == k) e1++;
                 const int n = dims[k];
+                cone_n[k] = n;
                 N += n;
                 if (N > 4096) { ok = false; break; }
                 std::vector<std::pair<int, int>> pr, cc;
@@ -176,7 +179,8 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
                     else { pr.push_back({raw[e].row, raw[e].col}); cons.push_back(raw[e].con); }
                 }
                 std::sort(pr.begin(), pr.end());
-                Ptot += (long)(std::unique(pr.begin(), pr.end()) - pr.begin());
+                cone_lds[k] = (long)(std::unique(pr.begin(), pr.end()) - pr.begin());
+                Ptot += cone_lds[k];
                 std::sort(cons.begin(), cons.end());
                 const long nnzRows = (long)(std::unique(cons.begin(), cons.end()) - cons.begin());
                 std::sort(cc.begin(), cc.end());
@@ -208,8 +212,23 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
                 ldmin = std::min(ldmin, ldk);
                 e0 = e1;
             }
-            auto_const = ok && any && ldmax <= 64 && ldmin == ldmax &&
-                         (2L * N * (ldmax + 2) + Ptot) * (long)sizeof(double) <= kSmallLdsBudget;
+            bool fits = (2L * N * (ldmax + 2) + Ptot) * (long)sizeof(double) <= kSmallLdsBudget;
+            if (ok && !fits && K >= 2 && K <= kSmallAutoMaxCones) {
+                // one workgroup per cone (lrs_kernels.hip small_alm_args): every constraint within
+                // one cone and each cone's R, D and slots within the budget
+                std::vector<int> owner(m + 1, -1);
+                bool sep = true;
+                for (size_t e = 0; e < raw.size() && sep; ++e) {
+                    if (raw[e].con == 0) continue;
+                    int &o = owner[raw[e].con];
+                    if (o < 0) o = raw[e].cone;
+                    else if (o != raw[e].cone) sep = false;
+                }
+                fits = sep;
+                for (int k = 0; k < K && fits; ++k)
+                    fits = (2L * cone_n[k] * (ldmax + 2) + cone_lds[k]) * (long)sizeof(double) <= kSmallLdsBudget;
+            }
+            auto_const = ok && any && ldmax <= 64 && ldmin == ldmax && fits;
         }
     }
     size_t q = 0;
@@ -767,6 +786,12 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
             }
             con_ptr[(long)k * m + i + 1] = (int)con_slot.size();
         }
+    }
+    dp.cone_sep = true;   // (the one-workgroup-per-cone inner loop needs no cross-cone sums per constraint)
+    for (int i = 0; i < m && dp.cone_sep; ++i) {
+        int nk = 0;
+        for (int k = 0; k < hp.K; ++k) nk += con_ptr[(long)k * m + i + 1] > con_ptr[(long)k * m + i] ? 1 : 0;
+        dp.cone_sep = nk <= 1;
     }
     // slot -> (con, a) CSR, constraints ascending per slot
     std::vector<int> slot_ptr(Ptot + 1, 0), slot_con(Z);

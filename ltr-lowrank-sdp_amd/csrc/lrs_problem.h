@@ -46,8 +46,9 @@ constexpr int kDenseCMinN = 1024;
 // rank-one products (any n >= 2).  LRS_CONST_C=1 every such block, =0 none; unset: only when
 // the whole problem fits the single-workgroup inner loop at every rank the solve can reach
 // (every cone's C constant or absent; R and D of all cones at the widest layout of
-// sqrt(2 nnzRows) + 1 columns plus the constraint pattern within kSmallLdsBudget of LDS; one
-// row layout for every cone; at most kSmallAutoMaxConst constant cones and, unless LRS_SMALL=1,
+// sqrt(2 nnzRows) + 1 columns plus the constraint pattern within kSmallLdsBudget of LDS -- or,
+// every constraint inside one cone and at most kSmallAutoMaxCones cones, each cone's within it
+// (a workgroup a cone); one row layout for every cone; at most kSmallAutoMaxConst constant cones and, unless LRS_SMALL=1,
 // kSmallAutoMaxGlobal multi-slot constraints; not under LRS_SMALL=0) --
 // that loop needs the constant form (the slot form's n (n + 1) / 2 objective slots do not fit
 // one CU), while the multi-launch iteration runs faster on the slot form (theta3: 44 us vs
@@ -56,6 +57,7 @@ constexpr int kConstCMinN = 2;
 constexpr long kSmallLdsBudget = 136 * 1024;   // = lrs_kernels.hip kSmallMaxDynLds
 constexpr int kSmallAutoMaxGlobal = 16;        // = lrs_solver.cpp kSmallMaxGlobal
 constexpr int kSmallAutoMaxConst = 4;          // = lrs_kernels.hip kSmallMaxConst
+constexpr int kSmallAutoMaxCones = 8;          // = lrs_kernels.hip kSmallMaxWg (one workgroup per cone)
 
 struct HostProblem {
     int m = 0, K = 0, nLp = 0;

@@ -1500,6 +1500,10 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
                             c->st));
         HIPC(hipStreamSynchronize(c->st));
         res = c->hpin + kHpCtrl;
+        if ((int)res[C_EXIT] == EXIT_XWG) {
+            set_err("single-workgroup inner loop: the cones' workgroups did not meet (exchange timed out)");
+            return -1;
+        }
         enq = std::max(0L, (long)res[C_INNER] - io.inner);
         c->dp.last_path = 4;
         if (c->stats) c->st_batches++;
@@ -2121,7 +2125,13 @@ static int admm_half_step(lrs_ctx *c, int k, int side, double rho, double tol, i
 
 static int admm_update_var(lrs_ctx *c, double rho, double tol, int maxit) {
     bool dev = false;
-    for (int k = 0; k < c->dp.K; ++k)
+    // cones with no constraint in common: the sweep's half-steps of one side side by side
+    // (LRS_SMALL_CG_BATCH=0: one launch a cone)
+    const char *eb = getenv("LRS_SMALL_CG_BATCH");
+    const bool batch = !(eb && eb[0] == '0') && use_small_cg(c, 0) && small_cg_batch_fits(c->dp);
+    for (int side = 0; side < 2 && batch; ++side) OPC(launch_small_cg_batch(c->dp, c->W, side, rho, tol, maxit, c->st));
+    dev = batch;
+    for (int k = 0; k < c->dp.K && !batch; ++k)
         for (int side = 0; side < 2; ++side) {
             bool d = false;
             if (admm_half_step(c, k, side, rho, tol, maxit, &d)) return -1;

@@ -140,3 +140,21 @@ def test_small_cg_tiny_cone_rank_below_16(solver_mod, monkeypatch, tmp_path):
     (ua, va), (ub, vb) = out
     assert np.all(np.isfinite(ua)) and np.all(np.isfinite(va))
     assert rel(ua, ub) < 1e-8 and rel(va, vb) < 1e-8, (rel(ua, ub), rel(va, vb))
+
+
+def test_small_cg_cones_side_by_side_equal_the_sweep(solver_mod, monkeypatch):
+    """theta25x3 (three cones, no constraint in two): every cone's half-step of one side in one
+    launch (a block a cone, LRS_SMALL_CG_BATCH default) against the reference's cone-by-cone
+    sweep (=0).  The cones' solves and refreshes touch disjoint rows and constraints, so the
+    whole solve is bitwise the same."""
+    res = {}
+    for batch in ("1", "0"):
+        monkeypatch.setenv("LRS_SMALL_CG_BATCH", batch)
+        sv = solver_mod.Solver(instance("theta25x3"))
+        res[batch] = sv.solve(reoptLevel=0)
+        sv.close()
+    a, b = res["1"], res["0"]
+    assert a["admm_iter"] > 0
+    for key in ("alm_inner", "admm_iter", "pobj", "dobj", "pinf", "gap", "cg_iter"):
+        if key in a:
+            assert a[key] == b[key], (key, a[key], b[key])

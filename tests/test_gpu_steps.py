@@ -185,17 +185,19 @@ def test_lbfgs_ring_of_one(solver_mod):
     assert r1["alm_pinf"] <= 1e-3 and r1["alm_inner"] > 0
 
 
-SMALL_CASES = [(n, c) for n in ["mc_rand200", "mc_torus12x10", "mc_rand300w", "theta40", "theta25x3", "rsparse60"]
-               for c in (["0", "1"] if n.startswith("theta") else ["0"])]
+SMALL_CASES = [(n, c, "0") for n in ["mc_rand200", "mc_torus12x10", "mc_rand300w", "theta40", "theta25x3", "rsparse60"]
+               for c in (["0", "1"] if n.startswith("theta") else ["0"])] + [("theta25x3", c, "1") for c in ("0", "1")]
 
 
-@pytest.mark.parametrize("name,const", SMALL_CASES)
-def test_single_workgroup_inner_loop_matches_reference(solver_mod, name, const, monkeypatch):
+@pytest.mark.parametrize("name,const,mc", SMALL_CASES)
+def test_single_workgroup_inner_loop_matches_reference(solver_mod, name, const, mc, monkeypatch):
     """Kernel path 4: the whole inner loop of each run_inner call in one launch of one workgroup
     (lrs_kernels.hip k_small_alm; R and D in LDS, barriers between the trips' phases), theta's
     C = -J as a slot pattern (LRS_CONST_C=0) and as the constant objective's column sums (=1):
-    the reference's own trips, 1e-9 as the multi-launch kernels."""
+    the reference's own trips, 1e-9 as the multi-launch kernels.  mc = 1 (LRS_SMALL_MC): one
+    workgroup per cone (theta25x3's three cones), the trips' sums exchanged between them."""
     monkeypatch.setenv("LRS_CONST_C", const)
+    monkeypatch.setenv("LRS_SMALL_MC", mc)
     z = np.load(os.path.join(GOLDEN, f"steps_{name}.npz"))
     rank = int(z["rank_flag"])
     kw = {"reoptLevel": 0}
