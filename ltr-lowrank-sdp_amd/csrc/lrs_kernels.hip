@@ -5849,33 +5849,46 @@ struct SmallArgs {
     double *xbuf;
     unsigned *xcnt;
 };
-// The per-trip sums of the workgroups of one multi-cone launch (SmallArgs::nwg > 1): thread 0
-// of each stores its nv partial sums (relaxed device-scope stores, which reach the coherence
-// point), waits for their completion, counts itself in, spins on the counter until every
-// workgroup of this exchange has arrived and sums the nwg partials in workgroup order, so every
-// workgroup holds the same totals.  Two parities of the buffer: a workgroup cannot reach
-// exchange e + 2 before every workgroup has read exchange e.  Returns false when the others do
-// not arrive within the spin limit (the caller ends the loop).
-__device__ __forceinline__ bool xwg_sum(const SmallArgs &A, int wg, unsigned &xe, int nv, const double *v,
-                                        double *out) {
+// The per-trip sums of the workgroups of one multi-cone launch (SmallArgs::nwg > 1), by wave 0
+// of each: lane q stores partial sum q (a relaxed device-scope store: write-through to the
+// coherence point), the wave waits for its stores, lane 0 counts the workgroup in and polls the
+// counter until every workgroup of this exchange has arrived, then lane (k, q) loads workgroup
+// k's sum q (device-scope loads, all in flight together) into xr and lane q adds them in
+// workgroup order -- every workgroup gets the same totals (MI355X_MICROARCH.md, the hand-off
+// table's first row: sc1 payload, drained, one counter add per workgroup, an sc1 poll, the
+// polling wave's own loads after the match).  Two parities of the buffer: a workgroup cannot
+// reach exchange e + 2 before every workgroup has read exchange e.  xs: this workgroup's nv
+// sums (LDS); out: the totals (LDS); returns false when the others do not arrive within the
+// spin limit (the caller ends the loop).
+__device__ __forceinline__ bool xwg_sum(const SmallArgs &A, int wg, unsigned &xe, int nv, const double *xs,
+                                        double *xr, double *out) {
+    const int lane = threadIdx.x & 63;
     double *buf = A.xbuf + (long)(xe & 1u) * kSmallMaxWg * 16;
-    for (int q = 0; q < nv; ++q)
-        __hip_atomic_store(buf + wg * 16 + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane < nv) __hip_atomic_store(buf + wg * 16 + lane, xs[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);   // the stores acknowledged before the arrival is counted
+    __builtin_amdgcn_s_waitcnt(0);   // the wave's stores acknowledged before the arrival is counted
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __hip_atomic_fetch_add(A.xcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned target = (xe + 1u) * (unsigned)A.nwg;
     xe++;
-    for (long spin = 0; __hip_atomic_load(A.xcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
-        if (spin > (1L << 26)) return false;
-        __builtin_amdgcn_s_sleep(1);
+    int ok = 1;
+    if (lane == 0) {
+        __hip_atomic_fetch_add(A.xcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (long spin = 0; __hip_atomic_load(A.xcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+            if (spin > (1L << 26)) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
     }
+    ok = __builtin_amdgcn_readfirstlane(ok);
+    if (!ok) return false;
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    for (int q = 0; q < nv; ++q) out[q] = 0.0;
-    for (int k = 0; k < A.nwg; ++k)
-        for (int q = 0; q < nv; ++q)
-            out[q] += __hip_atomic_load(buf + k * 16 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = lane / 16, q = lane % 16; k < A.nwg; k += 4)
+        if (q < nv) xr[k * 16 + q] = __hip_atomic_load(buf + k * 16 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nv) {
+        double t = 0.0;
+        for (int k = 0; k < A.nwg; ++k) t += xr[k * 16 + lane];
+        out[lane] = t;
+    }
     return true;
 }
 
@@ -5952,7 +5965,8 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
     __shared__ double csR[kSmallMaxConst][kSmallMaxLd], csD[kSmallMaxConst][kSmallMaxLd];
     __shared__ double cpart[kSmallThreads];
     __shared__ int xfail;
-    unsigned xe = 0;   // exchanges so far (thread 0)
+    __shared__ double xsum[16], xrecv[kSmallMaxWg * 16];   // the exchange's own sums, the received ones
+    unsigned xe = 0;   // exchanges so far (wave 0)
     const int lane = tid & 63, wv = tid >> 6, sl_lane = tid % TPR;
     const double rho = A.par[P_RHO], rhoInv = 1.0 / rho;
     if (tid < LS_N) ls[tid] = 0.0;
@@ -6174,12 +6188,12 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
                     s7[0] += a;
                     s7[1] += bb;
                 }
-                if (!mc) {
-                    for (int q = 0; q < 7; ++q) red[q] = s7[q];
-                } else if (!xwg_sum(A, wg, xe, 7, s7, red)) {
-                    xfail = 1;
-                }
+                for (int q = 0; q < 7; ++q) (mc ? xsum : red)[q] = s7[q];
             }
+        }
+        if (mc) {
+            __syncthreads();
+            if (wv == 0 && !xwg_sum(A, wg, xe, 7, xsum, xrecv, red) && lane == 0) xfail = 1;
         }
         __syncthreads();   // every rec written, the reduced sums in red
         if (xfail) break;
@@ -6404,13 +6418,12 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         {
             double s10[10];
             block_reduce<10, kSmallThreads>(bacc, s10);
-            if (tid == 0) {
-                if (!mc) {
-                    for (int q = 0; q < 10; ++q) red[q] = s10[q];
-                } else if (!xwg_sum(A, wg, xe, 10, s10, red)) {
-                    xfail = 1;
-                }
-            }
+            if (tid == 0)
+                for (int q = 0; q < 10; ++q) (mc ? xsum : red)[q] = s10[q];
+        }
+        if (mc) {
+            __syncthreads();
+            if (wv == 0 && !xwg_sum(A, wg, xe, 10, xsum, xrecv, red) && lane == 0) xfail = 1;
         }
         __syncthreads();
         if (xfail) break;
