@@ -136,6 +136,8 @@ struct lrs_ctx {
     DevWork W;
     bool walloc = false;
     double *hpin = nullptr;     // pinned scalars (layout: HpinSlot)
+    double *hgram = nullptr;    // pinned: every cone's r x r Gram of one oracle-rank evaluation
+    size_t hgram_n = 0;
     // L-BFGS mirror
     int head = 0, gcur = 0;
     double beta[2] = {0, 0}, yy[2] = {0, 0};
@@ -1194,15 +1196,34 @@ static int gram_of(lrs_ctx *c, int k, const double *X, const double *Y, int avg,
 }
 
 static int oracle_rank(lrs_ctx *c, int phase) {
+    const int K = c->dp.K;
+    // every cone's Gram copied behind its launch into one pinned buffer, one synchronisation
+    size_t need = 0;
+    for (int k = 0; k < K; ++k) need += (size_t)c->rank[k] * c->rank[k];
+    if (need > c->hgram_n) {
+        if (c->hgram) HIPC(hipHostFree(c->hgram));
+        c->hgram = nullptr;
+        HIPC(hipHostMalloc((void **)&c->hgram, sizeof(double) * need));
+        c->hgram_n = need;
+    }
+    size_t off = 0;
+    for (int k = 0; k < K; ++k) {
+        int nblk = 0;
+        if (phase == 1) OPC(launch_gram(c->dp, k, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st));
+        else OPC(launch_gram(c->dp, k, c->W.U, c->W.V, 1, c->W.gram, &nblk, c->st));
+        const size_t rr = (size_t)c->rank[k] * c->rank[k];
+        HIPC(hipMemcpyAsync(c->hgram + off, c->W.gram, sizeof(double) * rr, hipMemcpyDeviceToHost, c->st));
+        off += rr;
+    }
+    HIPC(hipStreamSynchronize(c->st));
     int tot = 0;
-    for (int k = 0; k < c->dp.K; ++k) {
-        std::vector<double> g;
-        if (phase == 1) {
-            if (gram_of(c, k, c->W.R, nullptr, 0, g)) return -1;
-        } else {
-            if (gram_of(c, k, c->W.U, c->W.V, 1, g)) return -1;
-        }
+    off = 0;
+    for (int k = 0; k < K; ++k) {
+        const size_t rr = (size_t)c->rank[k] * c->rank[k];
+        std::vector<double> g(c->hgram + off, c->hgram + off + rr);
+        if (sharded(c) && c->comm->allreduce_host(c, g.data(), (int)rr)) return -1;
         tot += sym_count(c->rank[k], g, 1e-6);
+        off += rr;
     }
     return tot;
 }
@@ -2549,6 +2570,7 @@ void lrs_ctx_destroy(lrs_ctx *c) {
     free_work(c);
     if (c->loaded) free_problem(c->dp);
     if (c->hpin) (void)hipHostFree(c->hpin);
+    if (c->hgram) (void)hipHostFree(c->hgram);
     if (c->hmir) (void)hipHostFree(c->hmir);
     for (auto &e : c->bev)
         if (e) (void)hipEventDestroy(e);
