@@ -125,6 +125,34 @@ def read_sdpa_dense(path):
     return m, dims, b, C, A
 
 
+def block_traces(path):
+    """Per block, tr(X_k) when one constraint is v I over that block alone (theta-type blocks,
+    each with its own trace constraint), else None for the file."""
+    with open(path) as f:
+        toks = [t for ln in f if not ln.lstrip().startswith(("*", '"')) for t in ln.replace(",", " ").replace("{", " ")
+                .replace("}", " ").replace("(", " ").replace(")", " ").split()]
+    m, nb = int(toks[0]), int(toks[1])
+    dims = [abs(int(float(t))) for t in toks[2:2 + nb]]
+    b = [float(t) for t in toks[2 + nb:2 + nb + m]]
+    ents = {}
+    q = 2 + nb + m
+    while q + 4 < len(toks):
+        c, blk, i, j, v = int(toks[q]), int(toks[q + 1]), int(toks[q + 2]), int(toks[q + 3]), float(toks[q + 4])
+        q += 5
+        if c >= 1 and v != 0.0:
+            ents.setdefault(c, []).append((blk, i, j, v))
+    tr = [None] * nb
+    for c, e in ents.items():
+        blks = {blk for blk, *_ in e}
+        if len(blks) != 1:
+            continue
+        k = next(iter(blks)) - 1
+        if len(e) == dims[k] and all(i == j for _, i, j, _ in e) and len({v for *_, v in e}) == 1 and \
+                len({i for _, i, _, _ in e}) == dims[k]:
+            tr[k] = b[c - 1] / e[0][3]
+    return None if any(t is None for t in tr) else tr
+
+
 def fixed_trace(path):
     """tr(X) when the constraints fix it for every feasible X of the SDPA file at `path`, else
     None: either every diagonal entry of every block is its own single-entry constraint

@@ -102,3 +102,47 @@ def test_config_solve_matches_reference(mods, tmp_path, name):
         assert reached(s["gap"], s["pinf"]) == reached(ref["admm_gap"], ref["admm_pinf"]), (s["gap"], ref["admm_gap"])
         # the inner-iteration count of a chaotic trajectory: same order (+-25 %)
         assert abs(s["alm_inner"] - ref["alm_inner"]) <= 0.25 * ref["alm_inner"], (s["alm_inner"], ref["alm_inner"])
+
+
+@pytest.mark.parametrize("name", ["theta3", "theta3x3"])
+def test_theta_configs_certified_intervals(mods, name, tmp_path):
+    """theta's objectives pinned beyond the loose bar above, as tests/test_tight_objectives.py
+    does for the general SDPs: each trace block X_k has tr X_k fixed (1), so any multipliers
+    certify  OPT >= b^T lambda + sum_k min(lambda_min(S_k), 0) tr X_k  (rigorous), and a final
+    iterate with residual A(X) - b is optimal for the right-hand side A(X), so to first order
+    OPT <= <C, X> + |lambda|_2 |A(X) - b|_2 (pinf = |A(X) - b|_2 / (1 + |b|_1), lorads_alg_common.c:424).  The
+    reference's final iterate (tests/golden/configs_final_<name>.npz, REF_DUMP of
+    scripts/make_golden_configs_final.py) is evaluated on the device operators (its pObj to
+    1e-12), the device's own solve takes the same flags, and the two intervals must intersect."""
+    import numpy as np
+    from golden_util import block_traces
+    solver, inst = mods
+    g = {c["config"]: c for c in cases()}[name]
+    ref = g["result"]
+    path = inst.config_instance(name, str(tmp_path))
+    traces = block_traces(path)
+    assert traces is not None
+    z = np.load(os.path.join(GOLDEN, f"configs_final_{name}.npz"))
+    sv = solver.Solver(path)
+    from golden_util import read_sdpa_dense
+    b1 = 1.0 + float(np.sum(np.abs(read_sdpa_dense(path)[2])))
+
+    def interval(ev, lam):
+        _, lmin = sv.dual_infeasibility()
+        lo = ev["dobj"] + sum(min(float(l), 0.0) * t for l, t in zip(np.atleast_1d(lmin), traces))
+        hi = ev["pobj"] + float(np.linalg.norm(lam)) * ev["pinf"] * b1
+        return lo, hi, np.atleast_1d(lmin)
+
+    sv.set_rank([int(q) for q in z["ranks"]])
+    sv.set_factor(solver.R, z["R"])
+    sv.set_vec(solver.LAMBDA, z["lam"])
+    ev = sv.dimacs()
+    assert abs(ev["pobj"] - ref["admm_pobj"]) <= 1e-12 * abs(ref["admm_pobj"]), (ev, ref)
+    lo_r, hi_r, lm_r = interval(ev, z["lam"])
+    r = sv.solve(**kwargs(g["flags"]))
+    lo_d, hi_d, lm_d = interval(r, sv.get_vec(solver.LAMBDA))
+    sv.close()
+    print(f"{name}: reference [{lo_r:.9g}, {hi_r:.9g}] (lambda_min {lm_r.min():.2e}, pinf {ev['pinf']:.1e}); "
+          f"device [{lo_d:.9g}, {hi_d:.9g}] (lambda_min {lm_d.min():.2e}, pinf {r['pinf']:.1e}); "
+          f"pObj {r['pobj']:.9g} vs {ref['admm_pobj']:.9g}")
+    assert max(lo_r, lo_d) <= min(hi_r, hi_d) + 1e-9 * abs(ref["admm_pobj"]), (lo_r, hi_r, lo_d, hi_d)
