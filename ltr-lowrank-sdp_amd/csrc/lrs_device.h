@@ -384,6 +384,10 @@ int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double 
 // every cone's half-step of one side in one launch (a block a cone; cones whose constraints
 // each lie in one cone, all fitting k_small_cg with the same variant)
 bool small_cg_batch_fits(const DevProblem &P);
+// the ADMM iteration's evaluation (R = (U + V) / 2, A(R R^T) into cvs / cvc, and per cone
+// {sum (b - A(X))^2, <C, R R^T>, b^T lambda} into out[4k..]) in one launch, a block a cone
+bool small_eval_fits(const DevProblem &P);
+int launch_small_eval(const DevProblem &P, DevWork &W, const double *U, const double *V, double *out, hipStream_t st);
 int launch_small_cg_batch(const DevProblem &P, DevWork &W, int side, double rho, double tol, int maxit,
                           hipStream_t st);
 

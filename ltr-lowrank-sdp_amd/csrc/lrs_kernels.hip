@@ -7364,4 +7364,123 @@ int launch_small_cg_batch(const DevProblem &P, DevWork &W, int side, double rho,
     return launch_small_cg_v(small_cg_variant(P.cones[0]), B, P.K, lds, st);
 }
 
+// ------------------------------------------------------------------------
+// The ADMM iteration's evaluation for small cones in one launch (LORADSCalObjUV_ADMM
+// lorads_admm.c:398-410 + update_dimacs_admm on R = (U + V) / 2): block k takes cone k --
+// R = (U + V) / 2 of its rows (into W.R and LDS), R_p . R_q on its constraint slots (the
+// k_small_cg lists, DevCone::cg_*), each of its constraints' A(R R^T) in entry order (the
+// gather's arithmetic) into A(X) and the cone's share, and the cone's partial sums
+// {sum (b - A(X))^2, <C, R R^T>, sum b lambda} over its constraints.  Cones whose constraints
+// each lie in one cone (DevProblem::cone_sep) and together cover all m; the host adds the
+// cones' partials in cone order.
+// ------------------------------------------------------------------------
+struct SmallEvalCone {
+    int n, r, ld, ncs, ncl, cconst, cslot;
+    long foff;
+    double calpha;
+    const int *cadj_ptr, *cadj, *cl_con, *cl_ptr, *ce, *cc_ptr, *cc;
+    const double *ce_w;
+};
+struct SmallEvalArgs {
+    SmallEvalCone c[kSmallMaxWg];
+    int m;
+    const double *U, *V, *b, *lam, *Craw;
+    double *R, *cvs, *cvc, *out;   // out: [K][4]
+};
+constexpr int kSeT = 256;
+__global__ void __launch_bounds__(kSeT) k_small_eval(SmallEvalArgs A) {
+    const int k = blockIdx.x, tid = threadIdx.x;
+    const SmallEvalCone &C = A.c[k];
+    const int n = C.n, r = C.r;
+    extern __shared__ __attribute__((aligned(16))) double se[];
+    double *Rs = se;                   // [n][r]
+    double *T = Rs + (long)n * r;      // [ncs] slot values
+    double *cs = T + C.ncs;            // [r] column sums (constant objective)
+    for (int t = tid; t < n * C.ld; t += kSeT) {   // every column of the rows, as k_avg
+        const int i = t / C.ld, c = t - i * C.ld;
+        const long o = C.foff + t;
+        const double v = (A.U[o] + A.V[o]) / 2;
+        A.R[o] = v;
+        if (c < r) Rs[(long)i * r + c] = v;
+    }
+    __syncthreads();
+    // the lower constraint slots of each row: T[slot] = R_i . R_j (a thread a row)
+    for (int i = tid; i < n; i += kSeT)
+        for (int q = C.cadj_ptr[i]; q < C.cadj_ptr[i + 1]; ++q) {
+            const int w = C.cadj[q], j = w >> 16;
+            if (j > i) continue;
+            double d = 0.0;
+            for (int c = 0; c < r; ++c) d += Rs[(long)i * r + c] * Rs[(long)j * r + c];
+            T[w & 0xffff] = d;
+        }
+    if (C.cconst && tid < r) {
+        double t = 0.0;
+        for (int i = 0; i < n; ++i) t += Rs[(long)i * r + tid];
+        cs[tid] = t;
+    }
+    __syncthreads();
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (int j = tid; j < C.ncl; j += kSeT) {
+        double v = 0.0;
+        for (int e = C.cl_ptr[j]; e < C.cl_ptr[j + 1]; ++e) v += C.ce_w[e] * T[C.ce[e] >> 1];
+        const int gi = C.cl_con[j];
+        A.cvs[gi] = v;
+        A.cvc[(long)k * A.m + gi] = v;
+        const double d = A.b[gi] - v;
+        acc[0] += d * d;
+        acc[2] += A.b[gi] * A.lam[gi];
+    }
+    if (C.cconst) {
+        if (tid == 0) {
+            const double a = C.cconst == 2 ? C.calpha : A.Craw[C.cslot];
+            double t = 0.0;
+            for (int c = 0; c < r; ++c) t += cs[c] * cs[c];
+            acc[1] = a * t;
+        }
+    } else {
+        for (int i = tid; i < n; i += kSeT)
+            for (int q = C.cc_ptr[i]; q < C.cc_ptr[i + 1]; ++q) {
+                const int j = C.cc[2 * q], sl = C.cc[2 * q + 1];
+                double d = 0.0;
+                for (int c = 0; c < r; ++c) d += Rs[(long)i * r + c] * Rs[(long)j * r + c];
+                acc[1] += A.Craw[sl] * d;
+            }
+    }
+    double s3[3];
+    block_reduce<3, kSeT>(acc, s3);
+    if (tid == 0)
+        for (int q = 0; q < 3; ++q) A.out[4 * k + q] = s3[q];
+}
+static size_t small_eval_lds(const DevCone &c) { return ((size_t)c.n * c.r + c.cg_ncs + c.r) * sizeof(double); }
+bool small_eval_fits(const DevProblem &P) {
+    if (P.shard || P.K > kSmallMaxWg || (P.K > 1 && !P.cone_sep)) return false;
+    long ncl = 0;
+    for (int k = 0; k < P.K; ++k) {
+        const DevCone &c = P.cones[k];
+        if (!c.cg_ok || c.dense_c == 1 || c.n > kScMaxN || small_eval_lds(c) > 64 * 1024) return false;
+        ncl += c.cg_ncl;
+    }
+    return ncl == P.m;   // every constraint in one cone's list
+}
+int launch_small_eval(const DevProblem &P, DevWork &W, const double *U, const double *V, double *out, hipStream_t st) {
+    if (!small_eval_fits(P)) {
+        snprintf(g_err, sizeof(g_err), "single-workgroup ADMM evaluation: the cones do not fit");
+        return -1;
+    }
+    SmallEvalArgs A{};
+    size_t lds = 0;
+    for (int k = 0; k < P.K; ++k) {
+        const DevCone &c = P.cones[k];
+        A.c[k] = SmallEvalCone{c.n, c.r, c.ld, c.cg_ncs, c.cg_ncl, c.dense_c == 2 ? 2 : c.cg_cconst, c.cg_cslot, c.foff,
+                               P.dense_scale * c.c_alpha, c.cg_cadj_ptr, c.cg_cadj, c.cg_cl_con, c.cg_cl_ptr, c.cg_ce,
+                               c.cg_cc_ptr, c.cg_cc, c.cg_ce_w};
+        lds = std::max(lds, small_eval_lds(c));
+    }
+    A.m = P.m; A.U = U; A.V = V; A.b = P.b; A.lam = W.lam; A.Craw = P.Craw;
+    A.R = W.R; A.cvs = W.cvs; A.cvc = W.cvc; A.out = out;
+    hipLaunchKernelGGL(k_small_eval, dim3(P.K), dim3(kSeT), lds, st, A);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
 }  // namespace lrs

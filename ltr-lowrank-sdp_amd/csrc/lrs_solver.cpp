@@ -2173,9 +2173,29 @@ static int update_dimacs_admm(lrs_ctx *c) {   // lorads_alg_common.c:454-462
 // objective <C, R R^T> of R = (U + V) / 2 comes out of the same SDDMM as A(R R^T), so the
 // three evaluations share one set of launches and one host read
 static int admm_eval(lrs_ctx *c) {
-    OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
     double pinf, obj, blam;
-    if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj, &blam)) return -1;
+    // small cones (the single-workgroup half-steps' lists): R, A(R R^T), the residual, the
+    // objective and b^T lambda in one launch, the cones' partials added here in cone order
+    // (LRS_SMALL_EVAL=0: the operator launches below)
+    const char *ev = getenv("LRS_SMALL_EVAL");
+    if (!(ev && ev[0] == '0') && use_small_cg(c, 0) && small_eval_fits(c->dp)) {
+        const int K = c->dp.K;
+        OPC(launch_small_eval(c->dp, c->W, c->W.U, c->W.V, c->W.tot, c->st));
+        HIPC(hipMemcpyAsync(c->hpin + kHpRead, c->W.tot, sizeof(double) * 4 * K, hipMemcpyDeviceToHost, c->st));
+        HIPC(hipStreamSynchronize(c->st));
+        double r2 = 0.0;
+        obj = 0.0;
+        blam = 0.0;
+        for (int k = 0; k < K; ++k) {
+            r2 += c->hpin[kHpRead + 4 * k];
+            obj += c->hpin[kHpRead + 4 * k + 1];
+            blam += c->hpin[kHpRead + 4 * k + 2];
+        }
+        pinf = std::sqrt(r2) / (1 + c->hp.bNrm1);
+    } else {
+        OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
+        if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj, &blam)) return -1;
+    }
     c->pObjVal = obj / c->scaleObjHis;
     c->dObjVal = blam / c->scaleObjHis;
     c->dimPinf = pinf;
@@ -2988,13 +3008,18 @@ int lrs_op_auv(lrs_ctx *c, int u, int v, double *out_m, double *cobj) {
 int lrs_op_dimacs(lrs_ctx *c, int admm, double *out5) {
     LRS_NEED_STATE(c);
     LRS_NEED_ARG(out5);
-    if (admm) OPC(launch_avg(c->dp.NRpad, c->W.U, c->W.V, c->W.R, c->st));
-    double pinf, obj, blam;
-    if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj, &blam)) return -1;
-    c->pObjVal = obj / c->scaleObjHis;
-    c->dObjVal = blam / c->scaleObjHis;
-    c->dimPinf = pinf;
-    c->dimGap = std::fabs(c->pObjVal - c->dObjVal) / (1 + std::fabs(c->pObjVal) + std::fabs(c->dObjVal));
+    double pinf;
+    if (admm) {   // the ADMM loop's own evaluation (admm_eval: R = (U + V) / 2 first)
+        if (admm_eval(c)) return -1;
+        pinf = c->dimPinf;
+    } else {
+        double obj, blam;
+        if (op_constr_xx(c, c->W.R, nullptr, &pinf, &obj, &blam)) return -1;
+        c->pObjVal = obj / c->scaleObjHis;
+        c->dObjVal = blam / c->scaleObjHis;
+        c->dimPinf = pinf;
+        c->dimGap = std::fabs(c->pObjVal - c->dObjVal) / (1 + std::fabs(c->pObjVal) + std::fabs(c->dObjVal));
+    }
     out5[0] = c->pObjVal;
     out5[1] = c->dObjVal;
     out5[2] = pinf;

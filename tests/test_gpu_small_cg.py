@@ -158,3 +158,31 @@ def test_small_cg_cones_side_by_side_equal_the_sweep(solver_mod, monkeypatch):
     for key in ("alm_inner", "admm_iter", "pobj", "dobj", "pinf", "gap", "cg_iter"):
         if key in a:
             assert a[key] == b[key], (key, a[key], b[key])
+
+
+@pytest.mark.parametrize("name", ["theta25x3", "theta40", "mc_rand200"])
+def test_small_eval_matches_operators(solver_mod, monkeypatch, name):
+    """The ADMM iteration's evaluation of small cones in one launch (k_small_eval: R = (U + V) / 2,
+    A(R R^T), the residual, <C, R R^T>, b^T lambda) against the operator launches
+    (LRS_SMALL_EVAL=0: k_avg, the SDDMM, the gather, the dots) on the reference sweep's inputs:
+    the same values up to summation order."""
+    k = np.load(os.path.join(ROOT, "tests", "golden", f"kernels_{name}.npz"))
+    vec, m, rank = k["inputs"], int(k["m"]), int(k["rank"])
+    dims = [int(d) for d in k["dims"]]
+    NR = sum(d * rank for d in dims)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("LRS_SMALL_EVAL", flag)
+        sv = solver_mod.Solver(instance(name))
+        sv.set_rank([rank] * len(dims))
+        sv.set_factor(solver_mod.U, vec[7 * NR:8 * NR])
+        sv.set_factor(solver_mod.V, vec[8 * NR:9 * NR])
+        sv.set_vec(solver_mod.LAMBDA, vec[9 * NR:9 * NR + m])
+        out[flag] = (sv.dimacs(admm=True), sv.get_factor(solver_mod.R), sv.get_vec(solver_mod.CVS))
+        sv.close()
+    (a, ra, ca), (b, rb, cb) = out["1"], out["0"]
+    assert np.array_equal(ra, rb)
+    assert rel(ca, cb) < 1e-13
+    for key in ("pobj", "dobj"):
+        assert abs(a[key] - b[key]) <= 1e-12 * max(1.0, abs(b[key])), (key, a[key], b[key])
+    assert abs(a["pinf"] - b["pinf"]) <= 1e-10 * b["pinf"] + 1e-300, (a["pinf"], b["pinf"])
