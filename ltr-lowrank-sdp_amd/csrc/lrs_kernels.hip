@@ -5364,12 +5364,25 @@ bool alm_stage_a_split(const DevProblem &P) {
     return false;
 }
 
+// Stage B in the bandwidth regime on the plain row kernel (not the long-row / tiled kernels,
+// not sharded): ONE launch (k_it_b MODE 0: every block's line search from the stage-A / G
+// partials, the neighbours' R_new = R + tau D recomputed per entry) instead of the two of the
+// split form (R_new written by the first, read back by the second).  G81-like r = 64: 14.5K ->
+// 15.2K it/s; 2000^2 torus +2 % (profiles/r05zk_bfused_ab.txt).  LRS_B_FUSED=0: the split form.
+static bool b_fused_on() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("LRS_B_FUSED");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v != 0;
+}
 // Whether stage B runs as two launches (bandwidth regime).
 bool alm_stage_b_split(const DevProblem &P) {
     for (int k = 0; k < P.K; ++k) {
         StagePlan pb;
         if (plan_b(P.cones[k], P.K, pb, multi_path(P))) return false;
-        if (!pb.small) return true;
+        if (!pb.small && (pb.wide || P.shard || !b_fused_on())) return true;
     }
     return false;
 }
@@ -5469,6 +5482,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     // long-row kernels in column tiles (k_wide_a / k_wide_b TL): the cone's column segments and
     // the partial-gradient buffer exist, one cone per launch, not sharded; B adds k_wide_bf's blocks
     bool tla[kMaxCones], tlb[kMaxCones];
+    auto bfused = [&](const StagePlan &pl, bool tiled) { return b_fused_on() && !sh && !pl.small && !pl.wide && !tiled; };
     int offBF = nblkB;
     for (int k = 0; k < KL; ++k) {
         // measured slower (C5: A 2.05 -> 2.95 ms, B 1.68 -> 2.08 ms) although the Infinity-Cache fetch
@@ -5710,6 +5724,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
                 if (small) LRS_LAUNCH_B(4, 0);
+                else if (bfused(pb[k], tbt[k])) LRS_LAUNCH_B(1, 0);
                 else LRS_LAUNCH_B(1, 1);
             });
         }
@@ -5734,7 +5749,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     for (int k = 0; k < KL && (mask & 4); ++k) {
         const DevCone &c = cone_of(k);
         const int grid = pb[k].grid;
-        if (pb[k].small) { off += grid; continue; }
+        if (pb[k].small || bfused(pb[k], tbt[k])) { off += grid; continue; }
         if (tbt[k]) {
             static int rcb = 0;   // the resident blocks stride over the items (stage B 864 -> 803 us on C5)
             const int nwb = std::min(grid, resident_blocks(k_tile_b1, &rcb, kRowBlock));
