@@ -1965,9 +1965,11 @@ __global__ void __launch_bounds__(kBlock) k_pack_shared(int m, const int *__rest
 // :38-57), G_new = 2 S R_new, A(R_new R_new^T) on the lower slots with the local
 // constraints' values and residual (primalInfeasibility), the L-BFGS pair s = tau D,
 // y = G_new - G_old (setlbfgsHisTwo :842-863) and nine dots.  Partials written (10).
-// MODE 0: the whole stage.  Bandwidth regime, split in two launches: MODE 1 = line search
-// + R_new = R + tau D of every row (own and halo), MODE 2 = the rest with the neighbours'
-// R_new read back (one row per neighbour instead of R and D) and tau from MODE 1.
+// MODE 0: the whole stage (small regime, and the bandwidth regime's plain rows: b_fused_on).
+// Split in two launches where the second half is the long-row / tiled kernels or the solve is
+// sharded: MODE 1 = line search + R_new = R + tau D of every row (own and halo), MODE 2 = the
+// rest with the neighbours' R_new read back (one row per neighbour instead of R and D) and tau
+// from MODE 1.
 template <int G, int E, int U, int MODE>
 __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_it_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
