@@ -51,22 +51,52 @@ STAGES = ("A: {a} (control, L-BFGS direction, SDDMM sym(RD^T)/DD^T, local q1/q2)
 STAGE_KERNELS = {0: ("k_lat_a", "k_lat_b"), 1: ("k_it_a", "k_it_b")}
 
 
-def pmc_traffic(kernel):
-    """HBM-side bytes per dispatch of `kernel` from the newest committed rocprofv3 PMC
-    summary of this same bench run (profiles/<tag>_pmc.json, scripts/profile_r01.sh:
-    separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per MI355X_MICROARCH.md)."""
+def leg_profile(leg):
+    """The newest committed rocprofv3 leg summary of `leg` (profiles/<tag>_<leg>_pmc.json, written by
+    scripts/leg_profile.sh -> scripts/leg_summary.py): per stage of the split iteration and for
+    A(UU^T), the summed kernel time over the FULL launches of lrs_time_stages / lrs_time_auut
+    relaunch loops and the HBM-side bytes per launch (separate FETCH_SIZE / WRITE_SIZE passes,
+    FETCH doubled per MI355X_MICROARCH.md "HBM").  None if absent."""
     import glob
-    # newest round tag last (r01f < r01h ...): file names, not mtimes, which a checkout resets
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    # newest round tag last (r05 < r06a < r06b ...): file names, not mtimes, which a checkout resets
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{leg}_pmc.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        for k, v in d.items():
-            if k.split("<")[0].endswith(kernel):
-                return v["fetch_bytes"] + v["write_bytes"], v["source"]
-    return None, None
+        if "_stages" in d:
+            d["_source"] = os.path.relpath(f, ROOT).replace("_pmc.json", "_summary.md")
+            return d
+    return None
+
+
+def attach_traffic(res, leg):
+    """roofline.traffic (and per-stage / A(UU^T) traffic) from the leg's committed rocprof summary;
+    the summary's per-stage rocprof kernel time sits beside the bench's HIP-event time so the two
+    can be compared (the probe's relaunch loops are the same lrs_time_stages calls)."""
+    prof = leg_profile(leg)
+    if prof is None:
+        return res
+    st = prof["_stages"]
+    for o in res["stages"]:
+        s = st.get(o["stage"][0])
+        if s:
+            o["traffic"] = s["traffic_bytes"]
+            o["rocprof_us"] = s["rocprof_us"]
+            o["rocprof_frac"] = s["frac_rocprof"]
+    if "auut" in st:
+        res["a_uut"]["traffic"] = st["auut"]["traffic_bytes"]
+        res["a_uut"]["rocprof_us"] = st["auut"]["rocprof_us"]
+        res["a_uut"]["rocprof_frac"] = st["auut"]["frac_rocprof"]
+    dom = st.get(res["kernel"][0])
+    if dom:
+        res["traffic"] = dom["traffic_bytes"]
+        res["rocprof_us"] = dom["rocprof_us"]
+        res["rocprof_frac"] = dom["frac_rocprof"]
+    res["traffic_source"] = (f"{prof['_source']}: per launch, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE summed over the "
+                             "stage's kernels, full relaunches only (scripts/leg_profile.sh)")
+    return res
 
 
 def instance_for(rank_id, rows, cols, cache, seed0=67):
@@ -153,7 +183,7 @@ def tile_bounds(us, lds_bytes, flop):
             "fp64_TFs": flop / s / 1e12, "fp64_frac": flop / s / 1e12 / FP64_VALU_PEAK_TFS}
 
 
-def stage_roofline(sv, reps, with_traffic=False, rank=None):
+def stage_roofline(sv, reps, leg=None, rank=None):
     """Per-launch ms of the split-iteration stages (back-to-back relaunches between two
     HIP events on the solver stream) and their algorithmic bytes -> GB/s.  With `rank` and
     the 2-D tile kernels active, also each tile stage's LDS-read and FP64 fractions
@@ -188,7 +218,6 @@ def stage_roofline(sv, reps, with_traffic=False, rank=None):
             elif o["stage"].startswith("B"):
                 o["tile_bounds"] = tile_bounds(o["avg_launch_us"], (P * 2 + adj) * rank * 8, (P + adj) * rank * 2)
     dom = max(out, key=lambda s: s["avg_launch_us"])
-    traffic, tsrc = pmc_traffic(dom["kernel"]) if with_traffic else (None, None)
     # the north-star's named operator: A(UU^T) straight from the constraint entries
     ams = sv.time_auut(reps)
     aby = sv.auut_bytes()
@@ -202,12 +231,9 @@ def stage_roofline(sv, reps, with_traffic=False, rank=None):
     if rank and auv_tiles:
         auut["tile_bounds"] = tile_bounds(ams * 1e3, sv.nnz * 2 * rank * 8, sv.nnz * rank * 2)
     res = {"bound": "hbm", "kernel": dom["stage"], "achieved": dom["achieved_GBs"], "peak": HBM_PEAK_GBS,
-           "unit": "GB/s", "frac": dom["frac"], "traffic": traffic, "bytes_per_launch": dom["bytes_per_launch"],
+           "unit": "GB/s", "frac": dom["frac"], "traffic": None, "bytes_per_launch": dom["bytes_per_launch"],
            "avg_launch_us": dom["avg_launch_us"], "stages": out, "a_uut": auut}
-    if traffic is not None:
-        res["traffic_source"] = (f"{tsrc}: FETCH_SIZE x2 + WRITE_SIZE per dispatch (bytes); the x2 correction is "
-                                 "calibrated for 16-B/lane reads, these rows mix 16-B and 8-B loads")
-    return res
+    return attach_traffic(res, leg) if leg else res
 
 
 def config_c5(solver, local, iters=20, cpu_seconds=0.0, cache=None):
@@ -220,7 +246,7 @@ def config_c5(solver, local, iters=20, cpu_seconds=0.0, cache=None):
     kw = dict(fixedRank=128, reoptLevel=0)
     # one solve: warmup trips, then `iters` timed trips of the same solve (no setup inside)
     o = sv.alm_timed(3, iters, **kw)
-    rl = stage_roofline(sv, 3, rank=128)
+    rl = stage_roofline(sv, 10, leg="c5", rank=128)
     ms, kms = sv.time_gram(0, 20)
     ceil_tf, probe = mfma_probe(sv)
     n = sv.dims[0]
@@ -586,7 +612,7 @@ def main():
                    "parallelism": f"replicas x{world} (instance-level, weak)"},
         "alm_phase_rate": done / out["seconds"],
         "build": build_provenance(),
-        "roofline": stage_roofline(sv, 300, with_traffic=True),
+        "roofline": stage_roofline(sv, 300, leg="g67"),
     }
     if rank_id == 0 and world == 1 and not args.no_eps:
         eps_flags = dict(reoptLevel=0, heuristicFactor=10.0, phase1Tol=1e-2, phase2Tol=1e-5)
@@ -628,7 +654,7 @@ def main():
         s81.alm_throughput(0, 100, **kw81)
         o81 = s81.alm_throughput(0, 1000, **kw81)
         ns = {"workload": "MaxCut torus 100x200 (G81 structure), n=m=20000, --fixedRank 64",
-              "gpu_it_s": o81["done"] / o81["seconds"], "roofline": stage_roofline(s81, 100)}
+              "gpu_it_s": o81["done"] / o81["seconds"], "roofline": stage_roofline(s81, 100, leg="g81")}
         s81.close()
         if not args.no_cpu:
             it, sec, kind = cpu_reference_rate(p81, 64, min(args.cpu_seconds, 10.0))
@@ -668,7 +694,7 @@ def main():
         load_s = time.perf_counter() - t1
         kwb = dict(fixedRank=16, reoptLevel=0)
         ob = big.alm_timed(5, 60, **kwb)
-        rl = stage_roofline(big, 20)
+        rl = stage_roofline(big, 20, leg="torus2000")
         rl["workload"] = "MaxCut torus 2000x2000 (n=m=4e6), --fixedRank 16, in-memory load"
         rl["it_s"] = ob["done"] / ob["seconds"]
         rl["load_sec"] = load_s

@@ -22,6 +22,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -138,6 +139,7 @@ struct lrs_ctx {
     double *hpin = nullptr;     // pinned scalars (layout: HpinSlot)
     double *hgram = nullptr;    // pinned: every cone's r x r Gram of one oracle-rank evaluation
     size_t hgram_n = 0;
+    bool naive_warned = false;   // --oracleRankNaive: the fallback line printed this solve
     // L-BFGS mirror
     int head = 0, gcur = 0;
     double beta[2] = {0, 0}, yy[2] = {0, 0};
@@ -1227,6 +1229,53 @@ static int oracle_rank(lrs_ctx *c, int phase) {
     }
     return tot;
 }
+// --oracleRankNaive (LORADS_ORACLE_RANK_NAIVE, lorads_logging.c:406-451 selected at :516-533):
+// per cone of at most kNaiveMaxN rows the n x n matrix X = R R^T (phase 1) or
+// ((U+V)/2)((U+V)/2)^T (phase 2) formed in full on the host from the device factor and its
+// eigenvalues above 1e-6 lambda_max counted (sym_count: the same Householder + Sturm count the
+// Gram path uses, i.e. count_significant_from_matrix's rule on the n x n matrix); larger cones
+// take the Gram path after one log line, as the reference prints once per solve.  A sharded
+// context holds only its rows, so it keeps the Gram path (the all-reduced Gram is exact).
+constexpr int kNaiveMaxN = 2000;
+static int oracle_rank_naive(lrs_ctx *c, const lrs_params *p, int phase) {
+    if (sharded(c)) return oracle_rank(c, phase);
+    int tot = 0;
+    for (int k = 0; k < c->dp.K; ++k) {
+        const DevCone &d = c->dp.cones[k];
+        const int n = d.n, r = c->rank[k];
+        if (n > kNaiveMaxN) {
+            if (!c->naive_warned) {
+                logf_(c, p, "skip naive oracle rank for n=%ld, falling back to gram approach.\n", (long)n);
+                c->naive_warned = true;
+            }
+            std::vector<double> g;
+            if (phase == 1) OPC(gram_of(c, k, c->W.R, nullptr, 0, g));
+            else OPC(gram_of(c, k, c->W.U, c->W.V, 1, g));
+            tot += sym_count(r, g, 1e-6);
+            continue;
+        }
+        std::vector<double> F((size_t)n * d.ld), F2;
+        HIPC(hipStreamSynchronize(c->st));
+        HIPC(hipMemcpy(F.data(), (phase == 1 ? c->W.R : c->W.U) + d.foff, sizeof(double) * F.size(),
+                       hipMemcpyDeviceToHost));
+        if (phase != 1) {
+            F2.resize(F.size());
+            HIPC(hipMemcpy(F2.data(), c->W.V + d.foff, sizeof(double) * F2.size(), hipMemcpyDeviceToHost));
+            for (size_t q = 0; q < F.size(); ++q) F[q] = 0.5 * (F[q] + F2[q]);
+        }
+        std::vector<double> X((size_t)n * n);
+        for (int i = 0; i < n; ++i)
+            for (int j = i; j < n; ++j) {
+                double s = 0.0;
+                for (int q = 0; q < r; ++q) s += F[(size_t)i * d.ld + q] * F[(size_t)j * d.ld + q];
+                X[(size_t)i * n + j] = s;
+                X[(size_t)j * n + i] = s;
+            }
+        tot += sym_count(n, std::move(X), 1e-6);
+    }
+    return tot;
+}
+
 static int sum_rank(lrs_ctx *c) {
     int t = 0;
     for (int r : c->rank) t += r;
@@ -1235,7 +1284,7 @@ static int sum_rank(lrs_ctx *c) {
 
 static void record_state(lrs_ctx *c, const lrs_params *p, int phase) {
     int cur = sum_rank(c);
-    int orc = p->disableOracle ? cur : oracle_rank(c, phase);
+    int orc = p->disableOracle ? cur : p->oracleRankNaive ? oracle_rank_naive(c, p, phase) : oracle_rank(c, phase);
     if (orc < 0) orc = 0;
     if (phase == 1) { c->t1c.push_back(cur); c->t1o.push_back(orc); }
     else { c->t2c.push_back(cur); c->t2o.push_back(orc); }
@@ -3066,6 +3115,7 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     c->rank_max = rm;
     if (init_point(c)) return -1;
     c->t1c.clear(); c->t1o.clear(); c->t2c.clear(); c->t2o.clear();
+    c->naive_warned = false;
     c->scaleObjHis = 1.0;
     c->pObjVal = c->dObjVal = 0;
     AlmState alm;
@@ -3180,7 +3230,7 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     else if (admm.gap <= 5 * p->phase2Tol && admm.pinf1 <= p->phase2Tol) res->status = 2;
     else res->status = 3;
     res->final_rank = sum_rank(c);
-    int orc = (p->disableOracle || p->skipADMM) ? res->final_rank : oracle_rank(c, 2);
+    int orc = (p->disableOracle || p->skipADMM) ? res->final_rank : p->oracleRankNaive ? oracle_rank_naive(c, p, 2) : oracle_rank(c, 2);
     res->oracle_rank = orc < 0 ? 0 : orc;
     res->traj1_len = (int)c->t1c.size();
     res->traj2_len = (int)c->t2c.size();
@@ -3370,10 +3420,18 @@ int lrs_time_stages(lrs_ctx *c, int reps, double *stage_ms) {
     AlmIterArgs a{&c->dp, &c->W, nullptr};
     // one full iteration first so that every buffer the stages read is populated
     OPC(enqueue_alm_stages(a, 0, 7, c->st));
+    // profiling aid (scripts/leg_profile.sh): an idle host gap after the priming iteration and
+    // after each stage's loop, so a kernel trace splits into the stages by time alone
+    const char *gap_env = getenv("LRS_TIME_STAGES_GAP_US");
+    const long gap_us = gap_env ? atol(gap_env) : 0;
     hipEvent_t e[4];
     for (auto &x : e) HIPC(hipEventCreate(&x));
     const int masks[3] = {1, 2, 4};
     for (int q = 0; q < 3; ++q) {
+        if (gap_us > 0) {
+            HIPC(hipStreamSynchronize(c->st));
+            std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
+        }
         HIPC(hipEventRecord(e[0], c->st));
         for (int t = 0; t < reps; ++t) OPC(enqueue_alm_stages(a, 0, masks[q], c->st));
         HIPC(hipEventRecord(e[1], c->st));

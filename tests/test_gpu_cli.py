@@ -181,3 +181,42 @@ def test_learned_schedule_round_trip(solver_mod, tmp_path):
     assert out["trajectory"]["phase_1"]["curr_rank"][0] == sched[0]
     # near the reference's optimum (theta40's certified gap ~1e-5 on both sides)
     assert abs(pobj - s["json"]["metrics"]["primal_obj"]) <= 1e-3 * abs(s["json"]["metrics"]["primal_obj"])
+
+
+def _naive_cases():
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "solves_naive.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_oracle_rank_naive_matches_reference(solver_mod, tmp_path, case):
+    """--oracleRankNaive (lorads_logging.c:406-451, :516-533) against the reference's own runs
+    with the flag (tests/golden/solves_naive.json, scripts/make_golden_naive.py): the n x n
+    eigen count for cones of <= 2000 rows, the Gram fallback with its one log line above that
+    (the 50 x 50 torus, n = 2500).  MaxCut trajectories are reproduced step for step, so the
+    oracle-rank arrays must be identical; on theta cases (chaotic trajectories, see above) the
+    final oracle rank and the distinct-value schedule must match.  The naive count also equals
+    the device's own Gram count on the same run (R R^T and R^T R share their nonzero spectrum)."""
+    import hashlib
+    g = _naive_cases()[case]
+    if g["generator"]:
+        inst_mod = __import__("importlib").import_module("ltr-lowrank-sdp_amd.instances")
+        path = str(tmp_path / f"{g['instance']}.dat-s")
+        rows, cols, seed = g["generator"]
+        inst_mod.maxcut_torus(path, rows, cols, seed=seed)
+        assert hashlib.sha256(open(path, "rb").read()).hexdigest() == g["sha256"]
+    else:
+        path = instance(g["instance"])
+    _, js, out = run_cli(solver_mod, path, g["flags"], tmp_path, "naive")
+    assert out.count("skip naive oracle rank for n=") == g["fallback_lines"]
+    tr, rtr = js["trajectory"], g["json"]["trajectory"]
+    if g["instance"].startswith(("mc_", "torus")):
+        for ph in ("phase_1", "phase_2"):
+            assert tr[ph]["oracle_rank"] == rtr[ph]["oracle_rank"], ph
+    else:
+        assert extract_rank_schedule(tr)[-1] == extract_rank_schedule(rtr)[-1]
+    assert js["metrics"]["oracle_rank"] == g["json"]["metrics"]["oracle_rank"]
+    # same run through the Gram path: the counts agree
+    _, jg, _ = run_cli(solver_mod, path, [f for f in g["flags"] if f != "--oracleRankNaive"], tmp_path, "gram")
+    for ph in ("phase_1", "phase_2"):
+        assert tr[ph]["oracle_rank"] == jg["trajectory"][ph]["oracle_rank"], ph
