@@ -6,9 +6,12 @@ Workload: G67-structured MaxCut (2-D toroidal grid 100 x 100, weights +-1, n = m
 default LoRADS rank r = ceil(2 ln n) = 19 held fixed so every step costs the same.
 A "step" is one ALM inner iteration (alm_state.innerIter, lorads_alm.c:1372) of the
 real phase-1 control flow (dual/rho updates and oracle-rank records included) on
-the device.  Multi-GPU: one process per GPU, each solving its own instance (the
-reference's instance-level batching, dataset/run_lorads.sh:85-114): weak scaling,
-no data-path collective; barrier + max-over-ranks timing.
+the device.  Multi-GPU (the north star's constraint sharding): one process
+per GPU, ONE G67 instance row-sharded over the N ranks through RCCL (lrs_shard_rccl: halo
+exchange of the direction rows + all-reduced stage totals per inner iteration) -- strong
+scaling of a single instance; barrier + max-over-ranks timing.  The instance-level replicas
+(each rank its own instance, dataset/run_lorads.sh:85-114, weak scaling, no data-path
+collective) are reported beside it under `replicas`.
 
 Prints one JSON line (rank 0).  Besides the contract keys:
   roofline          dominant split-iteration stage on the workload (HIP-event timed,
@@ -492,6 +495,40 @@ def spawn_ranks(n, argv):
     return rc
 
 
+def sharded_headline_line(args, world, rank_id, dist, replicas, solver, local, cache):
+    """N > 1: the headline instance (seed 67, the same file on every rank) row-sharded over the N
+    ranks through RCCL; W warmup trips, K timed trips of the same solve between barrier + device
+    synchronisation, max over ranks.  Returns (rank, it/s, done, seconds, shard info)."""
+    path = instance_for(0, args.rows, args.cols, cache)
+    sv = solver.Solver(path, device=local)
+    r = args.rank if args.rank > 0 else sv.determine_rank()[0]
+    uid = solver.comm_unique_id() if rank_id == 0 else None
+    if dist is not None:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    sv.shard_rccl(world, rank_id, uid)
+    if sv.comm_ranks() != world:
+        raise RuntimeError(f"RCCL communicator counts {sv.comm_ranks()} ranks, expected {world}")
+    info = sv.shard_info()
+    clock = {}
+
+    def on_start():
+        sv.sync()
+        replicas.barrier_sync(dist)
+        clock["t0"] = time.perf_counter()
+
+    def on_stop():
+        sv.sync()
+        replicas.barrier_sync(dist)
+        clock["t1"] = time.perf_counter()
+
+    out = sv.alm_timed(max(1, args.warmup), args.steps, on_start, on_stop, fixedRank=r, reoptLevel=0)
+    sv.close()
+    _, t_max = replicas.aggregate(dist, 0, clock["t1"] - clock["t0"])
+    return r, out["done"] / t_max, out["done"], t_max, info
+
+
 def dry_run_line(args, world, rank_id, dist, replicas):
     """--dry-run: the launch and timing protocol only (no GPU, no solver): every rank joins the
     process group, meets the barriers around an empty timed region and contributes to the
@@ -503,11 +540,20 @@ def dry_run_line(args, world, rank_id, dist, replicas):
     joined, t_max = replicas.aggregate(dist, 1, dt)   # each rank counts itself once
     return {"metric": "ALM iters/sec, MaxCut G67 (torus 100x100 +-1, n=m=10000), fixed default rank",
             "value": 0.0, "unit": "ALM inner iterations/s", "n_gpus": world, "steps": 0, "warmup": 0,
-            "ms_per_step": t_max * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": t_max * 1e3, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "f64", "data": "dry run: launch and timing protocol only, no GPU work",
-            "config": {"workload": "none (dry run)", "parallelism": f"replicas x{world} (instance-level, weak)"},
+            "config": {"workload": "none (dry run)", "parallelism": headline_parallelism(world)},
+            "headline": headline_kind(world), "replicas": {"scaling": "weak", "value": None},
             "dry_run": True, "backend": dist.get_backend() if dist is not None else None,
             "ranks_aggregated": int(joined)}
+
+
+def headline_kind(world):
+    return "single instance" if world == 1 else "sharded (one instance row-sharded over RCCL, lrs_shard_rccl)"
+
+
+def headline_parallelism(world):
+    return "none (1 GPU)" if world == 1 else f"row-sharded x{world} (one instance; RCCL halo + all-reduce)"
 
 
 def main():
@@ -567,6 +613,27 @@ def main():
     solver = importlib.import_module(PKG + ".solver")
     cache = os.path.join(ROOT, ".bench_instances")
     os.makedirs(cache, exist_ok=True)
+    failed = 0
+    sharded_head = None
+    if world > 1:
+        # the headline at N > 1: ONE instance row-sharded over the ranks (a watchdog keeps a stuck
+        # collective from swallowing the run: the replicas line below is then labelled as such)
+        import threading
+
+        def fire_head():
+            print(f"bench.py rank {rank_id}: sharded headline hung for {args.sharded_timeout:.0f} s", file=sys.stderr,
+                  flush=True)
+            os._exit(3)
+        wd0 = threading.Timer(args.sharded_timeout, fire_head)
+        wd0.daemon = True
+        wd0.start()
+        try:
+            sharded_head = sharded_headline_line(args, world, rank_id, dist, replicas, solver, local, cache)
+        except Exception as e:
+            sharded_head = {"error": repr(e)[:300]}
+            print(f"bench.py rank {rank_id}: sharded headline failed: {e!r}", file=sys.stderr, flush=True)
+            failed = 4
+        wd0.cancel()
     path = instance_for(rank_id, args.rows, args.cols, cache)
     sv = solver.Solver(path, device=local)
     r = args.rank if args.rank > 0 else sv.determine_rank()[0]
@@ -602,18 +669,37 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": t_max * 1e3 / max(1, done),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: seeded G67-structured toroidal grid (real Gset file absent), one instance per rank",
+        "data": "synthetic: seeded G67-structured toroidal grid (real Gset file absent)",
         "config": {"workload": f"MaxCut torus {args.rows}x{args.cols} (G67 structure)", "n": n, "m": sv.m,
                    "rank": r, "pattern_slots": sv.nslots, "constraint_nnz": sv.nnz,
                    "flags": "--fixedRank %d --reoptLevel 0, phase-1 exit disabled, budget = steps" % r,
-                   "parallelism": f"replicas x{world} (instance-level, weak)"},
+                   "parallelism": headline_parallelism(world)},
+        "headline": headline_kind(world),
         "alm_phase_rate": done / out["seconds"],
         "build": build_provenance(),
         "roofline": stage_roofline(sv, 300, leg="g67"),
     }
+    if world > 1:
+        # value = the single row-sharded instance; the per-rank instances (this run's unsharded
+        # solves above) are the weak-scaling replicas
+        line["replicas"] = {"value": done_tot / t_max, "unit": "ALM inner iterations/s (sum over ranks)",
+                            "scaling": "weak", "steps_per_rank": int(done), "seconds_max": t_max,
+                            "workload": "one G67-structured instance per rank (seeds 67 + rank), no data-path collective"}
+        if isinstance(sharded_head, tuple):
+            rs, rate, sdone, ssec, info = sharded_head
+            line["value"] = rate
+            line["steps"] = int(sdone)
+            line["ms_per_step"] = ssec * 1e3 / max(1, sdone)
+            line["config"]["rank"] = rs
+            line["sharded_headline"] = {"transport": "RCCL (ncclSend/Recv halo, ncclAllReduce totals)",
+                                        "rank0_rows": info[3], "rank0_halo_rows": info[4], "seconds_max": ssec}
+        else:
+            line["value"] = 0.0
+            line["headline"] = "sharded headline FAILED (see sharded_headline.error); replicas under `replicas`"
+            line["sharded_headline"] = sharded_head
     if rank_id == 0 and world == 1 and not args.no_eps:
         eps_flags = dict(reoptLevel=0, heuristicFactor=10.0, phase1Tol=1e-2, phase2Tol=1e-5)
         t1 = time.perf_counter()
@@ -704,7 +790,6 @@ def main():
         line["config_c5"] = config_c5(solver, local, cpu_seconds=0.0 if args.no_cpu else 20.0, cache=cache)
     if rank_id == 0 and world == 1 and not args.no_c5b:
         line["config_c5b"] = config_c5b(solver, local, ref_densec=ref_densec_rates())
-    failed = 0
     if not args.no_sharded:
         # a watchdog keeps a stuck collective from swallowing the result line
         import threading

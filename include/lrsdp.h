@@ -130,6 +130,18 @@ int lrs_op_admm_constr(lrs_ctx *ctx);
  * right-hand side, column-major n_k x r_k. */
 int lrs_op_admm_half(lrs_ctx *ctx, int cone, int side, double rho, double cg_tol, int cg_maxit, int *cg_iters,
                      double *rhs);
+/* LP blocks (LORADSSetLpCone, data/lorads_lp_conic.c:347; the *LP slots of lorads_func bound in
+ * LORADSInitFuncSet, data/lorads_solver.c:1014-1053): a problem whose last SDPA block has negative
+ * size -k carries its k LP columns (x_j = r_j^2) as one more cone, the LAST one, of k rows at rank 1
+ * (lrs_get_rank reports 1 for it; lrs_set_rank refuses another rank).  Factors therefore hold the
+ * LP values after the SDP cones' (the reference's rLp / uLp / vLp), and every operator above acts on
+ * it as on an SDP cone with a diagonal pattern -- which is the LP algebra.  Two exceptions follow
+ * the reference: lrs_op_admm_half(ctx, lp_cone, 0, ...) runs the LP block's whole ADMM update, the
+ * closed-form column sweep of LORADSUpdateSDPLPVar (u_j then v_j per column, lorads_admm.c:759-792;
+ * side 1 is refused, cg_iters = 0, rhs untouched), and lrs_op_dual_infeasibility's LP term is
+ * sum_j |min(c_j - sum_i lambda_i a_ij, 0)| (lam_min[lp_cone] = the smallest such value).  The
+ * oracle rank, AUG_RANK and the reported ranks cover the SDP cones only.  Sharded contexts refuse
+ * LP blocks. */
 /* LORADSUpdateDualVar (lorads_alg_common.c:511-524): LAMBDA += rho (b - CVS). */
 int lrs_op_dual_update(lrs_ctx *ctx, double rho);
 /* The second half of one ALM inner trip after the line search (lorads_alm.c:1340-1355):
@@ -251,8 +263,9 @@ int lrs_profile_stages(lrs_ctx *ctx, const lrs_params *p, long steps, double *st
 
 /* In-memory problem in SDPA entry semantics (replaces LReadSDPA for callers that
  * already hold the data, io/lorads_file_io.c:59-455): nblk blocks of sizes dims
- * (last may be negative = LP, unsupported), b[m], and nnz entries (con, blk, row,
- * col, val) with 1-based blk/row/col and con 0 = F0 (C = -F0). */
+ * (the last may be negative: an LP block of -dims[nblk-1] columns, entry row = column, col
+ * unused), b[m], and nnz entries (con, blk, row, col, val) with 1-based blk/row/col and con 0 =
+ * F0 (C = -F0). */
 int lrs_load_coo(lrs_ctx *ctx, int m, int nblk, const int *dims, const double *b, long nnz, const int *con,
                  const int *blk, const int *row, const int *col, const double *val);
 
@@ -311,6 +324,16 @@ int lrs_shard_info(lrs_ctx *ctx, int *world, int *rank, int *row0, int *nown, in
 /* ranks the context's transport counts itself (RCCL: ncclCommCount; loopback: its group's
  * world; 1 unsharded), so a launcher can check that every GPU joined the communicator */
 int lrs_shard_comm_ranks(lrs_ctx *ctx, int *count);
+/* Recording of the transport's operations (sharded contexts): on != 0 clears the log and records
+ * every later operation, 0 stops.  lrs_shard_comm_log: *n = entries recorded; out (may be NULL)
+ * receives min(cap, *n) records of 5 longs {kind, peer, cone, count, offset}: kind 0 = the start
+ * of one halo-exchange group (cone = the vector's cone or -1 for factor rows, count = its ops),
+ * 1 = send to peer, 2 = receive from peer (count doubles; offset: send-buffer position, or the
+ * landing rows' local offset x ld), 3 / 4 = device / host all-reduce of count doubles.  Both
+ * transports issue their groups from one op list, so the loopback transport's log is the
+ * sequence of ncclSend / ncclRecv / ncclAllReduce calls the RCCL transport makes. */
+int lrs_shard_comm_record(lrs_ctx *ctx, int on);
+int lrs_shard_comm_log(lrs_ctx *ctx, long *out, long cap, long *n);
 /* Host-only (no device, no context) view of the row partition of a sharded solve of the
    instance at `path`: counts[8] = {n_global, first owned global row, owned rows, local rows
    (owned + halo), send rows (all peers), shared constraints, local constraints, world}, then

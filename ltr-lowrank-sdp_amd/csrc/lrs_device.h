@@ -91,6 +91,11 @@ Layout choose_layout(int r);
 
 struct DevCone {
     int n = 0, r = 0, ld = 0, G = 0, E = 0;
+    bool lp = false;    // the LP block as the diagonal cone at rank 1 (lrs_problem.cpp build_problem)
+    // LP cone: per row (LP column) its local slot or -1 (a column without data), and per row
+    // the column's squared 2-norm (lp_cone_presolve nrm2Square, lorads_lp_conic.c:132-133)
+    int *lp_slot = nullptr;
+    double *lp_nrm2 = nullptr;
     // rows the kernels compute: [row0, row0 + nown) -- the whole cone, or in a sharded
     // solve this process's rows (the others, the halo, are read as neighbours only)
     int row0 = 0, nown = 0;
@@ -206,6 +211,7 @@ struct DevProblem {
     mutable int last_path = -1;          // path of the last enqueued iteration (0 lat, 1 general)
     mutable int last_tiles = 0;          // the last enqueued iteration ran stage A / B over the 2-D tiles
     int m = 0, K = 0;
+    int lp_cone = -1;   // the LP block's cone (the last), -1 without one
     long NRpad = 0;     // factor buffer length (doubles)
     int Ptot = 0;
     long Z = 0;
@@ -268,6 +274,7 @@ struct DevWork {
     double *uvp = nullptr;   // [Ptot][2] the tiled stage A's (sym(RD^T), DD^T) per slot, for k_it_g
     double *lam = nullptr, *cvs = nullptr, *q1 = nullptr, *q2 = nullptr, *M1 = nullptr, *wtmp = nullptr;
     double *cvc = nullptr;                                   // per-cone A(UV^T), K*m
+    double *lpw = nullptr;                                   // the LP sweep's scratch (lp_sweep_scratch)
     double *part = nullptr;    // [kMaxPartialVals][kMaxPartialBlocks] partial sums (scratch A)
     double *partB = nullptr;   // second partial buffer (scratch B)
     double *partC = nullptr;   // third partial buffer (scratch C)
@@ -388,6 +395,9 @@ bool small_cg_batch_fits(const DevProblem &P);
 // {sum (b - A(X))^2, <C, R R^T>, b^T lambda} into out[4k..]) in one launch, a block a cone
 bool small_eval_fits(const DevProblem &P);
 int launch_small_eval(const DevProblem &P, DevWork &W, const double *U, const double *V, double *out, hipStream_t st);
+// the LP block's ADMM update: the reference's closed-form column sweep (k_lp_admm), both sides
+int launch_lp_admm(const DevProblem &P, DevWork &W, double rho, hipStream_t st);
+long lp_sweep_scratch(const DevProblem &P);
 int launch_small_cg_batch(const DevProblem &P, DevWork &W, int side, double rho, double tol, int maxit,
                           hipStream_t st);
 

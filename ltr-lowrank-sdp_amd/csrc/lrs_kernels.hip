@@ -6536,6 +6536,7 @@ static bool small_alm_args(const DevProblem &P, DevWork &W, SmallArgs &A, int *l
     return true;
 }
 bool small_alm_fits(const DevProblem &P, DevWork &W) {
+    if (P.lp_cone >= 0) return false;   // an LP block: the multi-launch iteration (its own ADMM sweep)
     SmallArgs A{};
     return small_alm_args(P, W, A, nullptr);
 }
@@ -7358,7 +7359,7 @@ int launch_small_cg(const DevProblem &P, DevWork &W, int cone, int side, double 
 // Every cone's half-step on one side in one launch (a block a cone): the cones each fit the
 // single-workgroup kernel with the same variant, no constraint spans two cones (DevProblem::cone_sep).
 bool small_cg_batch_fits(const DevProblem &P) {
-    if (P.K < 2 || P.K > kSmallMaxWg || !P.cone_sep) return false;
+    if (P.K < 2 || P.K > kSmallMaxWg || !P.cone_sep || P.lp_cone >= 0) return false;
     const int v = small_cg_fits(P, 0) ? small_cg_variant(P.cones[0]) : 0;
     if (!v) return false;
     for (int k = 1; k < P.K; ++k)
@@ -7470,7 +7471,7 @@ __global__ void __launch_bounds__(kSeT) k_small_eval(SmallEvalArgs A) {
 }
 static size_t small_eval_lds(const DevCone &c) { return ((size_t)c.n * c.r + c.cg_ncs + c.r) * sizeof(double); }
 bool small_eval_fits(const DevProblem &P) {
-    if (P.shard || P.K > kSmallMaxWg || (P.K > 1 && !P.cone_sep)) return false;
+    if (P.shard || P.K > kSmallMaxWg || (P.K > 1 && !P.cone_sep) || P.lp_cone >= 0) return false;
     long ncl = 0;
     for (int k = 0; k < P.K; ++k) {
         const DevCone &c = P.cones[k];
@@ -7496,6 +7497,172 @@ int launch_small_eval(const DevProblem &P, DevWork &W, const double *U, const do
     A.m = P.m; A.U = U; A.V = V; A.b = P.b; A.lam = W.lam; A.Craw = P.Craw;
     A.R = W.R; A.cvs = W.cvs; A.cvc = W.cvc; A.out = out;
     hipLaunchKernelGGL(k_small_eval, dim3(P.K), dim3(kSeT), lds, st, A);
+    LRS_CHECK_LAUNCH();
+    return 0;
+}
+
+
+// ---- the LP block's ADMM update (LORADSUpdateSDPLPVar's LP loop, lorads_alg_common.c:352-372):
+// for every LP column j in column order, LORADSUpdateLPVarOne (lorads_admm.c:759-792) for u_j with
+// v_j fixed, the constraint sums refreshed, then the same for v_j with u_j fixed.  The update is
+// closed form (a 1 x 1 system), but each column reads the constraint sums its predecessors left
+// (Gauss-Seidel), so the sweep is one thread's ordered loop: the block stages the operands the
+// chain touches -- the constraint sums, lambda and b, the columns' (u, v, c, ||a||^2) and their
+// entries -- in LDS with coalesced loads, one thread walks the columns from LDS, and the block
+// writes u, v and the sums back.  Arithmetic in the reference's operation order:
+//   M1_i = ((-b_i + cvs_i) + (-1) (u v) a_ij) rho + (-1) lambda_i   (scal/axpy sequence :764-779)
+//   w = c_j + sum_i a_ij M1_i (entry order, lp_cone_ObjCoeffSum + LPdataMatSparseWeightSum)
+//   x = (-1 (w y - rho y)) / rho / (1 + ||a_j||^2 y y)
+//   cvs_i += (-1) (u v)_old a_ij; cvs_i += (u v)_new a_ij   (constrValLP add / recompute / add)
+// The LP cone's own total A_lp(U V^T) (cvc[lp]) takes the same two adds.
+constexpr int kLpT = 256;
+constexpr size_t kLpMaxDynLds = 152 * 1024;
+struct LpSweepArgs {
+    int m, n, ld, slot_off, P;
+    long foff, e0, ne;          // the cone's entries: slot CSR range [e0, e0 + ne)
+    const int *lp_slot, *slot_ptr, *slot_con;
+    const double *slot_a, *lp_nrm2, *Craw, *b, *lam;
+    double *U, *V, *cvs, *cvc;
+    double rho;
+};
+__device__ inline void lp_sweep_serial(int m, int n, double rho, const int *__restrict__ lslot,
+                                       const int *__restrict__ ebeg, const int *__restrict__ econ,
+                                       const double *__restrict__ ea, const double *__restrict__ cj,
+                                       const double *__restrict__ nr, const double *__restrict__ b,
+                                       const double *__restrict__ lam, double *u, double *v, double *cvs,
+                                       double *cvc) {
+    for (int j = 0; j < n; ++j) {
+        const int t = lslot[j];
+        const int a0 = t >= 0 ? ebeg[t] : 0, a1 = t >= 0 ? ebeg[t + 1] : 0;
+        const double c = t >= 0 ? cj[t] : 0.0, n2 = nr[j];
+        for (int side = 0; side < 2; ++side) {
+            const double uv = u[j] * v[j];
+            double w = 0.0;
+            w += c;
+            for (int e = a0; e < a1; ++e) {
+                const int i = econ[e];
+                const double a = ea[e];
+                double m1 = -b[i];
+                m1 = m1 + cvs[i];
+                m1 = m1 + (-1.0) * (uv * a);
+                m1 = m1 * rho;
+                m1 = m1 + (-1.0) * lam[i];
+                w += a * m1;
+            }
+            const double y = side == 0 ? v[j] : u[j];
+            double M2 = w * y;
+            M2 = M2 - rho * y;
+            const double blin = -1.0 * M2 / rho;
+            const double x = blin / (1 + n2 * y * y);
+            if (side == 0) u[j] = x;
+            else v[j] = x;
+            const double uvn = u[j] * v[j];
+            for (int e = a0; e < a1; ++e) {
+                const int i = econ[e];
+                const double a = ea[e];
+                cvs[i] += (-1.0) * (uv * a);
+                cvc[i] += (-1.0) * (uv * a);
+            }
+            for (int e = a0; e < a1; ++e) {
+                const int i = econ[e];
+                const double a = ea[e];
+                cvs[i] += 1.0 * (uvn * a);
+                cvc[i] += 1.0 * (uvn * a);
+            }
+        }
+    }
+}
+// STAGED: operands in LDS (lp_sweep_lds bytes fit kLpMaxDynLds); else straight from global
+// memory with a scratch copy of the (u, v) columns and per-slot entry starts in W.lpw.
+template <bool STAGED>
+__global__ void __launch_bounds__(kLpT) k_lp_admm(LpSweepArgs A, double *__restrict__ scratch) {
+    extern __shared__ __align__(16) double lds_lp[];
+    const int m = A.m, n = A.n, P = A.P;
+    double *cvs, *cvc, *lam, *b, *u, *v, *cj, *nr, *ea;
+    int *econ, *ebeg, *lslot;
+    if (STAGED) {
+        cvs = lds_lp; cvc = cvs + m; lam = cvc + m; b = lam + m; u = b + m; v = u + n; cj = v + n; nr = cj + P;
+        ea = nr + n;
+        econ = reinterpret_cast<int *>(ea + A.ne);
+        ebeg = econ + A.ne;
+        lslot = ebeg + (P + 1);
+        for (int i = threadIdx.x; i < m; i += kLpT) { cvs[i] = A.cvs[i]; cvc[i] = A.cvc[i]; lam[i] = A.lam[i]; b[i] = A.b[i]; }
+        for (long e = threadIdx.x; e < A.ne; e += kLpT) { econ[e] = A.slot_con[A.e0 + e]; ea[e] = A.slot_a[A.e0 + e]; }
+        for (int t = threadIdx.x; t < P; t += kLpT) cj[t] = A.Craw[A.slot_off + t];
+        for (int t = threadIdx.x; t <= P; t += kLpT) ebeg[t] = A.slot_ptr[A.slot_off + t] - (int)A.e0;
+        for (int j = threadIdx.x; j < n; j += kLpT) {
+            lslot[j] = A.lp_slot[j];
+            nr[j] = A.lp_nrm2[j];
+            u[j] = A.U[A.foff + (long)j * A.ld];
+            v[j] = A.V[A.foff + (long)j * A.ld];
+        }
+    } else {
+        cvs = A.cvs; cvc = A.cvc; lam = const_cast<double *>(A.lam); b = const_cast<double *>(A.b);
+        u = scratch; v = scratch + n; cj = const_cast<double *>(A.Craw) + A.slot_off;
+        nr = const_cast<double *>(A.lp_nrm2); ea = const_cast<double *>(A.slot_a) + A.e0;
+        econ = const_cast<int *>(A.slot_con) + A.e0;
+        ebeg = reinterpret_cast<int *>(scratch + 2L * n);
+        lslot = const_cast<int *>(A.lp_slot);
+        for (int t = threadIdx.x; t <= P; t += kLpT) ebeg[t] = A.slot_ptr[A.slot_off + t] - (int)A.e0;
+        for (int j = threadIdx.x; j < n; j += kLpT) {
+            u[j] = A.U[A.foff + (long)j * A.ld];
+            v[j] = A.V[A.foff + (long)j * A.ld];
+        }
+        __threadfence_block();
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) lp_sweep_serial(m, n, A.rho, lslot, ebeg, econ, ea, cj, nr, b, lam, u, v, cvs, cvc);
+    __syncthreads();
+    if (!STAGED) __threadfence_block();
+    for (int j = threadIdx.x; j < n; j += kLpT) {
+        A.U[A.foff + (long)j * A.ld] = u[j];
+        A.V[A.foff + (long)j * A.ld] = v[j];
+    }
+    if (STAGED)
+        for (int i = threadIdx.x; i < m; i += kLpT) { A.cvs[i] = cvs[i]; A.cvc[i] = cvc[i]; }
+}
+static size_t lp_sweep_lds(int m, int n, int P, long ne) {
+    return sizeof(double) * (4L * m + 3L * n + P + ne) + sizeof(int) * (ne + P + 1 + n);
+}
+long lp_sweep_scratch(const DevProblem &P) {   // doubles of W.lpw the unstaged sweep needs
+    if (P.lp_cone < 0) return 0;
+    const DevCone &c = P.cones[P.lp_cone];
+    return 2L * c.n + (c.P + 2) / 2 + 1;
+}
+int launch_lp_admm(const DevProblem &P, DevWork &W, double rho, hipStream_t st) {
+    if (P.lp_cone < 0) return 0;
+    const DevCone &c = P.cones[P.lp_cone];
+    LpSweepArgs A{};
+    A.m = P.m; A.n = c.n; A.ld = c.ld; A.slot_off = c.slot_off; A.P = c.P; A.foff = c.foff;
+    std::vector<int> sp(2);
+    if (hipMemcpy(sp.data(), P.slot_ptr + c.slot_off, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(sp.data() + 1, P.slot_ptr + c.slot_off + c.P, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "launch_lp_admm: slot range read failed");
+        return -1;
+    }
+    A.e0 = sp[0]; A.ne = sp[1] - sp[0];
+    A.lp_slot = c.lp_slot; A.slot_ptr = P.slot_ptr; A.slot_con = P.slot_con; A.slot_a = P.slot_a;
+    A.lp_nrm2 = c.lp_nrm2; A.Craw = P.Craw; A.b = P.b; A.lam = W.lam;
+    A.U = W.U; A.V = W.V; A.cvs = W.cvs; A.cvc = W.cvc + (long)P.lp_cone * P.m; A.rho = rho;
+    const size_t lds = lp_sweep_lds(P.m, c.n, c.P, A.ne);
+    if (lds <= kLpMaxDynLds) {
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_lp_admm<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLpMaxDynLds) != hipSuccess) {
+                snprintf(g_err, sizeof(g_err), "launch_lp_admm: LDS attribute");
+                return -1;
+            }
+            attr = true;
+        }
+        hipLaunchKernelGGL(k_lp_admm<true>, dim3(1), dim3(kLpT), lds, st, A, W.lpw);
+    } else {
+        if (!W.lpw) {
+            snprintf(g_err, sizeof(g_err), "launch_lp_admm: no scratch for the unstaged sweep");
+            return -1;
+        }
+        hipLaunchKernelGGL(k_lp_admm<false>, dim3(1), dim3(kLpT), 0, st, A, W.lpw);
+    }
     LRS_CHECK_LAUNCH();
     return 0;
 }

@@ -105,7 +105,15 @@ bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err) {
         }
         ib -= 1; ii -= 1; ij -= 1;
         if (std::fabs(v) < 1e-12) continue;                 // :288-294
-        if (ib == K && nLp > 0) { lpEntries = true; continue; }
+        if (ib == K && nLp > 0) {
+            // LP block (io/lorads_file_io.c:297-309): column i of the diagonal block, j unused,
+            // C = -F0 as for the SDP blocks
+            if (ic < 0 || ic > m || ii < 0 || ii >= nLp) { err = "LP entry out of range"; return false; }
+            if (ic == 0) v = -v;
+            raw.push_back({K, ic, ii, ii, v});
+            lpEntries = true;
+            continue;
+        }
         if (ib < 0 || ib >= K || ic < 0 || ic > m) { err = "entry out of range"; return false; }
         if (ii > ij) std::swap(ii, ij);                     // :311-315
         if (ii < 0 || ij >= dims[ib]) { err = "entry index out of block"; return false; }
@@ -119,10 +127,21 @@ bool read_sdpa(const std::string &path, HostProblem &hp, std::string &err) {
 // pattern; shard_problem installs a dense cone's owned row block itself.
 static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, bool lpEntries,
                           std::vector<RawEntry> &raw, HostProblem &hp, std::string &err, bool allow_dense) {
-    if (nLp > 0 || lpEntries) {
-        err = "LP blocks are not supported by the device path yet (SURVEY.md §2, out of scope)";
-        return false;
-    }
+    (void)lpEntries;
+    // An LP block of nLp columns (x_j = r_j^2, data/lorads_lp_conic.c) is the diagonal SDP cone
+    // of nLp rows at rank 1: X = r r^T has X_jj = r_j^2, and the LP data (objective c_j,
+    // constraint coefficients a_ij) touch only the diagonal, so A(X), <C, X>, the gradient
+    // 2 (c_j + sum_i M1_i a_ij) r_j (ALMSetGradLP, lorads_alm.c:99-121), q1 / q2 / p1 / p2
+    // (ALMCalq12p12LP, :748-765) and the L-BFGS streams are the SDP cone's formulas on that
+    // cone.  It is appended after the SDP cones (cone K), where the reference draws its random
+    // start (lpRandom after the SDP cones' R, data/lorads_solver.c:668-676).  What differs is
+    // host policy (rank fixed at 1, no AUG_RANK, no oracle rank, rho0 and curr_rank over the SDP
+    // cones only, ||C||_2^2 taken as ||c||_1^2 like lp_cone_obj_nrm2Square) and the ADMM update,
+    // which is the reference's closed-form column sweep (LORADSUpdateLPVarOne, lorads_admm.c:759-
+    // 792) instead of a CG (lrs_kernels.hip k_lp_admm).
+    std::vector<int> dimsx(dims.begin(), dims.begin() + K);
+    if (nLp > 0) { dimsx.push_back(nLp); K += 1; }
+    const std::vector<int> &dims_all = dimsx;
     hp.m = m; hp.K = K; hp.nLp = nLp;
     hp.nEntries = (long)raw.size();
     hp.cones.assign(K, HostCone());
@@ -141,7 +160,7 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
         const char *ek = getenv("LRS_CONST_C");
         const char *ev = getenv("LRS_DENSE_C");
         const char *es = getenv("LRS_SMALL");
-        if (allow_dense && !ek && !(ev && ev[0] == '0') && !(es && atoi(es) == 0)) {
+        if (allow_dense && nLp == 0 && !ek && !(ev && ev[0] == '0') && !(es && atoi(es) == 0)) {
             bool ok = true, any = false;
             long N = 0, Ptot = 0;
             int ldmax = 0, ldmin = 1 << 30, nconst = 0;
@@ -168,7 +187,7 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
             for (int k = 0; k < K && ok; ++k) {
                 size_t e1 = e0;
                 while (e1 < raw.size() && raw[e1].cone == k) e1++;
-                const int n = dims[k];
+                const int n = dims_all[k];
                 cone_n[k] = n;
                 N += n;
                 if (N > 4096) { ok = false; break; }
@@ -234,7 +253,8 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
     size_t q = 0;
     for (int k = 0; k < K; ++k) {
         HostCone &c = hp.cones[k];
-        c.n = dims[k];
+        c.n = dims_all[k];
+        c.lp = nLp > 0 && k == K - 1;
         size_t b0 = q;
         while (q < raw.size() && raw[q].cone == k) q++;
         // merged entries of this cone
@@ -246,6 +266,25 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
             else
                 me.push_back(raw[e]);
         }
+        if (c.lp) {
+            // the LP block's columns as lp_cone_presolve types them (lorads_lp_conic.c:110-125):
+            // a column in >= 1/4 of the constraints is LP_COEFF_DENSE, whose create routine never
+            // sets its row count (LPdataMatCreateDenseImpl, lorads_lp_data.c:178-193: calloc'ed
+            // nRows = 0), so the reference's A(x), A^*(y) and constraint values see none of its
+            // coefficients; only ||a_j||^2 (taken from the raw entries, :132-133) reaches the ADMM
+            // update's denominator.  Reproduced: those entries leave the cone, their norm stays.
+            std::vector<int> cnt(c.n, 0);
+            c.lp_nrm2.assign(c.n, 0.0);
+            for (auto &e : me)
+                if (e.con != 0) { cnt[e.row]++; c.lp_nrm2[e.row] += e.v * e.v; }
+            for (auto &v : c.lp_nrm2) { const double t = std::sqrt(v); v = t * t; }   // nrm2, then squared
+            std::vector<RawEntry> keep;
+            keep.reserve(me.size());
+            for (auto &e : me)
+                if (e.con == 0 || !(cnt[e.row] != 0 && (double)cnt[e.row] / (double)m >= 0.25)) keep.push_back(e);
+                else c.lp_dense_dropped++;
+            me.swap(keep);
+        }
         // dense objective: C out of the pattern, into a full matrix (lrs_problem.h policy)
         long ncobj = 0;
         for (auto &e : me) ncobj += e.con == 0 ? 1 : 0;
@@ -255,10 +294,10 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
             if (ev && ev[0] == '0') c.dense_c = false;
             else if (ev && ev[0] == '1') c.dense_c = ncobj > 0;
             else c.dense_c = c.n >= kDenseCMinN && 4 * ncobj >= tri;
-            if (!allow_dense) c.dense_c = false;
+            if (!allow_dense || c.lp) c.dense_c = false;
             // constant C (all entries one value): the rank-one products, no n x n matrix
             const char *ek = getenv("LRS_CONST_C");
-            if (allow_dense && ((ek && ek[0] == '1') || auto_const) && !(ev && ev[0] == '0') && c.n >= kConstCMinN &&
+            if (allow_dense && !c.lp && ((ek && ek[0] == '1') || auto_const) && !(ev && ev[0] == '0') && c.n >= kConstCMinN &&
                 ncobj == tri) {
                 double v0 = 0.0;
                 bool same = true, first = true;
@@ -324,6 +363,10 @@ static bool build_problem(int m, int K, const std::vector<int> &dims, int nLp, b
         }
         if (lastCon > 0 && cnt > fill) c.denseCoeff = true;
         if ((double)cn > fill) c.denseCoeff = true;
+        if (c.lp) {
+            c.denseCoeff = false;
+            c.cNrm2sq = c.cNrm1 * c.cNrm1;   // lp_cone_obj_nrm2Square (lorads_lp_conic.c:171-176): nrm1^2
+        }
         // symmetric adjacency, columns ascending per row; lower prefix = col <= row
         std::vector<int> deg(c.n, 0);
         for (int t = 0; t < P; ++t) {
@@ -393,7 +436,13 @@ bool build_problem_coo(int m, int nblk, const int *dims_in, const double *b, lon
         int ic = con[t], ib = blk[t] - 1, ii = row[t] - 1, ij = col[t] - 1;
         double v = val[t];
         if (std::fabs(v) < 1e-12) continue;
-        if (ib == K && nLp > 0) { lpEntries = true; continue; }
+        if (ib == K && nLp > 0) {   // LP block: column i (read_sdpa)
+            if (ic < 0 || ic > m || ii < 0 || ii >= nLp) { err = "LP entry out of range"; return false; }
+            if (ic == 0) v = -v;
+            raw.push_back({K, ic, ii, ii, v});
+            lpEntries = true;
+            continue;
+        }
         if (ib < 0 || ib >= K || ic < 0 || ic > m) { err = "entry out of range"; return false; }
         if (ii > ij) std::swap(ii, ij);
         if (ii < 0 || ij >= dims[ib]) { err = "entry index out of block"; return false; }
@@ -407,6 +456,12 @@ bool shard_problem(const HostProblem &g, int world, int rank, HostProblem &out, 
     const int K = g.K;
     if (world < 1 || world > kMaxShards || rank < 0 || rank >= world) {
         err = "sharded solve: bad world/rank";
+        return false;
+    }
+    if (g.nLp > 0) {
+        // the LP block's ADMM update is the reference's sequential column sweep (each column
+        // sees the constraint sums its predecessors left): one workgroup walks it, unsharded
+        err = "sharded solve: an LP block is not supported (its ADMM update is a sequential column sweep)";
         return false;
     }
     for (int k = 0; k < K; ++k)
@@ -752,6 +807,7 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
     if (hp.K > kMaxCones) { err = "at most " + std::to_string(kMaxCones) + " SDP cones are supported"; return false; }
     dp.m = hp.m;
     dp.K = hp.K;
+    dp.lp_cone = -1;
     dp.cones.assign(hp.K, DevCone());
     dp.ndense = 0;
     dp.dense_scale = 1.0;
@@ -1210,6 +1266,15 @@ bool upload_problem(const HostProblem &hp, DevProblem &dp, std::string &err) {
                 }
             }
         }
+        d.lp = c.lp;
+        if (c.lp) {
+            dp.lp_cone = k;
+            std::vector<int> ls(std::max(1, c.n), -1);
+            for (int t = 0; t < (int)c.prow.size(); ++t) ls[c.prow[t]] = t;
+            std::vector<double> nr(c.lp_nrm2);
+            if (nr.empty()) nr.push_back(0.0);
+            if (!dput(&d.lp_slot, ls, err) || !dput(&d.lp_nrm2, nr, err)) return false;
+        }
         if (c.dense_c) {
             if (c.const_c) {
                 d.dense_c = 2;
@@ -1233,7 +1298,7 @@ void free_problem(DevProblem &dp) {
     for (auto &c : dp.cones) { f(c.adj_ptr); f(c.adj_low); f(c.adj_col); f(c.adj_slot); f(c.dra); f(c.drb); f(c.Cd); f(c.colseg); f(c.auv_item); f(c.auv_pq); f(c.auv_pos); f(c.auv_val); f(c.sa_item); f(c.sa_sub); f(c.sa_grp); f(c.sa_pq); f(c.sa_slot);
         f(c.sb_blk); f(c.sb_tp); f(c.sb_rp); f(c.sb_ent); f(c.sa_S); f(c.sx_slot);
         f(c.cg_cadj_ptr); f(c.cg_cadj); f(c.cg_cl_con); f(c.cg_cl_ptr); f(c.cg_ce); f(c.cg_sp); f(c.cg_sj);
-        f(c.cg_cc_ptr); f(c.cg_cc); f(c.cg_ce_w); f(c.cg_sa); f(c.cobj_slot); }
+        f(c.cg_cc_ptr); f(c.cg_cc); f(c.cg_ce_w); f(c.cg_sa); f(c.cobj_slot); f(c.lp_slot); f(c.lp_nrm2); }
     if (dp.has_merged) {
         f(dp.merged.adj_ptr); f(dp.merged.adj_low); f(dp.merged.adj_col); f(dp.merged.adj_slot);
         f(dp.merged.dra); f(dp.merged.drb);

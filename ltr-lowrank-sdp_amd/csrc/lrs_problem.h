@@ -37,6 +37,11 @@ struct HostCone {
     // sharded solve: this shard's owned local rows [own0, own1) (own1 < 0: every row, unsharded).
     // The 2-D tiles of the stage kernels then cover the owned rows only.
     int own0 = 0, own1 = -1;
+    // the LP block (last block of negative size in SDPA) as the diagonal cone at rank 1
+    // (build_problem): its columns are the rows, every slot (j, j)
+    bool lp = false;
+    std::vector<double> lp_nrm2;   // LP block: per column ||a_j||_2^2 of its raw entries
+    long lp_dense_dropped = 0;     // LP block: constraint entries of LP_COEFF_DENSE columns (dropped)
 };
 // Dense-objective policy: LRS_DENSE_C=0 never, =1 every cone with objective entries, unset:
 // cones with n >= kDenseCMinN whose C fills >= 1/4 of the lower triangle (measured: the dense
@@ -60,7 +65,7 @@ constexpr int kSmallAutoMaxConst = 4;          // = lrs_kernels.hip kSmallMaxCon
 constexpr int kSmallAutoMaxCones = 8;          // = lrs_kernels.hip kSmallMaxWg (one workgroup per cone)
 
 struct HostProblem {
-    int m = 0, K = 0, nLp = 0;
+    int m = 0, K = 0, nLp = 0;   // K counts the LP cone (the last one) when nLp > 0
     std::vector<double> b;
     std::vector<HostCone> cones;
     long nEntries = 0;

@@ -224,7 +224,24 @@ struct lrs_ctx {
 // sharded solve: transports.  Every collective is called by all shards in the same
 // order (the host control flow is identical on every shard: it only sees summed values).
 // ------------------------------------------------------------------------
+// One point-to-point or collective operation of a shard, as the transport issues it: the halo
+// exchanges' per-(peer, cone) send / receive in the order of halo_ops (the RCCL transport's group
+// body), the all-reduces with their lengths.  Recorded when the context's record flag is on
+// (lrs_shard_comm_record), so a test can check on the loopback transport that every send pairs
+// with the peer's receive of the same length in the same order, and that every shard issues the
+// same collectives -- the sequence the RCCL transport drives from the same op list.
+enum CommOpKind { COP_GROUP = 0, COP_SEND = 1, COP_RECV = 2, COP_ALLREDUCE_DEV = 3, COP_ALLREDUCE_HOST = 4 };
+struct CommOp {
+    int kind, peer, cone;
+    long count;      // doubles
+    long offset;     // send: offset in the packed send buffer; recv: local row of the landing rows x ld
+};
 struct ShardComm {
+    bool recording = false;
+    std::vector<CommOp> log;
+    void rec(int kind, int peer, int cone, long count, long offset = 0) {
+        if (recording) log.push_back(CommOp{kind, peer, cone, count, offset});
+    }
     virtual ~ShardComm() {}
     // in-place sum over shards of n device doubles, ordered on stream st
     virtual int allreduce_dev(lrs_ctx *c, double *buf, int n, hipStream_t st) = 0;
@@ -238,6 +255,9 @@ struct ShardComm {
     virtual int ranks(int *n) = 0;
 };
 static bool sharded(const lrs_ctx *c) { return c->comm != nullptr; }
+// the LP block's cone (lrs_problem.cpp build_problem: the diagonal cone at rank 1, appended last)
+static bool is_lp(const lrs_ctx *c, int k) { return k == c->dp.lp_cone; }
+static int n_sdp(const lrs_ctx *c) { return c->dp.K - (c->dp.lp_cone >= 0 ? 1 : 0); }
 static int cone_n_global(const lrs_ctx *c, int k) {
     return sharded(c) ? c->plan.cones[k].n_global : c->hp.cones[k].n;
 }
@@ -278,6 +298,25 @@ static int pack_send_vec(lrs_ctx *c, int k, const double *x, hipStream_t st) {
     return 0;
 }
 
+// The halo exchange's operations in issue order, shared by both transports: per peer, per cone
+// (cone order on both sides), this shard's send rows to the peer, then the peer's rows into the
+// halo.  `vec_cone` >= 0: one vector of that cone's rows (ld 1) instead of every cone's factor rows.
+static void halo_ops(const lrs_ctx *c, int vec_cone, std::vector<CommOp> &ops) {
+    const ShardPlan &pl = c->plan;
+    ops.clear();
+    for (int q = 0; q < pl.world; ++q)
+        for (int k = 0; k < c->dp.K; ++k) {
+            if (vec_cone >= 0 && k != vec_cone) continue;
+            const ShardConePlan &cp = pl.cones[k];
+            const int ld = vec_cone >= 0 ? 1 : c->dp.cones[k].ld;
+            const long base = vec_cone >= 0 ? 0 : send_base(pl, c->dp, k);
+            const int ns = cp.send_ptr[q + 1] - cp.send_ptr[q];
+            if (ns > 0) ops.push_back(CommOp{COP_SEND, q, k, (long)ns * ld, base + (long)cp.send_ptr[q] * ld});
+            if (cp.recv_cnt[q] > 0)
+                ops.push_back(CommOp{COP_RECV, q, k, (long)cp.recv_cnt[q] * ld, (long)cp.recv_start[q] * ld});
+        }
+}
+
 #define LRS_STR_(x) #x
 #define LRS_STR(x) LRS_STR_(x)
 #define NCCLC(x)                                                                            \
@@ -311,6 +350,7 @@ struct RcclComm : ShardComm {
         if (dscr) (void)hipFree(dscr);
     }
     int allreduce_dev(lrs_ctx *, double *buf, int n, hipStream_t st) override {
+        rec(COP_ALLREDUCE_DEV, -1, -1, n);
         NCCLC(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, comm, st));
         return 0;
     }
@@ -321,43 +361,37 @@ struct RcclComm : ShardComm {
             dscr_len = n;
         }
         HIPC(hipMemcpyAsync(dscr, v, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+        rec(COP_ALLREDUCE_HOST, -1, -1, n);
         NCCLC(ncclAllReduce(dscr, dscr, n, ncclDouble, ncclSum, comm, c->st));
         HIPC(hipMemcpyAsync(v, dscr, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
         HIPC(hipStreamSynchronize(c->st));
         return 0;
     }
-    int halo(lrs_ctx *c, double *D, hipStream_t st) override {
-        const ShardPlan &pl = c->plan;
-        if (pack_send_rows(c, D, st)) return -1;
-        // per peer, one send and one receive per cone, in cone order on both sides
+    // one group per exchange, its body the shared op list (halo_ops): each send from the packed
+    // send buffer, each receive in place into the peer's halo rows (contiguous locally)
+    int group(lrs_ctx *c, int vec_cone, const double *sendbuf, double *base, hipStream_t st) {
+        halo_ops(c, vec_cone, ops);
+        rec(COP_GROUP, -1, vec_cone, (long)ops.size());
         NCCLC(ncclGroupStart());
-        for (int q = 0; q < pl.world; ++q)
-            for (int k = 0; k < c->dp.K; ++k) {
-                const ShardConePlan &cp = pl.cones[k];
-                const DevCone &dc = c->dp.cones[k];
-                const int ld = dc.ld;
-                const int ns = cp.send_ptr[q + 1] - cp.send_ptr[q];
-                if (ns > 0)
-                    NCCLG(ncclSend(c->d_sendbuf + send_base(pl, c->dp, k) + (long)cp.send_ptr[q] * ld, (size_t)ns * ld,
-                                   ncclDouble, q, comm, st));
-                if (cp.recv_cnt[q] > 0)
-                    NCCLG(ncclRecv(D + dc.foff + (long)cp.recv_start[q] * ld, (size_t)cp.recv_cnt[q] * ld, ncclDouble, q,
-                                   comm, st));
-            }
-        NCCLC(ncclGroupEnd());
-        return 0;
-    }
-    int halo_vec(lrs_ctx *c, int k, double *x, hipStream_t st) override {
-        const ShardConePlan &cp = c->plan.cones[k];
-        if (pack_send_vec(c, k, x, st)) return -1;
-        NCCLC(ncclGroupStart());
-        for (int q = 0; q < c->plan.world; ++q) {
-            const int ns = cp.send_ptr[q + 1] - cp.send_ptr[q];
-            if (ns > 0) NCCLG(ncclSend(c->d_sendvec + cp.send_ptr[q], (size_t)ns, ncclDouble, q, comm, st));
-            if (cp.recv_cnt[q] > 0) NCCLG(ncclRecv(x + cp.recv_start[q], (size_t)cp.recv_cnt[q], ncclDouble, q, comm, st));
+        for (const CommOp &o : ops) {
+            rec(o.kind, o.peer, o.cone, o.count, o.offset);
+            if (o.kind == COP_SEND)
+                NCCLG(ncclSend(sendbuf + o.offset, (size_t)o.count, ncclDouble, o.peer, comm, st));
+            else
+                NCCLG(ncclRecv(base + (vec_cone >= 0 ? 0 : c->dp.cones[o.cone].foff) + o.offset, (size_t)o.count,
+                               ncclDouble, o.peer, comm, st));
         }
         NCCLC(ncclGroupEnd());
         return 0;
+    }
+    std::vector<CommOp> ops;
+    int halo(lrs_ctx *c, double *D, hipStream_t st) override {
+        if (pack_send_rows(c, D, st)) return -1;
+        return group(c, -1, c->d_sendbuf, D, st);
+    }
+    int halo_vec(lrs_ctx *c, int k, double *x, hipStream_t st) override {
+        if (pack_send_vec(c, k, x, st)) return -1;
+        return group(c, k, c->d_sendvec, x, st);
     }
     int ranks(int *n) override {
         NCCLC(ncclCommCount(comm, n));
@@ -413,6 +447,7 @@ struct LoopComm : ShardComm {
             dsum_len = n;
         }
         g->bufs[rank] = buf;
+        rec(COP_ALLREDUCE_DEV, -1, -1, n);
         if (pre(st)) return -1;
         OPC(launch_sum_shards(n, g->world, g->bufs.data(), dsum, st));
         if (post(st)) return -1;
@@ -420,6 +455,7 @@ struct LoopComm : ShardComm {
         return 0;
     }
     int allreduce_host(lrs_ctx *, double *v, int n) override {
+        rec(COP_ALLREDUCE_HOST, -1, -1, n);
         g->hv[rank].assign(v, v + n);
         g->barrier();
         for (int i = 0; i < n; ++i) {
@@ -430,8 +466,16 @@ struct LoopComm : ShardComm {
         g->barrier();
         return 0;
     }
+    std::vector<CommOp> ops;
+    void record_ops(lrs_ctx *c, int vec_cone) {   // what the RCCL transport's group would issue
+        if (!recording) return;
+        halo_ops(c, vec_cone, ops);
+        rec(COP_GROUP, -1, vec_cone, (long)ops.size());
+        for (const CommOp &o : ops) rec(o.kind, o.peer, o.cone, o.count, o.offset);
+    }
     int halo(lrs_ctx *c, double *D, hipStream_t st) override {
         if (pack_send_rows(c, D, st)) return -1;
+        record_ops(c, -1);
         g->sendbufs[rank] = c->d_sendbuf;
         if (pre(st)) return -1;
         for (int q = 0; q < g->world; ++q)
@@ -451,6 +495,7 @@ struct LoopComm : ShardComm {
     }
     int halo_vec(lrs_ctx *c, int k, double *x, hipStream_t st) override {
         if (pack_send_vec(c, k, x, st)) return -1;
+        record_ops(c, k);
         g->sendbufs[rank] = c->d_sendvec;
         if (pre(st)) return -1;
         const ShardConePlan &cp = c->plan.cones[k];
@@ -518,7 +563,7 @@ static void free_work(lrs_ctx *c) {
     double *ptrs[] = {W.R, W.D, W.G[0], W.G[1], W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.U, W.V, W.X, W.cg_r,
                       W.cg_p, W.cg_Q, W.cg_b, W.M2, W.uvt0, W.uvt1, W.uvt2, W.S, W.lam, W.cvs, W.q1, W.q2,
                       W.M1, W.wtmp, W.cvc, W.part, W.partB, W.partC, W.ctrl, W.lsres, W.par, W.gram, W.rec, W.R2,
-                      W.cgc, W.tot, W.gl, W.CR, W.CD, W.GP, W.CGK, W.uvp};
+                      W.cgc, W.tot, W.gl, W.CR, W.CD, W.GP, W.CGK, W.uvp, W.lpw};
     for (double *p : ptrs)
         if (p) (void)hipFree(p);
     for (double *q : c->ring_s) if (q) (void)hipFree(q);
@@ -600,6 +645,7 @@ static int alloc_work(lrs_ctx *c, const std::vector<int> &ranks) {
         W.gl_len = gl;
     }
     if (P.ndense && (A(&W.CR, NR) || A(&W.CD, NR))) return -1;
+    if (P.lp_cone >= 0 && A(&W.lpw, std::max(2L, lp_sweep_scratch(P)))) return -1;   // k_lp_admm, unstaged
     {   // k_cgemm2's split-K slabs for the large dense cones
         bool big = false;
         for (const DevCone &dc : P.cones) big = big || (dc.dense_c == 1 && dc.n >= 2048);
@@ -1088,6 +1134,24 @@ static int dual_infeasibility(lrs_ctx *c, double *l1, double *lmin, int *all_con
         double lk = 0.0;
         bool conv = true;
         int steps = 0, iters = 0;
+        if (is_lp(c, k)) {
+            // the LP block (calculate_dual_infeasibility_solver, data/lorads_solver.c:1405-1412):
+            // per column |min(c_j - sum_i lambda_i a_ij, 0)|, i.e. the negative part of every
+            // diagonal slot of S; a column without data contributes 0
+            const DevCone &d = c->dp.cones[k];
+            std::vector<double> s(std::max(1, d.P));
+            HIPC(hipMemcpyAsync(s.data(), W.S + d.slot_off, sizeof(double) * d.P, hipMemcpyDeviceToHost, c->st));
+            HIPC(hipStreamSynchronize(c->st));
+            double lpe = 0.0;
+            lk = d.P < d.n ? 0.0 : 1e300;
+            for (int t = 0; t < d.P; ++t) {
+                lpe += std::fabs(std::min(s[t], 0.0));
+                lk = std::min(lk, s[t]);
+            }
+            if (lmin) lmin[k] = lk;
+            err += lpe;
+            continue;
+        }
         if (trl_min(c, k, W.S, &lk, &steps, &iters, &conv)) return -1;
         c->dinf_steps += steps;
         c->dinf_iters += iters;
@@ -1210,6 +1274,7 @@ static int oracle_rank(lrs_ctx *c, int phase) {
     }
     size_t off = 0;
     for (int k = 0; k < K; ++k) {
+        if (is_lp(c, k)) continue;   // lorads_compute_oracle_rank runs over the SDP cones
         int nblk = 0;
         if (phase == 1) OPC(launch_gram(c->dp, k, c->W.R, nullptr, 0, c->W.gram, &nblk, c->st));
         else OPC(launch_gram(c->dp, k, c->W.U, c->W.V, 1, c->W.gram, &nblk, c->st));
@@ -1221,6 +1286,7 @@ static int oracle_rank(lrs_ctx *c, int phase) {
     int tot = 0;
     off = 0;
     for (int k = 0; k < K; ++k) {
+        if (is_lp(c, k)) continue;
         const size_t rr = (size_t)c->rank[k] * c->rank[k];
         std::vector<double> g(c->hgram + off, c->hgram + off + rr);
         if (sharded(c) && c->comm->allreduce_host(c, g.data(), (int)rr)) return -1;
@@ -1241,6 +1307,7 @@ static int oracle_rank_naive(lrs_ctx *c, const lrs_params *p, int phase) {
     if (sharded(c)) return oracle_rank(c, phase);
     int tot = 0;
     for (int k = 0; k < c->dp.K; ++k) {
+        if (is_lp(c, k)) continue;
         const DevCone &d = c->dp.cones[k];
         const int n = d.n, r = c->rank[k];
         if (n > kNaiveMaxN) {
@@ -1276,9 +1343,9 @@ static int oracle_rank_naive(lrs_ctx *c, const lrs_params *p, int phase) {
     return tot;
 }
 
-static int sum_rank(lrs_ctx *c) {
+static int sum_rank(lrs_ctx *c) {   // curr_rank: the SDP cones' (the reference's rankElem)
     int t = 0;
-    for (int r : c->rank) t += r;
+    for (int k = 0; k < (int)c->rank.size(); ++k) t += is_lp(c, k) ? 0 : c->rank[k];
     return t;
 }
 
@@ -1312,6 +1379,7 @@ static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &ra
     std::vector<int> dflt(K);
     for (int k = 0; k < K; ++k) {
         const HostCone &hc = c->hp.cones[k];
+        if (hc.lp) { rank[k] = rmax[k] = dflt[k] = 1; continue; }   // x_j = r_j^2: rank 1, no growth
         const int hn = cone_n_global(c, k);
         int nnzRows = hc.nnzRows;
         int calc = std::min((int)std::sqrt(2.0 * nnzRows) + 1, hn);
@@ -1326,7 +1394,7 @@ static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &ra
         int rk;
         if (p->initRank > 0) rk = std::min(p->initRank, hn);
         else if (p->timesLogRank <= 1e-6) rk = calc;
-        else if (nnzRows / hn >= 20 && hn <= 400 && K <= 3) rk = calc;
+        else if (nnzRows / hn >= 20 && hn <= 400 && K - (c->hp.nLp > 0 ? 1 : 0) <= 3) rk = calc;   // nCones: SDP blocks
         else rk = (int)std::min(std::ceil(p->timesLogRank * std::log((double)hn)), (double)calc);
         rank[k] = std::max(1, rk);
         dflt[k] = rank[k];
@@ -1336,6 +1404,7 @@ static void determine_rank(lrs_ctx *c, const lrs_params *p, std::vector<int> &ra
         // entry 0 is the initial TOTAL rank, split across cones in proportion to the default ranks
         int tot = std::max(1, p->rankSchedule[0]);
         for (int k = 0; k < K; ++k) {
+            if (c->hp.cones[k].lp) continue;
             int rk = (int)std::lround((double)tot * dflt[k] / std::max(1, tot_default));
             rank[k] = std::max(1, std::min(rk, cone_n_global(c, k)));
             rmax[k] = std::max(rmax[k], rank[k]);
@@ -1392,10 +1461,11 @@ static int init_point(lrs_ctx *c) {
 static int check_all_rank_max(lrs_ctx *c, double f) {
     int cnt = 0;
     for (int k = 0; k < c->dp.K; ++k) {
+        if (is_lp(c, k)) continue;   // CheckAllRankMax runs over the SDP cones
         int nr = (int)std::min(std::ceil(c->rank[k] * f), (double)c->rank_max[k]);
         if (nr >= c->rank_max[k]) cnt++;
     }
-    return cnt == c->dp.K;
+    return cnt == n_sdp(c);
 }
 
 static int regrow(lrs_ctx *c, const std::vector<int> &nr) {
@@ -1452,12 +1522,14 @@ static int aug_rank(lrs_ctx *c, double f, const lrs_params *p, int *sched_pos, i
         *sched_pos = pos;
         int tot = std::max(1, p->rankSchedule[pos]), cur = sum_rank(c);
         for (int k = 0; k < c->dp.K; ++k) {
+            if (is_lp(c, k)) { nr[k] = 1; continue; }
             int rk = (int)std::lround((double)tot * c->rank[k] / std::max(1, cur));
             nr[k] = clamp_rank(std::max(c->rank[k], std::min(rk, cone_n_global(c, k))), &c->rank_warned);
             c->rank_max[k] = std::max(c->rank_max[k], nr[k]);
         }
     } else {
-        for (int k = 0; k < c->dp.K; ++k) nr[k] = (int)std::min(std::ceil(c->rank[k] * f), (double)c->rank_max[k]);
+        for (int k = 0; k < c->dp.K; ++k)
+            nr[k] = is_lp(c, k) ? 1 : (int)std::min(std::ceil(c->rank[k] * f), (double)c->rank_max[k]);
     }
     if (regrow(c, nr)) return -1;
     if (sched) *is_max = (*sched_pos + 1 >= p->rankScheduleLen) ? 1 : 0;
@@ -2180,7 +2252,7 @@ static int admm_init_constr(lrs_ctx *c) {
 static bool use_small_cg(lrs_ctx *c, int k) {
     const char *e = getenv("LRS_SMALL_CG");
     const int env = e ? atoi(e) : -1;
-    return env != 0 && small_cg_fits(c->dp, k);
+    return env != 0 && !is_lp(c, k) && c->dp.lp_cone < 0 && small_cg_fits(c->dp, k);
 }
 static int admm_half_step(lrs_ctx *c, int k, int side, double rho, double tol, int maxit, bool *on_device) {
     if (use_small_cg(c, k)) {
@@ -2202,11 +2274,13 @@ static int admm_update_var(lrs_ctx *c, double rho, double tol, int maxit) {
     for (int side = 0; side < 2 && batch; ++side) OPC(launch_small_cg_batch(c->dp, c->W, side, rho, tol, maxit, c->st));
     dev = batch;
     for (int k = 0; k < c->dp.K && !batch; ++k)
-        for (int side = 0; side < 2; ++side) {
+        for (int side = 0; side < 2 && !is_lp(c, k); ++side) {
             bool d = false;
             if (admm_half_step(c, k, side, rho, tol, maxit, &d)) return -1;
             dev |= d;
         }
+    // the LP block after every SDP cone (LORADSUpdateSDPLPVar, lorads_alg_common.c:352-372)
+    if (c->dp.lp_cone >= 0) OPC(launch_lp_admm(c->dp, c->W, rho, c->st));
     // the device-counted CG iterations, read behind the next stream sync (admm_eval's)
     if (dev)
         HIPC(hipMemcpyAsync(c->hpin + kHpCgTotal, c->W.cgc + CG_TOTAL, sizeof(double), hipMemcpyDeviceToHost, c->st));
@@ -2257,7 +2331,7 @@ static void admm_log(lrs_ctx *c, const lrs_params *p, const AdmmState &st, doubl
     logf_(c, p, "ADMM Iter:%ld pObj:%5.5e dObj:%5.5e pInfea(1):%5.5e pInfea(Inf):%5.5e pdGap:%5.5e rho:%3.2f cgIter:%d "
            "CurrRank:%d OracleRank:%d Time:%3.2f\n",
            st.iter, st.pobj, st.dobj, st.pinf1, st.pinfinf, st.gap, st.rho,
-           (int)((double)st.cg_iter / (double)c->dp.K), c->t2c.empty() ? 0 : c->t2c.back(),
+           (int)((double)st.cg_iter / (double)std::max(1, n_sdp(c))), c->t2c.empty() ? 0 : c->t2c.back(),
            c->t2o.empty() ? 0 : c->t2o.back(), t);
 }
 
@@ -2792,6 +2866,10 @@ int lrs_set_rank(lrs_ctx *c, const int *ranks) {
     LRS_NEED_LOADED(c);
     LRS_NEED_ARG(ranks);
     std::vector<int> r(ranks, ranks + c->hp.K);
+    if (c->dp.lp_cone >= 0 && r[c->dp.lp_cone] != 1) {
+        set_err("lrs_set_rank: the LP cone (cone %d) has rank 1 (x_j = r_j^2), got %d", c->dp.lp_cone, r[c->dp.lp_cone]);
+        return -1;
+    }
     c->rank_max = r;
     return alloc_work(c, r);
 }
@@ -2934,6 +3012,15 @@ int lrs_op_admm_half(lrs_ctx *c, int cone, int side, double rho, double cg_tol, 
     // for V): solve the side with the other fixed, then the cone's constraint-value refresh
     c->cgIterCone[cone] = 0;
     bool dev = false;
+    if (is_lp(c, cone)) {
+        // the LP block: its update interleaves u_j and v_j column by column
+        // (LORADSUpdateSDPLPVar's LP loop), so side 0 runs the whole sweep and side 1 is refused
+        if (side != 0) { set_err("lrs_op_admm_half: the LP cone's sweep updates U and V together (side 0)"); return -1; }
+        OPC(launch_lp_admm(P, c->W, rho, c->st));
+        HIPC(hipStreamSynchronize(c->st));
+        if (cg_iters) *cg_iters = 0;
+        return 0;
+    }
     if (admm_half_step(c, cone, side, rho, cg_tol, cg_maxit, &dev)) return -1;
     HIPC(hipStreamSynchronize(c->st));
     if (cg_iters) {
@@ -3123,7 +3210,7 @@ static int solve_impl(lrs_ctx *c, const lrs_params *pin, lrs_result *res) {
     double rho = p->initRho;
     if (rho == 0) {   // initial_solver_state, data/lorads_solver.c:1599-1606
         long sd = 0;
-        for (int k = 0; k < c->hp.K; ++k) sd += cone_n_global(c, k);
+        for (int k = 0; k < c->hp.K; ++k) sd += is_lp(c, k) ? 0 : cone_n_global(c, k);   // SDP blocks only
         rho = 1 / std::sqrt((double)sd);
     }
     alm.rho = rho; admm.rho = rho;
@@ -3682,6 +3769,26 @@ int lrs_shard_info(lrs_ctx *c, int *world, int *rank, int *row0, int *nown, int 
     return 0;
 }
 
+int lrs_shard_comm_record(lrs_ctx *c, int on) {
+    LRS_NEED_CTX(c);
+    if (!c->comm) { set_err("lrs_shard_comm_record: the context is not sharded"); return -1; }
+    c->comm->recording = on != 0;
+    c->comm->log.clear();
+    return 0;
+}
+int lrs_shard_comm_log(lrs_ctx *c, long *out, long cap, long *n) {
+    LRS_NEED_CTX(c);
+    LRS_NEED_ARG(n);
+    if (!c->comm) { set_err("lrs_shard_comm_log: the context is not sharded"); return -1; }
+    const std::vector<CommOp> &L = c->comm->log;
+    *n = (long)L.size();
+    if (out)
+        for (long i = 0; i < std::min(cap, (long)L.size()); ++i) {
+            out[5 * i] = L[i].kind; out[5 * i + 1] = L[i].peer; out[5 * i + 2] = L[i].cone;
+            out[5 * i + 3] = L[i].count; out[5 * i + 4] = L[i].offset;
+        }
+    return 0;
+}
 int lrs_shard_comm_ranks(lrs_ctx *c, int *count) {
     if (!c || !count) { set_err("null argument"); return -1; }
     if (!sharded(c)) { *count = 1; return 0; }

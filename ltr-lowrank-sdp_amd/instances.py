@@ -10,6 +10,8 @@ restated as a generator with the same structure:
 * Lovász theta: C = -J (dense), tr(X) = 1, X_ij = 0 on edges.
 * random sparse SDP (C5): C = I (or dense), A_i with k random lower entries,
   b_i = <A_i, I> so X = I is feasible.
+* MaxCut with an LP block (the SDPA negative block size, io/lorads_file_io.c:104-194):
+  X_ii + s_i = 1 with LP slacks s_i >= 0, plus LP columns that touch many constraints.
 
 Files are written in plain SDPA ``.dat-s`` text, one entry per line.
 """
@@ -30,6 +32,7 @@ __all__ = [
     "random_sparse_problem",
     "write_sdpa",
     "config_instance",
+    "maxcut_lp",
 ]
 
 
@@ -220,3 +223,38 @@ def config_instance(name, directory):
     fn(tmp, **spec)
     os.replace(tmp, path)
     return path
+
+
+def maxcut_lp(path, n, p_edge, seed):
+    """MaxCut relaxation with inequality constraints through an LP block (LoRADS's LP cone,
+    data/lorads_lp_conic.c): SDP block n (C = -L/2 of a G(n, p) graph, unit weights), LP block of
+    n + 3 columns.  Constraint i (1..n): X_ii + s_i + [i % 3 == 0] 0.01 d = 1 (slack s_i, column i;
+    d = column n + 3 touches every third constraint: a dense LP column, >= 25 % of the rows);
+    constraint n + 1: X_12 + t_1 - t_2 = 0 (columns n + 1, n + 2: a free variable split in two).
+    LP costs c_s = 0.1, c_t = 0.5, c_d = 1 (written as F0 = -c, the reader's C = -F0)."""
+    rng = np.random.default_rng(seed)
+    iu, ju = np.triu_indices(n, 1)
+    keep = rng.random(iu.size) < p_edge
+    ei, ej = iu[keep], ju[keep]
+    m = n + 1
+    nlp = n + 3
+    deg = np.zeros(n)
+    np.add.at(deg, ei, 1.0)
+    np.add.at(deg, ej, 1.0)
+    ents = []
+    # SDP objective F0 = L / 2 (C = -L/2)
+    ents.append((np.zeros(ei.size, int), 1, ei + 1, ej + 1, -0.5 * np.ones(ei.size)))
+    ents.append((np.zeros(n, int), 1, np.arange(n) + 1, np.arange(n) + 1, 0.5 * deg))
+    # LP objective F0 = -c
+    cs = np.concatenate([np.full(n, 0.1), [0.5, 0.5, 1.0]])
+    ents.append((np.zeros(nlp, int), 2, np.arange(nlp) + 1, np.arange(nlp) + 1, -cs))
+    # X_ii + s_i (+ 0.01 d) = 1
+    ents.append((np.arange(n) + 1, 1, np.arange(n) + 1, np.arange(n) + 1, np.ones(n)))
+    ents.append((np.arange(n) + 1, 2, np.arange(n) + 1, np.arange(n) + 1, np.ones(n)))
+    rows3 = np.arange(0, n, 3)
+    ents.append((rows3 + 1, 2, np.full(rows3.size, n + 3), np.full(rows3.size, n + 3), np.full(rows3.size, 0.01)))
+    # X_12 + t_1 - t_2 = 0 (SDP entry (1, 2) is the symmetric pair: coefficient 1/2 each side)
+    ents.append((np.array([m]), 1, np.array([1]), np.array([2]), np.array([0.5])))
+    ents.append((np.array([m, m]), 2, np.array([n + 1, n + 2]), np.array([n + 1, n + 2]), np.array([1.0, -1.0])))
+    b = np.concatenate([np.ones(n), [0.0]])
+    return write_sdpa(path, m, [n, -nlp], b, ents)

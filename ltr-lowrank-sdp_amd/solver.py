@@ -139,6 +139,8 @@ def load_library(path=None):
         "lrs_shard_loopback": (C.c_int, [vp, vp, C.c_int]),
         "lrs_shard_info": (C.c_int, [vp, ip, ip, ip, ip, ip]),
         "lrs_shard_comm_ranks": (C.c_int, [vp, ip]),
+        "lrs_shard_comm_record": (C.c_int, [vp, C.c_int]),
+        "lrs_shard_comm_log": (C.c_int, [vp, C.POINTER(C.c_long), C.c_long, C.POINTER(C.c_long)]),
         "lrs_shard_plan": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_long), ip, ip, ip, ip, ip, ip, ip]),
     }
     for name, (res, args) in sig.items():
@@ -270,6 +272,20 @@ class Solver:
         v = [C.c_int() for _ in range(5)]
         self._check(self.lib.lrs_shard_info(self.ctx, *[C.byref(x) for x in v]), "shard_info")
         return tuple(x.value for x in v)
+
+    def comm_record(self, on=True):
+        """Start (clearing the log) or stop recording the transport's operations."""
+        self._check(self.lib.lrs_shard_comm_record(self.ctx, 1 if on else 0), "comm_record")
+
+    def comm_log(self):
+        """The recorded operations: an (n, 5) int64 array {kind, peer, cone, count, offset}
+        (include/lrsdp.h lrs_shard_comm_log)."""
+        n = C.c_long()
+        self._check(self.lib.lrs_shard_comm_log(self.ctx, None, 0, C.byref(n)), "comm_log")
+        out = np.zeros(5 * max(1, n.value), dtype=np.int64)
+        self._check(self.lib.lrs_shard_comm_log(self.ctx, out.ctypes.data_as(C.POINTER(C.c_long)), n.value,
+                                                C.byref(n)), "comm_log")
+        return out[:5 * n.value].reshape(-1, 5)
 
     def comm_ranks(self):
         """Ranks the shard transport counts itself (RCCL ncclCommCount; 1 unsharded)."""

@@ -204,11 +204,15 @@ END:;
     if (dump) {
         FILE *fd = fopen(dump, "wb");
         if (fd) {
-            double v = (double)S->nCones;
+            /* an LP block: one more "cone" of rank 1 holding r (the device's layout) */
+            const int lp = S->nLpCols > 0;
+            double v = (double)(S->nCones + lp);
             fwrite(&v, 8, 1, fd);
             for (lorads_int k = 0; k < S->nCones; ++k) { v = (double)S->var->R[k]->rank; fwrite(&v, 8, 1, fd); }
+            if (lp) { v = 1.0; fwrite(&v, 8, 1, fd); }
             for (lorads_int k = 0; k < S->nCones; ++k)
                 fwrite(S->var->R[k]->matElem, 8, (size_t)S->var->R[k]->nRows * S->var->R[k]->rank, fd);
+            if (lp) fwrite(S->var->rLp->matElem, 8, (size_t)S->nLpCols, fd);
             v = (double)S->nRows;
             fwrite(&v, 8, 1, fd);
             fwrite(S->var->dualVar, 8, (size_t)S->nRows, fd);
@@ -416,10 +420,14 @@ static int steps_dump(lorads_solver *S, const double *trips, long done, const ch
     double dd = (double)done;
     fwrite(&dd, 8, 1, fo);
     fwrite(trips, 8, 4 * done, fo);
+    /* an LP block's r and gradient follow the SDP cones' (the device appends the LP block as the
+       last cone at rank 1; the L-BFGS pairs hold the LP part last too, setlbfgsHisTwoLP) */
     for (lorads_int k = 0; k < S->nCones; ++k)
         fwrite(S->var->R[k]->matElem, 8, S->var->R[k]->nRows * S->var->R[k]->rank, fo);
+    if (S->nLpCols > 0) fwrite(S->var->rLp->matElem, 8, S->nLpCols, fo);
     for (lorads_int k = 0; k < S->nCones; ++k)
         fwrite(S->var->Grad[k]->matElem, 8, S->var->Grad[k]->nRows * S->var->Grad[k]->rank, fo);
+    if (S->nLpCols > 0) fwrite(S->var->gradLp->matElem, 8, S->nLpCols, fo);
     fwrite(S->var->constrValSum, 8, m, fo);
     fwrite(S->var->dualVar, 8, m, fo);
     lbfgs_node *newest = S->lbfgsHis->prev;
@@ -429,6 +437,62 @@ static int steps_dump(lorads_solver *S, const double *trips, long done, const ch
     fclose(fo);
     printf("REF_STEPS_DUMP K=%ld done=%ld\n", K, done);
     fflush(stdout);
+    return 0;
+}
+
+/* admm_sweep_lp <file> <rank> <in> <out>: the ADMM sweep of a problem with an LP block
+ * (LORADSUpdateSDPLPVar, lorads_alg_common.c:352-372: every SDP cone's U / V half-steps, then per
+ * LP column LORADSUpdateLPVarOne for u_j and v_j, lorads_admm.c:759-792) and the dual update, on
+ * given U, V, lambda.  Input doubles: U, V (SDP cones column-major, then the LP block's nLpCols
+ * values: the device's LP cone at rank 1), lambda[m], rho_admm, cg_tol.  Dump: U, V (same
+ * layout), constrValSum[m], dualVar[m], total CG iterations. */
+static int mode_admm_sweep_lp(int argc, char **argv) {
+    if (argc < 6) return 2;
+    lorads_params p; default_params(&p);
+    p.fname = argv[2];
+    p.fixedRank = atoi(argv[3]);
+    ref_ctx c; memset(&c, 0, sizeof(c));
+    double t_read, tss;
+    if (ref_setup(&c, &p, &t_read, &tss)) { fprintf(stderr, "read failed\n"); return 1; }
+    lorads_solver *S = c.S;
+    lorads_int m = S->nRows, K = S->nCones, NR = 0, nlp = S->nLpCols;
+    for (lorads_int k = 0; k < K; ++k) NR += S->var->R[k]->nRows * S->var->R[k]->rank;
+    const lorads_int NA = NR + nlp;
+    FILE *fi = fopen(argv[4], "rb");
+    if (!fi) return 1;
+    fseek(fi, 0, SEEK_END); long sz = ftell(fi); fseek(fi, 0, SEEK_SET);
+    double *in = malloc(sz); if (fread(in, 1, sz, fi) != (size_t)sz) return 1; fclose(fi);
+    if (sz != (long)(8 * (2 * NA + m + 2))) { fprintf(stderr, "input size %ld, expected %ld\n", sz, (long)(8 * (2 * NA + m + 2))); return 1; }
+    const double *U = in, *V = in + NA, *lam = in + 2 * NA;
+    const double rho_admm = in[2 * NA + m], cg_tol = in[2 * NA + m + 1];
+    lorads_int off;
+    LOAD(S->var->U, U); LOAD(S->var->V, V);
+    if (nlp > 0) { memcpy(S->var->uLp->matElem, U + NR, 8 * nlp); memcpy(S->var->vLp->matElem, V + NR, 8 * nlp); }
+    memcpy(S->var->dualVar, lam, 8 * m);
+    if (nlp > 0) {
+        LORADSInitConstrValAllLP(S, S->var->uLp, S->var->vLp, S->var->U, S->var->V);
+        LORADSInitConstrValSumLP(S);
+    } else {
+        LORADSInitConstrValAll(S, S->var->uLp, S->var->vLp, S->var->U, S->var->V);
+        LORADSInitConstrValSum(S);
+    }
+    S->cgIter = 0;
+    if (nlp > 0) LORADSUpdateSDPLPVar(S, rho_admm, cg_tol, 800);
+    else LORADSUpdateSDPVar(S, rho_admm, cg_tol, 800);
+    LORADSUpdateDualVar(S, rho_admm);
+    FILE *fo = fopen(argv[5], "wb");
+    if (!fo) return 1;
+    DUMPF(S->var->U);
+    if (nlp > 0) fwrite(S->var->uLp->matElem, 8, nlp, fo);
+    DUMPF(S->var->V);
+    if (nlp > 0) fwrite(S->var->vLp->matElem, 8, nlp, fo);
+    fwrite(S->var->constrValSum, 8, m, fo);
+    fwrite(S->var->dualVar, 8, m, fo);
+    double it = (double)S->cgIter;
+    fwrite(&it, 8, 1, fo);
+    fclose(fo);
+    free(in);
+    printf("REF_ADMM_SWEEP_LP cg=%ld\n", (long)S->cgIter);
     return 0;
 }
 
@@ -543,6 +607,7 @@ int main(int argc, char **argv) {
     if (argc < 3) { fprintf(stderr, "usage: %s solve|alm_rate|kernels file ...\n", argv[0]); return 2; }
     if (!strcmp(argv[1], "solve")) return mode_solve(argc, argv);
     if (!strcmp(argv[1], "alm_rate")) return mode_alm_rate(argc, argv);
+    if (!strcmp(argv[1], "admm_sweep_lp")) return mode_admm_sweep_lp(argc, argv);
     if (!strcmp(argv[1], "kernels")) return mode_kernels(argc, argv);
     if (!strcmp(argv[1], "alm_steps")) return mode_alm_steps(argc, argv);
     if (!strcmp(argv[1], "admm_sweep")) return mode_admm_sweep(argc, argv);

@@ -47,6 +47,9 @@ CASES = [
     # (a ring of 1 crashes the reference: its node links are only set in the loop that adds nodes 2..L)
     ("mc_rand200_l3", os.path.join(GOLD, "instances", "mc_rand200.dat-s"), -1, [1, 2, 3, 4, 5, 8]),
     ("theta40_l3", os.path.join(GOLD, "instances", "theta40.dat-s"), -1, [1, 2, 3, 4, 5, 8]),
+    # an LP block (instances.maxcut_lp: slacks, a free variable split in two, a dense LP column): r and
+    # its gradient appended after the SDP cone (the device's LP cone at rank 1), the pairs LP part last
+    ("mc_lp60", os.path.join(GOLD, "instances", "mc_lp60.dat-s"), -1, [1, 2, 3, 4, 5, 8]),
 ]
 FLAGS = {"mc_rand200_l3": ["--lbfgsListLength", "3"], "theta40_l3": ["--lbfgsListLength", "3"]}
 GEN = {"rdense300": (300, 3000, 6, 7)}

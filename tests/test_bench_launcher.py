@@ -25,6 +25,9 @@ def test_self_launch_two_ranks_dry_run():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["dry_run"] and d["backend"] == "gloo"
+    # N > 1: the headline is the single row-sharded instance (strong scaling), replicas beside it
+    assert d["headline"].startswith("sharded") and d["scaling"] == "strong"
+    assert d["config"]["parallelism"].startswith("row-sharded x2") and d["replicas"]["scaling"] == "weak"
     assert d["ranks_aggregated"] == 2   # both ranks met the barrier and the aggregate
 
 

@@ -26,7 +26,7 @@ from golden_util import GOLDEN, ROOT, rel_err
 
 pytestmark = pytest.mark.gpu
 STEP_CASES = ["mc_rand200", "mc_torus12x10", "mc_rand300w", "theta40", "theta25x3", "rsparse60", "checker_1.5",
-              "mc_rand300w_r290"]
+              "mc_rand300w_r290", "mc_lp60"]
 # fixtures whose n x r arrays are stored as n x k projections V @ Omega (scripts/make_golden_steps.py)
 PROJ = {"mc_rand300w_r290": 4}
 
