@@ -157,6 +157,10 @@ int lrs_op_alm_update(lrs_ctx *ctx, double rho, double tau, double *lag_norm_sq,
  * sum_i y[i] A_i) X, X the factor `which` (LRS_R, LRS_U, ...), y[m] host, out column-major like
  * lrs_factor_get.  Unsharded contexts. */
 int lrs_op_adjoint(lrs_ctx *ctx, const double *y, int which, double *out, double scale, int with_C);
+/*   lrs_op_adjoint works in the solver's scratch: the constraint weights (the M1 buffer), the slot
+ *   values S, and the X / CG-Q work factors are overwritten.  No operator reads those across
+ *   calls -- lrs_op_grad, lrs_op_admm_half and the fused loops form M1 and S afresh -- so the
+ *   iterate (R, U, V, D, G, the L-BFGS pairs), LAMBDA and CVS are unchanged by it. */
 /* coneAUV + objAUV (data/def_lorads_sdp_conic.h:106-111) summed over the cones: out_m[i] =
  * <A_i, sym(X_u X_v^T)> (u == v: X_u X_u^T), cobj = <C, sym(X_u X_v^T)> before the division by
  * the reopt objective scale.  Leaves the solver state (CVS) unchanged.  out_m, cobj may be NULL.
@@ -333,6 +337,11 @@ int lrs_shard_comm_ranks(lrs_ctx *ctx, int *count);
  * transports issue their groups from one op list, so the loopback transport's log is the
  * sequence of ncclSend / ncclRecv / ncclAllReduce calls the RCCL transport makes. */
 int lrs_shard_comm_record(lrs_ctx *ctx, int on);
+/* Inner-loop calls whose one-workgroup-per-cone launch timed out in its
+ * workgroups' exchange and was rerun from the kept state on the multi-launch iteration (the
+ * context then stays on it).  LRS_XWG_SPIN=k sets the exchange's spin limit to 2^k polls
+ * (default 26) -- small k forces the fallback (tests). */
+int lrs_xwg_fallbacks(lrs_ctx *ctx, int *count);
 int lrs_shard_comm_log(lrs_ctx *ctx, long *out, long cap, long *n);
 /* Host-only (no device, no context) view of the row partition of a sharded solve of the
    instance at `path`: counts[8] = {n_global, first owned global row, owned rows, local rows

@@ -366,6 +366,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
 // ---- single-workgroup persistent inner loop (lrs_kernels.hip "Single-workgroup"): small
 // problems (R and D of every cone in one CU's LDS, ld <= 64, no full dense C) ----
 bool small_alm_fits(const DevProblem &P, DevWork &W);
+// workgroups of the single-workgroup inner loop for this problem (> 1: one per cone, the
+// exchanges between them), 0 when it does not fit
+int small_alm_workgroups(const DevProblem &P, DevWork &W);
 int launch_small_alm(const DevProblem &P, DevWork &W, const double *ctrl_in, double *ctrl_out, double *ls_out,
                      hipStream_t st);
 

@@ -5862,6 +5862,7 @@ struct SmallArgs {
     // adjacency; the per-trip sums are exchanged through xbuf ([2][kSmallMaxWg][16]) and the
     // arrival counter xcnt
     int nwg, xs;
+    int spin_log2;             // the exchange's spin limit, 2^spin_log2 polls (LRS_XWG_SPIN; default 26)
     SmallWg wg[kSmallMaxWg];   // [0]: the single workgroup's (all cones, merged adjacency) when nwg == 1
     double *xbuf;
     unsigned *xcnt;
@@ -5891,7 +5892,7 @@ __device__ __forceinline__ bool xwg_sum(const SmallArgs &A, int wg, unsigned &xe
     if (lane == 0) {
         __hip_atomic_fetch_add(A.xcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (long spin = 0; __hip_atomic_load(A.xcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
-            if (spin > (1L << 26)) { ok = 0; break; }
+            if (spin > (1L << A.spin_log2)) { ok = 0; break; }
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -6456,6 +6457,22 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         c[C_RCUR] = 0.0;
         if (xfail) { c[C_ACTIVE] = 0.0; c[C_EXIT] = (double)EXIT_XWG; }
     }
+    if (MC) {
+        // the control block goes out through the buffer it came in by (ctrl_out == ctrl_in): every
+        // workgroup counts itself out once more, and workgroup 0 writes only after all have --
+        // each read ctrl_in at its start, so none can still be reading it
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_fetch_add(A.xcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (wg == 0 && !xfail) {
+                const unsigned target = (xe + 1u) * (unsigned)A.nwg;
+                for (long spin = 0; __hip_atomic_load(A.xcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+                    if (spin > (1L << A.spin_log2)) { c[C_ACTIVE] = 0.0; c[C_EXIT] = (double)EXIT_XWG; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+        }
+    }
     __syncthreads();
     if (wg == 0 && tid < C_NCTRL) A.ctrl_out[tid] = c[tid];
     if (wg == 0 && tid < LS_N) A.ls_out[tid] = ls[tid];
@@ -6540,6 +6557,10 @@ bool small_alm_fits(const DevProblem &P, DevWork &W) {
     SmallArgs A{};
     return small_alm_args(P, W, A, nullptr);
 }
+int small_alm_workgroups(const DevProblem &P, DevWork &W) {
+    SmallArgs A{};
+    return small_alm_args(P, W, A, nullptr) ? A.nwg : 0;
+}
 template <int LD, bool AL, bool MC>
 static int launch_small_ld(const SmallArgs &A, size_t lds, hipStream_t st) {
     static bool attr = false;
@@ -6575,6 +6596,10 @@ int launch_small_alm(const DevProblem &P, DevWork &W, const double *ctrl_in, dou
     A.ctrl_in = ctrl_in;
     A.ctrl_out = ctrl_out;
     A.ls_out = ls_out;
+    {
+        const char *e = getenv("LRS_XWG_SPIN");
+        A.spin_log2 = e ? std::max(0, std::min(40, atoi(e))) : 26;
+    }
     size_t lds = small_lds_bytes(A.N, ld, A.Ptot, A.nadj, A.al != 0);
     if (A.nwg > 1) {   // the largest cone's
         lds = 0;
@@ -7227,7 +7252,10 @@ __global__ void __launch_bounds__(kScT) k_small_cg(SmallCgBatch Bt) {
             }
         LRS_SC_T(11);
         if (tid == 0) {
-            A.cgc[CG_ITERS] = iters;
+            // a batch launch (one block per cone, launch_small_cg_batch) has no single count to report:
+            // CG_ITERS is the one-cone launch's (lrs_op_admm_half reads it); every launch adds its
+            // cones' counts to CG_TOTAL, the one the ADMM log and lrs_result use
+            if (gridDim.x == 1) A.cgc[CG_ITERS] = iters;
             atomicAdd(A.cgc + CG_TOTAL, (double)iters);   // several cones' blocks: integers, exact in any order
 #ifdef LRS_PHASE_TIMING
             g_phase[1][14] += iters;

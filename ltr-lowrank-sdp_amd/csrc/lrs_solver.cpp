@@ -140,6 +140,12 @@ struct lrs_ctx {
     double *hgram = nullptr;    // pinned: every cone's r x r Gram of one oracle-rank evaluation
     size_t hgram_n = 0;
     bool naive_warned = false;   // --oracleRankNaive: the fallback line printed this solve
+    // one-workgroup-per-cone inner loop: the pre-launch state (xwg_snapshot), whether an exchange
+    // timed out in this context (the multi-launch iteration from then on) and how often
+    double *xwg_snap = nullptr;
+    long xwg_snap_len = 0;
+    bool small_off = false;
+    int xwg_fallbacks = 0;
     // L-BFGS mirror
     int head = 0, gcur = 0;
     double beta[2] = {0, 0}, yy[2] = {0, 0};
@@ -1594,12 +1600,38 @@ constexpr int kSmallMaxGlobal = 16;
 static bool use_small(lrs_ctx *c) {
     const char *e = getenv("LRS_SMALL");
     const int env = e ? atoi(e) : -1;
-    if (sharded(c) || c->lbfgsL != 2) return false;
+    if (sharded(c) || c->lbfgsL != 2 || c->small_off) return false;
     if (c->dp.no_lat != 4) {
         if (c->dp.no_lat != 0 || env == 0) return false;
         if (env != 1 && c->dp.mg > kSmallMaxGlobal) return false;
     }
     return small_alm_fits(c->dp, c->W);
+}
+
+// what k_small_alm writes (the iterate, both gradients, the L-BFGS pairs, A(RR^T), the
+// constraint records, the control blocks, the line search): kept before a one-workgroup-per-cone
+// launch (save = true) and put back after its exchange timed out (save = false)
+static int xwg_snapshot(lrs_ctx *c, bool save) {
+    DevWork &W = c->W;
+    const long NR = std::max(2L, c->dp.NRpad), m = std::max(1, c->dp.m);
+    struct B { double *p; long n; } bs[] = {{W.R, NR}, {W.G[0], NR}, {W.G[1], NR}, {W.ls[0], NR}, {W.ly[0], NR},
+                                            {W.ls[1], NR}, {W.ly[1], NR}, {W.cvs, m}, {W.rec, 4 * m},
+                                            {W.ctrl, 2 * C_NCTRL}, {W.lsres, 2 * LS_N}};
+    long need = 0;
+    for (auto &b : bs) need += b.n;
+    if (need > c->xwg_snap_len) {
+        if (c->xwg_snap) HIPC(hipFree(c->xwg_snap));
+        c->xwg_snap = nullptr;
+        HIPC(hipMalloc((void **)&c->xwg_snap, sizeof(double) * need));
+        c->xwg_snap_len = need;
+    }
+    long off = 0;
+    for (auto &b : bs) {
+        if (save) HIPC(hipMemcpyAsync(c->xwg_snap + off, b.p, sizeof(double) * b.n, hipMemcpyDeviceToDevice, c->st));
+        else HIPC(hipMemcpyAsync(b.p, c->xwg_snap + off, sizeof(double) * b.n, hipMemcpyDeviceToDevice, c->st));
+        off += b.n;
+    }
+    return 0;
 }
 
 static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, double gap, long budget, InnerIo &io,
@@ -1635,21 +1667,41 @@ static int run_inner(lrs_ctx *c, const lrs_params *p, double rho, double rctol, 
     const double t_in = c->stats ? now_s() : 0.0;
     long enq = 0;
     // the single-workgroup inner loop (small problems): the whole call is one launch
-    const bool small = !c->prof && use_small(c);
+    bool small = !c->prof && use_small(c);
+    bool fell_back = false;
     if (small) {
+        // one workgroup per cone: the workgroups hand sums to each other through device memory,
+        // which assumes they are co-resident; another stream or context holding the CUs can delay
+        // one past the exchange's spin limit (EXIT_XWG).  The state the loop writes is kept
+        // first, so such a call is rerun from it on the multi-launch iteration.
+        const bool mc = small_alm_workgroups(c->dp, c->W) > 1;
+        if (mc && xwg_snapshot(c, true)) return -1;
         OPC(launch_small_alm(c->dp, c->W, c->W.ctrl + C_NCTRL, c->W.ctrl + C_NCTRL, c->W.lsres, c->st));
         HIPC(hipMemcpyAsync(c->hpin + kHpCtrl, c->W.ctrl + C_NCTRL, sizeof(double) * C_NCTRL, hipMemcpyDeviceToHost,
                             c->st));
         HIPC(hipStreamSynchronize(c->st));
         res = c->hpin + kHpCtrl;
         if ((int)res[C_EXIT] == EXIT_XWG) {
-            set_err("single-workgroup inner loop: the cones' workgroups did not meet (exchange timed out)");
-            return -1;
+            if (!mc) {
+                set_err("single-workgroup inner loop: exchange timed out");
+                return -1;
+            }
+            if (xwg_snapshot(c, false)) return -1;
+            if (!c->small_off)
+                fprintf(stderr, "[lrsdp] one-workgroup-per-cone inner loop: the workgroups' exchange timed out; "
+                                "this solve continues on the multi-launch iteration\n");
+            c->small_off = true;
+            c->xwg_fallbacks++;
+            small = false;
+            fell_back = true;
+            res = c->hpin + kHpCtrl;
+        } else {
+            enq = std::max(0L, (long)res[C_INNER] - io.inner);
+            c->dp.last_path = 4;
+            if (c->stats) c->st_batches++;
         }
-        enq = std::max(0L, (long)res[C_INNER] - io.inner);
-        c->dp.last_path = 4;
-        if (c->stats) c->st_batches++;
     }
+    (void)fell_back;
     if (!c->prof && !small) {
         // Two batches in flight: batch k+1 is enqueued before the host waits for batch k, so
         // the GPU never idles on the host's submission or on the wait's wake-up.  Each batch
@@ -2719,7 +2771,7 @@ void lrs_ctx_destroy(lrs_ctx *c) {
         if (e) (void)hipEventDestroy(e);
     delete c->comm;
     for (void *q : {(void *)c->s_tickets, (void *)c->s_tmpfin, (void *)c->s_rpart, (void *)c->s_fin, (void *)c->d_sendbuf,
-                    (void *)c->d_sendvec, (void *)c->Cw0, (void *)c->Craw0})
+                    (void *)c->d_sendvec, (void *)c->Cw0, (void *)c->Craw0, (void *)c->xwg_snap})
         if (q) (void)hipFree(q);
     for (int *q : c->d_send_rows)
         if (q) (void)hipFree(q);
@@ -3769,6 +3821,12 @@ int lrs_shard_info(lrs_ctx *c, int *world, int *rank, int *row0, int *nown, int 
     return 0;
 }
 
+int lrs_xwg_fallbacks(lrs_ctx *c, int *count) {
+    LRS_NEED_CTX(c);
+    LRS_NEED_ARG(count);
+    *count = c->xwg_fallbacks;
+    return 0;
+}
 int lrs_shard_comm_record(lrs_ctx *c, int on) {
     LRS_NEED_CTX(c);
     if (!c->comm) { set_err("lrs_shard_comm_record: the context is not sharded"); return -1; }

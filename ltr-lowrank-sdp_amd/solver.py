@@ -140,6 +140,7 @@ def load_library(path=None):
         "lrs_shard_info": (C.c_int, [vp, ip, ip, ip, ip, ip]),
         "lrs_shard_comm_ranks": (C.c_int, [vp, ip]),
         "lrs_shard_comm_record": (C.c_int, [vp, C.c_int]),
+        "lrs_xwg_fallbacks": (C.c_int, [vp, ip]),
         "lrs_shard_comm_log": (C.c_int, [vp, C.POINTER(C.c_long), C.c_long, C.POINTER(C.c_long)]),
         "lrs_shard_plan": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_long), ip, ip, ip, ip, ip, ip, ip]),
     }
@@ -272,6 +273,13 @@ class Solver:
         v = [C.c_int() for _ in range(5)]
         self._check(self.lib.lrs_shard_info(self.ctx, *[C.byref(x) for x in v]), "shard_info")
         return tuple(x.value for x in v)
+
+    def xwg_fallbacks(self):
+        """Inner-loop calls rerun on the multi-launch iteration after a one-workgroup-per-cone
+        exchange timed out (include/lrsdp.h lrs_xwg_fallbacks)."""
+        n = C.c_int()
+        self._check(self.lib.lrs_xwg_fallbacks(self.ctx, C.byref(n)), "xwg_fallbacks")
+        return n.value
 
     def comm_record(self, on=True):
         """Start (clearing the log) or stop recording the transport's operations."""

@@ -80,9 +80,10 @@ def solver_mod():
 
 
 def certified(sv, r, trace):
-    """[b^T lambda + min(lambda_min(S), 0) tr X, <C, X>] of the context's current iterate."""
+    """[b^T lambda + min(lambda_min(S), 0) tr X, <C, X>] of the context's current iterate (lambda_min
+    of the context's S = f (C - A^*(lambda)) divided by the reopt objective scale f, like dobj)."""
     _, lmin = sv.dual_infeasibility()
-    return r["dobj"] + min(float(np.min(lmin)), 0.0) * trace, r["pobj"]
+    return r["dobj"] + min(float(np.min(lmin)), 0.0) / r.get("obj_scale", 1.0) * trace, r["pobj"]
 
 
 def intersect(a, b, scale):

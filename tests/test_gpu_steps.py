@@ -248,3 +248,31 @@ def test_single_workgroup_solve_matches_default(solver_mod, name, monkeypatch):
         for k in ("pobj", "dobj"):
             assert abs(a[k] - b[k]) <= tol * (1 + abs(a[k])), (k, a[k], b[k], tol)
         assert b["pinf"] <= 1e-4
+
+
+def test_one_workgroup_per_cone_timeout_falls_back(solver_mod, monkeypatch):
+    """the one-workgroup-per-cone inner loop assumes its workgroups are co-resident; an
+    exchange that times out (forced here: LRS_XWG_SPIN=0, a spin limit of two polls) must not end
+    the solve nor leave a half-updated iterate -- the call is rerun from the state kept before the
+    launch on the multi-launch iteration, and the trips still equal the reference's at 1e-9."""
+    monkeypatch.setenv("LRS_SMALL_MC", "1")
+    monkeypatch.setenv("LRS_XWG_SPIN", "0")
+    z = np.load(os.path.join(GOLDEN, "steps_theta25x3.npz"))
+    sv = solver_mod.Solver(_path("theta25x3"))
+    sv.set_kernel_path(4)
+    for K in [int(k) for k in z["ks"]]:
+        trips = z[f"K{K}_trips"]
+        if trips.shape[0] < K:
+            continue
+        d = sv.alm_steps(K, reoptLevel=0)
+        assert d["inner"] == K, (K, d["inner"])
+        tau, rn, lag, pinf = trips[K - 1]
+        assert abs(d["tau"] - tau) <= TOL * abs(tau), (K, d["tau"], tau)
+        assert abs(d["lag"] - lag) <= TOL * abs(lag), (K, d["lag"], lag)
+        for key in ("R", "G", "cvs", "s", "y"):
+            assert rel_err(d[key], z[f"K{K}_{key}"]) < TOL, (K, key)
+    assert sv.xwg_fallbacks() >= 1
+    # the whole solve also completes (ALM, ADMM) on the fallback path
+    res = sv.solve(reoptLevel=0)
+    assert res["pinf"] <= 1e-4
+    sv.close()

@@ -79,9 +79,11 @@ def _path(name, tmp_path):
     return os.path.join(DATA, f"{name}.dat-s")
 
 
-def _interval(dobj, lam_min, trace, pobj):
-    """[b^T lambda + min(lambda_min(S), 0) tr X, <C, X>]: weak duality for a primal-feasible X."""
-    return dobj + min(float(np.min(lam_min)), 0.0) * trace, pobj
+def _interval(dobj, lam_min, trace, pobj, obj_scale=1.0):
+    """[b^T lambda + min(lambda_min(S), 0) tr X, <C, X>]: weak duality for a primal-feasible X.
+    dobj is reported unscaled (divided by the reopt objective scale f); lambda_min comes from the
+    context's current S = f (C - A^*(lambda)), so it is divided by f too."""
+    return dobj + min(float(np.min(lam_min)), 0.0) / obj_scale * trace, pobj
 
 
 @pytest.mark.gpu
@@ -107,7 +109,7 @@ def test_objectives_agree_within_both_certificates(solver_mod, name, tmp_path):
     r = sv.solve(**kwargs_of(g["flags"]))
     _, lmin_dev = sv.dual_infeasibility()
     sv.close()
-    lo_dev, hi_dev = _interval(r["dobj"], lmin_dev, trace, r["pobj"])
+    lo_dev, hi_dev = _interval(r["dobj"], lmin_dev, trace, r["pobj"], r["obj_scale"])
     rel = abs(r["pobj"] - ref["admm_pobj"]) / abs(ref["admm_pobj"])
     print(f"{name}: reference [{lo_ref:.9g}, {hi_ref:.9g}] (lambda_min {np.min(lmin_ref):.3e}); device "
           f"[{lo_dev:.9g}, {hi_dev:.9g}] (lambda_min {np.min(lmin_dev):.3e}, pinf {r['pinf']:.1e}, gap {r['gap']:.1e}); "
@@ -131,7 +133,8 @@ def test_reopt_level2_narrows_the_certificate(solver_mod):
     r = sv.solve(**kw)
     _, lmin = sv.dual_infeasibility()
     sv.close()
-    lo, hi = _interval(r["dobj"], lmin, trace, r["pobj"])
+    assert r["obj_scale"] > 0
+    lo, hi = _interval(r["dobj"], lmin, trace, r["pobj"], r["obj_scale"])
     z = np.load(os.path.join(ROOT, "tests", "golden", f"tight_final_{name}.npz"))
     ref = g["result"]
     print(f"{name} level 2: [{lo:.9g}, {hi:.9g}] width {(hi - lo) / abs(hi):.2e}, lambda_min {np.min(lmin):.3e}; "
