@@ -340,7 +340,7 @@ int lrs_shard_comm_record(lrs_ctx *ctx, int on);
 /* Inner-loop calls whose one-workgroup-per-cone launch timed out in its
  * workgroups' exchange and was rerun from the kept state on the multi-launch iteration (the
  * context then stays on it).  LRS_XWG_SPIN=k sets the exchange's spin limit to 2^k polls
- * (default 26) -- small k forces the fallback (tests). */
+ * (default 26; -1: no wait) -- k = -1 forces the fallback (tests). */
 int lrs_xwg_fallbacks(lrs_ctx *ctx, int *count);
 int lrs_shard_comm_log(lrs_ctx *ctx, long *out, long cap, long *n);
 /* Host-only (no device, no context) view of the row partition of a sharded solve of the

@@ -1970,8 +1970,14 @@ __global__ void __launch_bounds__(kBlock) k_pack_shared(int m, const int *__rest
 // sharded: MODE 1 = line search + R_new = R + tau D of every row (own and halo), MODE 2 = the
 // rest with the neighbours' R_new read back (one row per neighbour instead of R and D) and tau
 // from MODE 1.
+#ifndef LRS_BW_UB
+#define LRS_BW_UB 1   // neighbours in flight per lane group in the bandwidth regime's fused stage B
+#endif
+#ifndef LRS_BW_UB_MINB
+#define LRS_BW_UB_MINB 3
+#endif
 template <int G, int E, int U, int MODE>
-__global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : 1)) k_it_b(
+__global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : (MODE == 0 && U == LRS_BW_UB ? LRS_BW_UB_MINB : 1))) k_it_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
     const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0, double *s1, double *y1,
@@ -5726,7 +5732,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
                 if (small) LRS_LAUNCH_B(4, 0);
-                else if (bfused(pb[k], tbt[k])) LRS_LAUNCH_B(1, 0);
+                else if (bfused(pb[k], tbt[k])) LRS_LAUNCH_B(LRS_BW_UB, 0);
                 else LRS_LAUNCH_B(1, 1);
             });
         }
@@ -5862,7 +5868,7 @@ struct SmallArgs {
     // adjacency; the per-trip sums are exchanged through xbuf ([2][kSmallMaxWg][16]) and the
     // arrival counter xcnt
     int nwg, xs;
-    int spin_log2;             // the exchange's spin limit, 2^spin_log2 polls (LRS_XWG_SPIN; default 26)
+    int spin_log2;             // the exchange's spin limit, 2^spin_log2 polls (LRS_XWG_SPIN; default 26; -1 none)
     SmallWg wg[kSmallMaxWg];   // [0]: the single workgroup's (all cones, merged adjacency) when nwg == 1
     double *xbuf;
     unsigned *xcnt;
@@ -5892,7 +5898,7 @@ __device__ __forceinline__ bool xwg_sum(const SmallArgs &A, int wg, unsigned &xe
     if (lane == 0) {
         __hip_atomic_fetch_add(A.xcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (long spin = 0; __hip_atomic_load(A.xcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
-            if (spin > (1L << A.spin_log2)) { ok = 0; break; }
+            if (spin > (A.spin_log2 < 0 ? -1L : (1L << A.spin_log2))) { ok = 0; break; }
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -6467,7 +6473,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
             if (wg == 0 && !xfail) {
                 const unsigned target = (xe + 1u) * (unsigned)A.nwg;
                 for (long spin = 0; __hip_atomic_load(A.xcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
-                    if (spin > (1L << A.spin_log2)) { c[C_ACTIVE] = 0.0; c[C_EXIT] = (double)EXIT_XWG; break; }
+                    if (spin > (A.spin_log2 < 0 ? -1L : (1L << A.spin_log2))) { c[C_ACTIVE] = 0.0; c[C_EXIT] = (double)EXIT_XWG; break; }
                     __builtin_amdgcn_s_sleep(1);
                 }
             }
@@ -6598,7 +6604,7 @@ int launch_small_alm(const DevProblem &P, DevWork &W, const double *ctrl_in, dou
     A.ls_out = ls_out;
     {
         const char *e = getenv("LRS_XWG_SPIN");
-        A.spin_log2 = e ? std::max(0, std::min(40, atoi(e))) : 26;
+        A.spin_log2 = e ? std::max(-1, std::min(40, atoi(e))) : 26;   // -1: no wait at all (tests)
     }
     size_t lds = small_lds_bytes(A.N, ld, A.Ptot, A.nadj, A.al != 0);
     if (A.nwg > 1) {   // the largest cone's

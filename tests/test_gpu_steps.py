@@ -252,11 +252,11 @@ def test_single_workgroup_solve_matches_default(solver_mod, name, monkeypatch):
 
 def test_one_workgroup_per_cone_timeout_falls_back(solver_mod, monkeypatch):
     """the one-workgroup-per-cone inner loop assumes its workgroups are co-resident; an
-    exchange that times out (forced here: LRS_XWG_SPIN=0, a spin limit of two polls) must not end
+    exchange that times out (forced here: LRS_XWG_SPIN=-1, no waiting at all) must not end
     the solve nor leave a half-updated iterate -- the call is rerun from the state kept before the
     launch on the multi-launch iteration, and the trips still equal the reference's at 1e-9."""
     monkeypatch.setenv("LRS_SMALL_MC", "1")
-    monkeypatch.setenv("LRS_XWG_SPIN", "0")
+    monkeypatch.setenv("LRS_XWG_SPIN", "-1")
     z = np.load(os.path.join(GOLDEN, "steps_theta25x3.npz"))
     sv = solver_mod.Solver(_path("theta25x3"))
     sv.set_kernel_path(4)
