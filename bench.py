@@ -697,8 +697,10 @@ def main():
             line["sharded_headline"] = {"transport": "RCCL (ncclSend/Recv halo, ncclAllReduce totals)",
                                         "rank0_rows": info[3], "rank0_halo_rows": info[4], "seconds_max": ssec}
         else:
-            line["value"] = 0.0
-            line["headline"] = "sharded headline FAILED (see sharded_headline.error); replicas under `replicas`"
+            # labelled fallback: the replicas' rate (weak scaling), and a non-zero exit status
+            line["scaling"] = "weak"
+            line["config"]["parallelism"] = f"replicas x{world} (instance-level, weak) -- sharded headline FAILED"
+            line["headline"] = "replicas (the sharded headline FAILED: see sharded_headline.error)"
             line["sharded_headline"] = sharded_head
     if rank_id == 0 and world == 1 and not args.no_eps:
         eps_flags = dict(reoptLevel=0, heuristicFactor=10.0, phase1Tol=1e-2, phase2Tol=1e-5)
