@@ -92,6 +92,12 @@ typedef struct {
     ocoeff *A;
     double *uvt;             /* pattern scratch: sdp_obj_sum / sdp_coeff_w_sum */
     int rank, rank_max;
+    /* the LP block (lorads_lp_conic.c) restated as the diagonal cone at rank 1, as the product
+       does (lrs_problem.cpp build_problem): its columns the rows, x_j = r_j^2; per column its
+       (constraint, a) list in constraint order (lp_cone_presolve, :90-125), c_j and ||a_j||^2 */
+    int lp;
+    int *lp_ptr, *lp_con;
+    double *lp_a, *lp_c, *lp_nrm2;
 } ocone;
 
 struct oproblem {
@@ -112,6 +118,7 @@ void oracle_free(oproblem *p) {
         coeff_free(&c->C);
         for (int i = 0; i < c->ncoef; ++i) coeff_free(&c->A[i]);
         free(c->A); free(c->con); free(c->prow); free(c->pcol); free(c->uvt);
+        free(c->lp_ptr); free(c->lp_con); free(c->lp_a); free(c->lp_c); free(c->lp_nrm2);
     }
     free(p->cones); free(p->b); free(p);
 }
@@ -202,7 +209,8 @@ static int slot_lookup(const ocone *c, int row, int col) {
 static void presolve_cone(ocone *c) {
     int n = c->n;
     int dense = (n < 20) || c->C.dense;
-    for (int i = 0; i < c->ncoef && !dense; ++i) dense |= c->A[i].dense;
+    if (c->lp) dense = 0;   /* the LP block: per-column operations, never the packed dense path */
+    for (int i = 0; i < c->ncoef && !dense && !c->lp; ++i) dense |= c->A[i].dense;
     if (!dense) {
         long tot = c->C.nnz;
         for (int i = 0; i < c->ncoef; ++i) tot += c->A[i].nnz;
@@ -276,10 +284,7 @@ oproblem *oracle_read(const char *path) {
         if (k == nb - 1 && d < 0) { nlp = (int)-d; K = nb - 1; }            /* :187-190 */
         dims[k] = (int)d;
     }
-    if (nlp > 0) {
-        fprintf(stderr, "[lrsdp-oracle] LP block (-%d) not supported by this restatement\n", nlp);
-        free(t.s); free(dims); return NULL;
-    }
+    if (nlp > 0) { dims[nb - 1] = nlp; K = nb; }   /* the LP block: cone nb - 1, diagonal */
     double *b = calloc(m, sizeof(double));
     for (int i = 0; i < m; ++i) {
         if (!skip_to_number(&t)) { free(t.s); free(dims); free(b); return NULL; }
@@ -311,6 +316,7 @@ oproblem *oracle_read(const char *path) {
         ib -= 1; ii -= 1; ij -= 1;
         if (fabs(v) < 1e-12) continue;                        /* :288-294 */
         if (ib < 0 || ib >= K) continue;
+        if (nlp > 0 && ib == K - 1) ij = ii;                  /* LP: column iRow, :297-309 */
         if (ii > ij) { int tmp = ii; ii = ij; ij = tmp; }    /* :311-315 */
         if (ic == 0) v = -v;                                 /* :317-319, C = -F0 */
         if (cnt == cap) { cap *= 2; ent = realloc(ent, sizeof(oentry) * cap); blk = realloc(blk, sizeof(int) * cap); }
@@ -328,6 +334,7 @@ oproblem *oracle_read(const char *path) {
     for (int k = 0; k < K; ++k) {
         ocone *c = &p->cones[k];
         c->n = dims[k];
+        c->lp = nlp > 0 && k == K - 1;
         size_t nk = 0;
         for (size_t e = 0; e < cnt; ++e) if (blk[e] == k) nk++;
         oentry *ek = malloc(sizeof(oentry) * (nk ? nk : 1));
@@ -351,6 +358,50 @@ oproblem *oracle_read(const char *path) {
         }
         c->ncoef = ncoef;
         free(ek);
+        if (c->lp) {
+            /* lp_cone_presolve (lorads_lp_conic.c:85-147): per column its constraints in order, the
+               column's ||a||^2 from its raw entries; a column in >= 1/4 of the constraints is
+               LP_COEFF_DENSE, whose create routine leaves its row count 0 (lorads_lp_data.c:178-193:
+               calloc), so its coefficients reach neither A(x) nor A^*(y) -- dropped here, norm kept */
+            int n = c->n;
+            int *cnt = calloc(n, sizeof(int));
+            c->lp_nrm2 = calloc(n, sizeof(double));
+            c->lp_c = calloc(n, sizeof(double));
+            for (int q = 0; q < c->C.nnz; ++q) c->lp_c[c->C.row[q]] += c->C.val[q];
+            for (int i = 0; i < ncoef; ++i)
+                for (int q = 0; q < c->A[i].nnz; ++q) {
+                    cnt[c->A[i].row[q]]++;
+                    c->lp_nrm2[c->A[i].row[q]] += c->A[i].val[q] * c->A[i].val[q];
+                }
+            for (int j = 0; j < n; ++j) { double tq = sqrt(c->lp_nrm2[j]); c->lp_nrm2[j] = tq * tq; }
+            for (int i = 0; i < ncoef; ++i) {
+                int w = 0;
+                for (int q = 0; q < c->A[i].nnz; ++q) {
+                    int j = c->A[i].row[q];
+                    if (cnt[j] != 0 && (double)cnt[j] / (double)m >= 0.25) continue;
+                    c->A[i].row[w] = c->A[i].row[q]; c->A[i].col[w] = c->A[i].col[q]; c->A[i].val[w] = c->A[i].val[q];
+                    w++;
+                }
+                c->A[i].nnz = w;
+                c->A[i].dense = 0;
+            }
+            c->lp_ptr = calloc(n + 1, sizeof(int));
+            long tot = 0;
+            for (int i = 0; i < ncoef; ++i)
+                for (int q = 0; q < c->A[i].nnz; ++q) { c->lp_ptr[c->A[i].row[q] + 1]++; tot++; }
+            for (int j = 0; j < n; ++j) c->lp_ptr[j + 1] += c->lp_ptr[j];
+            c->lp_con = malloc(sizeof(int) * (tot ? tot : 1));
+            c->lp_a = malloc(sizeof(double) * (tot ? tot : 1));
+            int *fill = calloc(n, sizeof(int));
+            for (int i = 0; i < ncoef; ++i)   /* constraints ascending: each column's list in order */
+                for (int q = 0; q < c->A[i].nnz; ++q) {
+                    int j = c->A[i].row[q];
+                    c->lp_con[c->lp_ptr[j] + fill[j]] = c->con[i];
+                    c->lp_a[c->lp_ptr[j] + fill[j]] = c->A[i].val[q];
+                    fill[j]++;
+                }
+            free(cnt); free(fill);
+        }
         presolve_cone(c);
     }
     free(ent); free(blk); free(dims);
@@ -476,6 +527,7 @@ static void nrm_consts(osolver *s) {   /* cal_sdp_const, data/lorads_solver.c:14
             n1 += 2 * fabs(a); n2 += 2 * a * a; ni = OMAX(ni, fabs(a));
             if (C->row[q] == C->col[q]) { n1 -= fabs(a); n2 -= a * a; }
         }
+        if (p->cones[k].lp) n2 = n1 * n1;   /* lp_cone_obj_nrm2Square, lorads_lp_conic.c:171-176 */
         s->cObjNrm1 += n1; s->cObjNrm2 += n2; s->cObjNrmInf = OMAX(s->cObjNrmInf, ni);
     }
     s->cObjNrm2 = pow(s->cObjNrm2, 0.5);
@@ -493,9 +545,11 @@ static void nrm_consts(osolver *s) {   /* cal_sdp_const, data/lorads_solver.c:14
 }
 
 /* LORADSDetermineRank, data/lorads_solver.c:406-459 */
+static int n_sdp(const osolver *s) { return s->K - (s->K > 0 && s->p->cones[s->K - 1].lp ? 1 : 0); }
 static void determine_rank(osolver *s) {
     for (int k = 0; k < s->K; ++k) {
         ocone *c = &s->p->cones[k];
+        if (c->lp) { s->rank[k] = 1; c->rank_max = 1; continue; }   /* x_j = r_j^2 */
         int nnzRows = c->ncoef;
         int calc_max = OMIN((int)sqrt(2.0 * nnzRows) + 1, c->n);
         if (s->prm.fixedRank > 0) {
@@ -509,7 +563,7 @@ static void determine_rank(osolver *s) {
         } else {
             int rk;
             if (s->prm.timesLogRank <= 1e-6) rk = calc_max;
-            else if (nnzRows / c->n >= 20 && c->n <= 400 && s->K <= 3) rk = calc_max;
+            else if (nnzRows / c->n >= 20 && c->n <= 400 && n_sdp(s) <= 3) rk = calc_max;   /* nCones */
             else rk = (int)OMIN(ceil(s->prm.timesLogRank * log((double)c->n)), (double)calc_max);
             s->rank[k] = OMAX(1, rk);
         }
@@ -793,6 +847,7 @@ static int count_significant(int r, double *gram, double eps) {
 static int oracle_rank(osolver *s, int phase) {
     int tot = 0;
     for (int k = 0; k < s->K; ++k) {
+        if (s->p->cones[k].lp) continue;   /* lorads_compute_oracle_rank: the SDP cones */
         int n = s->p->cones[k].n, r = s->rank[k];
         double *gram = calloc((long)r * r, 8);
         const double *X = s->R + s->off[k], *U = s->U + s->off[k], *V = s->V + s->off[k];
@@ -812,7 +867,11 @@ static int oracle_rank(osolver *s, int phase) {
     return tot;
 }
 
-static int sum_rank(osolver *s) { int t = 0; for (int k = 0; k < s->K; ++k) t += s->rank[k]; return t; }
+static int sum_rank(osolver *s) {
+    int t = 0;
+    for (int k = 0; k < s->K; ++k) t += s->p->cones[k].lp ? 0 : s->rank[k];
+    return t;
+}
 
 static void append_traj(osolver *s, int phase, int cur, int orc) {
     int **cv = phase == 1 ? &s->traj1_cur : &s->traj2_cur, **ov = phase == 1 ? &s->traj1_orc : &s->traj2_orc;
@@ -831,10 +890,11 @@ static void record_state(osolver *s, int phase) {   /* ALMRecordState / ADMMReco
 static int check_all_rank_max(osolver *s, double f) {
     int cnt = 0;
     for (int k = 0; k < s->K; ++k) {
+        if (s->p->cones[k].lp) continue;
         int nr = (int)OMIN(ceil(s->rank[k] * f), (double)s->p->cones[k].rank_max);
         if (nr >= s->p->cones[k].rank_max) cnt++;
     }
-    return cnt == s->K;
+    return cnt == n_sdp(s);
 }
 
 static double *grow_cols(const double *old, long off_old_k, int n, int r_old, int r_new, long NR_new,
@@ -1131,14 +1191,59 @@ static void refresh_cone_constr(osolver *s, int k) {
     for (int i = 0; i < s->m; ++i) s->cvs[i] += cv[i];
 }
 
-/* LORADSUpdateSDPVar, lorads_alg_common.c:298-326 */
+/* the LP block's loop of LORADSUpdateSDPLPVar (lorads_alg_common.c:352-372): per column j in
+   order, LORADSUpdateLPVarOne (lorads_admm.c:759-792) for u_j with v_j fixed, the constraint
+   sums refreshed (constrValLP add / recompute / add), then v_j with u_j fixed */
+static void lp_update_var(osolver *s, int k, double rho) {
+    ocone *c = &s->p->cones[k];
+    double *u = s->U + s->off[k], *v = s->V + s->off[k], *cv = s->cvc + (long)k * s->m;
+    const double *b = s->p->b;
+    for (int j = 0; j < c->n; ++j) {
+        for (int side = 0; side < 2; ++side) {
+            double uv = u[j] * v[j];
+            double w = 0.0;
+            w += c->lp_c[j];
+            for (int e = c->lp_ptr[j]; e < c->lp_ptr[j + 1]; ++e) {
+                int i = c->lp_con[e];
+                double a = c->lp_a[e];
+                double m1 = -b[i];
+                m1 = m1 + s->cvs[i];
+                m1 = m1 + (-1.0) * (uv * a);
+                m1 = m1 * rho;
+                m1 = m1 + (-1.0) * s->lam[i];
+                w += a * m1;
+            }
+            double y = side == 0 ? v[j] : u[j];
+            double M2 = w * y;
+            M2 = M2 - rho * y;
+            double x = (-1.0 * M2 / rho) / (1 + c->lp_nrm2[j] * y * y);
+            if (side == 0) u[j] = x; else v[j] = x;
+            double uvn = u[j] * v[j];
+            for (int e = c->lp_ptr[j]; e < c->lp_ptr[j + 1]; ++e) {
+                int i = c->lp_con[e];
+                s->cvs[i] += (-1.0) * (uv * c->lp_a[e]);
+                cv[i] += (-1.0) * (uv * c->lp_a[e]);
+            }
+            for (int e = c->lp_ptr[j]; e < c->lp_ptr[j + 1]; ++e) {
+                int i = c->lp_con[e];
+                s->cvs[i] += 1.0 * (uvn * c->lp_a[e]);
+                cv[i] += 1.0 * (uvn * c->lp_a[e]);
+            }
+        }
+    }
+}
+
+/* LORADSUpdateSDPVar, lorads_alg_common.c:298-326 (+ the LP block's loop after the cones) */
 static void admm_update_var(osolver *s, double rho, double tol, int maxit) {
     for (int k = 0; k < s->K; ++k) {
+        if (s->p->cones[k].lp) continue;
         update_var_one(s, k, s->U + s->off[k], s->V + s->off[k], rho, tol, maxit);
         refresh_cone_constr(s, k);
         update_var_one(s, k, s->V + s->off[k], s->U + s->off[k], rho, tol, maxit);
         refresh_cone_constr(s, k);
     }
+    for (int k = 0; k < s->K; ++k)
+        if (s->p->cones[k].lp) lp_update_var(s, k, rho);
 }
 
 static void average_uv(osolver *s) {   /* averageUV, lorads_admm.c:372-377 */
@@ -1274,7 +1379,11 @@ int oracle_solve(const char *path, int nflags, char **flags, double *res) {
     osolver *s = osolver_new(p, &prm);
     ostate alm = {0}, admm = {0};
     double rho = prm.initRho;
-    if (rho == 0) { long sd = 0; for (int k = 0; k < s->K; ++k) sd += p->cones[k].n; rho = 1 / sqrt((double)sd); }
+    if (rho == 0) {   /* initial_solver_state, data/lorads_solver.c:1599-1606: the SDP blocks */
+        long sd = 0;
+        for (int k = 0; k < s->K; ++k) sd += p->cones[k].lp ? 0 : p->cones[k].n;
+        rho = 1 / sqrt((double)sd);
+    }
     alm.rho = rho; admm.rho = rho;
     alm.pobj = alm.dobj = alm.pinf1 = alm.pinfinf = 1e30; alm.gap = 0.0;
     admm.pobj = admm.dobj = admm.pinf1 = admm.pinfinf = admm.gap = 1e30;
@@ -1323,7 +1432,7 @@ long oracle_alm_rate(const char *path, int rank, double seconds, double *elapsed
     osolver *s = osolver_new(p, &prm);
     ostate alm = {0};
     long sd = 0;
-    for (int k = 0; k < s->K; ++k) sd += p->cones[k].n;
+    for (int k = 0; k < s->K; ++k) sd += p->cones[k].lp ? 0 : p->cones[k].n;
     alm.rho = 1 / sqrt((double)sd);
     alm.pobj = alm.dobj = alm.pinf1 = alm.pinfinf = 1e30;
     double t0 = o_now();
@@ -1349,7 +1458,7 @@ long oracle_alm_steps(const char *path, int rank, long K, double *out, long cap)
     osolver *s = osolver_new(p, &prm);
     ostate alm = {0};
     long sd = 0;
-    for (int k = 0; k < s->K; ++k) sd += p->cones[k].n;
+    for (int k = 0; k < s->K; ++k) sd += p->cones[k].lp ? 0 : p->cones[k].n;
     alm.rho = 1 / sqrt((double)sd);
     alm.pobj = alm.dobj = alm.pinf1 = alm.pinfinf = 1e30;
     alm_optimize(s, &alm, o_now(), K);
@@ -1468,6 +1577,34 @@ int oracle_admm_sweep(oproblem *p, int rank, const double *in, double *out) {
     memcpy(op, s->lam, 8 * m); op += m;
     *op++ = (double)s->cgIter;
     for (int k = 0; k < s->K; ++k) *op++ = (double)s->cgIterCone[k];
+    osolver_free(s);
+    return (int)(op - out);
+}
+
+/* oracle/ref_harness.c admm_sweep_lp's layout: in = U, V (the LP block after the SDP cones),
+ * lambda[m], rho_admm, cg_tol; out = U, V, constrValSum, lambda (after the dual update), total
+ * CG iterations.  LORADSUpdateSDPLPVar + LORADSUpdateDualVar. */
+int oracle_admm_sweep_lp(oproblem *p, int rank, const double *in, double *out) {
+    oparams prm;
+    default_oparams(&prm);
+    prm.fixedRank = rank;
+    osolver *s = osolver_new(p, &prm);
+    long NR = s->NR;
+    int m = s->m;
+    memcpy(s->U, in, 8 * NR); memcpy(s->V, in + NR, 8 * NR);
+    memcpy(s->lam, in + 2 * NR, 8 * m);
+    const double rho = in[2 * NR + m], cg_tol = in[2 * NR + m + 1];
+    constr_val_all(s, s->U, s->V);
+    s->cgIter = 0;
+    admm_update_var(s, rho, cg_tol, 800);
+    for (int i = 0; i < m; ++i) s->lam[i] += rho * s->p->b[i];
+    for (int i = 0; i < m; ++i) s->lam[i] += -rho * s->cvs[i];
+    double *op = out;
+    memcpy(op, s->U, 8 * NR); op += NR;
+    memcpy(op, s->V, 8 * NR); op += NR;
+    memcpy(op, s->cvs, 8 * m); op += m;
+    memcpy(op, s->lam, 8 * m); op += m;
+    *op++ = (double)s->cgIter;
     osolver_free(s);
     return (int)(op - out);
 }

@@ -29,6 +29,10 @@ int oracle_kernels(oproblem *p, int rank, const double *in, double *out);
 /* LORADSUpdateSDPVar over every cone + LORADSUpdateDualVar on the same input layout; out = U,
  * V, A(UV^T), lambda, total CG iterations, per cone its last CG count (returns the length) */
 int oracle_admm_sweep(oproblem *p, int rank, const double *in, double *out);
+/* The same with the LP block (the last cone, rank 1): the SDP cones' CG half-steps, then the LP
+ * column sweep; out = U, V, A(UV^T), lambda, total CG iterations (oracle/ref_harness.c
+ * admm_sweep_lp's layout; returns the length) */
+int oracle_admm_sweep_lp(oproblem *p, int rank, const double *in, double *out);
 
 /* Full solve with LoRADS flags (argv-style, e.g. {"--reoptLevel","0"}).
  * res[0..15] = alm_inner, alm_outer, alm_pobj, alm_dobj, alm_pinf, alm_gap, alm_rho,

@@ -54,7 +54,7 @@ def test_oracle_solve_matches_reference(oracle_lib, case):
 
 
 STEP_CASES = ["mc_rand200", "mc_torus12x10", "mc_rand300w", "theta40", "theta25x3", "rsparse60", "checker_1.5",
-              "mc_rand300w_r290"]
+              "mc_rand300w_r290", "mc_lp60"]
 PROJ = {"mc_rand300w_r290": 4}   # n x r arrays stored as n x 4 projections (make_golden_steps.py)
 
 
@@ -124,3 +124,51 @@ def test_oracle_admm_sweep_matches_reference(oracle_lib, name):
         ref = float(g["cg_last"][c])
         assert abs(cg_last[c] - ref) <= max(2, 0.25 * ref), (cg_last, g["cg_last"])
     assert abs(out[2 * NR + 2 * m] - float(g["cg_total"])) <= max(4, 0.15 * float(g["cg_total"]))
+
+
+def test_oracle_lp_sweep_matches_reference(oracle_lib):
+    """The restatement's LP block (the diagonal cone at rank 1; its ADMM update the column sweep of
+    LORADSUpdateSDPLPVar) + LORADSUpdateDualVar against the reference on the same seeded U, V,
+    lambda (tests/golden/admm_sweep_lp_mc_lp60.npz, scripts/make_golden_lp.py).  The LP block's
+    own entries are a closed-form Gauss-Seidel sweep: within 1e-9 of the reference's."""
+    import ctypes as C
+    import os
+    from golden_util import GOLDEN, instance
+    g = np.load(os.path.join(GOLDEN, "admm_sweep_lp_mc_lp60.npz"))
+    rank, m = int(g["rank"]), int(g["m"])
+    dims = [int(d) for d in g["dims"]]
+    NR = dims[0] * rank + dims[1]
+    vec = np.concatenate([g["U0"], g["V0"], g["lam0"], [float(g["rho"]), float(g["cg_tol"])]])
+    oracle_lib.oracle_admm_sweep_lp.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    p = oracle_lib.oracle_read(instance("mc_lp60").encode())
+    assert p
+    out = np.zeros(2 * NR + 2 * m + 1)
+    n = oracle_lib.oracle_admm_sweep_lp(p, rank, vec.ctypes.data_as(C.POINTER(C.c_double)),
+                                        out.ctypes.data_as(C.POINTER(C.c_double)))
+    oracle_lib.oracle_free(p)
+    assert n == out.size
+    U, V = out[:NR], out[NR:2 * NR]
+    cvs, lam = out[2 * NR:2 * NR + m], out[2 * NR + m:2 * NR + 2 * m]
+    for key, ours in (("U", U), ("V", V), ("cvs", cvs), ("lam", lam)):
+        assert rel_err(ours, g[key]) < 1e-6, (key, rel_err(ours, g[key]))
+    nsdp = dims[0] * rank
+    for key, ours in (("U", U), ("V", V)):
+        assert rel_err(ours[nsdp:], g[key][nsdp:]) < 1e-6, (key, "LP block")
+    assert abs(out[-1] - float(g["cg_total"])) <= max(4, 0.15 * float(g["cg_total"]))
+
+
+def test_oracle_lp_solve_matches_reference(oracle_lib):
+    """mc_lp60 (LP slacks, a split free variable, a dense LP column) solved whole by the
+    restatement: the reference's trajectory step for step (tests/golden/solves_lp.json)."""
+    import json
+    import os
+    from golden_util import GOLDEN
+    with open(os.path.join(GOLDEN, "solves_lp.json")) as f:
+        s = {x["instance"]: x for x in json.load(f)}["mc_lp60"]
+    o = oracle_solve(oracle_lib, s["instance"], s["flags"])
+    r = s["result"]
+    assert o["rank"] == r["rank"]   # the SDP cone's rank (the reference's rankElem)
+    assert abs(o["alm_inner"] - r["alm_inner"]) <= 2
+    assert abs(o["admm_iter"] - r["admm_iter"]) <= 1
+    for k in ("alm_pobj", "alm_dobj", "admm_pobj", "admm_dobj"):
+        assert abs(o[k] - r[k]) <= 1e-6 * max(1.0, abs(r[k])), k
