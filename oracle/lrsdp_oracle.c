@@ -12,7 +12,10 @@
  * (data/lorads_sdp_conic.c:1201-1280) simply has the full packed lower triangle
  * as its pattern, which is the same arithmetic as the reference's
  * dsyr2k/dsymm/packed-dot formulation (lorads_alg_common.c:72-89,
- * data/lorads_sdp_data.c:948-1034) up to summation order.
+ * data/lorads_sdp_data.c:948-1034) up to summation order.  An LP block (the SDPA
+ * block of negative size, data/lorads_lp_conic.c) is the last cone, diagonal, at
+ * rank 1 (x_j = r_j^2) -- the product's layout -- and its ADMM update is the
+ * reference's column sweep (lp_update_var).
  *
  * Parity pin: tests/test_oracle_golden.py checks this file against fixtures
  * written by the reference itself (oracle/_ref, scripts/make_golden.py).

@@ -95,7 +95,8 @@ def read_sdpa_dense(path):
     """Test-side SDPA reader (the contract of LReadSDPA, io/lorads_file_io.c:59-455: '*' / '"'
     comment lines, '{ ( ' ,' as separators, C = -F0, A_i = F_i, |v| < 1e-12 dropped, entries
     symmetric).  Returns m, block dims, b, dense C per block, A as {(i, blk): [(r, c, v)]}.
-    LP blocks (negative dims) are not supported (as the device reader)."""
+    LP blocks (negative dims) are not supported by this test-side reader (the device and oracle
+    readers take them; tests/test_gpu_lp.py has its own LP-block reader)."""
     toks = []
     with open(path) as f:
         for line in f:
