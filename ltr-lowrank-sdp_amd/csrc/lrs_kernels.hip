@@ -126,6 +126,16 @@ __device__ __forceinline__ double dpp_mov(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// A copy of x the compiler cannot prove equal to x.  k_bw_b meets the diagonal entry with the
+// row's own registers where k_it_b loads the row again; a dot of a row with itself is then known
+// non-negative, which lets the compiler fold the "0 +" of the sum and fuse the other product (one
+// ulp off on a diagonal slot's value, seen on a restructured stage-A kernel; profiles/r06j).
+// Opaque, the operand compiles as k_it_b's does: bitwise the same results.
+__device__ __forceinline__ double opaque(double x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // Sum over an aligned group of G lanes; every lane of the group gets the same value.
 template <int G>
 __device__ __forceinline__ double group_sum(double v) {
@@ -169,6 +179,18 @@ __device__ __forceinline__ double read_lane(double v, int l) {
     const int lo = __builtin_amdgcn_readlane((int)b, l);
     const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Value of lane u of this lane's aligned group of G lanes (u group-uniform)
+template <int G>
+__device__ __forceinline__ int bcast_i(int v, int u) {
+    if constexpr (G == 64) return __builtin_amdgcn_readlane(v, u);
+    else return __shfl(v, (int)(threadIdx.x & 63 & ~(G - 1)) + u, 64);
+}
+template <int G>
+__device__ __forceinline__ double bcast_d(double v, int u) {
+    if constexpr (G == 64) return read_lane(v, u);
+    else return __shfl(v, (int)(threadIdx.x & 63 & ~(G - 1)) + u, 64);
 }
 
 // Wave (64-lane) sum, wave-uniform result: DPP within rows of 16, then the four
@@ -1976,8 +1998,17 @@ __global__ void __launch_bounds__(kBlock) k_pack_shared(int m, const int *__rest
 #ifndef LRS_BW_UB_MINB
 #define LRS_BW_UB_MINB 3
 #endif
+// Occupancy bound of k_it_b (the launch bound's second argument): the fused bandwidth-regime
+// kernel (U == 1, MODE 0) holds the row's R, D, gradient and the L-BFGS operands at once and
+// spilled 8-15 VGPRs at 6 / 5 waves a SIMD (44 B a lane of scratch at G81 r = 64: ~20 MB of
+// extra writes per launch, profiles/r06a_g81_summary.md); one wave a SIMD less keeps it in
+// registers.  E = 8 (r > 256) needs the whole file.
+constexpr int itb_min_blocks(int E, int U, int MODE) {
+    return U == 1 ? (E >= 8 ? 2 : MODE == 0 ? (E >= 3 ? 4 : 5) : (E >= 3 ? 5 : 6))
+                  : (MODE == 0 && U == LRS_BW_UB ? LRS_BW_UB_MINB : 1);
+}
 template <int G, int E, int U, int MODE>
-__global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : (MODE == 0 && U == LRS_BW_UB ? LRS_BW_UB_MINB : 1))) k_it_b(
+__global__ void __launch_bounds__(kRowBlock, itb_min_blocks(E, U, MODE)) k_it_b(
     int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
     const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
     const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0, double *s1, double *y1,
@@ -2247,6 +2278,312 @@ __global__ void __launch_bounds__(kRowBlock, (U == 1 ? (E >= 3 ? 5 : 6) : (MODE 
     if (blockIdx.x == 0 && threadIdx.x == 0)
         for (int q_ = 5; q_ < 12; ++q_) g_phase[2][q_] = g_phase_tmp[2][q_];
 #endif
+    LRS_BLK_END(2);
+}
+
+// ------------------------------------------------------------------------
+// B, bandwidth regime, plain rows (T == 1): the fused stage of k_it_b<., ., 1, 0> restructured
+// around its dependency chain.  k_it_b walks a row's entries one after another, each entry three
+// dependent memory trips deep (adjacency -> R_j, D_j and the slot record -> the constraint
+// record) plus two more on lower entries (the local constraints after the dot product): about
+// 20 trips a row on G81, where every lane group holds one or two rows and the launch is latency-
+// bound (32 us for 96 MB, 0.37 of HBM).  Here a row takes four trips, as in k_lat_b's row
+// waves: (1) the row header and own operands, (2) the first NO + 1 entries' columns and slots,
+// (3) their factor rows and, lane-distributed (lane u of the group: entry u, lane NO: the
+// diagonal), each entry's slot, objective and local-constraint records, (4) the constraint
+// records and b.  Lane u finishes entry u's S value (its multi-constraint slot list too); the
+// entries are then summed in k_it_b's adjacency order and their slots finished by lane 0 with
+// the records broadcast from their lanes -- the same arithmetic in the same order, bitwise
+// k_it_b's results (tests/test_gpu_bw_kernels.py).  The further entries of a long row take
+// k_it_b's walk.  (The first row's trips issued before the block's line search, as k_lat_b's
+// row waves do beside its control wave, kept ~100 VGPRs live through the line search: 148-440 B
+// a lane of spills.)
+// ------------------------------------------------------------------------
+constexpr int kBwNo = 4;   // off-diagonal entries prefetched per row (torus rows: all of them)
+template <int G, int E, int NO>
+struct BwRow {
+    int i, kb, kl, ke, no, sd;
+    bool dg;
+    double ri[E], di[E];
+    int ss[NO];
+    bool lw[NO];
+    double rjp[NO][E], djp[NO][E];
+    // this lane's entry (lane u < NO: off-diagonal entry u; lane NO: the diagonal)
+    int msl;
+    double msv, mbq;
+    double2 ms1, ml1, mra, mrb;
+};
+
+template <int G, int E, int NO>
+__device__ __forceinline__ void bw_prefetch(BwRow<G, E, NO> &w, int i, int ld, int lane, int m,
+                                            const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
+                                            const int *__restrict__ adj_col, const int *__restrict__ adj_slot,
+                                            const double *__restrict__ R, const double *__restrict__ D,
+                                            const double *__restrict__ Craw, const double2 *__restrict__ slot1,
+                                            const double2 *__restrict__ loc1, const double *__restrict__ rec,
+                                            const double *__restrict__ b) {
+    w.i = i;
+    const long oi = (long)i * ld + lane * E;
+    w.kb = adj_ptr[i];
+    w.kl = adj_low[i];
+    w.ke = adj_ptr[i + 1];
+    ld_row<E>(R + oi, w.ri);
+    ld_row<E>(D + oi, w.di);
+    const int nt = w.ke - w.kb;
+    const int kd = (nt > 0 && w.kl > w.kb) ? w.kl - 1 : w.kb;   // the diagonal is the last lower entry
+    const int kdc = nt > 0 ? kd : 0;
+    const int jd = adj_col[kdc];
+    w.sd = adj_slot[kdc];
+    int ja[NO + 1], sa[NO + 1];
+#pragma unroll
+    for (int u = 0; u <= NO; ++u) {
+        const int k = nt > 0 ? w.kb + min(u, nt - 1) : 0;
+        ja[u] = adj_col[k];
+        sa[u] = adj_slot[k];
+    }
+    w.dg = nt > 0 && w.kl > w.kb && jd == i;
+    w.no = nt - (w.dg ? 1 : 0);
+    const int pd = w.dg ? w.kl - 1 - w.kb : NO + 1;   // the diagonal's position among the first
+    int my = w.sd;
+#pragma unroll
+    for (int u = 0; u < NO; ++u) {
+        const bool past = u >= pd;
+        const int j = past ? ja[u + 1] : ja[u];
+        w.ss[u] = past ? sa[u + 1] : sa[u];
+        w.lw[u] = w.kb + u + (past ? 1 : 0) < w.kl;
+        const long oj = (long)(u < w.no ? j : i) * ld + lane * E;
+        ld_row<E>(R + oj, w.rjp[u]);
+        ld_row<E>(D + oj, w.djp[u]);
+        if (lane == u) my = w.ss[u];
+    }
+    w.msl = my;
+    w.msv = Craw[my];
+    w.ms1 = slot1[my];
+    w.ml1 = loc1[my];
+    // slots without a single constraint read the row's own (spread, cached) index instead of a
+    // common one (k_lat_b)
+    const int ispare = min(i, m - 1);
+    const int c1 = (int)w.ms1.y >= 0 ? (int)w.ms1.y : ispare;
+    const int cl = (int)w.ml1.y >= 0 ? (int)w.ml1.y : ispare;
+    const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * c1);
+    w.mra = r[0];
+    w.mrb = r[1];
+    w.mbq = b[cl];
+}
+
+// occupancy bound: the row state without spills (E <= 2: 128 VGPRs, E = 3: 168, above: 256)
+constexpr int bwb_min_blocks(int E) { return E <= 2 ? 4 : (E == 3 ? 3 : 2); }
+template <int G, int E, int NO>
+__global__ void __launch_bounds__(kRowBlock, bwb_min_blocks(E)) k_bw_b(
+    int n, int ld, long foff, const int *__restrict__ adj_ptr, const int *__restrict__ adj_low,
+    const int *__restrict__ adj_col, const int *__restrict__ adj_slot, double *Rb0, double *Rb1,
+    const double *__restrict__ Dall, double *G0, double *G1, double *s0, double *y0, double *s1, double *y1,
+    double *__restrict__ uRR, const double *__restrict__ Craw, const int *__restrict__ slot_ptr,
+    const int *__restrict__ slot_con, const double *__restrict__ slot_a, const double2 *__restrict__ slot1,
+    const double *__restrict__ rec, const int *__restrict__ loc_ptr, const int *__restrict__ loc_con,
+    const double *__restrict__ loc_w, const double2 *__restrict__ loc1, const double *__restrict__ b,
+    double *__restrict__ cvs, const double *__restrict__ par, const double *__restrict__ ctrl,
+    const double *__restrict__ partA, int nblkA, const double *__restrict__ partB, int nblkB,
+    double *__restrict__ ls_cur, int L, double *__restrict__ partC, int pblk_off, int row0, int m, int pstr,
+    double *hmirror, double seq, double *CRb, const double *__restrict__ CDb) {
+    static_assert(NO < G, "lane NO holds the diagonal's records");
+    __shared__ double red[12];
+    __shared__ double ls[LS_N];
+    LRS_TS(2, 0);
+    LRS_BLK_BEGIN();
+    mirror_ctrl(ctrl, hmirror, seq);
+    if (ctrl[C_ACT2] == 0.0) return;
+    const int gcur = (int)ctrl[C_GCUR], h = (int)ctrl[C_HEAD];
+    const bool r1 = ctrl[C_RCUR] != 0.0;
+    const double *__restrict__ R = (r1 ? Rb1 : Rb0) + foff;
+    double *__restrict__ Rn = (r1 ? Rb0 : Rb1) + foff;
+    const double *__restrict__ D = Dall + foff;
+    double *__restrict__ Gold = (gcur == 0 ? G0 : G1) + foff;
+    double *__restrict__ Gnew = (gcur == 0 ? G1 : G0) + foff;
+    double *__restrict__ sh = (h == 0 ? s0 : s1) + foff;
+    double *__restrict__ yh = (h == 0 ? y0 : y1) + foff;
+    const double *__restrict__ so = (h == 0 ? s1 : s0) + foff;
+    const double *__restrict__ yo = (h == 0 ? y1 : y0) + foff;
+    const bool two = (L == 2);
+    const int lane = threadIdx.x & (G - 1);
+    const RowRange rr = row_range(n, kRowBlock / G, (int)threadIdx.x / G);
+    // the line search from stage A's (and G's) partials, every block (k_it_b MODE 0)
+    reduce_partials<7, kRowBlock>(partA, nblkA, red, pstr);
+    if (nblkB > 0) {
+        reduce_partials<5, kRowBlock>(partB, nblkB, red + 7, pstr);
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) red[2 + q] += red[7 + q];
+        }
+        __syncthreads();
+    }
+    LRS_TS(2, 1);
+    if (threadIdx.x < 64) line_search_t<true>(par, red[0], red[1], red + 2, ls);   // wave 0
+    __syncthreads();
+    LRS_TS(2, 2);
+    if (pblk_off == 0 && blockIdx.x == 0 && threadIdx.x < LS_N) ls_cur[threadIdx.x] = ls[threadIdx.x];
+    if (ls[LS_FLAG] != 0.0) return;
+    const double tau = ls[LS_TAU], tau2 = tau * tau, rho = par[P_RHO];
+    // acc: GG, ys, yy, sG, yG, soG, yoG, soy, yoy, residual
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int ib = rr.first; ib < rr.end; ib += rr.stride) {
+        BwRow<G, E, NO> w;
+        bw_prefetch<G, E, NO>(w, row0 + ib, ld, lane, m, adj_ptr, adj_low, adj_col, adj_slot, R, D, Craw, slot1, loc1,
+                              rec, b);
+        const int i = w.i;
+        const long oi = (long)i * ld + lane * E;
+        double go[E], sov[E], yov[E];
+        ld_row<E>(Gold + oi, go);
+        if (two) { ld_row<E>(so + oi, sov); ld_row<E>(yo + oi, yov); }
+        double ri[E], g[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) { ri[e] = w.ri[e] + tau * w.di[e]; g[e] = 0.0; }
+        st_row<E>(Rn + oi, ri);
+        // this lane's entry: S = C + A^*(M1) on its slot (ALMSetGrad lorads_alm.c:38-57)
+        double msv = w.msv;
+        {
+            const int c1 = (int)w.ms1.y;
+            const int e0 = c1 == -2 ? slot_ptr[w.msl] : 0;
+            const int e1 = c1 == -2 ? slot_ptr[w.msl + 1] : (c1 >= 0 ? 1 : 0);
+            for (int e = e0; e < e1; ++e) {
+                double2 x = w.mra, y = w.mrb;
+                if (c1 < 0) {
+                    const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * slot_con[e]);
+                    x = r[0];
+                    y = r[1];
+                }
+                double cv = x.x + tau * x.y;
+                cv = cv + tau2 * y.x;
+                const double M1 = y.y + rho * cv;
+                msv += M1 * (c1 >= 0 ? w.ms1.x : slot_a[e]);
+            }
+        }
+        // k_it_b's order (and its lane-0 code for the slots): every entry in adjacency order, the
+        // diagonal at its place (the last lower entry); positions [0, win) from the prefetch --
+        // the first NO off-diagonal entries and a diagonal among them -- the rest walked
+        const int nt = w.ke - w.kb;
+        const int pd = w.dg ? w.kl - 1 - w.kb : (1 << 30);
+        const int win = min(nt, pd <= NO ? NO + 1 : NO);
+        auto lower_slot = [&](int sl, double d, double wx, int cl, double bq) {
+            uRR[sl] = d;
+            const int f0 = cl == -2 ? loc_ptr[sl] : 0;
+            const int f1 = cl == -2 ? loc_ptr[sl + 1] : (cl >= 0 ? 1 : 0);
+            for (int e = f0; e < f1; ++e) {
+                const int ci = cl >= 0 ? cl : loc_con[e];
+                const double tot = (cl >= 0 ? wx : loc_w[e]) * d;
+                cvs[ci] = tot;
+                const double dd = (cl >= 0 ? bq : b[ci]) - tot;
+                acc[9] += dd * dd;
+            }
+        };
+#pragma unroll
+        for (int p = 0; p <= NO; ++p) {
+            if (p < win) {
+                const bool isd = p == pd, past = p > pd;
+                double rj[E];
+                if (isd) {   // R_new of the row itself as k_it_b sees it: a second copy
+#pragma unroll
+                    for (int e = 0; e < E; ++e) rj[e] = opaque(ri[e]);
+                } else {
+                    const int ua = p < NO ? p : NO - 1, ub = p > 0 ? p - 1 : 0;
+#pragma unroll
+                    for (int e = 0; e < E; ++e)
+                        rj[e] = (past ? w.rjp[ub][e] : w.rjp[ua][e]) + tau * (past ? w.djp[ub][e] : w.djp[ua][e]);
+                }
+                const int o = isd ? NO : (past ? p - 1 : p);   // the lane holding this entry's records
+                const double su = bcast_d<G>(msv, o);
+#pragma unroll
+                for (int e = 0; e < E; ++e) g[e] += su * rj[e];
+                if (w.kb + p < w.kl) {   // lower entry (j <= i): A(RR^T) slot owned by this row
+                    double d = 0.0;
+#pragma unroll
+                    for (int e = 0; e < E; ++e) d += ri[e] * rj[e];
+                    d = group_sum<G>(d);
+                    const int sl = bcast_i<G>(w.msl, o);
+                    const double wx = bcast_d<G>(w.ml1.x, o), wy = bcast_d<G>(w.ml1.y, o), bq = bcast_d<G>(w.mbq, o);
+                    if (lane == 0) lower_slot(sl, d, wx, (int)wy, bq);
+                }
+            }
+        }
+        // the rest of a long row (the diagonal among them when it lies past the window): k_it_b's walk
+        for (int k = w.kb + win; k < w.ke; ++k) {
+            const int j = adj_col[k], sl = adj_slot[k];
+            const long oj = (long)j * ld + lane * E;
+            double rj[E], dj[E];
+            ld_row<E>(R + oj, rj);
+            ld_row<E>(D + oj, dj);
+#pragma unroll
+            for (int e = 0; e < E; ++e) rj[e] += tau * dj[e];
+            const double2 s1u = slot1[sl];
+            const int c1 = (int)s1u.y;
+            double sv = Craw[sl];
+            const int e0 = c1 == -2 ? slot_ptr[sl] : 0;
+            const int e1 = c1 == -2 ? slot_ptr[sl + 1] : (c1 >= 0 ? 1 : 0);
+            for (int e = e0; e < e1; ++e) {
+                const int con = c1 >= 0 ? c1 : slot_con[e];
+                const double2 *r = reinterpret_cast<const double2 *>(rec + 4L * con);
+                const double2 ra = r[0], rb = r[1];
+                double cv = ra.x + tau * ra.y;
+                cv = cv + tau2 * rb.x;
+                const double M1 = rb.y + rho * cv;
+                sv += M1 * (c1 >= 0 ? s1u.x : slot_a[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) g[e] += sv * rj[e];
+            if (k < w.kl) {
+                double d = 0.0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) d += ri[e] * rj[e];
+                d = group_sum<G>(d);
+                if (lane == 0) {
+                    const double2 l1u = loc1[sl];
+                    const int cl = (int)l1u.y;
+                    lower_slot(sl, d, l1u.x, cl, cl >= 0 ? b[cl] : 0.0);
+                }
+            }
+        }
+        // gradient G_new = 2 S R_new, L-BFGS pair s = tau D, y = G_new - G_old, dots
+        if (CRb) {
+            // dense objective: C R_new = C R + tau C D (carried), S R_new += C R_new
+            double cr[E], cd[E];
+            ld_row<E>(CRb + foff + oi, cr);
+            ld_row<E>(CDb + foff + oi, cd);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                cr[e] += tau * cd[e];
+                g[e] += cr[e];
+            }
+            st_row<E>(CRb + foff + oi, cr);
+        }
+        double sv2[E], yv[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) g[e] *= 2.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { sv2[e] = tau * w.di[e]; yv[e] = g[e] - go[e]; }
+        st_row<E>(Gnew + oi, g);
+        st_row<E>(sh + oi, sv2);
+        st_row<E>(yh + oi, yv);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            acc[0] += g[e] * g[e];
+            acc[1] += yv[e] * sv2[e];
+            acc[2] += yv[e] * yv[e];
+            acc[3] += sv2[e] * g[e];
+            acc[4] += yv[e] * g[e];
+        }
+        if (two) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                acc[5] += sov[e] * g[e];
+                acc[6] += yov[e] * g[e];
+                acc[7] += sov[e] * yv[e];
+                acc[8] += yov[e] * yv[e];
+            }
+        }
+    }
+    LRS_TS(2, 3);
+    write_partials<10, kRowBlock>(acc, partC, pblk_off + blockIdx.x);
+    LRS_TS_END(2, 4);
     LRS_BLK_END(2);
 }
 
@@ -3037,16 +3374,6 @@ __global__ void __launch_bounds__(kRowBlock) k_lat_f(
 // of three per entry) -- then the entries' factor rows U at a time, the column broadcast
 // from the lane that fetched it, which also stores the entry's results.
 // ------------------------------------------------------------------------
-template <int G>
-__device__ __forceinline__ int bcast_i(int v, int u) {
-    if constexpr (G == 64) return __builtin_amdgcn_readlane(v, u);
-    else return __shfl(v, (int)(threadIdx.x & 63 & ~(G - 1)) + u, 64);
-}
-template <int G>
-__device__ __forceinline__ double bcast_d(double v, int u) {
-    if constexpr (G == 64) return read_lane(v, u);
-    else return __shfl(v, (int)(threadIdx.x & 63 & ~(G - 1)) + u, 64);
-}
 
 // Column tiles (TL): the random long-row pattern (C5) reads ~10^3 neighbour rows per row from
 // anywhere in the factor, and a 10 MB factor does not fit one XCD's 4 MB L2, so nearly every
@@ -5219,9 +5546,28 @@ static int res_a() {
     static int c = 0;
     return resident_blocks(k_it_a<GG, EE, UU, UU == 1 ? 2 : 0>, &c);
 }
+// k_bw_b (the bandwidth regime's fused stage B on plain rows); LRS_BW_B=0: k_it_b<., ., 1, 0>
+static bool bw_b_on() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("LRS_BW_B");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v != 0;
+}
 template <int GG, int EE, int UU>
-static int res_b() {
+static int res_b(bool fused = false) {
     static int c = 0;
+    if constexpr (UU == 1) {
+        // the bandwidth regime's grid: a fused stage B (one launch, not sharded) runs k_bw_b or
+        // k_it_b MODE 0, a split one k_it_b MODE 1 / 2 (or the long-row kernels); the fused
+        // kernels' smaller residency, so that no block waits for a second round
+        static int c0 = 0, c1 = 0;
+        const int r = resident_blocks(k_it_b<GG, EE, 1, 2>, &c);
+        if (!fused) return r;
+        const int r0 = std::min(r, resident_blocks(k_it_b<GG, EE, LRS_BW_UB, 0>, &c0));
+        return bw_b_on() ? std::min(r0, resident_blocks(k_bw_b<GG, EE, kBwNo>, &c1)) : r0;
+    }
     return resident_blocks(k_it_b<GG, EE, UU, (UU == 1 ? 2 : 0)>, &c);
 }
 
@@ -5283,10 +5629,13 @@ static int plan_a(const DevCone &c, int K, StagePlan &p, int force) {
     p.wide = !p.small && (deg / T >= 32.0 || force == 3) && c.E <= 2;
     return 0;
 }
-static int plan_b(const DevCone &c, int K, StagePlan &p, int force) {
+static int plan_b(const DevCone &c, int K, StagePlan &p, int force, bool fused) {
     const double deg = c.nown > 0 ? (double)c.adj_nnz / c.nown : 0.0;
     const int T = team_size(c, deg, 4);
-    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_b<GG, EE, 4>(), res_b<GG, EE, 1>(), K, T, force); });
+    const bool wide_rows = (deg / T >= 64.0 || force == 3) && c.E <= 2;   // p.wide below, but for the grid
+    LRS_LAYOUT_SWITCH(c.G, c.E, {
+        p = plan_stage((long)c.nown * c.G, res_b<GG, EE, 4>(), res_b<GG, EE, 1>(fused && !wide_rows), K, T, force);
+    });
     p.wide = !p.small && (deg / T >= 64.0 || force == 3) && c.E <= 2;
     return 0;
 }
@@ -5389,7 +5738,7 @@ static bool b_fused_on() {
 bool alm_stage_b_split(const DevProblem &P) {
     for (int k = 0; k < P.K; ++k) {
         StagePlan pb;
-        if (plan_b(P.cones[k], P.K, pb, multi_path(P))) return false;
+        if (plan_b(P.cones[k], P.K, pb, multi_path(P), !P.shard && b_fused_on())) return false;
         if (!pb.small && (pb.wide || P.shard || !b_fused_on())) return true;
     }
     return false;
@@ -5482,7 +5831,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     int nblkA = 0, nblkB = 0;
     bool split = sh != nullptr;   // stage A as two launches (bandwidth regime; always when sharded)
     for (int k = 0; k < KL; ++k) {
-        if (plan_a(cone_of(k), KL, pa[k], multi_path(P)) || plan_b(cone_of(k), KL, pb[k], multi_path(P))) return -1;
+        if (plan_a(cone_of(k), KL, pa[k], multi_path(P)) ||
+            plan_b(cone_of(k), KL, pb[k], multi_path(P), !sh && b_fused_on()))
+            return -1;
         nblkA += pa[k].grid;
         nblkB += pb[k].grid;
         if (!pa[k].small) split = true;
@@ -5732,6 +6083,15 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
                 if (small) LRS_LAUNCH_B(4, 0);
+                else if (bfused(pb[k], tbt[k]) && pb[k].T == 1 && bw_b_on())
+                    hipLaunchKernelGGL((k_bw_b<GG, EE, kBwNo>), dim3(grid), dim3(kRowBlock), 0, st, c.nown, c.ld, c.foff,
+                                       c.adj_ptr, c.adj_low, c.adj_col, c.adj_slot, W.R, W.R2, W.D, W.G[0], W.G[1],
+                                       W.ls[0], W.ly[0], W.ls[1], W.ly[1], W.uvt2, P.Craw, P.slot_ptr, P.slot_con,
+                                       P.slot_a, reinterpret_cast<const double2 *>(P.slot1), W.rec, P.loc_ptr,
+                                       P.loc_con, P.loc_w, reinterpret_cast<const double2 *>(P.loc1), P.b, W.cvs,
+                                       W.par, ctrl_cur, inA, nA, sh ? totB : W.partB, P.mg > 0 ? (sh ? 1 : gg) : 0,
+                                       ls_cur, L, W.partC, off, c.row0, P.m, pstr, k == 0 ? a.hmirror : nullptr, a.seq,
+                                       P.ndense ? W.CR : nullptr, W.CD);
                 else if (bfused(pb[k], tbt[k])) LRS_LAUNCH_B(LRS_BW_UB, 0);
                 else LRS_LAUNCH_B(1, 1);
             });

@@ -113,10 +113,15 @@ def test_device_reads_quirks_like_plain(tmp_path, solver_mod, oracle_lib):
 def test_reader_errors(tmp_path, solver_mod):
     with pytest.raises(RuntimeError):
         solver_mod.Solver(str(tmp_path / "missing.dat-s"))
+    # an LP block (negative size) is taken as the last block only (io/lorads_file_io.c:104-194)
     lp = tmp_path / "lp.dat-s"
-    lp.write_text("1\n2\n2 -3\n1.0\n1 1 1 1 1.0\n1 2 1 1 1.0\n")
+    lp.write_text("1\n2\n-3 2\n1.0\n1 2 1 1 1.0\n1 1 1 1 1.0\n")
     with pytest.raises(RuntimeError, match="LP"):
         solver_mod.Solver(str(lp))
+    lp.write_text("1\n2\n2 -3\n1.0\n1 1 1 1 1.0\n1 2 1 1 1.0\n")
+    sv = solver_mod.Solver(str(lp))
+    assert sv.dims == [2, 3]
+    sv.close()
     bad = tmp_path / "bad.dat-s"
     bad.write_text("2\n1\n3\n1.0 1.0\n1 1 1 1 x\n2 1 2 2 1.0\n")
     with pytest.raises(RuntimeError, match="bad entry line"):
