@@ -82,12 +82,28 @@ def attach_traffic(res, leg):
     if prof is None:
         return res
     st = prof["_stages"]
+    # the kernels the profile saw per stage (which row kernel family ran: e.g. k_bw_b for the
+    # bandwidth regime's fused stage B on plain rows, k_it_b on team rows)
+    ran = {}
+    for name, v in prof.items():
+        if not name.startswith("_") and isinstance(v, dict) and "stage" in v:
+            short = name.split("::")[-1].split("<")[0]
+            if short not in ran.setdefault(v["stage"], []):
+                ran[v["stage"]].append(short)
     for o in res["stages"]:
         s = st.get(o["stage"][0])
         if s:
             o["traffic"] = s["traffic_bytes"]
             o["rocprof_us"] = s["rocprof_us"]
             o["rocprof_frac"] = s["frac_rocprof"]
+        ks = ran.get(o["stage"][0])
+        if ks:
+            label = " + ".join(ks)
+            old_stage = o["stage"]
+            o["stage"] = old_stage.replace(o["kernel"], label, 1)
+            if res["kernel"] == old_stage:
+                res["kernel"] = o["stage"]
+            o["kernel"] = label
     if "auut" in st:
         res["a_uut"]["traffic"] = st["auut"]["traffic_bytes"]
         res["a_uut"]["rocprof_us"] = st["auut"]["rocprof_us"]
