@@ -5541,9 +5541,30 @@ static int resident_blocks(KernelT kern, int *cache, int nt = kRowBlock) {
     }
     return *cache;
 }
+// Stage A as ONE launch in the bandwidth regime (k_it_a<., ., 1, 0>: the lower neighbours' D
+// recomputed from G and the pairs instead of written by a first launch and read back by a second)
+// on plain rows (T = 1, not the long-row kernels), unsharded, while a factor is at most 32 MB:
+// the neighbours' five operand rows then come from L2 / the Infinity Cache.  G81 r = 64 (10 MB
+// factors): stage A 35.7 -> 31.6-32.2 us, 14.6K -> 15.6-15.8K it/s; the 2000^2 torus (512 MB
+// factors) 1 240 -> 1 551 us, so it stays split (profiles/r06m_stage_a_fused_ab.txt).
+// LRS_A_FUSED=0 / 1 forces it off / on (where the rows allow).
+static int a_fused_env() {
+    static int v = -2;
+    if (v == -2) {
+        const char *e = getenv("LRS_A_FUSED");
+        v = !e ? -1 : (e[0] == '1' ? 1 : 0);
+    }
+    return v;
+}
+constexpr long kAFusedMaxFactor = 32L << 20;   // bytes of one factor (n x ld doubles)
 template <int GG, int EE, int UU>
 static int res_a() {
-    static int c = 0;
+    static int c = 0, c0 = 0;
+    if constexpr (UU == 1) {
+        // the fused (MODE 0) and split second-half (MODE 2) launches share the plan's grid
+        const int r = resident_blocks(k_it_a<GG, EE, 1, 2>, &c);
+        return a_fused_env() != 0 ? std::min(r, resident_blocks(k_it_a<GG, EE, 1, 0>, &c0)) : r;
+    }
     return resident_blocks(k_it_a<GG, EE, UU, UU == 1 ? 2 : 0>, &c);
 }
 // k_bw_b (the bandwidth regime's fused stage B on plain rows); LRS_BW_B=0: k_it_b<., ., 1, 0>
@@ -5712,11 +5733,17 @@ static int lat_forced_waves() {
 static int multi_path(const DevProblem &P) { return P.no_lat == 4 ? 0 : P.no_lat; }
 
 // Whether stage A runs as two launches (bandwidth regime) for the current layouts.
+// (a_fused_env above: the rule and its measurements)
+static bool a_fused(const DevCone &c, const StagePlan &pa, bool sharded) {
+    if (sharded || pa.small || pa.wide || pa.T != 1) return false;
+    const int e = a_fused_env();
+    return e >= 0 ? e == 1 : 8L * c.nown * c.ld <= kAFusedMaxFactor;
+}
 bool alm_stage_a_split(const DevProblem &P) {
     for (int k = 0; k < P.K; ++k) {
         StagePlan pa;
         if (plan_a(P.cones[k], P.K, pa, multi_path(P))) return false;
-        if (!pa.small) return true;
+        if (!pa.small && !a_fused(P.cones[k], pa, P.shard)) return true;
     }
     return false;
 }
@@ -5836,7 +5863,7 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
             return -1;
         nblkA += pa[k].grid;
         nblkB += pb[k].grid;
-        if (!pa[k].small) split = true;
+        if (!pa[k].small && !a_fused(cone_of(k), pa[k], sh != nullptr)) split = true;
     }
     // long-row kernels in column tiles (k_wide_a / k_wide_b TL): the cone's column segments and
     // the partial-gradient buffer exist, one cone per launch, not sharded; B adds k_wide_bf's blocks
@@ -5980,8 +6007,9 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
             });
         } else {
             LRS_LAYOUT_SWITCH(c.G, c.E, {
-                if (!split) LRS_LAUNCH_A(2, 0);
-                else LRS_LAUNCH_A(1, 1);
+                if (split) LRS_LAUNCH_A(1, 1);
+                else if (pa[k].small) LRS_LAUNCH_A(2, 0);
+                else LRS_LAUNCH_A(1, 0);
             });
         }
         LRS_CHECK_LAUNCH();

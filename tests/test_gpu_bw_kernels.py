@@ -63,3 +63,19 @@ def test_bw_kernels_bitwise(tmp_path, name, K):
     assert int(new["inner"]) == int(old["inner"]) == K
     for key in ("R", "G", "cvs", "lam", "s", "y", "tau", "D"):
         assert np.array_equal(new[key], old[key]), (name, key, float(np.max(np.abs(new[key] - old[key]))))
+
+
+@pytest.mark.parametrize("name,K", [("mc_torus12x10", 12), ("mc_lp60", 8), ("rsp:400:1200:1:11", 10)])
+def test_fused_stage_a_matches_split(tmp_path, name, K):
+    """Stage A as one launch in the bandwidth regime (k_it_a MODE 0 at U = 1: the lower neighbours'
+    D recomputed from G and the pairs; the default for factors up to 32 MB) against the split
+    form (LRS_A_FUSED=0: D written by MODE 1, read back by MODE 2): the same formulas, so K trips
+    agree to rounding (the recomputed D may fuse the other of its two-product sums)."""
+    src = name if name.startswith("rsp:") else instance(name)
+    fused = run(src, K, str(tmp_path / "fused.npz"), {"LRS_A_FUSED": "1"})
+    split = run(src, K, str(tmp_path / "split.npz"), {"LRS_A_FUSED": "0"})
+    assert int(fused["inner"]) == int(split["inner"]) == K
+    for key in ("R", "G", "cvs", "lam", "s", "y", "D"):
+        a, b = fused[key], split[key]
+        err = float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+        assert err <= 1e-12, (name, key, err)
