@@ -5557,13 +5557,18 @@ static int a_fused_env() {
     return v;
 }
 constexpr long kAFusedMaxFactor = 32L << 20;   // bytes of one factor (n x ld doubles)
+static bool a_fused_rows(const DevCone &c, int T, bool wide_rows, bool sharded) {
+    if (sharded || wide_rows || T != 1) return false;
+    const int e = a_fused_env();
+    return e >= 0 ? e == 1 : 8L * c.nown * c.ld <= kAFusedMaxFactor;
+}
 template <int GG, int EE, int UU>
-static int res_a() {
+static int res_a(bool fused = false) {
     static int c = 0, c0 = 0;
     if constexpr (UU == 1) {
-        // the fused (MODE 0) and split second-half (MODE 2) launches share the plan's grid
+        // bandwidth regime: the split halves (MODE 1 / 2), or the fused launch (MODE 0)
         const int r = resident_blocks(k_it_a<GG, EE, 1, 2>, &c);
-        return a_fused_env() != 0 ? std::min(r, resident_blocks(k_it_a<GG, EE, 1, 0>, &c0)) : r;
+        return fused ? std::min(r, resident_blocks(k_it_a<GG, EE, 1, 0>, &c0)) : r;
     }
     return resident_blocks(k_it_a<GG, EE, UU, UU == 1 ? 2 : 0>, &c);
 }
@@ -5599,6 +5604,7 @@ struct StagePlan {
     int T = 1;         // lane groups per row (team)
     bool wide = false; // bandwidth regime, long rows: the neighbour half unrolled by 4 (more
                        // gathers in flight per lane group; E <= 2 keeps the registers low)
+    bool afused = false;   // bandwidth regime, stage A as one MODE 0 launch (a_fused_rows)
 };
 // Team size for rows of average degree `deg`: split a row's neighbour list over T lane
 // groups while every group still gets two unrolled chunks and the chip is not
@@ -5643,11 +5649,16 @@ static StagePlan plan_stage(long rows_threads, int res_small, int res_large, int
 }
 // force == 3 (lrs_set_kernel_path): the long-row neighbour kernels k_wide_a / k_wide_b on
 // every row the layout allows (tests run them on short rows that way)
-static int plan_a(const DevCone &c, int K, StagePlan &p, int force) {
+static int plan_a(const DevCone &c, int K, StagePlan &p, int force, bool sharded) {
     const double deg = c.nown > 0 ? (double)c.P / c.nown : 0.0;    // lower entries per row
     const int T = team_size(c, deg, 2);
-    LRS_LAYOUT_SWITCH(c.G, c.E, { p = plan_stage((long)c.nown * c.G, res_a<GG, EE, 2>(), res_a<GG, EE, 1>(), K, T, force); });
-    p.wide = !p.small && (deg / T >= 32.0 || force == 3) && c.E <= 2;
+    const bool wide_rows = (deg / T >= 32.0 || force == 3) && c.E <= 2;   // p.wide below, but for the grid
+    const bool fused = a_fused_rows(c, T, wide_rows, sharded);
+    LRS_LAYOUT_SWITCH(c.G, c.E, {
+        p = plan_stage((long)c.nown * c.G, res_a<GG, EE, 2>(), res_a<GG, EE, 1>(fused), K, T, force);
+    });
+    p.wide = !p.small && wide_rows;
+    p.afused = !p.small && fused;
     return 0;
 }
 static int plan_b(const DevCone &c, int K, StagePlan &p, int force, bool fused) {
@@ -5733,17 +5744,11 @@ static int lat_forced_waves() {
 static int multi_path(const DevProblem &P) { return P.no_lat == 4 ? 0 : P.no_lat; }
 
 // Whether stage A runs as two launches (bandwidth regime) for the current layouts.
-// (a_fused_env above: the rule and its measurements)
-static bool a_fused(const DevCone &c, const StagePlan &pa, bool sharded) {
-    if (sharded || pa.small || pa.wide || pa.T != 1) return false;
-    const int e = a_fused_env();
-    return e >= 0 ? e == 1 : 8L * c.nown * c.ld <= kAFusedMaxFactor;
-}
 bool alm_stage_a_split(const DevProblem &P) {
     for (int k = 0; k < P.K; ++k) {
         StagePlan pa;
-        if (plan_a(P.cones[k], P.K, pa, multi_path(P))) return false;
-        if (!pa.small && !a_fused(P.cones[k], pa, P.shard)) return true;
+        if (plan_a(P.cones[k], P.K, pa, multi_path(P), P.shard != nullptr)) return false;
+        if (!pa.small && !pa.afused) return true;
     }
     return false;
 }
@@ -5858,12 +5863,12 @@ int enqueue_alm_stages(const AlmIterArgs &a, int parity, int mask, hipStream_t s
     int nblkA = 0, nblkB = 0;
     bool split = sh != nullptr;   // stage A as two launches (bandwidth regime; always when sharded)
     for (int k = 0; k < KL; ++k) {
-        if (plan_a(cone_of(k), KL, pa[k], multi_path(P)) ||
+        if (plan_a(cone_of(k), KL, pa[k], multi_path(P), sh != nullptr) ||
             plan_b(cone_of(k), KL, pb[k], multi_path(P), !sh && b_fused_on()))
             return -1;
         nblkA += pa[k].grid;
         nblkB += pb[k].grid;
-        if (!pa[k].small && !a_fused(cone_of(k), pa[k], sh != nullptr)) split = true;
+        if (!pa[k].small && !pa[k].afused) split = true;
     }
     // long-row kernels in column tiles (k_wide_a / k_wide_b TL): the cone's column segments and
     // the partial-gradient buffer exist, one cone per launch, not sharded; B adds k_wide_bf's blocks
