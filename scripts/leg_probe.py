@@ -19,6 +19,8 @@ solver = importlib.import_module("ltr-lowrank-sdp_amd.solver")
 inst = importlib.import_module("ltr-lowrank-sdp_amd.instances")
 bench = importlib.import_module("bench")
 
+if os.environ.get("LRS_LIB"):   # A/B of a variant build (ltr-lowrank-sdp_amd/_build/liblrsdp_<v>.so)
+    solver.load_library(os.environ["LRS_LIB"])
 leg = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 cache = os.path.join(ROOT, ".bench_instances")
