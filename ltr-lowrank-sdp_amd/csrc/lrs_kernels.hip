@@ -6234,6 +6234,7 @@ constexpr int kSmallMaxConst = 4;     // constant-objective cones the kernel car
 constexpr int kSmallMaxWg = 8;        // cones of a one-workgroup-per-cone launch
 constexpr int kSmallXcds = 8;         // block stride between those cones' workgroups (MI355X: 8 XCDs)
 constexpr int kSmallMaxLd = 64;       // widest factor row
+constexpr int kSmallMaxRows = 1024;   // rows of a workgroup's cone(s): the rows phase's order in LDS
 struct SmallWg {
     int n, r0, s0, P, nadj;                      // rows, first (all-cone) row, first slot, slots, adjacency
     const int *adj_ptr, *adj_low, *adj_col, *adj_slot;
@@ -6262,6 +6263,7 @@ struct SmallArgs {
     // arrival counter xcnt
     int nwg, xs;
     int spin_log2;             // the exchange's spin limit, 2^spin_log2 polls (LRS_XWG_SPIN; default 26; -1 none)
+    int row_sort;              // rows phase in adjacency-length order (LRS_SMALL_ROWSORT; default 1)
     SmallWg wg[kSmallMaxWg];   // [0]: the single workgroup's (all cones, merged adjacency) when nwg == 1
     double *xbuf;
     unsigned *xcnt;
@@ -6382,6 +6384,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
     __shared__ double csR[kSmallMaxConst][kSmallMaxLd], csD[kSmallMaxConst][kSmallMaxLd];
     __shared__ double cpart[kSmallThreads];
     __shared__ int xfail;
+    __shared__ int Lord[kSmallMaxRows];   // the rows phase's row order
     __shared__ double xsum[16], xrecv[kSmallMaxWg * 16];   // the exchange's own sums, the received ones
     unsigned xe = 0;   // exchanges so far (wave 0)
     const int lane = tid & 63, wv = tid >> 6, sl_lane = tid % TPR;
@@ -6401,6 +6404,32 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
             if (e < N) Llow[e] = adj_low[e];
         }
     }
+    __syncthreads();
+    // the rows phase's order (row_sort): rows by adjacency length, longest first (ties by index),
+    // dealt to the row groups in alternating directions pass by pass -- a wave's pass lasts as
+    // long as its longest row, so the long rows share the first pass's waves and the short ones
+    // fill the last, partial pass beside the first pass's shortest; a row's own sums keep their order
+    constexpr int RK = (kSmallMaxRows + T - 1) / T;
+    for (int i = tid; i < N; i += T) Lord[i] = A.row_sort ? aptr(i + 1) - aptr(i) : 0;
+    __syncthreads();
+    int rk[RK];
+#pragma unroll
+    for (int u = 0; u < RK; ++u) {
+        const int i = tid + u * T;
+        rk[u] = i;
+        if (i >= N || !A.row_sort) continue;
+        const int di = Lord[i];
+        int k = 0;
+        for (int j = 0; j < N; ++j) {
+            const int dj = Lord[j];
+            k += (dj > di || (dj == di && j < i)) ? 1 : 0;
+        }
+        rk[u] = k;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < RK; ++u)
+        if (tid + u * T < N) Lord[rk[u]] = tid + u * T;
     __syncthreads();
     // constant objectives: column sums (C R = sa 1 (1^T R), carried with tau like C R)
     auto colsums = [&](const double *X, double (*cs)[kSmallMaxLd]) {
@@ -6675,9 +6704,10 @@ __global__ void __launch_bounds__(kSmallThreads) k_small_alm(SmallArgs A) {
         const double *__restrict__ so = h == 0 ? (MC ? A.s1 + rbo : A.s1) : (MC ? A.s0 + rbo : A.s0), *__restrict__ yo = h == 0 ? (MC ? A.y1 + rbo : A.y1) : (MC ? A.y0 + rbo : A.y0);
         double bacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (int i0 = 0; i0 < N; i0 += RPP) {
-            const int r = i0 + tid / TPR;
-            const bool valid = r < N;
-            const int ii = valid ? r : N - 1;
+            const int gi = tid / TPR;
+            const int pos = i0 + ((A.row_sort && ((i0 / RPP) & 1)) ? RPP - 1 - gi : gi);
+            const bool valid = pos < N;
+            const int ii = Lord[valid ? pos : N - 1];
             double2 g[H2], rii[H2];
             const long ob = ((long)ii * LD) / 2 + sl_lane;     // double2 index of this lane's first pair
 #pragma unroll
@@ -6912,7 +6942,7 @@ static bool small_alm_args(const DevProblem &P, DevWork &W, SmallArgs &A, int *l
     // LRS_SMALL_MC=1 (tests): one workgroup per cone wherever that applies, also where all fit one
     const bool force_mc = getenv("LRS_SMALL_MC") && atoi(getenv("LRS_SMALL_MC")) != 0;
     if ((P.K == 1 || P.has_merged) && !(force_mc && P.K >= 2 && P.cone_sep) &&
-        small_lds_bytes(N, ld, P.Ptot, a.adj_nnz, false) <= kSmallMaxDynLds) {
+        N <= kSmallMaxRows && small_lds_bytes(N, ld, P.Ptot, a.adj_nnz, false) <= kSmallMaxDynLds) {
         A.al = small_lds_bytes(N, ld, P.Ptot, a.adj_nnz, true) <= kSmallMaxDynLds;
     } else {
         // one workgroup per cone: every constraint within one cone, each cone in one CU's LDS
@@ -6920,7 +6950,7 @@ static bool small_alm_args(const DevProblem &P, DevWork &W, SmallArgs &A, int *l
         bool al = true;
         for (int k = 0; k < P.K; ++k) {
             const DevCone &ck = P.cones[k];
-            if (small_lds_bytes(ck.n, ld, ck.P, ck.adj_nnz, false) > kSmallMaxDynLds) return false;
+            if (ck.n > kSmallMaxRows || small_lds_bytes(ck.n, ld, ck.P, ck.adj_nnz, false) > kSmallMaxDynLds) return false;
             al = al && small_lds_bytes(ck.n, ld, ck.P, ck.adj_nnz, true) <= kSmallMaxDynLds;
         }
         A.al = al;
@@ -6998,6 +7028,8 @@ int launch_small_alm(const DevProblem &P, DevWork &W, const double *ctrl_in, dou
     {
         const char *e = getenv("LRS_XWG_SPIN");
         A.spin_log2 = e ? std::max(-1, std::min(40, atoi(e))) : 26;   // -1: no wait at all (tests)
+        const char *o = getenv("LRS_SMALL_ROWSORT");
+        A.row_sort = o ? (atoi(o) != 0) : 1;
     }
     size_t lds = small_lds_bytes(A.N, ld, A.Ptot, A.nadj, A.al != 0);
     if (A.nwg > 1) {   // the largest cone's
